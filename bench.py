@@ -1,0 +1,194 @@
+#!/usr/bin/env python3
+"""bench.py — GP fits/sec on the BASELINE.json headline configuration.
+
+Workload (BASELINE.json configs[2], the config the metric "GP fits/sec + predict pts/sec,
+N=16384 d=32 fp64" is quoted on): N=16384 training points, d=32, m=1, fp64,
+SumKernel(GaussianKernel(2,0.15), PeriodicKernel(0.1,pi,1)), noise sigma=1.0, synthetic
+SplitMix64 data (gpr_amd/synth.py).  One step = one full GP fit = covariance build +
+Cholesky factorisation + regression-vector solve (the reference's
+GaussianProcess<double>::Initialize, lib/GaussianProcess.cpp:118-130), inputs resident in
+HBM before the timed region.
+
+Multi-GPU: launched by torch.distributed.run, one process per GPU.  Until the distributed
+row-block Cholesky lands, each rank fits its own independent GP (replicas, weak scaling):
+value = fits completed by all ranks / max-over-ranks time.
+
+Prints ONE JSON line on rank 0 (plus human-readable detail on stderr).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_FP64_TFLOPS = 78.6   # MI355X dense fp64 (vector = matrix), MI355X_MICROARCH.md / SURVEY.md §8(d)
+PEAK_HBM_GBS = 8000.0     # HBM3E spec
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def fit_roofline_ms(n, d, m, gpus=1):
+    """T_roof = B_build/BW + F_potrf/(peak*g) + B_solve/BW (comm excluded)."""
+    b_build = 8.0 * (n * d + n * (n + 1) / 2)
+    f_potrf = n ** 3 / 3.0
+    b_solve = 2 * 8.0 * n * (n + 1) / 2 * m
+    return 1e3 * (b_build / (PEAK_HBM_GBS * 1e9) + f_potrf / (PEAK_FP64_TFLOPS * 1e12 * gpus)
+                  + b_solve / (PEAK_HBM_GBS * 1e9))
+
+
+def cpu_baseline(cfg, n_cpu):
+    """The CPU restatement of the reference's fit (oracle/: kernel pair loop + LAPACK
+    dgetrf+dgetri in fp64 + C*Y), timed on this host's cores: one fit at n_cpu."""
+    from oracle import oracle as O
+    from gpr_amd.synth import make_data
+    X, Y = make_data(n_cpu, cfg["d"], cfg["m"])
+    t0 = time.perf_counter()
+    O.fit(cfg["kernel"], X, Y, cfg["sigma"], np.float64, want_core=False)
+    dt = time.perf_counter() - t0
+    scale = (n_cpu / cfg["n"]) ** 3  # fits/s at the bench N (LU inverse is 2N^3)
+    return {
+        "value": (1.0 / dt) * scale,
+        "unit": "fits/s",
+        "cores": O.num_threads(),
+        "kind": "port",
+        "sample": (f"1 fit at N={n_cpu} (d={cfg['d']}, same kernel) in {dt:.2f} s, LAPACK={O.lapack_name()}"
+                   + ("" if n_cpu == cfg["n"] else f", cubic-scaled to N={cfg['n']}")),
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--n", type=int, default=None)
+    ap.add_argument("--d", type=int, default=None)
+    ap.add_argument("--predict-q", type=int, default=65536)
+    ap.add_argument("--cpu-n", type=int, default=16384, help="N of the CPU-baseline sample (0 = skip)")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as tdist
+        torch.cuda.set_device(local_rank)
+        tdist.init_process_group("nccl")
+        dist = tdist
+
+    import gpr_amd
+    from gpr_amd.synth import C3, make_data, make_queries
+
+    cfg = dict(C3)
+    if args.n:
+        cfg["n"] = args.n
+    if args.d:
+        cfg["d"] = args.d
+    n, d, m = cfg["n"], cfg["d"], cfg["m"]
+
+    ctx = gpr_amd.Context(local_rank)
+    X, Y = make_data(n, d, m)
+    model = gpr_amd.Model(ctx, np.float64)
+    model.set_data(X, Y)
+    model.set_kernel(cfg["kernel"])
+    model.set_noise(cfg["sigma"])
+
+    for _ in range(args.warmup):
+        model.fit()
+
+    def barrier_sync():
+        if dist is not None:
+            import torch
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    ctx.set_stats(True)
+    barrier_sync()
+    t0 = time.perf_counter()
+    infos = [model.fit() for _ in range(args.steps)]
+    barrier_sync()
+    elapsed = time.perf_counter() - t0
+    stats = ctx.stats()
+    ctx.set_stats(False)
+
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    fits = args.steps * world
+    value = fits / elapsed
+    ms_per_step = 1e3 * elapsed / args.steps
+
+    # prediction throughput (device time of the fused predict kernels, mean only)
+    pred = None
+    if args.predict_q > 0:
+        Xq = make_queries(args.predict_q, d)
+        ctx.set_stats(True)
+        tq0 = time.perf_counter()
+        model.predict(Xq)
+        tq = time.perf_counter() - tq0
+        ps = ctx.stats().get("predict")
+        ctx.set_stats(False)
+        pred = {"q": args.predict_q, "pts_per_s_device": args.predict_q / (ps["ms"] * 1e-3) if ps else None,
+                "pts_per_s_wall_incl_pcie": args.predict_q / tq}
+
+    upd = stats.get("potrf_update", {"ms": 0, "flops": 0, "launches": 0})
+    achieved = (upd["flops"] / (upd["ms"] * 1e-3) / 1e12) if upd["ms"] > 0 else 0.0
+    phases = {k: {"ms_per_fit": v["ms"] / args.steps, "launches_per_fit": v["launches"] / args.steps,
+                  "tflops": (v["flops"] / (v["ms"] * 1e-3) / 1e12) if v["ms"] and v["flops"] else None,
+                  "gbs": (v["bytes"] / (v["ms"] * 1e-3) / 1e9) if v["ms"] and v["bytes"] else None}
+              for k, v in stats.items()}
+    t_roof = fit_roofline_ms(n, d, m)
+    fit_ms = np.median([i.ms_build + i.ms_factor + i.ms_solve for i in infos])
+
+    if rank == 0:
+        cpu = None
+        if world == 1 and args.cpu_n > 0:
+            try:
+                cpu = cpu_baseline(cfg, args.cpu_n)
+            except Exception as e:  # the baseline is reported, never required
+                log("cpu baseline failed:", e)
+        line = {
+            "metric": "GP fits/sec (kernel build + Cholesky + solve), N=16384 d=32 fp64",
+            "value": value,
+            "unit": "fits/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (SplitMix64 seed 0x47505231, gpr_amd/synth.py)",
+            "config": {"workload": "C3: GP fit N=16384 d=32 m=1 Sum(Gaussian(2,0.15)+Periodic(0.1,pi,1)) "
+                                   "sigma=1.0 fp64 (BASELINE.json configs[2])",
+                       "n": n, "d": d, "m": m, "kernel": cfg["kernel"],
+                       "parallelism": "replicas" if world > 1 else "single-gpu"},
+            "roofline": {"bound": "mfma", "kernel": "gemm_nt trailing update (potrf_update)",
+                         "achieved": achieved, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
+                         "frac": achieved / PEAK_FP64_TFLOPS, "traffic": None},
+            "fit_roofline": {"t_roof_ms": t_roof, "t_fit_device_ms": fit_ms, "frac": t_roof / fit_ms},
+            "phases": phases,
+            "predict": pred,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,13 @@
+"""gpr_amd — MI355X-native Gaussian-process regression core (agiger/GPR hot path).
+
+The numerics live in libgprx (gpr_amd/lib/libgprx.so, hand-written gfx950 HIP kernels
+behind the C ABI of include/gprx.h).  This package holds the Python binding used by the
+tests and bench.py; the C++ host API mirroring the reference classes is in include/gpr/.
+"""
+from . import kernels
+from .kernels import (Gaussian, GaussianExp, White, RationalQuadratic, Periodic, Sum, Product, parse_kernel,
+                      general_kernel)
+from .gprx import Context, Model, GprxError, lib, device_count, LIB_PATH
+
+__all__ = ["kernels", "Gaussian", "GaussianExp", "White", "RationalQuadratic", "Periodic", "Sum", "Product",
+           "parse_kernel", "general_kernel", "Context", "Model", "GprxError", "lib", "device_count", "LIB_PATH"]

@@ -1,0 +1,919 @@
+// gprx_api.cpp — the C ABI of libgprx (include/gprx.h): contexts, resident models and the
+// host-side orchestration of the HIP kernels.  No entry point throws across the ABI.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <climits>
+#include <cmath>
+#include <cstring>
+#include <limits>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "gprx_internal.h"
+
+namespace gprx {
+
+// ---- extra launchers (k_predict.hip, k_lml.hip) -----------------------------------------
+template <typename T>
+void launch_pair_kernel(const KCanon<T>& K, const T* Xa, const T* Xb, int64_t q, int d, T* out, hipStream_t s);
+template <typename T>
+void launch_rowdot(const T* Va, const T* Vb, int64_t ld, int64_t q, int64_t n, const T* kab, T* out, hipStream_t s);
+template <typename T>
+void trsm_rows(const T* A, int64_t ldA, int64_t np, const T* Linv, T* R, int64_t ld, int64_t qp, hipStream_t s);
+template <typename T>
+void launch_spd_inverse_from_factor(const T* A, int64_t ldA, int64_t np, const T* Linv, T* V, T* C, hipStream_t s);
+template <typename T>
+void launch_lml_grad(const KCanon<T>& K, const T* X, const T* tab, int64_t n, int d, const T* alpha, const T* C,
+                     int64_t ldc, double* acc /* MAX_LEAF*3 */, hipStream_t s);
+template <typename T>
+void launch_set_identity_pad(T* A, int64_t ld, int64_t n, int64_t np, hipStream_t s);
+
+static thread_local std::string t_last_error;
+thread_local Prof* g_prof = nullptr;
+
+// ---------------------------------------------------------------------------------------
+// canonical kernel form
+// ---------------------------------------------------------------------------------------
+static int leaf_nparams(int op) {
+    switch (op) {
+        case GPRX_K_GAUSSIAN:
+        case GPRX_K_GAUSSIAN_EXP:
+            return 2;
+        case GPRX_K_WHITE:
+            return 1;
+        case GPRX_K_RATIONAL_QUADRATIC:
+        case GPRX_K_PERIODIC:
+            return 3;
+    }
+    return 0;
+}
+
+template <typename T>
+std::string canonicalize(const gprx_kernel_desc& desc, KCanon<T>& K) {
+    std::memset(&K, 0, sizeof(K));
+    if (desc.n_nodes <= 0 || desc.n_nodes > GPRX_MAX_KNODES) return "kernel descriptor: bad node count";
+    std::vector<std::vector<unsigned>> st;
+    int nleaf = 0, nparams = 0, nper = 0;
+    bool r2 = false;
+    for (int i = 0; i < desc.n_nodes; i++) {
+        const gprx_knode& nd = desc.node[i];
+        const int op = nd.op;
+        if (op == GPRX_K_SUM || op == GPRX_K_PRODUCT) {
+            if (st.size() < 2) return "kernel descriptor: malformed post-order program";
+            std::vector<unsigned> b = st.back();
+            st.pop_back();
+            std::vector<unsigned> a = st.back();
+            st.pop_back();
+            std::vector<unsigned> r;
+            if (op == GPRX_K_SUM) {
+                r = a;
+                r.insert(r.end(), b.begin(), b.end());
+            } else {
+                for (unsigned ta : a)
+                    for (unsigned tb : b) r.push_back(ta | tb);
+            }
+            if ((int)r.size() > MAX_TERM) return "kernel descriptor: too many product terms for the device form";
+            st.push_back(r);
+            continue;
+        }
+        const int np = leaf_nparams(op);
+        if (np == 0) return "kernel descriptor: unknown node op";
+        if (nleaf >= MAX_LEAF) return "kernel descriptor: too many leaf kernels for the device form";
+        KLeaf<T>& L = K.leaf[nleaf];
+        const T p0 = (T)nd.p[0], p1 = (T)nd.p[1], p2 = (T)nd.p[2];
+        L.p[0] = p0;
+        L.p[1] = p1;
+        L.p[2] = p2;
+        switch (op) {
+            case GPRX_K_GAUSSIAN:  // include/Kernel.h:529-537
+                if (p0 == T(0)) return "GaussianKernel: sigma has to be positive";
+                if (p1 == T(0)) return "GaussianKernel: scale has to be positive";
+                L.type = L_GAUSS;
+                L.c0 = p1 * p1;
+                L.c1 = T(-0.5) / (p0 * p0);
+                r2 = true;
+                break;
+            case GPRX_K_GAUSSIAN_EXP: {
+                const T es = std::exp(p1), eg = std::exp(p0);
+                L.type = L_GAUSS_EXP;
+                L.c0 = es * es;
+                L.c1 = T(-0.5) / (eg * eg);
+                r2 = true;
+                break;
+            }
+            case GPRX_K_WHITE:
+                L.type = L_WHITE;
+                L.c0 = p0 * p0;
+                r2 = true;
+                break;
+            case GPRX_K_RATIONAL_QUADRATIC:
+                L.type = L_RQ;
+                L.c0 = p0 * p0;
+                L.c1 = T(0.5) / (p1 * p1 * p2);
+                L.c2 = p2;
+                r2 = true;
+                break;
+            case GPRX_K_PERIODIC:  // include/Kernel.h:1003-1005
+                if (p0 == T(0)) return "PeriodicKernel: scale parameter has to be positive.";
+                if (p1 == T(0)) return "PeriodicKernel: period length parameter has to be positive.";
+                if (p2 == T(0)) return "PeriodicKernel: sigma parameter has to be positive.";
+                if (nper >= MAX_PER) return "kernel descriptor: at most 2 periodic leaves on the device";
+                L.type = L_PERIODIC;
+                L.pslot = nper;
+                K.b[nper] = p1;
+                nper++;
+                L.c0 = p0 * p0;
+                L.c1 = T(-0.5) / (p2 * p2);
+                break;
+        }
+        K.param_base[nleaf] = nparams;
+        nparams += np;
+        st.push_back(std::vector<unsigned>{1u << nleaf});
+        nleaf++;
+    }
+    if (st.size() != 1) return "kernel descriptor: malformed post-order program";
+    K.nleaf = nleaf;
+    K.nterm = (int)st[0].size();
+    K.sum_leaves = 1;
+    for (int t = 0; t < K.nterm; t++) {
+        K.term_mask[t] = st[0][t];
+        if (st[0][t] != (1u << t)) K.sum_leaves = 0;
+    }
+    K.nper = nper;
+    K.need_r2 = r2 ? 1 : 0;
+    K.nparams = nparams;
+    if (nparams > GPRX_MAX_KPARAMS) return "kernel descriptor: too many parameters";
+    return "";
+}
+template std::string canonicalize<float>(const gprx_kernel_desc&, KCanon<float>&);
+template std::string canonicalize<double>(const gprx_kernel_desc&, KCanon<double>&);
+
+// ---------------------------------------------------------------------------------------
+// device buffers
+// ---------------------------------------------------------------------------------------
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    void ensure(size_t b) {
+        if (b <= bytes && p) return;
+        release();
+        if (b == 0) return;
+        GPRX_HIP(hipMalloc(&p, b));
+        bytes = b;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    template <typename T>
+    T* as() const {
+        return reinterpret_cast<T*>(p);
+    }
+    ~DevBuf() { release(); }
+};
+
+static int64_t round_up(int64_t x, int64_t g) { return (x + g - 1) / g * g; }
+
+}  // namespace gprx
+
+using namespace gprx;
+
+struct gprx_ctx {
+    int device = 0;
+    int rank = 0, world = 1;
+    hipStream_t stream = nullptr;
+    hipStream_t aux = nullptr;  // look-ahead stream of the factorisation
+    Exec ex;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    Prof prof;
+    std::string err;
+    std::mutex mu;
+};
+
+// Per-call profiler binding: sets the thread's current profiler and resolves the
+// recorded events (after draining both streams) when the call returns.
+struct ProfBind {
+    gprx_ctx* ctx;
+    explicit ProfBind(gprx_ctx* c) : ctx(c) { g_prof = (c && c->prof.on) ? &c->prof : nullptr; }
+    ~ProfBind() {
+        if (ctx && ctx->prof.on) {
+            (void)hipStreamSynchronize(ctx->stream);
+            (void)hipStreamSynchronize(ctx->aux);
+            ctx->prof.resolve();
+        }
+        g_prof = nullptr;
+    }
+};
+
+struct gprx_model {
+    gprx_ctx* ctx = nullptr;
+    gprx_dtype dt = GPRX_F64;
+    int64_t n = 0;
+    int d = 0, m = 0;
+    int64_t np = 0, mp = 0, ld = 0;
+    double sigma = 0;
+    bool has_data = false, has_kernel = false, fitted = false;
+    gprx_kernel_desc desc{};
+    KCanon<double> kd{};
+    KCanon<float> kf{};
+    DevBuf X, Y, tab, A, Linv, z, alpha, info, flag, red, V, C, scratch1, scratch2, grad;
+    std::mutex mu;
+};
+
+// ---------------------------------------------------------------------------------------
+// error plumbing
+// ---------------------------------------------------------------------------------------
+static gprx_status fail(gprx_ctx* ctx, gprx_status st, const std::string& msg) {
+    t_last_error = msg;
+    if (ctx) ctx->err = msg;
+    return st;
+}
+
+#define API_BEGIN try {
+#define API_END(ctx)                                                                   \
+    }                                                                                  \
+    catch (const gprx::Error& e) {                                                     \
+        return fail(ctx, e.st, e.msg);                                                 \
+    }                                                                                  \
+    catch (const std::exception& e) {                                                  \
+        return fail(ctx, GPRX_ERR_HIP, e.what());                                      \
+    }                                                                                  \
+    catch (...) {                                                                      \
+        return fail(ctx, GPRX_ERR_HIP, "unknown exception");                           \
+    }
+
+static size_t esize(gprx_dtype dt) { return dt == GPRX_F64 ? sizeof(double) : sizeof(float); }
+
+template <typename T>
+static const KCanon<T>& kcanon(const gprx_model* m);
+template <>
+const KCanon<double>& kcanon<double>(const gprx_model* m) {
+    return m->kd;
+}
+template <>
+const KCanon<float>& kcanon<float>(const gprx_model* m) {
+    return m->kf;
+}
+
+// ---------------------------------------------------------------------------------------
+// fit
+// ---------------------------------------------------------------------------------------
+template <typename T>
+static gprx_status model_fit(gprx_model* M, uint32_t flags, gprx_fit_info* out) {
+    (void)flags;
+    gprx_ctx* ctx = M->ctx;
+    GPRX_REQUIRE(M->has_data, GPRX_ERR_STATE, "GaussianProcess::Initialize: no input samples defined during initialization");
+    GPRX_REQUIRE(M->has_kernel, GPRX_ERR_STATE, "gprx: no kernel set");
+    GPRX_HIP(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    const KCanon<T>& K = kcanon<T>(M);
+    const int64_t n = M->n, np = round_up(n, DB), mp = round_up(M->m, GT), ld = np + mp;
+    M->np = np;
+    M->mp = mp;
+    M->ld = ld;
+    M->A.ensure(sizeof(T) * ld * np);
+    M->Linv.ensure(sizeof(T) * np * DB);
+    M->z.ensure(sizeof(T) * M->m * np);
+    M->alpha.ensure(sizeof(T) * np * M->m);
+    M->info.ensure(sizeof(int));
+    M->flag.ensure(sizeof(int));
+    M->red.ensure(sizeof(double) * 2);
+    if (K.nper > 0) {
+        M->tab.ensure(sizeof(T) * 2 * K.nper * n * M->d);
+        launch_sincos_tables<T>(K, M->X.as<T>(), n, M->d, M->tab.as<T>(), s);
+    }
+    GPRX_HIP(hipMemsetD32Async((hipDeviceptr_t)M->info.p, INT_MAX, 1, s));
+    GPRX_HIP(hipMemsetAsync(M->flag.p, 0, sizeof(int), s));
+    const T sig = (T)M->sigma;
+    const T sigma2 = sig * sig;  // m_Sigma*m_Sigma in T (lib/GaussianProcess.cpp:379)
+    GPRX_HIP(hipEventRecord(ctx->ev[0], s));
+    launch_kbuild<T>(K, M->X.as<T>(), M->tab.as<T>(), n, M->X.as<T>(), M->tab.as<T>(), n, M->d, M->A.as<T>(), ld, np,
+                     true, sigma2, M->flag.as<int>(), s);
+    launch_aug_rows<T>(M->Y.as<T>(), n, M->m, M->A.as<T>(), ld, np, mp, s);
+    GPRX_HIP(hipEventRecord(ctx->ev[1], s));
+    potrf_blocked<T>(M->A.as<T>(), ld, np, ld, M->Linv.as<T>(), M->info.as<int>(), ctx->ex);
+    GPRX_HIP(hipEventRecord(ctx->ev[2], s));
+    launch_fit_reductions<T>(M->A.as<T>(), ld, n, np, M->m, M->red.as<double>(), s);
+    launch_backsolve<T>(M->A.as<T>(), ld, np, M->m, M->Linv.as<T>(), M->z.as<T>(), M->alpha.as<T>(), s);
+    GPRX_HIP(hipEventRecord(ctx->ev[3], s));
+    GPRX_HIP(hipStreamSynchronize(s));
+    GPRX_HIP(hipGetLastError());
+    int hflag = 0, hinfo = 0;
+    double hred[2];
+    GPRX_HIP(hipMemcpy(&hflag, M->flag.p, sizeof(int), hipMemcpyDeviceToHost));
+    GPRX_HIP(hipMemcpy(&hinfo, M->info.p, sizeof(int), hipMemcpyDeviceToHost));
+    GPRX_HIP(hipMemcpy(hred, M->red.p, sizeof(hred), hipMemcpyDeviceToHost));
+    M->fitted = false;
+    if (out) {
+        std::memset(out, 0, sizeof(*out));
+        float t01 = 0, t12 = 0, t23 = 0;
+        hipEventElapsedTime(&t01, ctx->ev[0], ctx->ev[1]);
+        hipEventElapsedTime(&t12, ctx->ev[1], ctx->ev[2]);
+        hipEventElapsedTime(&t23, ctx->ev[2], ctx->ev[3]);
+        out->ms_build = t01;
+        out->ms_factor = t12;
+        out->ms_solve = t23;
+        out->logdet = hred[0];
+        out->datafit = hred[1];
+        out->info = (hinfo == INT_MAX) ? 0 : hinfo;
+        out->method = 0;
+    }
+    if (hflag)
+        throw Error{GPRX_ERR_NONFINITE,
+                    "GaussianProcess::ComputeKernelMatrixInternal: kernel matrix contains entries which are not finite."};
+    if (hinfo != INT_MAX)
+        throw Error{GPRX_ERR_NOT_SPD, "gprx: kernel matrix is not positive definite (Cholesky pivot " +
+                                          std::to_string(hinfo) + " <= 0)"};
+    M->fitted = true;
+    return GPRX_OK;
+}
+
+// V = L^{-T} (upper), C = V V^T (lower, ld = np) from the stored factor
+template <typename T>
+static void model_inverse(gprx_model* M) {
+    hipStream_t s = M->ctx->stream;
+    const int64_t np = M->np;
+    M->V.ensure(sizeof(T) * np * np);
+    M->C.ensure(sizeof(T) * np * np);
+    launch_spd_inverse_from_factor<T>(M->A.as<T>(), M->ld, np, M->Linv.as<T>(), M->V.as<T>(), M->C.as<T>(), s);
+}
+
+// Host <-> device transfers use pageable caller memory: always synchronous, after the
+// work stream has drained (no async copies from/to pageable memory).
+template <typename T>
+static void upload(DevBuf& b, const void* host, size_t bytes, hipStream_t s) {
+    b.ensure(bytes);
+    GPRX_HIP(hipStreamSynchronize(s));
+    if (bytes) GPRX_HIP(hipMemcpy(b.p, host, bytes, hipMemcpyHostToDevice));
+}
+
+static void download(void* host, const void* dev, size_t bytes, hipStream_t s) {
+    GPRX_HIP(hipStreamSynchronize(s));
+    GPRX_HIP(hipGetLastError());
+    if (bytes) GPRX_HIP(hipMemcpy(host, dev, bytes, hipMemcpyDeviceToHost));
+}
+
+template <typename T>
+static gprx_status model_predict(gprx_model* M, const void* Xq, int64_t q, void* mean, void* deriv) {
+    GPRX_REQUIRE(M->fitted, GPRX_ERR_STATE, "GaussianProcess::ComputeKernelVectorInternal: gaussian process is not initialized.");
+    hipStream_t s = M->ctx->stream;
+    const KCanon<T>& K = kcanon<T>(M);
+    const int d = M->d, m = M->m;
+    DevBuf dq, dtab, dmean, dder;
+    upload<T>(dq, Xq, sizeof(T) * q * d, s);
+    if (K.nper > 0) {
+        dtab.ensure(sizeof(T) * 2 * K.nper * q * d);
+        launch_sincos_tables<T>(K, dq.as<T>(), q, d, dtab.as<T>(), s);
+    }
+    dmean.ensure(sizeof(T) * q * m);
+    if (deriv) dder.ensure(sizeof(T) * q * d * m);
+    const int64_t ncz = (int64_t)m * (deriv ? (1 + d) : 1);
+    M->scratch1.ensure(sizeof(T) * M->n * ncz);
+    M->scratch2.ensure(sizeof(T) * q * ncz);
+    launch_predict<T>(K, M->X.as<T>(), M->tab.as<T>(), M->n, d, m, M->alpha.as<T>(), dq.as<T>(), dtab.as<T>(), q,
+                      dmean.as<T>(), deriv ? dder.as<T>() : nullptr, M->scratch1.as<T>(), M->scratch2.as<T>(), s);
+    download(mean, dmean.p, sizeof(T) * q * m, s);
+    if (deriv) download(deriv, dder.p, sizeof(T) * q * d * m, s);
+    return GPRX_OK;
+}
+
+template <typename T>
+static void solve_rows_for(gprx_model* M, const T* dXq, const T* dtabQ, int64_t q, int64_t qp, T* R) {
+    hipStream_t s = M->ctx->stream;
+    const KCanon<T>& K = kcanon<T>(M);
+    GPRX_HIP(hipMemsetAsync(R, 0, sizeof(T) * qp * M->np, s));
+    launch_kbuild<T>(K, dXq, dtabQ, q, M->X.as<T>(), M->tab.as<T>(), M->n, M->d, R, qp, 0, false, T(0),
+                     M->flag.as<int>(), s);
+    trsm_rows<T>(M->A.as<T>(), M->ld, M->np, M->Linv.as<T>(), R, qp, qp, s);
+}
+
+template <typename T>
+static gprx_status model_posterior_cov(gprx_model* M, const void* Xa, const void* Xb, int64_t q, void* out) {
+    GPRX_REQUIRE(M->fitted, GPRX_ERR_STATE, "GaussianProcess::ComputeKernelVectorInternal: gaussian process is not initialized.");
+    hipStream_t s = M->ctx->stream;
+    const KCanon<T>& K = kcanon<T>(M);
+    const int d = M->d;
+    const int64_t qp = round_up(q, GT);
+    DevBuf da, db, ta, tb, Ra, Rb, kab, res;
+    upload<T>(da, Xa, sizeof(T) * q * d, s);
+    upload<T>(db, Xb, sizeof(T) * q * d, s);
+    if (K.nper > 0) {
+        ta.ensure(sizeof(T) * 2 * K.nper * q * d);
+        tb.ensure(sizeof(T) * 2 * K.nper * q * d);
+        launch_sincos_tables<T>(K, da.as<T>(), q, d, ta.as<T>(), s);
+        launch_sincos_tables<T>(K, db.as<T>(), q, d, tb.as<T>(), s);
+    }
+    Ra.ensure(sizeof(T) * qp * M->np);
+    Rb.ensure(sizeof(T) * qp * M->np);
+    solve_rows_for<T>(M, da.as<T>(), ta.as<T>(), q, qp, Ra.as<T>());
+    solve_rows_for<T>(M, db.as<T>(), tb.as<T>(), q, qp, Rb.as<T>());
+    kab.ensure(sizeof(T) * q);
+    res.ensure(sizeof(T) * q);
+    launch_pair_kernel<T>(K, da.as<T>(), db.as<T>(), q, d, kab.as<T>(), s);
+    launch_rowdot<T>(Ra.as<T>(), Rb.as<T>(), qp, q, M->np, kab.as<T>(), res.as<T>(), s);
+    download(out, res.p, sizeof(T) * q, s);
+    return GPRX_OK;
+}
+
+template <typename T>
+static gprx_status model_core_matrix(gprx_model* M, void* Cout) {
+    GPRX_REQUIRE(M->fitted, GPRX_ERR_STATE, "gprx: model is not fitted");
+    hipStream_t s = M->ctx->stream;
+    model_inverse<T>(M);
+    const int64_t n = M->n, np = M->np;
+    std::vector<T> h((size_t)n * n);
+    // column j of C (lower part rows >= j) -> row-major; C symmetric
+    GPRX_HIP(hipStreamSynchronize(s));
+    GPRX_HIP(hipGetLastError());
+    GPRX_HIP(hipMemcpy2D(h.data(), sizeof(T) * n, M->C.p, sizeof(T) * np, sizeof(T) * n, n, hipMemcpyDeviceToHost));
+    T* C = reinterpret_cast<T*>(Cout);
+    // h[j*n + i] = C(i, j) valid for i >= j
+    for (int64_t j = 0; j < n; j++)
+        for (int64_t i = j; i < n; i++) {
+            const T v = h[(size_t)j * n + i];
+            C[(size_t)i * n + j] = v;
+            C[(size_t)j * n + i] = v;
+        }
+    return GPRX_OK;
+}
+
+template <typename T>
+static gprx_status model_lml(gprx_model* M, uint32_t flags, double* value, double* grad, int32_t* nparams,
+                             double* logdet) {
+    GPRX_REQUIRE(M->m == 1, GPRX_ERR_DIM,
+                 "GaussianLogLikelihood: only one output dimension is supported (the reference's data-fit term is "
+                 "m x m, include/Likelihood.h:175)");
+    gprx_fit_info fi;
+    gprx_status st = model_fit<T>(M, GPRX_FIT_NO_LU_FALLBACK, &fi);
+    if (st != GPRX_OK) return st;
+    const KCanon<T>& K = kcanon<T>(M);
+    const double n = (double)M->n;
+    const T df = (T)(-0.5 * fi.datafit);
+    const T ct = (T)(-n / 2.0 * std::log(2 * M_PI));  // include/Likelihood.h:192
+    double v;
+    if (flags & GPRX_LML_COMPAT) {
+        // include/Likelihood.h:77-79 narrows the long-double determinant to T, :180-188 clamps
+        typedef long double HP;
+        const HP det_ld = std::exp((HP)fi.logdet);
+        const HP det = (HP)(T)det_ld;
+        HP cp;
+        if (det <= std::numeric_limits<HP>::min()) cp = -0.5L * std::log(std::numeric_limits<HP>::min());
+        else if (det > std::numeric_limits<HP>::max()) cp = -0.5L * std::log(std::numeric_limits<HP>::max());
+        else cp = -0.5L * std::log(det);
+        v = (double)(T)(df + (T)(cp + ct));
+    } else {
+        v = (double)df - 0.5 * fi.logdet + (double)ct;
+    }
+    if (std::isinf(v))
+        throw Error{GPRX_ERR_NONFINITE, "GaussianLogLikelihood::GetValueAndParameterDerivatives: likelihood is infinite."};
+    if (value) *value = v;
+    if (logdet) *logdet = fi.logdet;
+    if (nparams) *nparams = K.nparams;
+    if (grad && (flags & GPRX_LML_GRAD)) {
+        hipStream_t s = M->ctx->stream;
+        model_inverse<T>(M);
+        M->grad.ensure(sizeof(double) * MAX_LEAF * 3);
+        GPRX_HIP(hipMemsetAsync(M->grad.p, 0, sizeof(double) * MAX_LEAF * 3, s));
+        launch_lml_grad<T>(K, M->X.as<T>(), M->tab.as<T>(), M->n, M->d, M->alpha.as<T>(), M->C.as<T>(), M->np,
+                           M->grad.as<double>(), s);
+        double acc[MAX_LEAF * 3];
+        download(acc, M->grad.p, sizeof(acc), s);
+        for (int l = 0; l < K.nleaf; l++) {
+            const int t = K.leaf[l].type;
+            const int np = (t == L_WHITE) ? 1 : ((t == L_GAUSS || t == L_GAUSS_EXP) ? 2 : 3);
+            for (int q = 0; q < np; q++) grad[K.param_base[l] + q] = 0.5 * acc[l * 3 + q];
+        }
+    }
+    return GPRX_OK;
+}
+
+// ---------------------------------------------------------------------------------------
+// standalone building blocks
+// ---------------------------------------------------------------------------------------
+template <typename T>
+static gprx_status kernel_matrix_impl(gprx_ctx* ctx, const gprx_kernel_desc* desc, const void* X, int64_t n, int d,
+                                      void* Kout, bool deriv) {
+    KCanon<T> K;
+    std::string e = canonicalize<T>(*desc, K);
+    GPRX_REQUIRE(e.empty(), GPRX_ERR_ARG, e);
+    hipStream_t s = ctx->stream;
+    DevBuf dx, tab, dk, flag;
+    upload<T>(dx, X, sizeof(T) * n * d, s);
+    if (K.nper > 0) {
+        tab.ensure(sizeof(T) * 2 * K.nper * n * d);
+        launch_sincos_tables<T>(K, dx.as<T>(), n, d, tab.as<T>(), s);
+    }
+    if (deriv) {
+        dk.ensure(sizeof(T) * K.nparams * n * n);
+        launch_deriv_matrix<T>(K, dx.as<T>(), tab.as<T>(), n, d, dk.as<T>(), s);
+        download(Kout, dk.p, sizeof(T) * K.nparams * n * n, s);
+        return GPRX_OK;
+    }
+    dk.ensure(sizeof(T) * n * n);
+    flag.ensure(sizeof(int));
+    GPRX_HIP(hipMemsetAsync(flag.p, 0, sizeof(int), s));
+    launch_kbuild<T>(K, dx.as<T>(), tab.as<T>(), n, dx.as<T>(), tab.as<T>(), n, d, dk.as<T>(), n, n, true, T(0),
+                     flag.as<int>(), s);
+    std::vector<T> h((size_t)n * n);
+    download(h.data(), dk.p, sizeof(T) * n * n, s);
+    int hf = 0;
+    download(&hf, flag.p, sizeof(int), s);
+    T* out = reinterpret_cast<T*>(Kout);
+    for (int64_t j = 0; j < n; j++)
+        for (int64_t i = j; i < n; i++) {
+            const T v = h[(size_t)j * n + i];
+            out[(size_t)i * n + j] = v;
+            out[(size_t)j * n + i] = v;
+        }
+    if (hf)
+        throw Error{GPRX_ERR_NONFINITE,
+                    "GaussianProcess::ComputeKernelMatrixInternal: kernel matrix contains entries which are not finite."};
+    return GPRX_OK;
+}
+
+template <typename T>
+static gprx_status cross_matrix_impl(gprx_ctx* ctx, const gprx_kernel_desc* desc, const void* A, int64_t na,
+                                     const void* B, int64_t nb, int d, void* Kout) {
+    KCanon<T> K;
+    std::string e = canonicalize<T>(*desc, K);
+    GPRX_REQUIRE(e.empty(), GPRX_ERR_ARG, e);
+    hipStream_t s = ctx->stream;
+    DevBuf da, dbb, ta, tb, dk, flag;
+    upload<T>(da, A, sizeof(T) * na * d, s);
+    upload<T>(dbb, B, sizeof(T) * nb * d, s);
+    if (K.nper > 0) {
+        ta.ensure(sizeof(T) * 2 * K.nper * na * d);
+        tb.ensure(sizeof(T) * 2 * K.nper * nb * d);
+        launch_sincos_tables<T>(K, da.as<T>(), na, d, ta.as<T>(), s);
+        launch_sincos_tables<T>(K, dbb.as<T>(), nb, d, tb.as<T>(), s);
+    }
+    dk.ensure(sizeof(T) * na * nb);
+    flag.ensure(sizeof(int));
+    GPRX_HIP(hipMemsetAsync(flag.p, 0, sizeof(int), s));
+    launch_kbuild<T>(K, da.as<T>(), ta.as<T>(), na, dbb.as<T>(), tb.as<T>(), nb, d, dk.as<T>(), na, 0, false, T(0),
+                     flag.as<int>(), s);
+    std::vector<T> h((size_t)na * nb);
+    download(h.data(), dk.p, sizeof(T) * na * nb, s);
+    T* out = reinterpret_cast<T*>(Kout);
+    for (int64_t j = 0; j < nb; j++)
+        for (int64_t i = 0; i < na; i++) out[(size_t)i * nb + j] = h[(size_t)j * na + i];
+    return GPRX_OK;
+}
+
+template <typename T>
+static gprx_status cholesky_impl(gprx_ctx* ctx, void* Ahost, int64_t n, int32_t* info, bool inverse) {
+    hipStream_t s = ctx->stream;
+    const int64_t np = round_up(n, DB);
+    DevBuf dA, dLinv, dinfo, dV, dC;
+    dA.ensure(sizeof(T) * np * np);
+    dLinv.ensure(sizeof(T) * np * DB);
+    dinfo.ensure(sizeof(int));
+    GPRX_HIP(hipMemsetAsync(dA.p, 0, sizeof(T) * np * np, s));
+    GPRX_HIP(hipStreamSynchronize(s));
+    // row i of the (symmetric) host matrix = column i of the column-major device matrix
+    GPRX_HIP(hipMemcpy2D(dA.p, sizeof(T) * np, Ahost, sizeof(T) * n, sizeof(T) * n, n, hipMemcpyHostToDevice));
+    launch_set_identity_pad<T>(dA.as<T>(), np, n, np, s);
+    GPRX_HIP(hipMemsetD32Async((hipDeviceptr_t)dinfo.p, INT_MAX, 1, s));
+    potrf_blocked<T>(dA.as<T>(), np, np, np, dLinv.as<T>(), dinfo.as<int>(), ctx->ex);
+    int hinfo = 0;
+    download(&hinfo, dinfo.p, sizeof(int), s);
+    hinfo = (hinfo == INT_MAX) ? 0 : hinfo;
+    if (info) *info = hinfo;
+    std::vector<T> h((size_t)n * n);
+    T* out = reinterpret_cast<T*>(Ahost);
+    if (!inverse) {
+        GPRX_HIP(hipMemcpy2D(h.data(), sizeof(T) * n, dA.p, sizeof(T) * np, sizeof(T) * n, n, hipMemcpyDeviceToHost));
+        // h[j*n + i] = L(i, j) for i >= j
+        for (int64_t i = 0; i < n; i++)
+            for (int64_t j = 0; j < n; j++) out[(size_t)i * n + j] = (i >= j) ? h[(size_t)j * n + i] : T(0);
+        return hinfo ? GPRX_ERR_NOT_SPD : GPRX_OK;
+    }
+    if (hinfo) return fail(ctx, GPRX_ERR_NOT_SPD, "gprx_spd_inverse: matrix is not positive definite");
+    dV.ensure(sizeof(T) * np * np);
+    dC.ensure(sizeof(T) * np * np);
+    launch_spd_inverse_from_factor<T>(dA.as<T>(), np, np, dLinv.as<T>(), dV.as<T>(), dC.as<T>(), s);
+    GPRX_HIP(hipStreamSynchronize(s));
+    GPRX_HIP(hipGetLastError());
+    GPRX_HIP(hipMemcpy2D(h.data(), sizeof(T) * n, dC.p, sizeof(T) * np, sizeof(T) * n, n, hipMemcpyDeviceToHost));
+    for (int64_t j = 0; j < n; j++)
+        for (int64_t i = j; i < n; i++) {
+            const T v = h[(size_t)j * n + i];
+            out[(size_t)i * n + j] = v;
+            out[(size_t)j * n + i] = v;
+        }
+    return GPRX_OK;
+}
+
+// ---------------------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------------------
+extern "C" {
+
+int gprx_abi_version(void) { return GPRX_ABI_VERSION; }
+
+gprx_status gprx_device_count(int* count) {
+    API_BEGIN
+    int c = 0;
+    hipError_t e = hipGetDeviceCount(&c);
+    if (e != hipSuccess) c = 0;
+    if (count) *count = c;
+    return GPRX_OK;
+    API_END(nullptr)
+}
+
+gprx_status gprx_ctx_create(int device, gprx_ctx** out) {
+    API_BEGIN
+    GPRX_REQUIRE(out, GPRX_ERR_ARG, "gprx_ctx_create: out is NULL");
+    int c = 0;
+    if (hipGetDeviceCount(&c) != hipSuccess || c == 0)
+        throw Error{GPRX_ERR_NO_DEVICE, "gprx_ctx_create: no HIP device visible (libgprx has no CPU fallback)"};
+    GPRX_REQUIRE(device >= 0 && device < c, GPRX_ERR_ARG, "gprx_ctx_create: bad device index");
+    GPRX_HIP(hipSetDevice(device));
+    gprx_ctx* ctx = new gprx_ctx();
+    ctx->device = device;
+    // The main stream carries the factorisation's critical path (panel chain): give it the
+    // highest priority so its small kernels are dispatched ahead of the bulk trailing update
+    // running on the aux stream.
+    int prio_lo = 0, prio_hi = 0;
+    GPRX_HIP(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+    GPRX_HIP(hipStreamCreateWithPriority(&ctx->stream, hipStreamNonBlocking, prio_hi));
+    GPRX_HIP(hipStreamCreateWithPriority(&ctx->aux, hipStreamNonBlocking, prio_lo));
+    ctx->ex.s0 = ctx->stream;
+    ctx->ex.s1 = ctx->aux;
+    for (auto& e : ctx->ev) GPRX_HIP(hipEventCreate(&e));
+    *out = ctx;
+    return GPRX_OK;
+    API_END(nullptr)
+}
+
+void gprx_ctx_destroy(gprx_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    for (auto& e : ctx->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
+    delete ctx;
+}
+
+const char* gprx_last_error(const gprx_ctx* ctx) { return ctx ? ctx->err.c_str() : t_last_error.c_str(); }
+
+gprx_status gprx_model_create(gprx_ctx* ctx, gprx_dtype dtype, gprx_model** out) {
+    API_BEGIN
+    GPRX_REQUIRE(ctx && out, GPRX_ERR_ARG, "gprx_model_create: NULL argument");
+    GPRX_REQUIRE(dtype == GPRX_F32 || dtype == GPRX_F64, GPRX_ERR_ARG, "gprx_model_create: bad dtype");
+    gprx_model* m = new gprx_model();
+    m->ctx = ctx;
+    m->dt = dtype;
+    *out = m;
+    return GPRX_OK;
+    API_END(ctx)
+}
+
+void gprx_model_destroy(gprx_model* model) {
+    if (!model) return;
+    (void)hipSetDevice(model->ctx->device);
+    delete model;
+}
+
+gprx_status gprx_model_set_data(gprx_model* M, const void* X, const void* Y, int64_t n, int32_t d, int32_t m) {
+    gprx_ctx* ctx = M ? M->ctx : nullptr;
+    API_BEGIN
+    GPRX_REQUIRE(M && X && Y, GPRX_ERR_ARG, "gprx_model_set_data: NULL argument");
+    GPRX_REQUIRE(n > 0, GPRX_ERR_STATE, "GaussianProcess::Initialize: no input samples defined during initialization");
+    GPRX_REQUIRE(d > 0 && m > 0, GPRX_ERR_DIM, "gprx_model_set_data: input and output dimensions must be positive");
+    std::lock_guard<std::mutex> lk(M->mu);
+    GPRX_HIP(hipSetDevice(ctx->device));
+    const size_t es = esize(M->dt);
+    M->X.ensure(es * n * d);
+    M->Y.ensure(es * n * m);
+    GPRX_HIP(hipMemcpy(M->X.p, X, es * n * d, hipMemcpyHostToDevice));
+    GPRX_HIP(hipMemcpy(M->Y.p, Y, es * n * m, hipMemcpyHostToDevice));
+    M->n = n;
+    M->d = d;
+    M->m = m;
+    M->has_data = true;
+    M->fitted = false;
+    return GPRX_OK;
+    API_END(ctx)
+}
+
+gprx_status gprx_model_set_kernel(gprx_model* M, const gprx_kernel_desc* k) {
+    gprx_ctx* ctx = M ? M->ctx : nullptr;
+    API_BEGIN
+    GPRX_REQUIRE(M && k, GPRX_ERR_ARG, "gprx_model_set_kernel: NULL argument");
+    std::lock_guard<std::mutex> lk(M->mu);
+    std::string e = (M->dt == GPRX_F64) ? canonicalize<double>(*k, M->kd) : canonicalize<float>(*k, M->kf);
+    GPRX_REQUIRE(e.empty(), GPRX_ERR_ARG, e);
+    M->desc = *k;
+    M->has_kernel = true;
+    M->fitted = false;
+    return GPRX_OK;
+    API_END(ctx)
+}
+
+gprx_status gprx_model_set_noise(gprx_model* M, double sigma) {
+    gprx_ctx* ctx = M ? M->ctx : nullptr;
+    API_BEGIN
+    GPRX_REQUIRE(M, GPRX_ERR_ARG, "gprx_model_set_noise: NULL model");
+    std::lock_guard<std::mutex> lk(M->mu);
+    M->sigma = sigma;
+    M->fitted = false;
+    return GPRX_OK;
+    API_END(ctx)
+}
+
+gprx_status gprx_model_fit(gprx_model* M, uint32_t flags, gprx_fit_info* info) {
+    gprx_ctx* ctx = M ? M->ctx : nullptr;
+    API_BEGIN
+    ProfBind pb_(ctx);
+    GPRX_REQUIRE(M, GPRX_ERR_ARG, "gprx_model_fit: NULL model");
+    std::lock_guard<std::mutex> lk(M->mu);
+    return M->dt == GPRX_F64 ? model_fit<double>(M, flags, info) : model_fit<float>(M, flags, info);
+    API_END(ctx)
+}
+
+gprx_status gprx_model_get_alpha(gprx_model* M, void* alpha) {
+    gprx_ctx* ctx = M ? M->ctx : nullptr;
+    API_BEGIN
+    GPRX_REQUIRE(M && alpha, GPRX_ERR_ARG, "gprx_model_get_alpha: NULL argument");
+    std::lock_guard<std::mutex> lk(M->mu);
+    GPRX_REQUIRE(M->fitted, GPRX_ERR_STATE, "gprx: model is not fitted");
+    GPRX_HIP(hipSetDevice(ctx->device));
+    GPRX_HIP(hipMemcpy(alpha, M->alpha.p, esize(M->dt) * M->n * M->m, hipMemcpyDeviceToHost));
+    return GPRX_OK;
+    API_END(ctx)
+}
+
+gprx_status gprx_model_predict(gprx_model* M, const void* Xq, int64_t q, void* mean, void* deriv) {
+    gprx_ctx* ctx = M ? M->ctx : nullptr;
+    API_BEGIN
+    ProfBind pb_(ctx);
+    GPRX_REQUIRE(M && Xq && mean, GPRX_ERR_ARG, "gprx_model_predict: NULL argument");
+    if (q == 0) return GPRX_OK;
+    std::lock_guard<std::mutex> lk(M->mu);
+    GPRX_HIP(hipSetDevice(ctx->device));
+    return M->dt == GPRX_F64 ? model_predict<double>(M, Xq, q, mean, deriv)
+                             : model_predict<float>(M, Xq, q, mean, deriv);
+    API_END(ctx)
+}
+
+gprx_status gprx_model_posterior_cov(gprx_model* M, const void* Xa, const void* Xb, int64_t q, void* out) {
+    gprx_ctx* ctx = M ? M->ctx : nullptr;
+    API_BEGIN
+    ProfBind pb_(ctx);
+    GPRX_REQUIRE(M && Xa && Xb && out, GPRX_ERR_ARG, "gprx_model_posterior_cov: NULL argument");
+    if (q == 0) return GPRX_OK;
+    std::lock_guard<std::mutex> lk(M->mu);
+    GPRX_HIP(hipSetDevice(ctx->device));
+    return M->dt == GPRX_F64 ? model_posterior_cov<double>(M, Xa, Xb, q, out)
+                             : model_posterior_cov<float>(M, Xa, Xb, q, out);
+    API_END(ctx)
+}
+
+gprx_status gprx_model_core_matrix(gprx_model* M, void* C) {
+    gprx_ctx* ctx = M ? M->ctx : nullptr;
+    API_BEGIN
+    ProfBind pb_(ctx);
+    GPRX_REQUIRE(M && C, GPRX_ERR_ARG, "gprx_model_core_matrix: NULL argument");
+    std::lock_guard<std::mutex> lk(M->mu);
+    GPRX_HIP(hipSetDevice(ctx->device));
+    return M->dt == GPRX_F64 ? model_core_matrix<double>(M, C) : model_core_matrix<float>(M, C);
+    API_END(ctx)
+}
+
+gprx_status gprx_model_lml(gprx_model* M, uint32_t flags, double* value, double* grad, int32_t* nparams,
+                           double* logdet) {
+    gprx_ctx* ctx = M ? M->ctx : nullptr;
+    API_BEGIN
+    ProfBind pb_(ctx);
+    GPRX_REQUIRE(M, GPRX_ERR_ARG, "gprx_model_lml: NULL model");
+    std::lock_guard<std::mutex> lk(M->mu);
+    GPRX_HIP(hipSetDevice(ctx->device));
+    return M->dt == GPRX_F64 ? model_lml<double>(M, flags, value, grad, nparams, logdet)
+                             : model_lml<float>(M, flags, value, grad, nparams, logdet);
+    API_END(ctx)
+}
+
+gprx_status gprx_kernel_matrix(gprx_ctx* ctx, gprx_dtype dt, const gprx_kernel_desc* k, const void* X, int64_t n,
+                               int32_t d, void* K) {
+    API_BEGIN
+    ProfBind pb_(ctx);
+    GPRX_REQUIRE(ctx && k && X && K, GPRX_ERR_ARG, "gprx_kernel_matrix: NULL argument");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    GPRX_HIP(hipSetDevice(ctx->device));
+    return dt == GPRX_F64 ? kernel_matrix_impl<double>(ctx, k, X, n, d, K, false)
+                          : kernel_matrix_impl<float>(ctx, k, X, n, d, K, false);
+    API_END(ctx)
+}
+
+gprx_status gprx_deriv_matrix(gprx_ctx* ctx, gprx_dtype dt, const gprx_kernel_desc* k, const void* X, int64_t n,
+                              int32_t d, void* D) {
+    API_BEGIN
+    ProfBind pb_(ctx);
+    GPRX_REQUIRE(ctx && k && X && D, GPRX_ERR_ARG, "gprx_deriv_matrix: NULL argument");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    GPRX_HIP(hipSetDevice(ctx->device));
+    return dt == GPRX_F64 ? kernel_matrix_impl<double>(ctx, k, X, n, d, D, true)
+                          : kernel_matrix_impl<float>(ctx, k, X, n, d, D, true);
+    API_END(ctx)
+}
+
+gprx_status gprx_cross_matrix(gprx_ctx* ctx, gprx_dtype dt, const gprx_kernel_desc* k, const void* A, int64_t na,
+                              const void* B, int64_t nb, int32_t d, void* K) {
+    API_BEGIN
+    ProfBind pb_(ctx);
+    GPRX_REQUIRE(ctx && k && A && B && K, GPRX_ERR_ARG, "gprx_cross_matrix: NULL argument");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    GPRX_HIP(hipSetDevice(ctx->device));
+    return dt == GPRX_F64 ? cross_matrix_impl<double>(ctx, k, A, na, B, nb, d, K)
+                          : cross_matrix_impl<float>(ctx, k, A, na, B, nb, d, K);
+    API_END(ctx)
+}
+
+gprx_status gprx_cholesky(gprx_ctx* ctx, gprx_dtype dt, void* A, int64_t n, int32_t* info) {
+    API_BEGIN
+    ProfBind pb_(ctx);
+    GPRX_REQUIRE(ctx && A && n > 0, GPRX_ERR_ARG, "gprx_cholesky: bad argument");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    GPRX_HIP(hipSetDevice(ctx->device));
+    gprx_status st = dt == GPRX_F64 ? cholesky_impl<double>(ctx, A, n, info, false)
+                                    : cholesky_impl<float>(ctx, A, n, info, false);
+    if (st == GPRX_ERR_NOT_SPD) return fail(ctx, st, "gprx_cholesky: matrix is not positive definite");
+    return st;
+    API_END(ctx)
+}
+
+gprx_status gprx_spd_inverse(gprx_ctx* ctx, gprx_dtype dt, void* A, int64_t n, int32_t* info) {
+    API_BEGIN
+    ProfBind pb_(ctx);
+    GPRX_REQUIRE(ctx && A && n > 0, GPRX_ERR_ARG, "gprx_spd_inverse: bad argument");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    GPRX_HIP(hipSetDevice(ctx->device));
+    return dt == GPRX_F64 ? cholesky_impl<double>(ctx, A, n, info, true) : cholesky_impl<float>(ctx, A, n, info, true);
+    API_END(ctx)
+}
+
+static const char* kclass_name(int c) {
+    static const char* names[KC_COUNT] = {"kbuild", "potrf_diag", "potrf_trsm", "potrf_update", "backsolve",
+                                          "predict", "lml_grad", "spd_inverse", "other_gemm"};
+    return names[c];
+}
+
+gprx_status gprx_ctx_set_stats(gprx_ctx* ctx, int32_t enable) {
+    API_BEGIN
+    GPRX_REQUIRE(ctx, GPRX_ERR_ARG, "gprx_ctx_set_stats: NULL ctx");
+    ctx->prof.on = enable != 0;
+    ctx->prof.reset();
+    return GPRX_OK;
+    API_END(ctx)
+}
+
+gprx_status gprx_ctx_get_stats(gprx_ctx* ctx, gprx_kstat* out, int32_t max, int32_t* count) {
+    API_BEGIN
+    GPRX_REQUIRE(ctx, GPRX_ERR_ARG, "gprx_ctx_get_stats: NULL ctx");
+    int k = 0;
+    for (int c = 0; c < KC_COUNT; c++) {
+        const Prof::Acc& a = ctx->prof.acc[c];
+        if (a.launches == 0) continue;
+        if (out && k < max) {
+            std::memset(&out[k], 0, sizeof(gprx_kstat));
+            std::strncpy(out[k].name, kclass_name(c), sizeof(out[k].name) - 1);
+            out[k].launches = a.launches;
+            out[k].ms = a.ms;
+            out[k].flops = a.flops;
+            out[k].bytes = a.bytes;
+        }
+        k++;
+    }
+    if (count) *count = k;
+    return GPRX_OK;
+    API_END(ctx)
+}
+
+gprx_status gprx_dist_unique_id(void* out) {
+    return fail(nullptr, GPRX_ERR_RCCL, "gprx_dist_unique_id: multi-GPU path not built yet");
+    (void)out;
+}
+
+gprx_status gprx_ctx_create_dist(int device, int rank, int world, const void* unique_id, gprx_ctx** out) {
+    (void)device;
+    (void)rank;
+    (void)world;
+    (void)unique_id;
+    (void)out;
+    return fail(nullptr, GPRX_ERR_RCCL, "gprx_ctx_create_dist: multi-GPU path not built yet");
+}
+
+gprx_status gprx_sparse_fit(gprx_ctx* ctx, gprx_dtype dtype, const gprx_kernel_desc* kernel, const void* X,
+                            const void* Y, int64_t n, int32_t d, int32_t m, const void* Xm, int64_t M, double sigma,
+                            double jitter, void* Kinv, void* RV, void* RM) {
+    (void)dtype; (void)kernel; (void)X; (void)Y; (void)n; (void)d; (void)m; (void)Xm; (void)M; (void)sigma;
+    (void)jitter; (void)Kinv; (void)RV; (void)RM;
+    return fail(ctx, GPRX_ERR_STATE, "gprx_sparse_fit: not built yet");
+}
+
+}  // extern "C"

@@ -1,0 +1,325 @@
+// gprx_internal.h — shared declarations of libgprx (MI355X / gfx950).
+//
+// Kernel representation on the device
+// -----------------------------------
+// The reference evaluates a covariance pair through a virtual call per node
+// (include/Kernel.h:52, Sum :165, Product :314).  On the GPU the tree is canonicalised on
+// the host into a SUM OF PRODUCTS OF LEAVES: k = sum_t prod_{l in t} leaf_l.  Every leaf
+// depends on the pair only through a few streaming statistics that are accumulated over
+// the d input dimensions in one pass:
+//     r2        = sum_k (x_k - y_k)^2                 (Gaussian, GaussianExp, RQ, White)
+//     S_p       = sum_k sin^2(b_p (x_k - y_k))         (Periodic leaf p)
+//     F_p       = sum_k 2 (x_k-y_k) sin cos(b_p(...))  (Periodic d/db, gradient only)
+// sin(b(x-y)) is formed from per-sample sin/cos tables (sin(bx)cos(by) - cos(bx)sin(by)),
+// so the pair loop is pure FMA work.  Leaf and term loops have compile-time trip counts
+// (MAX_LEAF / MAX_TERM), so all per-pair state lives in registers.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "../../include/gprx.h"
+
+namespace gprx {
+
+constexpr int MAX_LEAF = 8;
+constexpr int MAX_TERM = 16;
+constexpr int MAX_PER = 2;  // periodic leaves with distinct tables
+
+enum LeafType { L_GAUSS = 1, L_GAUSS_EXP = 2, L_WHITE = 3, L_RQ = 4, L_PERIODIC = 5 };
+
+template <typename T>
+struct KLeaf {
+    int type;
+    int pslot;   // periodic table slot
+    T c0, c1, c2;  // value constants (see leaf_value)
+    T p[3];        // raw reference parameters (gradient formulas)
+};
+
+template <typename T>
+struct KCanon {
+    int nleaf;
+    int nterm;
+    int nper;
+    int need_r2;
+    int nparams;
+    int sum_leaves;  // every term is a single leaf: k = sum_l leaf_l
+    unsigned term_mask[MAX_TERM];
+    int param_base[MAX_LEAF];
+    KLeaf<T> leaf[MAX_LEAF];
+    T b[MAX_PER];
+};
+
+// Build the canonical form from the ABI post-order program.  Returns "" on success or an
+// error message.  Parameters are narrowed to T first (the reference stores them in T).
+template <typename T>
+std::string canonicalize(const gprx_kernel_desc& desc, KCanon<T>& out);
+
+// ---------------------------------------------------------------------------------
+// Leaf evaluation (device + host).  Formulas follow include/Kernel.h:
+//   Gaussian       s^2 exp(-0.5 r2 / sigma^2)                      :465-468
+//   GaussianExp    exp(scale)^2 exp(-0.5 r2 / exp(sigma)^2)         :580-585
+//   White          r2 == 0 ? s^2 : 0 (exact equality)               :695-702
+//   RQ             s^2 (1 + 0.5 r2 / (sigma^2 alpha))^(-alpha)      :794-797
+//   Periodic       s^2 exp(-0.5 S / sigma^2)                        :912-920
+// ---------------------------------------------------------------------------------
+template <typename T>
+__host__ __device__ inline T leaf_value(const KLeaf<T>& L, T r2, T s0, T s1) {
+    switch (L.type) {
+        case L_GAUSS:
+        case L_GAUSS_EXP:
+            return L.c0 * exp(L.c1 * r2);
+        case L_WHITE:
+            return (r2 == T(0)) ? L.c0 : T(0);
+        case L_RQ:
+            return L.c0 * exp(-L.c2 * log1p(L.c1 * r2));
+        case L_PERIODIC:
+            return L.c0 * exp(L.c1 * (L.pslot == 0 ? s0 : s1));
+    }
+    return T(0);
+}
+
+// d leaf / d params (up to 3), the reference's GetDerivative formulas
+// (Gaussian :471-479, GaussianExp :588-598, White :704-713, RQ :799-808, Periodic :922-948).
+template <typename T>
+__host__ __device__ inline void leaf_grad(const KLeaf<T>& L, T r2, T s0, T s1, T f0, T f1, T* g) {
+    switch (L.type) {
+        case L_GAUSS: {  // p = (sigma, scale)
+            T sig = L.p[0], sc = L.p[1];
+            T f = exp(L.c1 * r2);
+            g[0] = sc * sc * r2 / (sig * sig * sig) * f;
+            g[1] = T(2) * sc * f;
+            g[2] = 0;
+            return;
+        }
+        case L_GAUSS_EXP: {  // p = (sigma, scale) in log space
+            T sig = L.p[0], sc = L.p[1];
+            T e2 = exp(T(-2) * sig);
+            g[0] = r2 * exp(T(2) * sc - T(2) * sig - T(0.5) * r2 * e2);
+            g[1] = T(2) * exp(T(2) * sc - T(0.5) * r2 * e2);
+            g[2] = 0;
+            return;
+        }
+        case L_WHITE: {
+            g[0] = (r2 == T(0)) ? T(2) * L.p[0] : T(0);
+            g[1] = 0;
+            g[2] = 0;
+            return;
+        }
+        case L_RQ: {  // p = (scale, sigma, alpha)
+            T sc = L.p[0], sig = L.p[1], al = L.p[2];
+            T f = T(0.5) * r2 / (sig * sig * al) + T(1);
+            T lf = log(f);
+            T pw = exp(-al * lf);
+            g[0] = T(2) * sc * pw;
+            g[1] = sc * sc * r2 * pw / f / (sig * sig * sig);
+            g[2] = sc * sc * (r2 / (T(2) * sig * sig * f * al) - lf) * pw;
+            return;
+        }
+        case L_PERIODIC: {  // p = (scale, b, sigma)
+            T sc = L.p[0], sig = L.p[2];
+            T s = (L.pslot == 0) ? s0 : s1, fb = (L.pslot == 0) ? f0 : f1;
+            T e = exp(L.c1 * s);
+            g[0] = T(2) * sc * e;
+            g[1] = T(-0.5) * sc * sc * e * fb / (sig * sig);
+            g[2] = sc * sc * e * s / (sig * sig * sig);
+            return;
+        }
+    }
+    g[0] = g[1] = g[2] = 0;
+}
+
+// Value of the whole kernel from the pair statistics.
+template <typename T>
+__host__ __device__ inline T kernel_value(const KCanon<T>& K, T r2, T s0, T s1) {
+    T lv[MAX_LEAF];
+#pragma unroll
+    for (int l = 0; l < MAX_LEAF; l++) lv[l] = (l < K.nleaf) ? leaf_value(K.leaf[l], r2, s0, s1) : T(0);
+    if (K.sum_leaves) {
+        T v = lv[0];
+#pragma unroll
+        for (int l = 1; l < MAX_LEAF; l++)
+            if (l < K.nleaf) v += lv[l];
+        return v;
+    }
+    T v = 0;
+#pragma unroll
+    for (int t = 0; t < MAX_TERM; t++) {
+        if (t < K.nterm) {
+            unsigned m = K.term_mask[t];
+            T p = 1;
+#pragma unroll
+            for (int l = 0; l < MAX_LEAF; l++)
+                if (m & (1u << l)) p *= lv[l];
+            v += p;
+        }
+    }
+    return v;
+}
+
+// sincos for both scalar types
+__device__ inline void gsincos(double x, double* s, double* c) { sincos(x, s, c); }
+__device__ inline void gsincos(float x, float* s, float* c) { sincosf(x, s, c); }
+
+// ---------------------------------------------------------------------------------
+// Error helpers (host)
+// ---------------------------------------------------------------------------------
+struct Error {
+    gprx_status st;
+    std::string msg;
+};
+
+#define GPRX_HIP(call)                                                                             \
+    do {                                                                                           \
+        hipError_t e_ = (call);                                                                    \
+        if (e_ != hipSuccess)                                                                      \
+            throw ::gprx::Error{e_ == hipErrorOutOfMemory ? GPRX_ERR_OOM : GPRX_ERR_HIP,           \
+                                std::string(#call) + ": " + hipGetErrorString(e_)};                \
+    } while (0)
+
+#define GPRX_REQUIRE(cond, status, msg)                                                            \
+    do {                                                                                           \
+        if (!(cond)) throw ::gprx::Error{status, msg};                                             \
+    } while (0)
+
+
+// ---------------------------------------------------------------------------------
+// Opt-in per-kernel device timing (gprx_ctx_set_stats): HIP events around every launch
+// of the classes below, on the stream the kernel is launched on.
+// ---------------------------------------------------------------------------------
+enum KClass { KC_BUILD = 0, KC_DIAG, KC_TRSM, KC_UPDATE, KC_BACKSOLVE, KC_PREDICT, KC_LML_GRAD, KC_INVERSE, KC_OTHER,
+              KC_COUNT };
+struct Prof {
+    bool on = false;
+    struct Rec {
+        int cls;
+        hipEvent_t a, b;
+        double flops, bytes;
+    };
+    struct Acc {
+        int64_t launches = 0;
+        double ms = 0, flops = 0, bytes = 0;
+    };
+    std::vector<hipEvent_t> pool;
+    size_t used = 0;
+    std::vector<Rec> recs;
+    Acc acc[KC_COUNT];
+    hipEvent_t next() {
+        if (used == pool.size()) {
+            hipEvent_t e;
+            (void)hipEventCreate(&e);
+            pool.push_back(e);
+        }
+        return pool[used++];
+    }
+    void resolve() {  // caller has synchronised the streams
+        for (auto& r : recs) {
+            float ms = 0;
+            (void)hipEventElapsedTime(&ms, r.a, r.b);
+            acc[r.cls].launches++;
+            acc[r.cls].ms += ms;
+            acc[r.cls].flops += r.flops;
+            acc[r.cls].bytes += r.bytes;
+        }
+        recs.clear();
+        used = 0;
+    }
+    void reset() {
+        recs.clear();
+        used = 0;
+        for (auto& a : acc) a = Acc();
+    }
+    ~Prof() {
+        for (auto e : pool) (void)hipEventDestroy(e);
+    }
+};
+extern thread_local Prof* g_prof;
+
+struct ProfScope {
+    Prof* p;
+    int cls;
+    hipStream_t s;
+    double flops, bytes;
+    hipEvent_t a = nullptr;
+    ProfScope(int c, hipStream_t st, double f = 0, double b = 0) : p(g_prof), cls(c), s(st), flops(f), bytes(b) {
+        if (p && p->on) {
+            a = p->next();
+            (void)hipEventRecord(a, s);
+        }
+    }
+    ~ProfScope() {
+        if (p && p->on) {
+            hipEvent_t b = p->next();
+            (void)hipEventRecord(b, s);
+            p->recs.push_back(Prof::Rec{cls, a, b, flops, bytes});
+        }
+    }
+};
+
+// ---------------------------------------------------------------------------------
+// Launchers implemented in the .hip files.  All device matrices are column-major.
+// ---------------------------------------------------------------------------------
+constexpr int BT = 64;     // build tile edge
+constexpr int DB = 128;    // Cholesky diagonal block edge (also the padding granule)
+constexpr int GT = 128;    // GEMM output tile edge
+
+// per-sample sin/cos tables for the periodic leaves: tab[(slot*2 + {0:sin,1:cos})][i*d + k]
+template <typename T>
+void launch_sincos_tables(const KCanon<T>& K, const T* X, int64_t n, int d, T* tab, hipStream_t s);
+
+// Covariance tiles.  lower=true: square lower-triangle build of K(X,X) into A (column-major,
+// ld), rows/cols >= n padded with the identity, sigma2 added to the diagonal (for i < n).
+// lower=false: rectangular cross matrix K(Xa, Xb) (na x nb) into A.
+template <typename T>
+void launch_kbuild(const KCanon<T>& K, const T* Xa, const T* tabA, int64_t na, const T* Xb, const T* tabB,
+                   int64_t nb, int d, T* A, int64_t ld, int64_t npad, bool lower, T sigma2, int* flag,
+                   hipStream_t s);
+
+// Stacked derivative matrices (tests): D[p] (n x n, column-major, ld = n).
+template <typename T>
+void launch_deriv_matrix(const KCanon<T>& K, const T* X, const T* tab, int64_t n, int d, T* D, hipStream_t s);
+
+// Augmented label rows: A[np + r, j] = Y[j, r] (j < n, r < m), zero elsewhere in the block.
+template <typename T>
+void launch_aug_rows(const T* Y, int64_t n, int m, T* A, int64_t ld, int64_t np, int64_t mp, hipStream_t s);
+
+// Blocked right-looking Cholesky of the leading np x np block of A (ld rows; rows np..ld
+// are extra rows solved along: they end up holding (L^{-1} B)^T).  Linv receives the
+// inverses of the np/DB diagonal blocks (DB x DB each, column-major).  info: device int,
+// first failing column (1-based) via atomicMin semantics (initialised to INT_MAX).
+struct Exec {
+    hipStream_t s0 = nullptr;  // main stream (panel chain)
+    hipStream_t s1 = nullptr;  // look-ahead stream (bulk trailing updates); may be null
+    std::vector<hipEvent_t> ev;
+    hipEvent_t event(size_t i);
+    ~Exec();
+};
+int outer_block();
+template <typename T>
+void potrf_blocked(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info, Exec& ex);
+
+// Generic C = beta C + alpha A B^T on GT-multiples (column-major).  lower: only tiles
+// with col-tile <= row-tile are computed, and inside diagonal tiles only row >= col.
+template <typename T>
+void launch_gemm_nt(T* C, int64_t ldc, const T* A, int64_t lda, const T* B, int64_t ldb, int64_t M, int64_t N,
+                    int64_t K, T alpha, T beta, bool lower, hipStream_t s);
+
+// Back substitution L^T alpha = z with z given as the m augmented rows (row-major output
+// alpha: np x m, ld m).  Uses the diagonal-block inverses.
+template <typename T>
+void launch_backsolve(const T* A, int64_t ld, int64_t np, int m, const T* Linv, T* z, T* alpha, hipStream_t s);
+
+// logdet partial = 2 sum log L_ii over i < n, datafit = sum of squares of the augmented
+// rows; results accumulated in double on the device (out[0], out[1]).
+template <typename T>
+void launch_fit_reductions(const T* A, int64_t ld, int64_t n, int64_t np, int m, double* out, hipStream_t s);
+
+// Fused prediction: mean (q x m row-major) and optional derivative (q x d x m).
+template <typename T>
+void launch_predict(const KCanon<T>& K, const T* X, const T* tabX, int64_t n, int d, int m, const T* alpha,
+                    const T* Xq, const T* tabQ, int64_t q, T* mean, T* deriv, T* Z, T* out, hipStream_t s);
+
+}  // namespace gprx

@@ -1,0 +1,635 @@
+// k_potrf.hip — Cholesky factorisation and triangular solves on gfx950.
+//
+// Replaces the reference's factorise/invert step, lapack::lu_invert -> dgetrf_+dgetri_
+// (include/LAPACKUtils.h:38-56, 85-97, the default FullPivotLU branch of
+// GaussianProcess::InvertKernelMatrix, lib/GaussianProcess.cpp:545-559) and the product
+// alpha = C*Y (lib/GaussianProcess.cpp:661), with
+//     K + sigma^2 I = L L^T      (right-looking blocked potrf, 128-wide blocks)
+//     z = L^{-1} Y               (fused: Y^T rides along as extra rows of the matrix)
+//     alpha = L^{-T} z           (blocked back substitution)
+//
+// Per 128-column block k:
+//   diag_potrf_kernel  one workgroup factors the 128x128 diagonal block in LDS (blocked
+//                      Crout, 8-wide column blocks) and forms its inverse Linv_k;
+//   gemm_nt (trsm)     L_ik = A_ik Linv_k^T for every row block below (in place);
+//   gemm_nt (syrk)     A_ij -= L_ik L_jk^T on the lower trailing matrix.
+// gemm_nt is an LDS double-buffered MFMA kernel: v_mfma_f64_16x16x4_f64 (fp64) or
+// v_mfma_f32_16x16x4_f32 (fp32), 128x128 output tile per 256-thread workgroup, 4 waves of
+// 64x64, K staged 16 deep.  The dense fp64 matrix peak of MI355X is 78.6 TFLOP/s.
+#include "gprx_internal.h"
+
+#include <climits>
+#include <cstdlib>
+
+namespace gprx {
+
+// ======================================================================================
+// Diagonal block: factor + inverse, one workgroup of 512 threads (4 per row / column).
+// Every register array below is indexed with compile-time indices only (no scratch).
+// ======================================================================================
+constexpr int LS = DB + 2;  // LDS row stride (elements); even, keeps 16-B alignment
+constexpr int DT = 512;     // threads of the diagonal kernel
+
+template <typename T>
+__device__ __forceinline__ T quad_sum(T v) {
+    v += __shfl_xor(v, 1);
+    v += __shfl_xor(v, 2);
+    return v;
+}
+
+template <typename T>
+__global__ __launch_bounds__(DT) void diag_potrf_kernel(T* __restrict__ A, int64_t ld, T* __restrict__ Linv,
+                                                        int* __restrict__ info, int64_t col0) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    T(*sL)[LS] = reinterpret_cast<T(*)[LS]>(smem_raw);
+    T* sDinv = reinterpret_cast<T*>(smem_raw + sizeof(T) * DB * LS);
+    T(*sS)[8] = reinterpret_cast<T(*)[8]>(smem_raw + sizeof(T) * (DB * LS + DB));  // 8x8 Schur block
+
+    const int t = threadIdx.x;
+    {   // lower triangle, column-major global -> row-major LDS
+        const int r = t & (DB - 1);
+        for (int c = t >> 7; c < DB; c += DT / DB)
+            if (r >= c) sL[r][c] = A[r + (int64_t)c * ld];
+    }
+    __syncthreads();
+
+    const int i = t >> 2;  // row owned by this thread quad
+    const int h = t & 3;
+    bool failed = false;
+    int fail_col = 0;
+
+    // ---- blocked Crout factorisation, 8-wide column blocks ------------------------------
+    for (int j0 = 0; j0 < DB; j0 += 8) {
+        T s[8];
+        const bool active = i >= j0;
+        if (active) {
+#pragma unroll
+            for (int q = 0; q < 8; q++) s[q] = (h == 0 && j0 + q <= i) ? sL[i][j0 + q] : T(0);
+            const int quarter = j0 >> 2;  // even
+            const int kb = h * quarter, ke = kb + quarter;
+            for (int k = kb; k < ke; k += 2) {
+                const T li0 = sL[i][k], li1 = sL[i][k + 1];
+#pragma unroll
+                for (int q = 0; q < 8; q++) {
+                    s[q] = fma(-li0, sL[j0 + q][k], s[q]);
+                    s[q] = fma(-li1, sL[j0 + q][k + 1], s[q]);
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < 8; q++) s[q] = quad_sum(s[q]);
+            if (h == 0 && i < j0 + 8) {
+#pragma unroll
+                for (int q = 0; q < 8; q++)
+                    if (j0 + q <= i) sS[i - j0][q] = s[q];
+            }
+        }
+        __syncthreads();
+        // The 8x8 Schur complement of the diagonal block (in its own LDS buffer, so the
+        // L writes below cannot race these reads), factored redundantly by everyone.
+        T Ld[8][8], dinv[8];
+#pragma unroll
+        for (int c = 0; c < 8; c++) {
+            T dsum = sS[c][c];
+#pragma unroll
+            for (int k = 0; k < c; k++) dsum = fma(-Ld[c][k], Ld[c][k], dsum);
+            if (!(dsum > T(0)) && !failed) {
+                failed = true;
+                fail_col = j0 + c;
+            }
+            const T dg = sqrt(dsum);
+            Ld[c][c] = dg;
+            dinv[c] = T(1) / dg;
+#pragma unroll
+            for (int r = c + 1; r < 8; r++) {
+                T v = sS[r][c];
+#pragma unroll
+                for (int k = 0; k < c; k++) v = fma(-Ld[r][k], Ld[c][k], v);
+                Ld[r][c] = v * dinv[c];
+            }
+        }
+        if (i >= j0 + 8) {
+            T x[8];
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                T v = s[q];
+#pragma unroll
+                for (int q2 = 0; q2 < q; q2++) v = fma(-x[q2], Ld[q][q2], v);
+                x[q] = v * dinv[q];
+            }
+            if (h == 0) {
+#pragma unroll
+                for (int q = 0; q < 8; q++) sL[i][j0 + q] = x[q];
+            }
+        } else if (active && h == 0) {
+#pragma unroll
+            for (int r = 0; r < 8; r++) {
+                if (i == j0 + r) {
+#pragma unroll
+                    for (int c = 0; c <= r; c++) sL[i][j0 + c] = Ld[r][c];
+                }
+            }
+        }
+        __syncthreads();
+    }
+    if (t == 0 && failed) atomicMin(info, (int)(col0 + fail_col + 1));
+
+    {   // L (lower) back to global
+        const int r = t & (DB - 1);
+        for (int c = t >> 7; c < DB; c += DT / DB)
+            if (r >= c) A[r + (int64_t)c * ld] = sL[r][c];
+    }
+    // ---- Linv = L^{-1}: column c owned by a thread quad, stored transposed in the free
+    //      upper triangle (sL[c][k] = Linv[k][c], k > c) plus sDinv[c] = 1 / L[c][c].
+    if (h == 0) sDinv[i] = T(1) / sL[i][i];
+    __syncthreads();
+    {
+        const int c = i;
+        const T dinv_c = sDinv[c];
+        for (int i0 = (c & ~7); i0 < DB; i0 += 8) {
+            T acc[8];
+#pragma unroll
+            for (int r = 0; r < 8; r++) acc[r] = T(0);
+            if (i0 > c) {  // acc[r] = sum_{k=c}^{i0-1} L[i0+r][k] Linv[k][c]
+                if (h == 0) {
+#pragma unroll
+                    for (int r = 0; r < 8; r++) acc[r] = sL[i0 + r][c] * dinv_c;
+                }
+                const int kb0 = c + 1, len = i0 - kb0;
+                const int kb = kb0 + (h * len) / 4, ke = kb0 + ((h + 1) * len) / 4;
+                for (int k = kb; k < ke; k++) {
+                    const T u = sL[c][k];
+#pragma unroll
+                    for (int r = 0; r < 8; r++) acc[r] = fma(sL[i0 + r][k], u, acc[r]);
+                }
+#pragma unroll
+                for (int r = 0; r < 8; r++) acc[r] = quad_sum(acc[r]);
+            }
+            T x[8];
+#pragma unroll
+            for (int r = 0; r < 8; r++) {
+                const int row = i0 + r;
+                if (row < c) {
+                    x[r] = T(0);
+                } else if (row == c) {
+                    x[r] = dinv_c;
+                } else {
+                    T v = -acc[r];
+#pragma unroll
+                    for (int r2 = 0; r2 < r; r2++) v = fma(-sL[row][i0 + r2], x[r2], v);
+                    x[r] = v * sDinv[row];
+                }
+            }
+            if (h == 0) {
+#pragma unroll
+                for (int r = 0; r < 8; r++)
+                    if (i0 + r > c) sL[c][i0 + r] = x[r];
+            }
+        }
+    }
+    __syncthreads();
+    {   // Linv -> global (column-major, ld = DB, zeros above the diagonal)
+        const int r = t & (DB - 1);
+        for (int c = t >> 7; c < DB; c += DT / DB) {
+            const T v = (r > c) ? sL[c][r] : ((r == c) ? sDinv[c] : T(0));
+            Linv[r + c * DB] = v;
+        }
+    }
+}
+
+// ======================================================================================
+// MFMA GEMM  C = beta C + alpha A B^T   (all column-major, sizes multiples of 128 / 16)
+// ======================================================================================
+constexpr int BK = 16;
+constexpr int PADT = 16;
+constexpr int SROW = GT + PADT;  // LDS row (one k) length in elements
+
+typedef double d4_t __attribute__((ext_vector_type(4)));
+typedef float f4_t __attribute__((ext_vector_type(4)));
+typedef double d2_t __attribute__((ext_vector_type(2)));
+typedef float f4v_t __attribute__((ext_vector_type(4)));
+
+template <typename T>
+struct MfmaTraits;
+template <>
+struct MfmaTraits<double> {
+    typedef d4_t acc_t;
+    typedef d2_t vec_t;  // 16-byte global/LDS move
+    static constexpr int VEC = 2;
+    __device__ static inline acc_t mma(double a, double b, acc_t c) {
+        return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+    }
+    // output row (within the 16x16 block) of accumulator register `reg` for lane group lk
+    __device__ static inline int orow(int lk, int reg) { return lk + 4 * reg; }
+};
+template <>
+struct MfmaTraits<float> {
+    typedef f4_t acc_t;
+    typedef f4v_t vec_t;
+    static constexpr int VEC = 4;
+    __device__ static inline acc_t mma(float a, float b, acc_t c) {
+        return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+    }
+    __device__ static inline int orow(int lk, int reg) { return 4 * lk + reg; }
+};
+
+template <typename T, bool LOWER, bool BETA, bool KSKIP>
+__global__ __launch_bounds__(256, 2) void gemm_nt_kernel(T* __restrict__ C, int64_t ldc, const T* __restrict__ A,
+                                                         int64_t lda, const T* __restrict__ B, int64_t ldb,
+                                                         int64_t K, T alpha, T beta, int64_t ntm, int64_t ntn) {
+    typedef MfmaTraits<T> Tr;
+    typedef typename Tr::acc_t acc_t;
+    typedef typename Tr::vec_t vec_t;
+    constexpr int VEC = Tr::VEC;
+    constexpr int TPC = GT / VEC;       // threads per staged column
+    constexpr int CPP = 256 / TPC;      // columns per pass
+    constexpr int PASSES = BK / CPP;
+
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    T* sA = reinterpret_cast<T*>(smem_raw);            // [2][BK][SROW]
+    T* sB = sA + 2 * BK * SROW;                          // [2][BK][SROW]
+
+    // ---- tile coordinates ---------------------------------------------------------------
+    int64_t ti, tj;
+    {
+        const int64_t b = blockIdx.x;
+        if (LOWER) {
+            const int64_t tri = ntn * (ntn + 1) / 2;
+            if (b < tri) {
+                int64_t i = (int64_t)((sqrt(8.0 * (double)b + 1.0) - 1.0) * 0.5);
+                while ((i + 1) * (i + 2) / 2 <= b) i++;
+                while (i * (i + 1) / 2 > b) i--;
+                ti = i;
+                tj = b - i * (i + 1) / 2;
+            } else {
+                const int64_t b2 = b - tri;
+                ti = ntn + b2 / ntn;
+                tj = b2 % ntn;
+            }
+        } else {
+            ti = b % ntm;
+            tj = b / ntm;
+        }
+    }
+    const int64_t i0 = ti * GT, j0 = tj * GT;
+    // KSKIP: both operands are zero left of column i0 (C = V V^T with V upper triangular)
+    const int64_t kbeg = KSKIP ? i0 : 0;
+    const T* Ablk = A + i0 + kbeg * lda;
+    const T* Bblk = B + j0 + kbeg * ldb;
+
+    const int t = threadIdx.x;
+    const int lane = t & 63, w = t >> 6;
+    const int wr = w >> 1, wc = w & 1;
+    const int lr = lane & 15, lk = lane >> 4;
+
+    // staging coordinates
+    const int st_row = (t % TPC) * VEC;
+    const int st_col = t / TPC;
+
+    vec_t ra[PASSES], rb[PASSES];
+    auto gload = [&](int64_t k0) {
+#pragma unroll
+        for (int p = 0; p < PASSES; p++) {
+            const int64_t kk = k0 + st_col + p * CPP;
+            ra[p] = *reinterpret_cast<const vec_t*>(Ablk + st_row + kk * lda);
+            rb[p] = *reinterpret_cast<const vec_t*>(Bblk + st_row + kk * ldb);
+        }
+    };
+    auto lstore = [&](int buf) {
+        T* a = sA + buf * BK * SROW;
+        T* bb = sB + buf * BK * SROW;
+#pragma unroll
+        for (int p = 0; p < PASSES; p++) {
+            const int kk = st_col + p * CPP;
+            *reinterpret_cast<vec_t*>(a + kk * SROW + st_row) = ra[p];
+            *reinterpret_cast<vec_t*>(bb + kk * SROW + st_row) = rb[p];
+        }
+    };
+
+    acc_t acc[4][4];
+#pragma unroll
+    for (int x = 0; x < 4; x++)
+#pragma unroll
+        for (int y = 0; y < 4; y++) acc[x][y] = acc_t{0};
+
+    const int nstage = (int)((K - kbeg) / BK);
+    gload(0);
+    lstore(0);
+    __syncthreads();
+    for (int sidx = 0; sidx < nstage; sidx++) {
+        const int buf = sidx & 1;
+        if (sidx + 1 < nstage) gload((int64_t)(sidx + 1) * BK);
+        const T* a = sA + buf * BK * SROW;
+        const T* bb = sB + buf * BK * SROW;
+#pragma unroll
+        for (int kq = 0; kq < BK / 4; kq++) {
+            const int kr = kq * 4 + lk;
+            T fa[4], fb[4];
+#pragma unroll
+            for (int x = 0; x < 4; x++) fb[x] = bb[kr * SROW + wc * 64 + x * 16 + lr];  // MFMA A: our columns
+#pragma unroll
+            for (int y = 0; y < 4; y++) fa[y] = a[kr * SROW + wr * 64 + y * 16 + lr];   // MFMA B: our rows
+#pragma unroll
+            for (int x = 0; x < 4; x++)
+#pragma unroll
+                for (int y = 0; y < 4; y++) acc[x][y] = Tr::mma(fb[x], fa[y], acc[x][y]);
+        }
+        if (sidx + 1 < nstage) lstore(buf ^ 1);
+        __syncthreads();
+    }
+
+    // ---- epilogue: acc[x][y][reg] = C(i = ... y*16 + lr, j = ... x*16 + orow(lk, reg)) ----
+    const bool diag_tile = LOWER && (ti == tj);
+#pragma unroll
+    for (int x = 0; x < 4; x++) {
+#pragma unroll
+        for (int reg = 0; reg < 4; reg++) {
+            const int jl = wc * 64 + x * 16 + Tr::orow(lk, reg);
+            T* ccol = C + (j0 + jl) * ldc + i0;
+#pragma unroll
+            for (int y = 0; y < 4; y++) {
+                const int il = wr * 64 + y * 16 + lr;
+                if (diag_tile && il < jl) continue;
+                T v = alpha * acc[x][y][reg];
+                if (BETA) v = fma(beta, ccol[il], v);
+                ccol[il] = v;
+            }
+        }
+    }
+}
+
+template <typename T>
+static size_t gemm_lds_bytes() {
+    return sizeof(T) * 4 * BK * SROW;
+}
+
+template <typename T>
+void launch_gemm_nt(T* C, int64_t ldc, const T* A, int64_t lda, const T* B, int64_t ldb, int64_t M, int64_t N,
+                    int64_t K, T alpha, T beta, bool lower, hipStream_t s) {
+    if (M <= 0 || N <= 0) return;
+    const int64_t ntm = M / GT, ntn = N / GT;
+    int64_t ntiles;
+    if (lower) {
+        // rows beyond the square part are full tile rows
+        ntiles = ntn * (ntn + 1) / 2 + (ntm - ntn) * ntn;
+    } else {
+        ntiles = ntm * ntn;
+    }
+    const size_t lds = gemm_lds_bytes<T>();
+    const bool use_beta = beta != T(0);
+    const double elems = lower ? ((double)N * (N + 1) / 2 + (double)(M - N) * N) : (double)M * N;
+    ProfScope ps(lower ? KC_UPDATE : (use_beta ? KC_OTHER : KC_TRSM), s, 2.0 * elems * K,
+                 (double)sizeof(T) * (elems * (use_beta ? 2 : 1) + (double)(M + N) * K));
+#define GPRX_GEMM(L, Bt)                                                                                  \
+    do {                                                                                                  \
+        static bool attr_done = false;                                                                    \
+        if (!attr_done) {                                                                                 \
+            hipFuncSetAttribute((const void*)gemm_nt_kernel<T, L, Bt, false>,                             \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                    \
+            attr_done = true;                                                                             \
+        }                                                                                                 \
+        hipLaunchKernelGGL((gemm_nt_kernel<T, L, Bt, false>), dim3((unsigned)ntiles), dim3(256), lds, s, C, ldc, A, \
+                           lda, B, ldb, K, alpha, beta, ntm, ntn);                                        \
+    } while (0)
+    if (lower) {
+        if (use_beta) GPRX_GEMM(true, true);
+        else GPRX_GEMM(true, false);
+    } else {
+        if (use_beta) GPRX_GEMM(false, true);
+        else GPRX_GEMM(false, false);
+    }
+#undef GPRX_GEMM
+}
+
+// C (lower) = A B^T where both operands vanish left of their row (LAUUM shape).
+template <typename T>
+void launch_gemm_nt_kskip(T* C, int64_t ldc, const T* A, int64_t lda, const T* B, int64_t ldb, int64_t M, int64_t N,
+                          int64_t K, hipStream_t s) {
+    if (M <= 0 || N <= 0) return;
+    const int64_t ntm = M / GT, ntn = N / GT;
+    const int64_t ntiles = ntn * (ntn + 1) / 2 + (ntm - ntn) * ntn;
+    const size_t lds = gemm_lds_bytes<T>();
+    ProfScope ps(KC_INVERSE, s, 2.0 * (double)N * N * N / 6.0, 0.0);
+    static bool attr_done = false;
+    if (!attr_done) {
+        hipFuncSetAttribute((const void*)gemm_nt_kernel<T, true, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds);
+        attr_done = true;
+    }
+    hipLaunchKernelGGL((gemm_nt_kernel<T, true, false, true>), dim3((unsigned)ntiles), dim3(256), lds, s, C, ldc, A, lda,
+                       B, ldb, K, T(1), T(0), ntm, ntn);
+}
+
+template <typename T>
+static size_t diag_lds_bytes() {
+    return sizeof(T) * (DB * LS + DB + 64);
+}
+
+template <typename T>
+static void launch_diag(T* Akk, int64_t ld, T* Lk, int* info, int64_t col0, hipStream_t s) {
+    static bool attr_done = false;
+    const size_t lds = diag_lds_bytes<T>();
+    if (!attr_done) {
+        hipFuncSetAttribute((const void*)diag_potrf_kernel<T>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        attr_done = true;
+    }
+    ProfScope ps(KC_DIAG, s, 2.0 * DB * DB * DB / 3.0, 0.0);
+    hipLaunchKernelGGL(diag_potrf_kernel<T>, dim3(1), dim3(DT), lds, s, Akk, ld, Lk, info, col0);
+}
+
+int outer_block() {
+    static int nbo = [] {
+        int v = 256;
+        if (const char* e = std::getenv("GPRX_NBO")) v = std::atoi(e);
+        if (v < DB) v = DB;
+        return (v / DB) * DB;
+    }();
+    return nbo;
+}
+
+hipEvent_t Exec::event(size_t i) {
+    while (ev.size() <= i) {
+        hipEvent_t e;
+        GPRX_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        ev.push_back(e);
+    }
+    return ev[i];
+}
+
+Exec::~Exec() {
+    for (auto e : ev) (void)hipEventDestroy(e);
+}
+
+// Two-level right-looking Cholesky with look-ahead.
+//   Panel(K)      columns [c0, c0+w) of every row below: per 128-block diag + trsm + the
+//                 update of the remaining panel columns (stream P = ex.s0)
+//   TrailNext(K)  next panel's columns -= P_K P_K^T   (stream P)
+//   TrailRest(K)  the rest of the trailing matrix     (stream B = ex.s1, K = w deep)
+// Panel(K+1) runs on P while TrailRest(K) runs on B.
+template <typename T>
+void potrf_blocked(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info, Exec& ex) {
+    const int64_t NBO = outer_block();
+    hipStream_t P = ex.s0, B = ex.s1 ? ex.s1 : ex.s0;
+    const int64_t nK = (np + NBO - 1) / NBO;
+    auto panel = [&](int64_t c0, int64_t w) {
+        for (int64_t kk = c0; kk < c0 + w; kk += DB) {
+            T* Lk = Linv + (kk / DB) * (int64_t)DB * DB;
+            launch_diag<T>(A + kk + kk * ld, ld, Lk, info, kk, P);
+            const int64_t rows_below = nrows - (kk + DB);
+            if (rows_below <= 0) continue;
+            T* Pk = A + (kk + DB) + kk * ld;
+            launch_gemm_nt<T>(Pk, ld, Pk, ld, Lk, DB, rows_below, DB, DB, T(1), T(0), false, P);
+            const int64_t inner = c0 + w - (kk + DB);
+            if (inner > 0)
+                launch_gemm_nt<T>(A + (kk + DB) + (kk + DB) * ld, ld, Pk, ld, Pk, ld, rows_below, inner, DB, T(-1),
+                                  T(1), true, P);
+        }
+    };
+    for (int64_t K = 0; K < nK; K++) {
+        const int64_t c0 = K * NBO, w = std::min(NBO, np - c0);
+        if (K >= 2 && B != P) GPRX_HIP(hipStreamWaitEvent(P, ex.event(2 * (K - 2) + 1), 0));
+        panel(c0, w);
+        if (K == nK - 1) break;
+        const int64_t c1 = c0 + w, wn = std::min(NBO, np - c1);
+        const T* Pan = A + c0 * ld;  // column c0; row offsets added below
+        if (B != P) {
+            GPRX_HIP(hipEventRecord(ex.event(2 * K), P));
+            if (K >= 1) GPRX_HIP(hipStreamWaitEvent(P, ex.event(2 * (K - 1) + 1), 0));
+        }
+        // TrailNext(K)
+        launch_gemm_nt<T>(A + c1 + c1 * ld, ld, Pan + c1, ld, Pan + c1, ld, nrows - c1, wn, w, T(-1), T(1), true, P);
+        // TrailRest(K)
+        const int64_t c2 = c1 + wn;
+        if (B != P) GPRX_HIP(hipStreamWaitEvent(B, ex.event(2 * K), 0));
+        if (c2 < np)
+            launch_gemm_nt<T>(A + c2 + c2 * ld, ld, Pan + c2, ld, Pan + c2, ld, nrows - c2, np - c2, w, T(-1), T(1),
+                              true, B);
+        if (B != P) GPRX_HIP(hipEventRecord(ex.event(2 * K + 1), B));
+    }
+    if (B != P && nK >= 2) GPRX_HIP(hipStreamWaitEvent(P, ex.event(2 * (nK - 2) + 1), 0));
+}
+
+// ======================================================================================
+// Back substitution  L^T alpha = z   (z: m rows of length np, alpha: np x m row-major)
+// ======================================================================================
+template <typename T>
+__global__ void copy_aug_kernel(const T* __restrict__ A, int64_t ld, int64_t np, int m, T* __restrict__ z) {
+    int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= (int64_t)m * np) return;
+    int64_t r = e / np, c = e % np;
+    z[e] = A[np + r + c * ld];
+}
+
+
+// alpha_j = Linv_j^T z_j  (one workgroup)
+template <typename T>
+__global__ __launch_bounds__(DB) void backsolve_alpha_kernel(int64_t np, int m, const T* __restrict__ Linv,
+                                                             const T* __restrict__ z, T* __restrict__ alpha,
+                                                             int64_t j0) {
+    __shared__ T sz[DB];
+    const int t = threadIdx.x;
+    for (int r = 0; r < m; r++) {
+        sz[t] = z[(int64_t)r * np + j0 + t];
+        __syncthreads();
+        const T* col = Linv + t * DB;
+        T acc = 0;
+        for (int p = t; p < DB; p++) acc = fma(col[p], sz[p], acc);
+        alpha[(j0 + t) * m + r] = acc;
+        __syncthreads();
+    }
+}
+
+// z[c] -= sum_p L[j0+p][c] alpha_j[p] for c < j0.  16 lanes per column (each lane 8
+// consecutive rows = 64 contiguous bytes), 4 columns per wave, 16 columns per workgroup.
+constexpr int BS_COLS_WG = 16;
+template <typename T>
+__global__ __launch_bounds__(256) void backsolve_update_kernel(const T* __restrict__ A, int64_t ld, int64_t np, int m,
+                                                               const T* __restrict__ alpha, T* __restrict__ z,
+                                                               int64_t j0) {
+    const int t = threadIdx.x;
+    const int lane = t & 63, w = t >> 6;
+    const int sub = lane >> 4, l16 = lane & 15;
+    const int64_t c = (int64_t)blockIdx.x * BS_COLS_WG + w * 4 + sub;
+    const bool ok = c < j0;
+    T Lv[8];
+    if (ok) {
+        const T* Lc = A + j0 + c * ld + l16 * 8;
+#pragma unroll
+        for (int e = 0; e < 8; e++) Lv[e] = Lc[e];
+    }
+    for (int r = 0; r < m; r++) {
+        T v = 0;
+        if (ok) {
+#pragma unroll
+            for (int e = 0; e < 8; e++) v = fma(Lv[e], alpha[(j0 + l16 * 8 + e) * m + r], v);
+        }
+        v += __shfl_xor(v, 8);
+        v += __shfl_xor(v, 4);
+        v += __shfl_xor(v, 2);
+        v += __shfl_xor(v, 1);
+        if (ok && l16 == 0) z[(int64_t)r * np + c] -= v;
+    }
+}
+
+template <typename T>
+void launch_backsolve(const T* A, int64_t ld, int64_t np, int m, const T* Linv, T* z, T* alpha, hipStream_t s) {
+    const int64_t e = (int64_t)m * np;
+    ProfScope ps(KC_BACKSOLVE, s, 2.0 * (double)np * np * m / 2.0, (double)sizeof(T) * np * (np + 1) / 2.0);
+    hipLaunchKernelGGL(copy_aug_kernel<T>, dim3((unsigned)((e + 255) / 256)), dim3(256), 0, s, A, ld, np, m, z);
+    for (int64_t j0 = np - DB; j0 >= 0; j0 -= DB) {
+        hipLaunchKernelGGL(backsolve_alpha_kernel<T>, dim3(1), dim3(DB), 0, s, np, m,
+                           Linv + (j0 / DB) * (int64_t)DB * DB, (const T*)z, alpha, j0);
+        if (j0 > 0)
+            hipLaunchKernelGGL(backsolve_update_kernel<T>, dim3((unsigned)((j0 + BS_COLS_WG - 1) / BS_COLS_WG)),
+                               dim3(256), 0, s, A, ld, np, m, (const T*)alpha, z, j0);
+    }
+}
+
+// ======================================================================================
+// logdet = 2 sum log L_ii, datafit = || z ||^2  (double accumulation)
+// ======================================================================================
+template <typename T>
+__global__ __launch_bounds__(1024) void fit_reduce_kernel(const T* __restrict__ A, int64_t ld, int64_t n, int64_t np,
+                                                          int m, double* __restrict__ out) {
+    __shared__ double s0[1024], s1[1024];
+    const int t = threadIdx.x;
+    double a = 0, b = 0;
+    for (int64_t i = t; i < n; i += 1024) a += log((double)A[i + i * ld]);
+    for (int64_t e = t; e < (int64_t)m * np; e += 1024) {
+        const int64_t r = e % m, c = e / m;
+        const double v = (double)A[np + r + c * ld];
+        b += v * v;
+    }
+    s0[t] = a;
+    s1[t] = b;
+    __syncthreads();
+    for (int off = 512; off > 0; off >>= 1) {
+        if (t < off) {
+            s0[t] += s0[t + off];
+            s1[t] += s1[t + off];
+        }
+        __syncthreads();
+    }
+    if (t == 0) {
+        out[0] = 2.0 * s0[0];
+        out[1] = s1[0];
+    }
+}
+
+template <typename T>
+void launch_fit_reductions(const T* A, int64_t ld, int64_t n, int64_t np, int m, double* out, hipStream_t s) {
+    hipLaunchKernelGGL(fit_reduce_kernel<T>, dim3(1), dim3(1024), 0, s, A, ld, n, np, m, out);
+}
+
+#define GPRX_INST(T)                                                                                      \
+    template void potrf_blocked<T>(T*, int64_t, int64_t, int64_t, T*, int*, Exec&);                      \
+    template void launch_gemm_nt<T>(T*, int64_t, const T*, int64_t, const T*, int64_t, int64_t, int64_t, \
+                                    int64_t, T, T, bool, hipStream_t);                                    \
+    template void launch_backsolve<T>(const T*, int64_t, int64_t, int, const T*, T*, T*, hipStream_t);   \
+    template void launch_fit_reductions<T>(const T*, int64_t, int64_t, int64_t, int, double*, hipStream_t); \
+    template void launch_gemm_nt_kskip<T>(T*, int64_t, const T*, int64_t, const T*, int64_t, int64_t, int64_t,   \
+                                          int64_t, hipStream_t);
+GPRX_INST(double)
+GPRX_INST(float)
+#undef GPRX_INST
+
+}  // namespace gprx

@@ -1,0 +1,337 @@
+"""ctypes binding of libgprx (include/gprx.h) — the Python face of the drop-in boundary.
+
+This module is the binding a Python caller (tests, bench.py) uses; the C++ host API in
+include/gpr/ binds the same symbols natively.  There is no CPU fallback: if the HIP
+library or a GPU is missing every compute call raises GprxError.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from .kernels import as_node
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libgprx.so")
+
+GPRX_F32 = 0
+GPRX_F64 = 1
+MAX_KNODES = 32
+MAX_KPARAMS = 48
+UNIQUE_ID_BYTES = 128
+
+FIT_DEFAULT = 0
+FIT_NO_LU_FALLBACK = 1
+LML_GRAD = 1
+LML_COMPAT = 2
+
+STATUS = {0: "OK", 1: "NONFINITE", 2: "NOT_SPD", 3: "SINGULAR", 4: "DIM", 5: "HIP", 6: "RCCL", 7: "OOM",
+          8: "ARG", 9: "STATE", 10: "NO_DEVICE"}
+
+# Every symbol include/gprx.h declares (checked by tests/test_abi.py).
+EXPORTED = [
+    "gprx_abi_version", "gprx_device_count", "gprx_ctx_create", "gprx_dist_unique_id", "gprx_ctx_create_dist",
+    "gprx_ctx_destroy", "gprx_last_error", "gprx_model_create", "gprx_model_destroy", "gprx_model_set_data",
+    "gprx_model_set_kernel", "gprx_model_set_noise", "gprx_model_fit", "gprx_model_get_alpha",
+    "gprx_model_predict", "gprx_model_posterior_cov", "gprx_model_core_matrix", "gprx_model_lml",
+    "gprx_kernel_matrix", "gprx_cross_matrix", "gprx_deriv_matrix", "gprx_cholesky", "gprx_spd_inverse",
+    "gprx_sparse_fit", "gprx_ctx_set_stats", "gprx_ctx_get_stats",
+]
+
+
+class GprxError(RuntimeError):
+    def __init__(self, status, msg):
+        super().__init__(f"[{STATUS.get(status, status)}] {msg}")
+        self.status = status
+        self.msg = msg
+
+
+class KNode(ctypes.Structure):
+    _fields_ = [("op", ctypes.c_int32), ("pad", ctypes.c_int32), ("p", ctypes.c_double * 3)]
+
+
+class KernelDesc(ctypes.Structure):
+    _fields_ = [("n_nodes", ctypes.c_int32), ("pad", ctypes.c_int32), ("node", KNode * MAX_KNODES)]
+
+
+class KStat(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char * 32), ("launches", ctypes.c_int64), ("ms", ctypes.c_double),
+                ("flops", ctypes.c_double), ("bytes", ctypes.c_double)]
+
+
+class FitInfo(ctypes.Structure):
+    _fields_ = [("logdet", ctypes.c_double), ("datafit", ctypes.c_double), ("info", ctypes.c_int32),
+                ("method", ctypes.c_int32), ("ms_build", ctypes.c_double), ("ms_factor", ctypes.c_double),
+                ("ms_solve", ctypes.c_double)]
+
+
+_lib = None
+
+
+def lib():
+    """Load libgprx.so (built in-tree by `make` / __graft_entry__.build())."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise GprxError(5, f"libgprx.so not built ({LIB_PATH}); run `make`")
+        L = ctypes.CDLL(LIB_PATH)
+        L.gprx_last_error.restype = ctypes.c_char_p
+        L.gprx_last_error.argtypes = [ctypes.c_void_p]
+        L.gprx_ctx_create.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
+        L.gprx_ctx_create_dist.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                           ctypes.POINTER(ctypes.c_void_p)]
+        L.gprx_ctx_destroy.argtypes = [ctypes.c_void_p]
+        L.gprx_model_create.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
+        L.gprx_model_destroy.argtypes = [ctypes.c_void_p]
+        L.gprx_model_set_data.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                          ctypes.c_int32, ctypes.c_int32]
+        L.gprx_model_set_kernel.argtypes = [ctypes.c_void_p, ctypes.POINTER(KernelDesc)]
+        L.gprx_model_set_noise.argtypes = [ctypes.c_void_p, ctypes.c_double]
+        L.gprx_model_fit.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(FitInfo)]
+        L.gprx_model_get_alpha.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        L.gprx_model_predict.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
+                                         ctypes.c_void_p]
+        L.gprx_model_posterior_cov.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                               ctypes.c_void_p]
+        L.gprx_model_core_matrix.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        L.gprx_model_lml.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_double),
+                                     ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_double)]
+        for f in ("gprx_kernel_matrix", "gprx_deriv_matrix"):
+            getattr(L, f).argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(KernelDesc), ctypes.c_void_p,
+                                      ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p]
+        L.gprx_cross_matrix.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(KernelDesc), ctypes.c_void_p,
+                                        ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
+                                        ctypes.c_void_p]
+        for f in ("gprx_cholesky", "gprx_spd_inverse"):
+            getattr(L, f).argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int64,
+                                      ctypes.POINTER(ctypes.c_int32)]
+        L.gprx_sparse_fit.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(KernelDesc), ctypes.c_void_p,
+                                      ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
+                                      ctypes.c_void_p, ctypes.c_int64, ctypes.c_double, ctypes.c_double,
+                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        L.gprx_dist_unique_id.argtypes = [ctypes.c_void_p]
+        L.gprx_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
+        L.gprx_ctx_set_stats.argtypes = [ctypes.c_void_p, ctypes.c_int32]
+        L.gprx_ctx_get_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(KStat), ctypes.c_int32,
+                                         ctypes.POINTER(ctypes.c_int32)]
+        _lib = L
+    return _lib
+
+
+def _check(st, ctx=None):
+    if st != 0:
+        raise GprxError(st, lib().gprx_last_error(ctx).decode())
+
+
+def kernel_desc(kernel) -> KernelDesc:
+    node = as_node(kernel)
+    prog = node.postorder()
+    if len(prog) > MAX_KNODES:
+        raise GprxError(8, "kernel has too many nodes")
+    d = KernelDesc()
+    d.n_nodes = len(prog)
+    for i, (op, ps) in enumerate(prog):
+        d.node[i].op = op
+        for j, p in enumerate(ps):
+            d.node[i].p[j] = p
+    return d
+
+
+def _dt(dtype):
+    dtype = np.dtype(dtype)
+    if dtype == np.float64:
+        return GPRX_F64
+    if dtype == np.float32:
+        return GPRX_F32
+    raise TypeError(f"unsupported dtype {dtype}")
+
+
+def _ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
+
+
+def device_count():
+    c = ctypes.c_int()
+    _check(lib().gprx_device_count(ctypes.byref(c)))
+    return c.value
+
+
+class Context:
+    """One per process per GPU (gprx_ctx)."""
+
+    def __init__(self, device=0, dist=None):
+        h = ctypes.c_void_p()
+        if dist is None:
+            _check(lib().gprx_ctx_create(device, ctypes.byref(h)))
+        else:
+            rank, world, uid = dist
+            buf = ctypes.create_string_buffer(bytes(uid), UNIQUE_ID_BYTES)
+            _check(lib().gprx_ctx_create_dist(device, rank, world, buf, ctypes.byref(h)))
+        self.h = h
+
+    def close(self):
+        if self.h:
+            lib().gprx_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _c(self, st):
+        _check(st, self.h)
+
+    def set_stats(self, enable=True):
+        """Per-kernel HIP-event timing of the library's launches (gprx_ctx_set_stats)."""
+        self._c(lib().gprx_ctx_set_stats(self.h, 1 if enable else 0))
+
+    def stats(self):
+        arr = (KStat * 16)()
+        cnt = ctypes.c_int32()
+        self._c(lib().gprx_ctx_get_stats(self.h, arr, 16, ctypes.byref(cnt)))
+        return {arr[i].name.decode(): dict(launches=arr[i].launches, ms=arr[i].ms, flops=arr[i].flops,
+                                           bytes=arr[i].bytes) for i in range(min(cnt.value, 16))}
+
+    def kernel_matrix(self, kernel, X, dtype=np.float64):
+        X = np.ascontiguousarray(X, dtype)
+        n, d = X.shape
+        K = np.empty((n, n), dtype)
+        self._c(lib().gprx_kernel_matrix(self.h, _dt(dtype), ctypes.byref(kernel_desc(kernel)), _ptr(X), n, d,
+                                         _ptr(K)))
+        return K
+
+    def deriv_matrix(self, kernel, X, dtype=np.float64):
+        X = np.ascontiguousarray(X, dtype)
+        n, d = X.shape
+        P = as_node(kernel).num_params()
+        D = np.empty((P, n, n), dtype)
+        self._c(lib().gprx_deriv_matrix(self.h, _dt(dtype), ctypes.byref(kernel_desc(kernel)), _ptr(X), n, d,
+                                        _ptr(D)))
+        return D
+
+    def cross_matrix(self, kernel, A, B, dtype=np.float64):
+        A = np.ascontiguousarray(A, dtype)
+        B = np.ascontiguousarray(B, dtype)
+        K = np.empty((A.shape[0], B.shape[0]), dtype)
+        self._c(lib().gprx_cross_matrix(self.h, _dt(dtype), ctypes.byref(kernel_desc(kernel)), _ptr(A), A.shape[0],
+                                        _ptr(B), B.shape[0], A.shape[1], _ptr(K)))
+        return K
+
+    def cholesky(self, A):
+        A = np.array(A, copy=True, order="C")
+        info = ctypes.c_int32()
+        st = lib().gprx_cholesky(self.h, _dt(A.dtype), _ptr(A), A.shape[0], ctypes.byref(info))
+        if st not in (0, 2):
+            self._c(st)
+        return A, info.value
+
+    def spd_inverse(self, A):
+        A = np.array(A, copy=True, order="C")
+        info = ctypes.c_int32()
+        self._c(lib().gprx_spd_inverse(self.h, _dt(A.dtype), _ptr(A), A.shape[0], ctypes.byref(info)))
+        return A
+
+    def sparse_fit(self, kernel, X, Y, Xm, sigma, jitter, dtype=np.float64):
+        X = np.ascontiguousarray(X, dtype)
+        Y = np.ascontiguousarray(Y, dtype)
+        if Y.ndim == 1:
+            Y = Y[:, None]
+        Xm = np.ascontiguousarray(Xm, dtype)
+        n, d = X.shape
+        m = Y.shape[1]
+        M = Xm.shape[0]
+        Kinv = np.empty((M, M), dtype)
+        RV = np.empty((M, m), dtype)
+        RM = np.empty((M, M), dtype)
+        self._c(lib().gprx_sparse_fit(self.h, _dt(dtype), ctypes.byref(kernel_desc(kernel)), _ptr(X), _ptr(Y), n, d,
+                                      m, _ptr(Xm), M, sigma, jitter, _ptr(Kinv), _ptr(RV), _ptr(RM)))
+        return Kinv, RV, RM
+
+
+class Model:
+    """A resident dense GP (gprx_model): GaussianProcess<T> state on the GPU."""
+
+    def __init__(self, ctx: Context, dtype=np.float64):
+        self.ctx = ctx
+        self.dtype = np.dtype(dtype)
+        h = ctypes.c_void_p()
+        ctx._c(lib().gprx_model_create(ctx.h, _dt(dtype), ctypes.byref(h)))
+        self.h = h
+        self.n = self.d = self.m = 0
+        self.kernel = None
+
+    def close(self):
+        if self.h:
+            lib().gprx_model_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _c(self, st):
+        _check(st, self.ctx.h)
+
+    def set_data(self, X, Y):
+        X = np.ascontiguousarray(X, self.dtype)
+        Y = np.ascontiguousarray(Y, self.dtype)
+        if Y.ndim == 1:
+            Y = Y[:, None]
+        n, d = X.shape
+        self._c(lib().gprx_model_set_data(self.h, _ptr(X), _ptr(Y), n, d, Y.shape[1]))
+        self.n, self.d, self.m = n, d, Y.shape[1]
+
+    def set_kernel(self, kernel):
+        self.kernel = as_node(kernel)
+        self._c(lib().gprx_model_set_kernel(self.h, ctypes.byref(kernel_desc(self.kernel))))
+
+    def set_noise(self, sigma):
+        self._c(lib().gprx_model_set_noise(self.h, float(sigma)))
+
+    def fit(self, flags=FIT_DEFAULT):
+        info = FitInfo()
+        self._c(lib().gprx_model_fit(self.h, flags, ctypes.byref(info)))
+        return info
+
+    def alpha(self):
+        a = np.empty((self.n, self.m), self.dtype)
+        self._c(lib().gprx_model_get_alpha(self.h, _ptr(a)))
+        return a
+
+    def predict(self, Xq, deriv=False):
+        Xq = np.ascontiguousarray(Xq, self.dtype)
+        q = Xq.shape[0]
+        mean = np.empty((q, self.m), self.dtype)
+        D = np.empty((q, self.d, self.m), self.dtype) if deriv else None
+        self._c(lib().gprx_model_predict(self.h, _ptr(Xq), q, _ptr(mean), _ptr(D)))
+        return (mean, D) if deriv else mean
+
+    def posterior_cov(self, Xa, Xb):
+        Xa = np.ascontiguousarray(Xa, self.dtype)
+        Xb = np.ascontiguousarray(Xb, self.dtype)
+        out = np.empty(Xa.shape[0], self.dtype)
+        self._c(lib().gprx_model_posterior_cov(self.h, _ptr(Xa), _ptr(Xb), Xa.shape[0], _ptr(out)))
+        return out
+
+    def credible_interval(self, Xq):
+        """GetCredibleInterval (lib/GaussianProcess.cpp:102-114): 2 sqrt(max(0, gp(x,x)))."""
+        c = self.posterior_cov(Xq, Xq)
+        return 2 * np.sqrt(np.maximum(c, 0))
+
+    def core_matrix(self):
+        C = np.empty((self.n, self.n), self.dtype)
+        self._c(lib().gprx_model_core_matrix(self.h, _ptr(C)))
+        return C
+
+    def lml(self, grad=True, compat=False):
+        flags = (LML_GRAD if grad else 0) | (LML_COMPAT if compat else 0)
+        v = ctypes.c_double()
+        g = np.zeros(MAX_KPARAMS, np.float64)
+        npar = ctypes.c_int32()
+        ld = ctypes.c_double()
+        self._c(lib().gprx_model_lml(self.h, flags, ctypes.byref(v), _ptr(g), ctypes.byref(npar), ctypes.byref(ld)))
+        return v.value, (g[:npar.value].copy() if grad else None), ld.value

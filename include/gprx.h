@@ -1,0 +1,208 @@
+/*
+ * gprx.h — C ABI of libgprx, the MI355X (gfx950) numerics layer of gpr_amd.
+ *
+ * This is the drop-in boundary for the agiger/GPR hot path.  The reference crosses a
+ * foreign ABI exactly once on this path — the Fortran LAPACK calls in
+ * include/LAPACKUtils.h:13-27 (dgetrf_/dgetri_/dpotrf_/dpotri_/ilaenv_) — and otherwise
+ * runs everything inside the templated C++ classes GaussianProcess<T>
+ * (include/GaussianProcess.h:73-171, lib/GaussianProcess.cpp), Kernel<T>
+ * (include/Kernel.h:40-146), GaussianLogLikelihood<T> (include/Likelihood.h:154-350) and
+ * SparseGaussianProcess<T> (include/SparseGaussianProcess.h:33-411).  The C++ host layer
+ * of this repo (include/gpr/) keeps those class signatures and calls the entry points
+ * below instead of Eigen + LAPACK.  Each entry point names the reference code it replaces.
+ *
+ * Conventions
+ *   - plain C types only; every matrix a caller passes is HOST memory, row-major, in the
+ *     model's scalar type (float for GPRX_F32, double for GPRX_F64), exactly the layout of
+ *     the reference's Eigen RowMajor MatrixType (include/GaussianProcess.h:42);
+ *   - no entry point throws; each returns a gprx_status and records a message retrievable
+ *     with gprx_last_error();
+ *   - a model owns its device buffers (training inputs, labels, Cholesky factor, regression
+ *     vectors) and keeps them resident in HBM between calls;
+ *   - read-only model calls (predict, posterior covariance) may be issued concurrently from
+ *     several host threads after a fit (the reference's tests do this,
+ *     tests/PosteriorProcessTest.cpp:120-134); they are serialised internally.
+ */
+#ifndef GPRX_H
+#define GPRX_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GPRX_ABI_VERSION 1
+
+typedef enum gprx_status {
+    GPRX_OK = 0,
+    GPRX_ERR_NONFINITE = 1, /* lib/GaussianProcess.cpp:399-401 "kernel matrix contains entries which are not finite." */
+    GPRX_ERR_NOT_SPD = 2,   /* Cholesky pivot <= 0 (dpotrf_ INFO > 0, include/LAPACKUtils.h:64) */
+    GPRX_ERR_SINGULAR = 3,  /* LU pivot == 0 (dgetrf_ INFO > 0, include/LAPACKUtils.h:46-47) */
+    GPRX_ERR_DIM = 4,       /* lib/GaussianProcess.cpp:709-724 dimension checks */
+    GPRX_ERR_HIP = 5,
+    GPRX_ERR_RCCL = 6,
+    GPRX_ERR_OOM = 7,
+    GPRX_ERR_ARG = 8,
+    GPRX_ERR_STATE = 9,     /* e.g. predict before fit (lib/GaussianProcess.cpp:677-679) */
+    GPRX_ERR_NO_DEVICE = 10
+} gprx_status;
+
+typedef enum gprx_dtype { GPRX_F32 = 0, GPRX_F64 = 1 } gprx_dtype;
+
+/* Kernel identity.  Replaces virtual dispatch through Kernel<T>::operator() /
+ * GetDerivative (include/Kernel.h:52-59) and the string form parsed by
+ * KernelFactory<T>::GetKernel (include/KernelFactory.h:83-178).  A kernel is a POST-ORDER
+ * program: leaves push a value, SUM/PRODUCT pop two.  Leaf parameters are stored in the
+ * reference's GetParameters() order so gradient vectors line up:
+ *   GAUSSIAN          p = (sigma, scale)        include/Kernel.h:483-488
+ *   GAUSSIAN_EXP      p = (sigma, scale)        include/Kernel.h:602-607
+ *   WHITE             p = (scale)               include/Kernel.h:717-720
+ *   RATIONAL_QUADRATIC p = (scale, sigma, alpha) include/Kernel.h:812-819
+ *   PERIODIC          p = (scale, b, sigma)     include/Kernel.h:950-960
+ *   SUM / PRODUCT     gradient = [k1 params, k2 params] include/Kernel.h:169-178, 318-327 */
+typedef enum gprx_kop {
+    GPRX_K_GAUSSIAN = 1,
+    GPRX_K_GAUSSIAN_EXP = 2,
+    GPRX_K_WHITE = 3,
+    GPRX_K_RATIONAL_QUADRATIC = 4,
+    GPRX_K_PERIODIC = 5,
+    GPRX_K_SUM = 6,
+    GPRX_K_PRODUCT = 7
+} gprx_kop;
+
+#define GPRX_MAX_KNODES 32
+#define GPRX_MAX_KPARAMS 48
+
+typedef struct gprx_knode {
+    int32_t op;   /* gprx_kop */
+    int32_t pad;
+    double p[3];  /* leaf parameters as the reference stores them (in T, widened) */
+} gprx_knode;
+
+typedef struct gprx_kernel_desc {
+    int32_t n_nodes;
+    int32_t pad;
+    gprx_knode node[GPRX_MAX_KNODES];
+} gprx_kernel_desc;
+
+typedef struct gprx_ctx gprx_ctx;
+typedef struct gprx_model gprx_model;
+
+/* Fit diagnostics (per call). */
+typedef struct gprx_fit_info {
+    double logdet;       /* log det(K + sigma^2 I) = 2 sum log L_ii (exact, not clamped) */
+    double datafit;      /* sum over outputs of y^T (K + sigma^2 I)^{-1} y */
+    int32_t info;        /* 0, or the 1-based column of the first non-positive pivot */
+    int32_t method;      /* 0 = Cholesky (potrf/potrs), 1 = LU fallback */
+    double ms_build;     /* device time of the covariance build (HIP events) */
+    double ms_factor;    /* device time of the factorisation */
+    double ms_solve;     /* device time of the regression-vector solve */
+} gprx_fit_info;
+
+/* ---- library / context ---------------------------------------------------------- */
+int gprx_abi_version(void);
+gprx_status gprx_device_count(int* count);
+/* One context per process per GPU. */
+gprx_status gprx_ctx_create(int device, gprx_ctx** out);
+/* Multi-GPU context: one process per GPU, RCCL communicator over xGMI.  `unique_id` is
+ * GPRX_UNIQUE_ID_BYTES produced by gprx_dist_unique_id() on rank 0 and shared by the
+ * caller (e.g. torch.distributed broadcast).  New capability: the reference is
+ * single-host OpenMP only. */
+#define GPRX_UNIQUE_ID_BYTES 128
+gprx_status gprx_dist_unique_id(void* out);
+gprx_status gprx_ctx_create_dist(int device, int rank, int world, const void* unique_id, gprx_ctx** out);
+void gprx_ctx_destroy(gprx_ctx* ctx);
+/* Message of the last failing call on this context (ctx may be NULL: last failure of
+ * any call on this thread). */
+const char* gprx_last_error(const gprx_ctx* ctx);
+
+/* Opt-in per-kernel device timing: when enabled, every launch of the library's kernel
+ * classes (kbuild, potrf_diag, potrf_trsm, potrf_update, backsolve, predict, lml_grad,
+ * spd_inverse) is bracketed by HIP events on the stream it runs on; gprx_ctx_get_stats
+ * returns per-class launch counts, summed device milliseconds and the ALGORITHMIC flops
+ * and bytes of those launches.  Enabling resets the counters. */
+typedef struct gprx_kstat {
+    char name[32];
+    int64_t launches;
+    double ms;
+    double flops;
+    double bytes;
+} gprx_kstat;
+gprx_status gprx_ctx_set_stats(gprx_ctx* ctx, int32_t enable);
+gprx_status gprx_ctx_get_stats(gprx_ctx* ctx, gprx_kstat* out, int32_t max, int32_t* count);
+
+/* ---- dense GP model ------------------------------------------------------------- */
+/* Replaces the GaussianProcess<T> state (include/GaussianProcess.h:267-280). */
+gprx_status gprx_model_create(gprx_ctx* ctx, gprx_dtype dtype, gprx_model** out);
+void gprx_model_destroy(gprx_model* model);
+/* AddSample x N (lib/GaussianProcess.cpp:36-51) as one upload: X is N x d, Y is N x m. */
+gprx_status gprx_model_set_data(gprx_model* model, const void* X, const void* Y, int64_t n, int32_t d, int32_t m);
+/* SetKernel (include/GaussianProcess.h:118-121). */
+gprx_status gprx_model_set_kernel(gprx_model* model, const gprx_kernel_desc* kernel);
+/* SetSigma (include/GaussianProcess.h:140-143): noise standard deviation. */
+gprx_status gprx_model_set_noise(gprx_model* model, double sigma);
+
+#define GPRX_FIT_DEFAULT 0u
+#define GPRX_FIT_NO_LU_FALLBACK 1u /* report NOT_SPD instead of falling back to LU */
+/* Initialize (lib/GaussianProcess.cpp:118-130) = ComputeRegressionVectors (:642-672):
+ * kernel matrix (:384-402) + noise (:375-381) + factorisation (replaces the default
+ * lapack::lu_invert dgetrf_+dgetri_, include/LAPACKUtils.h:38-56,85-97) + regression
+ * vectors alpha = (K + sigma^2 I)^{-1} Y (:661).  Everything stays in HBM; `info` may be
+ * NULL. */
+gprx_status gprx_model_fit(gprx_model* model, uint32_t flags, gprx_fit_info* info);
+/* m_RegressionVectors (lib/GaussianProcess.cpp:661) -> host, N x m. */
+gprx_status gprx_model_get_alpha(gprx_model* model, void* alpha);
+/* Predict / PredictDerivative for q queries (lib/GaussianProcess.cpp:54-81, 684-706):
+ * mean is q x m; deriv (optional, may be NULL) is q x d x m with the reference's formula
+ * D(:,c) = -X^T (Kx o alpha_c) (:77-79). */
+gprx_status gprx_model_predict(gprx_model* model, const void* Xq, int64_t q, void* mean, void* deriv);
+/* operator()(x,y) = k(x,y) - Kx^T C Ky for q pairs (lib/GaussianProcess.cpp:84-99), via
+ * the Cholesky factor: k(x,y) - (L^{-1}Kx).(L^{-1}Ky).  GetCredibleInterval (:102-114) is
+ * 2*sqrt(max(0, out)) of the pair (x,x). */
+gprx_status gprx_model_posterior_cov(gprx_model* model, const void* Xa, const void* Xb, int64_t q, void* out);
+/* The core matrix C = (K + sigma^2 I)^{-1} (m_CoreMatrix, lib/GaussianProcess.cpp:652)
+ * materialised from the factor (potri) into host memory, N x N. */
+gprx_status gprx_model_core_matrix(gprx_model* model, void* C);
+
+#define GPRX_LML_GRAD 1u   /* also compute the hyper-parameter gradient */
+#define GPRX_LML_COMPAT 2u /* reproduce the reference's determinant narrowing + clamps
+                              (include/Likelihood.h:77-79, 240-257); otherwise exact */
+/* GaussianLogLikelihood::operator() / GetValueAndParameterDerivatives
+ * (include/Likelihood.h:166-285) for m = 1: value = -1/2 y^T C y - 1/2 log det - N/2 log 2pi,
+ * grad_p = 1/2 tr((alpha alpha^T - C) dK/dp).  Refits from scratch like the reference.
+ * grad may be NULL; nparams receives the kernel's parameter count. */
+gprx_status gprx_model_lml(gprx_model* model, uint32_t flags, double* value, double* grad, int32_t* nparams,
+                           double* logdet);
+
+/* ---- building blocks (host buffers; used by parity tests) --------------------------- */
+/* ComputeKernelMatrixInternal (lib/GaussianProcess.cpp:384-402): K = [k(x_i,x_j)], N x N. */
+gprx_status gprx_kernel_matrix(gprx_ctx* ctx, gprx_dtype dtype, const gprx_kernel_desc* kernel, const void* X,
+                               int64_t n, int32_t d, void* K);
+/* Cross-covariance [k(a_i, b_j)] (include/SparseGaussianProcess.h:218-235). */
+gprx_status gprx_cross_matrix(gprx_ctx* ctx, gprx_dtype dtype, const gprx_kernel_desc* kernel, const void* A,
+                              int64_t na, const void* B, int64_t nb, int32_t d, void* K);
+/* Stacked derivative matrices [D_0;...;D_{P-1}] (lib/GaussianProcess.cpp:472-495), P*N x N. */
+gprx_status gprx_deriv_matrix(gprx_ctx* ctx, gprx_dtype dtype, const gprx_kernel_desc* kernel, const void* X,
+                              int64_t n, int32_t d, void* D);
+/* In-place lower Cholesky of an SPD N x N matrix (replaces dpotrf_ 'L',
+ * include/LAPACKUtils.h:64).  Row-major in/out; the strict upper triangle of the output is
+ * zeroed.  *info as LAPACK: 0 or the 1-based column of the first non-positive pivot. */
+gprx_status gprx_cholesky(gprx_ctx* ctx, gprx_dtype dtype, void* A, int64_t n, int32_t* info);
+/* In-place explicit inverse of an SPD matrix via potrf + potri (replaces
+ * lapack::chol_invert, include/LAPACKUtils.h:59-73,100-111). */
+gprx_status gprx_spd_inverse(gprx_ctx* ctx, gprx_dtype dtype, void* A, int64_t n, int32_t* info);
+
+/* ---- sparse GP (subset of regressors) ----------------------------------------------- */
+/* SparseGaussianProcess::PreComputeRegression (include/SparseGaussianProcess.h:274-313)
+ * without the N x N core matrix (:309-311, infeasible at N = 1e6): returns Kmm^{-1}
+ * (M x M), the regression vectors RV (M x m) and the regression matrix RM (M x M), all
+ * host, row-major.  Any pointer may be NULL. */
+gprx_status gprx_sparse_fit(gprx_ctx* ctx, gprx_dtype dtype, const gprx_kernel_desc* kernel, const void* X,
+                            const void* Y, int64_t n, int32_t d, int32_t m, const void* Xm, int64_t M,
+                            double sigma, double jitter, void* Kinv, void* RV, void* RM);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GPRX_H */

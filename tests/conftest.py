@@ -1,0 +1,20 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (runs through libgprx on cuda:0)")
+
+
+@pytest.fixture(scope="session")
+def ctx():
+    import gpr_amd
+    c = gpr_amd.Context(0)
+    yield c
+    c.close()
