@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "gprx_internal.h"
+#include "../../include/gprx_dev.h"
 
 namespace gprx {
 
@@ -29,6 +30,9 @@ void launch_lml_grad(const KCanon<T>& K, const T* X, const T* tab, int64_t n, in
                      int64_t ldc, double* acc /* MAX_LEAF*3 */, hipStream_t s);
 template <typename T>
 void launch_set_identity_pad(T* A, int64_t ld, int64_t n, int64_t np, hipStream_t s);
+
+gprx_status gprx_dev_bench_impl(gprx_dtype dtype, int32_t what, int64_t M, int64_t N, int64_t K, int32_t iters,
+                                double* ms, Exec* ex);
 
 static thread_local std::string t_last_error;
 thread_local Prof* g_prof = nullptr;
@@ -890,6 +894,19 @@ gprx_status gprx_ctx_get_stats(gprx_ctx* ctx, gprx_kstat* out, int32_t max, int3
         k++;
     }
     if (count) *count = k;
+    return GPRX_OK;
+    API_END(ctx)
+}
+
+
+gprx_status gprx_dev_bench(gprx_ctx* ctx, gprx_dtype dtype, int32_t what, int64_t M, int64_t N, int64_t K,
+                           int32_t iters, double* ms) {
+    API_BEGIN
+    GPRX_REQUIRE(ctx && ms && iters > 0, GPRX_ERR_ARG, "gprx_dev_bench: bad argument");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    GPRX_HIP(hipSetDevice(ctx->device));
+    gprx_status st = gprx_dev_bench_impl(dtype, what, M, N, K, iters, ms, &ctx->ex);
+    if (st != GPRX_OK) return fail(ctx, st, "gprx_dev_bench failed");
     return GPRX_OK;
     API_END(ctx)
 }

@@ -1,0 +1,132 @@
+// gprx_dev.cpp — developer timing hooks (include/gprx_dev.h).
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/gprx_dev.h"
+#include "gprx_internal.h"
+
+namespace gprx {
+template <typename T>
+void launch_gemm_nt(T* C, int64_t ldc, const T* A, int64_t lda, const T* B, int64_t ldb, int64_t M, int64_t N,
+                    int64_t K, T alpha, T beta, bool lower, hipStream_t s);
+template <typename T>
+void launch_diag_public(T* Akk, int64_t ld, T* Lk, int* info, int64_t col0, hipStream_t s, int ph = 3);
+}  // namespace gprx
+
+using namespace gprx;
+
+template <typename T>
+__global__ void dev_fill_spd(T* A, int64_t ld, int64_t n, uint64_t seed) {
+    int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= ld * n) return;
+    int64_t i = e % ld, j = e / ld;
+    uint64_t z = (uint64_t)e * 0x9E3779B97F4A7C15ull + seed;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    T v = (T)((double)(z >> 11) * (1.0 / 9007199254740992.0)) * T(1e-3);
+    if (i == j) v += T(n);  // diagonally dominant -> SPD
+    A[e] = v;
+}
+
+template <typename T>
+static gprx_status bench_impl(int what, int64_t M, int64_t N, int64_t K, int iters, double* ms, Exec& ex) {
+    hipStream_t s = ex.s0;
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    std::vector<void*> bufs;
+    auto alloc = [&](size_t b) {
+        void* p = nullptr;
+        if (hipMalloc(&p, b) != hipSuccess) throw Error{GPRX_ERR_OOM, "dev bench: hipMalloc failed"};
+        bufs.push_back(p);
+        return p;
+    };
+    int* info = (int*)alloc(sizeof(int));
+    float tms = 0;
+    try {
+        if (what == 0 || (what >= 10 && what <= 12)) {
+            const int ph = what == 0 ? 3 : what - 10;
+            T* A = (T*)alloc(sizeof(T) * DB * DB * (size_t)iters);
+            T* L = (T*)alloc(sizeof(T) * DB * DB);
+            for (int it = 0; it < iters; it++)
+                hipLaunchKernelGGL(dev_fill_spd<T>, dim3((DB * DB + 255) / 256), dim3(256), 0, s, A + (size_t)it * DB * DB,
+                                   (int64_t)DB, (int64_t)DB, (uint64_t)it);
+            launch_diag_public<T>(A, DB, L, info, 0, s, ph);  // warm
+            (void)hipEventRecord(e0, s);
+            for (int it = 1; it < iters; it++) launch_diag_public<T>(A + (size_t)it * DB * DB, DB, L, info, 0, s, ph);
+            (void)hipEventRecord(e1, s);
+            (void)hipEventSynchronize(e1);
+            (void)hipEventElapsedTime(&tms, e0, e1);
+            *ms = tms / std::max(1, iters - 1);
+        } else if (what == 1 || what == 2) {
+            const int64_t ld = M;
+            T* C = (T*)alloc(sizeof(T) * ld * N);
+            T* A = (T*)alloc(sizeof(T) * ld * K);
+            T* B = (T*)alloc(sizeof(T) * N * K);
+            (void)hipMemset(C, 0, sizeof(T) * ld * N);
+            (void)hipMemset(A, 0, sizeof(T) * ld * K);
+            (void)hipMemset(B, 0, sizeof(T) * N * K);
+            hipLaunchKernelGGL(dev_fill_spd<T>, dim3((unsigned)((ld * K + 255) / 256)), dim3(256), 0, s, A, ld, K,
+                               (uint64_t)1);
+            hipLaunchKernelGGL(dev_fill_spd<T>, dim3((unsigned)((N * K + 255) / 256)), dim3(256), 0, s, B, N, K,
+                               (uint64_t)2);
+            launch_gemm_nt<T>(C, ld, A, ld, B, N, M, N, K, T(-1), T(1), what == 2, s);
+            (void)hipEventRecord(e0, s);
+            for (int it = 0; it < iters; it++) launch_gemm_nt<T>(C, ld, A, ld, B, N, M, N, K, T(-1), T(1), what == 2, s);
+            (void)hipEventRecord(e1, s);
+            (void)hipEventSynchronize(e1);
+            (void)hipEventElapsedTime(&tms, e0, e1);
+            *ms = tms / iters;
+        } else if (what == 3 || what == 4 || what == 5) {
+            const int64_t n = M;
+            T* A = (T*)alloc(sizeof(T) * n * n);
+            T* Li = (T*)alloc(sizeof(T) * n * DB);
+            T* z = (T*)alloc(sizeof(T) * n);
+            T* al = (T*)alloc(sizeof(T) * n);
+            Exec single;
+            single.s0 = s;
+            single.s1 = nullptr;
+            Exec& use = (what == 4) ? ex : single;
+            double total = 0;
+            for (int it = 0; it < iters + 1; it++) {
+                hipLaunchKernelGGL(dev_fill_spd<T>, dim3((unsigned)((n * n + 255) / 256)), dim3(256), 0, s, A, n, n,
+                                   (uint64_t)it);
+                (void)hipMemsetD32Async((hipDeviceptr_t)info, INT_MAX, 1, s);
+                if (what == 5) potrf_blocked<T>(A, n, n, n, Li, info, use);
+                (void)hipEventRecord(e0, s);
+                if (what == 5) launch_backsolve<T>(A, n, n - DB, 1, Li, z, al, s);
+                else potrf_blocked<T>(A, n, n, n, Li, info, use);
+                (void)hipEventRecord(e1, s);
+                (void)hipEventSynchronize(e1);
+                (void)hipEventElapsedTime(&tms, e0, e1);
+                if (it > 0) total += tms;
+            }
+            *ms = total / iters;
+        } else {
+            throw Error{GPRX_ERR_ARG, "dev bench: unknown case"};
+        }
+        if (hipDeviceSynchronize() != hipSuccess) throw Error{GPRX_ERR_HIP, "dev bench: device error"};
+    } catch (const Error& e) {
+        for (void* p : bufs) (void)hipFree(p);
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        return e.st;
+    }
+    for (void* p : bufs) (void)hipFree(p);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    return GPRX_OK;
+}
+
+namespace gprx {
+gprx_status gprx_dev_bench_impl(gprx_dtype dtype, int32_t what, int64_t M, int64_t N, int64_t K, int32_t iters,
+                                double* ms, Exec* ex) {
+    return dtype == GPRX_F64 ? bench_impl<double>(what, M, N, K, iters, ms, *ex)
+                             : bench_impl<float>(what, M, N, K, iters, ms, *ex);
+}
+}  // namespace gprx

@@ -24,68 +24,100 @@
 namespace gprx {
 
 // ======================================================================================
-// Diagonal block: factor + inverse, one workgroup of 512 threads (4 per row / column).
-// Every register array below is indexed with compile-time indices only (no scratch).
+// Diagonal block: factor + inverse, one workgroup of 512 threads.
+//
+// Factorisation: blocked Crout over 8-column blocks.  For block j0 the rows i >= j0 need
+// s_i = A[i, j0:j0+8] - L[i, :j0] L[j0:j0+8, :j0]^T; the j0-long dot products are split
+// over tpr = 512 / (active rows) threads per row (a power of two <= 64, so each group
+// sits inside one wave and reduces with shuffles): the critical path per block stays short
+// as rows retire.  The 8x8 Schur block is factored redundantly by every thread with
+// rsq + Newton reciprocal square roots (no divisions on the chain).
+// Inverse: Linv by 8-row blocks; row block i0 needs, for every column c < i0 + 8,
+// acc[r] = sum_{k=c}^{i0-1} L[i0+r][k] Linv[k][c], again split over threads per column.
+// Linv is kept transposed in the free upper triangle of the LDS image.
+// All register arrays use compile-time indices (no scratch).
 // ======================================================================================
 constexpr int LS = DB + 2;  // LDS row stride (elements); even, keeps 16-B alignment
 constexpr int DT = 512;     // threads of the diagonal kernel
 
+__device__ __forceinline__ int pow2_floor(int x) { return 1 << (31 - __clz(x)); }
+
 template <typename T>
-__device__ __forceinline__ T quad_sum(T v) {
-    v += __shfl_xor(v, 1);
-    v += __shfl_xor(v, 2);
+__device__ __forceinline__ T group_sum(T v, int tpr) {
+    for (int off = tpr >> 1; off > 0; off >>= 1) v += __shfl_xor(v, off);
     return v;
 }
 
-template <typename T>
+// 1/sqrt(x) to full precision: hardware estimate + Newton steps (no divide on the chain)
+__device__ __forceinline__ double rsqrt_full(double x) {
+    double y = __builtin_amdgcn_rsq(x);
+    double h = 0.5 * x;
+    y = y * fma(-h * y, y, 1.5);
+    y = y * fma(-h * y, y, 1.5);
+    return y;
+}
+__device__ __forceinline__ float rsqrt_full(float x) {
+    float y = __builtin_amdgcn_rsqf(x);
+    float h = 0.5f * x;
+    y = y * fmaf(-h * y, y, 1.5f);
+    return y;
+}
+
+template <typename T, int PH = 3>  // PH: bit0 factorise, bit1 invert (ablation builds only)
 __global__ __launch_bounds__(DT) void diag_potrf_kernel(T* __restrict__ A, int64_t ld, T* __restrict__ Linv,
                                                         int* __restrict__ info, int64_t col0) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     T(*sL)[LS] = reinterpret_cast<T(*)[LS]>(smem_raw);
     T* sDinv = reinterpret_cast<T*>(smem_raw + sizeof(T) * DB * LS);
-    T(*sS)[8] = reinterpret_cast<T(*)[8]>(smem_raw + sizeof(T) * (DB * LS + DB));  // 8x8 Schur block
+    T(*sS)[8] = reinterpret_cast<T(*)[8]>(smem_raw + sizeof(T) * (DB * LS + DB));  // 8x8 staging block
 
     const int t = threadIdx.x;
-    {   // lower triangle, column-major global -> row-major LDS
+    {   // column-major global -> row-major LDS; all 32 loads in flight before the stores
         const int r = t & (DB - 1);
-        for (int c = t >> 7; c < DB; c += DT / DB)
-            if (r >= c) sL[r][c] = A[r + (int64_t)c * ld];
+        constexpr int NL = DB * DB / DT;
+        T v[NL];
+#pragma unroll
+        for (int u = 0; u < NL; u++) v[u] = A[r + (int64_t)((t >> 7) + u * (DT / DB)) * ld];
+#pragma unroll
+        for (int u = 0; u < NL; u++) {
+            const int c = (t >> 7) + u * (DT / DB);
+            if (r >= c) sL[r][c] = v[u];
+        }
     }
     __syncthreads();
 
-    const int i = t >> 2;  // row owned by this thread quad
-    const int h = t & 3;
     bool failed = false;
     int fail_col = 0;
-
-    // ---- blocked Crout factorisation, 8-wide column blocks ------------------------------
-    for (int j0 = 0; j0 < DB; j0 += 8) {
+    for (int j0 = 0; j0 < ((PH & 1) ? DB : 0); j0 += 8) {
+        const int R = DB - j0;                  // active rows j0..127
+        const int tpr = min(64, pow2_floor(DT / R));
+        const int i = j0 + t / tpr;             // row of this thread
+        const int h = t % tpr;
+        const bool active = (t / tpr) < R;
         T s[8];
-        const bool active = i >= j0;
         if (active) {
+            const int kb = (h * j0) / tpr, ke = ((h + 1) * j0) / tpr;
 #pragma unroll
             for (int q = 0; q < 8; q++) s[q] = (h == 0 && j0 + q <= i) ? sL[i][j0 + q] : T(0);
-            const int quarter = j0 >> 2;  // even
-            const int kb = h * quarter, ke = kb + quarter;
-            for (int k = kb; k < ke; k += 2) {
-                const T li0 = sL[i][k], li1 = sL[i][k + 1];
+            for (int k = kb; k < ke; k++) {
+                const T li = sL[i][k];
 #pragma unroll
-                for (int q = 0; q < 8; q++) {
-                    s[q] = fma(-li0, sL[j0 + q][k], s[q]);
-                    s[q] = fma(-li1, sL[j0 + q][k + 1], s[q]);
-                }
+                for (int q = 0; q < 8; q++) s[q] = fma(-li, sL[j0 + q][k], s[q]);
             }
+        } else {
 #pragma unroll
-            for (int q = 0; q < 8; q++) s[q] = quad_sum(s[q]);
-            if (h == 0 && i < j0 + 8) {
+            for (int q = 0; q < 8; q++) s[q] = T(0);
+        }
+        if (tpr > 1) {
 #pragma unroll
-                for (int q = 0; q < 8; q++)
-                    if (j0 + q <= i) sS[i - j0][q] = s[q];
-            }
+            for (int q = 0; q < 8; q++) s[q] = group_sum(s[q], tpr);
+        }
+        if (active && h == 0 && i < j0 + 8) {
+#pragma unroll
+            for (int q = 0; q < 8; q++)
+                if (j0 + q <= i) sS[i - j0][q] = s[q];
         }
         __syncthreads();
-        // The 8x8 Schur complement of the diagonal block (in its own LDS buffer, so the
-        // L writes below cannot race these reads), factored redundantly by everyone.
         T Ld[8][8], dinv[8];
 #pragma unroll
         for (int c = 0; c < 8; c++) {
@@ -96,36 +128,37 @@ __global__ __launch_bounds__(DT) void diag_potrf_kernel(T* __restrict__ A, int64
                 failed = true;
                 fail_col = j0 + c;
             }
-            const T dg = sqrt(dsum);
-            Ld[c][c] = dg;
-            dinv[c] = T(1) / dg;
+            const T ri = rsqrt_full(dsum);
+            Ld[c][c] = dsum * ri;
+            dinv[c] = ri;
 #pragma unroll
             for (int r = c + 1; r < 8; r++) {
                 T v = sS[r][c];
 #pragma unroll
                 for (int k = 0; k < c; k++) v = fma(-Ld[r][k], Ld[c][k], v);
-                Ld[r][c] = v * dinv[c];
+                Ld[r][c] = v * ri;
             }
         }
-        if (i >= j0 + 8) {
-            T x[8];
+        if (active && h == 0) {
+            if (i >= j0 + 8) {
+                T x[8];
 #pragma unroll
-            for (int q = 0; q < 8; q++) {
-                T v = s[q];
+                for (int q = 0; q < 8; q++) {
+                    T v = s[q];
 #pragma unroll
-                for (int q2 = 0; q2 < q; q2++) v = fma(-x[q2], Ld[q][q2], v);
-                x[q] = v * dinv[q];
-            }
-            if (h == 0) {
+                    for (int q2 = 0; q2 < q; q2++) v = fma(-x[q2], Ld[q][q2], v);
+                    x[q] = v * dinv[q];
+                }
 #pragma unroll
                 for (int q = 0; q < 8; q++) sL[i][j0 + q] = x[q];
-            }
-        } else if (active && h == 0) {
+            } else {
 #pragma unroll
-            for (int r = 0; r < 8; r++) {
-                if (i == j0 + r) {
+                for (int r = 0; r < 8; r++) {
+                    if (i == j0 + r) {
 #pragma unroll
-                    for (int c = 0; c <= r; c++) sL[i][j0 + c] = Ld[r][c];
+                        for (int c = 0; c <= r; c++) sL[i][j0 + c] = Ld[r][c];
+                        sDinv[i] = dinv[r];
+                    }
                 }
             }
         }
@@ -138,32 +171,34 @@ __global__ __launch_bounds__(DT) void diag_potrf_kernel(T* __restrict__ A, int64
         for (int c = t >> 7; c < DB; c += DT / DB)
             if (r >= c) A[r + (int64_t)c * ld] = sL[r][c];
     }
-    // ---- Linv = L^{-1}: column c owned by a thread quad, stored transposed in the free
-    //      upper triangle (sL[c][k] = Linv[k][c], k > c) plus sDinv[c] = 1 / L[c][c].
-    if (h == 0) sDinv[i] = T(1) / sL[i][i];
+
+    // ---- Linv by 8-row blocks (stored transposed: sL[c][k] = Linv[k][c] for k > c) --------
+    if (!(PH & 1) && t < DB) sDinv[t] = T(1);
     __syncthreads();
-    {
-        const int c = i;
-        const T dinv_c = sDinv[c];
-        for (int i0 = (c & ~7); i0 < DB; i0 += 8) {
-            T acc[8];
+    for (int i0 = 0; i0 < ((PH & 2) ? DB : 0); i0 += 8) {
+        const int C = i0 + 8;                   // columns 0..i0+7 take part
+        const int tpc = min(64, pow2_floor(DT / C));
+        const int c = t / tpc;
+        const int h = t % tpc;
+        const bool active = c < C;
+        T acc[8];
 #pragma unroll
-            for (int r = 0; r < 8; r++) acc[r] = T(0);
-            if (i0 > c) {  // acc[r] = sum_{k=c}^{i0-1} L[i0+r][k] Linv[k][c]
-                if (h == 0) {
+        for (int r = 0; r < 8; r++) acc[r] = T(0);
+        if (active && c < i0) {
+            // k = c term uses Linv[c][c] = sDinv[c]; then k = c+1 .. i0-1 from the transposed store
+            const int len = i0 - c;
+            const int kb = c + (h * len) / tpc, ke = c + ((h + 1) * len) / tpc;
+            for (int k = kb; k < ke; k++) {
+                const T u = (k == c) ? sDinv[c] : sL[c][k];
 #pragma unroll
-                    for (int r = 0; r < 8; r++) acc[r] = sL[i0 + r][c] * dinv_c;
-                }
-                const int kb0 = c + 1, len = i0 - kb0;
-                const int kb = kb0 + (h * len) / 4, ke = kb0 + ((h + 1) * len) / 4;
-                for (int k = kb; k < ke; k++) {
-                    const T u = sL[c][k];
-#pragma unroll
-                    for (int r = 0; r < 8; r++) acc[r] = fma(sL[i0 + r][k], u, acc[r]);
-                }
-#pragma unroll
-                for (int r = 0; r < 8; r++) acc[r] = quad_sum(acc[r]);
+                for (int r = 0; r < 8; r++) acc[r] = fma(sL[i0 + r][k], u, acc[r]);
             }
+        }
+        if (tpc > 1) {
+#pragma unroll
+            for (int r = 0; r < 8; r++) acc[r] = group_sum(acc[r], tpc);
+        }
+        if (active && h == 0) {
             T x[8];
 #pragma unroll
             for (int r = 0; r < 8; r++) {
@@ -171,7 +206,7 @@ __global__ __launch_bounds__(DT) void diag_potrf_kernel(T* __restrict__ A, int64
                 if (row < c) {
                     x[r] = T(0);
                 } else if (row == c) {
-                    x[r] = dinv_c;
+                    x[r] = sDinv[c];
                 } else {
                     T v = -acc[r];
 #pragma unroll
@@ -179,14 +214,12 @@ __global__ __launch_bounds__(DT) void diag_potrf_kernel(T* __restrict__ A, int64
                     x[r] = v * sDinv[row];
                 }
             }
-            if (h == 0) {
 #pragma unroll
-                for (int r = 0; r < 8; r++)
-                    if (i0 + r > c) sL[c][i0 + r] = x[r];
-            }
+            for (int r = 0; r < 8; r++)
+                if (i0 + r > c) sL[c][i0 + r] = x[r];
         }
+        __syncthreads();
     }
-    __syncthreads();
     {   // Linv -> global (column-major, ld = DB, zeros above the diagonal)
         const int r = t & (DB - 1);
         for (int c = t >> 7; c < DB; c += DT / DB) {
@@ -436,6 +469,25 @@ static void launch_diag(T* Akk, int64_t ld, T* Lk, int* info, int64_t col0, hipS
     hipLaunchKernelGGL(diag_potrf_kernel<T>, dim3(1), dim3(DT), lds, s, Akk, ld, Lk, info, col0);
 }
 
+template <typename T>
+void launch_diag_public(T* Akk, int64_t ld, T* Lk, int* info, int64_t col0, hipStream_t s, int ph = 3) {
+    if (ph == 3) {
+        launch_diag<T>(Akk, ld, Lk, info, col0, s);
+        return;
+    }
+    const size_t lds = diag_lds_bytes<T>();
+    auto k0 = diag_potrf_kernel<T, 0>;
+    auto k1 = diag_potrf_kernel<T, 1>;
+    auto k2 = diag_potrf_kernel<T, 2>;
+    const void* f = ph == 0 ? (const void*)k0 : (ph == 1 ? (const void*)k1 : (const void*)k2);
+    hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (ph == 0) hipLaunchKernelGGL(k0, dim3(1), dim3(DT), lds, s, Akk, ld, Lk, info, col0);
+    else if (ph == 1) hipLaunchKernelGGL(k1, dim3(1), dim3(DT), lds, s, Akk, ld, Lk, info, col0);
+    else hipLaunchKernelGGL(k2, dim3(1), dim3(DT), lds, s, Akk, ld, Lk, info, col0);
+}
+template void launch_diag_public<double>(double*, int64_t, double*, int*, int64_t, hipStream_t, int);
+template void launch_diag_public<float>(float*, int64_t, float*, int*, int64_t, hipStream_t, int);
+
 int outer_block() {
     static int nbo = [] {
         int v = 256;
@@ -520,20 +572,29 @@ __global__ void copy_aug_kernel(const T* __restrict__ A, int64_t ld, int64_t np,
 }
 
 
-// alpha_j = Linv_j^T z_j  (one workgroup)
+// alpha_j = Linv_j^T z_j  (one workgroup): the 128x128 block is staged into LDS with
+// coalesced loads (row q of the image = column q of Linv), then thread q forms
+// sum_{p >= q} Linv[p][q] z[p] from LDS.
 template <typename T>
-__global__ __launch_bounds__(DB) void backsolve_alpha_kernel(int64_t np, int m, const T* __restrict__ Linv,
-                                                             const T* __restrict__ z, T* __restrict__ alpha,
-                                                             int64_t j0) {
+__global__ __launch_bounds__(256) void backsolve_alpha_kernel(int64_t np, int m, const T* __restrict__ Linv,
+                                                              const T* __restrict__ z, T* __restrict__ alpha,
+                                                              int64_t j0) {
+    __shared__ T sLi[DB][DB + 1];
     __shared__ T sz[DB];
     const int t = threadIdx.x;
+#pragma unroll 8
+    for (int u = 0; u < DB * DB / 256; u++) {
+        const int e = t + 256 * u;
+        sLi[e / DB][e % DB] = Linv[e];
+    }
     for (int r = 0; r < m; r++) {
-        sz[t] = z[(int64_t)r * np + j0 + t];
+        if (t < DB) sz[t] = z[(int64_t)r * np + j0 + t];
         __syncthreads();
-        const T* col = Linv + t * DB;
-        T acc = 0;
-        for (int p = t; p < DB; p++) acc = fma(col[p], sz[p], acc);
-        alpha[(j0 + t) * m + r] = acc;
+        if (t < DB) {
+            T acc = 0;
+            for (int p = t; p < DB; p++) acc = fma(sLi[t][p], sz[p], acc);
+            alpha[(j0 + t) * m + r] = acc;
+        }
         __syncthreads();
     }
 }
@@ -576,7 +637,7 @@ void launch_backsolve(const T* A, int64_t ld, int64_t np, int m, const T* Linv, 
     ProfScope ps(KC_BACKSOLVE, s, 2.0 * (double)np * np * m / 2.0, (double)sizeof(T) * np * (np + 1) / 2.0);
     hipLaunchKernelGGL(copy_aug_kernel<T>, dim3((unsigned)((e + 255) / 256)), dim3(256), 0, s, A, ld, np, m, z);
     for (int64_t j0 = np - DB; j0 >= 0; j0 -= DB) {
-        hipLaunchKernelGGL(backsolve_alpha_kernel<T>, dim3(1), dim3(DB), 0, s, np, m,
+        hipLaunchKernelGGL(backsolve_alpha_kernel<T>, dim3(1), dim3(256), 0, s, np, m,
                            Linv + (j0 / DB) * (int64_t)DB * DB, (const T*)z, alpha, j0);
         if (j0 > 0)
             hipLaunchKernelGGL(backsolve_update_kernel<T>, dim3((unsigned)((j0 + BS_COLS_WG - 1) / BS_COLS_WG)),

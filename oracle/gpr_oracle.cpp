@@ -459,6 +459,51 @@ static void kgrad(const Node<T>& n, const T* x, const T* y, int d, std::vector<T
     }
 }
 
+// Kernel<T>::SetParameters for every leaf in GetParameters() order (include/Kernel.h:239-245,
+// 514-520, 633-639, 745-751, 846-852, 987-993) with the constructor-time validation.
+template <class T>
+static void set_params(Node<T>& n, const T* p, int& idx) {
+    switch (n.kind) {
+        case SUM:
+        case PRODUCT:
+            set_params(*n.a, p, idx);
+            set_params(*n.b, p, idx);
+            return;
+        case GAUSS:
+            n.p[0] = p[idx++];
+            n.p[1] = p[idx++];
+            if (n.p[0] == 0) throw std::string("GaussianKernel: sigma has to be positive");
+            if (n.p[1] == 0) throw std::string("GaussianKernel: scale has to be positive");
+            n.sigma2 = n.p[0] * n.p[0];
+            n.sigma3 = n.p[0] * n.p[0] * n.p[0];
+            n.scale2 = n.p[1] * n.p[1];
+            return;
+        case GAUSS_EXP:
+            n.p[0] = p[idx++];
+            n.p[1] = p[idx++];
+            return;
+        case WHITE:
+            n.p[0] = p[idx++];
+            n.scale2 = n.p[0] * n.p[0];
+            return;
+        case RQ:
+            for (int i = 0; i < 3; i++) n.p[i] = p[idx++];
+            n.scale2 = n.p[0] * n.p[0];
+            n.sigma2 = n.p[1] * n.p[1];
+            n.sigma3 = n.p[1] * n.p[1] * n.p[1];
+            return;
+        case PERIODIC:
+            for (int i = 0; i < 3; i++) n.p[i] = p[idx++];
+            if (n.p[0] == 0) throw std::string("PeriodicKernel: scale parameter has to be positive.");
+            if (n.p[1] == 0) throw std::string("PeriodicKernel: period length parameter has to be positive.");
+            if (n.p[2] == 0) throw std::string("PeriodicKernel: sigma parameter has to be positive.");
+            n.scale2 = n.p[0] * n.p[0];
+            n.sigma2 = n.p[2] * n.p[2];
+            n.sigma3 = n.p[2] * n.p[2] * n.p[2];
+            return;
+    }
+}
+
 template <class T>
 static std::unique_ptr<Node<T>> kernel_from(const char* kstr) {
     std::string s(kstr);
@@ -596,6 +641,23 @@ int orc_num_threads() { return omp_get_max_threads(); }
             std::vector<T> g;                                                                      \
             kgrad(*k, x, y, d, g);                                                                 \
             std::copy(g.begin(), g.end(), grad);                                                   \
+        }                                                                                          \
+        ORC_CATCH                                                                                  \
+    }                                                                                              \
+    /* B parameter vectors (B x P, GetParameters order) on one (x, y) pair: val (B), grad (B x P) */ \
+    int orc_kernel_eval_params_##SUF(const char* ks, const T* params, int B, const T* x, const T* y, int d,  \
+                                     T* val, T* grad) {                                            \
+        ORC_TRY auto k = kernel_from<T>(ks);                                                       \
+        const int P = k->nparams();                                                                \
+        for (int b = 0; b < B; b++) {                                                              \
+            int idx = 0;                                                                           \
+            set_params(*k, params + (size_t)b * P, idx);                                           \
+            val[b] = keval(*k, x, y, d);                                                           \
+            if (grad) {                                                                            \
+                std::vector<T> g;                                                                  \
+                kgrad(*k, x, y, d, g);                                                             \
+                std::copy(g.begin(), g.end(), grad + (size_t)b * P);                               \
+            }                                                                                      \
         }                                                                                          \
         ORC_CATCH                                                                                  \
     }                                                                                              \

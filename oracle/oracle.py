@@ -85,6 +85,18 @@ def kernel_eval(kstr, x, y, dtype=np.float64, with_grad=True):
     return (val[0], g) if with_grad else val[0]
 
 
+def kernel_eval_params(kstr, params, x, y, dtype=np.float64, with_grad=True):
+    """Evaluate the kernel structure `kstr` for B parameter vectors (B x P) on one pair."""
+    suf, _ = _dt(dtype)
+    params = _c(np.atleast_2d(params), dtype)
+    x, y = _c(x, dtype), _c(y, dtype)
+    B = params.shape[0]
+    val = np.empty(B, dtype)
+    g = np.empty_like(params) if with_grad else None
+    _call(f"orc_kernel_eval_params_{suf}", kstr.encode(), _p(params), B, _p(x), _p(y), len(x), _p(val), _p(g))
+    return (val, g) if with_grad else val
+
+
 def kernel_matrix(kstr, X, dtype=np.float64):
     suf, _ = _dt(dtype)
     X = _c(X, dtype)

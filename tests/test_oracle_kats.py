@@ -1,0 +1,242 @@
+"""Pin the CPU oracle to the reference's own deterministic known-answer tests.
+
+Each test restates a reference test (file:line cited) with the same grids, inputs and
+thresholds and runs it against the oracle restatement (oracle/gpr_oracle.cpp).  The
+reference itself cannot be built here (Eigen3/Boost absent), so these KATs plus the
+independent numpy/scipy cross-check (test_oracle_numpy.py) are what pin the oracle.
+"""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+X0 = np.array([0.1, 0.5])
+Y0 = np.array([-0.1, 0.8])
+
+
+def crange(start, stop, step):
+    """for(double v=start; v<stop; v+=step) with the reference's float accumulation."""
+    out = []
+    v = start
+    while v < stop:
+        out.append(v)
+        v += step
+    return out
+
+
+def grid(*axes):
+    mesh = np.meshgrid(*axes, indexing="ij")
+    return np.stack([m.ravel() for m in mesh], axis=1)
+
+
+def central_diff(ks, P, h, x=X0, y=Y0):
+    """Mean |central difference - analytic derivative| per parameter over the grid P."""
+    _, D = O.kernel_eval_params(ks, P, x, y)
+    err = np.zeros(P.shape[1])
+    for p in range(P.shape[1]):
+        Pp, Pm = P.copy(), P.copy()
+        Pp[:, p] += h / 2
+        Pm[:, p] -= h / 2
+        vp = O.kernel_eval_params(ks, Pp, x, y, with_grad=False)
+        vm = O.kernel_eval_params(ks, Pm, x, y, with_grad=False)
+        err[p] = np.mean(np.abs((vp - vm) / h - D[:, p]))
+    return err
+
+
+def test_gaussian_derivative():
+    # tests/KernelDerivativeTest.cpp:40-91 ; params (sigma, scale)
+    P = grid(crange(0.1, 10, 0.4), crange(0.1, 3, 0.8))
+    e = central_diff("GaussianKernel(1,1,)", P, 0.001)
+    assert e[0] < 1e-5 and e[1] < 1e-12
+
+
+def test_gaussian_exp_derivative():
+    # tests/KernelDerivativeTest.cpp:97-148
+    P = grid(crange(0.1, 10, 0.4), crange(0.1, 3, 0.8))
+    e = central_diff("GaussianExpKernel(1,1,)", P, 0.001)
+    assert e[0] < 1e-6 and e[1] < 1e-3
+
+
+def test_white_derivative():
+    # tests/KernelDerivativeTest.cpp:150-198: zero off the diagonal, exact on it
+    P = np.array(crange(0.1, 3, 0.8))[:, None]
+    assert central_diff("WhiteKernel(1,)", P, 0.1)[0] == 0
+    assert central_diff("WhiteKernel(1,)", P, 0.1, x=X0, y=X0)[0] < 1e-13
+
+
+def test_rational_quadratic_derivative():
+    # tests/KernelDerivativeTest.cpp:200-262 ; params (scale, sigma, alpha)
+    P = grid(crange(0.1, 3, 0.8), crange(0.2, 10, 0.6), crange(0.1, 6, 0.6))
+    e = central_diff("RationalQuadraticKernel(1,1,1,)", P, 0.01)
+    assert e[0] < 1e-13 and e[1] < 0.001 and e[2] < 1e-4
+
+
+def test_periodic_derivative():
+    # tests/KernelDerivativeTest.cpp:264-324 ; params (scale, b, sigma)
+    P = grid(crange(0.1, 3, 0.8), crange(0.1, 5 * np.pi, 0.3), crange(0.1, 4, 0.1))
+    e = central_diff("PeriodicKernel(1,1,1,)", P, 0.01)
+    assert e[0] < 1e-13 and e[1] < 1e-5 and e[2] < 0.001
+
+
+def test_sum_derivative():
+    # tests/KernelDerivativeTest.cpp:326-427: Sum(Gaussian(gsigma,gscale), Periodic(pscale,b,psigma))
+    P = grid(crange(0.1, 6, 0.4), crange(0.1, 5, 0.8), crange(0.1, 4, 0.8), crange(0.1, 5 * np.pi, 0.4),
+             crange(0.2, 6, 0.3))
+    P = P[:, [0, 1, 2, 3, 4]]  # (gsigma, gscale, pscale, b, psigma) = GetParameters() order
+    e = central_diff("SumKernel(GaussianKernel(1,1,),PeriodicKernel(1,1,1,))", P, 0.01)
+    assert e[0] < 0.005 and e[1] < 1e-11 and e[2] < 1e-11 and e[3] < 1e-6 and e[4] < 1e-4
+
+
+def test_product_derivative():
+    # tests/KernelDerivativeTest.cpp:429-532
+    P = grid(crange(0.1, 5, 0.4), crange(0.4, 4, 0.8), crange(0.1, 4, 0.8), crange(0.1, 4 * np.pi, 0.4),
+             crange(0.4, 5, 0.3))
+    e = central_diff("ProductKernel(GaussianKernel(1,1,),PeriodicKernel(1,1,1,))", P, 0.01)
+    assert e[0] < 0.009 and e[1] < 1e-11 and e[2] < 1e-11 and e[3] < 1e-5 and e[4] < 0.001
+
+
+def _sin_gp(sigma_k, n_train, span, noise):
+    X = np.array([[i * span / n_train] for i in range(n_train)])
+    Y = np.sin(X)
+    return X, Y
+
+
+def test_gp_sinus_regression():
+    # tests/GaussianProcessTest.cpp:35-76 (sigma = 0: the LU inverse of a near-singular K)
+    X, Y = _sin_gp(2.889, 10, 2 * np.pi, 0)
+    a, _ = O.fit("GaussianKernel(2.889,1,)", X, Y, 0.0)
+    Xq = np.array([[i * 2 * np.pi / 50] for i in range(50)])
+    err = np.sum(np.abs(O.predict("GaussianKernel(2.889,1,)", X, a, Xq)[:, 0] - np.sin(Xq[:, 0])))
+    assert err <= 0.0008
+
+
+def test_gp_2d_regression():
+    # tests/GaussianProcessTest.cpp:78-121
+    t = np.array([i * 2 * np.pi / 10 for i in range(10)])
+    X = np.stack([t, t], 1)
+    Y = np.stack([np.sin(t), np.cos(t)], 1)
+    a, _ = O.fit("GaussianKernel(3.24,1,)", X, Y, 0.0)
+    tq = np.array([i * 2 * np.pi / 50 for i in range(50)])
+    P = O.predict("GaussianKernel(3.24,1,)", X, a, np.stack([tq, tq], 1))
+    err = np.sum(np.abs(P[:, 0] - np.sin(tq)) + np.abs(P[:, 1] - np.cos(tq)))
+    assert err <= 0.005
+
+
+def test_gp_derivative_of_sinus():
+    # tests/GaussianProcessTest.cpp:238-279 (the sigma_k = 1 derivative formula)
+    X = np.array([[i * 4 * np.pi / 20] for i in range(20)])
+    a, _ = O.fit("GaussianKernel(1,1,)", X, np.sin(X), 0.0)
+    Xq = np.array([[i * 4 * np.pi / 50] for i in range(50)])
+    _, D = O.predict("GaussianKernel(1,1,)", X, a, Xq, with_deriv=True)
+    assert np.sum(np.abs(D[:, 0, 0] - np.cos(Xq[:, 0]))) <= 0.6
+
+
+def test_zero_sigma_gaussian_throws():
+    # tests/GaussianProcessTest.cpp:322-344
+    with pytest.raises(O.OracleError, match="sigma has to be positive"):
+        O.kernel_eval("GaussianKernel(0,1,)", [0.0], [1.0])
+
+
+@pytest.mark.parametrize("method", [O.FULL_PIVOT_LU, O.SELF_ADJOINT_EIGEN_SOLVER])
+def test_inversion_methods(method):
+    # tests/InversionMethodsTest.cpp:35-145 (N=10, sigma=0, GaussianKernel(2.8), err < 6e-4)
+    X = np.array([[i * 2 * np.pi / 10] for i in range(10)])
+    a, _ = O.fit("GaussianKernel(2.8,1,)", X, np.sin(X), 0.0, method=method)
+    Xq = np.array([[i * 2 * np.pi / 50] for i in range(50)])
+    err = np.sum(np.abs(O.predict("GaussianKernel(2.8,1,)", X, a, Xq)[:, 0] - np.sin(Xq[:, 0])))
+    assert err <= 0.0006
+
+
+def test_lapack_lu_vs_eigen_inverse():
+    # tests/InversionMethodsTest.cpp:147-175 (random 200x200; LU within 1e-10, Cholesky 1e-4)
+    rng = np.random.default_rng(5)
+    e_lu = e_ch = 0.0
+    for _ in range(5):
+        M = rng.uniform(-1, 1, (200, 200))
+        MM = M @ M.T
+        e_lu += np.linalg.norm(np.linalg.inv(M) - O.invert(M, O.FULL_PIVOT_LU))
+        e_ch += np.linalg.norm(np.linalg.inv(MM) - O.invert(MM, O.SELF_ADJOINT_EIGEN_SOLVER))
+    assert e_lu / 5 < 1e-10 and e_ch / 5 < 1e-4
+
+
+def accumulate(n, step):
+    """val = 0; for i: x_i = val; val += step (the reference's signal generation)."""
+    out, v = [], 0.0
+    for _ in range(n):
+        out.append(v)
+        v += step
+    return np.array(out)
+
+
+def test_lml_brute_force_maximum():
+    # tests/GaussianLikelihoodTest.cpp:51-145: x^2 signal, grid search, mean abs err < 2
+    n = 100
+    xs = accumulate(n, 100.0 / n)
+    idx = list(range(10)) + list(range(80, 90))
+    X, Y = xs[idx][:, None], (xs[idx] ** 2)[:, None]
+    best = (-np.inf, None)
+    for scale in crange(1, 1000, 100):
+        for sigma in crange(1, 100, 2):
+            v = O.lml(f"GaussianKernel({sigma!r},{scale!r},)", X, Y, np.sqrt(0.001), with_grad=False)[0]
+            if v > best[0]:
+                best = (v, (sigma, scale))
+    # the reference predicts with the LAST kernel of the scan (it never re-sets the argmax,
+    # GaussianLikelihoodTest.cpp:117-129); every likelihood evaluation must succeed
+    assert best[1] is not None
+    ks = f"GaussianKernel({sigma!r},{scale!r},)"
+    a, _ = O.fit(ks, X, Y, np.sqrt(0.001))
+    err = np.mean(np.abs(O.predict(ks, X, a, xs[:, None])[:, 0] - xs ** 2))
+    assert err < 2
+
+
+def test_lml_gradient_ascent():
+    # tests/GaussianLikelihoodTest.cpp:147-234: 100 gradient steps from (50, 1300), err < 5
+    n = 101
+    xs = accumulate(n, 100.0 / n)
+    X, Y = xs[::10][:, None], (xs[::10] ** 2)[:, None]
+    sigma, scale = 50.0, 1300.0
+    for _ in range(100):
+        _, g, _, _ = O.lml(f"GaussianKernel({sigma!r},{scale!r},)", X, Y, np.sqrt(0.1))
+        sigma = float(sigma + g[0])
+        scale = float(scale + g[1])
+    ks = f"GaussianKernel({sigma!r},{scale!r},)"
+    a, _ = O.fit(ks, X, Y, np.sqrt(0.1))
+    err = np.mean(np.abs(O.predict(ks, X, a, xs[:, None])[:, 0] - xs ** 2))
+    assert err < 5
+
+
+def test_lml_periodic_period_scan():
+    # tests/GaussianLikelihoodTest.cpp:236-331: period scan, mean abs err < 1e-4
+    n = 200
+    xs = accumulate(n, 50.0 / n)
+    ys = 400 * np.sin(1.5 * xs)
+    idx = list(range(20)) + list(range(80, 100))
+    X, Y = xs[idx][:, None], ys[idx][:, None]
+    best = (-np.inf, None)
+    for period in crange(0.1, 2 * np.pi, 0.01):
+        v = O.lml(f"PeriodicKernel(400,{period!r},1,)", X, Y, np.sqrt(0.001), with_grad=False)[0]
+        if v > best[0]:
+            best = (v, period)
+    ks = f"PeriodicKernel(400,{best[1]!r},1,)"
+    a, _ = O.fit(ks, X, Y, np.sqrt(0.001))
+    err = np.mean(np.abs(O.predict(ks, X, a, xs[:, None])[:, 0] - ys))
+    assert err < 1e-4
+
+
+def test_credible_interval_identity():
+    # tests/PosteriorProcessTest.cpp:51-95: CI(x) == 2 sqrt(gp(x,x)) exactly
+    X = np.array([[i * 2 * np.pi / 20] for i in range(20)])
+    _, C = O.fit("GaussianKernel(0.5,1,)", X, np.sin(X), 0.00001)
+    Xq = np.array([[i * 2 * np.pi / 50 * 1.3] for i in range(50)])
+    c = O.posterior_cov("GaussianKernel(0.5,1,)", X, C, Xq, Xq)
+    ci = 2 * np.sqrt(np.maximum(0.0, c))
+    assert np.all(2 * np.sqrt(c[c >= 0]) - ci[c >= 0] == 0)
+
+
+def test_parameter_order_roundtrip():
+    # tests/{Sum,Product,Periodic,RationalQuadratic}KernelTest.cpp Test2/3:
+    # SetParameters(GetParameters()) leaves the kernel unchanged
+    ks = "SumKernel(GaussianKernel(1.5,0.7,),PeriodicKernel(0.3,2.2,0.9,))"
+    v0, g0 = O.kernel_eval(ks, X0, Y0)
+    v1, g1 = O.kernel_eval_params(ks, np.array([[1.5, 0.7, 0.3, 2.2, 0.9]]), X0, Y0)
+    assert v0 == v1[0] and np.array_equal(g0, g1[0])
