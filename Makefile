@@ -13,7 +13,12 @@ HIP_OBJS := $(patsubst gpr_amd/csrc/%.hip,$(BUILD)/%.o,$(HIP_SRCS))
 CPP_OBJS := $(patsubst gpr_amd/csrc/%.cpp,$(BUILD)/%.o,$(CPP_SRCS))
 HDRS     := $(wildcard gpr_amd/csrc/*.h) include/gprx.h
 
-all: $(LIBDIR)/libgprx.so oracle
+HOST_SRCS := $(wildcard gpr_amd/host/*.cpp)
+HOST_HDRS := $(wildcard include/gpr/*.h) include/gprx.h
+CXXFLAGS  ?= -O2 -std=c++17 -fPIC -Wall -Iinclude
+CPPTESTS  := $(LIBDIR)/gp_host_test $(LIBDIR)/host_cpu_test
+
+all: $(LIBDIR)/libgprx.so $(LIBDIR)/libgpr_amd.so cpptests oracle
 
 $(BUILD)/%.o: gpr_amd/csrc/%.hip $(HDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
@@ -24,6 +29,15 @@ $(BUILD)/%.o: gpr_amd/csrc/%.cpp $(HDRS) | $(BUILD)
 $(LIBDIR)/libgprx.so: $(HIP_OBJS) $(CPP_OBJS) | $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $^ -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 
+# C++ host API (GaussianProcess<T>, Kernel<T>, Likelihood<T>) over libgprx
+$(LIBDIR)/libgpr_amd.so: $(HOST_SRCS) $(HOST_HDRS) $(LIBDIR)/libgprx.so
+	$(CXX) $(CXXFLAGS) -shared -o $@ $(HOST_SRCS) -L$(LIBDIR) -lgprx -Wl,-rpath,'$$ORIGIN'
+
+cpptests: $(CPPTESTS)
+
+$(LIBDIR)/%: tests/cpp/%.cpp $(HOST_HDRS) $(LIBDIR)/libgpr_amd.so
+	$(CXX) $(CXXFLAGS) -o $@ $< -L$(LIBDIR) -lgpr_amd -lgprx -Wl,-rpath,'$$ORIGIN'
+
 oracle:
 	$(MAKE) -s -C oracle
 
@@ -31,7 +45,7 @@ $(BUILD) $(LIBDIR):
 	mkdir -p $@
 
 clean:
-	rm -rf $(BUILD) $(LIBDIR)/*.so
+	rm -rf $(BUILD) $(LIBDIR)/*.so $(CPPTESTS)
 	$(MAKE) -s -C oracle clean
 
-.PHONY: all oracle clean
+.PHONY: all oracle clean cpptests

@@ -220,6 +220,7 @@ struct gprx_model {
     int64_t np = 0, mp = 0, ld = 0;
     double sigma = 0;
     bool has_data = false, has_kernel = false, fitted = false;
+    bool has_alpha = false;  // regression vectors valid (fit, or gprx_model_set_alpha after Load)
     gprx_kernel_desc desc{};
     KCanon<double> kd{};
     KCanon<float> kf{};
@@ -311,6 +312,7 @@ static gprx_status model_fit(gprx_model* M, uint32_t flags, gprx_fit_info* out) 
     GPRX_HIP(hipMemcpy(&hinfo, M->info.p, sizeof(int), hipMemcpyDeviceToHost));
     GPRX_HIP(hipMemcpy(hred, M->red.p, sizeof(hred), hipMemcpyDeviceToHost));
     M->fitted = false;
+    M->has_alpha = false;
     if (out) {
         std::memset(out, 0, sizeof(*out));
         float t01 = 0, t12 = 0, t23 = 0;
@@ -332,6 +334,7 @@ static gprx_status model_fit(gprx_model* M, uint32_t flags, gprx_fit_info* out) 
         throw Error{GPRX_ERR_NOT_SPD, "gprx: kernel matrix is not positive definite (Cholesky pivot " +
                                           std::to_string(hinfo) + " <= 0)"};
     M->fitted = true;
+    M->has_alpha = true;
     return GPRX_OK;
 }
 
@@ -362,7 +365,7 @@ static void download(void* host, const void* dev, size_t bytes, hipStream_t s) {
 
 template <typename T>
 static gprx_status model_predict(gprx_model* M, const void* Xq, int64_t q, void* mean, void* deriv) {
-    GPRX_REQUIRE(M->fitted, GPRX_ERR_STATE, "GaussianProcess::ComputeKernelVectorInternal: gaussian process is not initialized.");
+    GPRX_REQUIRE(M->has_alpha, GPRX_ERR_STATE, "GaussianProcess::ComputeKernelVectorInternal: gaussian process is not initialized.");
     hipStream_t s = M->ctx->stream;
     const KCanon<T>& K = kcanon<T>(M);
     const int d = M->d, m = M->m;
@@ -701,6 +704,7 @@ gprx_status gprx_model_set_data(gprx_model* M, const void* X, const void* Y, int
     M->m = m;
     M->has_data = true;
     M->fitted = false;
+    M->has_alpha = false;
     return GPRX_OK;
     API_END(ctx)
 }
@@ -715,6 +719,7 @@ gprx_status gprx_model_set_kernel(gprx_model* M, const gprx_kernel_desc* k) {
     M->desc = *k;
     M->has_kernel = true;
     M->fitted = false;
+    M->has_alpha = false;
     return GPRX_OK;
     API_END(ctx)
 }
@@ -726,6 +731,7 @@ gprx_status gprx_model_set_noise(gprx_model* M, double sigma) {
     std::lock_guard<std::mutex> lk(M->mu);
     M->sigma = sigma;
     M->fitted = false;
+    M->has_alpha = false;
     return GPRX_OK;
     API_END(ctx)
 }
@@ -745,9 +751,35 @@ gprx_status gprx_model_get_alpha(gprx_model* M, void* alpha) {
     API_BEGIN
     GPRX_REQUIRE(M && alpha, GPRX_ERR_ARG, "gprx_model_get_alpha: NULL argument");
     std::lock_guard<std::mutex> lk(M->mu);
-    GPRX_REQUIRE(M->fitted, GPRX_ERR_STATE, "gprx: model is not fitted");
+    GPRX_REQUIRE(M->has_alpha, GPRX_ERR_STATE, "gprx: model is not fitted");
     GPRX_HIP(hipSetDevice(ctx->device));
     GPRX_HIP(hipMemcpy(alpha, M->alpha.p, esize(M->dt) * M->n * M->m, hipMemcpyDeviceToHost));
+    return GPRX_OK;
+    API_END(ctx)
+}
+
+gprx_status gprx_model_set_alpha(gprx_model* M, const void* alpha) {
+    gprx_ctx* ctx = M ? M->ctx : nullptr;
+    API_BEGIN
+    GPRX_REQUIRE(M && alpha, GPRX_ERR_ARG, "gprx_model_set_alpha: NULL argument");
+    std::lock_guard<std::mutex> lk(M->mu);
+    GPRX_REQUIRE(M->has_data && M->has_kernel, GPRX_ERR_STATE, "gprx_model_set_alpha: set data and kernel first");
+    GPRX_HIP(hipSetDevice(ctx->device));
+    const size_t es = esize(M->dt);
+    M->alpha.ensure(es * M->n * M->m);
+    GPRX_HIP(hipStreamSynchronize(ctx->stream));
+    GPRX_HIP(hipMemcpy(M->alpha.p, alpha, es * M->n * M->m, hipMemcpyHostToDevice));
+    if (M->dt == GPRX_F64 ? M->kd.nper > 0 : M->kf.nper > 0) {
+        const int nper = M->dt == GPRX_F64 ? M->kd.nper : M->kf.nper;
+        M->tab.ensure(es * 2 * nper * M->n * M->d);
+        if (M->dt == GPRX_F64)
+            launch_sincos_tables<double>(M->kd, M->X.as<double>(), M->n, M->d, M->tab.as<double>(), ctx->stream);
+        else
+            launch_sincos_tables<float>(M->kf, M->X.as<float>(), M->n, M->d, M->tab.as<float>(), ctx->stream);
+        GPRX_HIP(hipStreamSynchronize(ctx->stream));
+    }
+    M->has_alpha = true;
+    M->fitted = false;
     return GPRX_OK;
     API_END(ctx)
 }

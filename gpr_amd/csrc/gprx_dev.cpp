@@ -49,8 +49,8 @@ static gprx_status bench_impl(int what, int64_t M, int64_t N, int64_t K, int ite
     int* info = (int*)alloc(sizeof(int));
     float tms = 0;
     try {
-        if (what == 0 || (what >= 10 && what <= 12)) {
-            const int ph = what == 0 ? 3 : what - 10;
+        if (what == 0) {
+            const int ph = 3;
             T* A = (T*)alloc(sizeof(T) * DB * DB * (size_t)iters);
             T* L = (T*)alloc(sizeof(T) * DB * DB);
             for (int it = 0; it < iters; it++)

@@ -26,53 +26,46 @@ namespace gprx {
 // ======================================================================================
 // Diagonal block: factor + inverse, one workgroup of 512 threads.
 //
-// Factorisation: blocked Crout over 8-column blocks.  For block j0 the rows i >= j0 need
-// s_i = A[i, j0:j0+8] - L[i, :j0] L[j0:j0+8, :j0]^T; the j0-long dot products are split
-// over tpr = 512 / (active rows) threads per row (a power of two <= 64, so each group
-// sits inside one wave and reduces with shuffles): the critical path per block stays short
-// as rows retire.  The 8x8 Schur block is factored redundantly by every thread with
-// rsq + Newton reciprocal square roots (no divisions on the chain).
-// Inverse: Linv by 8-row blocks; row block i0 needs, for every column c < i0 + 8,
-// acc[r] = sum_{k=c}^{i0-1} L[i0+r][k] Linv[k][c], again split over threads per column.
-// Linv is kept transposed in the free upper triangle of the LDS image.
-// All register arrays use compile-time indices (no scratch).
+// Right-looking over 8-column steps on an LDS image that holds A's lower triangle and,
+// in the free strict upper triangle plus sDinv, the rows of B = L^{-T}: the identity is
+// appended below A as extra rows that ride along the factorisation (their solved rows are
+// B = I L^{-T}).  B is upper triangular, so it fits exactly in the unused half.  Per step:
+//   A  the 8x8 pivot block is factored redundantly by every thread (rsq + Newton, no
+//      divisions on the chain);
+//   B  one thread per row solves its 8 values x = v Ld^{-T}: rows below the block (L panel)
+//      and the B rows that are already non-zero in these columns;
+//   C  rank-8 update of the trailing lower triangle of A and of the B rows, 4x4 register
+//      blocks per thread, read-modify-write in LDS.
+// Two barriers per step, no cross-thread reductions.  All register arrays are indexed with
+// compile-time indices (no scratch).
 // ======================================================================================
 constexpr int LS = DB + 2;  // LDS row stride (elements); even, keeps 16-B alignment
 constexpr int DT = 512;     // threads of the diagonal kernel
 
-__device__ __forceinline__ int pow2_floor(int x) { return 1 << (31 - __clz(x)); }
-
-template <typename T>
-__device__ __forceinline__ T group_sum(T v, int tpr) {
-    for (int off = tpr >> 1; off > 0; off >>= 1) v += __shfl_xor(v, off);
-    return v;
-}
-
 // 1/sqrt(x) to full precision: hardware estimate + Newton steps (no divide on the chain)
 __device__ __forceinline__ double rsqrt_full(double x) {
     double y = __builtin_amdgcn_rsq(x);
-    double h = 0.5 * x;
+    const double h = 0.5 * x;
     y = y * fma(-h * y, y, 1.5);
     y = y * fma(-h * y, y, 1.5);
     return y;
 }
 __device__ __forceinline__ float rsqrt_full(float x) {
     float y = __builtin_amdgcn_rsqf(x);
-    float h = 0.5f * x;
+    const float h = 0.5f * x;
     y = y * fmaf(-h * y, y, 1.5f);
     return y;
 }
 
-template <typename T, int PH = 3>  // PH: bit0 factorise, bit1 invert (ablation builds only)
+template <typename T>
 __global__ __launch_bounds__(DT) void diag_potrf_kernel(T* __restrict__ A, int64_t ld, T* __restrict__ Linv,
                                                         int* __restrict__ info, int64_t col0) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     T(*sL)[LS] = reinterpret_cast<T(*)[LS]>(smem_raw);
-    T* sDinv = reinterpret_cast<T*>(smem_raw + sizeof(T) * DB * LS);
-    T(*sS)[8] = reinterpret_cast<T(*)[8]>(smem_raw + sizeof(T) * (DB * LS + DB));  // 8x8 staging block
+    T* sDinv = reinterpret_cast<T*>(smem_raw + sizeof(T) * DB * LS);  // B[r][r] = 1 / L[r][r]
 
     const int t = threadIdx.x;
-    {   // column-major global -> row-major LDS; all 32 loads in flight before the stores
+    {   // column-major global -> row-major LDS: A's lower triangle, zeros above (B = I)
         const int r = t & (DB - 1);
         constexpr int NL = DB * DB / DT;
         T v[NL];
@@ -81,47 +74,20 @@ __global__ __launch_bounds__(DT) void diag_potrf_kernel(T* __restrict__ A, int64
 #pragma unroll
         for (int u = 0; u < NL; u++) {
             const int c = (t >> 7) + u * (DT / DB);
-            if (r >= c) sL[r][c] = v[u];
+            sL[r][c] = (r >= c) ? v[u] : T(0);
         }
+        if (t < DB) sDinv[t] = T(1);
     }
     __syncthreads();
 
     bool failed = false;
     int fail_col = 0;
-    for (int j0 = 0; j0 < ((PH & 1) ? DB : 0); j0 += 8) {
-        const int R = DB - j0;                  // active rows j0..127
-        const int tpr = min(64, pow2_floor(DT / R));
-        const int i = j0 + t / tpr;             // row of this thread
-        const int h = t % tpr;
-        const bool active = (t / tpr) < R;
-        T s[8];
-        if (active) {
-            const int kb = (h * j0) / tpr, ke = ((h + 1) * j0) / tpr;
-#pragma unroll
-            for (int q = 0; q < 8; q++) s[q] = (h == 0 && j0 + q <= i) ? sL[i][j0 + q] : T(0);
-            for (int k = kb; k < ke; k++) {
-                const T li = sL[i][k];
-#pragma unroll
-                for (int q = 0; q < 8; q++) s[q] = fma(-li, sL[j0 + q][k], s[q]);
-            }
-        } else {
-#pragma unroll
-            for (int q = 0; q < 8; q++) s[q] = T(0);
-        }
-        if (tpr > 1) {
-#pragma unroll
-            for (int q = 0; q < 8; q++) s[q] = group_sum(s[q], tpr);
-        }
-        if (active && h == 0 && i < j0 + 8) {
-#pragma unroll
-            for (int q = 0; q < 8; q++)
-                if (j0 + q <= i) sS[i - j0][q] = s[q];
-        }
-        __syncthreads();
+    for (int j0 = 0; j0 < DB; j0 += 8) {
+        // ---- A: factor the 8x8 pivot block ------------------------------------------------
         T Ld[8][8], dinv[8];
 #pragma unroll
         for (int c = 0; c < 8; c++) {
-            T dsum = sS[c][c];
+            T dsum = sL[j0 + c][j0 + c];
 #pragma unroll
             for (int k = 0; k < c; k++) dsum = fma(-Ld[c][k], Ld[c][k], dsum);
             if (!(dsum > T(0)) && !failed) {
@@ -133,32 +99,82 @@ __global__ __launch_bounds__(DT) void diag_potrf_kernel(T* __restrict__ A, int64
             dinv[c] = ri;
 #pragma unroll
             for (int r = c + 1; r < 8; r++) {
-                T v = sS[r][c];
+                T v = sL[j0 + r][j0 + c];
 #pragma unroll
                 for (int k = 0; k < c; k++) v = fma(-Ld[r][k], Ld[c][k], v);
                 Ld[r][c] = v * ri;
             }
         }
-        if (active && h == 0) {
-            if (i >= j0 + 8) {
-                T x[8];
+        // ---- B: row solves x = v Ld^{-T} for all 128 rows --------------------------------
+        if (t < DB) {
+            const int row = t;
+            T v[8];
+            if (row >= j0 + 8 || row < j0) {
 #pragma unroll
-                for (int q = 0; q < 8; q++) {
-                    T v = s[q];
-#pragma unroll
-                    for (int q2 = 0; q2 < q; q2++) v = fma(-x[q2], Ld[q][q2], v);
-                    x[q] = v * dinv[q];
-                }
-#pragma unroll
-                for (int q = 0; q < 8; q++) sL[i][j0 + q] = x[q];
+                for (int q = 0; q < 8; q++) v[q] = sL[row][j0 + q];  // L panel row / B row (upper)
             } else {
 #pragma unroll
-                for (int r = 0; r < 8; r++) {
-                    if (i == j0 + r) {
+                for (int q = 0; q < 8; q++) v[q] = (row == j0 + q) ? T(1) : T(0);  // untouched identity row
+            }
+            T x[8];
 #pragma unroll
-                        for (int c = 0; c <= r; c++) sL[i][j0 + c] = Ld[r][c];
-                        sDinv[i] = dinv[r];
-                    }
+            for (int q = 0; q < 8; q++) {
+                T w = v[q];
+#pragma unroll
+                for (int q2 = 0; q2 < q; q2++) w = fma(-x[q2], Ld[q][q2], w);
+                x[q] = w * dinv[q];
+            }
+            if (row >= j0 + 8) {
+#pragma unroll
+                for (int q = 0; q < 8; q++) sL[row][j0 + q] = x[q];
+            } else {
+#pragma unroll
+                for (int q = 0; q < 8; q++) {
+                    const int c = j0 + q;
+                    if (c > row) sL[row][c] = x[q];
+                    else if (c == row) sDinv[row] = x[q];
+                }
+            }
+        }
+        __syncthreads();
+        // ---- C: rank-8 update of the trailing A triangle and the B rows --------------------
+        if (t == 0) {  // the pivot block's L (nobody reads these positions during C)
+#pragma unroll
+            for (int r = 0; r < 8; r++)
+#pragma unroll
+                for (int c = 0; c <= r; c++) sL[j0 + r][j0 + c] = Ld[r][c];
+        }
+        const int jn = j0 + 8;
+#pragma unroll
+        for (int half = 0; half < 2; half++) {
+            const int blk = t + half * DT;
+            const int R0 = (blk >> 5) * 4, C0 = (blk & 31) * 4;
+            if (C0 < jn) continue;
+            const bool arow = R0 >= jn;
+            if (arow && R0 < C0) continue;  // strictly upper part of the trailing A block
+            T Lc[4][8], U[4][8];
+#pragma unroll
+            for (int b = 0; b < 4; b++)
+#pragma unroll
+                for (int q = 0; q < 8; q++) Lc[b][q] = sL[C0 + b][j0 + q];
+#pragma unroll
+            for (int a = 0; a < 4; a++) {
+                const int r = R0 + a;
+#pragma unroll
+                for (int q = 0; q < 8; q++) {
+                    const int c = j0 + q;
+                    U[a][q] = (arow || c > r) ? sL[r][c] : ((c == r) ? sDinv[r] : T(0));
+                }
+            }
+#pragma unroll
+            for (int a = 0; a < 4; a++) {
+#pragma unroll
+                for (int b = 0; b < 4; b++) {
+                    if (arow && R0 + a < C0 + b) continue;
+                    T acc = sL[R0 + a][C0 + b];
+#pragma unroll
+                    for (int q = 0; q < 8; q++) acc = fma(-U[a][q], Lc[b][q], acc);
+                    sL[R0 + a][C0 + b] = acc;
                 }
             }
         }
@@ -166,63 +182,10 @@ __global__ __launch_bounds__(DT) void diag_potrf_kernel(T* __restrict__ A, int64
     }
     if (t == 0 && failed) atomicMin(info, (int)(col0 + fail_col + 1));
 
-    {   // L (lower) back to global
-        const int r = t & (DB - 1);
-        for (int c = t >> 7; c < DB; c += DT / DB)
-            if (r >= c) A[r + (int64_t)c * ld] = sL[r][c];
-    }
-
-    // ---- Linv by 8-row blocks (stored transposed: sL[c][k] = Linv[k][c] for k > c) --------
-    if (!(PH & 1) && t < DB) sDinv[t] = T(1);
-    __syncthreads();
-    for (int i0 = 0; i0 < ((PH & 2) ? DB : 0); i0 += 8) {
-        const int C = i0 + 8;                   // columns 0..i0+7 take part
-        const int tpc = min(64, pow2_floor(DT / C));
-        const int c = t / tpc;
-        const int h = t % tpc;
-        const bool active = c < C;
-        T acc[8];
-#pragma unroll
-        for (int r = 0; r < 8; r++) acc[r] = T(0);
-        if (active && c < i0) {
-            // k = c term uses Linv[c][c] = sDinv[c]; then k = c+1 .. i0-1 from the transposed store
-            const int len = i0 - c;
-            const int kb = c + (h * len) / tpc, ke = c + ((h + 1) * len) / tpc;
-            for (int k = kb; k < ke; k++) {
-                const T u = (k == c) ? sDinv[c] : sL[c][k];
-#pragma unroll
-                for (int r = 0; r < 8; r++) acc[r] = fma(sL[i0 + r][k], u, acc[r]);
-            }
-        }
-        if (tpc > 1) {
-#pragma unroll
-            for (int r = 0; r < 8; r++) acc[r] = group_sum(acc[r], tpc);
-        }
-        if (active && h == 0) {
-            T x[8];
-#pragma unroll
-            for (int r = 0; r < 8; r++) {
-                const int row = i0 + r;
-                if (row < c) {
-                    x[r] = T(0);
-                } else if (row == c) {
-                    x[r] = sDinv[c];
-                } else {
-                    T v = -acc[r];
-#pragma unroll
-                    for (int r2 = 0; r2 < r; r2++) v = fma(-sL[row][i0 + r2], x[r2], v);
-                    x[r] = v * sDinv[row];
-                }
-            }
-#pragma unroll
-            for (int r = 0; r < 8; r++)
-                if (i0 + r > c) sL[c][i0 + r] = x[r];
-        }
-        __syncthreads();
-    }
-    {   // Linv -> global (column-major, ld = DB, zeros above the diagonal)
+    {   // L (lower) and Linv = B^T (column-major, ld = DB, zeros above the diagonal) to global
         const int r = t & (DB - 1);
         for (int c = t >> 7; c < DB; c += DT / DB) {
+            if (r >= c) A[r + (int64_t)c * ld] = sL[r][c];
             const T v = (r > c) ? sL[c][r] : ((r == c) ? sDinv[c] : T(0));
             Linv[r + c * DB] = v;
         }
@@ -454,7 +417,7 @@ void launch_gemm_nt_kskip(T* C, int64_t ldc, const T* A, int64_t lda, const T* B
 
 template <typename T>
 static size_t diag_lds_bytes() {
-    return sizeof(T) * (DB * LS + DB + 64);
+    return sizeof(T) * (DB * LS + DB);
 }
 
 template <typename T>
@@ -470,27 +433,16 @@ static void launch_diag(T* Akk, int64_t ld, T* Lk, int* info, int64_t col0, hipS
 }
 
 template <typename T>
-void launch_diag_public(T* Akk, int64_t ld, T* Lk, int* info, int64_t col0, hipStream_t s, int ph = 3) {
-    if (ph == 3) {
-        launch_diag<T>(Akk, ld, Lk, info, col0, s);
-        return;
-    }
-    const size_t lds = diag_lds_bytes<T>();
-    auto k0 = diag_potrf_kernel<T, 0>;
-    auto k1 = diag_potrf_kernel<T, 1>;
-    auto k2 = diag_potrf_kernel<T, 2>;
-    const void* f = ph == 0 ? (const void*)k0 : (ph == 1 ? (const void*)k1 : (const void*)k2);
-    hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (ph == 0) hipLaunchKernelGGL(k0, dim3(1), dim3(DT), lds, s, Akk, ld, Lk, info, col0);
-    else if (ph == 1) hipLaunchKernelGGL(k1, dim3(1), dim3(DT), lds, s, Akk, ld, Lk, info, col0);
-    else hipLaunchKernelGGL(k2, dim3(1), dim3(DT), lds, s, Akk, ld, Lk, info, col0);
+void launch_diag_public(T* Akk, int64_t ld, T* Lk, int* info, int64_t col0, hipStream_t s, int ph) {
+    (void)ph;
+    launch_diag<T>(Akk, ld, Lk, info, col0, s);
 }
 template void launch_diag_public<double>(double*, int64_t, double*, int*, int64_t, hipStream_t, int);
 template void launch_diag_public<float>(float*, int64_t, float*, int*, int64_t, hipStream_t, int);
 
 int outer_block() {
     static int nbo = [] {
-        int v = 256;
+        int v = 512;
         if (const char* e = std::getenv("GPRX_NBO")) v = std::atoi(e);
         if (v < DB) v = DB;
         return (v / DB) * DB;

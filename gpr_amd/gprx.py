@@ -33,6 +33,7 @@ EXPORTED = [
     "gprx_abi_version", "gprx_device_count", "gprx_ctx_create", "gprx_dist_unique_id", "gprx_ctx_create_dist",
     "gprx_ctx_destroy", "gprx_last_error", "gprx_model_create", "gprx_model_destroy", "gprx_model_set_data",
     "gprx_model_set_kernel", "gprx_model_set_noise", "gprx_model_fit", "gprx_model_get_alpha",
+    "gprx_model_set_alpha",
     "gprx_model_predict", "gprx_model_posterior_cov", "gprx_model_core_matrix", "gprx_model_lml",
     "gprx_kernel_matrix", "gprx_cross_matrix", "gprx_deriv_matrix", "gprx_cholesky", "gprx_spd_inverse",
     "gprx_sparse_fit", "gprx_ctx_set_stats", "gprx_ctx_get_stats",
@@ -89,6 +90,7 @@ def lib():
         L.gprx_model_set_noise.argtypes = [ctypes.c_void_p, ctypes.c_double]
         L.gprx_model_fit.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(FitInfo)]
         L.gprx_model_get_alpha.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        L.gprx_model_set_alpha.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         L.gprx_model_predict.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
                                          ctypes.c_void_p]
         L.gprx_model_posterior_cov.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
@@ -301,6 +303,10 @@ class Model:
         a = np.empty((self.n, self.m), self.dtype)
         self._c(lib().gprx_model_get_alpha(self.h, _ptr(a)))
         return a
+
+    def set_alpha(self, alpha):
+        a = np.ascontiguousarray(alpha, self.dtype).reshape(self.n, self.m)
+        self._c(lib().gprx_model_set_alpha(self.h, _ptr(a)))
 
     def predict(self, Xq, deriv=False):
         Xq = np.ascontiguousarray(Xq, self.dtype)

@@ -153,6 +153,11 @@ gprx_status gprx_model_set_noise(gprx_model* model, double sigma);
 gprx_status gprx_model_fit(gprx_model* model, uint32_t flags, gprx_fit_info* info);
 /* m_RegressionVectors (lib/GaussianProcess.cpp:661) -> host, N x m. */
 gprx_status gprx_model_get_alpha(gprx_model* model, void* alpha);
+/* Install regression vectors (n x m, row-major) read back by GaussianProcess::Load
+ * (lib/GaussianProcess.cpp:184-268, which restores m_RegressionVectors from file rather
+ * than recomputing them).  Enables predict; the factor needed by posterior_cov / lml /
+ * core_matrix is rebuilt by the next gprx_model_fit. */
+gprx_status gprx_model_set_alpha(gprx_model* model, const void* alpha);
 /* Predict / PredictDerivative for q queries (lib/GaussianProcess.cpp:54-81, 684-706):
  * mean is q x m; deriv (optional, may be NULL) is q x d x m with the reference's formula
  * D(:,c) = -X^T (Kx o alpha_c) (:77-79). */

@@ -25,8 +25,7 @@ if cases in ("all", "diag"):
     for dt in (F64, F32):
         ms = run(dt, 0, 128, iters=50)
         res[f"diag128_{'f64' if dt else 'f32'}_us"] = ms * 1e3
-    for ph, name in ((10, "loadstore"), (11, "factor_only"), (12, "inverse_only")):
-        res[f"diag128_f64_{name}_us"] = run(F64, ph, 128, iters=50) * 1e3
+
 if cases in ("all", "gemm"):
     for (M, N, K, low) in [(16384, 16384, 256, 1), (16384, 16384, 512, 1), (8192, 8192, 256, 1), (16384, 128, 128, 0),
                            (16384, 256, 256, 0), (8192, 8192, 1024, 0), (4096, 4096, 4096, 0)]:

@@ -1,0 +1,310 @@
+// gp_host_test.cpp — the reference's GaussianProcessTest / IOTest scenarios
+// (tests/GaussianProcessTest.cpp:26-330, tests/IOTest.cpp:30-200) restated against the
+// gpr:: host API, which runs every fit / predict on the GPU through libgprx.  Same
+// inputs, same pass thresholds.  Prints one line per case; exit status = #failures.
+// Built by `make cpptests`; driven by tests/test_host_api.py (-m gpu).
+#include <cmath>
+#include <cstdio>
+#include <functional>
+#include <iostream>
+#include <sstream>
+
+#include "gpr/GaussianProcess.h"
+#include "gpr/Kernel.h"
+#include "gpr/Likelihood.h"
+#include "gpr/MatrixIO.h"
+
+using namespace gpr;
+
+template <class T>
+using GP = GaussianProcess<T>;
+
+static int g_fail = 0;
+static void run(const char* name, const std::function<void()>& f) {
+    try {
+        f();
+        std::printf("PASS %s\n", name);
+    } catch (const std::string& s) {
+        std::printf("FAIL %s: %s\n", name, s.c_str());
+        g_fail++;
+    }
+    std::fflush(stdout);
+}
+
+static void check(bool ok, const std::string& what) {
+    if (!ok) throw what;
+}
+static std::string num(double v) {
+    std::ostringstream s;
+    s << v;
+    return s.str();
+}
+
+// GaussianProcessTest Test1: sinus regression, threshold 0.0008
+static void gp_test1() {
+    typedef GP<double> G;
+    auto gp = std::make_shared<G>(std::make_shared<GaussianKernel<double>>(2.889));
+    gp->SetSigma(0);
+    const unsigned ns = 10;
+    for (unsigned i = 0; i < ns; i++) {
+        G::VectorType x(1), y(1);
+        x(0) = i * 2 * M_PI / ns;
+        y(0) = std::sin(x(0));
+        gp->AddSample(x, y);
+    }
+    gp->Initialize();
+    double err = 0;
+    for (unsigned i = 0; i < 50; i++) {
+        G::VectorType x(1);
+        x(0) = i * 2 * M_PI / 50;
+        err += std::fabs(gp->Predict(x)(0) - std::sin(x(0)));
+    }
+    check(err <= 0.0008, num(err));
+}
+
+// Test2: 2-D input, sin/cos output, threshold 0.005
+static void gp_test2() {
+    typedef GP<double> G;
+    auto gp = std::make_shared<G>(std::make_shared<GaussianKernel<double>>(3.24));
+    gp->SetSigma(0);
+    const unsigned ns = 10;
+    for (unsigned i = 0; i < ns; i++) {
+        G::VectorType x(2), y(2);
+        x(0) = x(1) = i * 2 * M_PI / ns;
+        y(0) = std::sin(x(0));
+        y(1) = std::cos(x(1));
+        gp->AddSample(x, y);
+    }
+    gp->Initialize();
+    double err = 0;
+    for (unsigned i = 0; i < 50; i++) {
+        G::VectorType x(2);
+        x(0) = x(1) = i * 2 * M_PI / 50;
+        G::VectorType p = gp->Predict(x);
+        err += std::fabs(p(0) - std::sin(x(0))) + std::fabs(p(1) - std::cos(x(1)));
+    }
+    check(err <= 0.005, num(err));
+}
+
+// Test3: 2500 random 73-D samples / labels, sigma 0.01 (a timing case in the reference)
+static void gp_test3() {
+    typedef GP<double> G;
+    auto gp = std::make_shared<G>(std::make_shared<GaussianKernel<double>>(4));
+    gp->SetSigma(0.01);
+    for (unsigned i = 0; i < 2500; i++) gp->AddSample(G::VectorType::Random(73), G::VectorType::Random(73));
+    gp->Initialize();
+    for (unsigned i = 0; i < 50; i++) {
+        G::VectorType p = gp->Predict(G::VectorType::Random(73));
+        for (std::size_t c = 0; c < p.size(); c++) check(std::isfinite(p(c)), "non-finite prediction");
+    }
+}
+
+// Test4: four 2-D landmarks, scalar output (the reference only checks it runs)
+static void gp_test4() {
+    typedef GP<double> G;
+    auto gp = std::make_shared<G>(std::make_shared<GaussianKernel<double>>(3.24));
+    gp->SetSigma(0);
+    const double pts[4][3] = {{0, 0, 10}, {5, 0, 3}, {5, 8, 3}, {3, 5, 5}};
+    for (auto& p : pts) {
+        G::VectorType x(2), y(1);
+        x(0) = p[0];
+        x(1) = p[1];
+        y(0) = p[2];
+        gp->AddSample(x, y);
+    }
+    gp->Initialize();
+    for (unsigned i = 0; i < 50; i++)
+        for (unsigned j = 0; j < 50; j++) {
+            G::VectorType x(2);
+            x(0) = double(i) / 8;
+            x(1) = double(j) / 8;
+            check(std::isfinite(gp->Predict(x)(0)), "non-finite prediction");
+        }
+    // the GP interpolates its landmarks (sigma = 0)
+    for (auto& p : pts) {
+        G::VectorType x(2);
+        x(0) = p[0];
+        x(1) = p[1];
+        check(std::fabs(gp->Predict(x)(0) - p[2]) < 1e-6, "landmark not interpolated");
+    }
+}
+
+// Test5: derivative process of a sinus is a cosinus, threshold 0.6
+static void gp_test5() {
+    typedef GP<double> G;
+    auto gp = std::make_shared<G>(std::make_shared<GaussianKernel<double>>(1));
+    gp->SetSigma(0);
+    const unsigned ns = 20;
+    for (unsigned i = 0; i < ns; i++) {
+        G::VectorType x(1), y(1);
+        x(0) = i * 4 * M_PI / ns;
+        y(0) = std::sin(x(0));
+        gp->AddSample(x, y);
+    }
+    gp->Initialize();
+    double err = 0;
+    for (unsigned i = 0; i < 50; i++) {
+        G::VectorType x(1);
+        x(0) = i * 4 * M_PI / 50;
+        G::MatrixType D;
+        gp->PredictDerivative(x, D);
+        err += std::fabs(D(0, 0) - std::cos(x(0)));
+    }
+    check(err <= 0.6, num(err));
+}
+
+// Test6: derivative of a vector-valued process (the reference prints the error only)
+static void gp_test6() {
+    typedef GP<double> G;
+    auto gp = std::make_shared<G>(std::make_shared<GaussianKernel<double>>(1.2));
+    gp->SetSigma(0.01);
+    const unsigned ns = 20;
+    for (unsigned i = 0; i < ns; i++) {
+        G::VectorType x(2), y(3);
+        x(0) = x(1) = i * 4 * M_PI / ns;
+        y(0) = std::sin(x(0));
+        y(1) = std::cos(x(1));
+        y(2) = x(0);
+        gp->AddSample(x, y);
+    }
+    gp->Initialize();
+    double err = 0;
+    for (unsigned i = 0; i < 50; i++) {
+        G::VectorType x(2);
+        x(0) = x(1) = i * 4 * M_PI / 50;
+        G::MatrixType D;
+        gp->PredictDerivative(x, D);
+        check(D.rows() == 2 && D.cols() == 3, "derivative shape");
+        err += std::fabs(D(0, 0) - std::cos(x(0))) + std::fabs(D(1, 0) - std::sin(x(1))) + std::fabs(D(2, 0) - 0.5);
+    }
+    check(std::isfinite(err), "non-finite derivative");
+}
+
+// Test7: a zero Gaussian sigma must throw on evaluation
+static void gp_test7() {
+    bool threw = false;
+    try {
+        GaussianKernel<double> k(0);
+        GP<double>::VectorType x(1), y(1);
+        x(0) = 3.4;
+        y(0) = 2.8;
+        (void)k(x, y);
+    } catch (...) {
+        threw = true;
+    }
+    check(threw, "zero sigma accepted");
+}
+
+// IOTest Test1: write / read random matrices (double and float) bit-exactly
+static void io_test1() {
+    GP<double>::MatrixType a = GP<double>::MatrixType::Random(100, 50);
+    WriteMatrix(a, "/tmp/gpr_amd_io_dp.txt");
+    auto ar = ReadMatrix<GP<double>::MatrixType>("/tmp/gpr_amd_io_dp.txt");
+    GP<float>::MatrixType b = GP<float>::MatrixType::Random(50, 100);
+    WriteMatrix(b, "/tmp/gpr_amd_io_sp.txt");
+    auto br = ReadMatrix<GP<float>::MatrixType>("/tmp/gpr_amd_io_sp.txt");
+    check((a - ar).norm() == 0 && (b - br).norm() == 0, "matrix io mismatch");
+}
+
+static std::shared_ptr<GP<float>> io_gp(bool efficient) {
+    auto gp = std::make_shared<GP<float>>(std::make_shared<GaussianKernel<float>>(std::sqrt(2)));
+    gp->SetSigma(0);
+    if (efficient) gp->SetEfficientStorage(true);
+    for (unsigned i = 0; i < 10; i++) {
+        GP<float>::VectorType x(2), y(2);
+        x(0) = x(1) = i * 2 * M_PI / 10;
+        y(0) = std::sin(x(0));
+        y(1) = std::cos(x(1));
+        gp->AddSample(x, y);
+    }
+    gp->Initialize();
+    return gp;
+}
+
+// IOTest Test2: save / load round trip compares equal
+static void io_test2() {
+    auto gp = io_gp(false);
+    gp->Save("/tmp/gpr_amd_io_test-");
+    auto rd = std::make_shared<GP<float>>(std::make_shared<GaussianKernel<float>>(1));
+    rd->Load("/tmp/gpr_amd_io_test-");
+    check(*gp == *rd, "read/write");
+}
+
+// IOTest Test3.1 / 3.2: efficient storage, late core construction changes ==
+static void io_test3() {
+    auto gp0 = std::make_shared<GP<float>>(std::make_shared<GaussianKernel<float>>(1));
+    check(!gp0->GetEfficientStorage(), "efficient storage must be off by default");
+    auto gp = io_gp(true);
+    GP<float>::VectorType x(2);
+    x(0) = x(1) = 2.56 * 2 * M_PI / 10;
+    GP<float>::VectorType yt = gp->Predict(x);
+    gp->Save("/tmp/gpr_amd_io_test-");
+    {
+        auto rd = std::make_shared<GP<float>>(std::make_shared<GaussianKernel<float>>(1));
+        rd->Load("/tmp/gpr_amd_io_test-");
+        check(*gp == *rd, "3.1 compare");
+        check((yt - rd->Predict(x)).norm() < 1e-6, "3.1 predict " + num((yt - rd->Predict(x)).norm()));
+    }
+    {
+        auto rd = std::make_shared<GP<float>>(std::make_shared<GaussianKernel<float>>(1));
+        rd->Load("/tmp/gpr_amd_io_test-");
+        (void)(*rd)(x, x);
+        check(!(*gp == *rd), "Comparison with late core matrix construction not right.");
+        (void)(*gp)(x, x);
+        check(*gp == *rd, "Comparison with late core matrix construction not right.");
+        check((yt - rd->Predict(x)).norm() < 1e-6, "3.2 predict");
+    }
+}
+
+// Likelihood: value and gradient through the host classes are finite and the gradient
+// matches a central difference of the value (GaussianLikelihoodTest's consistency idea).
+static void lik_test() {
+    typedef GP<double> G;
+    auto k = std::make_shared<GaussianKernel<double>>(1.3, 0.8);
+    auto gp = std::make_shared<G>(k);
+    gp->SetSigma(0.1);
+    for (unsigned i = 0; i < 64; i++) {
+        G::VectorType x(1), y(1);
+        x(0) = -3 + 6.0 * i / 63;
+        y(0) = std::sin(2 * x(0)) + 0.1 * std::cos(7 * x(0));
+        gp->AddSample(x, y);
+    }
+    GaussianLogLikelihood<double> lik;
+    auto vg = lik.GetValueAndParameterDerivatives(gp);
+    check(std::isfinite(vg.first(0)), "likelihood not finite");
+    auto p = k->GetParameters();
+    for (std::size_t i = 0; i < p.size(); i++) {
+        const double h = 1e-5;
+        auto pp = p, pm = p;
+        pp[i] += h;
+        pm[i] -= h;
+        k->SetParameters(pp);
+        gp->SetKernel(k);
+        const double vp = lik(gp)(0);
+        k->SetParameters(pm);
+        gp->SetKernel(k);
+        const double vm = lik(gp)(0);
+        const double fd = (vp - vm) / (2 * h);
+        check(std::fabs(fd - vg.second(i)) <= 1e-4 * std::max(1.0, std::fabs(fd)),
+              "grad " + num(vg.second(i)) + " vs fd " + num(fd));
+    }
+    k->SetParameters(p);
+    GaussianLikelihood<double> plain;
+    const double lv = plain(gp)(0);
+    check(std::isfinite(lv) && lv >= 0, "GaussianLikelihood value " + num(lv));
+}
+
+int main() {
+    run("GaussianProcessTest1", gp_test1);
+    run("GaussianProcessTest2", gp_test2);
+    run("GaussianProcessTest3", gp_test3);
+    run("GaussianProcessTest4", gp_test4);
+    run("GaussianProcessTest5", gp_test5);
+    run("GaussianProcessTest6", gp_test6);
+    run("GaussianProcessTest7", gp_test7);
+    run("IOTest1", io_test1);
+    run("IOTest2", io_test2);
+    run("IOTest3", io_test3);
+    run("LikelihoodGradient", lik_test);
+    return g_fail;
+}

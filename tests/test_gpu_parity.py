@@ -152,3 +152,28 @@ def test_nonfinite_kernel_matrix(ctx):
     with pytest.raises(gpr_amd.GprxError) as e:
         ctx.kernel_matrix("GaussianKernel(1,1,)", X)
     assert "not finite" in str(e.value)
+
+
+@pytest.mark.parametrize("ks", [KERNELS[0], KERNELS[4]])
+def test_set_alpha_restores_predict(ctx, ks):
+    """gprx_model_set_alpha (GaussianProcess::Load path, lib/GaussianProcess.cpp:184-268):
+    installed regression vectors give bit-identical predictions; the factor-based calls
+    need a refit first."""
+    import gpr_amd
+    from gpr_amd import gprx
+    n, d, m, sigma = 260, 3, 2, 0.5
+    X, Y = make_data(n, d, m)
+    M, _ = _fit(ctx, ks, X, Y, sigma, np.float64)
+    Xq = make_queries(33, d)
+    mean, D = M.predict(Xq, deriv=True)
+    M2 = gprx.Model(ctx, np.float64)
+    M2.set_data(X, Y)
+    M2.set_kernel(ks)
+    M2.set_noise(sigma)
+    M2.set_alpha(M.alpha())
+    mean2, D2 = M2.predict(Xq, deriv=True)
+    assert np.array_equal(mean, mean2) and np.array_equal(D, D2)
+    with pytest.raises(gpr_amd.GprxError):
+        M2.posterior_cov(Xq, Xq)
+    M2.fit()
+    assert np.array_equal(M2.alpha(), M.alpha())
