@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <climits>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <mutex>
@@ -647,7 +648,27 @@ gprx_status gprx_ctx_create(int device, gprx_ctx** out) {
     int prio_lo = 0, prio_hi = 0;
     GPRX_HIP(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
     GPRX_HIP(hipStreamCreateWithPriority(&ctx->stream, hipStreamNonBlocking, prio_hi));
-    GPRX_HIP(hipStreamCreateWithPriority(&ctx->aux, hipStreamNonBlocking, prio_lo));
+    // The aux stream (bulk trailing updates) is kept off a few CUs so the panel chain's
+    // one-workgroup diagonal kernels never queue behind a full-chip GEMM: GPRX_RESERVE_CU
+    // CUs (default 8, one per XCD when CUs are numbered XCD-major) are excluded from its mask.
+    int reserve = 8;
+    if (const char* e = std::getenv("GPRX_RESERVE_CU")) reserve = std::atoi(e);
+    hipDeviceProp_t prop;
+    GPRX_HIP(hipGetDeviceProperties(&prop, device));
+    const int ncu = prop.multiProcessorCount;
+    if (reserve > 0 && reserve < ncu) {
+        std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+        const int per = std::max(1, reserve / 8), stride = std::max(1, ncu / 8);
+        int excluded = 0;
+        for (int i = 0; i < ncu; i++) {
+            const bool res = (i % stride) < per && excluded < reserve;
+            if (res) excluded++;
+            else mask[i / 32] |= 1u << (i % 32);
+        }
+        GPRX_HIP(hipExtStreamCreateWithCUMask(&ctx->aux, (uint32_t)mask.size(), mask.data()));
+    } else {
+        GPRX_HIP(hipStreamCreateWithPriority(&ctx->aux, hipStreamNonBlocking, prio_lo));
+    }
     ctx->ex.s0 = ctx->stream;
     ctx->ex.s1 = ctx->aux;
     for (auto& e : ctx->ev) GPRX_HIP(hipEventCreate(&e));
@@ -778,8 +799,7 @@ gprx_status gprx_model_set_alpha(gprx_model* M, const void* alpha) {
             launch_sincos_tables<float>(M->kf, M->X.as<float>(), M->n, M->d, M->tab.as<float>(), ctx->stream);
         GPRX_HIP(hipStreamSynchronize(ctx->stream));
     }
-    M->has_alpha = true;
-    M->fitted = false;
+    M->has_alpha = true;  // the factor (if any) is left as it is
     return GPRX_OK;
     API_END(ctx)
 }

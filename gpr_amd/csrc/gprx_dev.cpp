@@ -15,6 +15,8 @@ void launch_gemm_nt(T* C, int64_t ldc, const T* A, int64_t lda, const T* B, int6
                     int64_t K, T alpha, T beta, bool lower, hipStream_t s);
 template <typename T>
 void launch_diag_public(T* Akk, int64_t ld, T* Lk, int* info, int64_t col0, hipStream_t s, int ph = 3);
+template <typename T>
+void launch_diag_prof(T* Akk, int64_t ld, T* Lk, int* info, long long* prof, hipStream_t s);
 }  // namespace gprx
 
 using namespace gprx;
@@ -49,7 +51,20 @@ static gprx_status bench_impl(int what, int64_t M, int64_t N, int64_t K, int ite
     int* info = (int*)alloc(sizeof(int));
     float tms = 0;
     try {
-        if (what == 0) {
+        if (what == 6) {  // in-kernel phase ticks of the diagonal kernel: ms[0..4] per launch
+            T* A = (T*)alloc(sizeof(T) * DB * DB * (size_t)iters);
+            T* L = (T*)alloc(sizeof(T) * DB * DB);
+            long long* pr = (long long*)alloc(sizeof(long long) * 8);
+            (void)hipMemset(pr, 0, sizeof(long long) * 8);
+            for (int it = 0; it < iters; it++)
+                hipLaunchKernelGGL(dev_fill_spd<T>, dim3((DB * DB + 255) / 256), dim3(256), 0, s, A + (size_t)it * DB * DB,
+                                   (int64_t)DB, (int64_t)DB, (uint64_t)it);
+            for (int it = 0; it < iters; it++) launch_diag_prof<T>(A + (size_t)it * DB * DB, DB, L, info, pr, s);
+            long long h[8];
+            (void)hipStreamSynchronize(s);
+            (void)hipMemcpy(h, pr, sizeof(h), hipMemcpyDeviceToHost);
+            for (int i = 0; i < 5; i++) ms[i] = (double)h[i] / iters;
+        } else if (what == 0) {
             const int ph = 3;
             T* A = (T*)alloc(sizeof(T) * DB * DB * (size_t)iters);
             T* L = (T*)alloc(sizeof(T) * DB * DB);

@@ -26,21 +26,33 @@ namespace gprx {
 // ======================================================================================
 // Diagonal block: factor + inverse, one workgroup of 512 threads.
 //
-// Right-looking over 8-column steps on an LDS image that holds A's lower triangle and,
-// in the free strict upper triangle plus sDinv, the rows of B = L^{-T}: the identity is
-// appended below A as extra rows that ride along the factorisation (their solved rows are
-// B = I L^{-T}).  B is upper triangular, so it fits exactly in the unused half.  Per step:
-//   A  the 8x8 pivot block is factored redundantly by every thread (rsq + Newton, no
-//      divisions on the chain);
-//   B  one thread per row solves its 8 values x = v Ld^{-T}: rows below the block (L panel)
-//      and the B rows that are already non-zero in these columns;
-//   C  rank-8 update of the trailing lower triangle of A and of the B rows, 4x4 register
-//      blocks per thread, read-modify-write in LDS.
-// Two barriers per step, no cross-thread reductions.  All register arrays are indexed with
-// compile-time indices (no scratch).
+// The 128x128 block lives in REGISTERS as a square image S: the lower triangle holds A
+// (becoming L), the strict upper triangle the rows of B = L^{-T} (its diagonal in Bd).  B
+// comes from appending the identity below A: its rows ride along the elimination and end as
+// I L^{-T}; being upper triangular they fit the unused half exactly.  Thread t owns a fixed
+// 4-row x 8-column block: wave w holds column blocks 2w, 2w+1 (lane>>5), row block lane&31.
+// Right-looking over 8-column steps J = [j0, j0+8):
+//   1  128 threads (waves 0-1, one row each) factor the 8x8 pivot redundantly (rsq +
+//      Newton, no divide) and solve their row x = v Ld^{-T} (A rows below J: L panel; B rows
+//      above J; pivot rows: identity rows), reading v from the LDS column panel sV that the
+//      owners of J published, writing x to sP (and Ld to sLd);
+//   2  every thread with trailing columns applies S -= x_r x_c^T to its block, unmasked:
+//      entries right of the diagonal in rows not yet reached are scratch and are zeroed when
+//      their rows become pivot rows (their identity rows are still zero there).  The owners
+//      of J take their final values from sP/sLd; the owners of the next column block
+//      publish it in sV.
+// Two barriers per step.  The result is staged through LDS so L and Linv = B^T leave in
+// coalesced column-major stores.  All register arrays use compile-time indices.
 // ======================================================================================
-constexpr int LS = DB + 2;  // LDS row stride (elements); even, keeps 16-B alignment
-constexpr int DT = 512;     // threads of the diagonal kernel
+constexpr int DT = 512;      // threads of the diagonal kernel
+constexpr int SPL = DB + 4;  // panel row stride (elements)
+constexpr int SIL = DB + 2;  // output staging image row stride (elements)
+
+template <typename T>
+constexpr size_t diag_lds_bytes() {
+    return sizeof(T) * ((size_t)DB * SIL + DB) > sizeof(T) * (2 * 8 * SPL + 64) ? sizeof(T) * ((size_t)DB * SIL + DB)
+                                                                             : sizeof(T) * (2 * 8 * SPL + 64);
+}
 
 // 1/sqrt(x) to full precision: hardware estimate + Newton steps (no divide on the chain)
 __device__ __forceinline__ double rsqrt_full(double x) {
@@ -57,138 +69,169 @@ __device__ __forceinline__ float rsqrt_full(float x) {
     return y;
 }
 
-template <typename T>
+template <typename T, bool PROF = false>
 __global__ __launch_bounds__(DT) void diag_potrf_kernel(T* __restrict__ A, int64_t ld, T* __restrict__ Linv,
-                                                        int* __restrict__ info, int64_t col0) {
+                                                        int* __restrict__ info, int64_t col0,
+                                                        long long* __restrict__ prof = nullptr) {
+    long long tp0 = 0, tp1 = 0, tph1 = 0, tph2 = 0, tmark = 0;
+    if (PROF) tp0 = __builtin_amdgcn_s_memtime();
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    T(*sL)[LS] = reinterpret_cast<T(*)[LS]>(smem_raw);
-    T* sDinv = reinterpret_cast<T*>(smem_raw + sizeof(T) * DB * LS);  // B[r][r] = 1 / L[r][r]
+    T(*sV)[SPL] = reinterpret_cast<T(*)[SPL]>(smem_raw);              // v of column block J
+    T(*sP)[SPL] = reinterpret_cast<T(*)[SPL]>(smem_raw + sizeof(T) * 8 * SPL);  // solved x
+    T(*sLd)[8] = reinterpret_cast<T(*)[8]>(smem_raw + sizeof(T) * 16 * SPL);   // pivot factor
 
-    const int t = threadIdx.x;
-    {   // column-major global -> row-major LDS: A's lower triangle, zeros above (B = I)
-        const int r = t & (DB - 1);
-        constexpr int NL = DB * DB / DT;
-        T v[NL];
+    const int t = threadIdx.x, w = t >> 6, l = t & 63;
+    const int R0 = (l & 31) * 4;
+    const int cbi = 2 * w + (l >> 5);  // column block index (8 columns)
+    const int C0 = cbi * 8;
+
+    T S[4][8];
+    T Bd[4];
 #pragma unroll
-        for (int u = 0; u < NL; u++) v[u] = A[r + (int64_t)((t >> 7) + u * (DT / DB)) * ld];
+    for (int b = 0; b < 8; b++)
 #pragma unroll
-        for (int u = 0; u < NL; u++) {
-            const int c = (t >> 7) + u * (DT / DB);
-            sL[r][c] = (r >= c) ? v[u] : T(0);
-        }
-        if (t < DB) sDinv[t] = T(1);
+        for (int a = 0; a < 4; a++) S[a][b] = A[R0 + a + (int64_t)(C0 + b) * ld];
+#pragma unroll
+    for (int a = 0; a < 4; a++) Bd[a] = T(1);
+    if (cbi == 0) {
+#pragma unroll
+        for (int a = 0; a < 4; a++)
+#pragma unroll
+            for (int b = 0; b < 8; b++) sV[b][R0 + a] = S[a][b];
     }
     __syncthreads();
+    if (PROF) tp1 = tmark = __builtin_amdgcn_s_memtime();
 
-    bool failed = false;
-    int fail_col = 0;
+    int fail_col = -1;
     for (int j0 = 0; j0 < DB; j0 += 8) {
-        // ---- A: factor the 8x8 pivot block ------------------------------------------------
-        T Ld[8][8], dinv[8];
-#pragma unroll
-        for (int c = 0; c < 8; c++) {
-            T dsum = sL[j0 + c][j0 + c];
-#pragma unroll
-            for (int k = 0; k < c; k++) dsum = fma(-Ld[c][k], Ld[c][k], dsum);
-            if (!(dsum > T(0)) && !failed) {
-                failed = true;
-                fail_col = j0 + c;
-            }
-            const T ri = rsqrt_full(dsum);
-            Ld[c][c] = dsum * ri;
-            dinv[c] = ri;
-#pragma unroll
-            for (int r = c + 1; r < 8; r++) {
-                T v = sL[j0 + r][j0 + c];
-#pragma unroll
-                for (int k = 0; k < c; k++) v = fma(-Ld[r][k], Ld[c][k], v);
-                Ld[r][c] = v * ri;
-            }
-        }
-        // ---- B: row solves x = v Ld^{-T} for all 128 rows --------------------------------
+        const int jn = j0 + 8;
+        // ---- 1: pivot factor + row solves, one row per thread ------------------------------
         if (t < DB) {
-            const int row = t;
-            T v[8];
-            if (row >= j0 + 8 || row < j0) {
+            T Ld[8][8], dinv[8];
 #pragma unroll
-                for (int q = 0; q < 8; q++) v[q] = sL[row][j0 + q];  // L panel row / B row (upper)
-            } else {
+            for (int c = 0; c < 8; c++) {
+                T dsum = sV[c][j0 + c];
 #pragma unroll
-                for (int q = 0; q < 8; q++) v[q] = (row == j0 + q) ? T(1) : T(0);  // untouched identity row
+                for (int k = 0; k < c; k++) dsum = fma(-Ld[c][k], Ld[c][k], dsum);
+                if (!(dsum > T(0)) && fail_col < 0) fail_col = j0 + c;
+                const T ri = rsqrt_full(dsum);
+                Ld[c][c] = dsum * ri;
+                dinv[c] = ri;
+#pragma unroll
+                for (int r = c + 1; r < 8; r++) {
+                    T v = sV[c][j0 + r];
+#pragma unroll
+                    for (int k = 0; k < c; k++) v = fma(-Ld[r][k], Ld[c][k], v);
+                    Ld[r][c] = v * ri;
+                }
             }
+            const int row = t;
+            const bool piv = row >= j0 && row < jn;
             T x[8];
 #pragma unroll
             for (int q = 0; q < 8; q++) {
-                T w = v[q];
+                T v = piv ? ((row - j0 == q) ? T(1) : T(0)) : sV[q][row];
 #pragma unroll
-                for (int q2 = 0; q2 < q; q2++) w = fma(-x[q2], Ld[q][q2], w);
-                x[q] = w * dinv[q];
+                for (int q2 = 0; q2 < q; q2++) v = fma(-x[q2], Ld[q][q2], v);
+                x[q] = v * dinv[q];
             }
-            if (row >= j0 + 8) {
 #pragma unroll
-                for (int q = 0; q < 8; q++) sL[row][j0 + q] = x[q];
+            for (int q = 0; q < 8; q++) sP[q][row] = x[q];
+            if (t == 0) {
+#pragma unroll
+                for (int r = 0; r < 8; r++)
+#pragma unroll
+                    for (int c = 0; c <= r; c++) sLd[r][c] = Ld[r][c];
+            }
+        }
+        __syncthreads();
+        if (PROF) {
+            const long long tn = __builtin_amdgcn_s_memtime();
+            tph1 += tn - tmark;
+            tmark = tn;
+        }
+        // ---- 2: final values of column block J; rank-8 update of the trailing blocks -------
+        const bool pivrows = R0 >= j0 && R0 < jn;
+        if (cbi == (j0 >> 3)) {
+            if (pivrows) {
+#pragma unroll
+                for (int a = 0; a < 4; a++) {
+                    const int p = R0 + a - j0;
+#pragma unroll
+                    for (int q = 0; q < 8; q++) {
+                        const T xq = sP[q][R0 + a];
+                        S[a][q] = (q <= p) ? sLd[p][q] : xq;
+                        if (q == p) Bd[a] = xq;
+                    }
+                }
             } else {
 #pragma unroll
-                for (int q = 0; q < 8; q++) {
-                    const int c = j0 + q;
-                    if (c > row) sL[row][c] = x[q];
-                    else if (c == row) sDinv[row] = x[q];
-                }
+                for (int a = 0; a < 4; a++)
+#pragma unroll
+                    for (int q = 0; q < 8; q++) S[a][q] = sP[q][R0 + a];
             }
+        }
+        if (C0 >= jn && (R0 < jn || R0 + 3 >= C0)) {
+            if (pivrows) {  // identity rows entering B: still zero right of the pivot block
+#pragma unroll
+                for (int a = 0; a < 4; a++)
+#pragma unroll
+                    for (int b = 0; b < 8; b++) S[a][b] = T(0);
+            }
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                T u[4], v[8];
+#pragma unroll
+                for (int a = 0; a < 4; a++) u[a] = sP[q][R0 + a];
+#pragma unroll
+                for (int b = 0; b < 8; b++) v[b] = sP[q][C0 + b];
+#pragma unroll
+                for (int a = 0; a < 4; a++)
+#pragma unroll
+                    for (int b = 0; b < 8; b++) S[a][b] = fma(-u[a], v[b], S[a][b]);
+            }
+        }
+        if (jn < DB && cbi == (jn >> 3)) {  // publish the next column block
+#pragma unroll
+            for (int a = 0; a < 4; a++)
+#pragma unroll
+                for (int b = 0; b < 8; b++) sV[b][R0 + a] = S[a][b];
         }
         __syncthreads();
-        // ---- C: rank-8 update of the trailing A triangle and the B rows --------------------
-        if (t == 0) {  // the pivot block's L (nobody reads these positions during C)
-#pragma unroll
-            for (int r = 0; r < 8; r++)
-#pragma unroll
-                for (int c = 0; c <= r; c++) sL[j0 + r][j0 + c] = Ld[r][c];
+        if (PROF) {
+            const long long tn = __builtin_amdgcn_s_memtime();
+            tph2 += tn - tmark;
+            tmark = tn;
         }
-        const int jn = j0 + 8;
-#pragma unroll
-        for (int half = 0; half < 2; half++) {
-            const int blk = t + half * DT;
-            const int R0 = (blk >> 5) * 4, C0 = (blk & 31) * 4;
-            if (C0 < jn) continue;
-            const bool arow = R0 >= jn;
-            if (arow && R0 < C0) continue;  // strictly upper part of the trailing A block
-            T Lc[4][8], U[4][8];
-#pragma unroll
-            for (int b = 0; b < 4; b++)
-#pragma unroll
-                for (int q = 0; q < 8; q++) Lc[b][q] = sL[C0 + b][j0 + q];
-#pragma unroll
-            for (int a = 0; a < 4; a++) {
-                const int r = R0 + a;
-#pragma unroll
-                for (int q = 0; q < 8; q++) {
-                    const int c = j0 + q;
-                    U[a][q] = (arow || c > r) ? sL[r][c] : ((c == r) ? sDinv[r] : T(0));
-                }
-            }
-#pragma unroll
-            for (int a = 0; a < 4; a++) {
-#pragma unroll
-                for (int b = 0; b < 4; b++) {
-                    if (arow && R0 + a < C0 + b) continue;
-                    T acc = sL[R0 + a][C0 + b];
-#pragma unroll
-                    for (int q = 0; q < 8; q++) acc = fma(-U[a][q], Lc[b][q], acc);
-                    sL[R0 + a][C0 + b] = acc;
-                }
-            }
-        }
-        __syncthreads();
     }
-    if (t == 0 && failed) atomicMin(info, (int)(col0 + fail_col + 1));
+    if (fail_col >= 0 && t == 0) atomicMin(info, (int)(col0 + fail_col + 1));
 
-    {   // L (lower) and Linv = B^T (column-major, ld = DB, zeros above the diagonal) to global
+    // ---- stage the image (row-major, L lower / B strict upper) and Bd --------------------
+    T(*sI)[SIL] = reinterpret_cast<T(*)[SIL]>(smem_raw);
+    T* sBd = reinterpret_cast<T*>(smem_raw + sizeof(T) * DB * SIL);
+#pragma unroll
+    for (int a = 0; a < 4; a++) {
+#pragma unroll
+        for (int b = 0; b < 8; b++) sI[R0 + a][C0 + b] = S[a][b];
+        if (R0 + a >= C0 && R0 + a < C0 + 8) sBd[R0 + a] = Bd[a];
+    }
+    __syncthreads();
+    // L[r][c] (r >= c) and Linv[r][c] = B[c][r] (r > c), Bd (r == c), 0 (r < c), column-major
+    {
         const int r = t & (DB - 1);
         for (int c = t >> 7; c < DB; c += DT / DB) {
-            if (r >= c) A[r + (int64_t)c * ld] = sL[r][c];
-            const T v = (r > c) ? sL[c][r] : ((r == c) ? sDinv[c] : T(0));
-            Linv[r + c * DB] = v;
+            if (r >= c) A[r + (int64_t)c * ld] = sI[r][c];
+            Linv[r + c * DB] = (r > c) ? sI[c][r] : ((r == c) ? sBd[r] : T(0));
         }
+    }
+    if (PROF) __syncthreads();
+    if (PROF && t == 0) {
+        const long long te = __builtin_amdgcn_s_memtime();
+        prof[0] += tp1 - tp0;
+        prof[1] += tph1;
+        prof[2] += tph2;
+        prof[3] += te - tmark;
+        prof[4] += te - tp0;
     }
 }
 
@@ -416,20 +459,17 @@ void launch_gemm_nt_kskip(T* C, int64_t ldc, const T* A, int64_t lda, const T* B
 }
 
 template <typename T>
-static size_t diag_lds_bytes() {
-    return sizeof(T) * (DB * LS + DB);
-}
-
-template <typename T>
 static void launch_diag(T* Akk, int64_t ld, T* Lk, int* info, int64_t col0, hipStream_t s) {
     static bool attr_done = false;
-    const size_t lds = diag_lds_bytes<T>();
     if (!attr_done) {
-        hipFuncSetAttribute((const void*)diag_potrf_kernel<T>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipFuncSetAttribute((const void*)diag_potrf_kernel<T, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)diag_lds_bytes<T>());
+        hipFuncSetAttribute((const void*)diag_potrf_kernel<T, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)diag_lds_bytes<T>());
         attr_done = true;
     }
     ProfScope ps(KC_DIAG, s, 2.0 * DB * DB * DB / 3.0, 0.0);
-    hipLaunchKernelGGL(diag_potrf_kernel<T>, dim3(1), dim3(DT), lds, s, Akk, ld, Lk, info, col0);
+    hipLaunchKernelGGL((diag_potrf_kernel<T, false>), dim3(1), dim3(DT), diag_lds_bytes<T>(), s, Akk, ld, Lk, info, col0);
 }
 
 template <typename T>
@@ -437,6 +477,16 @@ void launch_diag_public(T* Akk, int64_t ld, T* Lk, int* info, int64_t col0, hipS
     (void)ph;
     launch_diag<T>(Akk, ld, Lk, info, col0, s);
 }
+// in-kernel phase timing (s_memtime ticks, accumulated): load, solve phases, update
+// phases, store, total
+template <typename T>
+void launch_diag_prof(T* Akk, int64_t ld, T* Lk, int* info, long long* prof, hipStream_t s) {
+    launch_diag<T>(Akk, ld, Lk, info, 0, nullptr);  // attributes (one warm launch on the null stream)
+    hipLaunchKernelGGL((diag_potrf_kernel<T, true>), dim3(1), dim3(DT), diag_lds_bytes<T>(), s, Akk, ld, Lk, info,
+                       (int64_t)0, prof);
+}
+template void launch_diag_prof<double>(double*, int64_t, double*, int*, long long*, hipStream_t);
+template void launch_diag_prof<float>(float*, int64_t, float*, int*, long long*, hipStream_t);
 template void launch_diag_public<double>(double*, int64_t, double*, int*, int64_t, hipStream_t, int);
 template void launch_diag_public<float>(float*, int64_t, float*, int*, int64_t, hipStream_t, int);
 

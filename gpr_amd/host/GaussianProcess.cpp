@@ -120,6 +120,17 @@ void GaussianProcess<T>::FitDevice(gprx_fit_info* info) {
     m_DeviceFactor = true;
 }
 
+// The factor for operator()/core matrix.  A GP whose regression vectors are fixed (loaded
+// by Load, or computed by Initialize) keeps predicting with them, as the reference does:
+// the refit's alpha is replaced by m_RegressionVectors.
+template <class T>
+void GaussianProcess<T>::EnsureFactor() {
+    if (m_DeviceFactor) return;
+    FitDevice();
+    if (m_Initialized && m_RegressionVectors.rows() == m_SampleVectors.size())
+        ThrowIfFailed(gprx_model_set_alpha(m_Model, m_RegressionVectors.data()), DefaultContext());
+}
+
 // lib/GaussianProcess.cpp:118-130, 642-672
 template <class T>
 void GaussianProcess<T>::Initialize() {
@@ -143,7 +154,7 @@ template <class T>
 const typename GaussianProcess<T>::MatrixType& GaussianProcess<T>::GetCoreMatrix() {
     Initialize();
     if (!m_CoreValid) {
-        if (!m_DeviceFactor) FitDevice();
+        EnsureFactor();
         const std::size_t n = m_SampleVectors.size();
         m_CoreMatrix.resize(n, n);
         ThrowIfFailed(gprx_model_core_matrix(m_Model, m_CoreMatrix.data()), DefaultContext());
@@ -189,7 +200,7 @@ T GaussianProcess<T>::operator()(const VectorType& x, const VectorType& y) {
     Initialize();
     CheckInputDimension(x, "GaussianProcess::(): ");
     CheckInputDimension(y, "GaussianProcess::(): ");
-    if (!m_DeviceFactor) FitDevice();
+    EnsureFactor();
     m_CoreSize = m_SampleVectors.size();  // :95-97 builds the core matrix on demand
     T out = 0;
     ThrowIfFailed(gprx_model_posterior_cov(m_Model, x.data(), y.data(), 1, &out), DefaultContext());
@@ -210,7 +221,7 @@ T GaussianProcess<T>::GetCredibleInterval(const VectorType& x) {
 template <class T>
 std::vector<T> GaussianProcess<T>::CredibleIntervalBatch(const MatrixType& Xq) {
     Initialize();
-    if (!m_DeviceFactor) FitDevice();
+    EnsureFactor();
     std::vector<T> c(Xq.rows());
     ThrowIfFailed(gprx_model_posterior_cov(m_Model, Xq.data(), Xq.data(), (int64_t)Xq.rows(), c.data()),
                   DefaultContext());

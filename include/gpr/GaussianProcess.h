@@ -127,6 +127,7 @@ protected:
     gprx_model* Model();
     void UploadState();            // samples, kernel, noise -> device
     void FitDevice(gprx_fit_info* info = nullptr);
+    void EnsureFactor();           // factor for operator()/core; keeps the regression vectors
 
     friend class Likelihood<TScalarType>;
 };

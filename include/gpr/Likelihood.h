@@ -66,6 +66,10 @@ protected:
                       DefaultContext());
         gp->m_DeviceFactor = true;
         gp->m_CoreValid = false;
+        // the likelihood does not change the gp's regression vectors (the reference only
+        // reads its core matrix): keep predicting with them
+        if (gp->m_Initialized && gp->m_RegressionVectors.rows() == gp->m_SampleVectors.size())
+            ThrowIfFailed(gprx_model_set_alpha(gp->m_Model, gp->m_RegressionVectors.data()), DefaultContext());
         e.grad.resize(np);
         return e;
     }

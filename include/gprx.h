@@ -155,8 +155,9 @@ gprx_status gprx_model_fit(gprx_model* model, uint32_t flags, gprx_fit_info* inf
 gprx_status gprx_model_get_alpha(gprx_model* model, void* alpha);
 /* Install regression vectors (n x m, row-major) read back by GaussianProcess::Load
  * (lib/GaussianProcess.cpp:184-268, which restores m_RegressionVectors from file rather
- * than recomputing them).  Enables predict; the factor needed by posterior_cov / lml /
- * core_matrix is rebuilt by the next gprx_model_fit. */
+ * than recomputing them).  Enables predict.  The factor needed by posterior_cov / lml /
+ * core_matrix is untouched: after set_data/kernel/noise it is rebuilt by gprx_model_fit,
+ * which also overwrites alpha (re-install it afterwards to keep the loaded vectors). */
 gprx_status gprx_model_set_alpha(gprx_model* model, const void* alpha);
 /* Predict / PredictDerivative for q queries (lib/GaussianProcess.cpp:54-81, 684-706):
  * mean is q x m; deriv (optional, may be NULL) is q x d x m with the reference's formula

@@ -11,7 +11,9 @@ extern "C" {
 #endif
 /* what: 0 = diagonal 128-block factor+inverse, 1 = gemm_nt (C -= A B^T), 2 = lower gemm_nt,
  *       3 = full potrf of an n x n SPD matrix (single stream), 4 = potrf with look-ahead,
- *       5 = back substitution (m = 1) of an n x n factor.
+ *       5 = back substitution (m = 1) of an n x n factor,
+ *       6 = diagonal kernel phase profile: ms must hold 5 doubles, receiving the mean
+ *           s_memtime ticks per launch of (load, solve phases, update phases, store, total).
  * For 1/2: (M, N, K) are the gemm sizes; for 3/4/5: M = n.  Returns the mean device time
  * per call over `iters` calls (HIP events) in *ms. */
 gprx_status gprx_dev_bench(gprx_ctx* ctx, gprx_dtype dtype, int32_t what, int64_t M, int64_t N, int64_t K,

@@ -26,6 +26,14 @@ if cases in ("all", "diag"):
         ms = run(dt, 0, 128, iters=50)
         res[f"diag128_{'f64' if dt else 'f32'}_us"] = ms * 1e3
 
+if cases in ("all", "diag", "diagprof"):
+    for dt in (F64, F32):
+        arr = (ctypes.c_double * 5)()
+        st = L.gprx_dev_bench(ctx.h, dt, 6, 128, 0, 0, 20, ctypes.cast(arr, ctypes.POINTER(ctypes.c_double)))
+        if st:
+            raise RuntimeError(L.gprx_last_error(ctx.h).decode())
+        res[f"diagprof_{'f64' if dt else 'f32'}_ticks"] = dict(zip(["load", "solve", "update", "store", "total"], list(arr)))
+
 if cases in ("all", "gemm"):
     for (M, N, K, low) in [(16384, 16384, 256, 1), (16384, 16384, 512, 1), (8192, 8192, 256, 1), (16384, 128, 128, 0),
                            (16384, 256, 256, 0), (8192, 8192, 1024, 0), (4096, 4096, 4096, 0)]:
