@@ -650,8 +650,8 @@ gprx_status gprx_ctx_create(int device, gprx_ctx** out) {
     GPRX_HIP(hipStreamCreateWithPriority(&ctx->stream, hipStreamNonBlocking, prio_hi));
     // The aux stream (bulk trailing updates) is kept off a few CUs so the panel chain's
     // one-workgroup diagonal kernels never queue behind a full-chip GEMM: GPRX_RESERVE_CU
-    // CUs (default 8, one per XCD when CUs are numbered XCD-major) are excluded from its mask.
-    int reserve = 8;
+    // CUs (default 0 = off: measured no gain; 8 = one per XCD when CUs are numbered XCD-major) are excluded from its mask.
+    int reserve = 0;
     if (const char* e = std::getenv("GPRX_RESERVE_CU")) reserve = std::atoi(e);
     hipDeviceProp_t prop;
     GPRX_HIP(hipGetDeviceProperties(&prop, device));

@@ -24,35 +24,28 @@
 namespace gprx {
 
 // ======================================================================================
-// Diagonal block: factor + inverse, one workgroup of 512 threads.
+// Diagonal block: factor + inverse, one workgroup of 256 threads.
 //
 // The 128x128 block lives in REGISTERS as a square image S: the lower triangle holds A
 // (becoming L), the strict upper triangle the rows of B = L^{-T} (its diagonal in Bd).  B
 // comes from appending the identity below A: its rows ride along the elimination and end as
 // I L^{-T}; being upper triangular they fit the unused half exactly.  Thread t owns a fixed
-// 4-row x 8-column block: wave w holds column blocks 2w, 2w+1 (lane>>5), row block lane&31.
-// Right-looking over 8-column steps J = [j0, j0+8):
+// 4-row x 16-column block (two 8-column blocks): wave w holds columns 32w.., lane>>5 picks
+// the 16-column half, lane&31 the row block.  Right-looking over 8-column steps J:
 //   1  128 threads (waves 0-1, one row each) factor the 8x8 pivot redundantly (rsq +
 //      Newton, no divide) and solve their row x = v Ld^{-T} (A rows below J: L panel; B rows
 //      above J; pivot rows: identity rows), reading v from the LDS column panel sV that the
 //      owners of J published, writing x to sP (and Ld to sLd);
-//   2  every thread with trailing columns applies S -= x_r x_c^T to its block, unmasked:
-//      entries right of the diagonal in rows not yet reached are scratch and are zeroed when
-//      their rows become pivot rows (their identity rows are still zero there).  The owners
-//      of J take their final values from sP/sLd; the owners of the next column block
-//      publish it in sV.
-// Two barriers per step.  The result is staged through LDS so L and Linv = B^T leave in
-// coalesced column-major stores.  All register arrays use compile-time indices.
+//   2  every thread with trailing columns applies S -= x_r x_c^T to them, unmasked: entries
+//      right of the diagonal in rows not yet reached are scratch and are zeroed when their
+//      rows become pivot rows (their identity rows are still zero there).  The owners of J
+//      take their final values from sP/sLd; the owners of the next column block publish it.
+// Two barriers per step, 17 KB of LDS and <= 256 VGPRs, so the kernel fits on a CU next to
+// one trailing-update GEMM workgroup (it runs concurrently with them on the panel stream).
+// All register arrays use compile-time indices.
 // ======================================================================================
-constexpr int DT = 512;      // threads of the diagonal kernel
+constexpr int DT = 256;      // threads of the diagonal kernel
 constexpr int SPL = DB + 4;  // panel row stride (elements)
-constexpr int SIL = DB + 2;  // output staging image row stride (elements)
-
-template <typename T>
-constexpr size_t diag_lds_bytes() {
-    return sizeof(T) * ((size_t)DB * SIL + DB) > sizeof(T) * (2 * 8 * SPL + 64) ? sizeof(T) * ((size_t)DB * SIL + DB)
-                                                                             : sizeof(T) * (2 * 8 * SPL + 64);
-}
 
 // 1/sqrt(x) to full precision: hardware estimate + Newton steps (no divide on the chain)
 __device__ __forceinline__ double rsqrt_full(double x) {
@@ -70,30 +63,33 @@ __device__ __forceinline__ float rsqrt_full(float x) {
 }
 
 template <typename T, bool PROF = false>
-__global__ __launch_bounds__(DT) void diag_potrf_kernel(T* __restrict__ A, int64_t ld, T* __restrict__ Linv,
-                                                        int* __restrict__ info, int64_t col0,
-                                                        long long* __restrict__ prof = nullptr) {
+__global__ __launch_bounds__(DT) __attribute__((amdgpu_num_vgpr(296))) void diag_potrf_kernel(
+    T* __restrict__ A, int64_t ld, T* __restrict__ Linv, int* __restrict__ info, int64_t col0,
+    long long* __restrict__ prof = nullptr) {
     long long tp0 = 0, tp1 = 0, tph1 = 0, tph2 = 0, tmark = 0;
     if (PROF) tp0 = __builtin_amdgcn_s_memtime();
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    T(*sV)[SPL] = reinterpret_cast<T(*)[SPL]>(smem_raw);              // v of column block J
-    T(*sP)[SPL] = reinterpret_cast<T(*)[SPL]>(smem_raw + sizeof(T) * 8 * SPL);  // solved x
-    T(*sLd)[8] = reinterpret_cast<T(*)[8]>(smem_raw + sizeof(T) * 16 * SPL);   // pivot factor
+    __shared__ __attribute__((aligned(16))) T sV[8][SPL];  // v of column block J (column-major)
+    __shared__ __attribute__((aligned(16))) T sP[8][SPL];  // solved x
+    __shared__ T sLdW[2][8][9];                             // pivot factor (+ 1/diag), per wave
+    T(*sLd)[9] = sLdW[0];
 
     const int t = threadIdx.x, w = t >> 6, l = t & 63;
     const int R0 = (l & 31) * 4;
-    const int cbi = 2 * w + (l >> 5);  // column block index (8 columns)
-    const int C0 = cbi * 8;
+    const int C0 = 32 * w + 16 * (l >> 5);  // first of 16 columns
+    const int cb0 = C0 >> 3;                 // its first 8-column block
 
-    T S[4][8];
+    T S[4][16];
     T Bd[4];
+    {
+        const T* Ai = A + R0 + (int64_t)C0 * ld;
 #pragma unroll
-    for (int b = 0; b < 8; b++)
+        for (int b = 0; b < 16; b++)
 #pragma unroll
-        for (int a = 0; a < 4; a++) S[a][b] = A[R0 + a + (int64_t)(C0 + b) * ld];
+            for (int a = 0; a < 4; a++) S[a][b] = Ai[a + (int64_t)b * ld];
+    }
 #pragma unroll
     for (int a = 0; a < 4; a++) Bd[a] = T(1);
-    if (cbi == 0) {
+    if (cb0 == 0) {
 #pragma unroll
         for (int a = 0; a < 4; a++)
 #pragma unroll
@@ -104,25 +100,33 @@ __global__ __launch_bounds__(DT) void diag_potrf_kernel(T* __restrict__ A, int64
 
     int fail_col = -1;
     for (int j0 = 0; j0 < DB; j0 += 8) {
-        const int jn = j0 + 8;
+        const int jn = j0 + 8, J = j0 >> 3;
         // ---- 1: pivot factor + row solves, one row per thread ------------------------------
         if (t < DB) {
-            T Ld[8][8], dinv[8];
+            // every lane of waves 0-1 factors the pivot and keeps it in its wave's own LDS copy
+            // (identical values, no cross-wave sync), so the row solve reads it back instead
+            // of holding it in registers next to S
+            T(*myLd)[9] = sLdW[w];
+            {
+                T Ld[8][8];
 #pragma unroll
-            for (int c = 0; c < 8; c++) {
-                T dsum = sV[c][j0 + c];
+                for (int c = 0; c < 8; c++) {
+                    T dsum = sV[c][j0 + c];
 #pragma unroll
-                for (int k = 0; k < c; k++) dsum = fma(-Ld[c][k], Ld[c][k], dsum);
-                if (!(dsum > T(0)) && fail_col < 0) fail_col = j0 + c;
-                const T ri = rsqrt_full(dsum);
-                Ld[c][c] = dsum * ri;
-                dinv[c] = ri;
+                    for (int k = 0; k < c; k++) dsum = fma(-Ld[c][k], Ld[c][k], dsum);
+                    if (!(dsum > T(0)) && fail_col < 0) fail_col = j0 + c;
+                    const T ri = rsqrt_full(dsum);
+                    Ld[c][c] = dsum * ri;
+                    myLd[c][8] = ri;
+                    myLd[c][c] = Ld[c][c];
 #pragma unroll
-                for (int r = c + 1; r < 8; r++) {
-                    T v = sV[c][j0 + r];
+                    for (int r = c + 1; r < 8; r++) {
+                        T v = sV[c][j0 + r];
 #pragma unroll
-                    for (int k = 0; k < c; k++) v = fma(-Ld[r][k], Ld[c][k], v);
-                    Ld[r][c] = v * ri;
+                        for (int k = 0; k < c; k++) v = fma(-Ld[r][k], Ld[c][k], v);
+                        Ld[r][c] = v * ri;
+                        myLd[r][c] = Ld[r][c];
+                    }
                 }
             }
             const int row = t;
@@ -132,17 +136,11 @@ __global__ __launch_bounds__(DT) void diag_potrf_kernel(T* __restrict__ A, int64
             for (int q = 0; q < 8; q++) {
                 T v = piv ? ((row - j0 == q) ? T(1) : T(0)) : sV[q][row];
 #pragma unroll
-                for (int q2 = 0; q2 < q; q2++) v = fma(-x[q2], Ld[q][q2], v);
-                x[q] = v * dinv[q];
+                for (int q2 = 0; q2 < q; q2++) v = fma(-x[q2], myLd[q][q2], v);
+                x[q] = v * myLd[q][8];
             }
 #pragma unroll
             for (int q = 0; q < 8; q++) sP[q][row] = x[q];
-            if (t == 0) {
-#pragma unroll
-                for (int r = 0; r < 8; r++)
-#pragma unroll
-                    for (int c = 0; c <= r; c++) sLd[r][c] = Ld[r][c];
-            }
         }
         __syncthreads();
         if (PROF) {
@@ -152,50 +150,64 @@ __global__ __launch_bounds__(DT) void diag_potrf_kernel(T* __restrict__ A, int64
         }
         // ---- 2: final values of column block J; rank-8 update of the trailing blocks -------
         const bool pivrows = R0 >= j0 && R0 < jn;
-        if (cbi == (j0 >> 3)) {
-            if (pivrows) {
+        bool act[2];
 #pragma unroll
-                for (int a = 0; a < 4; a++) {
-                    const int p = R0 + a - j0;
+        for (int h = 0; h < 2; h++) {
+            const int cb = cb0 + h, c0h = 8 * cb;
+            act[h] = c0h >= jn && (R0 < jn || R0 + 3 >= c0h);
+            if (cb == J) {
+                if (pivrows) {
 #pragma unroll
-                    for (int q = 0; q < 8; q++) {
-                        const T xq = sP[q][R0 + a];
-                        S[a][q] = (q <= p) ? sLd[p][q] : xq;
-                        if (q == p) Bd[a] = xq;
+                    for (int a = 0; a < 4; a++) {
+                        const int p = R0 + a - j0;
+#pragma unroll
+                        for (int q = 0; q < 8; q++) {
+                            const T xq = sP[q][R0 + a];
+                            S[a][8 * h + q] = (q <= p) ? sLd[p][q] : xq;
+                            if (q == p) Bd[a] = xq;
+                        }
                     }
+                } else {
+#pragma unroll
+                    for (int a = 0; a < 4; a++)
+#pragma unroll
+                        for (int q = 0; q < 8; q++) S[a][8 * h + q] = sP[q][R0 + a];
                 }
-            } else {
+            }
+            if (act[h] && pivrows) {  // identity rows entering B: still zero right of the pivot
 #pragma unroll
                 for (int a = 0; a < 4; a++)
 #pragma unroll
-                    for (int q = 0; q < 8; q++) S[a][q] = sP[q][R0 + a];
+                    for (int b = 0; b < 8; b++) S[a][8 * h + b] = T(0);
             }
         }
-        if (C0 >= jn && (R0 < jn || R0 + 3 >= C0)) {
-            if (pivrows) {  // identity rows entering B: still zero right of the pivot block
-#pragma unroll
-                for (int a = 0; a < 4; a++)
-#pragma unroll
-                    for (int b = 0; b < 8; b++) S[a][b] = T(0);
-            }
-#pragma unroll
+        if (act[0] || act[1]) {
+#pragma unroll 2
             for (int q = 0; q < 8; q++) {
-                T u[4], v[8];
+                T u[4];
 #pragma unroll
                 for (int a = 0; a < 4; a++) u[a] = sP[q][R0 + a];
 #pragma unroll
-                for (int b = 0; b < 8; b++) v[b] = sP[q][C0 + b];
+                for (int h = 0; h < 2; h++) {
+                    if (!act[h]) continue;
+                    T v[8];
+#pragma unroll
+                    for (int b = 0; b < 8; b++) v[b] = sP[q][C0 + 8 * h + b];
+#pragma unroll
+                    for (int a = 0; a < 4; a++)
+#pragma unroll
+                        for (int b = 0; b < 8; b++) S[a][8 * h + b] = fma(-u[a], v[b], S[a][8 * h + b]);
+                }
+            }
+        }
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            if (jn < DB && cb0 + h == (jn >> 3)) {  // publish the next column block
 #pragma unroll
                 for (int a = 0; a < 4; a++)
 #pragma unroll
-                    for (int b = 0; b < 8; b++) S[a][b] = fma(-u[a], v[b], S[a][b]);
+                    for (int b = 0; b < 8; b++) sV[b][R0 + a] = S[a][8 * h + b];
             }
-        }
-        if (jn < DB && cbi == (jn >> 3)) {  // publish the next column block
-#pragma unroll
-            for (int a = 0; a < 4; a++)
-#pragma unroll
-                for (int b = 0; b < 8; b++) sV[b][R0 + a] = S[a][b];
         }
         __syncthreads();
         if (PROF) {
@@ -206,22 +218,28 @@ __global__ __launch_bounds__(DT) void diag_potrf_kernel(T* __restrict__ A, int64
     }
     if (fail_col >= 0 && t == 0) atomicMin(info, (int)(col0 + fail_col + 1));
 
-    // ---- stage the image (row-major, L lower / B strict upper) and Bd --------------------
-    T(*sI)[SIL] = reinterpret_cast<T(*)[SIL]>(smem_raw);
-    T* sBd = reinterpret_cast<T*>(smem_raw + sizeof(T) * DB * SIL);
+    // L (lower) in place; Linv = B^T: row r of B goes to column r of Linv (zeros above its
+    // diagonal), 16 consecutive elements per thread and row.  The opaque copies keep the
+    // compiler from hoisting these addresses above the loop (they would pin ~40 registers).
+    int64_t ldo = ld;
+    T* Ao = A;
+    T* Lo = Linv;
+    int R0o = R0, C0o = C0;
+    asm volatile("" : "+s"(ldo), "+s"(Ao), "+s"(Lo), "+v"(R0o), "+v"(C0o));
+#pragma unroll
+    for (int b = 0; b < 16; b++) {
+        const int c = C0o + b;
+#pragma unroll
+        for (int a = 0; a < 4; a++)
+            if (R0o + a >= c) Ao[R0o + a + (int64_t)c * ldo] = S[a][b];
+    }
 #pragma unroll
     for (int a = 0; a < 4; a++) {
+        const int r = R0o + a;
 #pragma unroll
-        for (int b = 0; b < 8; b++) sI[R0 + a][C0 + b] = S[a][b];
-        if (R0 + a >= C0 && R0 + a < C0 + 8) sBd[R0 + a] = Bd[a];
-    }
-    __syncthreads();
-    // L[r][c] (r >= c) and Linv[r][c] = B[c][r] (r > c), Bd (r == c), 0 (r < c), column-major
-    {
-        const int r = t & (DB - 1);
-        for (int c = t >> 7; c < DB; c += DT / DB) {
-            if (r >= c) A[r + (int64_t)c * ld] = sI[r][c];
-            Linv[r + c * DB] = (r > c) ? sI[c][r] : ((r == c) ? sBd[r] : T(0));
+        for (int b = 0; b < 16; b++) {
+            const int c = C0o + b;
+            Lo[c + r * DB] = (r < c) ? S[a][b] : ((r == c) ? Bd[a] : T(0));
         }
     }
     if (PROF) __syncthreads();
@@ -460,16 +478,8 @@ void launch_gemm_nt_kskip(T* C, int64_t ldc, const T* A, int64_t lda, const T* B
 
 template <typename T>
 static void launch_diag(T* Akk, int64_t ld, T* Lk, int* info, int64_t col0, hipStream_t s) {
-    static bool attr_done = false;
-    if (!attr_done) {
-        hipFuncSetAttribute((const void*)diag_potrf_kernel<T, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)diag_lds_bytes<T>());
-        hipFuncSetAttribute((const void*)diag_potrf_kernel<T, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)diag_lds_bytes<T>());
-        attr_done = true;
-    }
     ProfScope ps(KC_DIAG, s, 2.0 * DB * DB * DB / 3.0, 0.0);
-    hipLaunchKernelGGL((diag_potrf_kernel<T, false>), dim3(1), dim3(DT), diag_lds_bytes<T>(), s, Akk, ld, Lk, info, col0);
+    hipLaunchKernelGGL((diag_potrf_kernel<T, false>), dim3(1), dim3(DT), 0, s, Akk, ld, Lk, info, col0);
 }
 
 template <typename T>
@@ -481,9 +491,7 @@ void launch_diag_public(T* Akk, int64_t ld, T* Lk, int* info, int64_t col0, hipS
 // phases, store, total
 template <typename T>
 void launch_diag_prof(T* Akk, int64_t ld, T* Lk, int* info, long long* prof, hipStream_t s) {
-    launch_diag<T>(Akk, ld, Lk, info, 0, nullptr);  // attributes (one warm launch on the null stream)
-    hipLaunchKernelGGL((diag_potrf_kernel<T, true>), dim3(1), dim3(DT), diag_lds_bytes<T>(), s, Akk, ld, Lk, info,
-                       (int64_t)0, prof);
+    hipLaunchKernelGGL((diag_potrf_kernel<T, true>), dim3(1), dim3(DT), 0, s, Akk, ld, Lk, info, (int64_t)0, prof);
 }
 template void launch_diag_prof<double>(double*, int64_t, double*, int*, long long*, hipStream_t);
 template void launch_diag_prof<float>(float*, int64_t, float*, int*, long long*, hipStream_t);
@@ -523,13 +531,19 @@ template <typename T>
 void potrf_blocked(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info, Exec& ex) {
     const int64_t NBO = outer_block();
     hipStream_t P = ex.s0, B = ex.s1 ? ex.s1 : ex.s0;
+    // timing experiments only (results are wrong): 1 = no TrailRest, 2 = no diagonal kernel,
+    // 4 = no panel trsm / inner update
+    static const int skip = [] {
+        const char* e = std::getenv("GPRX_DEBUG_SKIP");
+        return e ? std::atoi(e) : 0;
+    }();
     const int64_t nK = (np + NBO - 1) / NBO;
     auto panel = [&](int64_t c0, int64_t w) {
         for (int64_t kk = c0; kk < c0 + w; kk += DB) {
             T* Lk = Linv + (kk / DB) * (int64_t)DB * DB;
-            launch_diag<T>(A + kk + kk * ld, ld, Lk, info, kk, P);
+            if (!(skip & 2)) launch_diag<T>(A + kk + kk * ld, ld, Lk, info, kk, P);
             const int64_t rows_below = nrows - (kk + DB);
-            if (rows_below <= 0) continue;
+            if (rows_below <= 0 || (skip & 4)) continue;
             T* Pk = A + (kk + DB) + kk * ld;
             launch_gemm_nt<T>(Pk, ld, Pk, ld, Lk, DB, rows_below, DB, DB, T(1), T(0), false, P);
             const int64_t inner = c0 + w - (kk + DB);
@@ -554,7 +568,7 @@ void potrf_blocked(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* in
         // TrailRest(K)
         const int64_t c2 = c1 + wn;
         if (B != P) GPRX_HIP(hipStreamWaitEvent(B, ex.event(2 * K), 0));
-        if (c2 < np)
+        if (c2 < np && !(skip & 1))
             launch_gemm_nt<T>(A + c2 + c2 * ld, ld, Pan + c2, ld, Pan + c2, ld, nrows - c2, np - c2, w, T(-1), T(1),
                               true, B);
         if (B != P) GPRX_HIP(hipEventRecord(ex.event(2 * K + 1), B));
