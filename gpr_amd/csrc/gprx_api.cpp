@@ -1,6 +1,7 @@
 // gprx_api.cpp — the C ABI of libgprx (include/gprx.h): contexts, resident models and the
 // host-side orchestration of the HIP kernels.  No entry point throws across the ABI.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <climits>
@@ -31,6 +32,10 @@ void launch_lml_grad(const KCanon<T>& K, const T* X, const T* tab, int64_t n, in
                      int64_t ldc, double* acc /* MAX_LEAF*3 */, hipStream_t s);
 template <typename T>
 void launch_set_identity_pad(T* A, int64_t ld, int64_t n, int64_t np, hipStream_t s);
+template <typename T>
+void launch_gemm_add_lower(T* S, int64_t lds, const T* K, int64_t ldk, int64_t n, hipStream_t s);
+template <typename T>
+void launch_sum_partials(T* S, int64_t stride, int P, hipStream_t s);
 
 gprx_status gprx_dev_bench_impl(gprx_dtype dtype, int32_t what, int64_t M, int64_t N, int64_t K, int32_t iters,
                                 double* ms, Exec* ex);
@@ -189,6 +194,7 @@ using namespace gprx;
 struct gprx_ctx {
     int device = 0;
     int rank = 0, world = 1;
+    ncclComm_t comm = nullptr;  // RCCL communicator (gprx_ctx_create_dist), world > 1
     hipStream_t stream = nullptr;
     hipStream_t aux = nullptr;  // look-ahead stream of the factorisation
     Exec ex;
@@ -616,6 +622,152 @@ static gprx_status cholesky_impl(gprx_ctx* ctx, void* Ahost, int64_t n, int32_t*
 }
 
 // ---------------------------------------------------------------------------------------
+// sparse GP (subset of regressors), SparseGaussianProcess::PreComputeRegression
+// (include/SparseGaussianProcess.h:274-313):
+//   K   = Kmm + jitter I                              (M x M)
+//   S   = K + sigma^-2 Knm^T Knm,   b = sigma^-2 Knm^T Y
+//   RV  = S^{-1} b          (the reference's Kinv (sigma^-2 K Sigma Knm^T Y), Kinv K = I)
+//   RM  = S^{-1} = Sigma    (the reference's Kinv (K Sigma K) Kinv)
+//   Kinv = K^{-1}
+// Knm is streamed in chunks of dense rows: each chunk is built as the (M + labels) x Nc
+// block [Kmn_c ; Y_c^T] and folded into the lower triangle of the augmented S with one
+// MFMA gemm (A A^T), so b rides along as extra rows, exactly like Y in the dense fit.  With
+// an RCCL context the dense rows are sharded over ranks (each rank passes its own rows) and
+// the accumulated (M + labels) x M block is all-reduced -- the one exchange of the path.
+// ---------------------------------------------------------------------------------------
+template <typename T>
+static ncclDataType_t nccl_type();
+template <>
+ncclDataType_t nccl_type<double>() {
+    return ncclFloat64;
+}
+template <>
+ncclDataType_t nccl_type<float>() {
+    return ncclFloat32;
+}
+
+template <typename T>
+static void download_sym(void* out, const DevBuf& C, int64_t ldc, int64_t n, hipStream_t s) {
+    std::vector<T> h((size_t)n * n);
+    GPRX_HIP(hipStreamSynchronize(s));
+    GPRX_HIP(hipGetLastError());
+    GPRX_HIP(hipMemcpy2D(h.data(), sizeof(T) * n, C.p, sizeof(T) * ldc, sizeof(T) * n, n, hipMemcpyDeviceToHost));
+    T* o = reinterpret_cast<T*>(out);
+    for (int64_t j = 0; j < n; j++)
+        for (int64_t i = j; i < n; i++) {
+            const T v = h[(size_t)j * n + i];
+            o[(size_t)i * n + j] = v;
+            o[(size_t)j * n + i] = v;
+        }
+}
+
+template <typename T>
+static gprx_status sparse_fit_impl(gprx_ctx* ctx, const gprx_kernel_desc* desc, const void* Xh, const void* Yh,
+                                   int64_t n, int d, int m, const void* Xmh, int64_t M, double sigma, double jitter,
+                                   void* Kinv, void* RV, void* RM) {
+    KCanon<T> K{};
+    const std::string e = canonicalize<T>(*desc, K);
+    GPRX_REQUIRE(e.empty(), GPRX_ERR_ARG, e);
+    GPRX_REQUIRE(M > 0 && d > 0 && m > 0 && n >= 0, GPRX_ERR_DIM, "gprx_sparse_fit: bad dimensions");
+    GPRX_REQUIRE(sigma > 0, GPRX_ERR_ARG, "SparseGaussianProcess::ComputeCoreMatrices: sigma must be positive.");
+    GPRX_HIP(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    const int64_t Mp = round_up(M, DB), mp = round_up(m, GT), ld = Mp + mp;
+    int64_t cmax = 32768;  // dense rows per streamed block (GPRX_SPARSE_CHUNK overrides, for tests)
+    if (const char* ev = std::getenv("GPRX_SPARSE_CHUNK")) cmax = std::max<int64_t>(64, round_up(std::atoll(ev), 64));
+    const int64_t chunk = std::max<int64_t>(BT, std::min<int64_t>(round_up(std::max<int64_t>(n, 1), 64), cmax));
+    DevBuf dXm, dtm, dX, dtx, dY, dS, dA, dK, dLinv, dLinvK, dinfo, dflag, dz, dalpha, dV, dC;
+    upload<T>(dXm, Xmh, sizeof(T) * M * d, s);
+    upload<T>(dX, Xh, sizeof(T) * std::max<int64_t>(n, 1) * d, s);
+    upload<T>(dY, Yh, sizeof(T) * std::max<int64_t>(n, 1) * m, s);
+    if (K.nper > 0) {
+        dtm.ensure(sizeof(T) * 2 * K.nper * M * d);
+        launch_sincos_tables<T>(K, dXm.as<T>(), M, d, dtm.as<T>(), s);
+        dtx.ensure(sizeof(T) * 2 * K.nper * chunk * d);  // per-chunk tables of the dense rows
+    }
+    dflag.ensure(sizeof(int));
+    dinfo.ensure(sizeof(int));
+    GPRX_HIP(hipMemsetAsync(dflag.p, 0, sizeof(int), s));
+    // ---- accumulate sigma^-2 [Kmn ; Y^T][Kmn ; Y^T]^T over the dense rows (lower part) ----
+    // split-K partials: enough (tiles x partials) workgroups to fill the chip
+    const int64_t ntiles = (Mp / GT) * (Mp / GT + 1) / 2 + (mp / GT) * (Mp / GT);
+    const int P = (int)std::max<int64_t>(1, std::min<int64_t>(8, (1024 + ntiles - 1) / ntiles));
+    const int64_t sstride = ld * Mp;
+    dS.ensure(sizeof(T) * sstride * P);
+    GPRX_HIP(hipMemsetAsync(dS.p, 0, sizeof(T) * sstride * P, s));
+    const int64_t acols = chunk + 16 * 8;  // slack: the last split-K slice may overhang ncp (zeros)
+    dA.ensure(sizeof(T) * ld * acols);
+    const T is2 = T(1) / (T(sigma) * T(sigma));  // inverse_sigma2 in T (:285)
+    for (int64_t off = 0; off < n; off += chunk) {
+        const int64_t nc = std::min(chunk, n - off), ncp = round_up(nc, 16);
+        if (nc < chunk || off == 0) GPRX_HIP(hipMemsetAsync(dA.p, 0, sizeof(T) * ld * acols, s));
+        const T* tabc = nullptr;
+        if (K.nper > 0) {
+            launch_sincos_tables<T>(K, dX.as<T>() + off * d, nc, d, dtx.as<T>(), s);
+            tabc = dtx.as<T>();
+        }
+        launch_kbuild<T>(K, dXm.as<T>(), dtm.as<T>(), M, dX.as<T>() + off * d, tabc, nc, d, dA.as<T>(), ld, 0,
+                         false, T(0), dflag.as<int>(), s);
+        launch_label_rows<T>(dY.as<T>() + off * m, nc, m, dA.as<T>(), ld, Mp, ncp, mp, s);
+        const int64_t kpart = round_up((ncp + P - 1) / P, 16);  // zero-padded columns make up the rest
+        const int Pc = (int)((ncp + kpart - 1) / kpart);
+        launch_gemm_nt_splitk<T>(dS.as<T>(), ld, sstride, dA.as<T>(), ld, dA.as<T>(), ld, ld, Mp, kpart, Pc, is2, true,
+                                 s);
+    }
+    launch_sum_partials<T>(dS.as<T>(), sstride, P, s);  // dS[0] += dS[1..P-1]
+    if (ctx->comm && ctx->world > 1) {
+        const ncclResult_t r =
+            ncclAllReduce(dS.p, dS.p, (size_t)(ld * Mp), nccl_type<T>(), ncclSum, ctx->comm, s);
+        if (r != ncclSuccess) throw Error{GPRX_ERR_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(r)};
+    }
+    // ---- S = K + accumulated; K separately for Kinv ----------------------------------------
+    dK.ensure(sizeof(T) * Mp * Mp);
+    launch_kbuild<T>(K, dXm.as<T>(), dtm.as<T>(), M, dXm.as<T>(), dtm.as<T>(), M, d, dK.as<T>(), Mp, Mp, true,
+                     T(jitter), dflag.as<int>(), s);
+    launch_gemm_add_lower<T>(dS.as<T>(), ld, dK.as<T>(), Mp, M, s);  // S[:M,:M] (lower) += K
+    launch_set_identity_pad<T>(dS.as<T>(), ld, M, Mp, s);
+    int hflag = 0;
+    download(&hflag, dflag.p, sizeof(int), s);
+    if (hflag)
+        throw Error{GPRX_ERR_NONFINITE,
+                    "GaussianProcess::ComputeKernelMatrixInternal: kernel matrix contains entries which are not finite."};
+    // ---- S = L L^T with b in the extra rows -> RV; S^{-1} -> RM -----------------------------
+    dLinv.ensure(sizeof(T) * Mp * DB);
+    GPRX_HIP(hipMemsetD32Async((hipDeviceptr_t)dinfo.p, INT_MAX, 1, s));
+    potrf_blocked<T>(dS.as<T>(), ld, Mp, ld, dLinv.as<T>(), dinfo.as<int>(), ctx->ex);
+    int hinfo = 0;
+    download(&hinfo, dinfo.p, sizeof(int), s);
+    if (hinfo != INT_MAX)
+        throw Error{GPRX_ERR_NOT_SPD, "gprx_sparse_fit: K + sigma^-2 Knm^T Knm is not positive definite (pivot " +
+                                          std::to_string(hinfo) + ")"};
+    if (RV) {
+        dz.ensure(sizeof(T) * m * Mp);
+        dalpha.ensure(sizeof(T) * Mp * m);
+        launch_backsolve<T>(dS.as<T>(), ld, Mp, m, dLinv.as<T>(), dz.as<T>(), dalpha.as<T>(), s);
+        download(RV, dalpha.p, sizeof(T) * M * m, s);
+    }
+    dV.ensure(sizeof(T) * Mp * Mp);
+    dC.ensure(sizeof(T) * Mp * Mp);
+    if (RM) {
+        launch_spd_inverse_from_factor<T>(dS.as<T>(), ld, Mp, dLinv.as<T>(), dV.as<T>(), dC.as<T>(), s);
+        download_sym<T>(RM, dC, Mp, M, s);
+    }
+    // ---- Kinv ------------------------------------------------------------------------------
+    if (Kinv) {
+        dLinvK.ensure(sizeof(T) * Mp * DB);
+        GPRX_HIP(hipMemsetD32Async((hipDeviceptr_t)dinfo.p, INT_MAX, 1, s));
+        potrf_blocked<T>(dK.as<T>(), Mp, Mp, Mp, dLinvK.as<T>(), dinfo.as<int>(), ctx->ex);
+        download(&hinfo, dinfo.p, sizeof(int), s);
+        if (hinfo != INT_MAX)
+            throw Error{GPRX_ERR_NOT_SPD, "gprx_sparse_fit: Kmm + jitter I is not positive definite (pivot " +
+                                              std::to_string(hinfo) + ")"};
+        launch_spd_inverse_from_factor<T>(dK.as<T>(), Mp, Mp, dLinvK.as<T>(), dV.as<T>(), dC.as<T>(), s);
+        download_sym<T>(Kinv, dC, Mp, M, s);
+    }
+    return GPRX_OK;
+}
+
+// ---------------------------------------------------------------------------------------
 // C ABI
 // ---------------------------------------------------------------------------------------
 extern "C" {
@@ -632,9 +784,7 @@ gprx_status gprx_device_count(int* count) {
     API_END(nullptr)
 }
 
-gprx_status gprx_ctx_create(int device, gprx_ctx** out) {
-    API_BEGIN
-    GPRX_REQUIRE(out, GPRX_ERR_ARG, "gprx_ctx_create: out is NULL");
+static gprx_ctx* ctx_new(int device) {
     int c = 0;
     if (hipGetDeviceCount(&c) != hipSuccess || c == 0)
         throw Error{GPRX_ERR_NO_DEVICE, "gprx_ctx_create: no HIP device visible (libgprx has no CPU fallback)"};
@@ -672,7 +822,13 @@ gprx_status gprx_ctx_create(int device, gprx_ctx** out) {
     ctx->ex.s0 = ctx->stream;
     ctx->ex.s1 = ctx->aux;
     for (auto& e : ctx->ev) GPRX_HIP(hipEventCreate(&e));
-    *out = ctx;
+    return ctx;
+}
+
+gprx_status gprx_ctx_create(int device, gprx_ctx** out) {
+    API_BEGIN
+    GPRX_REQUIRE(out, GPRX_ERR_ARG, "gprx_ctx_create: out is NULL");
+    *out = ctx_new(device);
     return GPRX_OK;
     API_END(nullptr)
 }
@@ -684,6 +840,7 @@ void gprx_ctx_destroy(gprx_ctx* ctx) {
         if (e) (void)hipEventDestroy(e);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
+    if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
     delete ctx;
 }
 
@@ -964,25 +1121,46 @@ gprx_status gprx_dev_bench(gprx_ctx* ctx, gprx_dtype dtype, int32_t what, int64_
 }
 
 gprx_status gprx_dist_unique_id(void* out) {
-    return fail(nullptr, GPRX_ERR_RCCL, "gprx_dist_unique_id: multi-GPU path not built yet");
-    (void)out;
+    API_BEGIN
+    GPRX_REQUIRE(out, GPRX_ERR_ARG, "gprx_dist_unique_id: out is NULL");
+    static_assert(sizeof(ncclUniqueId) == GPRX_UNIQUE_ID_BYTES, "unique id size");
+    ncclUniqueId id;
+    const ncclResult_t r = ncclGetUniqueId(&id);
+    if (r != ncclSuccess) throw Error{GPRX_ERR_RCCL, std::string("ncclGetUniqueId: ") + ncclGetErrorString(r)};
+    std::memcpy(out, &id, sizeof(id));
+    return GPRX_OK;
+    API_END(nullptr)
 }
 
 gprx_status gprx_ctx_create_dist(int device, int rank, int world, const void* unique_id, gprx_ctx** out) {
-    (void)device;
-    (void)rank;
-    (void)world;
-    (void)unique_id;
-    (void)out;
-    return fail(nullptr, GPRX_ERR_RCCL, "gprx_ctx_create_dist: multi-GPU path not built yet");
+    API_BEGIN
+    GPRX_REQUIRE(out && unique_id, GPRX_ERR_ARG, "gprx_ctx_create_dist: NULL argument");
+    GPRX_REQUIRE(world >= 1 && rank >= 0 && rank < world, GPRX_ERR_ARG, "gprx_ctx_create_dist: bad rank/world");
+    gprx_ctx* ctx = ctx_new(device);
+    ctx->rank = rank;
+    ctx->world = world;
+    ncclUniqueId id;
+    std::memcpy(&id, unique_id, sizeof(id));
+    const ncclResult_t r = ncclCommInitRank(&ctx->comm, world, id, rank);
+    if (r != ncclSuccess) {
+        gprx_ctx_destroy(ctx);
+        throw Error{GPRX_ERR_RCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(r)};
+    }
+    *out = ctx;
+    return GPRX_OK;
+    API_END(nullptr)
 }
 
 gprx_status gprx_sparse_fit(gprx_ctx* ctx, gprx_dtype dtype, const gprx_kernel_desc* kernel, const void* X,
                             const void* Y, int64_t n, int32_t d, int32_t m, const void* Xm, int64_t M, double sigma,
                             double jitter, void* Kinv, void* RV, void* RM) {
-    (void)dtype; (void)kernel; (void)X; (void)Y; (void)n; (void)d; (void)m; (void)Xm; (void)M; (void)sigma;
-    (void)jitter; (void)Kinv; (void)RV; (void)RM;
-    return fail(ctx, GPRX_ERR_STATE, "gprx_sparse_fit: not built yet");
+    API_BEGIN
+    ProfBind pb_(ctx);
+    GPRX_REQUIRE(ctx && kernel && Xm && (X || n == 0) && (Y || n == 0), GPRX_ERR_ARG, "gprx_sparse_fit: NULL argument");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    return dtype == GPRX_F64 ? sparse_fit_impl<double>(ctx, kernel, X, Y, n, d, m, Xm, M, sigma, jitter, Kinv, RV, RM)
+                             : sparse_fit_impl<float>(ctx, kernel, X, Y, n, d, m, Xm, M, sigma, jitter, Kinv, RV, RM);
+    API_END(ctx)
 }
 
 }  // extern "C"

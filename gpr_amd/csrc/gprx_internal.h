@@ -285,6 +285,11 @@ void launch_deriv_matrix(const KCanon<T>& K, const T* X, const T* tab, int64_t n
 // Augmented label rows: A[np + r, j] = Y[j, r] (j < n, r < m), zero elsewhere in the block.
 template <typename T>
 void launch_aug_rows(const T* Y, int64_t n, int m, T* A, int64_t ld, int64_t np, int64_t mp, hipStream_t s);
+// General form: A[row0 + r, j] = Y[j, r] for j < n, r < m; zero for the other of the mp rows
+// and for n <= j < ncols.
+template <typename T>
+void launch_label_rows(const T* Y, int64_t n, int m, T* A, int64_t ld, int64_t row0, int64_t ncols, int64_t mp,
+                       hipStream_t s);
 
 // Blocked right-looking Cholesky of the leading np x np block of A (ld rows; rows np..ld
 // are extra rows solved along: they end up holding (L^{-1} B)^T).  Linv receives the
@@ -306,6 +311,11 @@ void potrf_blocked(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* in
 template <typename T>
 void launch_gemm_nt(T* C, int64_t ldc, const T* A, int64_t lda, const T* B, int64_t ldb, int64_t M, int64_t N,
                     int64_t K, T alpha, T beta, bool lower, hipStream_t s);
+// Split-K accumulation: partial p (of P) += alpha A[:, pK:(p+1)K] B[:, pK:(p+1)K]^T into
+// C + p*cstride; K is the per-partial depth (multiple of 16).
+template <typename T>
+void launch_gemm_nt_splitk(T* C, int64_t ldc, int64_t cstride, const T* A, int64_t lda, const T* B, int64_t ldb,
+                           int64_t M, int64_t N, int64_t K, int P, T alpha, bool lower, hipStream_t s);
 
 // Back substitution L^T alpha = z with z given as the m augmented rows (row-major output
 // alpha: np x m, ld m).  Uses the diagonal-block inverses.

@@ -179,21 +179,27 @@ void launch_deriv_matrix(const KCanon<T>& K, const T* X, const T* tab, int64_t n
 // ---------------------------------------------------------------------------------------
 template <typename T>
 __global__ void aug_rows_kernel(const T* __restrict__ Y, int64_t n, int m, T* __restrict__ A, int64_t ld,
-                                int64_t np, int64_t mp) {
+                                int64_t row0, int64_t ncols, int64_t mp) {
     int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= mp * np) return;
+    if (e >= mp * ncols) return;
     int64_t r = e % mp, j = e / mp;
     T v = T(0);
     if (r < m && j < n) v = Y[j * m + r];
-    A[np + r + j * ld] = v;
+    A[row0 + r + j * ld] = v;
+}
+
+template <typename T>
+void launch_label_rows(const T* Y, int64_t n, int m, T* A, int64_t ld, int64_t row0, int64_t ncols, int64_t mp,
+                       hipStream_t s) {
+    int64_t e = mp * ncols;
+    if (e == 0) return;
+    hipLaunchKernelGGL(aug_rows_kernel<T>, dim3((unsigned)((e + 255) / 256)), dim3(256), 0, s, Y, n, m, A, ld, row0,
+                       ncols, mp);
 }
 
 template <typename T>
 void launch_aug_rows(const T* Y, int64_t n, int m, T* A, int64_t ld, int64_t np, int64_t mp, hipStream_t s) {
-    int64_t e = mp * np;
-    if (e == 0) return;
-    hipLaunchKernelGGL(aug_rows_kernel<T>, dim3((unsigned)((e + 255) / 256)), dim3(256), 0, s, Y, n, m, A, ld, np,
-                       mp);
+    launch_label_rows<T>(Y, n, m, A, ld, np, np, mp, s);
 }
 
 #define GPRX_INST(T)                                                                                       \
@@ -202,7 +208,9 @@ void launch_aug_rows(const T* Y, int64_t n, int m, T* A, int64_t ld, int64_t np,
                                    int64_t, int, T*, int64_t, int64_t, bool, T, int*, hipStream_t);       \
     template void launch_deriv_matrix<T>(const KCanon<T>&, const T*, const T*, int64_t, int, T*,          \
                                          hipStream_t);                                                     \
-    template void launch_aug_rows<T>(const T*, int64_t, int, T*, int64_t, int64_t, int64_t, hipStream_t);
+    template void launch_aug_rows<T>(const T*, int64_t, int, T*, int64_t, int64_t, int64_t, hipStream_t); \
+    template void launch_label_rows<T>(const T*, int64_t, int, T*, int64_t, int64_t, int64_t, int64_t,   \
+                                       hipStream_t);
 GPRX_INST(double)
 GPRX_INST(float)
 #undef GPRX_INST

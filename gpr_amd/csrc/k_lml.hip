@@ -32,6 +32,36 @@ void launch_set_identity_pad(T* A, int64_t ld, int64_t n, int64_t np, hipStream_
 }
 
 template <typename T>
+__global__ void add_lower_kernel(T* __restrict__ S, int64_t lds, const T* __restrict__ K, int64_t ldk, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, j = blockIdx.y;
+    if (i < n && i >= j) S[i + j * lds] += K[i + j * ldk];
+}
+
+// S (lower, n x n, ld lds) += K (lower, ld ldk)
+template <typename T>
+void launch_gemm_add_lower(T* S, int64_t lds, const T* K, int64_t ldk, int64_t n, hipStream_t s) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(add_lower_kernel<T>, dim3((unsigned)((n + 255) / 256), (unsigned)n), dim3(256), 0, s, S, lds, K,
+                       ldk, n);
+}
+
+template <typename T>
+__global__ void sum_partials_kernel(T* __restrict__ S, int64_t stride, int P) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= stride) return;
+    T v = S[e];
+    for (int p = 1; p < P; p++) v += S[e + p * stride];
+    S[e] = v;
+}
+
+// S[0:stride] += sum_p S[p*stride : (p+1)*stride] (split-K partials, fixed order)
+template <typename T>
+void launch_sum_partials(T* S, int64_t stride, int P, hipStream_t s) {
+    if (P <= 1) return;
+    hipLaunchKernelGGL(sum_partials_kernel<T>, dim3((unsigned)((stride + 255) / 256)), dim3(256), 0, s, S, stride, P);
+}
+
+template <typename T>
 void launch_spd_inverse_from_factor(const T* A, int64_t ldA, int64_t np, const T* Linv, T* V, T* C, hipStream_t s) {
     Prof* saved = g_prof;  // the trsm/gemm pieces are accounted as one INVERSE phase
     ProfScope ps(KC_INVERSE, s, 2.0 * (double)np * np * np / 3.0, 0.0);
@@ -217,6 +247,8 @@ void launch_lml_grad(const KCanon<T>& K, const T* X, const T* tab, int64_t n, in
 
 #define GPRX_INST(T)                                                                                            \
     template void launch_set_identity_pad<T>(T*, int64_t, int64_t, int64_t, hipStream_t);                      \
+    template void launch_gemm_add_lower<T>(T*, int64_t, const T*, int64_t, int64_t, hipStream_t);              \
+    template void launch_sum_partials<T>(T*, int64_t, int, hipStream_t);                                        \
     template void launch_spd_inverse_from_factor<T>(const T*, int64_t, int64_t, const T*, T*, T*, hipStream_t); \
     template void launch_lml_grad<T>(const KCanon<T>&, const T*, const T*, int64_t, int, const T*, const T*,   \
                                      int64_t, double*, hipStream_t);

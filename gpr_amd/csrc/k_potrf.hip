@@ -292,7 +292,15 @@ struct MfmaTraits<float> {
 template <typename T, bool LOWER, bool BETA, bool KSKIP>
 __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(T* __restrict__ C, int64_t ldc, const T* __restrict__ A,
                                                          int64_t lda, const T* __restrict__ B, int64_t ldb,
-                                                         int64_t K, T alpha, T beta, int64_t ntm, int64_t ntn) {
+                                                         int64_t K, T alpha, T beta, int64_t ntm, int64_t ntn,
+                                                         int64_t cstride = 0) {
+    // split-K: blockIdx.y = p works on k in [p*K, (p+1)*K) and writes its own C + p*cstride
+    if (gridDim.y > 1) {
+        const int64_t p = blockIdx.y;
+        A += p * K * lda;
+        B += p * K * ldb;
+        C += p * cstride;
+    }
     typedef MfmaTraits<T> Tr;
     typedef typename Tr::acc_t acc_t;
     typedef typename Tr::vec_t vec_t;
@@ -455,6 +463,33 @@ void launch_gemm_nt(T* C, int64_t ldc, const T* A, int64_t lda, const T* B, int6
         else GPRX_GEMM(false, false);
     }
 #undef GPRX_GEMM
+}
+
+// Split-K form: P partial products, partial p = A[:, pK:(p+1)K] B[:, pK:(p+1)K]^T accumulated
+// (beta = 1) into C + p*cstride, all in one launch (grid.y = P); K is the slice depth.
+template <typename T>
+void launch_gemm_nt_splitk(T* C, int64_t ldc, int64_t cstride, const T* A, int64_t lda, const T* B, int64_t ldb,
+                           int64_t M, int64_t N, int64_t K, int P, T alpha, bool lower, hipStream_t s) {
+    if (M <= 0 || N <= 0 || K <= 0) return;
+    const int64_t ntm = M / GT, ntn = N / GT;
+    const int64_t ntiles = lower ? ntn * (ntn + 1) / 2 + (ntm - ntn) * ntn : ntm * ntn;
+    const size_t lds = gemm_lds_bytes<T>();
+    const double elems = lower ? ((double)N * (N + 1) / 2 + (double)(M - N) * N) : (double)M * N;
+    ProfScope ps(KC_OTHER, s, 2.0 * elems * K * P, (double)sizeof(T) * (2 * elems * P + (double)(M + N) * K * P));
+#define GPRX_GEMM_SK(L)                                                                                      \
+    do {                                                                                                     \
+        static bool attr_done = false;                                                                       \
+        if (!attr_done) {                                                                                    \
+            hipFuncSetAttribute((const void*)gemm_nt_kernel<T, L, true, false>,                              \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                       \
+            attr_done = true;                                                                                \
+        }                                                                                                    \
+        hipLaunchKernelGGL((gemm_nt_kernel<T, L, true, false>), dim3((unsigned)ntiles, (unsigned)P), dim3(256), \
+                           lds, s, C, ldc, A, lda, B, ldb, K, alpha, T(1), ntm, ntn, cstride);               \
+    } while (0)
+    if (lower) GPRX_GEMM_SK(true);
+    else GPRX_GEMM_SK(false);
+#undef GPRX_GEMM_SK
 }
 
 // C (lower) = A B^T where both operands vanish left of their row (LAUUM shape).
@@ -699,6 +734,8 @@ void launch_fit_reductions(const T* A, int64_t ld, int64_t n, int64_t np, int m,
 
 #define GPRX_INST(T)                                                                                      \
     template void potrf_blocked<T>(T*, int64_t, int64_t, int64_t, T*, int*, Exec&);                      \
+    template void launch_gemm_nt_splitk<T>(T*, int64_t, int64_t, const T*, int64_t, const T*, int64_t,   \
+                                           int64_t, int64_t, int64_t, int, T, bool, hipStream_t);         \
     template void launch_gemm_nt<T>(T*, int64_t, const T*, int64_t, const T*, int64_t, int64_t, int64_t, \
                                     int64_t, T, T, bool, hipStream_t);                                    \
     template void launch_backsolve<T>(const T*, int64_t, int64_t, int, const T*, T*, T*, hipStream_t);   \

@@ -158,6 +158,13 @@ def device_count():
     return c.value
 
 
+def unique_id():
+    """RCCL unique id (bytes) for gprx_ctx_create_dist; call on rank 0 and share it."""
+    buf = ctypes.create_string_buffer(UNIQUE_ID_BYTES)
+    _check(lib().gprx_dist_unique_id(buf))
+    return buf.raw
+
+
 class Context:
     """One per process per GPU (gprx_ctx)."""
 

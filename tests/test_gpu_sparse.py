@@ -1,0 +1,73 @@
+"""Sparse GP (subset of regressors) on the GPU vs the oracle restatement of
+SparseGaussianProcess::PreComputeRegression (include/SparseGaussianProcess.h:274-313).
+
+The device computes RV = S^{-1} sigma^-2 Knm^T Y and RM = S^{-1} from one Cholesky of
+S = Kmm + jitter I + sigma^-2 Knm^T Knm (the reference's Kinv (sigma^-2 K Sigma Knm^T Y) and
+Kinv (K Sigma K) Kinv are algebraically these), streaming Knm in
+row chunks.  Sparse-path parity is otherwise unpinned by the reference's own tests
+(tests/SparseInferenceTest.cpp:486-489 are disabled); the oracle follows the reference's
+formulas literally.  Inducing points are rows i*(N/M) of X."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from tests.helpers import make_data, make_queries, relerr, TOL
+
+pytestmark = pytest.mark.gpu
+
+CASES = [
+    ("GaussianKernel(0.7,1.3,)", np.float64, 1e-4, 0.3),
+    ("SumKernel(GaussianKernel(2,0.15,),PeriodicKernel(0.1,3.141592653589793,1,))", np.float64, 1e-4, 0.5),
+    ("RationalQuadraticKernel(1.1,0.6,1.5,)", np.float64, 1e-3, 0.3),
+    # fp32: the reference itself is only meaningful when cond(S) * eps32 is small (at jitter
+    # 0.1, sigma 0.5 the oracle's own fp32 result is 11% off its fp64 one); cond(S) = 2.7e3 here
+    ("GaussianKernel(0.7,1.3,)", np.float32, 0.5, 5.0),
+]
+
+
+def _inputs(n, d, M, m, dtype):
+    X, Y = make_data(n, d, m)
+    Xm = X[:: n // M][:M].copy()
+    return X.astype(dtype), Y.astype(dtype), Xm.astype(dtype)
+
+
+@pytest.mark.parametrize("ks,dtype,jitter,sigma", CASES)
+@pytest.mark.parametrize("chunk", [None, 64])
+def test_sparse_fit(ctx, monkeypatch, ks, dtype, jitter, sigma, chunk):
+    if chunk:
+        monkeypatch.setenv("GPRX_SPARSE_CHUNK", str(chunk))
+    n, d, M, m = 700, 3, 40, 2
+    X, Y, Xm = _inputs(n, d, M, m, dtype)
+    Kinv, RV, RM = ctx.sparse_fit(ks, X, Y, Xm, sigma, jitter, dtype)
+    Ki_r, RV_r, RM_r = O.sparse_fit(ks, X, Y, Xm, sigma, jitter, dtype)
+    tol = TOL[np.dtype(dtype)]
+    assert relerr(Kinv, Ki_r) <= tol * 10
+    assert relerr(RV, RV_r) <= tol * 10
+    assert relerr(RM, RM_r) <= tol * 10
+
+
+def test_sparse_predict_through_dense_model(ctx):
+    """SparseGaussianProcess::Predict (:86-92) = Kx^T RV over the inducing points: served by a
+    resident model holding the inducing points and RV (gprx_model_set_alpha)."""
+    import gpr_amd
+    ks = "GaussianKernel(0.7,1.3,)"
+    X, Y, Xm = _inputs(1000, 4, 50, 1, np.float64)
+    _, RV, _ = ctx.sparse_fit(ks, X, Y, Xm, 0.3, 1e-4)
+    Mdl = gpr_amd.Model(ctx, np.float64)
+    Mdl.set_data(Xm, np.zeros((Xm.shape[0], 1)))
+    Mdl.set_kernel(ks)
+    Mdl.set_noise(0.0)
+    Mdl.set_alpha(RV)
+    Xq = make_queries(77, 4)
+    mean = Mdl.predict(Xq)
+    _, RV_r, _ = O.sparse_fit(ks, X, Y, Xm, 0.3, 1e-4)
+    ref = O.predict(ks, Xm, RV_r, Xq)
+    assert relerr(mean, ref) <= 1e-6
+
+
+def test_sparse_bad_sigma(ctx):
+    import gpr_amd
+    X, Y, Xm = _inputs(100, 2, 10, 1, np.float64)
+    with pytest.raises(gpr_amd.GprxError) as e:
+        ctx.sparse_fit("GaussianKernel(1,1,)", X, Y, Xm, 0.0, 1e-4)
+    assert "sigma must be positive" in str(e.value)
