@@ -13,6 +13,7 @@
 #include "gpr/Kernel.h"
 #include "gpr/Likelihood.h"
 #include "gpr/MatrixIO.h"
+#include "gpr/SparseGaussianProcess.h"
 
 using namespace gpr;
 
@@ -294,6 +295,32 @@ static void lik_test() {
     check(std::isfinite(lv) && lv >= 0, "GaussianLikelihood value " + num(lv));
 }
 
+// SparseGaussianProcess: dense sinus samples, every 10th as an inducing point
+// (the regression setting of tests/SparseInferenceTest.cpp), predictions close to sin.
+static void sparse_test() {
+    typedef SparseGaussianProcess<double> S;
+    auto gp = std::make_shared<S>(std::make_shared<GaussianKernel<double>>(0.8), 1e-6);
+    gp->SetSigma(0.01);
+    for (unsigned i = 0; i < 400; i++) {
+        S::VectorType x(1), y(1);
+        x(0) = i * 2 * M_PI / 400;
+        y(0) = std::sin(x(0));
+        gp->AddSample(x, y);
+        if (i % 10 == 0) gp->AddInducingSample(x, y);
+    }
+    gp->Initialize();
+    check(gp->GetNumberOfInducingSamples() == 40, "inducing count");
+    double err = 0;
+    for (unsigned i = 0; i < 50; i++) {
+        S::VectorType x(1);
+        x(0) = 0.1 + i * 6.0 / 50;
+        err += std::fabs(gp->Predict(x)(0) - std::sin(x(0)));
+        const double v = (*gp)(x, x);
+        check(std::isfinite(v) && v > -1e-6, "sparse posterior variance " + num(v));
+    }
+    check(err < 0.05, "sparse predict error " + num(err));
+}
+
 int main() {
     run("GaussianProcessTest1", gp_test1);
     run("GaussianProcessTest2", gp_test2);
@@ -306,5 +333,6 @@ int main() {
     run("IOTest2", io_test2);
     run("IOTest3", io_test3);
     run("LikelihoodGradient", lik_test);
+    run("SparseRegression", sparse_test);
     return g_fail;
 }
