@@ -231,7 +231,7 @@ struct gprx_model {
     gprx_kernel_desc desc{};
     KCanon<double> kd{};
     KCanon<float> kf{};
-    DevBuf X, Y, tab, A, Linv, z, alpha, info, flag, red, V, C, scratch1, scratch2, grad;
+    DevBuf X, Y, tab, A, Linv, z, alpha, info, flag, red, V, C, scratch1, scratch2, grad, pack;
     std::mutex mu;
 };
 
@@ -275,14 +275,19 @@ const KCanon<float>& kcanon<float>(const gprx_model* m) {
 // ---------------------------------------------------------------------------------------
 template <typename T>
 static gprx_status model_fit(gprx_model* M, uint32_t flags, gprx_fit_info* out) {
-    (void)flags;
     gprx_ctx* ctx = M->ctx;
     GPRX_REQUIRE(M->has_data, GPRX_ERR_STATE, "GaussianProcess::Initialize: no input samples defined during initialization");
     GPRX_REQUIRE(M->has_kernel, GPRX_ERR_STATE, "gprx: no kernel set");
     GPRX_HIP(hipSetDevice(ctx->device));
     hipStream_t s = ctx->stream;
     const KCanon<T>& K = kcanon<T>(M);
-    const int64_t n = M->n, np = round_up(n, DB), mp = round_up(M->m, GT), ld = np + mp;
+    // multi-GPU factorisation on an RCCL context (GPRX_FIT_DISTRIBUTED forces the same code
+    // path on a one-rank communicator)
+    const bool dist = (ctx->comm && ctx->world > 1) || ((flags & GPRX_FIT_DISTRIBUTED) && ctx->comm);
+    GPRX_REQUIRE(!(flags & GPRX_FIT_DISTRIBUTED) || ctx->comm, GPRX_ERR_STATE,
+                 "gprx_model_fit: GPRX_FIT_DISTRIBUTED needs a context from gprx_ctx_create_dist");
+    const int64_t n = M->n, np = round_up(n, dist ? (int64_t)outer_block() : (int64_t)DB), mp = round_up(M->m, GT),
+                  ld = np + mp;
     M->np = np;
     M->mp = mp;
     M->ld = ld;
@@ -302,11 +307,51 @@ static gprx_status model_fit(gprx_model* M, uint32_t flags, gprx_fit_info* out) 
     const T sig = (T)M->sigma;
     const T sigma2 = sig * sig;  // m_Sigma*m_Sigma in T (lib/GaussianProcess.cpp:379)
     GPRX_HIP(hipEventRecord(ctx->ev[0], s));
-    launch_kbuild<T>(K, M->X.as<T>(), M->tab.as<T>(), n, M->X.as<T>(), M->tab.as<T>(), n, M->d, M->A.as<T>(), ld, np,
-                     true, sigma2, M->flag.as<int>(), s);
-    launch_aug_rows<T>(M->Y.as<T>(), n, M->m, M->A.as<T>(), ld, np, mp, s);
+    if (!dist || ctx->world == 1) {
+        launch_kbuild<T>(K, M->X.as<T>(), M->tab.as<T>(), n, M->X.as<T>(), M->tab.as<T>(), n, M->d, M->A.as<T>(), ld,
+                         np, true, sigma2, M->flag.as<int>(), s);
+        launch_aug_rows<T>(M->Y.as<T>(), n, M->m, M->A.as<T>(), ld, np, mp, s);
+    } else {
+        // sharded build: each rank builds only the column panels it owns (rows c0.. of the
+        // lower triangle, the diagonal noise/padding and the label rows)
+        const int64_t NBO = outer_block(), d = M->d;
+        DevBuf tr, tc;
+        for (int64_t Kp = ctx->rank; Kp * NBO < np; Kp += ctx->world) {
+            const int64_t c0 = Kp * NBO;
+            T* Ap = M->A.as<T>() + c0 * ld;
+            GPRX_HIP(hipMemset2DAsync(Ap + c0, sizeof(T) * ld, 0, sizeof(T) * (ld - c0), NBO, s));
+            const int64_t nr = std::max<int64_t>(0, n - c0), nc = std::min<int64_t>(NBO, nr);
+            if (nc > 0) {
+                const T* tabr = nullptr;
+                const T* tabc = nullptr;
+                if (K.nper > 0) {
+                    tr.ensure(sizeof(T) * 2 * K.nper * nr * d);
+                    tc.ensure(sizeof(T) * 2 * K.nper * nc * d);
+                    launch_sincos_tables<T>(K, M->X.as<T>() + c0 * d, nr, (int)d, tr.as<T>(), s);
+                    launch_sincos_tables<T>(K, M->X.as<T>() + c0 * d, nc, (int)d, tc.as<T>(), s);
+                    tabr = tr.as<T>();
+                    tabc = tc.as<T>();
+                }
+                launch_kbuild<T>(K, M->X.as<T>() + c0 * d, tabr, nr, M->X.as<T>() + c0 * d, tabc, nc, (int)d, Ap + c0,
+                                 ld, 0, false, T(0), M->flag.as<int>(), s);
+            }
+            launch_diag_fix<T>(M->A.as<T>(), ld, c0, NBO, n, sigma2, s);
+            launch_label_rows<T>(M->Y.as<T>() + c0 * M->m, nc, M->m, Ap, ld, np, NBO, mp, s);
+            if (K.nper > 0) GPRX_HIP(hipStreamSynchronize(s));  // tr/tc reused next panel
+        }
+    }
     GPRX_HIP(hipEventRecord(ctx->ev[1], s));
-    potrf_blocked<T>(M->A.as<T>(), ld, np, ld, M->Linv.as<T>(), M->info.as<int>(), ctx->ex);
+    if (dist) {
+        M->pack.ensure(sizeof(T) * ld * outer_block());
+        potrf_dist<T>(M->A.as<T>(), ld, np, ld, M->Linv.as<T>(), M->info.as<int>(), ctx->ex, ctx->comm, ctx->rank,
+                      ctx->world, M->pack.as<T>());
+        if (ctx->world > 1) {  // the non-finite flag of every rank's panels
+            const ncclResult_t r = ncclAllReduce(M->flag.p, M->flag.p, 1, ncclInt32, ncclMax, ctx->comm, s);
+            if (r != ncclSuccess) throw Error{GPRX_ERR_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(r)};
+        }
+    } else {
+        potrf_blocked<T>(M->A.as<T>(), ld, np, ld, M->Linv.as<T>(), M->info.as<int>(), ctx->ex);
+    }
     GPRX_HIP(hipEventRecord(ctx->ev[2], s));
     launch_fit_reductions<T>(M->A.as<T>(), ld, n, np, M->m, M->red.as<double>(), s);
     launch_backsolve<T>(M->A.as<T>(), ld, np, M->m, M->Linv.as<T>(), M->z.as<T>(), M->alpha.as<T>(), s);

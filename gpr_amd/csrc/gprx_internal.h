@@ -16,6 +16,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 #include <cstdint>
 #include <cstdio>
 #include <string>
@@ -288,6 +289,8 @@ void launch_aug_rows(const T* Y, int64_t n, int m, T* A, int64_t ld, int64_t np,
 // General form: A[row0 + r, j] = Y[j, r] for j < n, r < m; zero for the other of the mp rows
 // and for n <= j < ncols.
 template <typename T>
+void launch_diag_fix(T* A, int64_t ld, int64_t c0, int64_t w, int64_t n, T sigma2, hipStream_t s);
+template <typename T>
 void launch_label_rows(const T* Y, int64_t n, int m, T* A, int64_t ld, int64_t row0, int64_t ncols, int64_t mp,
                        hipStream_t s);
 
@@ -305,6 +308,12 @@ struct Exec {
 int outer_block();
 template <typename T>
 void potrf_blocked(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info, Exec& ex);
+// Multi-GPU form: column panels of outer_block() columns dealt cyclically over `world`
+// ranks (np must be a multiple of outer_block()); the factored panels are RCCL-broadcast so
+// every rank ends with the full factor.  pack: device scratch of nrows * outer_block().
+template <typename T>
+void potrf_dist(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info, Exec& ex, ncclComm_t comm, int rank,
+                int world, T* pack);
 
 // Generic C = beta C + alpha A B^T on GT-multiples (column-major).  lower: only tiles
 // with col-tile <= row-tile are computed, and inside diagonal tiles only row >= col.

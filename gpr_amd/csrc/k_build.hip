@@ -202,6 +202,21 @@ void launch_aug_rows(const T* Y, int64_t n, int m, T* A, int64_t ld, int64_t np,
     launch_label_rows<T>(Y, n, m, A, ld, np, np, mp, s);
 }
 
+template <typename T>
+__global__ void diag_fix_kernel(T* __restrict__ A, int64_t ld, int64_t c0, int64_t w, int64_t n, T sigma2) {
+    const int64_t i = c0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= c0 + w) return;
+    A[i + i * ld] = (i < n) ? A[i + i * ld] + sigma2 : T(1);
+}
+
+// Diagonal of columns [c0, c0+w): += sigma2 for i < n (AddNoiseToKernelMatrix,
+// lib/GaussianProcess.cpp:375-381), 1 for the padding.
+template <typename T>
+void launch_diag_fix(T* A, int64_t ld, int64_t c0, int64_t w, int64_t n, T sigma2, hipStream_t s) {
+    if (w <= 0) return;
+    hipLaunchKernelGGL(diag_fix_kernel<T>, dim3((unsigned)((w + 255) / 256)), dim3(256), 0, s, A, ld, c0, w, n, sigma2);
+}
+
 #define GPRX_INST(T)                                                                                       \
     template void launch_sincos_tables<T>(const KCanon<T>&, const T*, int64_t, int, T*, hipStream_t);     \
     template void launch_kbuild<T>(const KCanon<T>&, const T*, const T*, int64_t, const T*, const T*,     \
@@ -210,7 +225,8 @@ void launch_aug_rows(const T* Y, int64_t n, int m, T* A, int64_t ld, int64_t np,
                                          hipStream_t);                                                     \
     template void launch_aug_rows<T>(const T*, int64_t, int, T*, int64_t, int64_t, int64_t, hipStream_t); \
     template void launch_label_rows<T>(const T*, int64_t, int, T*, int64_t, int64_t, int64_t, int64_t,   \
-                                       hipStream_t);
+                                       hipStream_t);                                                       \
+    template void launch_diag_fix<T>(T*, int64_t, int64_t, int64_t, int64_t, T, hipStream_t);
 GPRX_INST(double)
 GPRX_INST(float)
 #undef GPRX_INST

@@ -22,6 +22,7 @@ UNIQUE_ID_BYTES = 128
 
 FIT_DEFAULT = 0
 FIT_NO_LU_FALLBACK = 1
+FIT_DISTRIBUTED = 2
 LML_GRAD = 1
 LML_COMPAT = 2
 

@@ -144,7 +144,9 @@ gprx_status gprx_model_set_kernel(gprx_model* model, const gprx_kernel_desc* ker
 gprx_status gprx_model_set_noise(gprx_model* model, double sigma);
 
 #define GPRX_FIT_DEFAULT 0u
-#define GPRX_FIT_NO_LU_FALLBACK 1u /* report NOT_SPD instead of falling back to LU */
+#define GPRX_FIT_NO_LU_FALLBACK 1u /* reserved: the device path always reports NOT_SPD (no LU) */
+#define GPRX_FIT_DISTRIBUTED 2u    /* multi-GPU factorisation on a gprx_ctx_create_dist context
+                                      (implied when world > 1; forces the path at world = 1) */
 /* Initialize (lib/GaussianProcess.cpp:118-130) = ComputeRegressionVectors (:642-672):
  * kernel matrix (:384-402) + noise (:375-381) + factorisation (replaces the default
  * lapack::lu_invert dgetrf_+dgetri_, include/LAPACKUtils.h:38-56,85-97) + regression

@@ -177,3 +177,34 @@ def test_set_alpha_restores_predict(ctx, ks):
         M2.posterior_cov(Xq, Xq)
     M2.fit()
     assert np.array_equal(M2.alpha(), M.alpha())
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("n", [700, 1536])
+def test_distributed_fit_one_rank(dtype, n):
+    """The multi-GPU factorisation (potrf_dist: panel-cyclic ownership, look-ahead, RCCL
+    broadcast of factored panels) on a one-rank RCCL communicator, forced by
+    GPRX_FIT_DISTRIBUTED: same alpha / predictions / logdet as the single-GPU path."""
+    import gpr_amd
+    from gpr_amd import gprx
+    ks = KERNELS[4]
+    X, Y = make_data(n, 5, 2)
+    X, Y = X.astype(dtype), Y.astype(dtype)
+    dctx = gpr_amd.Context(0, dist=(0, 1, gpr_amd.unique_id()))
+    try:
+        Md = gpr_amd.Model(dctx, dtype)
+        Md.set_data(X, Y)
+        Md.set_kernel(ks)
+        Md.set_noise(0.5)
+        info_d = Md.fit(gprx.FIT_DISTRIBUTED)
+        a_ref, _ = O.fit(ks, X.astype(np.float64), Y.astype(np.float64), 0.5)
+        tol = TOL[np.dtype(dtype)]
+        assert relerr(Md.alpha(), a_ref) <= tol
+        Xq = make_queries(40, 5).astype(dtype)
+        mean = Md.predict(Xq)
+        assert relerr(mean, O.predict(ks, X.astype(np.float64), a_ref, Xq.astype(np.float64))) <= tol
+        K = O.kernel_matrix(ks, X.astype(np.float64)) + 0.25 * np.eye(n)
+        assert abs(info_d.logdet - np.linalg.slogdet(K)[1]) <= (1e-8 if dtype == np.float64 else 1e-3) * abs(info_d.logdet)
+        Md.close()
+    finally:
+        dctx.close()
