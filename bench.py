@@ -65,6 +65,23 @@ def cpu_baseline(cfg, n_cpu):
     }
 
 
+def traffic_from_profile():
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC passes
+    (profiles/*_pmc_traffic.json, written by scripts/pmc_traffic.py: FETCH_SIZE x 2 (gfx950
+    wide-read correction, MI355X_MICROARCH.md §HBM) + WRITE_SIZE, averaged over launches)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
+    if not files:
+        return None
+    try:
+        with open(files[-1]) as f:
+            t = json.load(f)
+        k = t["kernels"].get("gemm_nt_kernel<double, true, true, false>")
+        return None if k is None else {"bytes_per_launch": k["hbm_bytes_per_launch"], "source": os.path.basename(files[-1])}
+    except Exception:
+        return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -188,9 +205,13 @@ def main():
                        "n": n, "d": d, "m": m, "kernel": cfg["kernel"],
                        "parallelism": (f"panel-cyclic factorisation over {world} GPUs (RCCL)" if distributed_fit
                                        else ("replicas" if world > 1 else "single-gpu"))},
-            "roofline": {"bound": "mfma", "kernel": "gemm_nt trailing update (potrf_update)",
+            "roofline": {"bound": "mfma", "kernel": "gemm_nt_kernel<double,true,true,false> (potrf_update: "
+                                                      "trailing / look-ahead / in-panel updates)",
                          "achieved": achieved, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / PEAK_FP64_TFLOPS, "traffic": None},
+                         "frac": achieved / PEAK_FP64_TFLOPS,
+                         "avg_launch_us": (1e3 * upd["ms"] / upd["launches"]) if upd["launches"] else None,
+                         "algorithmic_flops_per_launch": (upd["flops"] / upd["launches"]) if upd["launches"] else None,
+                         "traffic": traffic_from_profile()},
             "fit_roofline": {"t_roof_ms": t_roof, "t_fit_device_ms": fit_ms, "frac": t_roof / fit_ms},
             "phases": phases,
             "predict": pred,

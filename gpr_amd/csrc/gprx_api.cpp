@@ -197,6 +197,7 @@ struct gprx_ctx {
     ncclComm_t comm = nullptr;  // RCCL communicator (gprx_ctx_create_dist), world > 1
     hipStream_t stream = nullptr;
     hipStream_t aux = nullptr;  // look-ahead stream of the factorisation
+    hipStream_t aux2 = nullptr;  // second look-ahead stream (next panel's later columns)
     Exec ex;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     Prof prof;
@@ -213,6 +214,7 @@ struct ProfBind {
         if (ctx && ctx->prof.on) {
             (void)hipStreamSynchronize(ctx->stream);
             (void)hipStreamSynchronize(ctx->aux);
+            (void)hipStreamSynchronize(ctx->aux2);
             ctx->prof.resolve();
         }
         g_prof = nullptr;
@@ -864,8 +866,10 @@ static gprx_ctx* ctx_new(int device) {
     } else {
         GPRX_HIP(hipStreamCreateWithPriority(&ctx->aux, hipStreamNonBlocking, prio_lo));
     }
+    GPRX_HIP(hipStreamCreateWithPriority(&ctx->aux2, hipStreamNonBlocking, prio_hi));
     ctx->ex.s0 = ctx->stream;
     ctx->ex.s1 = ctx->aux;
+    ctx->ex.s2 = ctx->aux2;
     for (auto& e : ctx->ev) GPRX_HIP(hipEventCreate(&e));
     return ctx;
 }
@@ -885,6 +889,7 @@ void gprx_ctx_destroy(gprx_ctx* ctx) {
         if (e) (void)hipEventDestroy(e);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
+    if (ctx->aux2) (void)hipStreamDestroy(ctx->aux2);
     if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
     delete ctx;
 }

@@ -301,6 +301,7 @@ void launch_label_rows(const T* Y, int64_t n, int m, T* A, int64_t ld, int64_t r
 struct Exec {
     hipStream_t s0 = nullptr;  // main stream (panel chain)
     hipStream_t s1 = nullptr;  // look-ahead stream (bulk trailing updates); may be null
+    hipStream_t s2 = nullptr;  // second look-ahead stream (next panel's later columns); may be null
     std::vector<hipEvent_t> ev;
     hipEvent_t event(size_t i);
     ~Exec();

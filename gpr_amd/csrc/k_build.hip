@@ -17,6 +17,7 @@
 #include "k_tile.h"
 
 #include <cmath>
+#include <cstdint>
 
 namespace gprx {
 
@@ -87,29 +88,50 @@ __global__ __launch_bounds__(256) void kbuild_kernel(KCanon<T> K, const T* __res
             for (int b = 0; b < 4; b++) r2[a][b] = s0[a][b] = s1[a][b] = T(0);
     }
 
+    // Stores: each thread owns 4 consecutive rows of 4 columns; the 16 lanes of a column
+    // cover 64 consecutive rows, so one 32-byte store per thread and column gives 512
+    // contiguous bytes per column and wave (whole cache lines: no read-for-ownership of
+    // partial lines at the memory side).
     bool bad = false;
+    const bool vec_ok = ((ld & 3) == 0) && ((reinterpret_cast<uintptr_t>(A) & 31) == 0);
 #pragma unroll
     for (int b = 0; b < 4; b++) {
         const int64_t gj = j0 + ty * 4 + b;
+        const int64_t gi0 = i0 + tx * 4;
+        T v[4];
+        bool ok[4];
 #pragma unroll
         for (int a = 0; a < 4; a++) {
-            const int64_t gi = i0 + tx * 4 + a;
-            T v;
+            const int64_t gi = gi0 + a;
             if (lower) {
-                if (gi >= npad || gj >= npad) continue;
+                ok[a] = gi < npad && gj < npad;
                 if (gi >= na || gj >= nb) {
-                    v = (gi == gj) ? T(1) : T(0);
+                    v[a] = (gi == gj) ? T(1) : T(0);
                 } else {
-                    v = kernel_value(K, r2[a][b], s0[a][b], s1[a][b]);
-                    if (!isfinite(v)) bad = true;
-                    if (gi == gj) v += sigma2;
+                    v[a] = kernel_value(K, r2[a][b], s0[a][b], s1[a][b]);
+                    if (!isfinite(v[a])) bad = true;
+                    if (gi == gj) v[a] += sigma2;
                 }
             } else {
-                if (gi >= na || gj >= nb) continue;
-                v = kernel_value(K, r2[a][b], s0[a][b], s1[a][b]);
-                if (!isfinite(v)) bad = true;
+                ok[a] = gi < na && gj < nb;
+                v[a] = ok[a] ? kernel_value(K, r2[a][b], s0[a][b], s1[a][b]) : T(0);
+                if (ok[a] && !isfinite(v[a])) bad = true;
             }
-            A[gi + gj * ld] = v;
+        }
+        T* dst = A + gi0 + gj * ld;
+        if (vec_ok && ok[3]) {  // ok[3] implies ok[0..2]
+            if constexpr (sizeof(T) == 8) {
+                typedef double d2 __attribute__((ext_vector_type(2)));
+                reinterpret_cast<d2*>(dst)[0] = d2{v[0], v[1]};
+                reinterpret_cast<d2*>(dst)[1] = d2{v[2], v[3]};
+            } else {
+                typedef float f4 __attribute__((ext_vector_type(4)));
+                *reinterpret_cast<f4*>(dst) = f4{v[0], v[1], v[2], v[3]};
+            }
+        } else {
+#pragma unroll
+            for (int a = 0; a < 4; a++)
+                if (ok[a]) dst[a] = v[a];
         }
     }
     if (bad) atomicOr(flag, 1);

@@ -260,7 +260,6 @@ __global__ __launch_bounds__(DT) __attribute__((amdgpu_num_vgpr(296))) void diag
 // ======================================================================================
 constexpr int BK = 16;
 constexpr int PADT = 16;
-constexpr int SROW = GT + PADT;  // LDS row (one k) length in elements
 
 typedef double d4_t __attribute__((ext_vector_type(4)));
 typedef float f4_t __attribute__((ext_vector_type(4)));
@@ -291,11 +290,26 @@ struct MfmaTraits<float> {
     __device__ static inline int orow(int lk, int reg) { return 4 * lk + reg; }
 };
 
-template <typename T, bool LOWER, bool BETA, bool KSKIP>
+// TM = 128: 4 waves of 64x64 (4x4 MFMA blocks each) -- the bulk trailing updates.
+// TM = 64:  4 waves of 32x32 (2x2 blocks) -- skinny panel-chain GEMMs (trsm, in-panel and
+//           look-ahead updates), 4x the workgroups so the short critical-path launches
+//           spread over the whole chip instead of running 64-128 long tiles.
+template <typename T, bool LOWER, bool BETA, bool KSKIP, int TM = 128>
 __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(T* __restrict__ C, int64_t ldc, const T* __restrict__ A,
                                                          int64_t lda, const T* __restrict__ B, int64_t ldb,
                                                          int64_t K, T alpha, T beta, int64_t ntm, int64_t ntn,
                                                          int64_t cstride = 0) {
+    typedef MfmaTraits<T> Tr;
+    typedef typename Tr::acc_t acc_t;
+    typedef typename Tr::vec_t vec_t;
+    constexpr int VEC = Tr::VEC;
+    constexpr int SR = TM + PADT;       // LDS row (one k) length in elements
+    constexpr int TPC = TM / VEC;       // threads per staged column
+    constexpr int CPP = 256 / TPC;      // columns per pass
+    constexpr int PASSES = (BK + CPP - 1) / CPP;
+    constexpr int NB = TM / 32;         // 16x16 MFMA blocks per wave edge (4 or 2)
+    constexpr int WT = TM / 2;          // wave tile edge
+
     // split-K: blockIdx.y = p works on k in [p*K, (p+1)*K) and writes its own C + p*cstride
     if (gridDim.y > 1) {
         const int64_t p = blockIdx.y;
@@ -303,17 +317,10 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(T* __restrict__ C, int6
         B += p * K * ldb;
         C += p * cstride;
     }
-    typedef MfmaTraits<T> Tr;
-    typedef typename Tr::acc_t acc_t;
-    typedef typename Tr::vec_t vec_t;
-    constexpr int VEC = Tr::VEC;
-    constexpr int TPC = GT / VEC;       // threads per staged column
-    constexpr int CPP = 256 / TPC;      // columns per pass
-    constexpr int PASSES = BK / CPP;
 
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    T* sA = reinterpret_cast<T*>(smem_raw);            // [2][BK][SROW]
-    T* sB = sA + 2 * BK * SROW;                          // [2][BK][SROW]
+    T* sA = reinterpret_cast<T*>(smem_raw);            // [2][BK][SR]
+    T* sB = sA + 2 * BK * SR;                            // [2][BK][SR]
 
     // ---- tile coordinates ---------------------------------------------------------------
     int64_t ti, tj;
@@ -337,7 +344,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(T* __restrict__ C, int6
             tj = b / ntm;
         }
     }
-    const int64_t i0 = ti * GT, j0 = tj * GT;
+    const int64_t i0 = ti * TM, j0 = tj * TM;
     // KSKIP: both operands are zero left of column i0 (C = V V^T with V upper triangular)
     const int64_t kbeg = KSKIP ? i0 : 0;
     const T* Ablk = A + i0 + kbeg * lda;
@@ -357,26 +364,30 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(T* __restrict__ C, int6
 #pragma unroll
         for (int p = 0; p < PASSES; p++) {
             const int64_t kk = k0 + st_col + p * CPP;
-            ra[p] = *reinterpret_cast<const vec_t*>(Ablk + st_row + kk * lda);
-            rb[p] = *reinterpret_cast<const vec_t*>(Bblk + st_row + kk * ldb);
+            if (st_col + p * CPP < BK) {
+                ra[p] = *reinterpret_cast<const vec_t*>(Ablk + st_row + kk * lda);
+                rb[p] = *reinterpret_cast<const vec_t*>(Bblk + st_row + kk * ldb);
+            }
         }
     };
     auto lstore = [&](int buf) {
-        T* a = sA + buf * BK * SROW;
-        T* bb = sB + buf * BK * SROW;
+        T* a = sA + buf * BK * SR;
+        T* bb = sB + buf * BK * SR;
 #pragma unroll
         for (int p = 0; p < PASSES; p++) {
             const int kk = st_col + p * CPP;
-            *reinterpret_cast<vec_t*>(a + kk * SROW + st_row) = ra[p];
-            *reinterpret_cast<vec_t*>(bb + kk * SROW + st_row) = rb[p];
+            if (kk < BK) {
+                *reinterpret_cast<vec_t*>(a + kk * SR + st_row) = ra[p];
+                *reinterpret_cast<vec_t*>(bb + kk * SR + st_row) = rb[p];
+            }
         }
     };
 
-    acc_t acc[4][4];
+    acc_t acc[NB][NB];
 #pragma unroll
-    for (int x = 0; x < 4; x++)
+    for (int x = 0; x < NB; x++)
 #pragma unroll
-        for (int y = 0; y < 4; y++) acc[x][y] = acc_t{0};
+        for (int y = 0; y < NB; y++) acc[x][y] = acc_t{0};
 
     const int nstage = (int)((K - kbeg) / BK);
     gload(0);
@@ -385,20 +396,20 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(T* __restrict__ C, int6
     for (int sidx = 0; sidx < nstage; sidx++) {
         const int buf = sidx & 1;
         if (sidx + 1 < nstage) gload((int64_t)(sidx + 1) * BK);
-        const T* a = sA + buf * BK * SROW;
-        const T* bb = sB + buf * BK * SROW;
+        const T* a = sA + buf * BK * SR;
+        const T* bb = sB + buf * BK * SR;
 #pragma unroll
         for (int kq = 0; kq < BK / 4; kq++) {
             const int kr = kq * 4 + lk;
-            T fa[4], fb[4];
+            T fa[NB], fb[NB];
 #pragma unroll
-            for (int x = 0; x < 4; x++) fb[x] = bb[kr * SROW + wc * 64 + x * 16 + lr];  // MFMA A: our columns
+            for (int x = 0; x < NB; x++) fb[x] = bb[kr * SR + wc * WT + x * 16 + lr];  // MFMA A: our columns
 #pragma unroll
-            for (int y = 0; y < 4; y++) fa[y] = a[kr * SROW + wr * 64 + y * 16 + lr];   // MFMA B: our rows
+            for (int y = 0; y < NB; y++) fa[y] = a[kr * SR + wr * WT + y * 16 + lr];   // MFMA B: our rows
 #pragma unroll
-            for (int x = 0; x < 4; x++)
+            for (int x = 0; x < NB; x++)
 #pragma unroll
-                for (int y = 0; y < 4; y++) acc[x][y] = Tr::mma(fb[x], fa[y], acc[x][y]);
+                for (int y = 0; y < NB; y++) acc[x][y] = Tr::mma(fb[x], fa[y], acc[x][y]);
         }
         if (sidx + 1 < nstage) lstore(buf ^ 1);
         __syncthreads();
@@ -407,14 +418,14 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(T* __restrict__ C, int6
     // ---- epilogue: acc[x][y][reg] = C(i = ... y*16 + lr, j = ... x*16 + orow(lk, reg)) ----
     const bool diag_tile = LOWER && (ti == tj);
 #pragma unroll
-    for (int x = 0; x < 4; x++) {
+    for (int x = 0; x < NB; x++) {
 #pragma unroll
         for (int reg = 0; reg < 4; reg++) {
-            const int jl = wc * 64 + x * 16 + Tr::orow(lk, reg);
+            const int jl = wc * WT + x * 16 + Tr::orow(lk, reg);
             T* ccol = C + (j0 + jl) * ldc + i0;
 #pragma unroll
-            for (int y = 0; y < 4; y++) {
-                const int il = wr * 64 + y * 16 + lr;
+            for (int y = 0; y < NB; y++) {
+                const int il = wr * WT + y * 16 + lr;
                 if (diag_tile && il < jl) continue;
                 T v = alpha * acc[x][y][reg];
                 if (BETA) v = fma(beta, ccol[il], v);
@@ -424,38 +435,28 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(T* __restrict__ C, int6
     }
 }
 
-template <typename T>
+template <typename T, int TM = 128>
 static size_t gemm_lds_bytes() {
-    return sizeof(T) * 4 * BK * SROW;
+    return sizeof(T) * 4 * BK * (TM + PADT);
 }
 
-template <typename T>
-void launch_gemm_nt(T* C, int64_t ldc, const T* A, int64_t lda, const T* B, int64_t ldb, int64_t M, int64_t N,
-                    int64_t K, T alpha, T beta, bool lower, hipStream_t s) {
-    if (M <= 0 || N <= 0) return;
-    const int64_t ntm = M / GT, ntn = N / GT;
-    int64_t ntiles;
-    if (lower) {
-        // rows beyond the square part are full tile rows
-        ntiles = ntn * (ntn + 1) / 2 + (ntm - ntn) * ntn;
-    } else {
-        ntiles = ntm * ntn;
-    }
-    const size_t lds = gemm_lds_bytes<T>();
+template <typename T, int TM>
+static void gemm_launch(T* C, int64_t ldc, const T* A, int64_t lda, const T* B, int64_t ldb, int64_t M, int64_t N,
+                        int64_t K, T alpha, T beta, bool lower, hipStream_t s) {
+    const int64_t ntm = M / TM, ntn = N / TM;
+    const int64_t ntiles = lower ? ntn * (ntn + 1) / 2 + (ntm - ntn) * ntn : ntm * ntn;
+    const size_t lds = gemm_lds_bytes<T, TM>();
     const bool use_beta = beta != T(0);
-    const double elems = lower ? ((double)N * (N + 1) / 2 + (double)(M - N) * N) : (double)M * N;
-    ProfScope ps(lower ? KC_UPDATE : (use_beta ? KC_OTHER : KC_TRSM), s, 2.0 * elems * K,
-                 (double)sizeof(T) * (elems * (use_beta ? 2 : 1) + (double)(M + N) * K));
 #define GPRX_GEMM(L, Bt)                                                                                  \
     do {                                                                                                  \
         static bool attr_done = false;                                                                    \
         if (!attr_done) {                                                                                 \
-            hipFuncSetAttribute((const void*)gemm_nt_kernel<T, L, Bt, false>,                             \
+            hipFuncSetAttribute((const void*)gemm_nt_kernel<T, L, Bt, false, TM>,                         \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                    \
             attr_done = true;                                                                             \
         }                                                                                                 \
-        hipLaunchKernelGGL((gemm_nt_kernel<T, L, Bt, false>), dim3((unsigned)ntiles), dim3(256), lds, s, C, ldc, A, \
-                           lda, B, ldb, K, alpha, beta, ntm, ntn);                                        \
+        hipLaunchKernelGGL((gemm_nt_kernel<T, L, Bt, false, TM>), dim3((unsigned)ntiles), dim3(256), lds, s, C, ldc, \
+                           A, lda, B, ldb, K, alpha, beta, ntm, ntn, (int64_t)0);                         \
     } while (0)
     if (lower) {
         if (use_beta) GPRX_GEMM(true, true);
@@ -467,6 +468,28 @@ void launch_gemm_nt(T* C, int64_t ldc, const T* A, int64_t lda, const T* B, int6
 #undef GPRX_GEMM
 }
 
+// Tile choice: 128x128 tiles when they give at least two workgroups per CU (bulk updates),
+// 64x64 tiles otherwise (the latency-bound launches of the panel chain).
+template <typename T>
+void launch_gemm_nt(T* C, int64_t ldc, const T* A, int64_t lda, const T* B, int64_t ldb, int64_t M, int64_t N,
+                    int64_t K, T alpha, T beta, bool lower, hipStream_t s) {
+    if (M <= 0 || N <= 0) return;
+    const bool use_beta = beta != T(0);
+    const double elems = lower ? ((double)N * (N + 1) / 2 + (double)(M - N) * N) : (double)M * N;
+    ProfScope ps(lower ? KC_UPDATE : (use_beta ? KC_OTHER : KC_TRSM), s, 2.0 * elems * K,
+                 (double)sizeof(T) * (elems * (use_beta ? 2 : 1) + (double)(M + N) * K));
+    static const int64_t small_tiles = [] {
+        const char* e = std::getenv("GPRX_SMALL_TILE_WG");
+        return e ? (int64_t)std::atoll(e) : (int64_t)1024;
+    }();
+    const int64_t ntm = M / GT, ntn = N / GT;
+    const int64_t nt128 = lower ? ntn * (ntn + 1) / 2 + (ntm - ntn) * ntn : ntm * ntn;
+    if (nt128 < small_tiles)
+        gemm_launch<T, 64>(C, ldc, A, lda, B, ldb, M, N, K, alpha, beta, lower, s);
+    else
+        gemm_launch<T, 128>(C, ldc, A, lda, B, ldb, M, N, K, alpha, beta, lower, s);
+}
+
 // Split-K form: P partial products, partial p = A[:, pK:(p+1)K] B[:, pK:(p+1)K]^T accumulated
 // (beta = 1) into C + p*cstride, all in one launch (grid.y = P); K is the slice depth.
 template <typename T>
@@ -475,7 +498,7 @@ void launch_gemm_nt_splitk(T* C, int64_t ldc, int64_t cstride, const T* A, int64
     if (M <= 0 || N <= 0 || K <= 0) return;
     const int64_t ntm = M / GT, ntn = N / GT;
     const int64_t ntiles = lower ? ntn * (ntn + 1) / 2 + (ntm - ntn) * ntn : ntm * ntn;
-    const size_t lds = gemm_lds_bytes<T>();
+    const size_t lds = gemm_lds_bytes<T, 128>();
     const double elems = lower ? ((double)N * (N + 1) / 2 + (double)(M - N) * N) : (double)M * N;
     ProfScope ps(KC_OTHER, s, 2.0 * elems * K * P, (double)sizeof(T) * (2 * elems * P + (double)(M + N) * K * P));
 #define GPRX_GEMM_SK(L)                                                                                      \
@@ -501,7 +524,7 @@ void launch_gemm_nt_kskip(T* C, int64_t ldc, const T* A, int64_t lda, const T* B
     if (M <= 0 || N <= 0) return;
     const int64_t ntm = M / GT, ntn = N / GT;
     const int64_t ntiles = ntn * (ntn + 1) / 2 + (ntm - ntn) * ntn;
-    const size_t lds = gemm_lds_bytes<T>();
+    const size_t lds = gemm_lds_bytes<T, 128>();
     ProfScope ps(KC_INVERSE, s, 2.0 * (double)N * N * N / 6.0, 0.0);
     static bool attr_done = false;
     if (!attr_done) {
@@ -567,9 +590,11 @@ Exec::~Exec() {
 // Factor the (already fully updated) column panel [c0, c0+w) over rows c0..nrows: per
 // 128-block the diagonal kernel, the trsm of every row below (GEMM with Linv) and the update
 // of the panel's remaining columns.  `skip` is the timing-experiment mask (see below).
+// inner_wait (may be null): event the first in-panel update waits for (the look-ahead
+// update of the panel's later columns running on another stream).
 template <typename T>
 static void potrf_panel(T* A, int64_t ld, int64_t nrows, int64_t c0, int64_t w, T* Linv, int* info, hipStream_t P,
-                        int skip) {
+                        int skip, hipEvent_t inner_wait = nullptr) {
     for (int64_t kk = c0; kk < c0 + w; kk += DB) {
         T* Lk = Linv + (kk / DB) * (int64_t)DB * DB;
         if (!(skip & 2)) launch_diag<T>(A + kk + kk * ld, ld, Lk, info, kk, P);
@@ -578,16 +603,26 @@ static void potrf_panel(T* A, int64_t ld, int64_t nrows, int64_t c0, int64_t w, 
         T* Pk = A + (kk + DB) + kk * ld;
         launch_gemm_nt<T>(Pk, ld, Pk, ld, Lk, DB, rows_below, DB, DB, T(1), T(0), false, P);
         const int64_t inner = c0 + w - (kk + DB);
+        if (kk == c0 && inner_wait) GPRX_HIP(hipStreamWaitEvent(P, inner_wait, 0));
         if (inner > 0)
             launch_gemm_nt<T>(A + (kk + DB) + (kk + DB) * ld, ld, Pk, ld, Pk, ld, rows_below, inner, DB, T(-1), T(1),
                               true, P);
     }
 }
 
+// Two-level right-looking Cholesky with look-ahead.
+//   Panel(K)      columns [c0, c0+w) of every row below: per 128-block diag + trsm + the
+//                 update of the remaining panel columns (stream P = ex.s0)
+//   TrailNext(K)  next panel's columns -= P_K P_K^T: its first 128 columns on P (so the next
+//                 diagonal kernel can start), the other columns on stream Q = ex.s2; the
+//                 next panel's first in-panel update waits for Q
+//   TrailRest(K)  the rest of the trailing matrix     (stream B = ex.s1, K = w deep)
+// Panel(K+1) runs on P while TrailRest(K) runs on B.  TrailNext(K) waits for TrailRest(K-1)
+// (both accumulate into the next panel's columns).
 template <typename T>
 void potrf_blocked(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info, Exec& ex) {
     const int64_t NBO = outer_block();
-    hipStream_t P = ex.s0, B = ex.s1 ? ex.s1 : ex.s0;
+    hipStream_t P = ex.s0, B = ex.s1 ? ex.s1 : ex.s0, Q = ex.s2 ? ex.s2 : ex.s0;
     // timing experiments only (results are wrong): 1 = no TrailRest, 2 = no diagonal kernel,
     // 4 = no panel trsm / inner update
     static const int skip = [] {
@@ -595,29 +630,45 @@ void potrf_blocked(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* in
         return e ? std::atoi(e) : 0;
     }();
     const int64_t nK = (np + NBO - 1) / NBO;
-    auto panel = [&](int64_t c0, int64_t w) { potrf_panel<T>(A, ld, nrows, c0, w, Linv, info, P, skip); };
+    // events: 4K panel(K) done, 4K+1 TrailRest(K) done, 4K+2 TrailNext-b(K) done,
+    // 4K+3 TrailNext may start (TrailRest(K-1) done)
+    hipEvent_t tnb_prev = nullptr;
     for (int64_t K = 0; K < nK; K++) {
         const int64_t c0 = K * NBO, w = std::min(NBO, np - c0);
-        if (K >= 2 && B != P) GPRX_HIP(hipStreamWaitEvent(P, ex.event(2 * (K - 2) + 1), 0));
-        panel(c0, w);
+        potrf_panel<T>(A, ld, nrows, c0, w, Linv, info, P, skip, tnb_prev);
+        tnb_prev = nullptr;
         if (K == nK - 1) break;
         const int64_t c1 = c0 + w, wn = std::min(NBO, np - c1);
         const T* Pan = A + c0 * ld;  // column c0; row offsets added below
         if (B != P) {
-            GPRX_HIP(hipEventRecord(ex.event(2 * K), P));
-            if (K >= 1) GPRX_HIP(hipStreamWaitEvent(P, ex.event(2 * (K - 1) + 1), 0));
+            GPRX_HIP(hipEventRecord(ex.event(4 * K), P));
+            if (K >= 1) GPRX_HIP(hipStreamWaitEvent(P, ex.event(4 * (K - 1) + 1), 0));
         }
-        // TrailNext(K)
-        launch_gemm_nt<T>(A + c1 + c1 * ld, ld, Pan + c1, ld, Pan + c1, ld, nrows - c1, wn, w, T(-1), T(1), true, P);
+        // TrailNext(K): first 128 columns on P, the rest on Q
+        const int64_t wa = (Q != P) ? std::min<int64_t>(DB, wn) : wn;
+        launch_gemm_nt<T>(A + c1 + c1 * ld, ld, Pan + c1, ld, Pan + c1, ld, nrows - c1, wa, w, T(-1), T(1), true, P);
+        if (wn > wa) {
+            const int64_t cb = c1 + wa;
+            GPRX_HIP(hipEventRecord(ex.event(4 * K + 3), P));
+            GPRX_HIP(hipStreamWaitEvent(Q, ex.event(4 * K + 3), 0));
+            launch_gemm_nt<T>(A + cb + cb * ld, ld, Pan + cb, ld, Pan + cb, ld, nrows - cb, wn - wa, w, T(-1), T(1),
+                              true, Q);
+            GPRX_HIP(hipEventRecord(ex.event(4 * K + 2), Q));
+            tnb_prev = ex.event(4 * K + 2);
+        }
         // TrailRest(K)
         const int64_t c2 = c1 + wn;
-        if (B != P) GPRX_HIP(hipStreamWaitEvent(B, ex.event(2 * K), 0));
+        if (B != P) GPRX_HIP(hipStreamWaitEvent(B, ex.event(4 * K), 0));
         if (c2 < np && !(skip & 1))
             launch_gemm_nt<T>(A + c2 + c2 * ld, ld, Pan + c2, ld, Pan + c2, ld, nrows - c2, np - c2, w, T(-1), T(1),
                               true, B);
-        if (B != P) GPRX_HIP(hipEventRecord(ex.event(2 * K + 1), B));
+        if (B != P) GPRX_HIP(hipEventRecord(ex.event(4 * K + 1), B));
     }
-    if (B != P && nK >= 2) GPRX_HIP(hipStreamWaitEvent(P, ex.event(2 * (nK - 2) + 1), 0));
+    if (B != P && nK >= 2) GPRX_HIP(hipStreamWaitEvent(P, ex.event(4 * (nK - 2) + 1), 0));
+    if (Q != P) {  // everything issued on Q is done before the caller's next work on P
+        GPRX_HIP(hipEventRecord(ex.event(4 * nK), Q));
+        GPRX_HIP(hipStreamWaitEvent(P, ex.event(4 * nK), 0));
+    }
 }
 
 // ======================================================================================
