@@ -122,6 +122,40 @@ static gprx_status bench_impl(int what, int64_t M, int64_t N, int64_t K, int ite
                 if (it > 0) total += tms;
             }
             *ms = total / iters;
+        } else if (what == 7 || what == 8) {  // the same sequences replayed from a captured hipGraph
+            const int64_t n = M;
+            T* A = (T*)alloc(sizeof(T) * n * n);
+            T* Li = (T*)alloc(sizeof(T) * n * DB);
+            T* z = (T*)alloc(sizeof(T) * n);
+            T* al = (T*)alloc(sizeof(T) * n);
+            hipLaunchKernelGGL(dev_fill_spd<T>, dim3((unsigned)((n * n + 255) / 256)), dim3(256), 0, s, A, n, n,
+                               (uint64_t)0);
+            if (what == 8) potrf_blocked<T>(A, n, n, n, Li, info, ex);
+            (void)hipStreamSynchronize(s);
+            hipGraph_t g = nullptr;
+            hipGraphExec_t ge = nullptr;
+            GPRX_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
+            if (what == 8) launch_backsolve<T>(A, n, n - DB, 1, Li, z, al, s);
+            else potrf_blocked<T>(A, n, n, n, Li, info, ex);
+            GPRX_HIP(hipStreamEndCapture(s, &g));
+            GPRX_HIP(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+            double total = 0;
+            for (int it = 0; it < iters + 1; it++) {
+                if (what == 7) {
+                    hipLaunchKernelGGL(dev_fill_spd<T>, dim3((unsigned)((n * n + 255) / 256)), dim3(256), 0, s, A, n, n,
+                                       (uint64_t)it);
+                    (void)hipMemsetD32Async((hipDeviceptr_t)info, INT_MAX, 1, s);
+                }
+                (void)hipEventRecord(e0, s);
+                GPRX_HIP(hipGraphLaunch(ge, s));
+                (void)hipEventRecord(e1, s);
+                (void)hipEventSynchronize(e1);
+                (void)hipEventElapsedTime(&tms, e0, e1);
+                if (it > 0) total += tms;
+            }
+            *ms = total / iters;
+            (void)hipGraphExecDestroy(ge);
+            (void)hipGraphDestroy(g);
         } else {
             throw Error{GPRX_ERR_ARG, "dev bench: unknown case"};
         }

@@ -44,6 +44,11 @@ if cases in ("all", "gemm"):
         ms = run(F32, 2 if low else 1, M, N, K, iters=5)
         fl = 2.0 * K * ((N * (N + 1) / 2 + (M - N) * N) if low else M * N)
         res[f"gemm_f32_{M}x{N}x{K}{'_low' if low else ''}"] = {"ms": ms, "tflops": fl / ms / 1e9}
+if cases in ("all", "graph"):
+    for n in (4096, 16384):
+        res[f"potrf_graph_f64_{n}_ms"] = run(F64, 7, n, iters=3)
+    res["backsolve_graph_f64_16384_ms"] = run(F64, 8, 16384, iters=5)
+
 if cases in ("all", "potrf"):
     for n in (4096, 16384):
         for what, name in ((3, "single"), (4, "lookahead")):
