@@ -191,6 +191,11 @@ static int64_t round_up(int64_t x, int64_t g) { return (x + g - 1) / g * g; }
 
 using namespace gprx;
 
+// info < 0: the device scheduler of potrf_tiles timed out waiting for a dependency
+static void check_sched(int hinfo) {
+    if (hinfo < 0) throw Error{GPRX_ERR_HIP, "gprx: device factorisation scheduler timed out (tile dependency wait)"};
+}
+
 struct gprx_ctx {
     int device = 0;
     int rank = 0, world = 1;
@@ -352,7 +357,7 @@ static gprx_status model_fit(gprx_model* M, uint32_t flags, gprx_fit_info* out) 
             if (r != ncclSuccess) throw Error{GPRX_ERR_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(r)};
         }
     } else {
-        potrf_blocked<T>(M->A.as<T>(), ld, np, ld, M->Linv.as<T>(), M->info.as<int>(), ctx->ex);
+        potrf_auto<T>(M->A.as<T>(), ld, np, ld, M->Linv.as<T>(), M->info.as<int>(), ctx->ex);
     }
     GPRX_HIP(hipEventRecord(ctx->ev[2], s));
     launch_fit_reductions<T>(M->A.as<T>(), ld, n, np, M->m, M->red.as<double>(), s);
@@ -384,6 +389,7 @@ static gprx_status model_fit(gprx_model* M, uint32_t flags, gprx_fit_info* out) 
     if (hflag)
         throw Error{GPRX_ERR_NONFINITE,
                     "GaussianProcess::ComputeKernelMatrixInternal: kernel matrix contains entries which are not finite."};
+    check_sched(hinfo);
     if (hinfo != INT_MAX)
         throw Error{GPRX_ERR_NOT_SPD, "gprx: kernel matrix is not positive definite (Cholesky pivot " +
                                           std::to_string(hinfo) + " <= 0)"};
@@ -638,9 +644,10 @@ static gprx_status cholesky_impl(gprx_ctx* ctx, void* Ahost, int64_t n, int32_t*
     GPRX_HIP(hipMemcpy2D(dA.p, sizeof(T) * np, Ahost, sizeof(T) * n, sizeof(T) * n, n, hipMemcpyHostToDevice));
     launch_set_identity_pad<T>(dA.as<T>(), np, n, np, s);
     GPRX_HIP(hipMemsetD32Async((hipDeviceptr_t)dinfo.p, INT_MAX, 1, s));
-    potrf_blocked<T>(dA.as<T>(), np, np, np, dLinv.as<T>(), dinfo.as<int>(), ctx->ex);
+    potrf_auto<T>(dA.as<T>(), np, np, np, dLinv.as<T>(), dinfo.as<int>(), ctx->ex);
     int hinfo = 0;
     download(&hinfo, dinfo.p, sizeof(int), s);
+    check_sched(hinfo);
     hinfo = (hinfo == INT_MAX) ? 0 : hinfo;
     if (info) *info = hinfo;
     std::vector<T> h((size_t)n * n);
@@ -781,9 +788,10 @@ static gprx_status sparse_fit_impl(gprx_ctx* ctx, const gprx_kernel_desc* desc, 
     // ---- S = L L^T with b in the extra rows -> RV; S^{-1} -> RM -----------------------------
     dLinv.ensure(sizeof(T) * Mp * DB);
     GPRX_HIP(hipMemsetD32Async((hipDeviceptr_t)dinfo.p, INT_MAX, 1, s));
-    potrf_blocked<T>(dS.as<T>(), ld, Mp, ld, dLinv.as<T>(), dinfo.as<int>(), ctx->ex);
+    potrf_auto<T>(dS.as<T>(), ld, Mp, ld, dLinv.as<T>(), dinfo.as<int>(), ctx->ex);
     int hinfo = 0;
     download(&hinfo, dinfo.p, sizeof(int), s);
+    check_sched(hinfo);
     if (hinfo != INT_MAX)
         throw Error{GPRX_ERR_NOT_SPD, "gprx_sparse_fit: K + sigma^-2 Knm^T Knm is not positive definite (pivot " +
                                           std::to_string(hinfo) + ")"};
@@ -803,9 +811,10 @@ static gprx_status sparse_fit_impl(gprx_ctx* ctx, const gprx_kernel_desc* desc, 
     if (Kinv) {
         dLinvK.ensure(sizeof(T) * Mp * DB);
         GPRX_HIP(hipMemsetD32Async((hipDeviceptr_t)dinfo.p, INT_MAX, 1, s));
-        potrf_blocked<T>(dK.as<T>(), Mp, Mp, Mp, dLinvK.as<T>(), dinfo.as<int>(), ctx->ex);
+        potrf_auto<T>(dK.as<T>(), Mp, Mp, Mp, dLinvK.as<T>(), dinfo.as<int>(), ctx->ex);
         download(&hinfo, dinfo.p, sizeof(int), s);
-        if (hinfo != INT_MAX)
+        check_sched(hinfo);
+    if (hinfo != INT_MAX)
             throw Error{GPRX_ERR_NOT_SPD, "gprx_sparse_fit: Kmm + jitter I is not positive definite (pivot " +
                                               std::to_string(hinfo) + ")"};
         launch_spd_inverse_from_factor<T>(dK.as<T>(), Mp, Mp, dLinvK.as<T>(), dV.as<T>(), dC.as<T>(), s);

@@ -97,7 +97,7 @@ static gprx_status bench_impl(int what, int64_t M, int64_t N, int64_t K, int ite
             (void)hipEventSynchronize(e1);
             (void)hipEventElapsedTime(&tms, e0, e1);
             *ms = tms / iters;
-        } else if (what == 3 || what == 4 || what == 5) {
+        } else if (what == 3 || what == 4 || what == 5 || what == 9) {
             const int64_t n = M;
             T* A = (T*)alloc(sizeof(T) * n * n);
             T* Li = (T*)alloc(sizeof(T) * n * DB);
@@ -115,6 +115,7 @@ static gprx_status bench_impl(int what, int64_t M, int64_t N, int64_t K, int ite
                 if (what == 5) potrf_blocked<T>(A, n, n, n, Li, info, use);
                 (void)hipEventRecord(e0, s);
                 if (what == 5) launch_backsolve<T>(A, n, n - DB, 1, Li, z, al, s);
+                else if (what == 9) potrf_tiles<T>(A, n, n, n, Li, info, ex);
                 else potrf_blocked<T>(A, n, n, n, Li, info, use);
                 (void)hipEventRecord(e1, s);
                 (void)hipEventSynchronize(e1);
@@ -170,6 +171,22 @@ static gprx_status bench_impl(int what, int64_t M, int64_t N, int64_t K, int ite
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     return GPRX_OK;
+}
+
+namespace gprx {
+int pt_debug_snapshot(int* out, int max_wg);
+}
+extern "C" int32_t gprx_dev_pt_debug(int32_t* out, int32_t max_wg) { return gprx::pt_debug_snapshot(out, max_wg); }
+
+extern "C" gprx_status gprx_dev_schedule(int32_t nc, int32_t nr, int32_t P, double* est_us, int64_t* ntasks) {
+    try {
+        const int64_t n = potrf_tiles_schedule_stats(nc, nr, P, est_us);
+        if (ntasks) *ntasks = n;
+        return GPRX_OK;
+    } catch (const Error& e) {
+        std::fprintf(stderr, "gprx_dev_schedule: %s\n", e.msg.c_str());
+        return e.st;
+    }
 }
 
 namespace gprx {

@@ -298,17 +298,28 @@ void launch_label_rows(const T* Y, int64_t n, int m, T* A, int64_t ld, int64_t r
 // are extra rows solved along: they end up holding (L^{-1} B)^T).  Linv receives the
 // inverses of the np/DB diagonal blocks (DB x DB each, column-major).  info: device int,
 // first failing column (1-based) via atomicMin semantics (initialised to INT_MAX).
+struct PtState;             // tile-dataflow potrf: cached schedules + counters (k_ptiles.hip)
+void pt_state_free(PtState* p);
 struct Exec {
     hipStream_t s0 = nullptr;  // main stream (panel chain)
     hipStream_t s1 = nullptr;  // look-ahead stream (bulk trailing updates); may be null
     hipStream_t s2 = nullptr;  // second look-ahead stream (next panel's later columns); may be null
     std::vector<hipEvent_t> ev;
+    PtState* pt = nullptr;
     hipEvent_t event(size_t i);
     ~Exec();
 };
 int outer_block();
 template <typename T>
 void potrf_blocked(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info, Exec& ex);
+// Same contract, one persistent launch: 128x128 tile tasks scheduled on the device by
+// dependency counters (k_ptiles.hip).  A timed-out dependency wait sets *info = -1.
+template <typename T>
+void potrf_tiles(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info, Exec& ex);
+// Factorisation used by the fit paths: potrf_tiles unless GPRX_POTRF=streams.
+template <typename T>
+void potrf_auto(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info, Exec& ex);
+int64_t potrf_tiles_schedule_stats(int nc, int nr, int P, double* est_us);
 // Multi-GPU form: column panels of outer_block() columns dealt cyclically over `world`
 // ranks (np must be a multiple of outer_block()); the factored panels are RCCL-broadcast so
 // every rank ends with the full factor.  pack: device scratch of nrows * outer_block().

@@ -579,6 +579,17 @@ hipEvent_t Exec::event(size_t i) {
 
 Exec::~Exec() {
     for (auto e : ev) (void)hipEventDestroy(e);
+    pt_state_free(pt);
+}
+
+template <typename T>
+void potrf_auto(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info, Exec& ex) {
+    static const bool streams = [] {
+        const char* e = std::getenv("GPRX_POTRF");
+        return e && std::string(e) == "streams";
+    }();
+    if (streams) potrf_blocked<T>(A, ld, np, nrows, Linv, info, ex);
+    else potrf_tiles<T>(A, ld, np, nrows, Linv, info, ex);
 }
 
 // Two-level right-looking Cholesky with look-ahead.
@@ -868,6 +879,7 @@ void launch_fit_reductions(const T* A, int64_t ld, int64_t n, int64_t np, int m,
 
 #define GPRX_INST(T)                                                                                      \
     template void potrf_blocked<T>(T*, int64_t, int64_t, int64_t, T*, int*, Exec&);                      \
+    template void potrf_auto<T>(T*, int64_t, int64_t, int64_t, T*, int*, Exec&);                         \
     template void potrf_dist<T>(T*, int64_t, int64_t, int64_t, T*, int*, Exec&, ncclComm_t, int, int, T*);   \
     template void launch_gemm_nt_splitk<T>(T*, int64_t, int64_t, const T*, int64_t, const T*, int64_t,   \
                                            int64_t, int64_t, int64_t, int, T, bool, hipStream_t);         \

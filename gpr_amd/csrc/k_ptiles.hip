@@ -1,0 +1,851 @@
+// k_ptiles.hip — tile-dataflow Cholesky in ONE persistent launch (gfx950).
+//
+// Replaces the same reference step as potrf_blocked (lapack::lu_invert -> dgetrf_+dgetri_,
+// include/LAPACKUtils.h:38-56, 85-97, called from GaussianProcess::InvertKernelMatrix,
+// lib/GaussianProcess.cpp:545-559) with K + sigma^2 I = L L^T, the forward solve z = L^{-1} Y
+// riding along as extra row blocks, exactly as k_potrf.hip does -- but scheduled on the device.
+//
+// Why: in the stream formulation every step of the panel chain (diagonal factor -> trsm ->
+// next-column update) is a kernel that must wait for CU slots held by the bulk trailing
+// GEMM, so at N = 16384 the chain (18 ms alone) stretches to most of the 37 ms
+// factorisation.  Here one workgroup per CU runs a loop over a ticket list of 128x128 TILE
+// TASKS with per-tile dependency counters in HBM:
+//
+//   DIAGX(k)        T = A_{k,k-1} Linv_{k-1}^T (the trsm of the critical tile),
+//                   A_kk -= T T^T, then factor A_kk = L_kk L_kk^T and form Linv_k
+//                   (one task = the whole critical step, no hand-off inside it)
+//   TRSM(i,k)       L_ik = A_ik Linv_k^T                  (i >= k+2, and the label rows)
+//   UPD(i,j,b0,nb)  A_ij -= sum_{b0<=b<b0+nb} L_ib L_jb^T  (nb = W for far-behind panels)
+//
+// Counters: ver[i][j] = number of b already applied to tile (i,j); lcnt[i] = number of
+// final blocks L_i0..L_i,lcnt-1 of row block i.  Wait conditions:
+//   DIAGX(k):  ver[k][k-1] == k-1, ver[k][k] == k-1, lcnt[k-1] >= k
+//   TRSM(i,k): ver[i][k] == k, lcnt[k] >= k+1
+//   UPD:       ver[i][j] == b0, lcnt[i] >= b0+nb, lcnt[j] >= b0+nb
+// The ticket order is a list schedule computed on the host (critical-path priorities,
+// simulated on P workers): every task's producers hold earlier tickets, and a workgroup that
+// holds a ticket is running, so the smallest unfinished ticket can always proceed -- no
+// deadlock whatever the real durations.  Every wait is also bounded in wall-clock time: a
+// timeout raises an error flag that drains every workgroup and is reported as info = -1.
+//
+// Hand-offs follow the gfx950 inter-workgroup recipe (MI355X_MICROARCH.md, "Workgroup
+// dispatch ... visibility"): producer stores -> s_waitcnt vmcnt(0) in every wave ->
+// barrier -> one lane: agent release fence, s_waitcnt vmcnt(0), relaxed agent-scope counter
+// store; consumer: one lane polls with relaxed agent loads, agent acquire fence,
+// s_waitcnt vmcnt(0), barrier, then plain loads.
+//
+// Tile GEMM: 512 threads = 8 waves of 64x32 (v_mfma_f64_16x16x4f64 / _f32_16x16x4f32),
+// operands staged 32-deep through LDS, double-buffered; 147 KB of LDS per workgroup also
+// keeps the launch at one workgroup per CU, so the critical DIAGX step has a whole CU.
+#include "gprx_internal.h"
+
+#include <algorithm>
+#include <climits>
+#include <cstring>
+#include <cstdlib>
+#include <functional>
+#include <map>
+#include <mutex>
+#include <queue>
+
+namespace gprx {
+
+namespace pt {
+
+constexpr int NT = 512;     // threads per workgroup
+constexpr int BK = 32;      // k depth per LDS stage
+constexpr int PAD = 16;     // LDS row pad (elements)
+constexpr int SR = GT + PAD;
+
+enum { T_DIAGX = 0, T_TRSM = 1, T_UPD = 2 };
+enum { C_TICKET = 0, C_ERR = 1, C_NCTL = 16 };  // control words at the head of the counter block
+
+typedef double d4_t __attribute__((ext_vector_type(4)));
+typedef float f4_t __attribute__((ext_vector_type(4)));
+typedef double d2_t __attribute__((ext_vector_type(2)));
+
+template <typename T>
+struct Mfma;
+template <>
+struct Mfma<double> {
+    typedef d4_t acc_t;
+    typedef d2_t vec_t;
+    static constexpr int VEC = 2;
+    __device__ static inline acc_t mma(double a, double b, acc_t c) {
+        return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+    }
+    __device__ static inline int orow(int lk, int reg) { return lk + 4 * reg; }
+};
+template <>
+struct Mfma<float> {
+    typedef f4_t acc_t;
+    typedef f4_t vec_t;
+    static constexpr int VEC = 4;
+    __device__ static inline acc_t mma(float a, float b, acc_t c) {
+        return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+    }
+    __device__ static inline int orow(int lk, int reg) { return 4 * lk + reg; }
+};
+
+template <typename T>
+constexpr size_t gemm_lds() {
+    return sizeof(T) * 2 * 2 * BK * SR;
+}
+
+// ------------------------------------------------------------------------------------------
+// One 128x128 tile:  C = A B^T (UPDATE = false)  or  C -= A B^T (UPDATE = true), K deep.
+// A: 128 rows x K (column-major, lda), B: 128 rows x K (ldb).  lower: diagonal tile, only
+// row >= col is stored and the waves wholly above the diagonal skip their MFMAs.
+// Wave w: rows 64*(w&1).., columns 32*(w>>1)..; acc[x][y][reg] = C(i = 64wr + 16y + lr,
+// j = 32wc + 16x + orow(lk, reg)).
+// ------------------------------------------------------------------------------------------
+template <typename T, bool UPDATE>
+__device__ __forceinline__ void tile_gemm(T* __restrict__ C, int64_t ldc, const T* __restrict__ A, int64_t lda,
+                                          const T* __restrict__ B, int64_t ldb, int K, bool lower, T* smem,
+                                          const int t) {
+    typedef Mfma<T> Tr;
+    typedef typename Tr::acc_t acc_t;
+    typedef typename Tr::vec_t vec_t;
+    constexpr int VEC = Tr::VEC;
+    constexpr int TPC = GT / VEC;       // threads per staged column
+    constexpr int CPP = NT / TPC;       // columns per pass
+    constexpr int PASSES = BK / CPP;
+    static_assert(BK % CPP == 0, "staging");
+
+    T* sA = smem;                  // [2][BK][SR]
+    T* sB = smem + 2 * BK * SR;    // [2][BK][SR]
+    const int lane = t & 63, w = t >> 6;
+    const int wr = w & 1, wc = w >> 1;
+    const int lr = lane & 15, lk = lane >> 4;
+    const int st_row = (t % TPC) * VEC, st_col = t / TPC;
+    const bool active = !(lower && wr == 0 && wc >= 2);
+
+    vec_t ra[PASSES], rb[PASSES];
+    auto gload = [&](int k0) {
+#pragma unroll
+        for (int p = 0; p < PASSES; p++) {
+            const int64_t kk = k0 + st_col + p * CPP;
+            ra[p] = *reinterpret_cast<const vec_t*>(A + st_row + kk * lda);
+            rb[p] = *reinterpret_cast<const vec_t*>(B + st_row + kk * ldb);
+        }
+    };
+    auto lstore = [&](int buf) {
+#pragma unroll
+        for (int p = 0; p < PASSES; p++) {
+            const int kk = st_col + p * CPP;
+            *reinterpret_cast<vec_t*>(sA + (buf * BK + kk) * SR + st_row) = ra[p];
+            *reinterpret_cast<vec_t*>(sB + (buf * BK + kk) * SR + st_row) = rb[p];
+        }
+    };
+
+    acc_t acc[2][4];
+#pragma unroll
+    for (int x = 0; x < 2; x++)
+#pragma unroll
+        for (int y = 0; y < 4; y++) acc[x][y] = acc_t{0};
+
+    const int nstage = K / BK;
+    gload(0);
+    lstore(0);
+    __syncthreads();
+#pragma nounroll
+    for (int s = 0; s < nstage; s++) {
+        const int buf = s & 1;
+        if (s + 1 < nstage) gload((s + 1) * BK);
+        if (active) {
+            const T* a = sA + buf * BK * SR;
+            const T* b = sB + buf * BK * SR;
+#pragma unroll
+            for (int kq = 0; kq < BK / 4; kq++) {
+                const int kr = kq * 4 + lk;
+                T fa[4], fb[2];
+#pragma unroll
+                for (int x = 0; x < 2; x++) fb[x] = b[kr * SR + wc * 32 + x * 16 + lr];
+#pragma unroll
+                for (int y = 0; y < 4; y++) fa[y] = a[kr * SR + wr * 64 + y * 16 + lr];
+#pragma unroll
+                for (int x = 0; x < 2; x++)
+#pragma unroll
+                    for (int y = 0; y < 4; y++) acc[x][y] = Tr::mma(fb[x], fa[y], acc[x][y]);
+            }
+        }
+        if (s + 1 < nstage) lstore(buf ^ 1);
+        __syncthreads();
+    }
+    if (!active) return;
+#pragma unroll
+    for (int x = 0; x < 2; x++) {
+#pragma unroll
+        for (int reg = 0; reg < 4; reg++) {
+            const int jl = wc * 32 + x * 16 + Tr::orow(lk, reg);
+            T* ccol = C + (int64_t)jl * ldc;
+#pragma unroll
+            for (int y = 0; y < 4; y++) {
+                const int il = wr * 64 + y * 16 + lr;
+                if (lower && il < jl) continue;
+                if (UPDATE) ccol[il] -= acc[x][y][reg];
+                else ccol[il] = acc[x][y][reg];
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Diagonal 128x128 block: L (in place, lower) and Linv (DB x DB, column-major), 512 threads.
+//
+// The block lives in REGISTERS as a square image S: lower triangle = A (becoming L), strict
+// upper triangle = rows of B = L^{-T} (diagonal in Bd).  B comes from the identity appended
+// below A riding along the elimination; being upper triangular it fills the unused half.
+// Thread t owns rows R0..R0+3 (R0 = 4*(lane&31)) of the 8-column block cb = 2w + (lane>>5).
+// Right-looking over 8-column steps:
+//   1  waves 0-1 (one row each) factor the 8x8 pivot redundantly (rsq + Newton, no divide)
+//      and solve their row x = v Ld^{-T}, v read from the column block published in sV;
+//   2  threads with trailing columns apply S -= x_r x_c^T (unmasked: right of the diagonal
+//      in rows not yet reached is scratch, zeroed when those rows become pivot rows); the
+//      owners of the next column block publish it.
+// The image is then staged through LDS so L and Linv leave in coalesced column stores.
+// ------------------------------------------------------------------------------------------
+constexpr int SPL = DB + 4;
+constexpr int SIL = DB + 2;
+
+__device__ __forceinline__ double rsqrt_full(double x) {
+    double y = __builtin_amdgcn_rsq(x);
+    const double h = 0.5 * x;
+    y = y * fma(-h * y, y, 1.5);
+    y = y * fma(-h * y, y, 1.5);
+    return y;
+}
+__device__ __forceinline__ float rsqrt_full(float x) {
+    float y = __builtin_amdgcn_rsqf(x);
+    const float h = 0.5f * x;
+    y = y * fmaf(-h * y, y, 1.5f);
+    return y;
+}
+
+template <typename T>
+constexpr size_t diag_lds() {
+    return sizeof(T) * ((size_t)DB * SIL + DB) > sizeof(T) * (2 * 8 * SPL + 144) ? sizeof(T) * ((size_t)DB * SIL + DB)
+                                                                              : sizeof(T) * (2 * 8 * SPL + 144);
+}
+
+__device__ __forceinline__ void dbg_mark(int* dbg, int q, int phase, int i, int j) {
+    if (dbg && __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0) {
+        int* p = dbg + 4 * blockIdx.x;
+        __hip_atomic_store(p + 0, q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(p + 2, i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(p + 3, j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(p + 1, phase, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ void diag_factor(T* __restrict__ A, int64_t ld, T* __restrict__ Linv, int* __restrict__ info,
+                                            int64_t col0, unsigned char* smem_raw, const int t, int* dbg = nullptr) {
+    T(*sV)[SPL] = reinterpret_cast<T(*)[SPL]>(smem_raw);
+    T(*sP)[SPL] = reinterpret_cast<T(*)[SPL]>(smem_raw + sizeof(T) * 8 * SPL);
+    T(*sLdW)[8][9] = reinterpret_cast<T(*)[8][9]>(smem_raw + sizeof(T) * 16 * SPL);  // per wave 0/1
+    T(*sLd)[9] = sLdW[0];
+
+    const int w = t >> 6, l = t & 63;
+    const int R0 = (l & 31) * 4;
+    const int cbi = 2 * w + (l >> 5);
+    const int C0 = cbi * 8;
+
+    T S[4][8];
+    T Bd[4];
+#pragma unroll
+    for (int b = 0; b < 8; b++)
+#pragma unroll
+        for (int a = 0; a < 4; a++) S[a][b] = A[R0 + a + (int64_t)(C0 + b) * ld];
+#pragma unroll
+    for (int a = 0; a < 4; a++) Bd[a] = T(1);
+    if (cbi == 0) {
+#pragma unroll
+        for (int a = 0; a < 4; a++)
+#pragma unroll
+            for (int b = 0; b < 8; b++) sV[b][R0 + a] = S[a][b];
+    }
+    __syncthreads();
+
+    int fail_col = -1;
+    for (int j0 = 0; j0 < DB; j0 += 8) {
+        const int jn = j0 + 8;
+        if (t < DB) {
+            // every lane of waves 0-1 factors the pivot (identical values) into its wave's own
+            // LDS copy, so the row solve reads it back instead of holding it next to S
+            T(*myLd)[9] = sLdW[w];
+            {
+                T Ld[8][8];
+#pragma unroll
+                for (int c = 0; c < 8; c++) {
+                    T dsum = sV[c][j0 + c];
+#pragma unroll
+                    for (int k = 0; k < c; k++) dsum = fma(-Ld[c][k], Ld[c][k], dsum);
+                    if (!(dsum > T(0)) && fail_col < 0) fail_col = j0 + c;
+                    const T ri = rsqrt_full(dsum);
+                    Ld[c][c] = dsum * ri;
+                    myLd[c][8] = ri;
+                    myLd[c][c] = Ld[c][c];
+#pragma unroll
+                    for (int r = c + 1; r < 8; r++) {
+                        T v = sV[c][j0 + r];
+#pragma unroll
+                        for (int k = 0; k < c; k++) v = fma(-Ld[r][k], Ld[c][k], v);
+                        Ld[r][c] = v * ri;
+                        myLd[r][c] = Ld[r][c];
+                    }
+                }
+            }
+            const int row = t;
+            const bool piv = row >= j0 && row < jn;
+            T x[8];
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                T v = piv ? ((row - j0 == q) ? T(1) : T(0)) : sV[q][row];
+#pragma unroll
+                for (int q2 = 0; q2 < q; q2++) v = fma(-x[q2], myLd[q][q2], v);
+                x[q] = v * myLd[q][8];
+            }
+#pragma unroll
+            for (int q = 0; q < 8; q++) sP[q][row] = x[q];
+        }
+        __syncthreads();
+        const bool pivrows = R0 >= j0 && R0 < jn;
+        if (cbi == (j0 >> 3)) {
+            if (pivrows) {
+#pragma unroll
+                for (int a = 0; a < 4; a++) {
+                    const int p = R0 + a - j0;
+#pragma unroll
+                    for (int q = 0; q < 8; q++) {
+                        const T xq = sP[q][R0 + a];
+                        S[a][q] = (q <= p) ? sLd[p][q] : xq;
+                        if (q == p) Bd[a] = xq;
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int a = 0; a < 4; a++)
+#pragma unroll
+                    for (int q = 0; q < 8; q++) S[a][q] = sP[q][R0 + a];
+            }
+        }
+        if (C0 >= jn && (R0 < jn || R0 + 3 >= C0)) {
+            if (pivrows) {
+#pragma unroll
+                for (int a = 0; a < 4; a++)
+#pragma unroll
+                    for (int b = 0; b < 8; b++) S[a][b] = T(0);
+            }
+#pragma unroll 2
+            for (int q = 0; q < 8; q++) {
+                T u[4], v[8];
+#pragma unroll
+                for (int a = 0; a < 4; a++) u[a] = sP[q][R0 + a];
+#pragma unroll
+                for (int b = 0; b < 8; b++) v[b] = sP[q][C0 + b];
+#pragma unroll
+                for (int a = 0; a < 4; a++)
+#pragma unroll
+                    for (int b = 0; b < 8; b++) S[a][b] = fma(-u[a], v[b], S[a][b]);
+            }
+        }
+        if (jn < DB && cbi == (jn >> 3)) {
+#pragma unroll
+            for (int a = 0; a < 4; a++)
+#pragma unroll
+                for (int b = 0; b < 8; b++) sV[b][R0 + a] = S[a][b];
+        }
+        __syncthreads();
+    }
+    if (fail_col >= 0) atomicMin(info, (int)(col0 + fail_col + 1));  // same value in every lane of waves 0-1
+
+    T(*sI)[SIL] = reinterpret_cast<T(*)[SIL]>(smem_raw);
+    T* sBd = reinterpret_cast<T*>(smem_raw + sizeof(T) * DB * SIL);
+#pragma unroll
+    for (int a = 0; a < 4; a++) {
+#pragma unroll
+        for (int b = 0; b < 8; b++) sI[R0 + a][C0 + b] = S[a][b];
+        if (R0 + a >= C0 && R0 + a < C0 + 8) sBd[R0 + a] = Bd[a];
+    }
+    __syncthreads();
+    {
+        const int r = t & (DB - 1);
+        for (int c = t >> 7; c < DB; c += NT / DB) {
+            if (r >= c) A[r + (int64_t)c * ld] = sI[r][c];
+            Linv[r + c * DB] = (r > c) ? sI[c][r] : ((r == c) ? sBd[r] : T(0));
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Hand-off helpers
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ int ld_agent(const int* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent(int* p, int v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// every wave's stores complete, then wave 0 releases and publishes *flag = v.  Wave 0 acts
+// with ALL its lanes (same value to the same word): no lane-divergent code near the task
+// loop's back edge, where the structurizer was seen to sink a `lane == 0` block past the
+// next iteration's barrier (a hang).
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
+__device__ __forceinline__ void publish(int* flag, int v) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (wave_id() == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        st_agent(flag, v);
+    }
+}
+
+// stores of this workgroup visible to its own later loads (same CU)
+__device__ __forceinline__ void local_sync() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+}
+
+template <typename T>
+struct Args {
+    T* A;
+    int64_t ld;
+    T* Linv;
+    const int4* tasks;
+    int ntasks;
+    int nc;        // column blocks (= diagonal blocks)
+    int* ctl;      // [C_NCTL] control words, then lcnt[nr], then ver[nr * nc]
+    int* lcnt;
+    int* ver;
+    int* info;
+    long long tlimit;  // wall-clock ticks (100 MHz) a single wait may take
+    int* dbg;          // GPRX_PT_DEBUG: per-workgroup {ticket, phase, i, j} in pinned host memory
+    int variant;       // GPRX_PT_VARIANT debug bits: 1 no TRSM math, 2 no UPD math, 4 no diag factor
+};
+
+
+// Every wave waits until the task's inputs are final (all lanes load the same words; the
+// values are made wave-uniform, so the loop is a scalar loop with no divergence).  Returns
+// false on timeout or when another workgroup raised the error flag.
+__device__ __forceinline__ int ld_uni(const int* p) { return __builtin_amdgcn_readfirstlane(ld_agent(p)); }
+
+template <typename T>
+__device__ bool wait_inputs(const Args<T>& a, int type, int i, int j, int b0, int nb) {
+    const int* vp;
+    int vwant;
+    const int* vp2;
+    int vwant2;
+    const int* lp1;
+    int lwant1;
+    const int* lp2;
+    int lwant2;
+    if (type == T_DIAGX) {
+        if (i == 0) return true;
+        vp = a.ver + (int64_t)i * a.nc + (i - 1);
+        vwant = i - 1;
+        vp2 = a.ver + (int64_t)i * a.nc + i;
+        vwant2 = i - 1;
+        lp1 = a.lcnt + (i - 1);
+        lwant1 = i;
+        lp2 = lp1;
+        lwant2 = lwant1;
+    } else if (type == T_TRSM) {
+        vp = a.ver + (int64_t)i * a.nc + j;
+        vwant = j;
+        vp2 = vp;
+        vwant2 = vwant;
+        lp1 = a.lcnt + j;
+        lwant1 = j + 1;
+        lp2 = lp1;
+        lwant2 = lwant1;
+    } else {
+        vp = a.ver + (int64_t)i * a.nc + j;
+        vwant = b0;
+        vp2 = vp;
+        vwant2 = vwant;
+        lp1 = a.lcnt + i;
+        lwant1 = b0 + nb;
+        lp2 = a.lcnt + j;
+        lwant2 = b0 + nb;
+    }
+    const long long t0 = wall_clock64();
+    for (;;) {
+        const int ok = (ld_uni(vp) == vwant) & (ld_uni(vp2) == vwant2) & (ld_uni(lp1) >= lwant1) &
+                       (ld_uni(lp2) >= lwant2);
+        if (ok) return true;
+        if (ld_uni(a.ctl + C_ERR)) return false;
+        if (wall_clock64() - t0 > a.tlimit) {
+            st_agent(a.ctl + C_ERR, 1);
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    __shared__ int s_q;
+    T* smem = reinterpret_cast<T*>(smem_raw);
+    const int t = threadIdx.x;
+    const int wv = wave_id();
+    const int64_t ld = a.ld;
+    for (;;) {
+        if (wv == 0) {  // one ticket per workgroup: lane 0 adds 1, the other lanes 0
+            const int v = __hip_atomic_fetch_add(a.ctl + C_TICKET, (t == 0) ? 1 : 0, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+            s_q = __builtin_amdgcn_readfirstlane(v);
+        }
+        __syncthreads();
+        // everything below is wave-uniform: keep it in SGPRs so the task dispatch is scalar
+        const int q = __builtin_amdgcn_readfirstlane(s_q);
+        if (q >= a.ntasks) break;
+        const int4 tk = a.tasks[q];
+        const int type = __builtin_amdgcn_readfirstlane(tk.x & 0xff), nb = __builtin_amdgcn_readfirstlane(tk.x >> 8);
+        const int i = __builtin_amdgcn_readfirstlane(tk.y), j = __builtin_amdgcn_readfirstlane(tk.z),
+                  b0 = __builtin_amdgcn_readfirstlane(tk.w);
+        dbg_mark(a.dbg, q, 1 + 10 * type, i, j);
+        const bool ok = wait_inputs<T>(a, type, i, j, b0, nb);  // every wave, uniform
+        if (!ok) break;
+        if (wv == 0) {  // wave 0 acquires for the workgroup (invalidates this CU's L1)
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+        dbg_mark(a.dbg, q, 2 + 10 * type, i, j);
+        // opaque copy of the thread index: keeps the per-task address arithmetic inside the
+        // task instead of hoisted (and held in registers) across the whole task loop
+        int tid = t;
+        asm volatile("" : "+v"(tid));
+        T* Ci = a.A + (int64_t)i * GT;  // row block i, column 0
+        if (type == T_UPD) {
+            if (!(a.variant & 2)) tile_gemm<T, true>(Ci + (int64_t)j * GT * ld, ld, Ci + (int64_t)b0 * GT * ld, ld,
+                               a.A + (int64_t)j * GT + (int64_t)b0 * GT * ld, ld, nb * GT, i == j, smem, tid);
+            publish(a.ver + (int64_t)i * a.nc + j, b0 + nb);
+        } else if (type == T_TRSM) {
+            T* Cik = Ci + (int64_t)j * GT * ld;
+            if (!(a.variant & 1)) tile_gemm<T, false>(Cik, ld, Cik, ld, a.Linv + (int64_t)j * DB * DB, DB, GT, false, smem, tid);
+            publish(a.lcnt + i, j + 1);
+        } else {  // DIAGX(k = i)
+            const int k = i;
+            T* Akk = Ci + (int64_t)k * GT * ld;
+            if (k > 0) {
+                T* Akm = Ci + (int64_t)(k - 1) * GT * ld;
+                tile_gemm<T, false>(Akm, ld, Akm, ld, a.Linv + (int64_t)(k - 1) * DB * DB, DB, GT, false, smem, tid);
+                publish(a.lcnt + k, k);  // L_{k,k-1} final: unblocks the updates of column k
+                tile_gemm<T, true>(Akk, ld, Akm, ld, Akm, ld, GT, true, smem, tid);
+                local_sync();
+            }
+            if (!(a.variant & 4)) diag_factor<T>(Akk, ld, a.Linv + (int64_t)k * DB * DB, a.info, (int64_t)k * DB, smem_raw, tid, a.dbg);
+            publish(a.lcnt + k, k + 1);
+        }
+    }
+    dbg_mark(a.dbg, -1, 9, 0, 0);
+    // the error flag of a timed-out wait ends up in info (reported by the caller)
+    if (wv == 0 && ld_agent(a.ctl + C_ERR)) atomicMin(a.info, -1);
+}
+
+// ==========================================================================================
+// Host: task list + list-schedule simulation
+// ==========================================================================================
+struct Cost {
+    double k128 = 17.5;  // us per 128-deep slice of a full tile update (one CU)
+    double ovh = 5.0;    // us per task: ticket, waits, fences, C read-modify-write
+    double diag = 40.0;  // us for the 128x128 factor + inverse
+};
+
+struct Task {
+    int type, i, j, b0, nb;
+    double dur;
+    std::vector<int> succ;
+    int ndep = 0;
+    double bl = 0;  // bottom level (longest path to the end, inclusive)
+};
+
+struct Schedule {
+    std::vector<int4> list;
+    double est_us = 0;
+    int64_t ntasks = 0;
+};
+
+// Chunks of the updates of tile (i, j): b in [0, e), e = j (i > j) or j - 1 (diagonal tile:
+// the last one is applied inside DIAGX(j)).  Aligned W-chunks up to the start of the panel
+// `look` panels before j's own, single blocks after that.
+static void tile_chunks(int i, int j, int W, int look, std::vector<std::pair<int, int>>& out) {
+    out.clear();
+    const int e = (i == j) ? j - 1 : j;
+    if (e <= 0) return;
+    int hb = W * (j / W) - W * look;
+    hb = std::max(0, std::min(hb, e));
+    hb -= hb % W;
+    int b = 0;
+    for (; b + W <= hb; b += W) out.push_back({b, W});
+    for (; b < e; b++) out.push_back({b, 1});
+}
+
+static Schedule make_schedule(int nc, int nr, int W, int look, int P, const Cost& cm) {
+    std::vector<Task> tasks;
+    tasks.reserve((size_t)nr * nc * 2);
+    auto add = [&](int type, int i, int j, int b0, int nb, double dur) {
+        Task tk;
+        tk.type = type;
+        tk.i = i;
+        tk.j = j;
+        tk.b0 = b0;
+        tk.nb = nb;
+        tk.dur = dur;
+        tasks.push_back(std::move(tk));
+        return (int)tasks.size() - 1;
+    };
+    std::vector<int> diagx(nc, -1);
+    std::vector<int> trsm((size_t)nr * nc, -1);
+    std::vector<int> last_upd((size_t)nr * nc, -1);
+    std::vector<std::vector<int>> deps;
+    auto dep = [&](int tsk, int on) {
+        if (on < 0) return;
+        if ((int)deps.size() <= tsk) deps.resize(tsk + 1);
+        deps[tsk].push_back(on);
+    };
+    // producer of L_{i,b}
+    auto prodL = [&](int i, int b) -> int {
+        if (i < nc && (b == i || b == i - 1)) return diagx[i];
+        return trsm[(size_t)i * nc + b];
+    };
+    // update chunks bucketed by their last block
+    struct Chunk {
+        int i, j, b0, nb;
+    };
+    std::vector<std::vector<Chunk>> by_last(nc);
+    {
+        std::vector<std::pair<int, int>> ch;
+        for (int j = 1; j < nc; j++)
+            for (int i = j; i < nr; i++) {
+                tile_chunks(i, j, W, look, ch);
+                for (auto& c : ch) by_last[c.first + c.second - 1].push_back(Chunk{i, j, c.first, c.second});
+            }
+    }
+    auto make_diagx = [&](int k) {
+        const double dur = (k == 0) ? cm.diag + cm.ovh : cm.diag + 1.75 * cm.k128 + 2 * cm.ovh;
+        const int id = add(T_DIAGX, k, k, 0, 0, dur);
+        diagx[k] = id;
+        if (k >= 1) {
+            dep(id, diagx[k - 1]);
+            dep(id, last_upd[(size_t)k * nc + (k - 1)]);
+            dep(id, last_upd[(size_t)k * nc + k]);
+        }
+    };
+    // Creation order (checked below) puts every producer before its consumers:
+    // DIAGX(0); per k: TRSM(., k), DIAGX(k+1), the update chunks ending at block k.
+    make_diagx(0);
+    for (int k = 0; k < nc; k++) {
+        for (int i = k + 1; i < nr; i++) {
+            if (i == k + 1 && i < nc) continue;  // inside DIAGX(k+1)
+            const int id = add(T_TRSM, i, k, 0, 0, cm.k128 + cm.ovh);
+            trsm[(size_t)i * nc + k] = id;
+            dep(id, diagx[k]);
+            dep(id, last_upd[(size_t)i * nc + k]);
+        }
+        if (k + 1 < nc) make_diagx(k + 1);
+        for (const Chunk& c : by_last[k]) {
+            const double dur = cm.ovh + c.nb * cm.k128 * (c.i == c.j ? 0.75 : 1.0);
+            const int id = add(T_UPD, c.i, c.j, c.b0, c.nb, dur);
+            dep(id, last_upd[(size_t)c.i * nc + c.j]);
+            dep(id, prodL(c.i, k));
+            dep(id, prodL(c.j, k));
+            last_upd[(size_t)c.i * nc + c.j] = id;
+        }
+    }
+    const int nt = (int)tasks.size();
+    deps.resize(nt);
+    for (int id = 0; id < nt; id++) {
+        auto& d = deps[id];
+        std::sort(d.begin(), d.end());
+        d.erase(std::unique(d.begin(), d.end()), d.end());
+        for (int on : d) {
+            if (on >= id) throw Error{GPRX_ERR_ARG, "potrf tile schedule: producer created after consumer"};
+            tasks[on].succ.push_back(id);
+        }
+        tasks[id].ndep = (int)d.size();
+    }
+    // creation order is topological: bottom levels in reverse
+    for (int id = nt - 1; id >= 0; id--) {
+        double m = 0;
+        for (int s : tasks[id].succ) m = std::max(m, tasks[s].bl);
+        tasks[id].bl = tasks[id].dur + m;
+    }
+    // list scheduling on P workers, highest bottom level first
+    typedef std::pair<double, int> PQ;
+    std::priority_queue<PQ> ready;
+    std::priority_queue<PQ, std::vector<PQ>, std::greater<PQ>> running;
+    std::vector<int> indeg(nt);
+    for (int id = 0; id < nt; id++) {
+        indeg[id] = tasks[id].ndep;
+        if (indeg[id] == 0) ready.push({tasks[id].bl, id});
+    }
+    Schedule S;
+    S.list.reserve(nt);
+    double now = 0;
+    int freew = P;
+    while ((int)S.list.size() < nt || !running.empty()) {
+        while (freew > 0 && !ready.empty()) {
+            const int id = ready.top().second;
+            ready.pop();
+            const Task& tk = tasks[id];
+            S.list.push_back(make_int4(tk.type | (tk.nb << 8), tk.i, tk.j, tk.b0));
+            running.push({now + tk.dur, id});
+            freew--;
+        }
+        if (running.empty()) throw Error{GPRX_ERR_ARG, "potrf tile schedule: dependency cycle"};
+        const PQ f = running.top();
+        running.pop();
+        now = f.first;
+        freew++;
+        for (int s : tasks[f.second].succ)
+            if (--indeg[s] == 0) ready.push({tasks[s].bl, s});
+    }
+    S.est_us = now;
+    S.ntasks = nt;
+    return S;
+}
+
+struct Params {
+    int W = 4, look = 0;
+    Cost cm;
+    Params() {
+        if (const char* e = std::getenv("GPRX_PT_W")) W = std::max(1, std::atoi(e));
+        if (const char* e = std::getenv("GPRX_PT_LOOK")) look = std::max(0, std::atoi(e));
+        if (const char* e = std::getenv("GPRX_PT_DIAG_US")) cm.diag = std::atof(e);
+        if (const char* e = std::getenv("GPRX_PT_K128_US")) cm.k128 = std::atof(e);
+        if (const char* e = std::getenv("GPRX_PT_OVH_US")) cm.ovh = std::atof(e);
+    }
+};
+static const Params& params() {
+    static Params p;
+    return p;
+}
+
+}  // namespace pt
+
+// Per-context state: cached schedules (host + device copies) and the counter block.
+struct PtState {
+    struct Dev {
+        int4* list = nullptr;
+        int64_t n = 0;
+        double est_us = 0;
+    };
+    std::map<std::pair<int, int>, Dev> sched;
+    int* ctr = nullptr;
+    size_t ctr_ints = 0;
+    int ncu = 0;
+    int* dbg = nullptr;  // pinned host status words (GPRX_PT_DEBUG)
+    ~PtState() {
+        if (dbg) (void)hipHostFree(dbg);
+        for (auto& kv : sched) (void)hipFree(kv.second.list);
+        if (ctr) (void)hipFree(ctr);
+    }
+};
+
+void pt_state_free(PtState* p) { delete p; }
+
+// debug snapshot of the last launch's per-workgroup status (GPRX_PT_DEBUG)
+static int* g_pt_dbg = nullptr;
+static int g_pt_dbg_n = 0;
+int pt_debug_snapshot(int* out, int max_wg) {
+    if (!g_pt_dbg) return 0;
+    const int n = std::min(max_wg, g_pt_dbg_n);
+    for (int k = 0; k < 4 * n; k++) out[k] = __atomic_load_n(g_pt_dbg + k, __ATOMIC_RELAXED);
+    return n;
+}
+
+template <typename T>
+void potrf_tiles(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info, Exec& ex) {
+    using namespace pt;
+    if (!ex.pt) ex.pt = new PtState();
+    PtState& st = *ex.pt;
+    if (st.ncu == 0) {
+        int dev = 0;
+        GPRX_HIP(hipGetDevice(&dev));
+        hipDeviceProp_t prop;
+        GPRX_HIP(hipGetDeviceProperties(&prop, dev));
+        st.ncu = prop.multiProcessorCount;
+    }
+    GPRX_REQUIRE(np % DB == 0 && nrows % GT == 0 && nrows >= np, GPRX_ERR_ARG, "potrf_tiles: bad sizes");
+    const int nc = (int)(np / DB), nr = (int)(nrows / GT);
+    auto key = std::make_pair(nc, nr);
+    auto it = st.sched.find(key);
+    if (it == st.sched.end()) {
+        const Params& pr = params();
+        Schedule S = make_schedule(nc, nr, pr.W, pr.look, st.ncu, pr.cm);
+        PtState::Dev d;
+        d.n = (int64_t)S.list.size();
+        d.est_us = S.est_us;
+        GPRX_HIP(hipMalloc(&d.list, sizeof(int4) * std::max<int64_t>(1, d.n)));
+        GPRX_HIP(hipMemcpy(d.list, S.list.data(), sizeof(int4) * d.n, hipMemcpyHostToDevice));
+        it = st.sched.emplace(key, d).first;
+    }
+    const PtState::Dev& sd = it->second;
+    const size_t need = (size_t)C_NCTL + nr + (size_t)nr * nc;
+    if (st.ctr_ints < need) {
+        if (st.ctr) GPRX_HIP(hipFree(st.ctr));
+        st.ctr = nullptr;
+        GPRX_HIP(hipMalloc(&st.ctr, sizeof(int) * need));
+        st.ctr_ints = need;
+    }
+    hipStream_t s = ex.s0;
+    GPRX_HIP(hipMemsetAsync(st.ctr, 0, sizeof(int) * need, s));
+    Args<T> a;
+    a.A = A;
+    a.ld = ld;
+    a.Linv = Linv;
+    a.tasks = sd.list;
+    a.ntasks = (int)sd.n;
+    a.nc = nc;
+    a.ctl = st.ctr;
+    a.lcnt = st.ctr + C_NCTL;
+    a.ver = st.ctr + C_NCTL + nr;
+    a.info = info;
+    a.dbg = nullptr;
+    static const int variant = std::getenv("GPRX_PT_VARIANT") ? std::atoi(std::getenv("GPRX_PT_VARIANT")) : 0;
+    a.variant = variant;
+    static const bool debug = std::getenv("GPRX_PT_DEBUG") != nullptr;
+    if (debug) {
+        if (!st.dbg) GPRX_HIP(hipHostMalloc((void**)&st.dbg, sizeof(int) * 4 * st.ncu, hipHostMallocCoherent));
+        std::memset(st.dbg, 0xff, sizeof(int) * 4 * st.ncu);
+        g_pt_dbg = st.dbg;
+        g_pt_dbg_n = st.ncu;
+        a.dbg = st.dbg;
+    }
+    // one wait may take at most 2 s + 20x the whole predicted factorisation
+    a.tlimit = (long long)(1e8 * (2.0 + 20.0 * sd.est_us * 1e-6));
+    const size_t lds = std::max<size_t>(std::max(gemm_lds<T>(), diag_lds<T>()), 96 * 1024);
+    static bool attr = false;
+    if (!attr) {
+        GPRX_HIP(hipFuncSetAttribute((const void*)potrf_tiles_kernel<double>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)std::max<size_t>(std::max(gemm_lds<double>(), diag_lds<double>()), 96 * 1024)));
+        GPRX_HIP(hipFuncSetAttribute((const void*)potrf_tiles_kernel<float>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)std::max<size_t>(std::max(gemm_lds<float>(), diag_lds<float>()), 96 * 1024)));
+        attr = true;
+    }
+    const double nn = (double)np;
+    ProfScope ps(KC_UPDATE, s, nn * nn * nn / 3.0 + (double)(nrows - np) * nn * nn, 0.0);
+    hipLaunchKernelGGL(potrf_tiles_kernel<T>, dim3((unsigned)st.ncu), dim3(NT), lds, s, a);
+    GPRX_HIP(hipGetLastError());
+}
+
+// Host-only schedule statistics (no device work): tasks, predicted makespan, and a check
+// that every task's producers come earlier in the ticket order.
+int64_t potrf_tiles_schedule_stats(int nc, int nr, int P, double* est_us) {
+    const pt::Params& pr = pt::params();
+    pt::Schedule S = pt::make_schedule(nc, nr, pr.W, pr.look, P, pr.cm);
+    if (est_us) *est_us = S.est_us;
+    return S.ntasks;
+}
+
+template void potrf_tiles<double>(double*, int64_t, int64_t, int64_t, double*, int*, Exec&);
+template void potrf_tiles<float>(float*, int64_t, int64_t, int64_t, float*, int*, Exec&);
+
+}  // namespace gprx

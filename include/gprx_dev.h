@@ -14,11 +14,19 @@ extern "C" {
  *       5 = back substitution (m = 1) of an n x n factor,
  *       6 = diagonal kernel phase profile: ms must hold 5 doubles, receiving the mean
  *           s_memtime ticks per launch of (load, solve phases, update phases, store, total),
- *       7 = potrf with look-ahead replayed from a captured hipGraph, 8 = backsolve from a graph.
+ *       7 = potrf with look-ahead replayed from a captured hipGraph, 8 = backsolve from a graph,
+ *       9 = potrf as one persistent tile-dataflow launch (potrf_tiles).
  * For 1/2: (M, N, K) are the gemm sizes; for 3/4/5: M = n.  Returns the mean device time
  * per call over `iters` calls (HIP events) in *ms. */
 gprx_status gprx_dev_bench(gprx_ctx* ctx, gprx_dtype dtype, int32_t what, int64_t M, int64_t N, int64_t K,
                            int32_t iters, double* ms);
+/* Host-only: build the tile-dataflow potrf schedule for nc diagonal blocks, nr row blocks
+ * and P workers; returns its task count and simulated makespan (us).  Throws nothing, needs no
+ * device: GPRX_ERR_ARG if the ticket order would violate a dependency. */
+gprx_status gprx_dev_schedule(int32_t nc, int32_t nr, int32_t P, double* est_us, int64_t* ntasks);
+/* GPRX_PT_DEBUG=1: copy the per-workgroup status {ticket, phase, i, j} of the running (or last)
+ * potrf_tiles launch out of pinned host memory, without synchronising; returns workgroups. */
+int32_t gprx_dev_pt_debug(int32_t* out, int32_t max_wg);
 #ifdef __cplusplus
 }
 #endif
