@@ -175,6 +175,15 @@ static gprx_status bench_impl(int what, int64_t M, int64_t N, int64_t K, int ite
 
 namespace gprx {
 int pt_debug_snapshot(int* out, int max_wg);
+int64_t pt_trace_copy(int32_t* tasks, long long* times, int64_t max);
+}
+extern "C" int64_t gprx_dev_pt_trace(int32_t* tasks, int64_t* times, int64_t max) {
+    try {
+        return gprx::pt_trace_copy(tasks, (long long*)times, max);
+    } catch (const gprx::Error& e) {
+        std::fprintf(stderr, "gprx_dev_pt_trace: %s\n", e.msg.c_str());
+        return -1;
+    }
 }
 extern "C" int32_t gprx_dev_pt_debug(int32_t* out, int32_t max_wg) { return gprx::pt_debug_snapshot(out, max_wg); }
 

@@ -145,6 +145,23 @@ __device__ __forceinline__ void tile_gemm(T* __restrict__ C, int64_t ldc, const 
         for (int y = 0; y < 4; y++) acc[x][y] = acc_t{0};
 
     const int nstage = K / BK;
+    // UPDATE: the whole C tile is fetched into registers before any store (a load-store-load
+    // sequence per element would serialise on possible aliasing)
+    T cv[2][4][4];
+    auto cload = [&]() {
+#pragma unroll
+        for (int x = 0; x < 2; x++)
+#pragma unroll
+            for (int reg = 0; reg < 4; reg++) {
+                const int jl = wc * 32 + x * 16 + Tr::orow(lk, reg);
+                const T* ccol = C + (int64_t)jl * ldc;
+#pragma unroll
+                for (int y = 0; y < 4; y++) {
+                    const int il = wr * 64 + y * 16 + lr;
+                    cv[x][y][reg] = (lower && il < jl) ? T(0) : ccol[il];
+                }
+            }
+    };
     gload(0);
     lstore(0);
     __syncthreads();
@@ -173,6 +190,7 @@ __device__ __forceinline__ void tile_gemm(T* __restrict__ C, int64_t ldc, const 
         __syncthreads();
     }
     if (!active) return;
+    if (UPDATE) cload();
 #pragma unroll
     for (int x = 0; x < 2; x++) {
 #pragma unroll
@@ -183,7 +201,7 @@ __device__ __forceinline__ void tile_gemm(T* __restrict__ C, int64_t ldc, const 
             for (int y = 0; y < 4; y++) {
                 const int il = wr * 64 + y * 16 + lr;
                 if (lower && il < jl) continue;
-                if (UPDATE) ccol[il] -= acc[x][y][reg];
+                if (UPDATE) ccol[il] = cv[x][y][reg] - acc[x][y][reg];
                 else ccol[il] = acc[x][y][reg];
             }
         }
@@ -394,11 +412,11 @@ __device__ __forceinline__ void st_agent(int* p, int v) {
 // next iteration's barrier (a hang).
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 
-__device__ __forceinline__ void publish(int* flag, int v) {
+__device__ __forceinline__ void publish(int* flag, int v, int variant = 0) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (wave_id() == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        if (!(variant & 16)) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         st_agent(flag, v);
     }
@@ -425,6 +443,7 @@ struct Args {
     long long tlimit;  // wall-clock ticks (100 MHz) a single wait may take
     int* dbg;          // GPRX_PT_DEBUG: per-workgroup {ticket, phase, i, j} in pinned host memory
     int variant;       // GPRX_PT_VARIANT debug bits: 1 no TRSM math, 2 no UPD math, 4 no diag factor
+    long long* trace;  // GPRX_PT_TRACE: per ticket {ticket taken, inputs ready, published, workgroup}
 };
 
 
@@ -504,6 +523,7 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
         // everything below is wave-uniform: keep it in SGPRs so the task dispatch is scalar
         const int q = __builtin_amdgcn_readfirstlane(s_q);
         if (q >= a.ntasks) break;
+        const long long tr0 = a.trace ? wall_clock64() : 0;
         const int4 tk = a.tasks[q];
         const int type = __builtin_amdgcn_readfirstlane(tk.x & 0xff), nb = __builtin_amdgcn_readfirstlane(tk.x >> 8);
         const int i = __builtin_amdgcn_readfirstlane(tk.y), j = __builtin_amdgcn_readfirstlane(tk.z),
@@ -511,11 +531,13 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
         dbg_mark(a.dbg, q, 1 + 10 * type, i, j);
         const bool ok = wait_inputs<T>(a, type, i, j, b0, nb);  // every wave, uniform
         if (!ok) break;
-        if (wv == 0) {  // wave 0 acquires for the workgroup (invalidates this CU's L1)
+        if (wv == 0 && !(a.variant & 32)) {  // wave 0 acquires for the workgroup (invalidates this CU's L1)
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         __syncthreads();
+        const long long tr1 = a.trace ? wall_clock64() : 0;
+        const long long tc1 = a.trace ? (long long)__builtin_amdgcn_s_memtime() : 0;
         dbg_mark(a.dbg, q, 2 + 10 * type, i, j);
         // opaque copy of the thread index: keeps the per-task address arithmetic inside the
         // task instead of hoisted (and held in registers) across the whole task loop
@@ -525,7 +547,7 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
         if (type == T_UPD) {
             if (!(a.variant & 2)) tile_gemm<T, true>(Ci + (int64_t)j * GT * ld, ld, Ci + (int64_t)b0 * GT * ld, ld,
                                a.A + (int64_t)j * GT + (int64_t)b0 * GT * ld, ld, nb * GT, i == j, smem, tid);
-            publish(a.ver + (int64_t)i * a.nc + j, b0 + nb);
+            publish(a.ver + (int64_t)i * a.nc + j, b0 + nb, a.variant);
         } else if (type == T_TRSM) {
             T* Cik = Ci + (int64_t)j * GT * ld;
             if (!(a.variant & 1)) tile_gemm<T, false>(Cik, ld, Cik, ld, a.Linv + (int64_t)j * DB * DB, DB, GT, false, smem, tid);
@@ -543,6 +565,13 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
             if (!(a.variant & 4)) diag_factor<T>(Akk, ld, a.Linv + (int64_t)k * DB * DB, a.info, (int64_t)k * DB, smem_raw, tid, a.dbg);
             publish(a.lcnt + k, k + 1);
         }
+        if (a.trace && wv == 0) {
+            long long* tp = a.trace + 4 * (int64_t)q;
+            tp[0] = tr0;
+            tp[1] = tr1;
+            tp[2] = wall_clock64();
+            tp[3] = (long long)blockIdx.x | (((long long)__builtin_amdgcn_s_memtime() - tc1) << 16);
+        }
     }
     dbg_mark(a.dbg, -1, 9, 0, 0);
     // the error flag of a timed-out wait ends up in info (reported by the caller)
@@ -552,10 +581,12 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
 // ==========================================================================================
 // Host: task list + list-schedule simulation
 // ==========================================================================================
-struct Cost {
-    double k128 = 17.5;  // us per 128-deep slice of a full tile update (one CU)
-    double ovh = 5.0;    // us per task: ticket, waits, fences, C read-modify-write
-    double diag = 40.0;  // us for the 128x128 factor + inverse
+struct Cost {  // per-task durations (us, one CU), calibrated from GPRX_PT_TRACE timelines
+    double k128 = 17.1;  // per 128-deep slice of a full tile update
+    double ovh = 12.0;   // per update task: ticket, waits, fences, C read-modify-write
+    double trsm = 22.0;  // TRSM tile
+    double diagx = 114.0;  // DIAGX(k > 0): trsm tile + syrk tile + 128x128 factor/inverse
+    double diag0 = 75.0;   // DIAGX(0): factor/inverse only
 };
 
 struct Task {
@@ -629,7 +660,7 @@ static Schedule make_schedule(int nc, int nr, int W, int look, int P, const Cost
             }
     }
     auto make_diagx = [&](int k) {
-        const double dur = (k == 0) ? cm.diag + cm.ovh : cm.diag + 1.75 * cm.k128 + 2 * cm.ovh;
+        const double dur = (k == 0) ? cm.diag0 : cm.diagx;
         const int id = add(T_DIAGX, k, k, 0, 0, dur);
         diagx[k] = id;
         if (k >= 1) {
@@ -644,7 +675,7 @@ static Schedule make_schedule(int nc, int nr, int W, int look, int P, const Cost
     for (int k = 0; k < nc; k++) {
         for (int i = k + 1; i < nr; i++) {
             if (i == k + 1 && i < nc) continue;  // inside DIAGX(k+1)
-            const int id = add(T_TRSM, i, k, 0, 0, cm.k128 + cm.ovh);
+            const int id = add(T_TRSM, i, k, 0, 0, cm.trsm);
             trsm[(size_t)i * nc + k] = id;
             dep(id, diagx[k]);
             dep(id, last_upd[(size_t)i * nc + k]);
@@ -713,12 +744,13 @@ static Schedule make_schedule(int nc, int nr, int W, int look, int P, const Cost
 }
 
 struct Params {
-    int W = 4, look = 0;
+    int W = 8, look = 0;
     Cost cm;
     Params() {
         if (const char* e = std::getenv("GPRX_PT_W")) W = std::max(1, std::atoi(e));
         if (const char* e = std::getenv("GPRX_PT_LOOK")) look = std::max(0, std::atoi(e));
-        if (const char* e = std::getenv("GPRX_PT_DIAG_US")) cm.diag = std::atof(e);
+        if (const char* e = std::getenv("GPRX_PT_DIAGX_US")) cm.diagx = std::atof(e);
+        if (const char* e = std::getenv("GPRX_PT_TRSM_US")) cm.trsm = std::atof(e);
         if (const char* e = std::getenv("GPRX_PT_K128_US")) cm.k128 = std::atof(e);
         if (const char* e = std::getenv("GPRX_PT_OVH_US")) cm.ovh = std::atof(e);
     }
@@ -736,13 +768,18 @@ struct PtState {
         int4* list = nullptr;
         int64_t n = 0;
         double est_us = 0;
+        std::vector<int4> host;
     };
     std::map<std::pair<int, int>, Dev> sched;
     int* ctr = nullptr;
     size_t ctr_ints = 0;
     int ncu = 0;
     int* dbg = nullptr;  // pinned host status words (GPRX_PT_DEBUG)
+    long long* trace = nullptr;  // GPRX_PT_TRACE timeline of the last launch
+    int64_t trace_n = 0;
+    const std::vector<int4>* last_list = nullptr;
     ~PtState() {
+        if (trace) (void)hipFree(trace);
         if (dbg) (void)hipHostFree(dbg);
         for (auto& kv : sched) (void)hipFree(kv.second.list);
         if (ctr) (void)hipFree(ctr);
@@ -750,6 +787,18 @@ struct PtState {
 };
 
 void pt_state_free(PtState* p) { delete p; }
+
+// timeline of the last traced launch (GPRX_PT_TRACE): per ticket {type|nb<<8, i, j, b0} and
+// {taken, ready, published, workgroup} (100 MHz wall clock)
+static PtState* g_pt_state = nullptr;
+int64_t pt_trace_copy(int32_t* tasks, long long* times, int64_t max) {
+    if (!g_pt_state || !g_pt_state->trace || !g_pt_state->last_list) return 0;
+    const int64_t n = std::min<int64_t>(max, g_pt_state->trace_n);
+    GPRX_HIP(hipDeviceSynchronize());
+    GPRX_HIP(hipMemcpy(times, g_pt_state->trace, sizeof(long long) * 4 * n, hipMemcpyDeviceToHost));
+    std::memcpy(tasks, g_pt_state->last_list->data(), sizeof(int4) * n);
+    return n;
+}
 
 // debug snapshot of the last launch's per-workgroup status (GPRX_PT_DEBUG)
 static int* g_pt_dbg = nullptr;
@@ -785,6 +834,7 @@ void potrf_tiles(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info
         d.est_us = S.est_us;
         GPRX_HIP(hipMalloc(&d.list, sizeof(int4) * std::max<int64_t>(1, d.n)));
         GPRX_HIP(hipMemcpy(d.list, S.list.data(), sizeof(int4) * d.n, hipMemcpyHostToDevice));
+        d.host = S.list;
         it = st.sched.emplace(key, d).first;
     }
     const PtState::Dev& sd = it->second;
@@ -809,6 +859,18 @@ void potrf_tiles(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info
     a.ver = st.ctr + C_NCTL + nr;
     a.info = info;
     a.dbg = nullptr;
+    a.trace = nullptr;
+    static const bool tracing = std::getenv("GPRX_PT_TRACE") != nullptr;
+    if (tracing) {
+        if (st.trace_n < sd.n) {
+            if (st.trace) GPRX_HIP(hipFree(st.trace));
+            GPRX_HIP(hipMalloc(&st.trace, sizeof(long long) * 4 * sd.n));
+        }
+        st.trace_n = sd.n;
+        a.trace = st.trace;
+        g_pt_state = &st;
+        st.last_list = &sd.host;
+    }
     static const int variant = std::getenv("GPRX_PT_VARIANT") ? std::atoi(std::getenv("GPRX_PT_VARIANT")) : 0;
     a.variant = variant;
     static const bool debug = std::getenv("GPRX_PT_DEBUG") != nullptr;

@@ -27,6 +27,10 @@ gprx_status gprx_dev_schedule(int32_t nc, int32_t nr, int32_t P, double* est_us,
 /* GPRX_PT_DEBUG=1: copy the per-workgroup status {ticket, phase, i, j} of the running (or last)
  * potrf_tiles launch out of pinned host memory, without synchronising; returns workgroups. */
 int32_t gprx_dev_pt_debug(int32_t* out, int32_t max_wg);
+/* GPRX_PT_TRACE=1: timeline of the last potrf_tiles launch.  tasks: 4 ints per ticket
+ * {type | nb << 8, i, j, b0}; times: 4 int64 per ticket {taken, inputs ready, published,
+ * workgroup} in 100 MHz wall-clock ticks.  Synchronises the device; returns tickets copied. */
+int64_t gprx_dev_pt_trace(int32_t* tasks, int64_t* times, int64_t max);
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,73 @@
+"""Timeline of one tile-dataflow factorisation (GPRX_PT_TRACE): per-type task durations,
+waits, worker utilisation and the DIAGX chain."""
+import ctypes, json, os, sys
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+os.environ.setdefault("GPRX_PT_TRACE", "1")
+import numpy as np
+import gpr_amd
+from gpr_amd.gprx import lib
+
+L = lib()
+L.gprx_dev_bench.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int32, ctypes.c_int64, ctypes.c_int64,
+                             ctypes.c_int64, ctypes.c_int32, ctypes.POINTER(ctypes.c_double)]
+L.gprx_dev_pt_trace.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
+L.gprx_dev_pt_trace.restype = ctypes.c_int64
+ctx = gpr_amd.Context(0)
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 16384
+ms = ctypes.c_double()
+assert L.gprx_dev_bench(ctx.h, 1, 9, n, 0, 0, 2, ctypes.byref(ms)) == 0
+MAX = 400000
+tasks = np.zeros((MAX, 4), np.int32)
+times = np.zeros((MAX, 4), np.int64)
+k = L.gprx_dev_pt_trace(tasks.ctypes.data, times.ctypes.data, MAX)
+tasks, times = tasks[:k], times[:k]
+out = os.environ.get("PT_TRACE_OUT")
+if out:
+    np.savez_compressed(out, tasks=tasks, times=times)
+t0 = times[:, 0].min()
+tk = (times[:, :3] - t0) / 100.0  # us
+span = tk[:, 2].max()
+typ = tasks[:, 0] & 0xff
+nb = tasks[:, 0] >> 8
+ex = tk[:, 2] - tk[:, 1]
+wt = tk[:, 1] - tk[:, 0]
+P = len(np.unique(times[:, 3] & 0xffff))
+cyc = times[:, 3] >> 16
+dur_ticks = times[:, 2] - times[:, 1]
+okc = dur_ticks > 500
+clock_ghz = float(np.median(cyc[okc] / dur_ticks[okc]) * 0.1)
+res = {"clock_ghz_median": clock_ghz, "n": n, "ms_devbench": ms.value, "span_us": span, "tasks": int(k), "workers": P,
+       "busy_frac": float(ex.sum() / (span * P)), "wait_frac": float(wt.sum() / (span * P))}
+names = {0: "DIAGX", 1: "TRSM", 2: "UPD"}
+for t in (0, 1, 2):
+    for b in sorted(set(nb[typ == t])):
+        m = (typ == t) & (nb == b)
+        diag = (tasks[:, 1] == tasks[:, 2])
+        key = f"{names[t]}{'' if t != 2 else '_nb' + str(b)}"
+        res[key] = {"count": int(m.sum()), "exec_us_mean": float(ex[m].mean()), "exec_us_p90": float(np.percentile(ex[m], 90)),
+                    "wait_us_mean": float(wt[m].mean())}
+        if t == 2:
+            md = m & diag
+            if md.any():
+                res[key]["diagtile_exec_us_mean"] = float(ex[md].mean())
+# DIAGX chain
+d = np.where(typ == 0)[0]
+order = np.argsort(tasks[d, 1])
+d = d[order]
+st = tk[d, 1]
+en = tk[d, 2]
+res["diagx_exec_mean_us"] = float((en - st).mean())
+gaps = st[1:] - en[:-1]
+res["diagx_gap_mean_us"] = float(gaps.mean())
+res["diagx_chain_first_last"] = [float(st[0]), float(en[-1])]
+# time profile: busy workers per 1 ms window
+bins = np.arange(0, span + 1000, 1000)
+busy = []
+for a in bins[:-1]:
+    b = a + 1000
+    ov = np.clip(np.minimum(tk[:, 2], b) - np.maximum(tk[:, 1], a), 0, None)
+    busy.append(round(float(ov.sum() / 1000 / P), 2))
+res["busy_per_ms"] = busy
+# late chain: k -> diag exec and gap for last 16
+res["diagx_last16"] = [[round(float(e - s_), 1), round(float(g), 1)] for s_, e, g in zip(st[-16:], en[-16:], np.r_[gaps, 0][-16:])]
+print(json.dumps(res, indent=1))
