@@ -53,7 +53,6 @@ namespace gprx {
 namespace pt {
 
 constexpr int NT = 512;     // threads per workgroup
-constexpr int BK = 32;      // k depth per LDS stage
 constexpr int PAD = 16;     // LDS row pad (elements)
 constexpr int SR = GT + PAD;
 
@@ -87,9 +86,43 @@ struct Mfma<float> {
     __device__ static inline int orow(int lk, int reg) { return 4 * lk + reg; }
 };
 
+// Operand staging: global_load_lds_dwordx4 (LDS-DMA, no VGPRs) into a ring of NBUF stage
+// buffers of BKS k-columns; loads run 3 stages ahead of the MFMAs and stay in flight across
+// the per-stage barrier (raw s_barrier + counted vmcnt: a __syncthreads() would drain them).
+// One wave-instruction moves 64 x 16 B = 1 KiB = one 128-row f64 column (two f32 columns),
+// written contiguously at a wave-uniform LDS base; columns (column pairs) are PAD apart.
+#ifndef GPRX_PT_BKS
+#define GPRX_PT_BKS 16
+#define GPRX_PT_NBUF 4
+#endif
+constexpr int BKS = GPRX_PT_BKS;
+constexpr int NBUF = GPRX_PT_NBUF;
+constexpr int AHEAD = NBUF - 1;  // stages in flight ahead of the one being computed
+
+template <typename T>
+struct Stage {
+    static constexpr int E = 16 / sizeof(T);     // elements per lane per load
+    static constexpr int LPC = GT / E;           // lanes per column
+    static constexpr int CPI = 64 / LPC;         // columns per wave-instruction
+    static constexpr int SRP = CPI * GT + PAD;   // LDS elements per instruction slot
+    static constexpr int GRP = BKS / CPI;        // instructions per operand per stage
+    static constexpr int IPW = 2 * GRP / 8;      // instructions per wave per stage
+    static constexpr int STG = 2 * GRP * SRP;    // elements per stage buffer (A slots, then B)
+};
+
 template <typename T>
 constexpr size_t gemm_lds() {
-    return sizeof(T) * 2 * 2 * BK * SR;
+    return sizeof(T) * NBUF * Stage<T>::STG;
+}
+
+template <typename T>
+__device__ __forceinline__ void st_sc1(T* p, T v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // global_store ... sc1
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
 // ------------------------------------------------------------------------------------------
@@ -105,36 +138,24 @@ __device__ __forceinline__ void tile_gemm(T* __restrict__ C, int64_t ldc, const 
                                           const int t) {
     typedef Mfma<T> Tr;
     typedef typename Tr::acc_t acc_t;
-    typedef typename Tr::vec_t vec_t;
-    constexpr int VEC = Tr::VEC;
-    constexpr int TPC = GT / VEC;       // threads per staged column
-    constexpr int CPP = NT / TPC;       // columns per pass
-    constexpr int PASSES = BK / CPP;
-    static_assert(BK % CPP == 0, "staging");
-
-    T* sA = smem;                  // [2][BK][SR]
-    T* sB = smem + 2 * BK * SR;    // [2][BK][SR]
+    typedef Stage<T> S;
     const int lane = t & 63, w = t >> 6;
     const int wr = w & 1, wc = w >> 1;
     const int lr = lane & 15, lk = lane >> 4;
-    const int st_row = (t % TPC) * VEC, st_col = t / TPC;
     const bool active = !(lower && wr == 0 && wc >= 2);
+    const int lcol = lane / S::LPC, lrow = (lane % S::LPC) * S::E;
 
-    vec_t ra[PASSES], rb[PASSES];
-    auto gload = [&](int k0) {
+    auto issue = [&](int st) {
+        T* buf = smem + (st % NBUF) * S::STG;
 #pragma unroll
-        for (int p = 0; p < PASSES; p++) {
-            const int64_t kk = k0 + st_col + p * CPP;
-            ra[p] = *reinterpret_cast<const vec_t*>(A + st_row + kk * lda);
-            rb[p] = *reinterpret_cast<const vec_t*>(B + st_row + kk * ldb);
-        }
-    };
-    auto lstore = [&](int buf) {
-#pragma unroll
-        for (int p = 0; p < PASSES; p++) {
-            const int kk = st_col + p * CPP;
-            *reinterpret_cast<vec_t*>(sA + (buf * BK + kk) * SR + st_row) = ra[p];
-            *reinterpret_cast<vec_t*>(sB + (buf * BK + kk) * SR + st_row) = rb[p];
+        for (int u = 0; u < S::IPW; u++) {
+            const int g = w * S::IPW + u;  // wave-uniform slot: A 0..GRP-1, B GRP..2GRP-1
+            const bool isB = g >= S::GRP;
+            const int gg = isB ? g - S::GRP : g;
+            const int64_t col = (int64_t)st * BKS + gg * S::CPI + lcol;
+            const T* src = isB ? (B + lrow + col * ldb) : (A + lrow + col * lda);
+            __builtin_amdgcn_global_load_lds((const void*)src,
+                                             (__attribute__((address_space(3))) void*)(buf + g * S::SRP), 16, 0, 0);
         }
     };
 
@@ -144,11 +165,11 @@ __device__ __forceinline__ void tile_gemm(T* __restrict__ C, int64_t ldc, const 
 #pragma unroll
         for (int y = 0; y < 4; y++) acc[x][y] = acc_t{0};
 
-    const int nstage = K / BK;
-    // UPDATE: the whole C tile is fetched into registers before any store (a load-store-load
-    // sequence per element would serialise on possible aliasing)
+    // UPDATE: the whole C tile is fetched into registers up front (its latency hides under the
+    // mainloop; loading it unconditionally, all before any store, avoids hipcc's per-element
+    // branches and vmcnt(0) waits)
     T cv[2][4][4];
-    auto cload = [&]() {
+    if (UPDATE && active) {
 #pragma unroll
         for (int x = 0; x < 2; x++)
 #pragma unroll
@@ -156,41 +177,53 @@ __device__ __forceinline__ void tile_gemm(T* __restrict__ C, int64_t ldc, const 
                 const int jl = wc * 32 + x * 16 + Tr::orow(lk, reg);
                 const T* ccol = C + (int64_t)jl * ldc;
 #pragma unroll
-                for (int y = 0; y < 4; y++) {
-                    const int il = wr * 64 + y * 16 + lr;
-                    cv[x][y][reg] = (lower && il < jl) ? T(0) : ccol[il];
-                }
+                for (int y = 0; y < 4; y++) cv[x][y][reg] = ccol[wr * 64 + y * 16 + lr];
             }
-    };
-    gload(0);
-    lstore(0);
-    __syncthreads();
+    }
+    const int nst = K / BKS;
+#pragma unroll
+    for (int p = 0; p < AHEAD; p++)
+        if (p < nst) issue(p);
 #pragma nounroll
-    for (int s = 0; s < nstage; s++) {
-        const int buf = s & 1;
-        if (s + 1 < nstage) gload((s + 1) * BK);
+    for (int st = 0; st < nst; st++) {
+        // this wave's loads of stage st have landed (later stages may stay in flight) ...
+        const int ahead = nst - 1 - st;
+        if (AHEAD >= 3 && ahead >= 2) wait_vm<(AHEAD >= 3 ? 2 : 0) * S::IPW>();
+        else if (AHEAD >= 2 && ahead >= 1) wait_vm<S::IPW>();
+        else wait_vm<0>();
+        // ... and every wave's, and every wave is done reading the buffer refilled next
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (st + AHEAD < nst) issue(st + AHEAD);
         if (active) {
-            const T* a = sA + buf * BK * SR;
-            const T* b = sB + buf * BK * SR;
-#pragma unroll
-            for (int kq = 0; kq < BK / 4; kq++) {
+            // fragments of step kq+1 are read while the MFMAs of step kq run (one LDS latency
+            // per stage instead of one per 4-deep step)
+            const T* a = smem + (st % NBUF) * S::STG;
+            const T* b = a + S::GRP * S::SRP;
+            T fa[2][4], fb[2][2];
+            auto frag = [&](int kq, int r) {
                 const int kr = kq * 4 + lk;
-                T fa[4], fb[2];
+                const int ko = (kr / S::CPI) * S::SRP + (kr % S::CPI) * GT;
 #pragma unroll
-                for (int x = 0; x < 2; x++) fb[x] = b[kr * SR + wc * 32 + x * 16 + lr];
+                for (int x = 0; x < 2; x++) fb[r][x] = b[ko + wc * 32 + x * 16 + lr];
 #pragma unroll
-                for (int y = 0; y < 4; y++) fa[y] = a[kr * SR + wr * 64 + y * 16 + lr];
+                for (int y = 0; y < 4; y++) fa[r][y] = a[ko + wr * 64 + y * 16 + lr];
+            };
+            frag(0, 0);
+#pragma unroll
+            for (int kq = 0; kq < BKS / 4; kq++) {
+                if (kq + 1 < BKS / 4) frag(kq + 1, (kq + 1) & 1);
+                __builtin_amdgcn_sched_barrier(0);  // keep those reads ahead of these MFMAs
 #pragma unroll
                 for (int x = 0; x < 2; x++)
 #pragma unroll
-                    for (int y = 0; y < 4; y++) acc[x][y] = Tr::mma(fb[x], fa[y], acc[x][y]);
+                    for (int y = 0; y < 4; y++) acc[x][y] = Tr::mma(fb[kq & 1][x], fa[kq & 1][y], acc[x][y]);
             }
         }
-        if (s + 1 < nstage) lstore(buf ^ 1);
-        __syncthreads();
     }
+    // UPDATE: the whole C tile is fetched into registers before any store (a load-store-load
+    // sequence per element would serialise on possible aliasing)
     if (!active) return;
-    if (UPDATE) cload();
 #pragma unroll
     for (int x = 0; x < 2; x++) {
 #pragma unroll
@@ -200,9 +233,13 @@ __device__ __forceinline__ void tile_gemm(T* __restrict__ C, int64_t ldc, const 
 #pragma unroll
             for (int y = 0; y < 4; y++) {
                 const int il = wr * 64 + y * 16 + lr;
-                if (lower && il < jl) continue;
-                if (UPDATE) ccol[il] = cv[x][y][reg] - acc[x][y][reg];
-                else ccol[il] = acc[x][y][reg];
+                // stores are unconditional (a branch per element makes hipcc wait for every
+                // previous store); above the diagonal of a diagonal tile the old value goes back.
+                // sc1 (write-through) stores: the hand-off needs no L2 write-back fence
+                if (UPDATE)
+                    st_sc1(ccol + il, (lower && il < jl) ? cv[x][y][reg] : cv[x][y][reg] - acc[x][y][reg]);
+                else if (!lower || il >= jl)
+                    st_sc1(ccol + il, acc[x][y][reg]);
             }
         }
     }
@@ -412,11 +449,13 @@ __device__ __forceinline__ void st_agent(int* p, int v) {
 // next iteration's barrier (a hang).
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 
-__device__ __forceinline__ void publish(int* flag, int v, int variant = 0) {
+// release = false: every handed-off byte was stored sc1 (tile_gemm), so draining the stores
+// (vmcnt(0) in every wave, then the barrier) is the release; the consumer still acquires.
+__device__ __forceinline__ void publish(int* flag, int v, bool release) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (wave_id() == 0) {
-        if (!(variant & 16)) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        if (release) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         st_agent(flag, v);
     }
@@ -426,6 +465,11 @@ __device__ __forceinline__ void publish(int* flag, int v, int variant = 0) {
 __device__ __forceinline__ void local_sync() {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+}
+
+template <typename T>
+constexpr size_t pt_lds_bytes() {
+    return gemm_lds<T>() > diag_lds<T>() ? gemm_lds<T>() : diag_lds<T>();
 }
 
 template <typename T>
@@ -508,7 +552,9 @@ __device__ bool wait_inputs(const Args<T>& a, int type, int i, int j, int b0, in
 template <typename T>
 __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    __shared__ int s_q;
+    // ONE __shared__ array (a second __shared__ object can make hipcc drain the LDS-DMA
+    // pipeline with vmcnt(0)); the ticket word sits after the largest per-task image
+    int& s_q = *reinterpret_cast<int*>(smem_raw + pt_lds_bytes<T>());
     T* smem = reinterpret_cast<T*>(smem_raw);
     const int t = threadIdx.x;
     const int wv = wave_id();
@@ -547,23 +593,23 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
         if (type == T_UPD) {
             if (!(a.variant & 2)) tile_gemm<T, true>(Ci + (int64_t)j * GT * ld, ld, Ci + (int64_t)b0 * GT * ld, ld,
                                a.A + (int64_t)j * GT + (int64_t)b0 * GT * ld, ld, nb * GT, i == j, smem, tid);
-            publish(a.ver + (int64_t)i * a.nc + j, b0 + nb, a.variant);
+            publish(a.ver + (int64_t)i * a.nc + j, b0 + nb, false);
         } else if (type == T_TRSM) {
             T* Cik = Ci + (int64_t)j * GT * ld;
             if (!(a.variant & 1)) tile_gemm<T, false>(Cik, ld, Cik, ld, a.Linv + (int64_t)j * DB * DB, DB, GT, false, smem, tid);
-            publish(a.lcnt + i, j + 1);
+            publish(a.lcnt + i, j + 1, false);
         } else {  // DIAGX(k = i)
             const int k = i;
             T* Akk = Ci + (int64_t)k * GT * ld;
             if (k > 0) {
                 T* Akm = Ci + (int64_t)(k - 1) * GT * ld;
                 tile_gemm<T, false>(Akm, ld, Akm, ld, a.Linv + (int64_t)(k - 1) * DB * DB, DB, GT, false, smem, tid);
-                publish(a.lcnt + k, k);  // L_{k,k-1} final: unblocks the updates of column k
+                publish(a.lcnt + k, k, false);  // L_{k,k-1} final: unblocks the updates of column k
                 tile_gemm<T, true>(Akk, ld, Akm, ld, Akm, ld, GT, true, smem, tid);
                 local_sync();
             }
             if (!(a.variant & 4)) diag_factor<T>(Akk, ld, a.Linv + (int64_t)k * DB * DB, a.info, (int64_t)k * DB, smem_raw, tid, a.dbg);
-            publish(a.lcnt + k, k + 1);
+            publish(a.lcnt + k, k + 1, true);  // diag_factor stores are plain
         }
         if (a.trace && wv == 0) {
             long long* tp = a.trace + 4 * (int64_t)q;
@@ -883,13 +929,15 @@ void potrf_tiles(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info
     }
     // one wait may take at most 2 s + 20x the whole predicted factorisation
     a.tlimit = (long long)(1e8 * (2.0 + 20.0 * sd.est_us * 1e-6));
-    const size_t lds = std::max<size_t>(std::max(gemm_lds<T>(), diag_lds<T>()), 96 * 1024);
+    // + the ticket word; at least 96 KB so the launch stays at one workgroup per CU
+    auto lds_of = [](size_t b) { return std::max<size_t>(b + 16, 96 * 1024); };
+    const size_t lds = lds_of(pt_lds_bytes<T>());
     static bool attr = false;
     if (!attr) {
         GPRX_HIP(hipFuncSetAttribute((const void*)potrf_tiles_kernel<double>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     (int)std::max<size_t>(std::max(gemm_lds<double>(), diag_lds<double>()), 96 * 1024)));
+                                     (int)lds_of(pt_lds_bytes<double>())));
         GPRX_HIP(hipFuncSetAttribute((const void*)potrf_tiles_kernel<float>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     (int)std::max<size_t>(std::max(gemm_lds<float>(), diag_lds<float>()), 96 * 1024)));
+                                     (int)lds_of(pt_lds_bytes<float>())));
         attr = true;
     }
     const double nn = (double)np;

@@ -12,7 +12,7 @@ import numpy as np
 from .kernels import as_node
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libgprx.so")
+LIB_PATH = os.environ.get("GPRX_LIB_OVERRIDE") or os.path.join(_HERE, "lib", "libgprx.so")  # override: dev experiments only
 
 GPRX_F32 = 0
 GPRX_F64 = 1
