@@ -361,7 +361,8 @@ static gprx_status model_fit(gprx_model* M, uint32_t flags, gprx_fit_info* out) 
     }
     GPRX_HIP(hipEventRecord(ctx->ev[2], s));
     launch_fit_reductions<T>(M->A.as<T>(), ld, n, np, M->m, M->red.as<double>(), s);
-    launch_backsolve<T>(M->A.as<T>(), ld, np, M->m, M->Linv.as<T>(), M->z.as<T>(), M->alpha.as<T>(), s);
+    launch_backsolve_chain<T>(M->A.as<T>(), ld, np, M->m, M->Linv.as<T>(), M->alpha.as<T>(), M->info.as<int>(), ctx->ex,
+                              s);
     GPRX_HIP(hipEventRecord(ctx->ev[3], s));
     GPRX_HIP(hipStreamSynchronize(s));
     GPRX_HIP(hipGetLastError());

@@ -97,7 +97,7 @@ static gprx_status bench_impl(int what, int64_t M, int64_t N, int64_t K, int ite
             (void)hipEventSynchronize(e1);
             (void)hipEventElapsedTime(&tms, e0, e1);
             *ms = tms / iters;
-        } else if (what == 3 || what == 4 || what == 5 || what == 9) {
+        } else if (what == 3 || what == 4 || what == 5 || what == 9 || what == 10) {
             const int64_t n = M;
             T* A = (T*)alloc(sizeof(T) * n * n);
             T* Li = (T*)alloc(sizeof(T) * n * DB);
@@ -112,9 +112,10 @@ static gprx_status bench_impl(int what, int64_t M, int64_t N, int64_t K, int ite
                 hipLaunchKernelGGL(dev_fill_spd<T>, dim3((unsigned)((n * n + 255) / 256)), dim3(256), 0, s, A, n, n,
                                    (uint64_t)it);
                 (void)hipMemsetD32Async((hipDeviceptr_t)info, INT_MAX, 1, s);
-                if (what == 5) potrf_blocked<T>(A, n, n, n, Li, info, use);
+                if (what == 5 || what == 10) potrf_blocked<T>(A, n, n, n, Li, info, use);
                 (void)hipEventRecord(e0, s);
                 if (what == 5) launch_backsolve<T>(A, n, n - DB, 1, Li, z, al, s);
+                else if (what == 10) launch_backsolve_chain<T>(A, n, n - DB, 1, Li, al, info, ex, s);
                 else if (what == 9) potrf_tiles<T>(A, n, n, n, Li, info, ex);
                 else potrf_blocked<T>(A, n, n, n, Li, info, use);
                 (void)hipEventRecord(e1, s);

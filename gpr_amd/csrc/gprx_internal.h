@@ -306,6 +306,9 @@ struct Exec {
     hipStream_t s2 = nullptr;  // second look-ahead stream (next panel's later columns); may be null
     std::vector<hipEvent_t> ev;
     PtState* pt = nullptr;
+    int* scratch = nullptr;  // device ints for in-launch counters/flags (grown on demand)
+    size_t scratch_n = 0;
+    int* scratch_ints(size_t n);
     hipEvent_t event(size_t i);
     ~Exec();
 };
@@ -342,6 +345,12 @@ void launch_gemm_nt_splitk(T* C, int64_t ldc, int64_t cstride, const T* A, int64
 // alpha: np x m, ld m).  Uses the diagonal-block inverses.
 template <typename T>
 void launch_backsolve(const T* A, int64_t ld, int64_t np, int m, const T* Linv, T* z, T* alpha, hipStream_t s);
+
+// Same solve in one launch: one workgroup per 128-block, chained by flags (k_bsolve.hip).
+// z is read from the label rows np..np+m-1 of A (ld).  A timed-out wait sets *info = -1.
+template <typename T>
+void launch_backsolve_chain(const T* A, int64_t ld, int64_t np, int m, const T* Linv, T* alpha, int* info, Exec& ex,
+                            hipStream_t s);
 
 // logdet partial = 2 sum log L_ii over i < n, datafit = sum of squares of the augmented
 // rows; results accumulated in double on the device (out[0], out[1]).

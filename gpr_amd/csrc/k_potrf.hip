@@ -580,6 +580,17 @@ hipEvent_t Exec::event(size_t i) {
 Exec::~Exec() {
     for (auto e : ev) (void)hipEventDestroy(e);
     pt_state_free(pt);
+    if (scratch) (void)hipFree(scratch);
+}
+
+int* Exec::scratch_ints(size_t n) {
+    if (n > scratch_n) {
+        if (scratch) GPRX_HIP(hipFree(scratch));
+        scratch = nullptr;
+        GPRX_HIP(hipMalloc(&scratch, sizeof(int) * n));
+        scratch_n = n;
+    }
+    return scratch;
 }
 
 template <typename T>

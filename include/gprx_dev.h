@@ -15,7 +15,8 @@ extern "C" {
  *       6 = diagonal kernel phase profile: ms must hold 5 doubles, receiving the mean
  *           s_memtime ticks per launch of (load, solve phases, update phases, store, total),
  *       7 = potrf with look-ahead replayed from a captured hipGraph, 8 = backsolve from a graph,
- *       9 = potrf as one persistent tile-dataflow launch (potrf_tiles).
+ *       9 = potrf as one persistent tile-dataflow launch (potrf_tiles),
+ *      10 = back substitution as one flag-chained launch (launch_backsolve_chain).
  * For 1/2: (M, N, K) are the gemm sizes; for 3/4/5: M = n.  Returns the mean device time
  * per call over `iters` calls (HIP events) in *ms. */
 gprx_status gprx_dev_bench(gprx_ctx* ctx, gprx_dtype dtype, int32_t what, int64_t M, int64_t N, int64_t K,
