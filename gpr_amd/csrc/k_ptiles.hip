@@ -295,7 +295,9 @@ __device__ __forceinline__ void dbg_mark(int* dbg, int q, int phase, int i, int 
 
 template <typename T>
 __device__ __forceinline__ void diag_factor(T* __restrict__ A, int64_t ld, T* __restrict__ Linv, int* __restrict__ info,
-                                            int64_t col0, unsigned char* smem_raw, const int t, int* dbg = nullptr) {
+                                            int64_t col0, unsigned char* smem_raw, const int t, int* dbg = nullptr,
+                                            long long* prof = nullptr) {
+    long long pt0 = prof ? wall_clock64() : 0, pacc1 = 0, pacc2 = 0, pm = 0;
     T(*sV)[SPL] = reinterpret_cast<T(*)[SPL]>(smem_raw);
     T(*sP)[SPL] = reinterpret_cast<T(*)[SPL]>(smem_raw + sizeof(T) * 8 * SPL);
     T(*sLdW)[8][9] = reinterpret_cast<T(*)[8][9]>(smem_raw + sizeof(T) * 16 * SPL);  // per wave 0/1
@@ -321,6 +323,8 @@ __device__ __forceinline__ void diag_factor(T* __restrict__ A, int64_t ld, T* __
             for (int b = 0; b < 8; b++) sV[b][R0 + a] = S[a][b];
     }
     __syncthreads();
+    if (prof) pm = wall_clock64();
+    const long long pload = pm;
 
     int fail_col = -1;
     for (int j0 = 0; j0 < DB; j0 += 8) {
@@ -339,15 +343,18 @@ __device__ __forceinline__ void diag_factor(T* __restrict__ A, int64_t ld, T* __
                     if (!(dsum > T(0)) && fail_col < 0) fail_col = j0 + c;
                     const T ri = rsqrt_full(dsum);
                     Ld[c][c] = dsum * ri;
-                    myLd[c][8] = ri;
-                    myLd[c][c] = Ld[c][c];
 #pragma unroll
                     for (int r = c + 1; r < 8; r++) {
                         T v = sV[c][j0 + r];
 #pragma unroll
                         for (int k = 0; k < c; k++) v = fma(-Ld[r][k], Ld[c][k], v);
                         Ld[r][c] = v * ri;
-                        myLd[r][c] = Ld[r][c];
+                    }
+                    // one lane per wave writes (64 lanes storing one word serialise in the LDS)
+                    if (l == 0) {
+                        myLd[c][8] = ri;
+#pragma unroll
+                        for (int r = c; r < 8; r++) myLd[r][c] = Ld[r][c];
                     }
                 }
             }
@@ -365,6 +372,11 @@ __device__ __forceinline__ void diag_factor(T* __restrict__ A, int64_t ld, T* __
             for (int q = 0; q < 8; q++) sP[q][row] = x[q];
         }
         __syncthreads();
+        if (prof) {
+            const long long tn = wall_clock64();
+            pacc1 += tn - pm;
+            pm = tn;
+        }
         const bool pivrows = R0 >= j0 && R0 < jn;
         if (cbi == (j0 >> 3)) {
             if (pivrows) {
@@ -412,6 +424,16 @@ __device__ __forceinline__ void diag_factor(T* __restrict__ A, int64_t ld, T* __
                 for (int b = 0; b < 8; b++) sV[b][R0 + a] = S[a][b];
         }
         __syncthreads();
+        if (prof) {
+            const long long tn = wall_clock64();
+            pacc2 += tn - pm;
+            pm = tn;
+        }
+    }
+    if (prof && t == 0) {
+        prof[0] = pload - pt0;
+        prof[1] = pacc1;
+        prof[2] = pacc2;
     }
     if (fail_col >= 0) atomicMin(info, (int)(col0 + fail_col + 1));  // same value in every lane of waves 0-1
 
@@ -601,15 +623,25 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
         } else {  // DIAGX(k = i)
             const int k = i;
             T* Akk = Ci + (int64_t)k * GT * ld;
+            long long dt[4] = {0, 0, 0, 0};
             if (k > 0) {
                 T* Akm = Ci + (int64_t)(k - 1) * GT * ld;
                 tile_gemm<T, false>(Akm, ld, Akm, ld, a.Linv + (int64_t)(k - 1) * DB * DB, DB, GT, false, smem, tid);
+                if (a.trace) dt[0] = wall_clock64();
                 publish(a.lcnt + k, k, false);  // L_{k,k-1} final: unblocks the updates of column k
+                if (a.trace) dt[1] = wall_clock64();
                 tile_gemm<T, true>(Akk, ld, Akm, ld, Akm, ld, GT, true, smem, tid);
                 local_sync();
             }
-            if (!(a.variant & 4)) diag_factor<T>(Akk, ld, a.Linv + (int64_t)k * DB * DB, a.info, (int64_t)k * DB, smem_raw, tid, a.dbg);
+            if (a.trace) dt[2] = wall_clock64();
+            diag_factor<T>(Akk, ld, a.Linv + (int64_t)k * DB * DB, a.info, (int64_t)k * DB, smem_raw, tid, a.dbg,
+                           a.trace ? a.trace + 4 * (int64_t)(a.ntasks + a.nc) + 4 * (int64_t)k : nullptr);
+            if (a.trace) dt[3] = wall_clock64();
             publish(a.lcnt + k, k + 1, true);  // diag_factor stores are plain
+            if (a.trace && wv == 0) {
+                long long* dp = a.trace + 4 * (int64_t)a.ntasks + 4 * (int64_t)k;
+                for (int u = 0; u < 4; u++) dp[u] = dt[u];
+            }
         }
         if (a.trace && wv == 0) {
             long long* tp = a.trace + 4 * (int64_t)q;
@@ -821,8 +853,8 @@ struct PtState {
     size_t ctr_ints = 0;
     int ncu = 0;
     int* dbg = nullptr;  // pinned host status words (GPRX_PT_DEBUG)
-    long long* trace = nullptr;  // GPRX_PT_TRACE timeline of the last launch
-    int64_t trace_n = 0;
+    long long* trace = nullptr;  // GPRX_PT_TRACE timeline of the last launch (+ DIAGX phases)
+    int64_t trace_n = 0, trace_nc = 0;
     const std::vector<int4>* last_list = nullptr;
     ~PtState() {
         if (trace) (void)hipFree(trace);
@@ -839,7 +871,7 @@ void pt_state_free(PtState* p) { delete p; }
 static PtState* g_pt_state = nullptr;
 int64_t pt_trace_copy(int32_t* tasks, long long* times, int64_t max) {
     if (!g_pt_state || !g_pt_state->trace || !g_pt_state->last_list) return 0;
-    const int64_t n = std::min<int64_t>(max, g_pt_state->trace_n);
+    const int64_t n = std::min<int64_t>(max, g_pt_state->trace_n + 2 * g_pt_state->trace_nc);
     GPRX_HIP(hipDeviceSynchronize());
     GPRX_HIP(hipMemcpy(times, g_pt_state->trace, sizeof(long long) * 4 * n, hipMemcpyDeviceToHost));
     std::memcpy(tasks, g_pt_state->last_list->data(), sizeof(int4) * n);
@@ -908,11 +940,12 @@ void potrf_tiles(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info
     a.trace = nullptr;
     static const bool tracing = std::getenv("GPRX_PT_TRACE") != nullptr;
     if (tracing) {
-        if (st.trace_n < sd.n) {
+        if (st.trace_n + 2 * st.trace_nc < sd.n + 2 * nc) {
             if (st.trace) GPRX_HIP(hipFree(st.trace));
-            GPRX_HIP(hipMalloc(&st.trace, sizeof(long long) * 4 * sd.n));
+            GPRX_HIP(hipMalloc(&st.trace, sizeof(long long) * 4 * (sd.n + 2 * nc)));
         }
         st.trace_n = sd.n;
+        st.trace_nc = nc;
         a.trace = st.trace;
         g_pt_state = &st;
         st.last_list = &sd.host;

@@ -20,7 +20,12 @@ MAX = 400000
 tasks = np.zeros((MAX, 4), np.int32)
 times = np.zeros((MAX, 4), np.int64)
 k = L.gprx_dev_pt_trace(tasks.ctypes.data, times.ctypes.data, MAX)
-tasks, times = tasks[:k], times[:k]
+ntask = int(((k - 1) // 1))
+# the last nc rows of `times` are DIAGX phase stamps {trsm done, published, syrk done, diag done}
+nc = n // 128
+dprof = times[k - nc:k].copy()          # diag_factor {load, pivot phases, update phases} ticks
+dph = times[k - 2 * nc:k - nc].copy()
+tasks, times = tasks[:k - 2 * nc], times[:k - 2 * nc]
 out = os.environ.get("PT_TRACE_OUT")
 if out:
     np.savez_compressed(out, tasks=tasks, times=times)
@@ -69,5 +74,13 @@ for a in bins[:-1]:
     busy.append(round(float(ov.sum() / 1000 / P), 2))
 res["busy_per_ms"] = busy
 # late chain: k -> diag exec and gap for last 16
+dv = dph[1:]
+res["diagx_phase_us"] = {"trsm_tile": float(np.mean((dv[:, 0] - (times[d[1:], 1])) / 100.0)),
+                         "publish": float(np.mean((dv[:, 1] - dv[:, 0]) / 100.0)),
+                         "syrk_tile": float(np.mean((dv[:, 2] - dv[:, 1]) / 100.0)),
+                         "diag_factor": float(np.mean((dv[:, 3] - dv[:, 2]) / 100.0)),
+                         "final_publish": float(np.mean((times[d[1:], 2] - dv[:, 3]) / 100.0))}
+res["diag_factor_us"] = {"load": float(dprof[:, 0].mean() / 100), "pivot_solve": float(dprof[:, 1].mean() / 100),
+                         "update": float(dprof[:, 2].mean() / 100)}
 res["diagx_last16"] = [[round(float(e - s_), 1), round(float(g), 1)] for s_, e, g in zip(st[-16:], en[-16:], np.r_[gaps, 0][-16:])]
 print(json.dumps(res, indent=1))
