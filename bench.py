@@ -65,21 +65,21 @@ def cpu_baseline(cfg, n_cpu):
     }
 
 
-def traffic_from_profile():
+def traffic_from_profile(kernel="potrf_tiles_kernel<double>"):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC passes
     (profiles/*_pmc_traffic.json, written by scripts/pmc_traffic.py: FETCH_SIZE x 2 (gfx950
     wide-read correction, MI355X_MICROARCH.md §HBM) + WRITE_SIZE, averaged over launches)."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
-    if not files:
-        return None
-    try:
-        with open(files[-1]) as f:
-            t = json.load(f)
-        k = t["kernels"].get("gemm_nt_kernel<double, true, true, false>")
-        return None if k is None else {"bytes_per_launch": k["hbm_bytes_per_launch"], "source": os.path.basename(files[-1])}
-    except Exception:
-        return None
+    for path in reversed(files):
+        try:
+            with open(path) as f:
+                k = json.load(f)["kernels"].get(kernel)
+        except Exception:
+            continue
+        if k is not None:
+            return {"bytes_per_launch": k["hbm_bytes_per_launch"], "source": os.path.basename(path)}
+    return None
 
 
 def main():
@@ -171,8 +171,12 @@ def main():
         pred = {"q": args.predict_q, "pts_per_s_device": args.predict_q / (ps["ms"] * 1e-3) if ps else None,
                 "pts_per_s_wall_incl_pcie": args.predict_q / tq}
 
-    upd = stats.get("potrf_update", {"ms": 0, "flops": 0, "launches": 0})
-    achieved = (upd["flops"] / (upd["ms"] * 1e-3) / 1e12) if upd["ms"] > 0 else 0.0
+    # dominant kernel: the persistent tile-dataflow factorisation, one launch per fit.
+    # Algorithmic work per launch = n^3/3 (Cholesky) + m n^2 (forward solve of the label rows).
+    fac = stats.get("potrf_tiles", {"ms": 0, "flops": 0, "launches": 0})
+    alg_flops = n ** 3 / 3.0 + m * float(n) ** 2
+    avg_ms = (fac["ms"] / fac["launches"]) if fac["launches"] else 0.0
+    achieved = (alg_flops / (avg_ms * 1e-3) / 1e12) if avg_ms > 0 else 0.0
     phases = {k: {"ms_per_fit": v["ms"] / args.steps, "launches_per_fit": v["launches"] / args.steps,
                   "tflops": (v["flops"] / (v["ms"] * 1e-3) / 1e12) if v["ms"] and v["flops"] else None,
                   "gbs": (v["bytes"] / (v["ms"] * 1e-3) / 1e9) if v["ms"] and v["bytes"] else None}
@@ -205,12 +209,12 @@ def main():
                        "n": n, "d": d, "m": m, "kernel": cfg["kernel"],
                        "parallelism": (f"panel-cyclic factorisation over {world} GPUs (RCCL)" if distributed_fit
                                        else ("replicas" if world > 1 else "single-gpu"))},
-            "roofline": {"bound": "mfma", "kernel": "gemm_nt_kernel<double,true,true,false> (potrf_update: "
-                                                      "trailing / look-ahead / in-panel updates)",
+            "roofline": {"bound": "mfma", "kernel": "potrf_tiles_kernel<double> (persistent tile-dataflow "
+                                                      "Cholesky + forward solve, k_ptiles.hip)",
                          "achieved": achieved, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved / PEAK_FP64_TFLOPS,
-                         "avg_launch_us": (1e3 * upd["ms"] / upd["launches"]) if upd["launches"] else None,
-                         "algorithmic_flops_per_launch": (upd["flops"] / upd["launches"]) if upd["launches"] else None,
+                         "avg_launch_us": 1e3 * avg_ms if avg_ms else None,
+                         "algorithmic_flops_per_launch": alg_flops,
                          "traffic": traffic_from_profile()},
             "fit_roofline": {"t_roof_ms": t_roof, "t_fit_device_ms": fit_ms, "frac": t_roof / fit_ms},
             "phases": phases,

@@ -1132,7 +1132,7 @@ gprx_status gprx_spd_inverse(gprx_ctx* ctx, gprx_dtype dt, void* A, int64_t n, i
 
 static const char* kclass_name(int c) {
     static const char* names[KC_COUNT] = {"kbuild", "potrf_diag", "potrf_trsm", "potrf_update", "backsolve",
-                                          "predict", "lml_grad", "spd_inverse", "other_gemm"};
+                                          "predict", "lml_grad", "spd_inverse", "other_gemm", "potrf_tiles"};
     return names[c];
 }
 

@@ -974,7 +974,7 @@ void potrf_tiles(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info
         attr = true;
     }
     const double nn = (double)np;
-    ProfScope ps(KC_UPDATE, s, nn * nn * nn / 3.0 + (double)(nrows - np) * nn * nn, 0.0);
+    ProfScope ps(KC_TILES, s, nn * nn * nn / 3.0 + (double)(nrows - np) * nn * nn, 0.0);
     hipLaunchKernelGGL(potrf_tiles_kernel<T>, dim3((unsigned)st.ncu), dim3(NT), lds, s, a);
     GPRX_HIP(hipGetLastError());
 }

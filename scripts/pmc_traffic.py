@@ -16,7 +16,7 @@ from collections import defaultdict
 
 
 def short(name):
-    m = re.match(r"(?:void )?(?:gprx::)?([A-Za-z_0-9]+<[^()]*>|[A-Za-z_0-9]+)", name)
+    m = re.match(r"(?:void )?(?:[A-Za-z_0-9]+::)*([A-Za-z_0-9]+<[^()]*>|[A-Za-z_0-9]+)", name)
     return m.group(1) if m else name
 
 
