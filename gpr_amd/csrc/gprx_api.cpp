@@ -238,7 +238,7 @@ struct gprx_model {
     gprx_kernel_desc desc{};
     KCanon<double> kd{};
     KCanon<float> kf{};
-    DevBuf X, Y, tab, A, Linv, z, alpha, info, flag, red, V, C, scratch1, scratch2, grad, pack;
+    DevBuf X, Y, tab, A, Linv, z, alpha, info, flag, red, V, C, scratch1, scratch2, grad, pack, featU, featV, kdev;
     std::mutex mu;
 };
 
@@ -314,7 +314,20 @@ static gprx_status model_fit(gprx_model* M, uint32_t flags, gprx_fit_info* out) 
     const T sig = (T)M->sigma;
     const T sigma2 = sig * sig;  // m_Sigma*m_Sigma in T (lib/GaussianProcess.cpp:379)
     GPRX_HIP(hipEventRecord(ctx->ev[0], s));
-    if (!dist || ctx->world == 1) {
+    static const bool direct_build = std::getenv("GPRX_KBUILD") && std::string(std::getenv("GPRX_KBUILD")) == "direct";
+    if ((!dist || ctx->world == 1) && !direct_build && pairs_mma_supported<T>(K, 1)) {
+        // pair statistics on the MFMA units from per-sample features (k_pairs.hip)
+        const int64_t kf = pairs_feature_cols<T>(K, M->d);
+        M->featU.ensure(sizeof(T) * np * kf);
+        M->featV.ensure(sizeof(T) * np * kf);
+        launch_pair_features<T>(K, M->X.as<T>(), n, M->d, M->X.as<T>(), false, M->featU.as<T>(), np, s);
+        launch_pair_features<T>(K, M->X.as<T>(), n, M->d, M->X.as<T>(), true, M->featV.as<T>(), np, s);
+        M->kdev.ensure(sizeof(KCanon<T>));
+        GPRX_HIP(hipMemcpyAsync(M->kdev.p, &K, sizeof(KCanon<T>), hipMemcpyHostToDevice, s));
+        launch_kbuild_mma<T>(K, M->kdev.as<KCanon<T>>(), M->featU.as<T>(), M->featV.as<T>(), np, M->d, M->A.as<T>(), ld,
+                             n, sigma2, M->flag.as<int>(), s);
+        launch_aug_rows<T>(M->Y.as<T>(), n, M->m, M->A.as<T>(), ld, np, mp, s);
+    } else if (!dist || ctx->world == 1) {
         launch_kbuild<T>(K, M->X.as<T>(), M->tab.as<T>(), n, M->X.as<T>(), M->tab.as<T>(), n, M->d, M->A.as<T>(), ld,
                          np, true, sigma2, M->flag.as<int>(), s);
         launch_aug_rows<T>(M->Y.as<T>(), n, M->m, M->A.as<T>(), ld, np, mp, s);
@@ -437,6 +450,22 @@ static gprx_status model_predict(gprx_model* M, const void* Xq, int64_t q, void*
         launch_sincos_tables<T>(K, dq.as<T>(), q, d, dtab.as<T>(), s);
     }
     dmean.ensure(sizeof(T) * q * m);
+    static const bool direct_pred = std::getenv("GPRX_PREDICT") && std::string(std::getenv("GPRX_PREDICT")) == "direct";
+    if (!deriv && !direct_pred && pairs_mma_supported<T>(K, m)) {
+        // mean only: MFMA pair statistics, K(Xq, X) never materialised (k_pairs.hip)
+        const int64_t kf = pairs_feature_cols<T>(K, d), qp = round_up(q, GT), npf = round_up(M->n, GT);
+        DevBuf fq;
+        fq.ensure(sizeof(T) * qp * kf);
+        M->featV.ensure(sizeof(T) * npf * kf);
+        launch_pair_features<T>(K, M->X.as<T>(), M->n, d, M->X.as<T>(), true, M->featV.as<T>(), npf, s);
+        launch_pair_features<T>(K, dq.as<T>(), q, d, M->X.as<T>(), false, fq.as<T>(), qp, s);
+        M->kdev.ensure(sizeof(KCanon<T>));
+        GPRX_HIP(hipMemcpyAsync(M->kdev.p, &K, sizeof(KCanon<T>), hipMemcpyHostToDevice, s));
+        launch_predict_mma<T>(K, M->kdev.as<KCanon<T>>(), fq.as<T>(), qp, M->featV.as<T>(), npf, d, M->alpha.as<T>(),
+                              M->n, m, q, dmean.as<T>(), s);
+        download(mean, dmean.p, sizeof(T) * q * m, s);
+        return GPRX_OK;
+    }
     if (deriv) dder.ensure(sizeof(T) * q * d * m);
     const int64_t ncz = (int64_t)m * (deriv ? (1 + d) : 1);
     M->scratch1.ensure(sizeof(T) * M->n * ncz);

@@ -279,6 +279,24 @@ void launch_kbuild(const KCanon<T>& K, const T* Xa, const T* tabA, int64_t na, c
                    int64_t nb, int d, T* A, int64_t ld, int64_t npad, bool lower, T sigma2, int* flag,
                    hipStream_t s);
 
+// MFMA pair statistics (k_pairs.hip): kernels without White leaves and with at most one
+// periodic frequency build their covariance / predict their mean from per-sample feature
+// matrices (np rows x pairs_feature_cols columns, column-major) and 128x128 MFMA tiles.
+template <typename T>
+bool pairs_mma_supported(const KCanon<T>& K, int m);
+template <typename T>
+int64_t pairs_feature_cols(const KCanon<T>& K, int d);
+template <typename T>
+void launch_pair_features(const KCanon<T>& K, const T* X, int64_t n, int d, const T* center, bool right, T* F,
+                          int64_t np, hipStream_t s);
+// Kd: a device copy of K (the kernels read the tree from memory)
+template <typename T>
+void launch_kbuild_mma(const KCanon<T>& K, const KCanon<T>* Kd, const T* FU, const T* FV, int64_t nf, int d, T* A,
+                       int64_t ld, int64_t n, T sigma2, int* flag, hipStream_t s);
+template <typename T>
+void launch_predict_mma(const KCanon<T>& K, const KCanon<T>* Kd, const T* FU, int64_t nfu, const T* FV, int64_t nfv,
+                        int d, const T* alpha, int64_t n, int m, int64_t q, T* mean, hipStream_t s);
+
 // Stacked derivative matrices (tests): D[p] (n x n, column-major, ld = n).
 template <typename T>
 void launch_deriv_matrix(const KCanon<T>& K, const T* X, const T* tab, int64_t n, int d, T* D, hipStream_t s);

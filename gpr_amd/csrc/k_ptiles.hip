@@ -38,6 +38,7 @@
 // operands staged 32-deep through LDS, double-buffered; 147 KB of LDS per workgroup also
 // keeps the launch at one workgroup per CU, so the critical DIAGX step has a whole CU.
 #include "gprx_internal.h"
+#include "k_mma.h"
 
 #include <algorithm>
 #include <climits>
@@ -52,85 +53,12 @@ namespace gprx {
 
 namespace pt {
 
-constexpr int NT = 512;     // threads per workgroup
-constexpr int PAD = 16;     // LDS row pad (elements)
-constexpr int SR = GT + PAD;
-
-enum { T_DIAGX = 0, T_TRSM = 1, T_UPD = 2 };
-enum { C_TICKET = 0, C_ERR = 1, C_NCTL = 16 };  // control words at the head of the counter block
-
-typedef double d4_t __attribute__((ext_vector_type(4)));
-typedef float f4_t __attribute__((ext_vector_type(4)));
-typedef double d2_t __attribute__((ext_vector_type(2)));
-
-template <typename T>
-struct Mfma;
-template <>
-struct Mfma<double> {
-    typedef d4_t acc_t;
-    typedef d2_t vec_t;
-    static constexpr int VEC = 2;
-    __device__ static inline acc_t mma(double a, double b, acc_t c) {
-        return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
-    }
-    __device__ static inline int orow(int lk, int reg) { return lk + 4 * reg; }
-};
-template <>
-struct Mfma<float> {
-    typedef f4_t acc_t;
-    typedef f4_t vec_t;
-    static constexpr int VEC = 4;
-    __device__ static inline acc_t mma(float a, float b, acc_t c) {
-        return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-    }
-    __device__ static inline int orow(int lk, int reg) { return 4 * lk + reg; }
-};
-
-// Operand staging: global_load_lds_dwordx4 (LDS-DMA, no VGPRs) into a ring of NBUF stage
-// buffers of BKS k-columns; loads run 3 stages ahead of the MFMAs and stay in flight across
-// the per-stage barrier (raw s_barrier + counted vmcnt: a __syncthreads() would drain them).
-// One wave-instruction moves 64 x 16 B = 1 KiB = one 128-row f64 column (two f32 columns),
-// written contiguously at a wave-uniform LDS base; columns (column pairs) are PAD apart.
-#ifndef GPRX_PT_BKS
-#define GPRX_PT_BKS 16
-#define GPRX_PT_NBUF 4
-#endif
-constexpr int BKS = GPRX_PT_BKS;
-constexpr int NBUF = GPRX_PT_NBUF;
-constexpr int AHEAD = NBUF - 1;  // stages in flight ahead of the one being computed
-
-template <typename T>
-struct Stage {
-    static constexpr int E = 16 / sizeof(T);     // elements per lane per load
-    static constexpr int LPC = GT / E;           // lanes per column
-    static constexpr int CPI = 64 / LPC;         // columns per wave-instruction
-    static constexpr int SRP = CPI * GT + PAD;   // LDS elements per instruction slot
-    static constexpr int GRP = BKS / CPI;        // instructions per operand per stage
-    static constexpr int IPW = 2 * GRP / 8;      // instructions per wave per stage
-    static constexpr int STG = 2 * GRP * SRP;    // elements per stage buffer (A slots, then B)
-};
-
-template <typename T>
-constexpr size_t gemm_lds() {
-    return sizeof(T) * NBUF * Stage<T>::STG;
-}
-
-template <typename T>
-__device__ __forceinline__ void st_sc1(T* p, T v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // global_store ... sc1
-}
-
-template <int N>
-__device__ __forceinline__ void wait_vm() {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
+using namespace mm;
 
 // ------------------------------------------------------------------------------------------
 // One 128x128 tile:  C = A B^T (UPDATE = false)  or  C -= A B^T (UPDATE = true), K deep.
 // A: 128 rows x K (column-major, lda), B: 128 rows x K (ldb).  lower: diagonal tile, only
 // row >= col is stored and the waves wholly above the diagonal skip their MFMAs.
-// Wave w: rows 64*(w&1).., columns 32*(w>>1)..; acc[x][y][reg] = C(i = 64wr + 16y + lr,
-// j = 32wc + 16x + orow(lk, reg)).
 // ------------------------------------------------------------------------------------------
 template <typename T, bool UPDATE>
 __device__ __forceinline__ void tile_gemm(T* __restrict__ C, int64_t ldc, const T* __restrict__ A, int64_t lda,
@@ -138,33 +66,10 @@ __device__ __forceinline__ void tile_gemm(T* __restrict__ C, int64_t ldc, const 
                                           const int t) {
     typedef Mfma<T> Tr;
     typedef typename Tr::acc_t acc_t;
-    typedef Stage<T> S;
     const int lane = t & 63, w = t >> 6;
     const int wr = w & 1, wc = w >> 1;
     const int lr = lane & 15, lk = lane >> 4;
     const bool active = !(lower && wr == 0 && wc >= 2);
-    const int lcol = lane / S::LPC, lrow = (lane % S::LPC) * S::E;
-
-    auto issue = [&](int st) {
-        T* buf = smem + (st % NBUF) * S::STG;
-#pragma unroll
-        for (int u = 0; u < S::IPW; u++) {
-            const int g = w * S::IPW + u;  // wave-uniform slot: A 0..GRP-1, B GRP..2GRP-1
-            const bool isB = g >= S::GRP;
-            const int gg = isB ? g - S::GRP : g;
-            const int64_t col = (int64_t)st * BKS + gg * S::CPI + lcol;
-            const T* src = isB ? (B + lrow + col * ldb) : (A + lrow + col * lda);
-            __builtin_amdgcn_global_load_lds((const void*)src,
-                                             (__attribute__((address_space(3))) void*)(buf + g * S::SRP), 16, 0, 0);
-        }
-    };
-
-    acc_t acc[2][4];
-#pragma unroll
-    for (int x = 0; x < 2; x++)
-#pragma unroll
-        for (int y = 0; y < 4; y++) acc[x][y] = acc_t{0};
-
     // UPDATE: the whole C tile is fetched into registers up front (its latency hides under the
     // mainloop; loading it unconditionally, all before any store, avoids hipcc's per-element
     // branches and vmcnt(0) waits)
@@ -180,49 +85,8 @@ __device__ __forceinline__ void tile_gemm(T* __restrict__ C, int64_t ldc, const 
                 for (int y = 0; y < 4; y++) cv[x][y][reg] = ccol[wr * 64 + y * 16 + lr];
             }
     }
-    const int nst = K / BKS;
-#pragma unroll
-    for (int p = 0; p < AHEAD; p++)
-        if (p < nst) issue(p);
-#pragma nounroll
-    for (int st = 0; st < nst; st++) {
-        // this wave's loads of stage st have landed (later stages may stay in flight) ...
-        const int ahead = nst - 1 - st;
-        if (AHEAD >= 3 && ahead >= 2) wait_vm<(AHEAD >= 3 ? 2 : 0) * S::IPW>();
-        else if (AHEAD >= 2 && ahead >= 1) wait_vm<S::IPW>();
-        else wait_vm<0>();
-        // ... and every wave's, and every wave is done reading the buffer refilled next
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        if (st + AHEAD < nst) issue(st + AHEAD);
-        if (active) {
-            // fragments of step kq+1 are read while the MFMAs of step kq run (one LDS latency
-            // per stage instead of one per 4-deep step)
-            const T* a = smem + (st % NBUF) * S::STG;
-            const T* b = a + S::GRP * S::SRP;
-            T fa[2][4], fb[2][2];
-            auto frag = [&](int kq, int r) {
-                const int kr = kq * 4 + lk;
-                const int ko = (kr / S::CPI) * S::SRP + (kr % S::CPI) * GT;
-#pragma unroll
-                for (int x = 0; x < 2; x++) fb[r][x] = b[ko + wc * 32 + x * 16 + lr];
-#pragma unroll
-                for (int y = 0; y < 4; y++) fa[r][y] = a[ko + wr * 64 + y * 16 + lr];
-            };
-            frag(0, 0);
-#pragma unroll
-            for (int kq = 0; kq < BKS / 4; kq++) {
-                if (kq + 1 < BKS / 4) frag(kq + 1, (kq + 1) & 1);
-                __builtin_amdgcn_sched_barrier(0);  // keep those reads ahead of these MFMAs
-#pragma unroll
-                for (int x = 0; x < 2; x++)
-#pragma unroll
-                    for (int y = 0; y < 4; y++) acc[x][y] = Tr::mma(fb[kq & 1][x], fa[kq & 1][y], acc[x][y]);
-            }
-        }
-    }
-    // UPDATE: the whole C tile is fetched into registers before any store (a load-store-load
-    // sequence per element would serialise on possible aliasing)
+    acc_t acc[2][4];
+    tile_mma<T>(acc, A, lda, B, ldb, K, active, smem, t);
     if (!active) return;
 #pragma unroll
     for (int x = 0; x < 2; x++) {

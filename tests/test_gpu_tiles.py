@@ -79,6 +79,34 @@ def test_tile_fit_predict(ctx, ks, n, d, m):
     M.close()
 
 
+MEAN_KERNELS = ["GaussianKernel(0.7,1.3,)", "PeriodicKernel(0.9,2.5,0.8,)", "RationalQuadraticKernel(1.1,0.6,1.5,)",
+                "GaussianExpKernel(-0.3,0.1,)",
+                "SumKernel(GaussianKernel(2,0.15,),PeriodicKernel(0.1,3.141592653589793,1,))",
+                "ProductKernel(GaussianKernel(1.5,1,),PeriodicKernel(1,1.3,0.9,))",
+                "SumKernel(GaussianKernel(0.8,1,),WhiteKernel(0.3,))"]
+
+
+@pytest.mark.parametrize("ks", MEAN_KERNELS)
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("n,d,q", [(300, 3, 1), (777, 33, 300)])
+def test_mean_predict_and_build_paths(ctx, ks, dtype, n, d, q):
+    """Mean-only prediction and the covariance build take the MFMA pair-statistics kernels
+    (k_pairs.hip) for White-free trees, the direct kernels otherwise; both against the oracle."""
+    sigma = 0.5
+    X, Y = make_data(n, d, 1)
+    M = gpr_amd.Model(ctx, dtype)
+    M.set_data(X.astype(dtype), Y.astype(dtype))
+    M.set_kernel(ks)
+    M.set_noise(sigma)
+    M.fit()
+    a_ref, _ = O.fit(ks, X, Y, sigma, np.float64)
+    tol = TOL[np.dtype(dtype)]
+    assert relerr(M.alpha(), a_ref) <= tol
+    Xq = make_queries(q, d)
+    assert relerr(M.predict(Xq.astype(dtype)), O.predict(ks, X, a_ref, Xq, np.float64)) <= tol
+    M.close()
+
+
 def test_c3_full_size_residual(ctx):
     """BASELINE.json configs[2] at full size (N = 16384, d = 32, Sum(Gaussian + Periodic),
     sigma = 1): the fit's alpha solves (K + s^2 I) alpha = Y to near machine precision."""
