@@ -20,6 +20,8 @@
 #include "gprx_internal.h"
 #include "k_mma.h"
 
+#include <type_traits>
+
 namespace gprx {
 
 namespace pr {
@@ -65,6 +67,65 @@ __global__ void features_kernel(const T* __restrict__ X, int64_t n, int d, const
     }
 }
 
+// Kernel values of E pairs from their (r2, S) for the trees this file accepts (no White
+// leaf, one periodic table).  Same formulas and products/sums as kernel_value/leaf_value
+// (0 + x and 1 * x are exact, so the results are bit-identical), but organised leaf-outer:
+// the loops over leaves and terms are wave-uniform (leaf constants come in through scalar
+// loads, the type test is a uniform branch) and the per-pair work is an unrolled,
+// statically indexed loop over E registers.  The generic kernel_value reached from 32
+// unrolled call sites per thread was emitted as an out-of-line call per pair.
+template <typename T, int E, bool MUL>
+__device__ __forceinline__ void leaf_into(const KLeaf<T>* __restrict__ L, const T (&r2)[E], const T (&s)[E],
+                                          T (&p)[E]) {
+    const int ty = L->type;
+    const T c0 = L->c0, c1 = L->c1, c2 = L->c2;
+    if (ty == L_PERIODIC) {
+#pragma unroll
+        for (int e = 0; e < E; e++) {
+            const T f = c0 * exp(c1 * s[e]);
+            p[e] = MUL ? p[e] * f : p[e] + f;
+        }
+    } else if (ty == L_RQ) {
+#pragma unroll
+        for (int e = 0; e < E; e++) {
+            const T f = c0 * exp(-c2 * log1p(c1 * r2[e]));
+            p[e] = MUL ? p[e] * f : p[e] + f;
+        }
+    } else {  // L_GAUSS, L_GAUSS_EXP
+#pragma unroll
+        for (int e = 0; e < E; e++) {
+            const T f = c0 * exp(c1 * r2[e]);
+            p[e] = MUL ? p[e] * f : p[e] + f;
+        }
+    }
+}
+
+template <typename T, int E>
+__device__ __forceinline__ void pair_values(const KCanon<T>* __restrict__ K, const T (&r2)[E], const T (&s)[E],
+                                            T (&v)[E]) {
+#pragma unroll
+    for (int e = 0; e < E; e++) v[e] = 0;
+    const int nl = K->nleaf;
+    if (K->sum_leaves) {
+#pragma unroll 1
+        for (int l = 0; l < nl; l++) leaf_into<T, E, false>(&K->leaf[l], r2, s, v);
+        return;
+    }
+    const int nt = K->nterm;
+#pragma unroll 1
+    for (int t = 0; t < nt; t++) {
+        const unsigned msk = K->term_mask[t];
+        T p[E];
+#pragma unroll
+        for (int e = 0; e < E; e++) p[e] = 1;
+#pragma unroll 1
+        for (int l = 0; l < nl; l++)
+            if (msk & (1u << l)) leaf_into<T, E, true>(&K->leaf[l], r2, s, p);
+#pragma unroll
+        for (int e = 0; e < E; e++) v[e] += p[e];
+    }
+}
+
 // Statistics of the 128 x 128 pair block (rows from FU + i0, columns from FV + j0).
 template <typename T, int NPER, bool R2>
 __device__ __forceinline__ void block_stats(const T* FU, int64_t nu, int64_t i0, const T* FV, int64_t nv, int64_t j0,
@@ -86,9 +147,8 @@ __global__ __launch_bounds__(NT) void kbuild_mma_kernel(const KCanon<T>* __restr
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     T* smem = reinterpret_cast<T*>(smem_raw);
     typedef Mfma<T> Tr;
-    // the kernel tree is read from device memory: as a by-value kernel argument, indexed per
-    // leaf/term in 32 unrolled evaluations, hipcc copied it to scratch
-    const KCanon<T>& K = *Kd;
+    // the kernel tree is read from device memory (scalar loads): as a by-value kernel
+    // argument indexed per leaf/term, hipcc copied it to scratch
     int64_t ti, tj;
     {
         const int64_t b = blockIdx.x;
@@ -104,28 +164,43 @@ __global__ __launch_bounds__(NT) void kbuild_mma_kernel(const KCanon<T>* __restr
     typename Tr::acc_t ar[2][4], ap[2][4];
     block_stats<T, NPER, R2>(FU, nf, i0, FV, nf, j0, Kr, Kp, smem, t, ar, ap);
     bool bad = false;
+    // four chunks of 8 pairs per thread (column group x, registers 2h, 2h+1):
+    // statistics -> values -> stores; 8 keeps the interleaved exp sequences within registers
+    auto chunk = [&](auto cc) {
+        constexpr int x = decltype(cc)::value >> 1, h = decltype(cc)::value & 1;
+        T r2[8], sp[8], v[8];
 #pragma unroll
-    for (int x = 0; x < 2; x++)
+        for (int reg = 2 * h; reg < 2 * h + 2; reg++)
 #pragma unroll
-        for (int reg = 0; reg < 4; reg++) {
+            for (int y = 0; y < 4; y++) {
+                const int64_t gj = j0 + wc * 32 + x * 16 + Tr::orow(lk, reg);
+                const int64_t gi = i0 + wr * 64 + y * 16 + lr;
+                r2[(reg - 2 * h) * 4 + y] = R2 ? (gi == gj ? T(0) : fmax(ar[x][y][reg], T(0))) : T(0);
+                sp[(reg - 2 * h) * 4 + y] = NPER ? (gi == gj ? T(0) : fmax(ap[x][y][reg], T(0))) : T(0);
+            }
+        pair_values<T, 8>(Kd, r2, sp, v);
+#pragma unroll
+        for (int reg = 2 * h; reg < 2 * h + 2; reg++) {
             const int64_t gj = j0 + wc * 32 + x * 16 + Tr::orow(lk, reg);
             T* col = A + gj * ld;
 #pragma unroll
             for (int y = 0; y < 4; y++) {
                 const int64_t gi = i0 + wr * 64 + y * 16 + lr;
-                T v;
+                T val = v[(reg - 2 * h) * 4 + y];
                 if (gi >= n || gj >= n) {
-                    v = (gi == gj) ? T(1) : T(0);
+                    val = (gi == gj) ? T(1) : T(0);
                 } else {
-                    const T r2 = R2 ? (gi == gj ? T(0) : fmax(ar[x][y][reg], T(0))) : T(0);
-                    const T sp = NPER ? (gi == gj ? T(0) : fmax(ap[x][y][reg], T(0))) : T(0);
-                    v = kernel_value(K, r2, sp, T(0));
-                    if (!isfinite(v)) bad = true;
-                    if (gi == gj) v += sigma2;
+                    if (!isfinite(val)) bad = true;
+                    if (gi == gj) val += sigma2;
                 }
-                if (gi >= gj) col[gi] = v;
+                if (gi >= gj) col[gi] = val;
             }
         }
+    };
+    chunk(std::integral_constant<int, 0>{});
+    chunk(std::integral_constant<int, 1>{});
+    chunk(std::integral_constant<int, 2>{});
+    chunk(std::integral_constant<int, 3>{});
     if (bad) atomicOr(flag, 1);
 }
 
@@ -143,7 +218,6 @@ __global__ __launch_bounds__(NT) void predict_mma_kernel(const KCanon<T>* __rest
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     T* smem = reinterpret_cast<T*>(smem_raw);
     typedef Mfma<T> Tr;
-    const KCanon<T>& K = *Kd;
     const int64_t i0 = (int64_t)blockIdx.x * GT;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int wr = w & 1, wc = w >> 1, lr = lane & 15, lk = lane >> 4;
@@ -155,10 +229,17 @@ __global__ __launch_bounds__(NT) void predict_mma_kernel(const KCanon<T>* __rest
     for (int64_t j0 = 0; j0 < n; j0 += GT) {
         typename Tr::acc_t ar[2][4], ap[2][4];
         block_stats<T, NPER, R2>(FU, nfu, i0, FV, nfv, j0, Kr, Kp, smem, t, ar, ap);
+        auto chunk = [&](auto cc) {  // 8 pairs per thread at a time, as in kbuild_mma_kernel
+            constexpr int x = decltype(cc)::value >> 1, h = decltype(cc)::value & 1;
+            T r2[8], sp[8], v[8];
 #pragma unroll
-        for (int x = 0; x < 2; x++)
+            for (int e = 0; e < 8; e++) {
+                r2[e] = R2 ? fmax(ar[x][e & 3][2 * h + (e >> 2)], T(0)) : T(0);
+                sp[e] = NPER ? fmax(ap[x][e & 3][2 * h + (e >> 2)], T(0)) : T(0);
+            }
+            pair_values<T, 8>(Kd, r2, sp, v);
 #pragma unroll
-            for (int reg = 0; reg < 4; reg++) {
+            for (int reg = 2 * h; reg < 2 * h + 2; reg++) {
                 const int64_t gj = j0 + wc * 32 + x * 16 + Tr::orow(lk, reg);
                 const bool okj = gj < n;
                 T al[PM];
@@ -166,13 +247,16 @@ __global__ __launch_bounds__(NT) void predict_mma_kernel(const KCanon<T>* __rest
                 for (int r = 0; r < PM; r++) al[r] = (okj && r < m) ? alpha[gj * m + r] : T(0);
 #pragma unroll
                 for (int y = 0; y < 4; y++) {
-                    const T r2 = R2 ? fmax(ar[x][y][reg], T(0)) : T(0);
-                    const T sp = NPER ? fmax(ap[x][y][reg], T(0)) : T(0);
-                    const T kv = okj ? kernel_value(K, r2, sp, T(0)) : T(0);
+                    const T kv = okj ? v[(reg - 2 * h) * 4 + y] : T(0);
 #pragma unroll
                     for (int r = 0; r < PM; r++) racc[r][y] = fma(kv, al[r], racc[r][y]);
                 }
             }
+        };
+        chunk(std::integral_constant<int, 0>{});
+        chunk(std::integral_constant<int, 1>{});
+        chunk(std::integral_constant<int, 2>{});
+        chunk(std::integral_constant<int, 3>{});
         __syncthreads();  // the staging ring is refilled by the next block's product
     }
     // rows 64 wr + 16 y + lr: sum over the lane groups lk, then over the 4 column waves (LDS)
