@@ -423,8 +423,9 @@ __device__ bool wait_inputs(const Args<T>& a, int type, int i, int j, int b0, in
     }
     const long long t0 = wall_clock64();
     for (;;) {
-        const int ok = (ld_uni(vp) == vwant) & (ld_uni(vp2) == vwant2) & (ld_uni(lp1) >= lwant1) &
-                       (ld_uni(lp2) >= lwant2);
+        // bitwise: all four loads are issued before any compare resolves
+        const int ok = int(ld_uni(vp) == vwant) & int(ld_uni(vp2) == vwant2) & int(ld_uni(lp1) >= lwant1) &
+                       int(ld_uni(lp2) >= lwant2);
         if (ok) return true;
         if (ld_uni(a.ctl + C_ERR)) return false;
         if (wall_clock64() - t0 > a.tlimit) {
@@ -447,6 +448,8 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
     const int64_t ld = a.ld;
     for (;;) {
         if (wv == 0) {  // one ticket per workgroup: lane 0 adds 1, the other lanes 0
+            // (not taken ahead of time: a ticket claimed while the previous task still runs
+            // delays critical-path tasks behind long updates -- measured 28.8 -> 33.2 ms)
             const int v = __hip_atomic_fetch_add(a.ctl + C_TICKET, (t == 0) ? 1 : 0, __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_AGENT);
             s_q = __builtin_amdgcn_readfirstlane(v);
@@ -477,8 +480,12 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
         asm volatile("" : "+v"(tid));
         T* Ci = a.A + (int64_t)i * GT;  // row block i, column 0
         if (type == T_UPD) {
-            if (!(a.variant & 2)) tile_gemm<T, true>(Ci + (int64_t)j * GT * ld, ld, Ci + (int64_t)b0 * GT * ld, ld,
-                               a.A + (int64_t)j * GT + (int64_t)b0 * GT * ld, ld, nb * GT, i == j, smem, tid);
+            // variant 64 (timing experiment, wrong results): every update streams the same
+            // L2-resident operands, to separate memory-feed from MFMA limits
+            const int64_t oa = (a.variant & 64) ? 0 : (int64_t)i * GT + (int64_t)b0 * GT * ld;
+            const int64_t ob = (a.variant & 64) ? GT : (int64_t)j * GT + (int64_t)b0 * GT * ld;
+            if (!(a.variant & 2)) tile_gemm<T, true>(Ci + (int64_t)j * GT * ld, ld, a.A + oa, ld, a.A + ob, ld, nb * GT,
+                                                     i == j, smem, tid);
             publish(a.ver + (int64_t)i * a.nc + j, b0 + nb, false);
         } else if (type == T_TRSM) {
             T* Cik = Ci + (int64_t)j * GT * ld;
@@ -525,16 +532,18 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
 // ==========================================================================================
 struct Cost {  // per-task durations (us, one CU), calibrated from GPRX_PT_TRACE timelines
     double k128 = 17.1;  // per 128-deep slice of a full tile update
-    double ovh = 12.0;   // per update task: ticket, waits, fences, C read-modify-write
-    double trsm = 22.0;  // TRSM tile
-    double diagx = 114.0;  // DIAGX(k > 0): trsm tile + syrk tile + 128x128 factor/inverse
-    double diag0 = 75.0;   // DIAGX(0): factor/inverse only
+    double ovh = 6.5;    // per update task: ticket, waits, fences, C read-modify-write
+    double trsm = 20.4;  // TRSM tile
+    double diagx = 106.0;  // DIAGX(k > 0): trsm tile + syrk tile + 128x128 factor/inverse
+    double diag0 = 70.0;   // DIAGX(0): factor/inverse only
+    double early = 20.0;   // DIAGX(k) publishes L_{k,k-1} after its trsm phase
+    double diagf = 0.97;   // diagonal-tile update relative to a full one (2 of 8 waves idle)
 };
 
 struct Task {
     int type, i, j, b0, nb;
     double dur;
-    std::vector<int> succ;
+    std::vector<int> succ, esucc;  // esucc: released at the early publication (DIAGX)
     int ndep = 0;
     double bl = 0;  // bottom level (longest path to the end, inclusive)
 };
@@ -546,21 +555,28 @@ struct Schedule {
 };
 
 // Chunks of the updates of tile (i, j): b in [0, e), e = j (i > j) or j - 1 (diagonal tile:
-// the last one is applied inside DIAGX(j)).  Aligned W-chunks up to the start of the panel
-// `look` panels before j's own, single blocks after that.
-static void tile_chunks(int i, int j, int W, int look, std::vector<std::pair<int, int>>& out) {
+// the last one is applied inside DIAGX(j)).  Aligned W-chunks up to the last multiple of W
+// at or before column j, then the remainder before the last `near` panels in power-of-two
+// pieces (W/2, W/4, ..., 1), then single panels -- few tasks (each costs a fixed ~6 us of
+// ticket, waits, fences and C read-modify-write), while the last panels of a tile, the ones
+// the diagonal chain waits for, still go one at a time.
+static void tile_chunks(int i, int j, int W, int near, std::vector<std::pair<int, int>>& out) {
     out.clear();
     const int e = (i == j) ? j - 1 : j;
     if (e <= 0) return;
-    int hb = W * (j / W) - W * look;
-    hb = std::max(0, std::min(hb, e));
+    int hb = std::max(0, std::min(W * (j / W), e));
     hb -= hb % W;
     int b = 0;
     for (; b + W <= hb; b += W) out.push_back({b, W});
+    for (int p = W / 2; p >= 1; p /= 2)
+        if (b + p <= e - near) {
+            out.push_back({b, p});
+            b += p;
+        }
     for (; b < e; b++) out.push_back({b, 1});
 }
 
-static Schedule make_schedule(int nc, int nr, int W, int look, int P, const Cost& cm) {
+static Schedule make_schedule(int nc, int nr, int W, int near, int P, const Cost& cm) {
     std::vector<Task> tasks;
     tasks.reserve((size_t)nr * nc * 2);
     auto add = [&](int type, int i, int j, int b0, int nb, double dur) {
@@ -577,14 +593,16 @@ static Schedule make_schedule(int nc, int nr, int W, int look, int P, const Cost
     std::vector<int> diagx(nc, -1);
     std::vector<int> trsm((size_t)nr * nc, -1);
     std::vector<int> last_upd((size_t)nr * nc, -1);
-    std::vector<std::vector<int>> deps;
-    auto dep = [&](int tsk, int on) {
+    std::vector<std::vector<int>> deps, edeps;  // edeps: on L_{k,k-1}, published early by DIAGX(k)
+    auto dep = [&](int tsk, int on, bool early = false) {
         if (on < 0) return;
-        if ((int)deps.size() <= tsk) deps.resize(tsk + 1);
-        deps[tsk].push_back(on);
+        auto& d = early ? edeps : deps;
+        if ((int)d.size() <= tsk) d.resize(tsk + 1);
+        d[tsk].push_back(on);
     };
-    // producer of L_{i,b}
-    auto prodL = [&](int i, int b) -> int {
+    // producer of L_{i,b} (early: the trsm phase of DIAGX(i) already published it)
+    auto prodL = [&](int i, int b, bool& early) -> int {
+        early = i < nc && b == i - 1;
         if (i < nc && (b == i || b == i - 1)) return diagx[i];
         return trsm[(size_t)i * nc + b];
     };
@@ -597,7 +615,7 @@ static Schedule make_schedule(int nc, int nr, int W, int look, int P, const Cost
         std::vector<std::pair<int, int>> ch;
         for (int j = 1; j < nc; j++)
             for (int i = j; i < nr; i++) {
-                tile_chunks(i, j, W, look, ch);
+                tile_chunks(i, j, W, near, ch);
                 for (auto& c : ch) by_last[c.first + c.second - 1].push_back(Chunk{i, j, c.first, c.second});
             }
     }
@@ -624,35 +642,50 @@ static Schedule make_schedule(int nc, int nr, int W, int look, int P, const Cost
         }
         if (k + 1 < nc) make_diagx(k + 1);
         for (const Chunk& c : by_last[k]) {
-            const double dur = cm.ovh + c.nb * cm.k128 * (c.i == c.j ? 0.75 : 1.0);
+            const double dur = cm.ovh + c.nb * cm.k128 * (c.i == c.j ? cm.diagf : 1.0);
             const int id = add(T_UPD, c.i, c.j, c.b0, c.nb, dur);
             dep(id, last_upd[(size_t)c.i * nc + c.j]);
-            dep(id, prodL(c.i, k));
-            dep(id, prodL(c.j, k));
+            bool e1, e2;
+            const int p1 = prodL(c.i, k, e1), p2 = prodL(c.j, k, e2);
+            dep(id, p1, e1);
+            dep(id, p2, e2);
             last_upd[(size_t)c.i * nc + c.j] = id;
         }
     }
     const int nt = (int)tasks.size();
     deps.resize(nt);
+    edeps.resize(nt);
     for (int id = 0; id < nt; id++) {
         auto& d = deps[id];
+        auto& ed = edeps[id];
         std::sort(d.begin(), d.end());
         d.erase(std::unique(d.begin(), d.end()), d.end());
+        std::sort(ed.begin(), ed.end());
+        ed.erase(std::unique(ed.begin(), ed.end()), ed.end());
         for (int on : d) {
             if (on >= id) throw Error{GPRX_ERR_ARG, "potrf tile schedule: producer created after consumer"};
             tasks[on].succ.push_back(id);
         }
-        tasks[id].ndep = (int)d.size();
+        int ne = 0;
+        for (int on : ed) {
+            if (on >= id) throw Error{GPRX_ERR_ARG, "potrf tile schedule: producer created after consumer"};
+            if (std::binary_search(d.begin(), d.end(), on)) continue;  // full dependency already
+            tasks[on].esucc.push_back(id);
+            ne++;
+        }
+        tasks[id].ndep = (int)d.size() + ne;
     }
     // creation order is topological: bottom levels in reverse
     for (int id = nt - 1; id >= 0; id--) {
         double m = 0;
         for (int s : tasks[id].succ) m = std::max(m, tasks[s].bl);
+        for (int s : tasks[id].esucc) m = std::max(m, tasks[s].bl - (tasks[id].dur - cm.early));
         tasks[id].bl = tasks[id].dur + m;
     }
     // list scheduling on P workers, highest bottom level first
     typedef std::pair<double, int> PQ;
     std::priority_queue<PQ> ready;
+    // events: (time, task) finishing, or (time, -1 - task) for an early publication
     std::priority_queue<PQ, std::vector<PQ>, std::greater<PQ>> running;
     std::vector<int> indeg(nt);
     for (int id = 0; id < nt; id++) {
@@ -670,12 +703,18 @@ static Schedule make_schedule(int nc, int nr, int W, int look, int P, const Cost
             const Task& tk = tasks[id];
             S.list.push_back(make_int4(tk.type | (tk.nb << 8), tk.i, tk.j, tk.b0));
             running.push({now + tk.dur, id});
+            if (!tk.esucc.empty()) running.push({now + std::min(cm.early, tk.dur), -1 - id});
             freew--;
         }
         if (running.empty()) throw Error{GPRX_ERR_ARG, "potrf tile schedule: dependency cycle"};
         const PQ f = running.top();
         running.pop();
         now = f.first;
+        if (f.second < 0) {
+            for (int s : tasks[-1 - f.second].esucc)
+                if (--indeg[s] == 0) ready.push({tasks[s].bl, s});
+            continue;
+        }
         freew++;
         for (int s : tasks[f.second].succ)
             if (--indeg[s] == 0) ready.push({tasks[s].bl, s});
@@ -686,11 +725,11 @@ static Schedule make_schedule(int nc, int nr, int W, int look, int P, const Cost
 }
 
 struct Params {
-    int W = 8, look = 0;
+    int W = 16, near = 1;
     Cost cm;
     Params() {
         if (const char* e = std::getenv("GPRX_PT_W")) W = std::max(1, std::atoi(e));
-        if (const char* e = std::getenv("GPRX_PT_LOOK")) look = std::max(0, std::atoi(e));
+        if (const char* e = std::getenv("GPRX_PT_NEAR")) near = std::max(0, std::atoi(e));
         if (const char* e = std::getenv("GPRX_PT_DIAGX_US")) cm.diagx = std::atof(e);
         if (const char* e = std::getenv("GPRX_PT_TRSM_US")) cm.trsm = std::atof(e);
         if (const char* e = std::getenv("GPRX_PT_K128_US")) cm.k128 = std::atof(e);
@@ -770,7 +809,7 @@ void potrf_tiles(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info
     auto it = st.sched.find(key);
     if (it == st.sched.end()) {
         const Params& pr = params();
-        Schedule S = make_schedule(nc, nr, pr.W, pr.look, st.ncu, pr.cm);
+        Schedule S = make_schedule(nc, nr, pr.W, pr.near, st.ncu, pr.cm);
         PtState::Dev d;
         d.n = (int64_t)S.list.size();
         d.est_us = S.est_us;
@@ -846,8 +885,9 @@ void potrf_tiles(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info
 // Host-only schedule statistics (no device work): tasks, predicted makespan, and a check
 // that every task's producers come earlier in the ticket order.
 int64_t potrf_tiles_schedule_stats(int nc, int nr, int P, double* est_us) {
+    if (nc < 1 || nr < nc || P < 1) throw Error{GPRX_ERR_ARG, "potrf tile schedule: need nc >= 1, nr >= nc, P >= 1"};
     const pt::Params& pr = pt::params();
-    pt::Schedule S = pt::make_schedule(nc, nr, pr.W, pr.look, P, pr.cm);
+    pt::Schedule S = pt::make_schedule(nc, nr, pr.W, pr.near, P, pr.cm);
     if (est_us) *est_us = S.est_us;
     return S.ntasks;
 }

@@ -20,7 +20,10 @@ def _sched(nc, nr, P=256, env=None):
     return st, n.value, est.value
 
 
-def _expected_tasks(nc, nr, W=8):
+def _expected_tasks(nc, nr, W=16, near=1):
+    """Task count of the chunking rule (k_ptiles.hip tile_chunks): W-aligned chunks up to the
+    last multiple of W at or before column j, then power-of-two pieces before the last `near`
+    panels, then single panels."""
     diag = nc
     trsm = sum(1 for k in range(nc) for i in range(k + 1, nr) if not (i == k + 1 and i < nc))
     upd = 0
@@ -31,7 +34,14 @@ def _expected_tasks(nc, nr, W=8):
                 continue
             hb = min(W * (j // W), e)
             hb -= hb % W
-            upd += hb // W + (e - hb)
+            upd += hb // W
+            b, p = hb, W // 2
+            while p >= 1:
+                if b + p <= e - near:
+                    upd += 1
+                    b += p
+                p //= 2
+            upd += e - b
     return diag + trsm + upd
 
 
