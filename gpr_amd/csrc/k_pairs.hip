@@ -9,14 +9,16 @@
 //
 // Every leaf depends on a pair only through r2 = sum_k (x_k - y_k)^2 and
 // S = sum_k sin^2(b (x_k - y_k)) (gprx_internal.h).  Both are inner products of per-sample
-// feature vectors, so a 128 x 128 block of pair statistics is a 128 x 128 x K MFMA tile
-// (k_mma.h) instead of O(d) VALU work per pair:
-//     r2 = [x~, |x~|^2, 1] . [-2 y~, 1, |y~|^2]                           (K = d + 2)
-//     S  = [s_x^2, c_x^2, s_x c_x] . [c_y^2, s_y^2, -2 s_y c_y]            (K = 3 d)
-// with x~ = x - x_0 (both sets centred on the first training sample: r2 and S are translation
-// invariant, and centring keeps |x~|^2 ~ r2 so the expansion loses no significant digits),
-// s = sin(b x~_k), c = cos(b x~_k).  Feature matrices are column-major (rows padded to 128,
-// columns to 16) so the tile kernel streams them with LDS-DMA like any GEMM operand.
+// feature vectors plus per-sample constants, so a 128 x 128 block of pair statistics is a
+// 128 x 128 x K MFMA tile (k_mma.h) instead of O(d) VALU work per pair:
+//     r2 = |x~|^2 + |y~|^2 + x~ . (-2 y~)                                   (K = d)
+//     S  = d/2 - 1/2 [C_x, S_x] . [C_y, S_y]                                (K = 2 d)
+// (sin^2 u = (1 - cos 2u) / 2 and cos(2b(x - y)) = C_x C_y + S_x S_y) with x~ = x - x_0
+// (both sets centred on the first training sample: r2 and S are translation invariant, and
+// centring keeps |x~|^2 ~ r2 so the expansion loses no significant digits), C = cos(2b x~_k),
+// S = sin(2b x~_k).  Feature matrices are column-major (rows padded to 128, columns to 16) so
+// the tile kernel streams them with LDS-DMA like any GEMM operand; the squared norms sit in
+// one more column after the MFMA operands and are added in the epilogue.
 #include "gprx_internal.h"
 #include "k_mma.h"
 
@@ -32,7 +34,8 @@ constexpr int KG = 16;  // feature-column granule (the tile kernel's k-stage)
 
 static int64_t rup(int64_t x, int64_t g) { return (x + g - 1) / g * g; }
 
-// F (np x (Kr + Kp), column-major, ld np): the left (U) or right (V) features of n samples.
+// F (np x (Kr + Kp + 1), column-major, ld np): the left (U) or right (V) features of n
+// samples, then their squared norms |x~|^2.  Padding rows are all zero.
 template <typename T>
 __global__ void features_kernel(const T* __restrict__ X, int64_t n, int d, const T* __restrict__ center, T b,
                                 int need_r2, int nper, int right, T* __restrict__ F, int64_t np, int Kr, int Kp) {
@@ -46,24 +49,19 @@ __global__ void features_kernel(const T* __restrict__ X, int64_t n, int d, const
             nrm = fma(xt, xt, nrm);
             F[i + (int64_t)k * np] = right ? T(-2) * xt : xt;
         }
-        F[i + (int64_t)d * np] = right ? T(1) : nrm;
-        F[i + (int64_t)(d + 1) * np] = right ? nrm : T(1);
-        if (!live) {  // padding rows: all-zero statistics
-            F[i + (int64_t)d * np] = 0;
-            F[i + (int64_t)(d + 1) * np] = 0;
-        }
-        for (int k = d + 2; k < Kr; k++) F[i + (int64_t)k * np] = 0;
+        for (int k = d; k < Kr; k++) F[i + (int64_t)k * np] = 0;
     }
+    F[i + (int64_t)(Kr + Kp) * np] = nrm;
     if (nper) {
         T* P = F + (int64_t)Kr * np;
+        const T b2 = T(2) * b;
         for (int k = 0; k < d; k++) {
             T sn = 0, cs = 0;
-            if (live) gsincos(b * (X[i * d + k] - center[k]), &sn, &cs);
-            P[i + (int64_t)k * np] = right ? cs * cs : sn * sn;
-            P[i + (int64_t)(d + k) * np] = right ? sn * sn : cs * cs;
-            P[i + (int64_t)(2 * d + k) * np] = right ? T(-2) * sn * cs : sn * cs;
+            if (live) gsincos(b2 * (X[i * d + k] - center[k]), &sn, &cs);
+            P[i + (int64_t)k * np] = cs;
+            P[i + (int64_t)(d + k) * np] = sn;
         }
-        for (int k = 3 * d; k < Kp; k++) P[i + (int64_t)k * np] = 0;
+        for (int k = 2 * d; k < Kp; k++) P[i + (int64_t)k * np] = 0;
     }
 }
 
@@ -138,12 +136,19 @@ __device__ __forceinline__ void block_stats(const T* FU, int64_t nu, int64_t i0,
     }
 }
 
+// (r2, S) of one pair from the tile products and the per-sample norms (hd = d / 2)
+template <typename T, int NPER, bool R2>
+__device__ __forceinline__ void pair_stats(T pr2, T pper, T nu, T nv, T hd, T& r2, T& sp) {
+    r2 = R2 ? fmax(nu + nv + pr2, T(0)) : T(0);
+    sp = NPER ? fmax(fma(T(-0.5), pper, hd), T(0)) : T(0);
+}
+
 // Lower triangle of K(X, X) (+ sigma2 on the diagonal, identity padding) into A (column-major).
 template <typename T, int NPER, bool R2>
 __global__ __launch_bounds__(NT) void kbuild_mma_kernel(const KCanon<T>* __restrict__ Kd, const T* __restrict__ FU,
                                                         const T* __restrict__ FV,
-                                                        int64_t nf, int Kr, int Kp, T* __restrict__ A, int64_t ld,
-                                                        int64_t n, T sigma2, int* __restrict__ flag) {
+                                                        int64_t nf, int Kr, int Kp, T hd, T* __restrict__ A,
+                                                        int64_t ld, int64_t n, T sigma2, int* __restrict__ flag) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     T* smem = reinterpret_cast<T*>(smem_raw);
     typedef Mfma<T> Tr;
@@ -161,6 +166,14 @@ __global__ __launch_bounds__(NT) void kbuild_mma_kernel(const KCanon<T>* __restr
     const int64_t i0 = ti * GT, j0 = tj * GT;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int wr = w & 1, wc = w >> 1, lr = lane & 15, lk = lane >> 4;
+    T nu[4], nv[2][4];  // squared norms of this thread's rows and columns
+#pragma unroll
+    for (int y = 0; y < 4; y++) nu[y] = R2 ? FU[(int64_t)(Kr + Kp) * nf + i0 + wr * 64 + y * 16 + lr] : T(0);
+#pragma unroll
+    for (int x = 0; x < 2; x++)
+#pragma unroll
+        for (int reg = 0; reg < 4; reg++)
+            nv[x][reg] = R2 ? FV[(int64_t)(Kr + Kp) * nf + j0 + wc * 32 + x * 16 + Tr::orow(lk, reg)] : T(0);
     typename Tr::acc_t ar[2][4], ap[2][4];
     block_stats<T, NPER, R2>(FU, nf, i0, FV, nf, j0, Kr, Kp, smem, t, ar, ap);
     bool bad = false;
@@ -175,8 +188,11 @@ __global__ __launch_bounds__(NT) void kbuild_mma_kernel(const KCanon<T>* __restr
             for (int y = 0; y < 4; y++) {
                 const int64_t gj = j0 + wc * 32 + x * 16 + Tr::orow(lk, reg);
                 const int64_t gi = i0 + wr * 64 + y * 16 + lr;
-                r2[(reg - 2 * h) * 4 + y] = R2 ? (gi == gj ? T(0) : fmax(ar[x][y][reg], T(0))) : T(0);
-                sp[(reg - 2 * h) * 4 + y] = NPER ? (gi == gj ? T(0) : fmax(ap[x][y][reg], T(0))) : T(0);
+                T a, b;
+                pair_stats<T, NPER, R2>(R2 ? ar[x][y][reg] : T(0), NPER ? ap[x][y][reg] : T(0), nu[y], nv[x][reg], hd,
+                                        a, b);
+                r2[(reg - 2 * h) * 4 + y] = gi == gj ? T(0) : a;
+                sp[(reg - 2 * h) * 4 + y] = gi == gj ? T(0) : b;
             }
         pair_values<T, 8>(Kd, r2, sp, v);
 #pragma unroll
@@ -212,7 +228,7 @@ constexpr int PM = 1;
 template <typename T, int NPER, bool R2>
 __global__ __launch_bounds__(NT) void predict_mma_kernel(const KCanon<T>* __restrict__ Kd, const T* __restrict__ FU,
                                                          int64_t nfu,
-                                                         const T* __restrict__ FV, int64_t nfv, int Kr, int Kp,
+                                                         const T* __restrict__ FV, int64_t nfv, int Kr, int Kp, T hd,
                                                          const T* __restrict__ alpha, int64_t n, int m, int64_t q,
                                                          T* __restrict__ mean) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
@@ -226,37 +242,48 @@ __global__ __launch_bounds__(NT) void predict_mma_kernel(const KCanon<T>* __rest
     for (int r = 0; r < PM; r++)
 #pragma unroll
         for (int y = 0; y < 4; y++) racc[r][y] = 0;
+    T nu[4];
+#pragma unroll
+    for (int y = 0; y < 4; y++) nu[y] = R2 ? FU[(int64_t)(Kr + Kp) * nfu + i0 + wr * 64 + y * 16 + lr] : T(0);
+    // column norms of the current block go through LDS (after the staging ring): held in
+    // registers across the two tile products they made this kernel spill
+    T* nvs = smem + gemm_lds<T>() / sizeof(T);
+    T* als = nvs + GT;
     for (int64_t j0 = 0; j0 < n; j0 += GT) {
+        // column norms and alpha of the current block go through LDS (after the staging ring;
+        // written here, read after tile_mma's barriers): held in registers across the two
+        // tile products they made this kernel spill.  alpha = 0 masks the padding columns.
+        if (t < GT) {
+            if (R2) nvs[t] = FV[(int64_t)(Kr + Kp) * nfv + j0 + t];
+            als[t] = (j0 + t < n) ? alpha[(j0 + t) * m] : T(0);
+        }
         typename Tr::acc_t ar[2][4], ap[2][4];
-        block_stats<T, NPER, R2>(FU, nfu, i0, FV, nfv, j0, Kr, Kp, smem, t, ar, ap);
-        auto chunk = [&](auto cc) {  // 8 pairs per thread at a time, as in kbuild_mma_kernel
-            constexpr int x = decltype(cc)::value >> 1, h = decltype(cc)::value & 1;
-            T r2[8], sp[8], v[8];
+        // opaque thread index: the query-side operand addresses are loop-invariant, and
+        // hoisted out of this loop they stayed live in registers across it (spills)
+        int tid = t;
+        asm volatile("" : "+v"(tid));
+        block_stats<T, NPER, R2>(FU, nfu, i0, FV, nfv, j0, Kr, Kp, smem, tid, ar, ap);
+        auto chunk = [&](auto cc) {  // 4 pairs per thread at a time: column (x, reg), rows y
+            constexpr int x = decltype(cc)::value >> 2, reg = decltype(cc)::value & 3;
+            const int jl = wc * 32 + x * 16 + Tr::orow(lk, reg);
+            T r2[4], sp[4], v[4];
 #pragma unroll
-            for (int e = 0; e < 8; e++) {
-                r2[e] = R2 ? fmax(ar[x][e & 3][2 * h + (e >> 2)], T(0)) : T(0);
-                sp[e] = NPER ? fmax(ap[x][e & 3][2 * h + (e >> 2)], T(0)) : T(0);
-            }
-            pair_values<T, 8>(Kd, r2, sp, v);
+            for (int y = 0; y < 4; y++)
+                pair_stats<T, NPER, R2>(R2 ? ar[x][y][reg] : T(0), NPER ? ap[x][y][reg] : T(0), nu[y],
+                                        R2 ? nvs[jl] : T(0), hd, r2[y], sp[y]);
+            pair_values<T, 4>(Kd, r2, sp, v);
+            const T al = als[jl];
 #pragma unroll
-            for (int reg = 2 * h; reg < 2 * h + 2; reg++) {
-                const int64_t gj = j0 + wc * 32 + x * 16 + Tr::orow(lk, reg);
-                const bool okj = gj < n;
-                T al[PM];
-#pragma unroll
-                for (int r = 0; r < PM; r++) al[r] = (okj && r < m) ? alpha[gj * m + r] : T(0);
-#pragma unroll
-                for (int y = 0; y < 4; y++) {
-                    const T kv = okj ? v[(reg - 2 * h) * 4 + y] : T(0);
-#pragma unroll
-                    for (int r = 0; r < PM; r++) racc[r][y] = fma(kv, al[r], racc[r][y]);
-                }
-            }
+            for (int y = 0; y < 4; y++) racc[0][y] = fma(v[y], al, racc[0][y]);
         };
         chunk(std::integral_constant<int, 0>{});
         chunk(std::integral_constant<int, 1>{});
         chunk(std::integral_constant<int, 2>{});
         chunk(std::integral_constant<int, 3>{});
+        chunk(std::integral_constant<int, 4>{});
+        chunk(std::integral_constant<int, 5>{});
+        chunk(std::integral_constant<int, 6>{});
+        chunk(std::integral_constant<int, 7>{});
         __syncthreads();  // the staging ring is refilled by the next block's product
     }
     // rows 64 wr + 16 y + lr: sum over the lane groups lk, then over the 4 column waves (LDS)
@@ -293,23 +320,34 @@ bool pairs_mma_supported(const KCanon<T>& K, int m) {
     return K.need_r2 || K.nper > 0;
 }
 
-// feature columns of one sample set (Kr + Kp), for the workspace size
+namespace pr {
+template <typename T>
+static int kr_of(const KCanon<T>& K, int d) {  // MFMA depth of the r2 product
+    return K.need_r2 ? (int)rup(d, KG) : 0;
+}
+template <typename T>
+static int kp_of(const KCanon<T>& K, int d) {  // MFMA depth of the periodic product
+    return K.nper ? (int)rup(2 * d, KG) : 0;
+}
+}  // namespace pr
+
+// feature columns of one sample set (Kr + Kp operand columns + the squared norms)
 template <typename T>
 int64_t pairs_feature_cols(const KCanon<T>& K, int d) {
-    return (K.need_r2 ? pr::rup(d + 2, pr::KG) : 0) + (K.nper ? pr::rup(3 * d, pr::KG) : 0);
+    return pr::kr_of(K, d) + pr::kp_of(K, d) + 1;
 }
 
 template <typename T>
 void launch_pair_features(const KCanon<T>& K, const T* X, int64_t n, int d, const T* center, bool right, T* F,
                           int64_t np, hipStream_t s) {
-    const int Kr = K.need_r2 ? (int)pr::rup(d + 2, pr::KG) : 0, Kp = K.nper ? (int)pr::rup(3 * d, pr::KG) : 0;
+    const int Kr = pr::kr_of(K, d), Kp = pr::kp_of(K, d);
     hipLaunchKernelGGL(pr::features_kernel<T>, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, s, X, n, d, center,
                        K.nper ? K.b[0] : T(0), K.need_r2 ? 1 : 0, K.nper, right ? 1 : 0, F, np, Kr, Kp);
 }
 
 template <typename T>
 static size_t pairs_lds() {
-    const size_t a = mm::gemm_lds<T>(), b = sizeof(T) * 4 * GT * pr::PM;
+    const size_t a = mm::gemm_lds<T>() + sizeof(T) * 2 * GT, b = sizeof(T) * 4 * GT * pr::PM;  // + norms, alpha
     return a > b ? a : b;
 }
 
@@ -331,22 +369,22 @@ static size_t pairs_lds() {
 template <typename T>
 void launch_kbuild_mma(const KCanon<T>& K, const KCanon<T>* Kd, const T* FU, const T* FV, int64_t nf, int d, T* A,
                        int64_t ld, int64_t n, T sigma2, int* flag, hipStream_t s) {
-    const int Kr = K.need_r2 ? (int)pr::rup(d + 2, pr::KG) : 0, Kp = K.nper ? (int)pr::rup(3 * d, pr::KG) : 0;
+    const int Kr = pr::kr_of(K, d), Kp = pr::kp_of(K, d);
     const int64_t nt = nf / GT;
     const dim3 grid((unsigned)(nt * (nt + 1) / 2));
     ProfScope ps(KC_BUILD, s, 2.0 * (double)GT * GT * (Kr + Kp) * nt * (nt + 1) / 2,
                  (double)sizeof(T) * (n * (double)d + (double)n * (n + 1) / 2));
-    GPRX_PAIRS_DISPATCH(kbuild_mma_kernel, Kd, FU, FV, nf, Kr, Kp, A, ld, n, sigma2, flag);
+    GPRX_PAIRS_DISPATCH(kbuild_mma_kernel, Kd, FU, FV, nf, Kr, Kp, T(0.5) * T(d), A, ld, n, sigma2, flag);
     GPRX_HIP(hipGetLastError());
 }
 
 template <typename T>
 void launch_predict_mma(const KCanon<T>& K, const KCanon<T>* Kd, const T* FU, int64_t nfu, const T* FV, int64_t nfv,
                         int d, const T* alpha, int64_t n, int m, int64_t q, T* mean, hipStream_t s) {
-    const int Kr = K.need_r2 ? (int)pr::rup(d + 2, pr::KG) : 0, Kp = K.nper ? (int)pr::rup(3 * d, pr::KG) : 0;
+    const int Kr = pr::kr_of(K, d), Kp = pr::kp_of(K, d);
     const dim3 grid((unsigned)(nfu / GT));
     ProfScope ps(KC_PREDICT, s, (double)q * n * (2.0 * d + 2.0 * m), (double)sizeof(T) * (double)(q + n) * d);
-    GPRX_PAIRS_DISPATCH(predict_mma_kernel, Kd, FU, nfu, FV, nfv, Kr, Kp, alpha, n, m, q, mean);
+    GPRX_PAIRS_DISPATCH(predict_mma_kernel, Kd, FU, nfu, FV, nfv, Kr, Kp, T(0.5) * T(d), alpha, n, m, q, mean);
     GPRX_HIP(hipGetLastError());
 }
 
