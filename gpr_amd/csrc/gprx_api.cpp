@@ -305,7 +305,7 @@ static gprx_status model_fit(gprx_model* M, uint32_t flags, gprx_fit_info* out) 
     M->info.ensure(sizeof(int));
     M->flag.ensure(sizeof(int));
     M->red.ensure(sizeof(double) * 2);
-    if (K.nper > 0) {
+    if (K.nper > 0) {  // per-sample sin/cos tables: the direct build, predict, posterior and LML paths
         M->tab.ensure(sizeof(T) * 2 * K.nper * n * M->d);
         launch_sincos_tables<T>(K, M->X.as<T>(), n, M->d, M->tab.as<T>(), s);
     }
@@ -315,6 +315,12 @@ static gprx_status model_fit(gprx_model* M, uint32_t flags, gprx_fit_info* out) 
     const T sigma2 = sig * sig;  // m_Sigma*m_Sigma in T (lib/GaussianProcess.cpp:379)
     GPRX_HIP(hipEventRecord(ctx->ev[0], s));
     static const bool direct_build = std::getenv("GPRX_KBUILD") && std::string(std::getenv("GPRX_KBUILD")) == "direct";
+    // GPRX_KBUILD=separate: the MFMA build as its own kernel instead of BUILD tasks inside
+    // the tile factorisation (where the tile builds fill the factorisation's start-up ramp)
+    static const bool separate_build =
+        std::getenv("GPRX_KBUILD") && std::string(std::getenv("GPRX_KBUILD")) == "separate";
+    TileBuild<T> tb;
+    std::memset(&tb, 0, sizeof(tb));
     if ((!dist || ctx->world == 1) && !direct_build && pairs_mma_supported<T>(K, 1)) {
         // pair statistics on the MFMA units from per-sample features (k_pairs.hip)
         const int64_t kf = pairs_feature_cols<T>(K, M->d);
@@ -324,8 +330,12 @@ static gprx_status model_fit(gprx_model* M, uint32_t flags, gprx_fit_info* out) 
         launch_pair_features<T>(K, M->X.as<T>(), n, M->d, M->X.as<T>(), true, M->featV.as<T>(), np, s);
         M->kdev.ensure(sizeof(KCanon<T>));
         GPRX_HIP(hipMemcpyAsync(M->kdev.p, &K, sizeof(KCanon<T>), hipMemcpyHostToDevice, s));
-        launch_kbuild_mma<T>(K, M->kdev.as<KCanon<T>>(), M->featU.as<T>(), M->featV.as<T>(), np, M->d, M->A.as<T>(), ld,
-                             n, sigma2, M->flag.as<int>(), s);
+        if (!dist && !separate_build && potrf_uses_tiles())
+            tb = pairs_tile_build<T>(K, M->kdev.as<KCanon<T>>(), M->featU.as<T>(), M->featV.as<T>(), np, M->d, n, sigma2,
+                                     M->flag.as<int>());
+        if (!tb.mode)
+            launch_kbuild_mma<T>(K, M->kdev.as<KCanon<T>>(), M->featU.as<T>(), M->featV.as<T>(), np, M->d, M->A.as<T>(),
+                                 ld, n, sigma2, M->flag.as<int>(), s);
         launch_aug_rows<T>(M->Y.as<T>(), n, M->m, M->A.as<T>(), ld, np, mp, s);
     } else if (!dist || ctx->world == 1) {
         launch_kbuild<T>(K, M->X.as<T>(), M->tab.as<T>(), n, M->X.as<T>(), M->tab.as<T>(), n, M->d, M->A.as<T>(), ld,
@@ -369,6 +379,8 @@ static gprx_status model_fit(gprx_model* M, uint32_t flags, gprx_fit_info* out) 
             const ncclResult_t r = ncclAllReduce(M->flag.p, M->flag.p, 1, ncclInt32, ncclMax, ctx->comm, s);
             if (r != ncclSuccess) throw Error{GPRX_ERR_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(r)};
         }
+    } else if (tb.mode) {
+        potrf_tiles<T>(M->A.as<T>(), ld, np, ld, M->Linv.as<T>(), M->info.as<int>(), ctx->ex, &tb);
     } else {
         potrf_auto<T>(M->A.as<T>(), ld, np, ld, M->Linv.as<T>(), M->info.as<int>(), ctx->ex);
     }

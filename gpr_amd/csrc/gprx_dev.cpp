@@ -188,9 +188,10 @@ extern "C" int64_t gprx_dev_pt_trace(int32_t* tasks, int64_t* times, int64_t max
 }
 extern "C" int32_t gprx_dev_pt_debug(int32_t* out, int32_t max_wg) { return gprx::pt_debug_snapshot(out, max_wg); }
 
-extern "C" gprx_status gprx_dev_schedule(int32_t nc, int32_t nr, int32_t P, double* est_us, int64_t* ntasks) {
+extern "C" gprx_status gprx_dev_schedule(int32_t nc, int32_t nr, int32_t P, int32_t build, double* est_us,
+                                         int64_t* ntasks) {
     try {
-        const int64_t n = potrf_tiles_schedule_stats(nc, nr, P, est_us);
+        const int64_t n = potrf_tiles_schedule_stats(nc, nr, P, build != 0, est_us);
         if (ntasks) *ntasks = n;
         return GPRX_OK;
     } catch (const Error& e) {

@@ -333,14 +333,38 @@ struct Exec {
 int outer_block();
 template <typename T>
 void potrf_blocked(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info, Exec& ex);
+// The covariance build fused into the tile factorisation: each lower tile of the leading
+// np x np block is built from the pair-statistics features (k_pairs.h) by a BUILD task of
+// the same persistent launch, ahead of its first consumer, instead of by a separate kernel.
+// mode: 1 = periodic + r2 statistics, 2 = r2 only, 3 = periodic only.  Rows >= np (the
+// label rows) must already be in A.  A non-finite value sets *flag.
+template <typename T>
+struct TileBuild {
+    const KCanon<T>* Kd;
+    const T* FU;
+    const T* FV;
+    int64_t nf;
+    int Kr, Kp;
+    T hd, sigma2;
+    int64_t n;
+    int* flag;
+    int mode;
+};
+// The BUILD description of K(X, X) + sigma2 I from the features of launch_pair_features
+// (k_pairs.hip; the same trees as launch_kbuild_mma).
+template <typename T>
+TileBuild<T> pairs_tile_build(const KCanon<T>& K, const KCanon<T>* Kd, const T* FU, const T* FV, int64_t nf, int d,
+                              int64_t n, T sigma2, int* flag);
 // Same contract, one persistent launch: 128x128 tile tasks scheduled on the device by
 // dependency counters (k_ptiles.hip).  A timed-out dependency wait sets *info = -1.
 template <typename T>
-void potrf_tiles(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info, Exec& ex);
+void potrf_tiles(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info, Exec& ex,
+                 const TileBuild<T>* build = nullptr);
 // Factorisation used by the fit paths: potrf_tiles unless GPRX_POTRF=streams.
 template <typename T>
 void potrf_auto(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info, Exec& ex);
-int64_t potrf_tiles_schedule_stats(int nc, int nr, int P, double* est_us);
+bool potrf_uses_tiles();
+int64_t potrf_tiles_schedule_stats(int nc, int nr, int P, bool build, double* est_us);
 // Multi-GPU form: column panels of outer_block() columns dealt cyclically over `world`
 // ranks (np must be a multiple of outer_block()); the factored panels are RCCL-broadcast so
 // every rank ends with the full factor.  pack: device scratch of nrows * outer_block().

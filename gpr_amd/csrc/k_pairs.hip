@@ -19,20 +19,11 @@
 // S = sin(2b x~_k).  Feature matrices are column-major (rows padded to 128, columns to 16) so
 // the tile kernel streams them with LDS-DMA like any GEMM operand; the squared norms sit in
 // one more column after the MFMA operands and are added in the epilogue.
-#include "gprx_internal.h"
-#include "k_mma.h"
-
-#include <type_traits>
+#include "k_pairs.h"
 
 namespace gprx {
 
 namespace pr {
-
-using namespace mm;
-
-constexpr int KG = 16;  // feature-column granule (the tile kernel's k-stage)
-
-static int64_t rup(int64_t x, int64_t g) { return (x + g - 1) / g * g; }
 
 // F (np x (Kr + Kp + 1), column-major, ld np): the left (U) or right (V) features of n
 // samples, then their squared norms |x~|^2.  Padding rows are all zero.
@@ -65,84 +56,6 @@ __global__ void features_kernel(const T* __restrict__ X, int64_t n, int d, const
     }
 }
 
-// Kernel values of E pairs from their (r2, S) for the trees this file accepts (no White
-// leaf, one periodic table).  Same formulas and products/sums as kernel_value/leaf_value
-// (0 + x and 1 * x are exact, so the results are bit-identical), but organised leaf-outer:
-// the loops over leaves and terms are wave-uniform (leaf constants come in through scalar
-// loads, the type test is a uniform branch) and the per-pair work is an unrolled,
-// statically indexed loop over E registers.  The generic kernel_value reached from 32
-// unrolled call sites per thread was emitted as an out-of-line call per pair.
-template <typename T, int E, bool MUL>
-__device__ __forceinline__ void leaf_into(const KLeaf<T>* __restrict__ L, const T (&r2)[E], const T (&s)[E],
-                                          T (&p)[E]) {
-    const int ty = L->type;
-    const T c0 = L->c0, c1 = L->c1, c2 = L->c2;
-    if (ty == L_PERIODIC) {
-#pragma unroll
-        for (int e = 0; e < E; e++) {
-            const T f = c0 * exp(c1 * s[e]);
-            p[e] = MUL ? p[e] * f : p[e] + f;
-        }
-    } else if (ty == L_RQ) {
-#pragma unroll
-        for (int e = 0; e < E; e++) {
-            const T f = c0 * exp(-c2 * log1p(c1 * r2[e]));
-            p[e] = MUL ? p[e] * f : p[e] + f;
-        }
-    } else {  // L_GAUSS, L_GAUSS_EXP
-#pragma unroll
-        for (int e = 0; e < E; e++) {
-            const T f = c0 * exp(c1 * r2[e]);
-            p[e] = MUL ? p[e] * f : p[e] + f;
-        }
-    }
-}
-
-template <typename T, int E>
-__device__ __forceinline__ void pair_values(const KCanon<T>* __restrict__ K, const T (&r2)[E], const T (&s)[E],
-                                            T (&v)[E]) {
-#pragma unroll
-    for (int e = 0; e < E; e++) v[e] = 0;
-    const int nl = K->nleaf;
-    if (K->sum_leaves) {
-#pragma unroll 1
-        for (int l = 0; l < nl; l++) leaf_into<T, E, false>(&K->leaf[l], r2, s, v);
-        return;
-    }
-    const int nt = K->nterm;
-#pragma unroll 1
-    for (int t = 0; t < nt; t++) {
-        const unsigned msk = K->term_mask[t];
-        T p[E];
-#pragma unroll
-        for (int e = 0; e < E; e++) p[e] = 1;
-#pragma unroll 1
-        for (int l = 0; l < nl; l++)
-            if (msk & (1u << l)) leaf_into<T, E, true>(&K->leaf[l], r2, s, p);
-#pragma unroll
-        for (int e = 0; e < E; e++) v[e] += p[e];
-    }
-}
-
-// Statistics of the 128 x 128 pair block (rows from FU + i0, columns from FV + j0).
-template <typename T, int NPER, bool R2>
-__device__ __forceinline__ void block_stats(const T* FU, int64_t nu, int64_t i0, const T* FV, int64_t nv, int64_t j0,
-                                            int Kr, int Kp, T* smem, int t, typename Mfma<T>::acc_t (&ar)[2][4],
-                                            typename Mfma<T>::acc_t (&ap)[2][4]) {
-    if (R2) tile_mma<T>(ar, FU + i0, nu, FV + j0, nv, Kr, true, smem, t);
-    if (NPER) {
-        __syncthreads();  // the second product reuses the staging ring
-        tile_mma<T>(ap, FU + (int64_t)Kr * nu + i0, nu, FV + (int64_t)Kr * nv + j0, nv, Kp, true, smem, t);
-    }
-}
-
-// (r2, S) of one pair from the tile products and the per-sample norms (hd = d / 2)
-template <typename T, int NPER, bool R2>
-__device__ __forceinline__ void pair_stats(T pr2, T pper, T nu, T nv, T hd, T& r2, T& sp) {
-    r2 = R2 ? fmax(nu + nv + pr2, T(0)) : T(0);
-    sp = NPER ? fmax(fma(T(-0.5), pper, hd), T(0)) : T(0);
-}
-
 // Lower triangle of K(X, X) (+ sigma2 on the diagonal, identity padding) into A (column-major).
 template <typename T, int NPER, bool R2>
 __global__ __launch_bounds__(NT) void kbuild_mma_kernel(const KCanon<T>* __restrict__ Kd, const T* __restrict__ FU,
@@ -151,7 +64,6 @@ __global__ __launch_bounds__(NT) void kbuild_mma_kernel(const KCanon<T>* __restr
                                                         int64_t ld, int64_t n, T sigma2, int* __restrict__ flag) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     T* smem = reinterpret_cast<T*>(smem_raw);
-    typedef Mfma<T> Tr;
     // the kernel tree is read from device memory (scalar loads): as a by-value kernel
     // argument indexed per leaf/term, hipcc copied it to scratch
     int64_t ti, tj;
@@ -163,60 +75,8 @@ __global__ __launch_bounds__(NT) void kbuild_mma_kernel(const KCanon<T>* __restr
         ti = i;
         tj = b - i * (i + 1) / 2;
     }
-    const int64_t i0 = ti * GT, j0 = tj * GT;
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    const int wr = w & 1, wc = w >> 1, lr = lane & 15, lk = lane >> 4;
-    T nu[4], nv[2][4];  // squared norms of this thread's rows and columns
-#pragma unroll
-    for (int y = 0; y < 4; y++) nu[y] = R2 ? FU[(int64_t)(Kr + Kp) * nf + i0 + wr * 64 + y * 16 + lr] : T(0);
-#pragma unroll
-    for (int x = 0; x < 2; x++)
-#pragma unroll
-        for (int reg = 0; reg < 4; reg++)
-            nv[x][reg] = R2 ? FV[(int64_t)(Kr + Kp) * nf + j0 + wc * 32 + x * 16 + Tr::orow(lk, reg)] : T(0);
-    typename Tr::acc_t ar[2][4], ap[2][4];
-    block_stats<T, NPER, R2>(FU, nf, i0, FV, nf, j0, Kr, Kp, smem, t, ar, ap);
-    bool bad = false;
-    // four chunks of 8 pairs per thread (column group x, registers 2h, 2h+1):
-    // statistics -> values -> stores; 8 keeps the interleaved exp sequences within registers
-    auto chunk = [&](auto cc) {
-        constexpr int x = decltype(cc)::value >> 1, h = decltype(cc)::value & 1;
-        T r2[8], sp[8], v[8];
-#pragma unroll
-        for (int reg = 2 * h; reg < 2 * h + 2; reg++)
-#pragma unroll
-            for (int y = 0; y < 4; y++) {
-                const int64_t gj = j0 + wc * 32 + x * 16 + Tr::orow(lk, reg);
-                const int64_t gi = i0 + wr * 64 + y * 16 + lr;
-                T a, b;
-                pair_stats<T, NPER, R2>(R2 ? ar[x][y][reg] : T(0), NPER ? ap[x][y][reg] : T(0), nu[y], nv[x][reg], hd,
-                                        a, b);
-                r2[(reg - 2 * h) * 4 + y] = gi == gj ? T(0) : a;
-                sp[(reg - 2 * h) * 4 + y] = gi == gj ? T(0) : b;
-            }
-        pair_values<T, 8>(Kd, r2, sp, v);
-#pragma unroll
-        for (int reg = 2 * h; reg < 2 * h + 2; reg++) {
-            const int64_t gj = j0 + wc * 32 + x * 16 + Tr::orow(lk, reg);
-            T* col = A + gj * ld;
-#pragma unroll
-            for (int y = 0; y < 4; y++) {
-                const int64_t gi = i0 + wr * 64 + y * 16 + lr;
-                T val = v[(reg - 2 * h) * 4 + y];
-                if (gi >= n || gj >= n) {
-                    val = (gi == gj) ? T(1) : T(0);
-                } else {
-                    if (!isfinite(val)) bad = true;
-                    if (gi == gj) val += sigma2;
-                }
-                if (gi >= gj) col[gi] = val;
-            }
-        }
-    };
-    chunk(std::integral_constant<int, 0>{});
-    chunk(std::integral_constant<int, 1>{});
-    chunk(std::integral_constant<int, 2>{});
-    chunk(std::integral_constant<int, 3>{});
+    const bool bad = build_tile<T, NPER, R2>(Kd, FU, FV, nf, Kr, Kp, hd, A, ld, n, sigma2, ti * GT, tj * GT, smem,
+                                                    threadIdx.x);
     if (bad) atomicOr(flag, 1);
 }
 
@@ -320,17 +180,6 @@ bool pairs_mma_supported(const KCanon<T>& K, int m) {
     return K.need_r2 || K.nper > 0;
 }
 
-namespace pr {
-template <typename T>
-static int kr_of(const KCanon<T>& K, int d) {  // MFMA depth of the r2 product
-    return K.need_r2 ? (int)rup(d, KG) : 0;
-}
-template <typename T>
-static int kp_of(const KCanon<T>& K, int d) {  // MFMA depth of the periodic product
-    return K.nper ? (int)rup(2 * d, KG) : 0;
-}
-}  // namespace pr
-
 // feature columns of one sample set (Kr + Kp operand columns + the squared norms)
 template <typename T>
 int64_t pairs_feature_cols(const KCanon<T>& K, int d) {
@@ -388,7 +237,34 @@ void launch_predict_mma(const KCanon<T>& K, const KCanon<T>* Kd, const T* FU, in
     GPRX_HIP(hipGetLastError());
 }
 
+template <typename T>
+TileBuild<T> pairs_tile_build(const KCanon<T>& K, const KCanon<T>* Kd, const T* FU, const T* FV, int64_t nf, int d,
+                              int64_t n, T sigma2, int* flag) {
+    TileBuild<T> b;
+    b.Kd = Kd;
+    b.FU = FU;
+    b.FV = FV;
+    b.nf = nf;
+    b.Kr = pr::kr_of(K, d);
+    b.Kp = pr::kp_of(K, d);
+    b.hd = T(0.5) * T(d);
+    b.sigma2 = sigma2;
+    b.n = n;
+    b.flag = flag;
+    // as GPRX_PAIRS_DISPATCH.  0 (no fused build: the caller launches kbuild_mma_kernel) for
+    // trees with products, which build_tile_sum does not separate, and for RationalQuadratic
+    // leaves: the fused path carries exp-form leaves only, to keep the factorisation kernel
+    // small (its code and register budget are shared with every other task type)
+    bool expform = K.sum_leaves != 0;
+    for (int l = 0; l < K.nleaf; l++)
+        if (K.leaf[l].type != L_GAUSS && K.leaf[l].type != L_GAUSS_EXP && K.leaf[l].type != L_PERIODIC) expform = false;
+    b.mode = !expform ? 0 : (K.nper && K.need_r2) ? 1 : (K.nper ? 3 : 2);
+    return b;
+}
+
 #define GPRX_PAIRS_INST(T)                                                                                    \
+    template TileBuild<T> pairs_tile_build<T>(const KCanon<T>&, const KCanon<T>*, const T*, const T*, int64_t, int, \
+                                              int64_t, T, int*);                                              \
     template bool pairs_mma_supported<T>(const KCanon<T>&, int);                                              \
     template int64_t pairs_feature_cols<T>(const KCanon<T>&, int);                                            \
     template void launch_pair_features<T>(const KCanon<T>&, const T*, int64_t, int, const T*, bool, T*, int64_t, \

@@ -593,14 +593,18 @@ int* Exec::scratch_ints(size_t n) {
     return scratch;
 }
 
-template <typename T>
-void potrf_auto(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info, Exec& ex) {
+bool potrf_uses_tiles() {
     static const bool streams = [] {
         const char* e = std::getenv("GPRX_POTRF");
         return e && std::string(e) == "streams";
     }();
-    if (streams) potrf_blocked<T>(A, ld, np, nrows, Linv, info, ex);
-    else potrf_tiles<T>(A, ld, np, nrows, Linv, info, ex);
+    return !streams;
+}
+
+template <typename T>
+void potrf_auto(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info, Exec& ex) {
+    if (potrf_uses_tiles()) potrf_tiles<T>(A, ld, np, nrows, Linv, info, ex);
+    else potrf_blocked<T>(A, ld, np, nrows, Linv, info, ex);
 }
 
 // Two-level right-looking Cholesky with look-ahead.

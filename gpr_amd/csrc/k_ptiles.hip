@@ -38,7 +38,7 @@
 // operands staged 32-deep through LDS, double-buffered; 147 KB of LDS per workgroup also
 // keeps the launch at one workgroup per CU, so the critical DIAGX step has a whole CU.
 #include "gprx_internal.h"
-#include "k_mma.h"
+#include "k_pairs.h"
 
 #include <algorithm>
 #include <climits>
@@ -48,6 +48,7 @@
 #include <map>
 #include <mutex>
 #include <queue>
+#include <tuple>
 
 namespace gprx {
 
@@ -374,6 +375,9 @@ struct Args {
     int* dbg;          // GPRX_PT_DEBUG: per-workgroup {ticket, phase, i, j} in pinned host memory
     int variant;       // GPRX_PT_VARIANT debug bits: 1 no TRSM math, 2 no UPD math, 4 no diag factor
     long long* trace;  // GPRX_PT_TRACE: per ticket {ticket taken, inputs ready, published, workgroup}
+    const TileBuild<T>* tb;  // BUILD tasks: covariance tiles from pair statistics (device copy,
+                             // read per task: as kernel arguments they stayed live in SGPRs and
+                             // pushed the whole kernel into spills)
 };
 
 
@@ -392,8 +396,18 @@ __device__ bool wait_inputs(const Args<T>& a, int type, int i, int j, int b0, in
     int lwant1;
     const int* lp2;
     int lwant2;
-    if (type == T_DIAGX) {
-        if (i == 0) return true;
+    if (type == T_DIAGX && i == 0) {  // the first diagonal tile is built
+        vp = a.ver;
+        vwant = 0;
+        vp2 = vp;
+        vwant2 = 0;
+        lp1 = a.lcnt;
+        lwant1 = 0;
+        lp2 = lp1;
+        lwant2 = 0;
+    } else if (type == T_BUILD) {
+        return true;
+    } else if (type == T_DIAGX) {
         vp = a.ver + (int64_t)i * a.nc + (i - 1);
         vwant = i - 1;
         vp2 = a.ver + (int64_t)i * a.nc + i;
@@ -479,7 +493,17 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
         int tid = t;
         asm volatile("" : "+v"(tid));
         T* Ci = a.A + (int64_t)i * GT;  // row block i, column 0
-        if (type == T_UPD) {
+        if (type == T_BUILD) {
+            // ver[i][j] goes from -1 (not built) to 0; the tile's values go out write-through
+            const TileBuild<T>& b = *a.tb;
+            bool bad;
+            // one instantiation for every mode: an absent statistic has a zero-depth product
+            // (its accumulators stay 0) and no leaves of its class
+            bad = pr::build_tile_sum<T, 1, true>(b.Kd, b.FU, b.FV, b.nf, b.Kr, b.Kp, b.hd, a.A, ld, b.n, b.sigma2,
+                                                 (int64_t)i * GT, (int64_t)j * GT, smem, tid);
+            if (__builtin_amdgcn_readfirstlane(__any(bad))) atomicOr(b.flag, 1);  // wave-uniform branch
+            publish(a.ver + (int64_t)i * a.nc + j, 0, false);
+        } else if (type == T_UPD) {
             // variant 64 (timing experiment, wrong results): every update streams the same
             // L2-resident operands, to separate memory-feed from MFMA limits
             const int64_t oa = (a.variant & 64) ? 0 : (int64_t)i * GT + (int64_t)b0 * GT * ld;
@@ -538,6 +562,7 @@ struct Cost {  // per-task durations (us, one CU), calibrated from GPRX_PT_TRACE
     double diag0 = 70.0;   // DIAGX(0): factor/inverse only
     double early = 20.0;   // DIAGX(k) publishes L_{k,k-1} after its trsm phase
     double diagf = 0.97;   // diagonal-tile update relative to a full one (2 of 8 waves idle)
+    double build = 28.0;   // BUILD tile (pair statistics + kernel values + stores)
 };
 
 struct Task {
@@ -576,7 +601,7 @@ static void tile_chunks(int i, int j, int W, int near, std::vector<std::pair<int
     for (; b < e; b++) out.push_back({b, 1});
 }
 
-static Schedule make_schedule(int nc, int nr, int W, int near, int P, const Cost& cm) {
+static Schedule make_schedule(int nc, int nr, int W, int near, int P, const Cost& cm, bool build) {
     std::vector<Task> tasks;
     tasks.reserve((size_t)nr * nc * 2);
     auto add = [&](int type, int i, int j, int b0, int nb, double dur) {
@@ -630,8 +655,13 @@ static Schedule make_schedule(int nc, int nr, int W, int near, int P, const Cost
         }
     };
     // Creation order (checked below) puts every producer before its consumers:
-    // DIAGX(0); per k: TRSM(., k), DIAGX(k+1), the update chunks ending at block k.
+    // [BUILD(i, j) for the lower tiles], DIAGX(0); per k: TRSM(., k), DIAGX(k+1), the update
+    // chunks ending at block k.  A tile's BUILD is its first "update".
+    if (build)
+        for (int i = 0; i < nc; i++)
+            for (int j = 0; j <= i; j++) last_upd[(size_t)i * nc + j] = add(T_BUILD, i, j, 0, 0, cm.build);
     make_diagx(0);
+    dep(diagx[0], last_upd[0]);
     for (int k = 0; k < nc; k++) {
         for (int i = k + 1; i < nr; i++) {
             if (i == k + 1 && i < nc) continue;  // inside DIAGX(k+1)
@@ -734,6 +764,7 @@ struct Params {
         if (const char* e = std::getenv("GPRX_PT_TRSM_US")) cm.trsm = std::atof(e);
         if (const char* e = std::getenv("GPRX_PT_K128_US")) cm.k128 = std::atof(e);
         if (const char* e = std::getenv("GPRX_PT_OVH_US")) cm.ovh = std::atof(e);
+        if (const char* e = std::getenv("GPRX_PT_BUILD_US")) cm.build = std::atof(e);
     }
 };
 static const Params& params() {
@@ -751,7 +782,7 @@ struct PtState {
         double est_us = 0;
         std::vector<int4> host;
     };
-    std::map<std::pair<int, int>, Dev> sched;
+    std::map<std::tuple<int, int, bool>, Dev> sched;
     int* ctr = nullptr;
     size_t ctr_ints = 0;
     int ncu = 0;
@@ -759,7 +790,9 @@ struct PtState {
     long long* trace = nullptr;  // GPRX_PT_TRACE timeline of the last launch (+ DIAGX phases)
     int64_t trace_n = 0, trace_nc = 0;
     const std::vector<int4>* last_list = nullptr;
+    void* tb = nullptr;  // device copy of the launch's TileBuild
     ~PtState() {
+        if (tb) (void)hipFree(tb);
         if (trace) (void)hipFree(trace);
         if (dbg) (void)hipHostFree(dbg);
         for (auto& kv : sched) (void)hipFree(kv.second.list);
@@ -792,7 +825,7 @@ int pt_debug_snapshot(int* out, int max_wg) {
 }
 
 template <typename T>
-void potrf_tiles(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info, Exec& ex) {
+void potrf_tiles(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info, Exec& ex, const TileBuild<T>* build) {
     using namespace pt;
     if (!ex.pt) ex.pt = new PtState();
     PtState& st = *ex.pt;
@@ -805,11 +838,12 @@ void potrf_tiles(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info
     }
     GPRX_REQUIRE(np % DB == 0 && nrows % GT == 0 && nrows >= np, GPRX_ERR_ARG, "potrf_tiles: bad sizes");
     const int nc = (int)(np / DB), nr = (int)(nrows / GT);
-    auto key = std::make_pair(nc, nr);
+    const bool fused = build && build->mode != 0;
+    auto key = std::make_tuple(nc, nr, fused);
     auto it = st.sched.find(key);
     if (it == st.sched.end()) {
         const Params& pr = params();
-        Schedule S = make_schedule(nc, nr, pr.W, pr.near, st.ncu, pr.cm);
+        Schedule S = make_schedule(nc, nr, pr.W, pr.near, st.ncu, pr.cm, fused);
         PtState::Dev d;
         d.n = (int64_t)S.list.size();
         d.est_us = S.est_us;
@@ -828,6 +862,8 @@ void potrf_tiles(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info
     }
     hipStream_t s = ex.s0;
     GPRX_HIP(hipMemsetAsync(st.ctr, 0, sizeof(int) * need, s));
+    if (fused)  // ver = -1 (not built) for the tiles of the leading block; the label rows are built
+        GPRX_HIP(hipMemsetAsync(st.ctr + C_NCTL + nr, 0xff, sizeof(int) * (size_t)nc * nc, s));
     Args<T> a;
     a.A = A;
     a.ld = ld;
@@ -839,6 +875,13 @@ void potrf_tiles(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info
     a.lcnt = st.ctr + C_NCTL;
     a.ver = st.ctr + C_NCTL + nr;
     a.info = info;
+    a.tb = nullptr;
+    if (fused) {
+        GPRX_REQUIRE(build->nf == np, GPRX_ERR_ARG, "potrf_tiles: build features must have np rows");
+        if (!st.tb) GPRX_HIP(hipMalloc(&st.tb, sizeof(TileBuild<double>)));
+        GPRX_HIP(hipMemcpyAsync(st.tb, build, sizeof(TileBuild<T>), hipMemcpyHostToDevice, s));
+        a.tb = reinterpret_cast<const TileBuild<T>*>(st.tb);
+    }
     a.dbg = nullptr;
     a.trace = nullptr;
     static const bool tracing = std::getenv("GPRX_PT_TRACE") != nullptr;
@@ -884,15 +927,15 @@ void potrf_tiles(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info
 
 // Host-only schedule statistics (no device work): tasks, predicted makespan, and a check
 // that every task's producers come earlier in the ticket order.
-int64_t potrf_tiles_schedule_stats(int nc, int nr, int P, double* est_us) {
+int64_t potrf_tiles_schedule_stats(int nc, int nr, int P, bool build, double* est_us) {
     if (nc < 1 || nr < nc || P < 1) throw Error{GPRX_ERR_ARG, "potrf tile schedule: need nc >= 1, nr >= nc, P >= 1"};
     const pt::Params& pr = pt::params();
-    pt::Schedule S = pt::make_schedule(nc, nr, pr.W, pr.near, P, pr.cm);
+    pt::Schedule S = pt::make_schedule(nc, nr, pr.W, pr.near, P, pr.cm, build);
     if (est_us) *est_us = S.est_us;
     return S.ntasks;
 }
 
-template void potrf_tiles<double>(double*, int64_t, int64_t, int64_t, double*, int*, Exec&);
-template void potrf_tiles<float>(float*, int64_t, int64_t, int64_t, float*, int*, Exec&);
+template void potrf_tiles<double>(double*, int64_t, int64_t, int64_t, double*, int*, Exec&, const TileBuild<double>*);
+template void potrf_tiles<float>(float*, int64_t, int64_t, int64_t, float*, int*, Exec&, const TileBuild<float>*);
 
 }  // namespace gprx

@@ -22,9 +22,10 @@ extern "C" {
 gprx_status gprx_dev_bench(gprx_ctx* ctx, gprx_dtype dtype, int32_t what, int64_t M, int64_t N, int64_t K,
                            int32_t iters, double* ms);
 /* Host-only: build the tile-dataflow potrf schedule for nc diagonal blocks, nr row blocks
- * and P workers; returns its task count and simulated makespan (us).  Throws nothing, needs no
+ * and P workers (build != 0: with the fused covariance-build tasks); returns its task count
+ * and simulated makespan (us).  Throws nothing, needs no
  * device: GPRX_ERR_ARG if the ticket order would violate a dependency. */
-gprx_status gprx_dev_schedule(int32_t nc, int32_t nr, int32_t P, double* est_us, int64_t* ntasks);
+gprx_status gprx_dev_schedule(int32_t nc, int32_t nr, int32_t P, int32_t build, double* est_us, int64_t* ntasks);
 /* GPRX_PT_DEBUG=1: copy the per-workgroup status {ticket, phase, i, j} of the running (or last)
  * potrf_tiles launch out of pinned host memory, without synchronising; returns workgroups. */
 int32_t gprx_dev_pt_debug(int32_t* out, int32_t max_wg);

@@ -15,7 +15,19 @@ L.gprx_dev_pt_trace.restype = ctypes.c_int64
 ctx = gpr_amd.Context(0)
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 16384
 ms = ctypes.c_double()
-assert L.gprx_dev_bench(ctx.h, 1, 9, n, 0, 0, 2, ctypes.byref(ms)) == 0
+if os.environ.get("PT_TRACE_FIT"):  # the C3 fit (fused covariance build) instead of a bare factorisation
+    from gpr_amd.synth import C3, make_data
+    X, Y = make_data(n, C3["d"], C3["m"])
+    M = gpr_amd.Model(ctx, np.float64)
+    M.set_data(X, Y)
+    M.set_kernel(C3["kernel"])
+    M.set_noise(C3["sigma"])
+    M.fit()
+    info = M.fit()
+    ms.value = info.ms_factor
+    n = ((n + 127) // 128) * 128
+else:
+    assert L.gprx_dev_bench(ctx.h, 1, 9, n, 0, 0, 2, ctypes.byref(ms)) == 0
 MAX = 400000
 tasks = np.zeros((MAX, 4), np.int32)
 times = np.zeros((MAX, 4), np.int64)
@@ -43,8 +55,8 @@ okc = dur_ticks > 500
 clock_ghz = float(np.median(cyc[okc] / dur_ticks[okc]) * 0.1)
 res = {"clock_ghz_median": clock_ghz, "n": n, "ms_devbench": ms.value, "span_us": span, "tasks": int(k), "workers": P,
        "busy_frac": float(ex.sum() / (span * P)), "wait_frac": float(wt.sum() / (span * P))}
-names = {0: "DIAGX", 1: "TRSM", 2: "UPD"}
-for t in (0, 1, 2):
+names = {0: "DIAGX", 1: "TRSM", 2: "UPD", 3: "BUILD"}
+for t in (0, 1, 2, 3):
     for b in sorted(set(nb[typ == t])):
         m = (typ == t) & (nb == b)
         diag = (tasks[:, 1] == tasks[:, 2])

@@ -10,13 +10,13 @@ import pytest
 from gpr_amd.gprx import lib
 
 
-def _sched(nc, nr, P=256, env=None):
+def _sched(nc, nr, P=256, build=False):
     L = lib()
-    L.gprx_dev_schedule.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+    L.gprx_dev_schedule.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                     ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]
     est = ctypes.c_double()
     n = ctypes.c_int64()
-    st = L.gprx_dev_schedule(nc, nr, P, ctypes.byref(est), ctypes.byref(n))
+    st = L.gprx_dev_schedule(nc, nr, P, 1 if build else 0, ctypes.byref(est), ctypes.byref(n))
     return st, n.value, est.value
 
 
@@ -51,6 +51,17 @@ def test_schedule_valid_and_counted(nc, extra):
     assert st == 0, "ticket order violates a dependency"
     assert n == _expected_tasks(nc, nc + extra)
     assert est > 0
+
+
+@pytest.mark.parametrize("nc", [1, 2, 9, 64])
+def test_schedule_with_fused_build(nc):
+    """BUILD tasks (one per lower tile of the leading block) come first in creation order and
+    every consumer of a tile depends on its build: still a valid ticket order."""
+    st, n, est = _sched(nc, nc + 1, build=True)
+    assert st == 0, "ticket order violates a dependency"
+    assert n == _expected_tasks(nc, nc + 1) + nc * (nc + 1) // 2
+    _, _, est0 = _sched(nc, nc + 1)
+    assert est >= est0  # the builds add work
 
 
 def test_schedule_makespan_scales():
