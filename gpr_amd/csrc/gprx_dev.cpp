@@ -177,6 +177,15 @@ static gprx_status bench_impl(int what, int64_t M, int64_t N, int64_t K, int ite
 namespace gprx {
 int pt_debug_snapshot(int* out, int max_wg);
 int64_t pt_trace_copy(int32_t* tasks, long long* times, int64_t max);
+int64_t bs_trace_copy(long long* out, int64_t max_blocks);
+}
+extern "C" int64_t gprx_dev_bs_trace(int64_t* times, int64_t max_blocks) {
+    try {
+        return gprx::bs_trace_copy((long long*)times, max_blocks);
+    } catch (const Error& e) {
+        std::fprintf(stderr, "gprx_dev_bs_trace: %s\n", e.msg.c_str());
+        return -1;
+    }
 }
 extern "C" int64_t gprx_dev_pt_trace(int32_t* tasks, int64_t* times, int64_t max) {
     try {

@@ -26,9 +26,16 @@ namespace gprx {
 
 namespace bs {
 
-constexpr int NT = 256;   // 4 waves; wave w owns columns 32w..32w+31 of the block
-constexpr int CPW = DB / 4;
+constexpr int NT = 512;        // 8 waves
+constexpr int QR = DB / 4;     // rows per thread in the column layout: thread t -> column
+                               // c = t & 127, rows QR q .. QR q + QR - 1, q = t >> 7
+constexpr int CPW = DB / 8;    // streamed tiles: wave w sums columns CPW w .. CPW w + CPW - 1
 enum { C_TICKET = 0, C_ERR = 1, C_NCTL = 4 };
+constexpr int LDL = DB + 1;    // padded LDS column of Linv_k (2-way bank conflicts at most)
+template <typename T>
+constexpr size_t bs_lds() {
+    return sizeof(T) * (size_t)DB * LDL;
+}
 
 __device__ __forceinline__ int ld_uni(const int* p) {
     return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -42,39 +49,44 @@ __device__ __forceinline__ void st_sc1(T* p, T v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// partial[c] += sum over the 128 rows of tile (column-major, ld) of tile[r][c] * v[r], for the
-// wave's 32 columns: lane l covers rows 2l, 2l+1 (one 16-byte load per column, coalesced).
+// A streamed tile's share of one lane: rows 2l, 2l+1 of the wave's CPW columns (one 16-byte
+// load per column, coalesced across the wave).  Loaded before the tile's alpha_j is waited
+// for, so the load latency hides under the wait.
 template <typename T>
-__device__ __forceinline__ void tile_gemv(const T* __restrict__ tile, int64_t ld, int w, int lane, T v0, T v1,
-                                          T (&p)[CPW]) {
+struct TileRows {
+    typedef T v2 __attribute__((ext_vector_type(2)));
+    v2 x[CPW];
+    __device__ __forceinline__ void load(const T* __restrict__ tile, int64_t ld, int w, int lane) {
 #pragma unroll
-    for (int cc = 0; cc < CPW; cc++) {
-        typedef T v2 __attribute__((ext_vector_type(2)));
-        const v2 c2 = *reinterpret_cast<const v2*>(tile + (int64_t)(w * CPW + cc) * ld + 2 * lane);
-        p[cc] = fma(c2[0], v0, fma(c2[1], v1, p[cc]));
+        for (int cc = 0; cc < CPW; cc++)
+            x[cc] = *reinterpret_cast<const v2*>(tile + (int64_t)(w * CPW + cc) * ld + 2 * lane);
     }
-}
+    // p[cc] += tile[2l][CPW w + cc] v0 + tile[2l + 1][CPW w + cc] v1
+    __device__ __forceinline__ void apply(T v0, T v1, T (&p)[CPW]) const {
+#pragma unroll
+        for (int cc = 0; cc < CPW; cc++) p[cc] = fma(x[cc][0], v0, fma(x[cc][1], v1, p[cc]));
+    }
+};
 
-// sum the 64 lane partials of each of the wave's 32 columns into out[32w + cc] (LDS), in two
-// passes of 16 columns (34 KB of LDS)
-constexpr int RH = CPW / 2;
+// Sum the 64 lane partials of each of the wave's CPW = 16 columns without LDS or barriers:
+// four halving exchanges (xor 32, 16, 8, 4) leave lane l with column
+// 8 b5 + 4 b4 + 2 b3 + b2 (b_i = bit i of l) summed over its 16 lanes' worth, two more
+// (xor 2, 1) finish the sum.  Returns that column's sum and sets col.
 template <typename T>
-__device__ __forceinline__ void reduce_cols(const T (&p)[CPW], int w, int lane, T (*red)[RH + 1], T* out) {
+__device__ __forceinline__ T wave_reduce_cols(T (&p)[CPW], int lane, int& col) {
+    T q8[8], q4[4], q2[2], q1;
+    const bool u5 = lane & 32, u4 = lane & 16, u3 = lane & 8, u2 = lane & 4;
 #pragma unroll
-    for (int half = 0; half < 2; half++) {
+    for (int i = 0; i < 8; i++) q8[i] = (u5 ? p[i + 8] : p[i]) + __shfl_xor(u5 ? p[i] : p[i + 8], 32);
 #pragma unroll
-        for (int cc = 0; cc < RH; cc++) red[w * 64 + lane][cc] = p[half * RH + cc];
-        __syncthreads();
-        // 4 lanes per column: each sums 16 of the 64 partials, then two shuffles
-        const int cc = lane & (RH - 1), qd = lane >> 4;
-        T s = 0;
+    for (int i = 0; i < 4; i++) q4[i] = (u4 ? q8[i + 4] : q8[i]) + __shfl_xor(u4 ? q8[i] : q8[i + 4], 16);
 #pragma unroll
-        for (int q = 0; q < 16; q++) s += red[w * 64 + qd * 16 + q][cc];
-        s += __shfl_xor(s, 16);
-        s += __shfl_xor(s, 32);
-        if (qd == 0) out[w * CPW + half * RH + cc] = s;
-        __syncthreads();
-    }
+    for (int i = 0; i < 2; i++) q2[i] = (u3 ? q4[i + 2] : q4[i]) + __shfl_xor(u3 ? q4[i] : q4[i + 2], 8);
+    q1 = (u2 ? q2[1] : q2[0]) + __shfl_xor(u2 ? q2[0] : q2[1], 4);
+    q1 += __shfl_xor(q1, 2);
+    q1 += __shfl_xor(q1, 1);
+    col = (u5 ? 8 : 0) + (u4 ? 4 : 0) + (u3 ? 2 : 0) + (u2 ? 1 : 0);
+    return q1;
 }
 
 template <typename T>
@@ -87,78 +99,157 @@ struct Args {
     int* ctl;         // [C_NCTL] then one flag per (block, rhs pass)
     int* info;        // set to -1 (atomicMin) when a wait timed out
     long long tlimit; // wall-clock ticks (100 MHz) per wait
+    long long* trace; // GPRX_BS_TRACE: per block {start, non-critical done, alpha_{k+1} seen, published}
 };
 
+// Wait until *f != 0; false on timeout or another workgroup's error (every wave polls on its
+// own: the caller agrees through LDS before the next barrier).
+__device__ __forceinline__ bool wait_flag(const int* f, int* ctl, long long t0, long long tlimit) {
+    while (ld_uni(f) == 0) {
+        if (ld_uni(ctl + C_ERR)) return false;
+        if (wall_clock64() - t0 > tlimit) {
+            __hip_atomic_store(ctl + C_ERR, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    return true;
+}
+
+// Load QR consecutive values starting at p (16-byte aligned) into registers.
+template <typename T>
+__device__ __forceinline__ void load_run(const T* __restrict__ p, T (&x)[QR]) {
+    typedef T v2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+    for (int i = 0; i < QR; i += 2) {
+        const v2 y = *reinterpret_cast<const v2*>(p + i);
+        x[i] = y[0];
+        x[i + 1] = y[1];
+    }
+}
+
+// Block k = nb - 1 - ticket.  While the later blocks are still being solved (off the
+// critical path) the workgroup loads Linv_k into LDS and the critical tile L_{k+1,k} into
+// registers in the column layout (thread: column c, rows QR q ..), and it streams the tiles
+// L_{j,k}, j >= k + 2 (coalesced, lanes over rows; each tile's loads issued before its
+// alpha_j is waited for), reducing them in-wave.  The critical path once alpha_{k+1} is
+// published: 32 FMAs per thread, a 4-way combine through LDS, 32 FMAs against Linv_k, a
+// combine, the alpha_k stores.
 template <typename T>
 __global__ __launch_bounds__(NT) void backsolve_chain_kernel(Args<T> a) {
-    __shared__ T red[NT][RH + 1];
-    __shared__ int s_fail;
-    __shared__ T svec[DB];
-    __shared__ int s_k;
+    __shared__ T s_alpha[DB];     // alpha_j being applied
+    __shared__ T s_part[4][DB];   // per-quarter partial sums
+    __shared__ T s_other[DB];     // sum over j >= k + 2 of L_jk^T alpha_j
+    __shared__ T s_v[DB];         // v = z_k - sum_{j > k} L_jk^T alpha_j
+    __shared__ int s_int[2];      // ticket, fail
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    T* s_linv = reinterpret_cast<T*>(smem_raw);  // column c of Linv_k at c * LDL (padded)
     const int t = threadIdx.x, w = __builtin_amdgcn_readfirstlane(t >> 6), lane = t & 63;
+    const int c = t & (DB - 1), q = t >> 7;
     const int nb = (int)(a.np / DB);
     int* flags = a.ctl + C_NCTL;
     if (w == 0) {
         const int v = __hip_atomic_fetch_add(a.ctl + C_TICKET, (t == 0) ? 1 : 0, __ATOMIC_RELAXED,
                                              __HIP_MEMORY_SCOPE_AGENT);
-        s_k = __builtin_amdgcn_readfirstlane(v);
+        s_int[0] = __builtin_amdgcn_readfirstlane(v);
     }
     __syncthreads();
-    const int tk = __builtin_amdgcn_readfirstlane(s_k);
+    const int tk = __builtin_amdgcn_readfirstlane(s_int[0]);
     if (tk >= nb) return;
     const int k = nb - 1 - tk;
     const int64_t r0 = (int64_t)k * DB;
-    const T* Lk = a.Linv + (int64_t)k * DB * DB;
+    const bool has1 = k + 1 < nb;
+    if (a.trace && t == 0) a.trace[4 * k] = wall_clock64();
+    // (Linv_k^T v)_c = sum_r Linv_k[r][c] v[r] from LDS; (L_jk^T x)_c likewise from registers
+    {
+        const T* Lk = a.Linv + (int64_t)k * DB * DB;
+        for (int e = t; e < DB * DB; e += NT) s_linv[(e / DB) * LDL + (e % DB)] = Lk[e];
+    }
+    T t1[QR];
+    if (has1) load_run<T>(a.A + (int64_t)(k + 1) * DB + (r0 + c) * a.ld + QR * q, t1);
+    // one alpha block into s_alpha, then every thread's partial of (L^T alpha)_c over its rows
+    auto apply = [&](const T(&x)[QR], const T* alpha_j, int r) {
+        if (t < DB) s_alpha[t] = ld_sc1(alpha_j + (int64_t)t * a.m + r);
+        __syncthreads();
+        T s = 0;
+#pragma unroll
+        for (int i = 0; i < QR; i++) s = fma(x[i], s_alpha[QR * q + i], s);
+        s_part[q][c] = s;
+        __syncthreads();
+    };
+    // agree on a failed wait (waves poll on their own) before using the barriers' results
+    auto agree = [&](bool ok) {
+        if (t == 0) s_int[1] = 0;
+        __syncthreads();
+        if (!ok && lane == 0) s_int[1] = 1;
+        __syncthreads();
+        return s_int[1] == 0;
+    };
     bool ok = true;
     for (int r = 0; r < a.m && ok; r++) {
         int* fl = flags + (int64_t)r * nb;
+        const long long t0 = wall_clock64();
         T p[CPW];
 #pragma unroll
         for (int cc = 0; cc < CPW; cc++) p[cc] = 0;
-        // s_k = sum_{j>k} L_jk^T alpha_j, tiles in the order their alpha_j appear
-        const long long t0 = wall_clock64();
-        for (int j = nb - 1; j > k && ok; j--) {
-            while (ld_uni(fl + j) == 0) {
-                if (ld_uni(a.ctl + C_ERR)) {
-                    ok = false;
-                    break;
-                }
-                if (wall_clock64() - t0 > a.tlimit) {
-                    __hip_atomic_store(a.ctl + C_ERR, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    ok = false;
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
-            }
+        for (int j = nb - 1; j > k + 1 && ok; j--) {
+            TileRows<T> tr;
+            tr.load(a.A + (int64_t)j * DB + r0 * a.ld, a.ld, w, lane);
+            ok = wait_flag(fl + j, a.ctl, t0, a.tlimit);
             if (!ok) break;
             const int64_t rj = (int64_t)j * DB + 2 * lane;
             const T v0 = ld_sc1(a.alpha + rj * a.m + r), v1 = ld_sc1(a.alpha + (rj + 1) * a.m + r);
-            tile_gemv<T>(a.A + (int64_t)j * DB + r0 * a.ld, a.ld, w, lane, v0, v1, p);
+            tr.apply(v0, v1, p);
         }
-        // the waves poll on their own: agree before the workgroup barriers
-        if (t == 0) s_fail = 0;
+        if (!agree(ok)) break;
+        {
+            int col;
+            const T sum = wave_reduce_cols<T>(p, lane, col);
+            if ((lane & 3) == 0) s_other[CPW * w + col] = sum;
+        }
+        const T zc = a.A[a.np + r + (r0 + c) * a.ld];  // label row r of block k (z^T)
+        if (a.trace && r == 0 && t == 0) a.trace[4 * k + 1] = wall_clock64();
+        // ---- critical path ----
+        T crit = 0;
+        if (has1) {
+            ok = wait_flag(fl + k + 1, a.ctl, t0, a.tlimit);
+            if (a.trace && r == 0 && t == 0) a.trace[4 * k + 2] = wall_clock64();
+            if (!agree(ok)) break;
+            apply(t1, a.alpha + (int64_t)(k + 1) * DB * a.m, r);
+            if (t < DB) crit = s_part[0][t] + s_part[1][t] + s_part[2][t] + s_part[3][t];
+        } else {
+            __syncthreads();  // s_other complete
+        }
+        if (t < DB) s_v[t] = zc - s_other[t] - crit;
         __syncthreads();
-        if (!ok && lane == 0) s_fail = 1;
-        __syncthreads();
-        if (s_fail) break;
-        reduce_cols<T>(p, w, lane, red, svec);
-        // v = z_k - s_k;  alpha_k = Linv_k^T v
-        if (t < DB) svec[t] = a.A[a.np + r + (r0 + t) * a.ld] - svec[t];
-        __syncthreads();
+        {
+            T s = 0;
 #pragma unroll
-        for (int cc = 0; cc < CPW; cc++) p[cc] = 0;
-        tile_gemv<T>(Lk, DB, w, lane, svec[2 * lane], svec[2 * lane + 1], p);
+            for (int i = 0; i < QR; i++) s = fma(s_linv[c * LDL + QR * q + i], s_v[QR * q + i], s);
+            s_part[q][c] = s;
+        }
         __syncthreads();
-        reduce_cols<T>(p, w, lane, red, svec);
-        if (t < DB) st_sc1(a.alpha + (r0 + t) * a.m + r, svec[t]);
+        if (t < DB) st_sc1(a.alpha + (r0 + t) * a.m + r, s_part[0][t] + s_part[1][t] + s_part[2][t] + s_part[3][t]);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (w == 0) __hip_atomic_store(fl + k, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (a.trace && r == 0 && t == 0) a.trace[4 * k + 3] = wall_clock64();
     }
     if (t == 0 && ld_uni(a.ctl + C_ERR)) atomicMin(a.info, -1);
 }
 
 }  // namespace bs
+
+// GPRX_BS_TRACE timeline of the last launch (per block, 100 MHz wall clock)
+static long long* g_bs_trace = nullptr;
+static int g_bs_trace_n = 0;
+int64_t bs_trace_copy(long long* out, int64_t max_blocks) {
+    if (!g_bs_trace) return 0;
+    const int64_t n = std::min<int64_t>(max_blocks, g_bs_trace_n);
+    GPRX_HIP(hipDeviceSynchronize());
+    GPRX_HIP(hipMemcpy(out, g_bs_trace, sizeof(long long) * 4 * n, hipMemcpyDeviceToHost));
+    return n;
+}
 
 template <typename T>
 void launch_backsolve_chain(const T* A, int64_t ld, int64_t np, int m, const T* Linv, T* alpha, int* info,
@@ -180,7 +271,25 @@ void launch_backsolve_chain(const T* A, int64_t ld, int64_t np, int m, const T* 
     a.ctl = scratch;
     a.info = info;
     a.tlimit = (long long)(1e8 * 4.0);
-    hipLaunchKernelGGL(backsolve_chain_kernel<T>, dim3((unsigned)nb), dim3(NT), 0, s, a);
+    a.trace = nullptr;
+    static const bool tracing = std::getenv("GPRX_BS_TRACE") != nullptr;
+    if (tracing) {
+        if (g_bs_trace_n < nb) {
+            if (g_bs_trace) GPRX_HIP(hipFree(g_bs_trace));
+            GPRX_HIP(hipMalloc(&g_bs_trace, sizeof(long long) * 4 * nb));
+        }
+        g_bs_trace_n = nb;
+        a.trace = g_bs_trace;
+    }
+    static bool attr = false;
+    if (!attr) {
+        GPRX_HIP(hipFuncSetAttribute((const void*)backsolve_chain_kernel<double>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)bs_lds<double>()));
+        GPRX_HIP(hipFuncSetAttribute((const void*)backsolve_chain_kernel<float>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)bs_lds<float>()));
+        attr = true;
+    }
+    hipLaunchKernelGGL(backsolve_chain_kernel<T>, dim3((unsigned)nb), dim3(NT), bs_lds<T>(), s, a);
     GPRX_HIP(hipGetLastError());
 }
 

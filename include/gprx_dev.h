@@ -33,6 +33,9 @@ int32_t gprx_dev_pt_debug(int32_t* out, int32_t max_wg);
  * {type | nb << 8, i, j, b0}; times: 4 int64 per ticket {taken, inputs ready, published,
  * workgroup} in 100 MHz wall-clock ticks.  Synchronises the device; returns tickets copied. */
 int64_t gprx_dev_pt_trace(int32_t* tasks, int64_t* times, int64_t max);
+/* GPRX_BS_TRACE=1: per block of the last back substitution {start, non-critical tiles done,
+ * alpha_{k+1} seen, alpha_k published} (100 MHz wall clock); returns blocks. */
+int64_t gprx_dev_bs_trace(int64_t* times, int64_t max_blocks);
 #ifdef __cplusplus
 }
 #endif
