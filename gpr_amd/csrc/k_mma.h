@@ -126,24 +126,32 @@ __device__ __forceinline__ void tile_mma(typename Mfma<T>::acc_t (&acc)[2][4], c
 #pragma unroll
     for (int p = 0; p < AHEAD; p++)
         if (p < nst) issue(p);
-#pragma nounroll
-    for (int st = 0; st < nst; st++) {
-        // this wave's loads of stage st have landed (later stages may stay in flight) ...
+    // this wave's loads of stage st have landed (later stages may stay in flight), and every
+    // wave's, and every wave is done reading the buffer refilled next; then the refill
+    auto stage_sync = [&](int st) {
         const int ahead = nst - 1 - st;
         if (AHEAD >= 3 && ahead >= 2) wait_vm<(AHEAD >= 3 ? 2 : 0) * S::IPW>();
         else if (AHEAD >= 2 && ahead >= 1) wait_vm<S::IPW>();
         else wait_vm<0>();
-        // ... and every wave's, and every wave is done reading the buffer refilled next.
         // (Reading the next stage's first fragments before this barrier, so the MFMAs start
         // right after it, measured +0.5% alone but cost 3% inside the factorisation: it
         // shortens the load lead to two stages.)
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         if (st + AHEAD < nst) issue(st + AHEAD);
-        if (active) {
+    };
+    // Idle waves (above the diagonal of a diagonal tile) run a loop of their own with the same
+    // barriers: with the wave-uniform test inside one loop, the accumulators merged from two
+    // paths every stage (64 register moves, and a wait for the last MFMAs, per stage).
+    if (__builtin_amdgcn_readfirstlane(active ? 1 : 0)) {
+        const T* a0 = smem;
+        const T* b0 = smem + S::GRP * S::SRP;
+#pragma nounroll
+        for (int st = 0; st < nst; st++) {
+            stage_sync(st);
             // fragments of step kq+1 are read while the MFMAs of step kq run
-            const T* a = smem + (st % NBUF) * S::STG;
-            const T* b = a + S::GRP * S::SRP;
+            const T* a = a0 + (st % NBUF) * S::STG;
+            const T* b = b0 + (st % NBUF) * S::STG;
             T fa[2][4], fb[2][2];
             auto frag = [&](int kq, int r) {
                 const int kr = kq * 4 + lk;
@@ -164,6 +172,9 @@ __device__ __forceinline__ void tile_mma(typename Mfma<T>::acc_t (&acc)[2][4], c
                     for (int y = 0; y < 4; y++) acc[x][y] = Tr::mma(fb[kq & 1][x], fa[kq & 1][y], acc[x][y]);
             }
         }
+    } else {
+#pragma nounroll
+        for (int st = 0; st < nst; st++) stage_sync(st);
     }
 }
 
