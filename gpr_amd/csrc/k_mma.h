@@ -89,11 +89,13 @@ __device__ __forceinline__ void wait_vm() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-// acc = A B^T over K (multiple of BKS) for the waves that are `active`; every wave takes part
-// in the staging and the barriers.  A, B: 128 rows x K, column-major (lda, ldb), 16-B aligned.
+// acc = A B^T over K (multiple of BKS); this wave multiplies only the first kact k-columns
+// (a multiple of BKS: 0 = idle, K = all; the rest of B is zero for it), but every wave takes
+// part in the staging and the barriers of all K.  A, B: 128 rows x K, column-major (lda,
+// ldb), 16-B aligned.
 template <typename T>
 __device__ __forceinline__ void tile_mma(typename Mfma<T>::acc_t (&acc)[2][4], const T* __restrict__ A, int64_t lda,
-                                         const T* __restrict__ B, int64_t ldb, int K, bool active, T* smem,
+                                         const T* __restrict__ B, int64_t ldb, int K, int kact, T* smem,
                                          const int t) {
     typedef Mfma<T> Tr;
     typedef typename Tr::acc_t acc_t;
@@ -140,14 +142,17 @@ __device__ __forceinline__ void tile_mma(typename Mfma<T>::acc_t (&acc)[2][4], c
         __builtin_amdgcn_s_barrier();
         if (st + AHEAD < nst) issue(st + AHEAD);
     };
-    // Idle waves (above the diagonal of a diagonal tile) run a loop of their own with the same
-    // barriers: with the wave-uniform test inside one loop, the accumulators merged from two
-    // paths every stage (64 register moves, and a wait for the last MFMAs, per stage).
-    if (__builtin_amdgcn_readfirstlane(active ? 1 : 0)) {
+    // The MFMA stages and the idle ones (above the diagonal of a diagonal tile, beyond the
+    // triangle of a triangular B) are loops of their own with the same barriers: with a
+    // wave-uniform test inside one loop, the accumulators merged from two paths every stage
+    // (64 register moves, and a wait for the last MFMAs, per stage).
+    const int nmf = __builtin_amdgcn_readfirstlane(kact < K ? kact : K) / BKS;
+    int st0 = 0;
+    {
         const T* a0 = smem;
         const T* b0 = smem + S::GRP * S::SRP;
 #pragma nounroll
-        for (int st = 0; st < nst; st++) {
+        for (int st = 0; st < nmf; st++) {
             stage_sync(st);
             // fragments of step kq+1 are read while the MFMAs of step kq run
             const T* a = a0 + (st % NBUF) * S::STG;
@@ -172,10 +177,10 @@ __device__ __forceinline__ void tile_mma(typename Mfma<T>::acc_t (&acc)[2][4], c
                     for (int y = 0; y < 4; y++) acc[x][y] = Tr::mma(fb[kq & 1][x], fa[kq & 1][y], acc[x][y]);
             }
         }
-    } else {
-#pragma nounroll
-        for (int st = 0; st < nst; st++) stage_sync(st);
+        st0 = nmf;
     }
+#pragma nounroll
+    for (int st = st0; st < nst; st++) stage_sync(st);
 }
 
 }  // namespace mm

@@ -90,10 +90,10 @@ template <typename T, int NPER, bool R2>
 __device__ __forceinline__ void block_stats(const T* FU, int64_t nu, int64_t i0, const T* FV, int64_t nv, int64_t j0,
                                             int Kr, int Kp, T* smem, int t, typename Mfma<T>::acc_t (&ar)[2][4],
                                             typename Mfma<T>::acc_t (&ap)[2][4]) {
-    if (R2) tile_mma<T>(ar, FU + i0, nu, FV + j0, nv, Kr, true, smem, t);
+    if (R2) tile_mma<T>(ar, FU + i0, nu, FV + j0, nv, Kr, Kr, smem, t);
     if (NPER) {
         __syncthreads();  // the second product reuses the staging ring
-        tile_mma<T>(ap, FU + (int64_t)Kr * nu + i0, nu, FV + (int64_t)Kr * nv + j0, nv, Kp, true, smem, t);
+        tile_mma<T>(ap, FU + (int64_t)Kr * nu + i0, nu, FV + (int64_t)Kr * nv + j0, nv, Kp, Kp, smem, t);
     }
 }
 
@@ -219,7 +219,7 @@ __device__ __forceinline__ bool build_tile_sum(const KCanon<T>* __restrict__ Kd,
         fn(std::integral_constant<int, 7>{});
     };
     if (R2) {
-        tile_mma<T>(ar, FU + i0, nf, FV + j0, nf, Kr, true, smem, t);
+        tile_mma<T>(ar, FU + i0, nf, FV + j0, nf, Kr, Kr, smem, t);
         T nu[4];
 #pragma unroll
         for (int y = 0; y < 4; y++) nu[y] = FU[(int64_t)(Kr + Kp) * nf + i0 + wr * 64 + y * 16 + lr];
@@ -241,7 +241,7 @@ __device__ __forceinline__ bool build_tile_sum(const KCanon<T>* __restrict__ Kd,
     }
     if (NPER) {
         if (R2) __syncthreads();  // the second product reuses the staging ring
-        tile_mma<T>(ap, FU + (int64_t)Kr * nf + i0, nf, FV + (int64_t)Kr * nf + j0, nf, Kp, true, smem, t);
+        tile_mma<T>(ap, FU + (int64_t)Kr * nf + i0, nf, FV + (int64_t)Kr * nf + j0, nf, Kp, Kp, smem, t);
     }
     bool bad = false;
     each([&](auto cc) {

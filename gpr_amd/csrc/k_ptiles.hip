@@ -59,12 +59,14 @@ using namespace mm;
 // ------------------------------------------------------------------------------------------
 // One 128x128 tile:  C = A B^T (UPDATE = false)  or  C -= A B^T (UPDATE = true), K deep.
 // A: 128 rows x K (column-major, lda), B: 128 rows x K (ldb).  lower: diagonal tile, only
-// row >= col is stored and the waves wholly above the diagonal skip their MFMAs.
+// row >= col is stored and the waves wholly above the diagonal skip their MFMAs.  tri: B is
+// lower triangular (K = 128, a diagonal-block inverse): output columns 32 wc .. 32 wc + 31
+// need only k < 32 wc + 32, the waves skip the MFMAs of the zero part.
 // ------------------------------------------------------------------------------------------
 template <typename T, bool UPDATE>
 __device__ __forceinline__ void tile_gemm(T* __restrict__ C, int64_t ldc, const T* __restrict__ A, int64_t lda,
                                           const T* __restrict__ B, int64_t ldb, int K, bool lower, T* smem,
-                                          const int t) {
+                                          const int t, bool tri = false) {
     typedef Mfma<T> Tr;
     typedef typename Tr::acc_t acc_t;
     const int lane = t & 63, w = t >> 6;
@@ -87,7 +89,7 @@ __device__ __forceinline__ void tile_gemm(T* __restrict__ C, int64_t ldc, const 
             }
     }
     acc_t acc[2][4];
-    tile_mma<T>(acc, A, lda, B, ldb, K, active, smem, t);
+    tile_mma<T>(acc, A, lda, B, ldb, K, !active ? 0 : (tri ? 32 * (wc + 1) : K), smem, t);
     if (!active) return;
 #pragma unroll
     for (int x = 0; x < 2; x++) {
@@ -513,7 +515,8 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
             publish(a.ver + (int64_t)i * a.nc + j, b0 + nb, false);
         } else if (type == T_TRSM) {
             T* Cik = Ci + (int64_t)j * GT * ld;
-            if (!(a.variant & 1)) tile_gemm<T, false>(Cik, ld, Cik, ld, a.Linv + (int64_t)j * DB * DB, DB, GT, false, smem, tid);
+            if (!(a.variant & 1))
+                tile_gemm<T, false>(Cik, ld, Cik, ld, a.Linv + (int64_t)j * DB * DB, DB, GT, false, smem, tid, true);
             publish(a.lcnt + i, j + 1, false);
         } else {  // DIAGX(k = i)
             const int k = i;
@@ -521,7 +524,8 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
             long long dt[4] = {0, 0, 0, 0};
             if (k > 0) {
                 T* Akm = Ci + (int64_t)(k - 1) * GT * ld;
-                tile_gemm<T, false>(Akm, ld, Akm, ld, a.Linv + (int64_t)(k - 1) * DB * DB, DB, GT, false, smem, tid);
+                tile_gemm<T, false>(Akm, ld, Akm, ld, a.Linv + (int64_t)(k - 1) * DB * DB, DB, GT, false, smem, tid,
+                                    true);
                 if (a.trace) dt[0] = wall_clock64();
                 publish(a.lcnt + k, k, false);  // L_{k,k-1} final: unblocks the updates of column k
                 if (a.trace) dt[1] = wall_clock64();
