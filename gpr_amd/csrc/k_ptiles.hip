@@ -759,7 +759,7 @@ static Schedule make_schedule(int nc, int nr, int W, int near, int P, const Cost
 }
 
 struct Params {
-    int W = 16, near = 1;
+    int W = 32, near = 1;
     Cost cm;
     Params() {
         if (const char* e = std::getenv("GPRX_PT_W")) W = std::max(1, std::atoi(e));

@@ -20,7 +20,7 @@ def _sched(nc, nr, P=256, build=False):
     return st, n.value, est.value
 
 
-def _expected_tasks(nc, nr, W=16, near=1):
+def _expected_tasks(nc, nr, W=32, near=1):
     """Task count of the chunking rule (k_ptiles.hip tile_chunks): W-aligned chunks up to the
     last multiple of W at or before column j, then power-of-two pieces before the last `near`
     panels, then single panels."""
