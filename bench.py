@@ -90,6 +90,8 @@ def main():
     ap.add_argument("--n", type=int, default=None)
     ap.add_argument("--d", type=int, default=None)
     ap.add_argument("--predict-q", type=int, default=65536)
+    ap.add_argument("--lml", type=int, default=1, help="also time one log-marginal likelihood + gradient "
+                                                        "(BASELINE.json configs[2]); 0 = skip")
     ap.add_argument("--cpu-n", type=int, default=16384, help="N of the CPU-baseline sample (0 = skip)")
     ap.add_argument("--mode", choices=["replicas", "dist"], default="replicas",
                     help="N>1: independent fits per GPU (replicas, weak scaling) or one fit whose "
@@ -171,8 +173,22 @@ def main():
         pred = {"q": args.predict_q, "pts_per_s_device": args.predict_q / (ps["ms"] * 1e-3) if ps else None,
                 "pts_per_s_wall_incl_pcie": args.predict_q / tq}
 
-    # dominant kernel: the persistent tile-dataflow factorisation, one launch per fit.
-    # Algorithmic work per launch = n^3/3 (Cholesky) + m n^2 (forward solve of the label rows).
+    # log-marginal likelihood + gradient (refit, explicit inverse, fused gradient pass)
+    lml = None
+    if args.lml and not distributed_fit:
+        model.lml(grad=True)
+        ctx.set_stats(True)
+        tl0 = time.perf_counter()
+        model.lml(grad=True)
+        tl = time.perf_counter() - tl0
+        ls = ctx.stats()
+        ctx.set_stats(False)
+        lml = {"ms_wall": 1e3 * tl, "phases_ms": {k: v["ms"] for k, v in ls.items()}}
+
+    # dominant kernel: the persistent tile-dataflow factorisation, one launch per fit (with
+    # the covariance build fused in as BUILD tasks for sum-of-exp-leaf kernel trees).
+    # Algorithmic work per launch = n^3/3 (Cholesky) + m n^2 (forward solve of the label
+    # rows); the build's work is not counted, so `achieved` understates the launch.
     fac = stats.get("potrf_tiles", {"ms": 0, "flops": 0, "launches": 0})
     alg_flops = n ** 3 / 3.0 + m * float(n) ** 2
     avg_ms = (fac["ms"] / fac["launches"]) if fac["launches"] else 0.0
@@ -210,7 +226,7 @@ def main():
                        "parallelism": (f"panel-cyclic factorisation over {world} GPUs (RCCL)" if distributed_fit
                                        else ("replicas" if world > 1 else "single-gpu"))},
             "roofline": {"bound": "mfma", "kernel": "potrf_tiles_kernel<double> (persistent tile-dataflow "
-                                                      "Cholesky + forward solve, k_ptiles.hip)",
+                                                      "covariance build + Cholesky + forward solve, k_ptiles.hip)",
                          "achieved": achieved, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved / PEAK_FP64_TFLOPS,
                          "avg_launch_us": 1e3 * avg_ms if avg_ms else None,
@@ -219,6 +235,7 @@ def main():
             "fit_roofline": {"t_roof_ms": t_roof, "t_fit_device_ms": fit_ms, "frac": t_roof / fit_ms},
             "phases": phases,
             "predict": pred,
+            "lml_grad": lml,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
