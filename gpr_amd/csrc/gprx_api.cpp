@@ -586,8 +586,29 @@ static gprx_status model_lml(gprx_model* M, uint32_t flags, double* value, doubl
         model_inverse<T>(M);
         M->grad.ensure(sizeof(double) * MAX_LEAF * 3);
         GPRX_HIP(hipMemsetAsync(M->grad.p, 0, sizeof(double) * MAX_LEAF * 3, s));
-        launch_lml_grad<T>(K, M->X.as<T>(), M->tab.as<T>(), M->n, M->d, M->alpha.as<T>(), M->C.as<T>(), M->np,
-                           M->grad.as<double>(), s);
+        static const bool direct_grad =
+            std::getenv("GPRX_LML_GRAD") && std::string(std::getenv("GPRX_LML_GRAD")) == "direct";
+        const int64_t np = M->np, npf = round_up(M->n, GT);
+        if (!direct_grad && npf == np && pairs_grad_supported<T>(K)) {
+            // pair statistics (and the periodic b-derivative statistic) on the MFMA units
+            const int64_t kf = pairs_feature_cols<T>(K, M->d), kg = pairs_grad_feature_cols<T>(K, M->d);
+            M->featU.ensure(sizeof(T) * np * kf);
+            M->featV.ensure(sizeof(T) * np * kf);
+            launch_pair_features<T>(K, M->X.as<T>(), M->n, M->d, M->X.as<T>(), false, M->featU.as<T>(), np, s);
+            launch_pair_features<T>(K, M->X.as<T>(), M->n, M->d, M->X.as<T>(), true, M->featV.as<T>(), np, s);
+            M->kdev.ensure(sizeof(KCanon<T>));
+            GPRX_HIP(hipMemcpyAsync(M->kdev.p, &K, sizeof(KCanon<T>), hipMemcpyHostToDevice, s));
+            M->scratch1.ensure(sizeof(T) * np * std::max<int64_t>(kg, 1));
+            M->scratch2.ensure(sizeof(T) * np * std::max<int64_t>(kg, 1));
+            const int64_t nt = np / GT;
+            M->pack.ensure(sizeof(double) * MAX_LEAF * 3 * nt * (nt + 1) / 2);
+            launch_lml_grad_mma<T>(K, M->kdev.as<KCanon<T>>(), M->X.as<T>(), M->n, M->d, M->featU.as<T>(),
+                                   M->featV.as<T>(), M->scratch1.as<T>(), M->scratch2.as<T>(), np, M->alpha.as<T>(),
+                                   M->C.as<T>(), M->np, M->pack.as<double>(), M->grad.as<double>(), s);
+        } else {
+            launch_lml_grad<T>(K, M->X.as<T>(), M->tab.as<T>(), M->n, M->d, M->alpha.as<T>(), M->C.as<T>(), M->np,
+                               M->grad.as<double>(), s);
+        }
         double acc[MAX_LEAF * 3];
         download(acc, M->grad.p, sizeof(acc), s);
         for (int l = 0; l < K.nleaf; l++) {

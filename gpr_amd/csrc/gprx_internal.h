@@ -350,6 +350,17 @@ struct TileBuild {
     int* flag;
     int mode;
 };
+// LML gradient on the MFMA units (k_pairs.hip): trees it covers, the extra feature columns
+// it needs per sample set, and the launch (partials of ntiles * 3 MAX_LEAF doubles, reduced
+// in a fixed order into acc[3 l + q]).
+template <typename T>
+bool pairs_grad_supported(const KCanon<T>& K);
+template <typename T>
+int64_t pairs_grad_feature_cols(const KCanon<T>& K, int d);
+template <typename T>
+void launch_lml_grad_mma(const KCanon<T>& K, const KCanon<T>* Kd, const T* X, int64_t n, int d, const T* FU,
+                         const T* FV, T* GU, T* GV, int64_t nf, const T* alpha, const T* C, int64_t ldc, double* part,
+                         double* acc, hipStream_t s);
 // The BUILD description of K(X, X) + sigma2 I from the features of launch_pair_features
 // (k_pairs.hip; the same trees as launch_kbuild_mma).
 template <typename T>

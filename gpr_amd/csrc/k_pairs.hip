@@ -170,6 +170,235 @@ __global__ __launch_bounds__(NT) void predict_mma_kernel(const KCanon<T>* __rest
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// LML gradient from pair statistics (replaces lml_grad_kernel, k_lml.hip, for sum-of-leaves
+// trees): sum_{i >= j} w_ij dk_l(x_i, x_j)/dp, w_ij = (alpha_i alpha_j - C_ij) (x2 off the
+// diagonal), the reference's tr((alpha alpha^T - C) D_p) (include/Likelihood.h:204-229).
+// The periodic derivative in b needs F = sum_k (x_k - y_k) sin(2b (x_k - y_k)), again an
+// inner product of per-sample features (K = 4d):
+//   F = [x~ s, -x~ c, -s, c] . [c', s', y~ c', y~ s']    (s = sin 2b x~, c = cos 2b x~)
+// ---------------------------------------------------------------------------------------
+template <typename T>
+__global__ void grad_features_kernel(const T* __restrict__ X, int64_t n, int d, const T* __restrict__ center, T b,
+                                     int right, T* __restrict__ G, int64_t np, int Kf) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= np) return;
+    const bool live = i < n;
+    const T b2 = T(2) * b;
+    for (int k = 0; k < d; k++) {
+        T sn = 0, cs = 0, xt = 0;
+        if (live) {
+            xt = X[i * d + k] - center[k];
+            gsincos(b2 * xt, &sn, &cs);
+        }
+        G[i + (int64_t)k * np] = right ? cs : xt * sn;
+        G[i + (int64_t)(d + k) * np] = right ? sn : -xt * cs;
+        G[i + (int64_t)(2 * d + k) * np] = right ? xt * cs : -sn;
+        G[i + (int64_t)(3 * d + k) * np] = right ? xt * sn : cs;
+    }
+    for (int k = 4 * d; k < Kf; k++) G[i + (int64_t)k * np] = 0;
+}
+
+// One workgroup per lower 128 x 128 tile; part[tile][3 l + q] = the tile's sums (reduced
+// afterwards in a fixed order: deterministic).  The statistics go one at a time through one
+// accumulator set: r2 (its leaves' derivatives summed at once), then S, where the periodic
+// leaf's w e and w e S are summed and w e is kept in place of S, then F (sum of w e F).
+// At most one periodic leaf (pairs_grad_supported).
+template <typename T, int NPER, bool R2>
+__global__ __launch_bounds__(NT) void grad_mma_kernel(const KCanon<T>* __restrict__ Kd, const T* __restrict__ FU,
+                                                      const T* __restrict__ FV, const T* __restrict__ GU,
+                                                      const T* __restrict__ GV, int64_t nf, int Kr, int Kp, int Kf,
+                                                      T hd, const T* __restrict__ alpha, const T* __restrict__ C,
+                                                      int64_t ldc, int64_t n, double* __restrict__ part) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    T* smem = reinterpret_cast<T*>(smem_raw);
+    double* sacc = reinterpret_cast<double*>(smem_raw + gemm_lds<T>());  // [8 waves][MAX_LEAF * 3]
+    typedef Mfma<T> Tr;
+    int64_t ti, tj;
+    {
+        const int64_t b = blockIdx.x;
+        int64_t i = (int64_t)((sqrt(8.0 * (double)b + 1.0) - 1.0) * 0.5);
+        while ((i + 1) * (i + 2) / 2 <= b) i++;
+        while (i * (i + 1) / 2 > b) i--;
+        ti = i;
+        tj = b - i * (i + 1) / 2;
+    }
+    const int64_t i0 = ti * GT, j0 = tj * GT;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int wr = w & 1, wc = w >> 1, lr = lane & 15, lk = lane >> 4;
+    const int nl = Kd->nleaf;
+    // compile-time (x, reg) chunks of 4 pairs (rows y): static indices keep the accumulators
+    // in registers around the run-time leaf loops
+    auto each = [&](auto fn) {
+        fn(std::integral_constant<int, 0>{});
+        fn(std::integral_constant<int, 1>{});
+        fn(std::integral_constant<int, 2>{});
+        fn(std::integral_constant<int, 3>{});
+        fn(std::integral_constant<int, 4>{});
+        fn(std::integral_constant<int, 5>{});
+        fn(std::integral_constant<int, 6>{});
+        fn(std::integral_constant<int, 7>{});
+    };
+    auto gj_of = [&](int x, int reg) { return j0 + wc * 32 + x * 16 + Tr::orow(lk, reg); };
+    auto gi_of = [&](int y) { return i0 + wr * 64 + y * 16 + lr; };
+    // pair weights, zero outside the lower triangle and the matrix; loaded after each tile
+    // product (held across one, they pushed the kernel into spills)
+    T wt[2][4][4];
+    auto load_weights = [&]() {
+        each([&](auto cc) {
+            constexpr int x = decltype(cc)::value >> 2, reg = decltype(cc)::value & 3;
+            const int64_t gj = gj_of(x, reg);
+#pragma unroll
+            for (int y = 0; y < 4; y++) {
+                const int64_t gi = gi_of(y);
+                const bool in = gi < n && gj < n && gi >= gj;
+                const int64_t ci = in ? gi : 0, cj = in ? gj : 0;
+                const T v = alpha[ci] * alpha[cj] - C[ci + cj * ldc];
+                wt[x][y][reg] = in ? v * (gi == gj ? T(1) : T(2)) : T(0);
+            }
+        });
+    };
+    // the wave's sums into its LDS row
+    auto flush = [&](int l, double a0, double a1, double a2) {
+        double v[3] = {a0, a1, a2};
+#pragma unroll
+        for (int q = 0; q < 3; q++) {
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) v[q] += __shfl_xor(v[q], off);
+            if (lane == 0) sacc[w * MAX_LEAF * 3 + l * 3 + q] += v[q];
+        }
+    };
+    if (t < 8 * MAX_LEAF * 3) sacc[t] = 0;
+    __syncthreads();
+    typename Tr::acc_t ar[2][4];
+    if (R2) {
+        tile_mma<T>(ar, FU + i0, nf, FV + j0, nf, Kr, Kr, smem, t);
+        load_weights();
+        T nu[4];
+#pragma unroll
+        for (int y = 0; y < 4; y++) nu[y] = FU[(int64_t)(Kr + Kp) * nf + i0 + wr * 64 + y * 16 + lr];
+        each([&](auto cc) {
+            constexpr int x = decltype(cc)::value >> 2, reg = decltype(cc)::value & 3;
+            const int64_t gj = gj_of(x, reg);
+            const T nv = FV[(int64_t)(Kr + Kp) * nf + gj];
+#pragma unroll
+            for (int y = 0; y < 4; y++)
+                ar[x][y][reg] = gi_of(y) == gj ? T(0) : fmax(nu[y] + nv + ar[x][y][reg], T(0));
+        });
+        // one element loop per leaf type, with the leaf's constants hoisted (the formulas of
+        // leaf_grad, gprx_internal.h, rearranged: one exp per pair, no per-pair division
+        // outside RQ)
+#pragma unroll 1
+        for (int l = 0; l < nl; l++) {
+            const KLeaf<T>& L = Kd->leaf[l];
+            const int ty = L.type;
+            if (ty == L_PERIODIC) continue;
+            double a0 = 0, a1 = 0, a2 = 0;
+            if (ty == L_GAUSS) {  // p = (sigma, scale): g = (sc^2 r2 / sig^3 e, 2 sc e), e = exp(c1 r2)
+                const T sig = L.p[0], sc = L.p[1], c1 = L.c1;
+                const T k0 = sc * sc / (sig * sig * sig), k1 = T(2) * sc;
+                each([&](auto cc) {
+                    constexpr int x = decltype(cc)::value >> 2, reg = decltype(cc)::value & 3;
+#pragma unroll
+                    for (int y = 0; y < 4; y++) {
+                        const T r2 = ar[x][y][reg], we = wt[x][y][reg] * exp(c1 * r2);
+                        a0 += (double)(we * (k0 * r2));
+                        a1 += (double)(we * k1);
+                    }
+                });
+            } else if (ty == L_GAUSS_EXP) {  // p = (sigma, scale) in log space
+                const T sig = L.p[0], sc = L.p[1];
+                const T ke = T(-0.5) * exp(T(-2) * sig), m0 = exp(T(2) * sc - T(2) * sig), m1 = T(2) * exp(T(2) * sc);
+                each([&](auto cc) {
+                    constexpr int x = decltype(cc)::value >> 2, reg = decltype(cc)::value & 3;
+#pragma unroll
+                    for (int y = 0; y < 4; y++) {
+                        const T r2 = ar[x][y][reg], we = wt[x][y][reg] * exp(ke * r2);
+                        a0 += (double)(we * (m0 * r2));
+                        a1 += (double)(we * m1);
+                    }
+                });
+            } else {  // L_RQ, p = (scale, sigma, alpha)
+                const T sc = L.p[0], sig = L.p[1], al = L.p[2];
+                const T kq = T(0.5) / (sig * sig * al), k0 = T(2) * sc, k1 = sc * sc / (sig * sig * sig), k2 = sc * sc;
+                each([&](auto cc) {
+                    constexpr int x = decltype(cc)::value >> 2, reg = decltype(cc)::value & 3;
+#pragma unroll
+                    for (int y = 0; y < 4; y++) {
+                        const T r2 = ar[x][y][reg], fq = fma(kq, r2, T(1)), lf = log(fq), inv = T(1) / fq;
+                        const T wp = wt[x][y][reg] * exp(-al * lf);
+                        a0 += (double)(wp * k0);
+                        a1 += (double)(wp * (k1 * r2 * inv));
+                        a2 += (double)(wp * (k2 * (kq * r2 * inv - lf)));
+                    }
+                });
+            }
+            flush(l, a0, a1, a2);
+        }
+    }
+    if (NPER) {
+        int lp = 0;
+        for (int l = 0; l < nl; l++)
+            if (Kd->leaf[l].type == L_PERIODIC) lp = l;
+        const KLeaf<T>& L = Kd->leaf[lp];
+        const T sc = L.p[0], sig = L.p[2], c1 = L.c1;
+        if (R2) __syncthreads();  // the staging ring is reused
+        tile_mma<T>(ar, FU + (int64_t)Kr * nf + i0, nf, FV + (int64_t)Kr * nf + j0, nf, Kp, Kp, smem, t);
+        load_weights();
+        double a0 = 0, a2 = 0;
+        each([&](auto cc) {
+            constexpr int x = decltype(cc)::value >> 2, reg = decltype(cc)::value & 3;
+            const int64_t gj = gj_of(x, reg);
+#pragma unroll
+            for (int y = 0; y < 4; y++) {
+                const T sp = gi_of(y) == gj ? T(0) : fmax(fma(T(-0.5), ar[x][y][reg], hd), T(0));
+                T we = wt[x][y][reg] * exp(c1 * sp);
+                // pinned here: sunk past the next product (to its use), S and the weights
+                // stayed live across it and spilled
+                asm volatile("" : "+v"(we));
+                a0 += (double)we;
+                a2 += (double)(we * sp);
+                ar[x][y][reg] = we;
+            }
+        });
+        __syncthreads();
+        typename Tr::acc_t af[2][4];
+        tile_mma<T>(af, GU + i0, nf, GV + j0, nf, Kf, Kf, smem, t);
+        double a1 = 0;
+        each([&](auto cc) {
+            constexpr int x = decltype(cc)::value >> 2, reg = decltype(cc)::value & 3;
+            const int64_t gj = gj_of(x, reg);
+#pragma unroll
+            for (int y = 0; y < 4; y++) a1 += (double)(ar[x][y][reg] * (gi_of(y) == gj ? T(0) : af[x][y][reg]));
+        });
+        // d/d(scale) = 2 sc e, d/db = -0.5 sc^2 e F / sigma^2, d/dsigma = sc^2 e S / sigma^3
+        flush(lp, (double)(T(2) * sc) * a0, (double)(T(-0.5) * sc * sc / (sig * sig)) * a1,
+              (double)(sc * sc / (sig * sig * sig)) * a2);
+    }
+    __syncthreads();
+    if (t < MAX_LEAF * 3) {
+        double v = 0;
+#pragma unroll
+        for (int ww = 0; ww < 8; ww++) v += sacc[ww * MAX_LEAF * 3 + t];
+        part[(int64_t)blockIdx.x * MAX_LEAF * 3 + t] = v;
+    }
+}
+
+// gout[p] = sum over tiles of part[tile][p], in tile order
+__global__ void grad_reduce_kernel(const double* __restrict__ part, int64_t ntiles, double* __restrict__ gout) {
+    __shared__ double red[256];
+    const int p = blockIdx.x, t = threadIdx.x;
+    double v = 0;
+    for (int64_t b = t; b < ntiles; b += 256) v += part[b * MAX_LEAF * 3 + p];
+    red[t] = v;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (t < o) red[t] += red[t + o];
+        __syncthreads();
+    }
+    if (t == 0) gout[p] = red[0];
+}
+
 }  // namespace pr
 
 template <typename T>
@@ -237,6 +466,53 @@ void launch_predict_mma(const KCanon<T>& K, const KCanon<T>* Kd, const T* FU, in
     GPRX_HIP(hipGetLastError());
 }
 
+// LML gradient trees: sum of Gaussian / GaussianExp / RQ / (one frequency) Periodic leaves
+template <typename T>
+bool pairs_grad_supported(const KCanon<T>& K) {
+    if (!pairs_mma_supported<T>(K, 1) || !K.sum_leaves) return false;
+    int nperleaf = 0;
+    for (int l = 0; l < K.nleaf; l++) {
+        const int ty = K.leaf[l].type;
+        if (ty != L_GAUSS && ty != L_GAUSS_EXP && ty != L_RQ && ty != L_PERIODIC) return false;
+        nperleaf += ty == L_PERIODIC;
+    }
+    return nperleaf <= 1;
+}
+
+template <typename T>
+int64_t pairs_grad_feature_cols(const KCanon<T>& K, int d) {
+    return K.nper ? pr::rup(4 * d, pr::KG) : 0;
+}
+
+// acc[3 l + q] = sum_{i >= j} w_ij d leaf_l / d p_q, from the features of launch_pair_features
+// (FU, FV: nf rows) and grad features GU, GV (computed here); part: ntiles * 3 MAX_LEAF doubles
+template <typename T>
+void launch_lml_grad_mma(const KCanon<T>& K, const KCanon<T>* Kd, const T* X, int64_t n, int d, const T* FU,
+                         const T* FV, T* GU, T* GV, int64_t nf, const T* alpha, const T* C, int64_t ldc, double* part,
+                         double* acc, hipStream_t s) {
+    const int Kr = pr::kr_of(K, d), Kp = pr::kp_of(K, d), Kf = (int)pairs_grad_feature_cols(K, d);
+    if (K.nper) {
+        const dim3 g((unsigned)((nf + 255) / 256));
+        hipLaunchKernelGGL(pr::grad_features_kernel<T>, g, dim3(256), 0, s, X, n, d, X, K.b[0], 0, GU, nf, Kf);
+        hipLaunchKernelGGL(pr::grad_features_kernel<T>, g, dim3(256), 0, s, X, n, d, X, K.b[0], 1, GV, nf, Kf);
+    }
+    const int64_t nt = nf / GT, ntiles = nt * (nt + 1) / 2;
+    const dim3 grid((unsigned)ntiles);
+    ProfScope ps(KC_LML_GRAD, s, 2.0 * (double)GT * GT * (Kr + Kp + Kf) * ntiles,
+                 (double)sizeof(T) * ((double)n * (n + 1) / 2 + (double)n * d));
+    const size_t lds = mm::gemm_lds<T>() + sizeof(double) * 8 * MAX_LEAF * 3;
+    auto go = [&](auto kfn) {
+        GPRX_HIP(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        hipLaunchKernelGGL(kfn, grid, dim3(mm::NT), lds, s, Kd, FU, FV, (const T*)GU, (const T*)GV, nf, Kr, Kp, Kf,
+                           T(0.5) * T(d), alpha, C, ldc, n, part);
+    };
+    if (K.nper && K.need_r2) go(pr::grad_mma_kernel<T, 1, true>);
+    else if (K.nper) go(pr::grad_mma_kernel<T, 1, false>);
+    else go(pr::grad_mma_kernel<T, 0, true>);
+    hipLaunchKernelGGL(pr::grad_reduce_kernel, dim3(MAX_LEAF * 3), dim3(256), 0, s, (const double*)part, ntiles, acc);
+    GPRX_HIP(hipGetLastError());
+}
+
 template <typename T>
 TileBuild<T> pairs_tile_build(const KCanon<T>& K, const KCanon<T>* Kd, const T* FU, const T* FV, int64_t nf, int d,
                               int64_t n, T sigma2, int* flag) {
@@ -263,6 +539,11 @@ TileBuild<T> pairs_tile_build(const KCanon<T>& K, const KCanon<T>* Kd, const T* 
 }
 
 #define GPRX_PAIRS_INST(T)                                                                                    \
+    template bool pairs_grad_supported<T>(const KCanon<T>&);                                                  \
+    template int64_t pairs_grad_feature_cols<T>(const KCanon<T>&, int);                                       \
+    template void launch_lml_grad_mma<T>(const KCanon<T>&, const KCanon<T>*, const T*, int64_t, int, const T*, \
+                                         const T*, T*, T*, int64_t, const T*, const T*, int64_t, double*,     \
+                                         double*, hipStream_t);                                               \
     template TileBuild<T> pairs_tile_build<T>(const KCanon<T>&, const KCanon<T>*, const T*, const T*, int64_t, int, \
                                               int64_t, T, int*);                                              \
     template bool pairs_mma_supported<T>(const KCanon<T>&, int);                                              \

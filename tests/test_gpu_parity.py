@@ -146,6 +146,22 @@ def test_lml(ctx, ks):
     assert abs(vc - vr) <= 1e-6 * max(1.0, abs(vr))
 
 
+@pytest.mark.parametrize("ks", ["SumKernel(GaussianKernel(2,0.15,),PeriodicKernel(0.1,3.141592653589793,1,))",
+                                "SumKernel(RationalQuadraticKernel(1.1,0.6,1.5,),GaussianExpKernel(-0.3,0.1,))",
+                                "PeriodicKernel(0.9,2.5,0.8,)"])
+def test_lml_gradient_multi_tile(ctx, ks):
+    """The MFMA pair-statistics gradient (k_pairs.hip grad_mma_kernel: r2, S and the
+    periodic sum (x-y) sin 2b(x-y) as feature inner products) over many 128 x 128 tiles,
+    ragged n, against the oracle's tr((alpha alpha^T - C) dK/dp) (include/Likelihood.h:204-229)."""
+    n, d, sigma = 777, 5, 0.7
+    X, Y = make_data(n, d)
+    M, _ = _fit(ctx, ks, X, Y, sigma, np.float64)
+    v, g, _ = M.lml(grad=True)
+    vr, gr, _, _ = O.lml(ks, X, Y, sigma)
+    assert abs(v - vr) <= 1e-6 * max(1.0, abs(vr))
+    assert relerr(g, gr) <= 1e-6
+
+
 def test_nonfinite_kernel_matrix(ctx):
     import gpr_amd
     X = np.array([[0.0], [np.inf]])
