@@ -235,6 +235,8 @@ struct gprx_model {
     double sigma = 0;
     bool has_data = false, has_kernel = false, fitted = false;
     bool has_alpha = false;  // regression vectors valid (fit, or gprx_model_set_alpha after Load)
+    bool want_inv = false;   // the next fit also forms C = (K + s^2 I)^{-1} (identity rows in the tiles)
+    bool inv_ready = false;  // C holds the inverse of the current fit
     gprx_kernel_desc desc{};
     KCanon<double> kd{};
     KCanon<float> kf{};
@@ -293,8 +295,11 @@ static gprx_status model_fit(gprx_model* M, uint32_t flags, gprx_fit_info* out) 
     const bool dist = (ctx->comm && ctx->world > 1) || ((flags & GPRX_FIT_DISTRIBUTED) && ctx->comm);
     GPRX_REQUIRE(!(flags & GPRX_FIT_DISTRIBUTED) || ctx->comm, GPRX_ERR_STATE,
                  "gprx_model_fit: GPRX_FIT_DISTRIBUTED needs a context from gprx_ctx_create_dist");
-    const int64_t n = M->n, np = round_up(n, dist ? (int64_t)outer_block() : (int64_t)DB), mp = round_up(M->m, GT),
-                  ld = np + mp;
+    const int64_t n = M->n, np = round_up(n, dist ? (int64_t)outer_block() : (int64_t)DB), mp = round_up(M->m, GT);
+    // the explicit inverse rides along in the tile factorisation as np identity rows
+    const bool want_inv = M->want_inv && !dist && potrf_uses_tiles();
+    const int64_t ld = np + mp + (want_inv ? np : 0);
+    M->inv_ready = false;
     M->np = np;
     M->mp = mp;
     M->ld = ld;
@@ -379,8 +384,9 @@ static gprx_status model_fit(gprx_model* M, uint32_t flags, gprx_fit_info* out) 
             const ncclResult_t r = ncclAllReduce(M->flag.p, M->flag.p, 1, ncclInt32, ncclMax, ctx->comm, s);
             if (r != ncclSuccess) throw Error{GPRX_ERR_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(r)};
         }
-    } else if (tb.mode) {
-        potrf_tiles<T>(M->A.as<T>(), ld, np, ld, M->Linv.as<T>(), M->info.as<int>(), ctx->ex, &tb);
+    } else if (tb.mode || want_inv) {
+        potrf_tiles<T>(M->A.as<T>(), ld, np, ld, M->Linv.as<T>(), M->info.as<int>(), ctx->ex, tb.mode ? &tb : nullptr,
+                       want_inv ? (int)(np / GT) : 0);
     } else {
         potrf_auto<T>(M->A.as<T>(), ld, np, ld, M->Linv.as<T>(), M->info.as<int>(), ctx->ex);
     }
@@ -388,6 +394,11 @@ static gprx_status model_fit(gprx_model* M, uint32_t flags, gprx_fit_info* out) 
     launch_fit_reductions<T>(M->A.as<T>(), ld, n, np, M->m, M->red.as<double>(), s);
     launch_backsolve_chain<T>(M->A.as<T>(), ld, np, M->m, M->Linv.as<T>(), M->alpha.as<T>(), M->info.as<int>(), ctx->ex,
                               s);
+    if (want_inv) {  // C = U U^T (lower), U = L^{-T} from the identity rows
+        M->C.ensure(sizeof(T) * np * np);
+        const T* U = M->A.as<T>() + np + mp;
+        launch_gemm_nt_kskip<T>(M->C.as<T>(), np, U, ld, U, ld, np, np, np, s);
+    }
     GPRX_HIP(hipEventRecord(ctx->ev[3], s));
     GPRX_HIP(hipStreamSynchronize(s));
     GPRX_HIP(hipGetLastError());
@@ -398,6 +409,7 @@ static gprx_status model_fit(gprx_model* M, uint32_t flags, gprx_fit_info* out) 
     GPRX_HIP(hipMemcpy(hred, M->red.p, sizeof(hred), hipMemcpyDeviceToHost));
     M->fitted = false;
     M->has_alpha = false;
+    M->inv_ready = false;
     if (out) {
         std::memset(out, 0, sizeof(*out));
         float t01 = 0, t12 = 0, t23 = 0;
@@ -421,6 +433,7 @@ static gprx_status model_fit(gprx_model* M, uint32_t flags, gprx_fit_info* out) 
                                           std::to_string(hinfo) + " <= 0)"};
     M->fitted = true;
     M->has_alpha = true;
+    M->inv_ready = want_inv;
     return GPRX_OK;
 }
 
@@ -556,7 +569,15 @@ static gprx_status model_lml(gprx_model* M, uint32_t flags, double* value, doubl
                  "GaussianLogLikelihood: only one output dimension is supported (the reference's data-fit term is "
                  "m x m, include/Likelihood.h:175)");
     gprx_fit_info fi;
-    gprx_status st = model_fit<T>(M, GPRX_FIT_NO_LU_FALLBACK, &fi);
+    M->want_inv = grad && (flags & GPRX_LML_GRAD);
+    gprx_status st;
+    try {
+        st = model_fit<T>(M, GPRX_FIT_NO_LU_FALLBACK, &fi);
+    } catch (...) {
+        M->want_inv = false;
+        throw;
+    }
+    M->want_inv = false;
     if (st != GPRX_OK) return st;
     const KCanon<T>& K = kcanon<T>(M);
     const double n = (double)M->n;
@@ -583,7 +604,7 @@ static gprx_status model_lml(gprx_model* M, uint32_t flags, double* value, doubl
     if (nparams) *nparams = K.nparams;
     if (grad && (flags & GPRX_LML_GRAD)) {
         hipStream_t s = M->ctx->stream;
-        model_inverse<T>(M);
+        if (!M->inv_ready) model_inverse<T>(M);
         M->grad.ensure(sizeof(double) * MAX_LEAF * 3);
         GPRX_HIP(hipMemsetAsync(M->grad.p, 0, sizeof(double) * MAX_LEAF * 3, s));
         static const bool direct_grad =
@@ -1005,6 +1026,7 @@ gprx_status gprx_model_set_data(gprx_model* M, const void* X, const void* Y, int
     M->has_data = true;
     M->fitted = false;
     M->has_alpha = false;
+    M->inv_ready = false;
     return GPRX_OK;
     API_END(ctx)
 }
@@ -1020,6 +1042,7 @@ gprx_status gprx_model_set_kernel(gprx_model* M, const gprx_kernel_desc* k) {
     M->has_kernel = true;
     M->fitted = false;
     M->has_alpha = false;
+    M->inv_ready = false;
     return GPRX_OK;
     API_END(ctx)
 }
@@ -1032,6 +1055,7 @@ gprx_status gprx_model_set_noise(gprx_model* M, double sigma) {
     M->sigma = sigma;
     M->fitted = false;
     M->has_alpha = false;
+    M->inv_ready = false;
     return GPRX_OK;
     API_END(ctx)
 }

@@ -368,14 +368,21 @@ TileBuild<T> pairs_tile_build(const KCanon<T>& K, const KCanon<T>* Kd, const T* 
                               int64_t n, T sigma2, int* flag);
 // Same contract, one persistent launch: 128x128 tile tasks scheduled on the device by
 // dependency counters (k_ptiles.hip).  A timed-out dependency wait sets *info = -1.
+// ni > 0: the last ni row blocks of the nrows are the identity, set up here, and leave as
+// L^{-T} (upper triangular, ni = np / 128): the inverse factor riding along as extra rows,
+// each identity block updated only from its own column block on.
 template <typename T>
 void potrf_tiles(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info, Exec& ex,
-                 const TileBuild<T>* build = nullptr);
+                 const TileBuild<T>* build = nullptr, int ni = 0);
+// C (lower) = A B^T where both operands vanish left of their row (LAUUM shape), k_potrf.hip
+template <typename T>
+void launch_gemm_nt_kskip(T* C, int64_t ldc, const T* A, int64_t lda, const T* B, int64_t ldb, int64_t M, int64_t N,
+                          int64_t K, hipStream_t s);
 // Factorisation used by the fit paths: potrf_tiles unless GPRX_POTRF=streams.
 template <typename T>
 void potrf_auto(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info, Exec& ex);
 bool potrf_uses_tiles();
-int64_t potrf_tiles_schedule_stats(int nc, int nr, int P, bool build, double* est_us);
+int64_t potrf_tiles_schedule_stats(int nc, int nr, int P, bool build, double* est_us, int ni = 0);
 // Multi-GPU form: column panels of outer_block() columns dealt cyclically over `world`
 // ranks (np must be a multiple of outer_block()); the factored panels are RCCL-broadcast so
 // every rank ends with the full factor.  pack: device scratch of nrows * outer_block().

@@ -589,23 +589,29 @@ struct Schedule {
 // pieces (W/2, W/4, ..., 1), then single panels -- few tasks (each costs a fixed ~6 us of
 // ticket, waits, fences and C read-modify-write), while the last panels of a tile, the ones
 // the diagonal chain waits for, still go one at a time.
-static void tile_chunks(int i, int j, int W, int near, std::vector<std::pair<int, int>>& out) {
+// s > 0 (an identity row block of the inverse, whose panels before s are zero): the same
+// rule on the panels [s, e), shifted.
+static void tile_chunks(int i, int j, int W, int near, std::vector<std::pair<int, int>>& out, int s = 0) {
     out.clear();
-    const int e = (i == j) ? j - 1 : j;
+    const int e = ((i == j) ? j - 1 : j) - s;
     if (e <= 0) return;
-    int hb = std::max(0, std::min(W * (j / W), e));
+    int hb = std::max(0, std::min(W * ((j - s) / W), e));
     hb -= hb % W;
     int b = 0;
-    for (; b + W <= hb; b += W) out.push_back({b, W});
+    for (; b + W <= hb; b += W) out.push_back({s + b, W});
     for (int p = W / 2; p >= 1; p /= 2)
         if (b + p <= e - near) {
-            out.push_back({b, p});
+            out.push_back({s + b, p});
             b += p;
         }
-    for (; b < e; b++) out.push_back({b, 1});
+    for (; b < e; b++) out.push_back({s + b, 1});
 }
 
-static Schedule make_schedule(int nc, int nr, int W, int near, int P, const Cost& cm, bool build) {
+// ni > 0: the last ni row blocks are the identity (the inverse L^{-1} riding along as
+// L^{-T} rows): identity block a = i - (nr - ni) has zero L blocks before column block a.
+static Schedule make_schedule(int nc, int nr, int W, int near, int P, const Cost& cm, bool build, int ni = 0) {
+    const int nr0 = nr - ni;
+    auto start_of = [&](int i) { return i >= nr0 ? i - nr0 : 0; };
     std::vector<Task> tasks;
     tasks.reserve((size_t)nr * nc * 2);
     auto add = [&](int type, int i, int j, int b0, int nb, double dur) {
@@ -644,7 +650,7 @@ static Schedule make_schedule(int nc, int nr, int W, int near, int P, const Cost
         std::vector<std::pair<int, int>> ch;
         for (int j = 1; j < nc; j++)
             for (int i = j; i < nr; i++) {
-                tile_chunks(i, j, W, near, ch);
+                tile_chunks(i, j, W, near, ch, start_of(i));
                 for (auto& c : ch) by_last[c.first + c.second - 1].push_back(Chunk{i, j, c.first, c.second});
             }
     }
@@ -669,6 +675,7 @@ static Schedule make_schedule(int nc, int nr, int W, int near, int P, const Cost
     for (int k = 0; k < nc; k++) {
         for (int i = k + 1; i < nr; i++) {
             if (i == k + 1 && i < nc) continue;  // inside DIAGX(k+1)
+            if (k < start_of(i)) continue;        // zero block of an identity row
             const int id = add(T_TRSM, i, k, 0, 0, cm.trsm);
             trsm[(size_t)i * nc + k] = id;
             dep(id, diagx[k]);
@@ -786,7 +793,7 @@ struct PtState {
         double est_us = 0;
         std::vector<int4> host;
     };
-    std::map<std::tuple<int, int, bool>, Dev> sched;
+    std::map<std::tuple<int, int, bool, int>, Dev> sched;
     int* ctr = nullptr;
     size_t ctr_ints = 0;
     int ncu = 0;
@@ -828,8 +835,27 @@ int pt_debug_snapshot(int* out, int max_wg) {
     return n;
 }
 
+// counters of the identity row blocks (the inverse riding along): block a = i - nr0 has its
+// first a panels "applied" (they are zero) and its first a L blocks "final"
+__global__ void pt_init_identity_counters(int* __restrict__ lcnt, int* __restrict__ ver, int nc, int nr0, int ni) {
+    const int a = blockIdx.x, j = threadIdx.x;
+    if (a >= ni) return;
+    if (j == 0) lcnt[nr0 + a] = a;
+    for (int c = j; c < nc; c += blockDim.x) ver[(int64_t)(nr0 + a) * nc + c] = a;
+}
+
+// identity rows: A[row0 + r][c] = (r == c) for the columns at or right of r's block
 template <typename T>
-void potrf_tiles(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info, Exec& ex, const TileBuild<T>* build) {
+__global__ void pt_init_identity_rows(T* __restrict__ A, int64_t ld, int64_t row0, int64_t nid, int64_t ncol) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t c = blockIdx.y;
+    if (r >= nid || c >= ncol || c < (r / GT) * GT) return;
+    A[row0 + r + c * ld] = (r == c) ? T(1) : T(0);
+}
+
+template <typename T>
+void potrf_tiles(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info, Exec& ex, const TileBuild<T>* build,
+                 int ni) {
     using namespace pt;
     if (!ex.pt) ex.pt = new PtState();
     PtState& st = *ex.pt;
@@ -843,11 +869,12 @@ void potrf_tiles(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info
     GPRX_REQUIRE(np % DB == 0 && nrows % GT == 0 && nrows >= np, GPRX_ERR_ARG, "potrf_tiles: bad sizes");
     const int nc = (int)(np / DB), nr = (int)(nrows / GT);
     const bool fused = build && build->mode != 0;
-    auto key = std::make_tuple(nc, nr, fused);
+    GPRX_REQUIRE(ni >= 0 && ni <= nr - nc, GPRX_ERR_ARG, "potrf_tiles: bad identity row blocks");
+    auto key = std::make_tuple(nc, nr, fused, ni);
     auto it = st.sched.find(key);
     if (it == st.sched.end()) {
         const Params& pr = params();
-        Schedule S = make_schedule(nc, nr, pr.W, pr.near, st.ncu, pr.cm, fused);
+        Schedule S = make_schedule(nc, nr, pr.W, pr.near, st.ncu, pr.cm, fused, ni);
         PtState::Dev d;
         d.n = (int64_t)S.list.size();
         d.est_us = S.est_us;
@@ -868,6 +895,12 @@ void potrf_tiles(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info
     GPRX_HIP(hipMemsetAsync(st.ctr, 0, sizeof(int) * need, s));
     if (fused)  // ver = -1 (not built) for the tiles of the leading block; the label rows are built
         GPRX_HIP(hipMemsetAsync(st.ctr + C_NCTL + nr, 0xff, sizeof(int) * (size_t)nc * nc, s));
+    if (ni > 0) {
+        hipLaunchKernelGGL(pt_init_identity_counters, dim3((unsigned)ni), dim3(128), 0, s, st.ctr + C_NCTL,
+                           st.ctr + C_NCTL + nr, nc, nr - ni, ni);
+        hipLaunchKernelGGL(pt_init_identity_rows<T>, dim3((unsigned)((ni * (int64_t)GT + 255) / 256), (unsigned)np),
+                           dim3(256), 0, s, A, ld, (int64_t)(nr - ni) * GT, (int64_t)ni * GT, np);
+    }
     Args<T> a;
     a.A = A;
     a.ld = ld;
@@ -924,22 +957,26 @@ void potrf_tiles(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info
         attr = true;
     }
     const double nn = (double)np;
-    ProfScope ps(KC_TILES, s, nn * nn * nn / 3.0 + (double)(nrows - np) * nn * nn, 0.0);
+    ProfScope ps(KC_TILES, s,
+                 nn * nn * nn / 3.0 + (double)(nrows - np - (int64_t)ni * GT) * nn * nn + (ni ? nn * nn * nn / 3.0 : 0.0),
+                 0.0);
     hipLaunchKernelGGL(potrf_tiles_kernel<T>, dim3((unsigned)st.ncu), dim3(NT), lds, s, a);
     GPRX_HIP(hipGetLastError());
 }
 
 // Host-only schedule statistics (no device work): tasks, predicted makespan, and a check
 // that every task's producers come earlier in the ticket order.
-int64_t potrf_tiles_schedule_stats(int nc, int nr, int P, bool build, double* est_us) {
-    if (nc < 1 || nr < nc || P < 1) throw Error{GPRX_ERR_ARG, "potrf tile schedule: need nc >= 1, nr >= nc, P >= 1"};
+int64_t potrf_tiles_schedule_stats(int nc, int nr, int P, bool build, double* est_us, int ni) {
+    if (nc < 1 || nr < nc || P < 1 || ni < 0 || ni > nr - nc)
+        throw Error{GPRX_ERR_ARG, "potrf tile schedule: need nc >= 1, nr >= nc + ni, P >= 1"};
     const pt::Params& pr = pt::params();
-    pt::Schedule S = pt::make_schedule(nc, nr, pr.W, pr.near, P, pr.cm, build);
+    pt::Schedule S = pt::make_schedule(nc, nr, pr.W, pr.near, P, pr.cm, build, ni);
     if (est_us) *est_us = S.est_us;
     return S.ntasks;
 }
 
-template void potrf_tiles<double>(double*, int64_t, int64_t, int64_t, double*, int*, Exec&, const TileBuild<double>*);
-template void potrf_tiles<float>(float*, int64_t, int64_t, int64_t, float*, int*, Exec&, const TileBuild<float>*);
+template void potrf_tiles<double>(double*, int64_t, int64_t, int64_t, double*, int*, Exec&, const TileBuild<double>*,
+                                  int);
+template void potrf_tiles<float>(float*, int64_t, int64_t, int64_t, float*, int*, Exec&, const TileBuild<float>*, int);
 
 }  // namespace gprx

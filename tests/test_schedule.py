@@ -10,13 +10,13 @@ import pytest
 from gpr_amd.gprx import lib
 
 
-def _sched(nc, nr, P=256, build=False):
+def _sched(nc, nr, P=256, build=False, ident=False):
     L = lib()
     L.gprx_dev_schedule.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                     ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]
     est = ctypes.c_double()
     n = ctypes.c_int64()
-    st = L.gprx_dev_schedule(nc, nr, P, 1 if build else 0, ctypes.byref(est), ctypes.byref(n))
+    st = L.gprx_dev_schedule(nc, nr, P, (1 if build else 0) | (2 if ident else 0), ctypes.byref(est), ctypes.byref(n))
     return st, n.value, est.value
 
 
@@ -62,6 +62,33 @@ def test_schedule_with_fused_build(nc):
     assert n == _expected_tasks(nc, nc + 1) + nc * (nc + 1) // 2
     _, _, est0 = _sched(nc, nc + 1)
     assert est >= est0  # the builds add work
+
+
+@pytest.mark.parametrize("nc,extra", [(1, 1), (3, 1), (9, 1), (40, 1)])
+def test_schedule_with_identity_rows(nc, extra):
+    """The inverse riding along (k_ptiles.hip make_schedule ni > 0): identity row block a
+    gets TRSM(., k) only for k >= a and updates only from panel a on; the ticket order still
+    respects every dependency, and the extra tasks match that count."""
+    nr = nc + extra + nc
+    st, n, est = _sched(nc, nr, build=False, ident=True)
+    assert st == 0, "ticket order violates a dependency"
+    W, near = 32, 1
+    extra_tasks = 0
+    for a in range(nc):
+        extra_tasks += nc - a  # TRSM(nr0 + a, k) for k = a .. nc - 1
+        for j in range(a + 1, nc):
+            e = j - a
+            hb = min(W * ((j - a) // W), e)
+            hb -= hb % W
+            cnt = hb // W
+            b, p = hb, W // 2
+            while p >= 1:
+                if b + p <= e - near:
+                    cnt += 1
+                    b += p
+                p //= 2
+            extra_tasks += cnt + (e - b)
+    assert n == _expected_tasks(nc, nc + extra) + extra_tasks
 
 
 def test_schedule_makespan_scales():
