@@ -8,9 +8,9 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:-r01}
 export TMPDIR=/tmp
 cd /tmp
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_$TAG -o bench -- python3 $R/bench.py --cpu-n 0 > $R/gpurun_out/prof_${TAG}.log 2>&1
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_$TAG -o bench -- python3 $R/bench.py --cpu-n 0 --lml 0 > $R/gpurun_out/prof_${TAG}.log 2>&1
 echo trace=$?
-timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/gpurun_out/pmcf_$TAG -o f -- python3 $R/bench.py --steps 2 --warmup 1 --cpu-n 0 --predict-q 1024 > $R/gpurun_out/pmcf_${TAG}.log 2>&1
+timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/gpurun_out/pmcf_$TAG -o f -- python3 $R/bench.py --steps 2 --warmup 1 --cpu-n 0 --predict-q 1024 --lml 0 > $R/gpurun_out/pmcf_${TAG}.log 2>&1
 echo fetch=$?
-timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/gpurun_out/pmcw_$TAG -o w -- python3 $R/bench.py --steps 2 --warmup 1 --cpu-n 0 --predict-q 1024 > $R/gpurun_out/pmcw_${TAG}.log 2>&1
+timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/gpurun_out/pmcw_$TAG -o w -- python3 $R/bench.py --steps 2 --warmup 1 --cpu-n 0 --predict-q 1024 --lml 0 > $R/gpurun_out/pmcw_${TAG}.log 2>&1
 echo write=$?
