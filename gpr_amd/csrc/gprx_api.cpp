@@ -309,7 +309,7 @@ static gprx_status model_fit(gprx_model* M, uint32_t flags, gprx_fit_info* out) 
     M->alpha.ensure(sizeof(T) * np * M->m);
     M->info.ensure(sizeof(int));
     M->flag.ensure(sizeof(int));
-    M->red.ensure(sizeof(double) * 2);
+    M->red.ensure(sizeof(double) * (2 + 2 * (np / GT + 1)));  // results, then per-block partials
     if (K.nper > 0) {  // per-sample sin/cos tables: the direct build, predict, posterior and LML paths
         M->tab.ensure(sizeof(T) * 2 * K.nper * n * M->d);
         launch_sincos_tables<T>(K, M->X.as<T>(), n, M->d, M->tab.as<T>(), s);

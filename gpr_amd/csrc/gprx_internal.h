@@ -415,7 +415,8 @@ void launch_backsolve_chain(const T* A, int64_t ld, int64_t np, int m, const T* 
 // logdet partial = 2 sum log L_ii over i < n, datafit = sum of squares of the augmented
 // rows; results accumulated in double on the device (out[0], out[1]).
 template <typename T>
-void launch_fit_reductions(const T* A, int64_t ld, int64_t n, int64_t np, int m, double* out, hipStream_t s);
+void launch_fit_reductions(const T* A, int64_t ld, int64_t n, int64_t np, int m, double* out,
+                           hipStream_t s);  // out: 2 + 2 * (np / 128) doubles
 
 // Fused prediction: mean (q x m row-major) and optional derivative (q x d x m).
 template <typename T>
