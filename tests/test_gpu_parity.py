@@ -162,6 +162,20 @@ def test_lml_gradient_multi_tile(ctx, ks):
     assert relerr(g, gr) <= 1e-6
 
 
+@pytest.mark.parametrize("ks", ["SumKernel(GaussianKernel(2,0.15,),PeriodicKernel(0.1,3.141592653589793,1,))",
+                                "GaussianKernel(0.7,1.3,)"])
+def test_lml_gradient_f32(ctx, ks):
+    """fp32 LML + gradient (the inverse riding along in the fp32 tile factorisation) against
+    the oracle in fp32 and fp64, at the fp32 tolerance."""
+    n, d, sigma = 600, 4, 0.7
+    X, Y = make_data(n, d)
+    M, _ = _fit(ctx, ks, X.astype(np.float32), Y.astype(np.float32), sigma, np.float32)
+    v, g, _ = M.lml(grad=True)
+    vr, gr, _, _ = O.lml(ks, X, Y, sigma)
+    assert abs(v - vr) <= 1e-3 * max(1.0, abs(vr))
+    assert relerr(g, gr) <= 1e-3
+
+
 def test_nonfinite_kernel_matrix(ctx):
     import gpr_amd
     X = np.array([[0.0], [np.inf]])
