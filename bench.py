@@ -198,6 +198,7 @@ def main():
                   "gbs": (v["bytes"] / (v["ms"] * 1e-3) / 1e9) if v["ms"] and v["bytes"] else None}
               for k, v in stats.items()}
     t_roof = fit_roofline_ms(n, d, m)
+    traffic = traffic_from_profile()
     fit_ms = np.median([i.ms_build + i.ms_factor + i.ms_solve for i in infos])
 
     if rank == 0:
@@ -231,7 +232,10 @@ def main():
                          "frac": achieved / PEAK_FP64_TFLOPS,
                          "avg_launch_us": 1e3 * avg_ms if avg_ms else None,
                          "algorithmic_flops_per_launch": alg_flops,
-                         "traffic": traffic_from_profile()},
+                         # HBM bytes per launch from the committed PMC passes (FETCH_SIZE x 2 +
+                         # WRITE_SIZE, MI355X_MICROARCH.md), null if none is committed
+                         "traffic": (traffic["bytes_per_launch"] if traffic else None),
+                         "traffic_source": (traffic["source"] if traffic else None)},
             "fit_roofline": {"t_roof_ms": t_roof, "t_fit_device_ms": fit_ms, "frac": t_roof / fit_ms},
             "phases": phases,
             "predict": pred,
