@@ -19,7 +19,7 @@ __global__ __launch_bounds__(NT) void probe(const double* A, const double* B, in
     __syncthreads();
     const long long t0 = __builtin_amdgcn_s_memtime();
     for (int r = 0; r < reps; r++) {
-        tile_mma<double>(acc, A + off, ld, B + off, ld, K, true, smem, threadIdx.x);
+        tile_mma<double>(acc, A + off, ld, B + off, ld, K, K, smem, threadIdx.x);
 #pragma unroll
         for (int x = 0; x < 2; x++)
 #pragma unroll
