@@ -35,6 +35,8 @@ void launch_set_identity_pad(T* A, int64_t ld, int64_t n, int64_t np, hipStream_
 template <typename T>
 void launch_gemm_add_lower(T* S, int64_t lds, const T* K, int64_t ldk, int64_t n, hipStream_t s);
 template <typename T>
+void launch_sym_fill(T* C, int64_t ldc, int64_t n, hipStream_t s);
+template <typename T>
 void launch_sum_partials(T* S, int64_t stride, int P, hipStream_t s);
 
 gprx_status gprx_dev_bench_impl(gprx_dtype dtype, int32_t what, int64_t M, int64_t N, int64_t K, int32_t iters,
@@ -786,17 +788,12 @@ ncclDataType_t nccl_type<float>() {
 
 template <typename T>
 static void download_sym(void* out, const DevBuf& C, int64_t ldc, int64_t n, hipStream_t s) {
-    std::vector<T> h((size_t)n * n);
-    GPRX_HIP(hipStreamSynchronize(s));
+    // mirrored on the device, then one strided copy: the full symmetric matrix reads the same
+    // row- or column-major, so it lands in the caller's buffer as is
+    launch_sym_fill<T>(C.as<T>(), ldc, n, s);
     GPRX_HIP(hipGetLastError());
-    GPRX_HIP(hipMemcpy2D(h.data(), sizeof(T) * n, C.p, sizeof(T) * ldc, sizeof(T) * n, n, hipMemcpyDeviceToHost));
-    T* o = reinterpret_cast<T*>(out);
-    for (int64_t j = 0; j < n; j++)
-        for (int64_t i = j; i < n; i++) {
-            const T v = h[(size_t)j * n + i];
-            o[(size_t)i * n + j] = v;
-            o[(size_t)j * n + i] = v;
-        }
+    GPRX_HIP(hipMemcpy2DAsync(out, sizeof(T) * n, C.p, sizeof(T) * ldc, sizeof(T) * n, n, hipMemcpyDeviceToHost, s));
+    GPRX_HIP(hipStreamSynchronize(s));
 }
 
 template <typename T>
@@ -814,43 +811,77 @@ static gprx_status sparse_fit_impl(gprx_ctx* ctx, const gprx_kernel_desc* desc, 
     int64_t cmax = 32768;  // dense rows per streamed block (GPRX_SPARSE_CHUNK overrides, for tests)
     if (const char* ev = std::getenv("GPRX_SPARSE_CHUNK")) cmax = std::max<int64_t>(64, round_up(std::atoll(ev), 64));
     const int64_t chunk = std::max<int64_t>(BT, std::min<int64_t>(round_up(std::max<int64_t>(n, 1), 64), cmax));
-    DevBuf dXm, dtm, dX, dtx, dY, dS, dA, dK, dLinv, dLinvK, dinfo, dflag, dz, dalpha, dV, dC;
+    DevBuf dXm, dtm, dX, dtx, dY, dS, dA, dK, dLinv, dLinvK, dinfo, dflag, dz, dalpha, dV, dC, dFU, dFV, dKd;
     upload<T>(dXm, Xmh, sizeof(T) * M * d, s);
     upload<T>(dX, Xh, sizeof(T) * std::max<int64_t>(n, 1) * d, s);
     upload<T>(dY, Yh, sizeof(T) * std::max<int64_t>(n, 1) * m, s);
+    // Kmn blocks as MFMA pair statistics (k_pairs.hip) when the tree allows it: features of
+    // the inducing points once, of each dense chunk per chunk, both centred on Xm's first row
+    const bool mma = pairs_mma_supported<T>(K, 1);
+    const int64_t chunk128 = round_up(chunk, GT);
+    if (mma) {
+        const int64_t fc = pairs_feature_cols<T>(K, d);
+        dKd.ensure(sizeof(KCanon<T>));
+        GPRX_HIP(hipMemcpyAsync(dKd.p, &K, sizeof(KCanon<T>), hipMemcpyHostToDevice, s));
+        dFU.ensure(sizeof(T) * Mp * fc);
+        dFV.ensure(sizeof(T) * chunk128 * fc);
+        launch_pair_features<T>(K, dXm.as<T>(), M, d, dXm.as<T>(), false, dFU.as<T>(), Mp, s);
+    }
     if (K.nper > 0) {
-        dtm.ensure(sizeof(T) * 2 * K.nper * M * d);
+        dtm.ensure(sizeof(T) * 2 * K.nper * M * d);  // Kmm below
         launch_sincos_tables<T>(K, dXm.as<T>(), M, d, dtm.as<T>(), s);
-        dtx.ensure(sizeof(T) * 2 * K.nper * chunk * d);  // per-chunk tables of the dense rows
+        if (!mma) dtx.ensure(sizeof(T) * 2 * K.nper * chunk * d);  // per-chunk tables of the dense rows
     }
     dflag.ensure(sizeof(int));
     dinfo.ensure(sizeof(int));
     GPRX_HIP(hipMemsetAsync(dflag.p, 0, sizeof(int), s));
     // ---- accumulate sigma^-2 [Kmn ; Y^T][Kmn ; Y^T]^T over the dense rows (lower part) ----
-    // split-K partials: enough (tiles x partials) workgroups to fill the chip
+    // split-K partials: tiles x partials workgroups in whole rounds of the chip's slots (one
+    // tile-mainloop workgroup per CU).  M = 2048: 152 tiles; P = 5 fills 3 rounds to 99% (an
+    // earlier P = 7 on two slots per CU left the third round 4% full).
     const int64_t ntiles = (Mp / GT) * (Mp / GT + 1) / 2 + (mp / GT) * (Mp / GT);
-    const int P = (int)std::max<int64_t>(1, std::min<int64_t>(8, (1024 + ntiles - 1) / ntiles));
+    int ncu = 0;
+    GPRX_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
+    const int64_t slots = (int64_t)std::max(1, ncu);
+    const int64_t ncp_max = round_up(chunk, 16);
+    int P = 1;
+    double best = 0.0;
+    for (int p = 1; p <= 16; p++) {
+        if (p > 1 && round_up((ncp_max + p - 1) / p, 16) < 256) break;  // keep each slice >= 256 deep
+        const int64_t wg = ntiles * p, rounds = (wg + slots - 1) / slots;
+        const double eff = (double)wg / (double)(rounds * slots);
+        if (eff > best + 1e-9) {
+            best = eff;
+            P = p;
+        }
+    }
     const int64_t sstride = ld * Mp;
     dS.ensure(sizeof(T) * sstride * P);
     GPRX_HIP(hipMemsetAsync(dS.p, 0, sizeof(T) * sstride * P, s));
-    const int64_t acols = chunk + 16 * 8;  // slack: the last split-K slice may overhang ncp (zeros)
+    const int64_t acols = chunk + 16 * 16;  // slack: the P <= 16 split-K slices may overhang ncp (zeros)
     dA.ensure(sizeof(T) * ld * acols);
     const T is2 = T(1) / (T(sigma) * T(sigma));  // inverse_sigma2 in T (:285)
     for (int64_t off = 0; off < n; off += chunk) {
         const int64_t nc = std::min(chunk, n - off), ncp = round_up(nc, 16);
         if (nc < chunk || off == 0) GPRX_HIP(hipMemsetAsync(dA.p, 0, sizeof(T) * ld * acols, s));
-        const T* tabc = nullptr;
-        if (K.nper > 0) {
-            launch_sincos_tables<T>(K, dX.as<T>() + off * d, nc, d, dtx.as<T>(), s);
-            tabc = dtx.as<T>();
+        if (mma) {
+            const int64_t nc128 = round_up(nc, GT);
+            launch_pair_features<T>(K, dX.as<T>() + off * d, nc, d, dXm.as<T>(), true, dFV.as<T>(), nc128, s);
+            launch_kcross_mma<T>(K, dKd.as<KCanon<T>>(), dFU.as<T>(), Mp, M, dFV.as<T>(), nc128, nc, d, dA.as<T>(), ld,
+                                 dflag.as<int>(), s);
+        } else {
+            const T* tabc = nullptr;
+            if (K.nper > 0) {
+                launch_sincos_tables<T>(K, dX.as<T>() + off * d, nc, d, dtx.as<T>(), s);
+                tabc = dtx.as<T>();
+            }
+            launch_kbuild<T>(K, dXm.as<T>(), dtm.as<T>(), M, dX.as<T>() + off * d, tabc, nc, d, dA.as<T>(), ld, 0,
+                             false, T(0), dflag.as<int>(), s);
         }
-        launch_kbuild<T>(K, dXm.as<T>(), dtm.as<T>(), M, dX.as<T>() + off * d, tabc, nc, d, dA.as<T>(), ld, 0,
-                         false, T(0), dflag.as<int>(), s);
         launch_label_rows<T>(dY.as<T>() + off * m, nc, m, dA.as<T>(), ld, Mp, ncp, mp, s);
         const int64_t kpart = round_up((ncp + P - 1) / P, 16);  // zero-padded columns make up the rest
         const int Pc = (int)((ncp + kpart - 1) / kpart);
-        launch_gemm_nt_splitk<T>(dS.as<T>(), ld, sstride, dA.as<T>(), ld, dA.as<T>(), ld, ld, Mp, kpart, Pc, is2, true,
-                                 s);
+        launch_syrk_splitk<T>(dS.as<T>(), ld, sstride, dA.as<T>(), ld, ld, Mp, kpart, Pc, is2, s);
     }
     launch_sum_partials<T>(dS.as<T>(), sstride, P, s);  // dS[0] += dS[1..P-1]
     if (ctx->comm && ctx->world > 1) {

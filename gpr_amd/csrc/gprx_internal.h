@@ -293,6 +293,12 @@ void launch_pair_features(const KCanon<T>& K, const T* X, int64_t n, int d, cons
 template <typename T>
 void launch_kbuild_mma(const KCanon<T>& K, const KCanon<T>* Kd, const T* FU, const T* FV, int64_t nf, int d, T* A,
                        int64_t ld, int64_t n, T sigma2, int* flag, hipStream_t s);
+// Cross matrix K(Xa, Xb) (na x nb, column-major, ld) from the features FU of Xa (nfu rows)
+// and FV of Xb (nfv rows, right = true), both centred on the same point; only valid entries
+// are stored.
+template <typename T>
+void launch_kcross_mma(const KCanon<T>& K, const KCanon<T>* Kd, const T* FU, int64_t nfu, int64_t na, const T* FV,
+                       int64_t nfv, int64_t nb, int d, T* A, int64_t ld, int* flag, hipStream_t s);
 template <typename T>
 void launch_predict_mma(const KCanon<T>& K, const KCanon<T>* Kd, const T* FU, int64_t nfu, const T* FV, int64_t nfv,
                         int d, const T* alpha, int64_t n, int m, int64_t q, T* mean, hipStream_t s);
@@ -400,6 +406,13 @@ void launch_gemm_nt(T* C, int64_t ldc, const T* A, int64_t lda, const T* B, int6
 template <typename T>
 void launch_gemm_nt_splitk(T* C, int64_t ldc, int64_t cstride, const T* A, int64_t lda, const T* B, int64_t ldb,
                            int64_t M, int64_t N, int64_t K, int P, T alpha, bool lower, hipStream_t s);
+
+// Split-K rank-k accumulation on the tile mainloop (k_syrk.hip): partial p (of P) +=
+// alpha A[:, pK:(p+1)K] A[:, pK:(p+1)K]^T into C + p*cstride, lower triangle of the leading
+// N x N block plus the M - N rows below it.
+template <typename T>
+void launch_syrk_splitk(T* C, int64_t ldc, int64_t cstride, const T* A, int64_t lda, int64_t M, int64_t N, int64_t K,
+                        int P, T alpha, hipStream_t s);
 
 // Back substitution L^T alpha = z with z given as the m augmented rows (row-major output
 // alpha: np x m, ld m).  Uses the diagonal-block inverses.

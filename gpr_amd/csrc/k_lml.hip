@@ -37,6 +37,34 @@ __global__ void add_lower_kernel(T* __restrict__ S, int64_t lds, const T* __rest
     if (i < n && i >= j) S[i + j * lds] += K[i + j * ldk];
 }
 
+// Mirror the lower triangle of C (n x n, column-major, ld ldc) into its upper triangle:
+// 32x32 tiles transposed through LDS, so both the reads and the writes are column runs.
+template <typename T>
+__global__ __launch_bounds__(256) void sym_fill_kernel(T* __restrict__ C, int64_t ldc, int64_t n) {
+    const int64_t bx = blockIdx.x, by = blockIdx.y;  // destination tile: rows bx, columns by
+    if (bx > by) return;
+    __shared__ T sh[32][33];
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {  // source tile: rows by, columns bx (lower)
+        const int64_t r = by * 32 + tx, c = bx * 32 + ty + 8 * k;
+        if (r < n && c < n) sh[ty + 8 * k][tx] = C[r + c * ldc];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int64_t i = bx * 32 + tx, j = by * 32 + ty + 8 * k;
+        if (j < n && i < j) C[i + j * ldc] = sh[tx][ty + 8 * k];
+    }
+}
+
+template <typename T>
+void launch_sym_fill(T* C, int64_t ldc, int64_t n, hipStream_t s) {
+    if (n <= 0) return;
+    const unsigned nt = (unsigned)((n + 31) / 32);
+    hipLaunchKernelGGL(sym_fill_kernel<T>, dim3(nt, nt), dim3(256), 0, s, C, ldc, n);
+}
+
 // S (lower, n x n, ld lds) += K (lower, ld ldk)
 template <typename T>
 void launch_gemm_add_lower(T* S, int64_t lds, const T* K, int64_t ldk, int64_t n, hipStream_t s) {
@@ -248,6 +276,7 @@ void launch_lml_grad(const KCanon<T>& K, const T* X, const T* tab, int64_t n, in
 #define GPRX_INST(T)                                                                                            \
     template void launch_set_identity_pad<T>(T*, int64_t, int64_t, int64_t, hipStream_t);                      \
     template void launch_gemm_add_lower<T>(T*, int64_t, const T*, int64_t, int64_t, hipStream_t);              \
+    template void launch_sym_fill<T>(T*, int64_t, int64_t, hipStream_t);                                       \
     template void launch_sum_partials<T>(T*, int64_t, int, hipStream_t);                                        \
     template void launch_spd_inverse_from_factor<T>(const T*, int64_t, int64_t, const T*, T*, T*, hipStream_t); \
     template void launch_lml_grad<T>(const KCanon<T>&, const T*, const T*, int64_t, int, const T*, const T*,   \

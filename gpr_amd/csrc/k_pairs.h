@@ -174,6 +174,65 @@ __device__ __forceinline__ bool build_tile(const KCanon<T>* __restrict__ Kd, con
 }
 
 
+// Tile (i0, j0) of the cross matrix K(Xa, Xb) into A (column-major, ld): rows from FU (nfu
+// rows, na valid), columns from FV (nfv rows, nb valid); only valid entries are stored.  The
+// sparse fit's Kmn blocks (include/SparseGaussianProcess.h:218-235).
+template <typename T, int NPER, bool R2>
+__device__ __forceinline__ bool cross_tile(const KCanon<T>* __restrict__ Kd, const T* __restrict__ FU, int64_t nfu,
+                                           int64_t na, const T* __restrict__ FV, int64_t nfv, int64_t nb, int Kr,
+                                           int Kp, T hd, T* __restrict__ A, int64_t ld, int64_t i0, int64_t j0,
+                                           T* smem, const int t) {
+    typedef Mfma<T> Tr;
+    const int lane = t & 63, w = t >> 6;
+    const int wr = w & 1, wc = w >> 1, lr = lane & 15, lk = lane >> 4;
+    T nu[4], nv[2][4];
+#pragma unroll
+    for (int y = 0; y < 4; y++) nu[y] = R2 ? FU[(int64_t)(Kr + Kp) * nfu + i0 + wr * 64 + y * 16 + lr] : T(0);
+#pragma unroll
+    for (int x = 0; x < 2; x++)
+#pragma unroll
+        for (int reg = 0; reg < 4; reg++)
+            nv[x][reg] = R2 ? FV[(int64_t)(Kr + Kp) * nfv + j0 + wc * 32 + x * 16 + Tr::orow(lk, reg)] : T(0);
+    typename Tr::acc_t ar[2][4], ap[2][4];
+    block_stats<T, NPER, R2>(FU, nfu, i0, FV, nfv, j0, Kr, Kp, smem, t, ar, ap);
+    bool bad = false;
+    constexpr int G = 2;
+    auto chunk = [&](auto cc) {
+        constexpr int x = decltype(cc)::value / (4 / G), h = decltype(cc)::value % (4 / G);
+        T r2[4 * G], sp[4 * G], v[4 * G];
+#pragma unroll
+        for (int reg = G * h; reg < G * h + G; reg++)
+#pragma unroll
+            for (int y = 0; y < 4; y++) {
+                T a, b;
+                pair_stats<T, NPER, R2>(R2 ? ar[x][y][reg] : T(0), NPER ? ap[x][y][reg] : T(0), nu[y], nv[x][reg], hd,
+                                        a, b);
+                r2[(reg - G * h) * 4 + y] = a;
+                sp[(reg - G * h) * 4 + y] = b;
+            }
+        pair_values<T, 4 * G>(Kd, r2, sp, v);
+#pragma unroll
+        for (int reg = G * h; reg < G * h + G; reg++) {
+            const int64_t gj = j0 + wc * 32 + x * 16 + Tr::orow(lk, reg);
+            T* col = A + gj * ld;
+#pragma unroll
+            for (int y = 0; y < 4; y++) {
+                const int64_t gi = i0 + wr * 64 + y * 16 + lr;
+                const T val = v[(reg - G * h) * 4 + y];
+                if (gi < na && gj < nb) {
+                    if (!isfinite(val)) bad = true;
+                    col[gi] = val;
+                }
+            }
+        }
+    };
+    chunk(std::integral_constant<int, 0>{});
+    chunk(std::integral_constant<int, 1>{});
+    chunk(std::integral_constant<int, 2>{});
+    chunk(std::integral_constant<int, 3>{});
+    return bad;
+}
+
 // Sum-of-leaves trees only (K.sum_leaves): the same tile as build_tile, stored whole (the
 // upper half of a diagonal tile gets the symmetric values) with write-through stores for a
 // hand-off to other workgroups, and with the value separated by statistic, v = sum_{r2 leaves} leaf(r2) + sum_{periodic} leaf(S).

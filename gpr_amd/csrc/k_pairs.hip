@@ -80,6 +80,20 @@ __global__ __launch_bounds__(NT) void kbuild_mma_kernel(const KCanon<T>* __restr
     if (bad) atomicOr(flag, 1);
 }
 
+// Cross matrix K(Xa, Xb) (na x nb) into A, one workgroup per 128x128 tile (grid.x over the
+// rows of Xa, grid.y over the rows of Xb).
+template <typename T, int NPER, bool R2>
+__global__ __launch_bounds__(NT) void kcross_mma_kernel(const KCanon<T>* __restrict__ Kd, const T* __restrict__ FU,
+                                                        int64_t nfu, int64_t na, const T* __restrict__ FV, int64_t nfv,
+                                                        int64_t nb, int Kr, int Kp, T hd, T* __restrict__ A, int64_t ld,
+                                                        int* __restrict__ flag) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    T* smem = reinterpret_cast<T*>(smem_raw);
+    const bool bad = cross_tile<T, NPER, R2>(Kd, FU, nfu, na, FV, nfv, nb, Kr, Kp, hd, A, ld, (int64_t)blockIdx.x * GT,
+                                             (int64_t)blockIdx.y * GT, smem, threadIdx.x);
+    if (bad) atomicOr(flag, 1);
+}
+
 // mean[q][r] = sum_j k(xq_q, x_j) alpha[j][r], r < m <= PM, one workgroup per 128 queries
 // streaming the training set in 128-point blocks; K(Xq, X) is never materialised.  (PM = 1:
 // more outputs per query would spill next to the two accumulator sets; they take the direct
@@ -457,6 +471,18 @@ void launch_kbuild_mma(const KCanon<T>& K, const KCanon<T>* Kd, const T* FU, con
 }
 
 template <typename T>
+void launch_kcross_mma(const KCanon<T>& K, const KCanon<T>* Kd, const T* FU, int64_t nfu, int64_t na, const T* FV,
+                       int64_t nfv, int64_t nb, int d, T* A, int64_t ld, int* flag, hipStream_t s) {
+    GPRX_REQUIRE(nfu % GT == 0 && nfv % GT == 0 && na <= nfu && nb <= nfv && ld >= nfu, GPRX_ERR_ARG,
+                 "launch_kcross_mma: feature rows must be multiples of 128 covering the samples");
+    const int Kr = pr::kr_of(K, d), Kp = pr::kp_of(K, d);
+    const dim3 grid((unsigned)(nfu / GT), (unsigned)(nfv / GT));
+    ProfScope ps(KC_BUILD, s, 2.0 * (double)nfu * nfv * (Kr + Kp), (double)sizeof(T) * (double)na * nb);
+    GPRX_PAIRS_DISPATCH(kcross_mma_kernel, Kd, FU, nfu, na, FV, nfv, nb, Kr, Kp, T(0.5) * T(d), A, ld, flag);
+    GPRX_HIP(hipGetLastError());
+}
+
+template <typename T>
 void launch_predict_mma(const KCanon<T>& K, const KCanon<T>* Kd, const T* FU, int64_t nfu, const T* FV, int64_t nfv,
                         int d, const T* alpha, int64_t n, int m, int64_t q, T* mean, hipStream_t s) {
     const int Kr = pr::kr_of(K, d), Kp = pr::kp_of(K, d);
@@ -552,6 +578,8 @@ TileBuild<T> pairs_tile_build(const KCanon<T>& K, const KCanon<T>* Kd, const T* 
                                           hipStream_t);                                                       \
     template void launch_kbuild_mma<T>(const KCanon<T>&, const KCanon<T>*, const T*, const T*, int64_t, int, T*,    \
                                        int64_t, int64_t, T, int*, hipStream_t);                               \
+    template void launch_kcross_mma<T>(const KCanon<T>&, const KCanon<T>*, const T*, int64_t, int64_t, const T*,  \
+                                       int64_t, int64_t, int, T*, int64_t, int*, hipStream_t);                  \
     template void launch_predict_mma<T>(const KCanon<T>&, const KCanon<T>*, const T*, int64_t, const T*, int64_t, \
                                         int, const T*, int64_t, int, int64_t, T*, hipStream_t);
 GPRX_PAIRS_INST(double)
