@@ -201,25 +201,35 @@ __device__ __forceinline__ void diag_factor(T* __restrict__ A, int64_t ld, T* __
             // LDS copy, so the row solve reads it back instead of holding it next to S
             T(*myLd)[9] = sLdW[w];
             {
-                T Ld[8][8];
+                // the whole pivot block is read up front (one LDS latency instead of one per
+                // column: the compiler cannot move these reads above the myLd stores), the
+                // factor runs in place in registers, and the stores follow in one branch
+                T Ld[8][8], ri[8];
+#pragma unroll
+                for (int c = 0; c < 8; c++)
+#pragma unroll
+                    for (int r = c; r < 8; r++) Ld[r][c] = sV[c][j0 + r];
 #pragma unroll
                 for (int c = 0; c < 8; c++) {
-                    T dsum = sV[c][j0 + c];
+                    T dsum = Ld[c][c];
 #pragma unroll
                     for (int k = 0; k < c; k++) dsum = fma(-Ld[c][k], Ld[c][k], dsum);
                     if (!(dsum > T(0)) && fail_col < 0) fail_col = j0 + c;
-                    const T ri = rsqrt_full(dsum);
-                    Ld[c][c] = dsum * ri;
+                    ri[c] = rsqrt_full(dsum);
+                    Ld[c][c] = dsum * ri[c];
 #pragma unroll
                     for (int r = c + 1; r < 8; r++) {
-                        T v = sV[c][j0 + r];
+                        T v = Ld[r][c];
 #pragma unroll
                         for (int k = 0; k < c; k++) v = fma(-Ld[r][k], Ld[c][k], v);
-                        Ld[r][c] = v * ri;
+                        Ld[r][c] = v * ri[c];
                     }
-                    // one lane per wave writes (64 lanes storing one word serialise in the LDS)
-                    if (l == 0) {
-                        myLd[c][8] = ri;
+                }
+                // one lane per wave writes (64 lanes storing one word serialise in the LDS)
+                if (l == 0) {
+#pragma unroll
+                    for (int c = 0; c < 8; c++) {
+                        myLd[c][8] = ri[c];
 #pragma unroll
                         for (int r = c; r < 8; r++) myLd[r][c] = Ld[r][c];
                     }
