@@ -71,3 +71,22 @@ def test_sparse_bad_sigma(ctx):
     with pytest.raises(gpr_amd.GprxError) as e:
         ctx.sparse_fit("GaussianKernel(1,1,)", X, Y, Xm, 0.0, 1e-4)
     assert "sigma must be positive" in str(e.value)
+
+
+@pytest.mark.parametrize("ks", ["GaussianKernel(0.7,1.3,)",
+                                "SumKernel(GaussianKernel(2,0.15,),PeriodicKernel(0.1,3.141592653589793,1,))"])
+def test_sparse_fit_multi_tile(ctx, monkeypatch, ks):
+    """Several 128-tiles of inducing points (M = 300: diagonal, off-diagonal and partial
+    tiles), several streamed chunks with split-K partials (P > 1) and a ragged last chunk.
+    Same tolerance as test_sparse_fit: the oracle follows the reference's Kinv-based formulas,
+    the device one Cholesky of S (algebraically equal)."""
+    monkeypatch.setenv("GPRX_SPARSE_CHUNK", "2048")
+    n, d, M, m = 5000, 8, 300, 1
+    X, Y, Xm = _inputs(n, d, M, m, np.float64)
+    Kinv, RV, RM = ctx.sparse_fit(ks, X, Y, Xm, 0.3, 1e-3, np.float64)
+    Ki_r, RV_r, RM_r = O.sparse_fit(ks, X, Y, Xm, 0.3, 1e-3, np.float64)
+    tol = TOL[np.dtype(np.float64)] * 10
+    assert relerr(Kinv, Ki_r) <= tol
+    assert relerr(RV, RV_r) <= tol
+    assert relerr(RM, RM_r) <= tol
+    assert np.array_equal(Kinv, Kinv.T) and np.array_equal(RM, RM.T)
