@@ -183,5 +183,95 @@ __device__ __forceinline__ void tile_mma(typename Mfma<T>::acc_t (&acc)[2][4], c
     for (int st = st0; st < nst; st++) stage_sync(st);
 }
 
+// Two products over consecutive column ranges of the same operands in ONE pass of the
+// staging ring: acc1 = A[:, 0:K1] B[:, 0:K1]^T, acc2 = A[:, K1:K1+K2] B[:, K1:K1+K2]^T (K1, K2
+// multiples of BKS).  Two back-to-back tile_mma calls pay the ring's fill and drain twice
+// and a barrier between them; the pair statistics of a periodic + r2 tree are such a pair
+// (k_pairs.h: the r2 and periodic feature columns are adjacent).  Every wave multiplies.
+template <typename T>
+__device__ __forceinline__ void ring_issue(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, int64_t ldb,
+                                           int st, T* smem, const int t) {
+    typedef Stage<T> S;
+    const int lane = t & 63, w = t >> 6;
+    const int lcol = lane / S::LPC, lrow = (lane % S::LPC) * S::E;
+    T* buf = smem + (st % NBUF) * S::STG;
+#pragma unroll
+    for (int u = 0; u < S::IPW; u++) {
+        const int g = w * S::IPW + u;
+        const bool isB = g >= S::GRP;
+        const int gg = isB ? g - S::GRP : g;
+        const int64_t col = (int64_t)st * BKS + gg * S::CPI + lcol;
+        const T* src = isB ? (B + lrow + col * ldb) : (A + lrow + col * lda);
+        __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(buf + g * S::SRP),
+                                         16, 0, 0);
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ void tile_mma2(typename Mfma<T>::acc_t (&acc1)[2][4], typename Mfma<T>::acc_t (&acc2)[2][4],
+                                          const T* __restrict__ A, int64_t lda, const T* __restrict__ B, int64_t ldb,
+                                          int K1, int K2, T* smem, const int t) {
+    typedef Mfma<T> Tr;
+    typedef typename Tr::acc_t acc_t;
+    typedef Stage<T> S;
+    const int lane = t & 63, w = t >> 6;
+    const int wr = w & 1, wc = w >> 1;
+    const int lr = lane & 15, lk = lane >> 4;
+    auto issue = [&](int st) { ring_issue<T>(A, lda, B, ldb, st, smem, t); };
+#pragma unroll
+    for (int x = 0; x < 2; x++)
+#pragma unroll
+        for (int y = 0; y < 4; y++) {
+            acc1[x][y] = acc_t{0};
+            acc2[x][y] = acc_t{0};
+        }
+    const int nst1 = __builtin_amdgcn_readfirstlane(K1) / BKS;
+    const int nst = nst1 + __builtin_amdgcn_readfirstlane(K2) / BKS;
+#pragma unroll
+    for (int p = 0; p < AHEAD; p++)
+        if (p < nst) issue(p);
+    auto stage_sync = [&](int st) {
+        const int ahead = nst - 1 - st;
+        if (AHEAD >= 3 && ahead >= 2) wait_vm<(AHEAD >= 3 ? 2 : 0) * S::IPW>();
+        else if (AHEAD >= 2 && ahead >= 1) wait_vm<S::IPW>();
+        else wait_vm<0>();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (st + AHEAD < nst) issue(st + AHEAD);
+    };
+    const T* a0 = smem;
+    const T* b0 = smem + S::GRP * S::SRP;
+    // one loop per accumulator set (a run-time choice inside one loop would merge them)
+    auto stages = [&](acc_t(&acc)[2][4], int sbeg, int send) {
+#pragma nounroll
+        for (int st = sbeg; st < send; st++) {
+            stage_sync(st);
+            const T* a = a0 + (st % NBUF) * S::STG;
+            const T* b = b0 + (st % NBUF) * S::STG;
+            T fa[2][4], fb[2][2];
+            auto frag = [&](int kq, int r) {
+                const int kr = kq * 4 + lk;
+                const int ko = (kr / S::CPI) * S::SRP + (kr % S::CPI) * GT;
+#pragma unroll
+                for (int x = 0; x < 2; x++) fb[r][x] = b[ko + wc * 32 + x * 16 + lr];
+#pragma unroll
+                for (int y = 0; y < 4; y++) fa[r][y] = a[ko + wr * 64 + y * 16 + lr];
+            };
+            frag(0, 0);
+#pragma unroll
+            for (int kq = 0; kq < BKS / 4; kq++) {
+                if (kq + 1 < BKS / 4) frag(kq + 1, (kq + 1) & 1);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int x = 0; x < 2; x++)
+#pragma unroll
+                    for (int y = 0; y < 4; y++) acc[x][y] = Tr::mma(fb[kq & 1][x], fa[kq & 1][y], acc[x][y]);
+            }
+        }
+    };
+    stages(acc1, 0, nst1);
+    stages(acc2, nst1, nst);
+}
+
 }  // namespace mm
 }  // namespace gprx

@@ -90,6 +90,10 @@ template <typename T, int NPER, bool R2>
 __device__ __forceinline__ void block_stats(const T* FU, int64_t nu, int64_t i0, const T* FV, int64_t nv, int64_t j0,
                                             int Kr, int Kp, T* smem, int t, typename Mfma<T>::acc_t (&ar)[2][4],
                                             typename Mfma<T>::acc_t (&ap)[2][4]) {
+    if (R2 && NPER) {  // adjacent column ranges: one pass of the staging ring
+        tile_mma2<T>(ar, ap, FU + i0, nu, FV + j0, nv, Kr, Kp, smem, t);
+        return;
+    }
     if (R2) tile_mma<T>(ar, FU + i0, nu, FV + j0, nv, Kr, Kr, smem, t);
     if (NPER) {
         __syncthreads();  // the second product reuses the staging ring

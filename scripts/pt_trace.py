@@ -27,7 +27,8 @@ if os.environ.get("PT_TRACE_FIT"):  # the C3 fit (fused covariance build) instea
     ms.value = info.ms_factor
     n = ((n + 127) // 128) * 128
 else:
-    assert L.gprx_dev_bench(ctx.h, 1, 9, n, 0, 0, 2, ctypes.byref(ms)) == 0
+    dt = int(os.environ.get("PT_TRACE_DTYPE", "1"))  # 1: f64, 0: f32 (gprx_dtype)
+    assert L.gprx_dev_bench(ctx.h, dt, 9, n, 0, 0, 2, ctypes.byref(ms)) == 0
 MAX = 400000
 tasks = np.zeros((MAX, 4), np.int32)
 times = np.zeros((MAX, 4), np.int64)
