@@ -572,7 +572,7 @@ struct Cost {  // per-task durations (us, one CU), calibrated from GPRX_PT_TRACE
     double k128 = 17.1;  // per 128-deep slice of a full tile update
     double ovh = 6.5;    // per update task: ticket, waits, fences, C read-modify-write
     double trsm = 20.4;  // TRSM tile
-    double diagx = 106.0;  // DIAGX(k > 0): trsm tile + syrk tile + 128x128 factor/inverse
+    double diagx = 96.0;   // DIAGX(k > 0): trsm tile + syrk tile + 128x128 factor/inverse (r01i trace)
     double diag0 = 70.0;   // DIAGX(0): factor/inverse only
     double early = 20.0;   // DIAGX(k) publishes L_{k,k-1} after its trsm phase
     double diagf = 0.97;   // diagonal-tile update relative to a full one (2 of 8 waves idle)
@@ -776,8 +776,11 @@ static Schedule make_schedule(int nc, int nr, int W, int near, int P, const Cost
 }
 
 struct Params {
-    int W = 32, near = 1;
+    // r01i sweep (scripts/sched_sweep.sh): at N = 16384 W = 64 with no single-panel tail is
+    // 1.6-2.0% faster than W = 32, near = 1; at N = 4096 (chain-bound) near = 1 stays 6% faster
+    int W = 64, near = -1;  // near < 0: by size (near_for)
     Cost cm;
+    int near_for(int nc) const { return near >= 0 ? near : (nc <= 64 ? 1 : 0); }
     Params() {
         if (const char* e = std::getenv("GPRX_PT_W")) W = std::max(1, std::atoi(e));
         if (const char* e = std::getenv("GPRX_PT_NEAR")) near = std::max(0, std::atoi(e));
@@ -884,7 +887,7 @@ void potrf_tiles(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info
     auto it = st.sched.find(key);
     if (it == st.sched.end()) {
         const Params& pr = params();
-        Schedule S = make_schedule(nc, nr, pr.W, pr.near, st.ncu, pr.cm, fused, ni);
+        Schedule S = make_schedule(nc, nr, pr.W, pr.near_for(nc), st.ncu, pr.cm, fused, ni);
         PtState::Dev d;
         d.n = (int64_t)S.list.size();
         d.est_us = S.est_us;
@@ -980,7 +983,7 @@ int64_t potrf_tiles_schedule_stats(int nc, int nr, int P, bool build, double* es
     if (nc < 1 || nr < nc || P < 1 || ni < 0 || ni > nr - nc)
         throw Error{GPRX_ERR_ARG, "potrf tile schedule: need nc >= 1, nr >= nc + ni, P >= 1"};
     const pt::Params& pr = pt::params();
-    pt::Schedule S = pt::make_schedule(nc, nr, pr.W, pr.near, P, pr.cm, build, ni);
+    pt::Schedule S = pt::make_schedule(nc, nr, pr.W, pr.near_for(nc), P, pr.cm, build, ni);
     if (est_us) *est_us = S.est_us;
     return S.ntasks;
 }

@@ -20,10 +20,18 @@ def _sched(nc, nr, P=256, build=False, ident=False):
     return st, n.value, est.value
 
 
-def _expected_tasks(nc, nr, W=32, near=1):
+W_DEF = 64  # k_ptiles.hip Params defaults: update chunk width, single-panel tail by size
+
+
+def near_def(nc):
+    return 1 if nc <= 64 else 0
+
+
+def _expected_tasks(nc, nr, W=W_DEF, near=None):
     """Task count of the chunking rule (k_ptiles.hip tile_chunks): W-aligned chunks up to the
     last multiple of W at or before column j, then power-of-two pieces before the last `near`
     panels, then single panels."""
+    near = near_def(nc) if near is None else near
     diag = nc
     trsm = sum(1 for k in range(nc) for i in range(k + 1, nr) if not (i == k + 1 and i < nc))
     upd = 0
@@ -72,7 +80,7 @@ def test_schedule_with_identity_rows(nc, extra):
     nr = nc + extra + nc
     st, n, est = _sched(nc, nr, build=False, ident=True)
     assert st == 0, "ticket order violates a dependency"
-    W, near = 32, 1
+    W, near = W_DEF, near_def(nc)
     extra_tasks = 0
     for a in range(nc):
         extra_tasks += nc - a  # TRSM(nr0 + a, k) for k = a .. nc - 1
