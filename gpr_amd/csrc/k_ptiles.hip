@@ -571,7 +571,7 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
 struct Cost {  // per-task durations (us, one CU), calibrated from GPRX_PT_TRACE timelines
     double k128 = 17.1;  // per 128-deep slice of a full tile update
     double ovh = 6.5;    // per update task: ticket, waits, fences, C read-modify-write
-    double trsm = 20.4;  // TRSM tile
+    double trsm = 16.0;  // TRSM tile (r01i trace: 15.9)
     double diagx = 96.0;   // DIAGX(k > 0): trsm tile + syrk tile + 128x128 factor/inverse (r01i trace)
     double diag0 = 70.0;   // DIAGX(0): factor/inverse only
     double early = 20.0;   // DIAGX(k) publishes L_{k,k-1} after its trsm phase
