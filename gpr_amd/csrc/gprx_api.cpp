@@ -839,7 +839,10 @@ static gprx_status sparse_fit_impl(gprx_ctx* ctx, const gprx_kernel_desc* desc, 
     // split-K partials: tiles x partials workgroups in whole rounds of the chip's slots (one
     // tile-mainloop workgroup per CU).  M = 2048: 152 tiles; P = 5 fills 3 rounds to 99% (an
     // earlier P = 7 on two slots per CU left the third round 4% full).
-    const int64_t ntiles = (Mp / GT) * (Mp / GT + 1) / 2 + (mp / GT) * (Mp / GT);
+    // fused: one label column (m = 1) with the MFMA cross build -- K Y comes out of the build's
+    // epilogue (kcross_mma_kernel), so the rank-k accumulation has no 128-row label tile
+    const bool fused = mma && m == 1;
+    const int64_t ntiles = (Mp / GT) * (Mp / GT + 1) / 2 + (fused ? 0 : (mp / GT) * (Mp / GT));
     int ncu = 0;
     GPRX_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
     const int64_t slots = (int64_t)std::max(1, ncu);
@@ -861,6 +864,8 @@ static gprx_status sparse_fit_impl(gprx_ctx* ctx, const gprx_kernel_desc* desc, 
     const int64_t acols = chunk + 16 * 16;  // slack: the P <= 16 split-K slices may overhang ncp (zeros)
     dA.ensure(sizeof(T) * ld * acols);
     const T is2 = T(1) / (T(sigma) * T(sigma));  // inverse_sigma2 in T (:285)
+    DevBuf dKY;
+    if (fused) dKY.ensure(sizeof(T) * (chunk128 / GT) * Mp);
     for (int64_t off = 0; off < n; off += chunk) {
         const int64_t nc = std::min(chunk, n - off), ncp = round_up(nc, 16);
         if (nc < chunk || off == 0) GPRX_HIP(hipMemsetAsync(dA.p, 0, sizeof(T) * ld * acols, s));
@@ -868,7 +873,10 @@ static gprx_status sparse_fit_impl(gprx_ctx* ctx, const gprx_kernel_desc* desc, 
             const int64_t nc128 = round_up(nc, GT);
             launch_pair_features<T>(K, dX.as<T>() + off * d, nc, d, dXm.as<T>(), true, dFV.as<T>(), nc128, s);
             launch_kcross_mma<T>(K, dKd.as<KCanon<T>>(), dFU.as<T>(), Mp, M, dFV.as<T>(), nc128, nc, d, dA.as<T>(), ld,
-                                 dflag.as<int>(), s);
+                                 dflag.as<int>(), s, fused ? dY.as<T>() + off : nullptr,
+                                 fused ? dKY.as<T>() : nullptr);
+            if (fused)  // label row Mp of partial 0, in chunk order
+                launch_ky_reduce<T>(dKY.as<T>(), Mp, (int)(nc128 / GT), M, is2, dS.as<T>(), ld, Mp, s);
         } else {
             const T* tabc = nullptr;
             if (K.nper > 0) {
@@ -878,10 +886,10 @@ static gprx_status sparse_fit_impl(gprx_ctx* ctx, const gprx_kernel_desc* desc, 
             launch_kbuild<T>(K, dXm.as<T>(), dtm.as<T>(), M, dX.as<T>() + off * d, tabc, nc, d, dA.as<T>(), ld, 0,
                              false, T(0), dflag.as<int>(), s);
         }
-        launch_label_rows<T>(dY.as<T>() + off * m, nc, m, dA.as<T>(), ld, Mp, ncp, mp, s);
+        if (!fused) launch_label_rows<T>(dY.as<T>() + off * m, nc, m, dA.as<T>(), ld, Mp, ncp, mp, s);
         const int64_t kpart = round_up((ncp + P - 1) / P, 16);  // zero-padded columns make up the rest
         const int Pc = (int)((ncp + kpart - 1) / kpart);
-        launch_syrk_splitk<T>(dS.as<T>(), ld, sstride, dA.as<T>(), ld, ld, Mp, kpart, Pc, is2, s);
+        launch_syrk_splitk<T>(dS.as<T>(), ld, sstride, dA.as<T>(), ld, fused ? Mp : ld, Mp, kpart, Pc, is2, s);
     }
     launch_sum_partials<T>(dS.as<T>(), sstride, P, s);  // dS[0] += dS[1..P-1]
     if (ctx->comm && ctx->world > 1) {

@@ -298,7 +298,14 @@ void launch_kbuild_mma(const KCanon<T>& K, const KCanon<T>* Kd, const T* FU, con
 // are stored.
 template <typename T>
 void launch_kcross_mma(const KCanon<T>& K, const KCanon<T>* Kd, const T* FU, int64_t nfu, int64_t na, const T* FV,
-                       int64_t nfv, int64_t nb, int d, T* A, int64_t ld, int* flag, hipStream_t s);
+                       int64_t nfv, int64_t nb, int d, T* A, int64_t ld, int* flag, hipStream_t s,
+                       const T* Y = nullptr, T* kyp = nullptr);
+// With Y (one label column of the nb samples of Xb): kyp[c * nfu + i] = the column tile c's
+// part of sum_j K(a_i, b_j) Y[j]; launch_ky_reduce adds alpha times their ordered sum into
+// row row0 of S (column i at S[row0 + i * lds]).
+template <typename T>
+void launch_ky_reduce(const T* kyp, int64_t nfu, int nct, int64_t na, T alpha, T* S, int64_t lds, int64_t row0,
+                      hipStream_t s);
 template <typename T>
 void launch_predict_mma(const KCanon<T>& K, const KCanon<T>* Kd, const T* FU, int64_t nfu, const T* FV, int64_t nfv,
                         int d, const T* alpha, int64_t n, int m, int64_t q, T* mean, hipStream_t s);

@@ -181,11 +181,15 @@ __device__ __forceinline__ bool build_tile(const KCanon<T>* __restrict__ Kd, con
 // Tile (i0, j0) of the cross matrix K(Xa, Xb) into A (column-major, ld): rows from FU (nfu
 // rows, na valid), columns from FV (nfv rows, nb valid); only valid entries are stored.  The
 // sparse fit's Kmn blocks (include/SparseGaussianProcess.h:218-235).
+// With Y (one label column, nb entries): also ky[r] = sum over this tile's columns j of
+// K(a_{i0+r}, b_j) Y[j], r < 128 (rows >= na get 0) -- the sparse fit's Kmn Y without a
+// 128-row label tile in the rank-k accumulation.
 template <typename T, int NPER, bool R2>
 __device__ __forceinline__ bool cross_tile(const KCanon<T>* __restrict__ Kd, const T* __restrict__ FU, int64_t nfu,
                                            int64_t na, const T* __restrict__ FV, int64_t nfv, int64_t nb, int Kr,
                                            int Kp, T hd, T* __restrict__ A, int64_t ld, int64_t i0, int64_t j0,
-                                           T* smem, const int t) {
+                                           T* smem, const int t, const T* __restrict__ Y = nullptr,
+                                           T* __restrict__ ky = nullptr) {
     typedef Mfma<T> Tr;
     const int lane = t & 63, w = t >> 6;
     const int wr = w & 1, wc = w >> 1, lr = lane & 15, lk = lane >> 4;
@@ -200,6 +204,7 @@ __device__ __forceinline__ bool cross_tile(const KCanon<T>* __restrict__ Kd, con
     typename Tr::acc_t ar[2][4], ap[2][4];
     block_stats<T, NPER, R2>(FU, nfu, i0, FV, nfv, j0, Kr, Kp, smem, t, ar, ap);
     bool bad = false;
+    T yacc[4] = {T(0), T(0), T(0), T(0)};
     constexpr int G = 2;
     auto chunk = [&](auto cc) {
         constexpr int x = decltype(cc)::value / (4 / G), h = decltype(cc)::value % (4 / G);
@@ -228,12 +233,32 @@ __device__ __forceinline__ bool cross_tile(const KCanon<T>* __restrict__ Kd, con
                     col[gi] = val;
                 }
             }
+            if (Y) {
+                const T yj = gj < nb ? Y[gj] : T(0);
+#pragma unroll
+                for (int y = 0; y < 4; y++) yacc[y] = fma(v[(reg - G * h) * 4 + y], yj, yacc[y]);
+            }
         }
     };
     chunk(std::integral_constant<int, 0>{});
     chunk(std::integral_constant<int, 1>{});
     chunk(std::integral_constant<int, 2>{});
     chunk(std::integral_constant<int, 3>{});
+    if (Y) {
+        // rows 64 wr + 16 y + lr: over the lane groups lk (shuffles), then the 4 column waves
+        // wc (LDS, in a fixed order); the staging ring is free once every wave is past it
+        __syncthreads();
+        T* red = smem;  // [4 wc][128 rows]
+#pragma unroll
+        for (int y = 0; y < 4; y++) {
+            T v = yacc[y];
+            v += __shfl_xor(v, 16);
+            v += __shfl_xor(v, 32);
+            if (lk == 0) red[wc * GT + wr * 64 + y * 16 + lr] = v;
+        }
+        __syncthreads();
+        if (t < GT) ky[t] = (i0 + t < na) ? ((red[t] + red[GT + t]) + (red[2 * GT + t] + red[3 * GT + t])) : T(0);
+    }
     return bad;
 }
 

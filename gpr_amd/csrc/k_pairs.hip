@@ -86,12 +86,38 @@ template <typename T, int NPER, bool R2>
 __global__ __launch_bounds__(NT) void kcross_mma_kernel(const KCanon<T>* __restrict__ Kd, const T* __restrict__ FU,
                                                         int64_t nfu, int64_t na, const T* __restrict__ FV, int64_t nfv,
                                                         int64_t nb, int Kr, int Kp, T hd, T* __restrict__ A, int64_t ld,
-                                                        int* __restrict__ flag) {
+                                                        int* __restrict__ flag, const T* __restrict__ Y,
+                                                        T* __restrict__ kyp) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     T* smem = reinterpret_cast<T*>(smem_raw);
+    // kyp: per column tile, the tile rows' partial K Y (nfu entries per column tile)
+    T* ky = Y ? kyp + (int64_t)blockIdx.y * nfu + (int64_t)blockIdx.x * GT : nullptr;
     const bool bad = cross_tile<T, NPER, R2>(Kd, FU, nfu, na, FV, nfv, nb, Kr, Kp, hd, A, ld, (int64_t)blockIdx.x * GT,
-                                             (int64_t)blockIdx.y * GT, smem, threadIdx.x);
+                                             (int64_t)blockIdx.y * GT, smem, threadIdx.x, Y, ky);
     if (bad) atomicOr(flag, 1);
+}
+
+// S[row0 + 0, i] += alpha sum_{c < nct} kyp[c * nfu + i] for i < na (the label row of the
+// sparse normal equations).  256 threads = 16 rows x 16 column-tile groups: group q sums
+// c = q, q + 16, ... (rows in consecutive lanes: coalesced), then the 16 group sums are added
+// in order through LDS -- a fixed summation order, so repeated fits agree bit for bit.
+template <typename T>
+__global__ __launch_bounds__(256) void ky_reduce_kernel(const T* __restrict__ kyp, int64_t nfu, int nct, int64_t na,
+                                                        T alpha, T* __restrict__ S, int64_t lds, int64_t row0) {
+    __shared__ T sh[16][17];
+    const int r = threadIdx.x & 15, q = threadIdx.x >> 4;
+    const int64_t i = (int64_t)blockIdx.x * 16 + r;
+    T v = 0;
+    if (i < na)
+        for (int c = q; c < nct; c += 16) v += kyp[(int64_t)c * nfu + i];
+    sh[q][r] = v;
+    __syncthreads();
+    if (q == 0 && i < na) {
+        T t = 0;
+#pragma unroll
+        for (int u = 0; u < 16; u++) t += sh[u][r];
+        S[row0 + i * lds] += alpha * t;
+    }
 }
 
 // mean[q][r] = sum_j k(xq_q, x_j) alpha[j][r], r < m <= PM, one workgroup per 128 queries
@@ -472,13 +498,23 @@ void launch_kbuild_mma(const KCanon<T>& K, const KCanon<T>* Kd, const T* FU, con
 
 template <typename T>
 void launch_kcross_mma(const KCanon<T>& K, const KCanon<T>* Kd, const T* FU, int64_t nfu, int64_t na, const T* FV,
-                       int64_t nfv, int64_t nb, int d, T* A, int64_t ld, int* flag, hipStream_t s) {
+                       int64_t nfv, int64_t nb, int d, T* A, int64_t ld, int* flag, hipStream_t s, const T* Y,
+                       T* kyp) {
     GPRX_REQUIRE(nfu % GT == 0 && nfv % GT == 0 && na <= nfu && nb <= nfv && ld >= nfu, GPRX_ERR_ARG,
                  "launch_kcross_mma: feature rows must be multiples of 128 covering the samples");
     const int Kr = pr::kr_of(K, d), Kp = pr::kp_of(K, d);
     const dim3 grid((unsigned)(nfu / GT), (unsigned)(nfv / GT));
     ProfScope ps(KC_BUILD, s, 2.0 * (double)nfu * nfv * (Kr + Kp), (double)sizeof(T) * (double)na * nb);
-    GPRX_PAIRS_DISPATCH(kcross_mma_kernel, Kd, FU, nfu, na, FV, nfv, nb, Kr, Kp, T(0.5) * T(d), A, ld, flag);
+    GPRX_PAIRS_DISPATCH(kcross_mma_kernel, Kd, FU, nfu, na, FV, nfv, nb, Kr, Kp, T(0.5) * T(d), A, ld, flag, Y, kyp);
+    GPRX_HIP(hipGetLastError());
+}
+
+template <typename T>
+void launch_ky_reduce(const T* kyp, int64_t nfu, int nct, int64_t na, T alpha, T* S, int64_t lds, int64_t row0,
+                      hipStream_t s) {
+    if (na <= 0) return;
+    hipLaunchKernelGGL(pr::ky_reduce_kernel<T>, dim3((unsigned)((na + 15) / 16)), dim3(256), 0, s, kyp, nfu, nct, na,
+                       alpha, S, lds, row0);
     GPRX_HIP(hipGetLastError());
 }
 
@@ -579,7 +615,8 @@ TileBuild<T> pairs_tile_build(const KCanon<T>& K, const KCanon<T>* Kd, const T* 
     template void launch_kbuild_mma<T>(const KCanon<T>&, const KCanon<T>*, const T*, const T*, int64_t, int, T*,    \
                                        int64_t, int64_t, T, int*, hipStream_t);                               \
     template void launch_kcross_mma<T>(const KCanon<T>&, const KCanon<T>*, const T*, int64_t, int64_t, const T*,  \
-                                       int64_t, int64_t, int, T*, int64_t, int*, hipStream_t);                  \
+                                       int64_t, int64_t, int, T*, int64_t, int*, hipStream_t, const T*, T*);   \
+    template void launch_ky_reduce<T>(const T*, int64_t, int, int64_t, T, T*, int64_t, int64_t, hipStream_t);   \
     template void launch_predict_mma<T>(const KCanon<T>&, const KCanon<T>*, const T*, int64_t, const T*, int64_t, \
                                         int, const T*, int64_t, int, int64_t, T*, hipStream_t);
 GPRX_PAIRS_INST(double)
