@@ -281,7 +281,7 @@ __device__ __forceinline__ void diag_factor(T* __restrict__ A, int64_t ld, T* __
 #pragma unroll
                     for (int b = 0; b < 8; b++) S[a][b] = T(0);
             }
-#pragma unroll 2
+#pragma unroll
             for (int q = 0; q < 8; q++) {
                 T u[4], v[8];
 #pragma unroll
