@@ -197,18 +197,23 @@ __device__ __forceinline__ void diag_factor(T* __restrict__ A, int64_t ld, T* __
     for (int j0 = 0; j0 < DB; j0 += 8) {
         const int jn = j0 + 8;
         if (t < DB) {
-            // every lane of waves 0-1 factors the pivot (identical values) into its wave's own
-            // LDS copy, so the row solve reads it back instead of holding it next to S
+            // every lane of waves 0-1 factors the pivot (identical values) in registers and
+            // solves its row with it; wave 0 also leaves the factor in LDS for the pivot rows
             T(*myLd)[9] = sLdW[w];
+            const int row = t;
+            const bool piv = row >= j0 && row < jn;
+            T x[8];
             {
-                // the whole pivot block is read up front (one LDS latency instead of one per
-                // column: the compiler cannot move these reads above the myLd stores), the
+                // the whole pivot block and this row's segment are read up front (one LDS
+                // latency: the compiler cannot move these reads above the myLd stores), the
                 // factor runs in place in registers, and the stores follow in one branch
-                T Ld[8][8], ri[8];
+                T Ld[8][8], ri[8], vr[8];
 #pragma unroll
                 for (int c = 0; c < 8; c++)
 #pragma unroll
                     for (int r = c; r < 8; r++) Ld[r][c] = sV[c][j0 + r];
+#pragma unroll
+                for (int q = 0; q < 8; q++) vr[q] = sV[q][row];
 #pragma unroll
                 for (int c = 0; c < 8; c++) {
                     T dsum = Ld[c][c];
@@ -234,16 +239,13 @@ __device__ __forceinline__ void diag_factor(T* __restrict__ A, int64_t ld, T* __
                         for (int r = c; r < 8; r++) myLd[r][c] = Ld[r][c];
                     }
                 }
-            }
-            const int row = t;
-            const bool piv = row >= j0 && row < jn;
-            T x[8];
 #pragma unroll
-            for (int q = 0; q < 8; q++) {
-                T v = piv ? ((row - j0 == q) ? T(1) : T(0)) : sV[q][row];
+                for (int q = 0; q < 8; q++) {
+                    T v = piv ? ((row - j0 == q) ? T(1) : T(0)) : vr[q];
 #pragma unroll
-                for (int q2 = 0; q2 < q; q2++) v = fma(-x[q2], myLd[q][q2], v);
-                x[q] = v * myLd[q][8];
+                    for (int q2 = 0; q2 < q; q2++) v = fma(-x[q2], Ld[q][q2], v);
+                    x[q] = v * ri[q];
+                }
             }
 #pragma unroll
             for (int q = 0; q < 8; q++) sP[q][row] = x[q];
