@@ -15,7 +15,7 @@ HDRS     := $(wildcard gpr_amd/csrc/*.h) include/gprx.h
 
 HOST_SRCS := $(wildcard gpr_amd/host/*.cpp)
 HOST_HDRS := $(wildcard include/gpr/*.h) include/gprx.h
-CXXFLAGS  ?= -O2 -std=c++17 -fPIC -Wall -Iinclude
+CXXFLAGS  ?= -O2 -std=c++17 -fPIC -Wall -pthread -Iinclude
 CPPTESTS  := $(LIBDIR)/gp_host_test $(LIBDIR)/host_cpu_test
 
 all: $(LIBDIR)/libgprx.so $(LIBDIR)/libgpr_amd.so cpptests oracle

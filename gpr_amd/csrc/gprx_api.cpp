@@ -11,6 +11,7 @@
 #include <limits>
 #include <mutex>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "gprx_internal.h"
@@ -243,7 +244,21 @@ struct gprx_model {
     KCanon<double> kd{};
     KCanon<float> kf{};
     DevBuf X, Y, tab, A, Linv, z, alpha, info, flag, red, V, C, scratch1, scratch2, grad, pack, featU, featV, kdev;
+    // fp32 models: fp64 iterative refinement state (k_refine.hip).  kd then holds the tree in
+    // double with the parameters rounded to float first (the reference stores them in T).
+    DevBuf Xd, Yd, ad, kxd, fud, fvd, kdev64, tabd, zd, outd, delta, nrm;
     std::mutex mu;
+};
+
+// Every model call holds its context's mutex, then the model's (always in that order): the
+// device work of a model runs on the context's streams and uses the context's scratch (the
+// tile factorisation's ticket and counter words, its cached schedules, the timing events),
+// so two models of one context must not interleave their launches -- a second fit's memset
+// of the ticket counter landing between another fit's memset and launch leaves that launch
+// with a spent ticket.  Calls on one model from several threads are serialised as well.
+struct ModelLock {
+    std::lock_guard<std::mutex> c, m;
+    explicit ModelLock(gprx_model* M) : c(M->ctx->mu), m(M->mu) {}
 };
 
 // ---------------------------------------------------------------------------------------
@@ -279,6 +294,96 @@ const KCanon<double>& kcanon<double>(const gprx_model* m) {
 template <>
 const KCanon<float>& kcanon<float>(const gprx_model* m) {
     return m->kf;
+}
+
+// ---------------------------------------------------------------------------------------
+// fp64 iterative refinement of an fp32 fit (k_refine.hip): alpha_d += (L L^T)^{-1}
+// (Y - (K + s2 I) alpha_d) with K evaluated in fp64 (pair statistics of the fp64-widened
+// samples, the predict path with the training set as the queries) and the correction solved
+// with the fp32 factor already in A (forward solve of the residual written into the label
+// rows, back substitution).  Stops when the correction is below fp32 resolution of alpha.
+// ---------------------------------------------------------------------------------------
+static void download(void* host, const void* dev, size_t bytes, hipStream_t s);
+
+static void refine_f32(gprx_model* M, gprx_fit_info* out) {
+    gprx_ctx* ctx = M->ctx;
+    hipStream_t s = ctx->stream;
+    const KCanon<double>& K = M->kd;
+    const int64_t n = M->n, np = M->np, mp = M->mp, ld = M->ld;
+    const int d = M->d, m = M->m;
+    int steps = 3;
+    if (const char* e = std::getenv("GPRX_REFINE_STEPS")) steps = std::max(0, std::atoi(e));
+    GPRX_HIP(hipEventRecord(ctx->ev[0], s));
+    M->Xd.ensure(sizeof(double) * n * d);
+    M->Yd.ensure(sizeof(double) * n * m);
+    M->ad.ensure(sizeof(double) * n * m);
+    M->kxd.ensure(sizeof(double) * n * m);
+    M->delta.ensure(sizeof(float) * np * m);
+    M->nrm.ensure(2 * sizeof(unsigned long long));
+    launch_convert<float, double>(M->X.as<float>(), M->Xd.as<double>(), n * d, s);
+    launch_convert<float, double>(M->Y.as<float>(), M->Yd.as<double>(), n * m, s);
+    launch_convert<float, double>(M->alpha.as<float>(), M->ad.as<double>(), n * m, s);
+    const bool mma = pairs_mma_supported<double>(K, 1);
+    if (mma) {
+        const int64_t kf = pairs_feature_cols<double>(K, d);
+        M->fud.ensure(sizeof(double) * np * kf);
+        M->fvd.ensure(sizeof(double) * np * kf);
+        launch_pair_features<double>(K, M->Xd.as<double>(), n, d, M->Xd.as<double>(), false, M->fud.as<double>(), np, s);
+        launch_pair_features<double>(K, M->Xd.as<double>(), n, d, M->Xd.as<double>(), true, M->fvd.as<double>(), np, s);
+        M->kdev64.ensure(sizeof(KCanon<double>));
+        GPRX_HIP(hipMemcpyAsync(M->kdev64.p, &K, sizeof(KCanon<double>), hipMemcpyHostToDevice, s));
+    } else {
+        if (K.nper > 0) {
+            M->tabd.ensure(sizeof(double) * 2 * K.nper * n * d);
+            launch_sincos_tables<double>(K, M->Xd.as<double>(), n, d, M->tabd.as<double>(), s);
+        }
+        M->zd.ensure(sizeof(double) * n * m);
+        M->outd.ensure(sizeof(double) * n * m);
+    }
+    const float sf = (float)M->sigma;
+    const double s2 = (double)(sf * sf);  // m_Sigma * m_Sigma in T (lib/GaussianProcess.cpp:379)
+    double rel = 0;
+    int taken = 0;
+    for (int it = 0; it < steps; it++) {
+        if (mma) {
+            for (int c = 0; c < m; c++)  // one label column per launch (alpha, Kx strided by m)
+                launch_predict_mma<double>(K, M->kdev64.as<KCanon<double>>(), M->fud.as<double>(), np,
+                                           M->fvd.as<double>(), np, d, M->ad.as<double>() + c, n, m, n,
+                                           M->kxd.as<double>() + c, s);
+        } else {
+            launch_predict<double>(K, M->Xd.as<double>(), M->tabd.as<double>(), n, d, m, M->ad.as<double>(),
+                                   M->Xd.as<double>(), M->tabd.as<double>(), n, M->kxd.as<double>(), nullptr,
+                                   M->zd.as<double>(), M->outd.as<double>(), s);
+        }
+        launch_residual_rows(M->Yd.as<double>(), M->kxd.as<double>(), M->ad.as<double>(), s2, n, m,
+                             M->A.as<float>(), ld, np, np, (int)mp, s);
+        trsm_rows<float>(M->A.as<float>(), ld, np, M->Linv.as<float>(), M->A.as<float>() + np, ld, mp, s);
+        GPRX_HIP(hipMemsetD32Async((hipDeviceptr_t)M->info.p, INT_MAX, 1, s));
+        launch_backsolve_chain<float>(M->A.as<float>(), ld, np, m, M->Linv.as<float>(), M->delta.as<float>(),
+                                      M->info.as<int>(), ctx->ex, s);
+        launch_refine_accumulate(M->delta.as<float>(), M->ad.as<double>(), M->alpha.as<float>(), n * m,
+                                 M->nrm.as<unsigned long long>(), s);
+        unsigned long long h[2];
+        int hinfo = 0;
+        download(h, M->nrm.p, sizeof(h), s);
+        download(&hinfo, M->info.p, sizeof(int), s);
+        check_sched(hinfo);
+        double dn, an;
+        std::memcpy(&dn, &h[0], sizeof(double));
+        std::memcpy(&an, &h[1], sizeof(double));
+        rel = an > 0 ? dn / an : dn;
+        taken = it + 1;
+        if (!(rel > 0x1p-26)) break;  // below fp32 resolution of alpha (NaN: stop too)
+    }
+    GPRX_HIP(hipEventRecord(ctx->ev[1], s));
+    GPRX_HIP(hipEventSynchronize(ctx->ev[1]));
+    if (out) {
+        float ms = 0;
+        hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[1]);
+        out->ms_refine = ms;
+        out->refine_delta = rel;
+        out->refine_steps = taken;
+    }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -333,7 +438,8 @@ static gprx_status model_fit(gprx_model* M, uint32_t flags, gprx_fit_info* out) 
         const int64_t kf = pairs_feature_cols<T>(K, M->d);
         M->featU.ensure(sizeof(T) * np * kf);
         M->featV.ensure(sizeof(T) * np * kf);
-        launch_pair_features<T>(K, M->X.as<T>(), n, M->d, M->X.as<T>(), false, M->featU.as<T>(), np, s);
+        launch_pair_features<T>(K, M->X.as<T>(), n, M->d, M->X.as<T>(), false, M->featU.as<T>(), np, s,
+                                M->flag.as<int>());
         launch_pair_features<T>(K, M->X.as<T>(), n, M->d, M->X.as<T>(), true, M->featV.as<T>(), np, s);
         M->kdev.ensure(sizeof(KCanon<T>));
         GPRX_HIP(hipMemcpyAsync(M->kdev.p, &K, sizeof(KCanon<T>), hipMemcpyHostToDevice, s));
@@ -436,6 +542,13 @@ static gprx_status model_fit(gprx_model* M, uint32_t flags, gprx_fit_info* out) 
     M->fitted = true;
     M->has_alpha = true;
     M->inv_ready = want_inv;
+    if constexpr (std::is_same<T, float>::value) {
+        // the reference inverts fp32 GPs in double (include/LAPACKUtils.h:85-97): refine alpha
+        // in fp64 against the fp32 factor.  Not for the LML's fit (its value and gradient come
+        // from the factor and its inverse) nor the distributed path (replicated factor, local
+        // solve: a refinement there is a later step).
+        if (!(flags & GPRX_FIT_F32_NO_REFINE) && !want_inv && !dist) refine_f32(M, out);
+    }
     return GPRX_OK;
 }
 
@@ -761,6 +874,63 @@ static gprx_status cholesky_impl(gprx_ctx* ctx, void* Ahost, int64_t n, int32_t*
     return GPRX_OK;
 }
 
+// gprx_dev_build_matrix: the fit's covariance tiles, written alone (include/gprx_dev.h)
+template <typename T>
+static gprx_status dev_build_impl(gprx_ctx* ctx, const gprx_kernel_desc* desc, const void* X, int64_t n, int d,
+                                  double sigma, int path, void* Kout) {
+    KCanon<T> K;
+    std::string e = canonicalize<T>(*desc, K);
+    GPRX_REQUIRE(e.empty(), GPRX_ERR_ARG, e);
+    GPRX_REQUIRE(n > 0 && d > 0, GPRX_ERR_DIM, "gprx_dev_build_matrix: bad dimensions");
+    GPRX_REQUIRE(pairs_mma_supported<T>(K, 1), GPRX_ERR_ARG,
+                 "gprx_dev_build_matrix: the tree takes the direct (VALU) build, see gprx_kernel_matrix");
+    hipStream_t s = ctx->stream;
+    const int64_t np = round_up(n, GT), kf = pairs_feature_cols<T>(K, d);
+    DevBuf dx, fu, fv, kd, A, Li, info, flag;
+    upload<T>(dx, X, sizeof(T) * n * d, s);
+    fu.ensure(sizeof(T) * np * kf);
+    fv.ensure(sizeof(T) * np * kf);
+    kd.ensure(sizeof(KCanon<T>));
+    flag.ensure(sizeof(int));
+    info.ensure(sizeof(int));
+    A.ensure(sizeof(T) * np * np);
+    Li.ensure(sizeof(T) * np * DB);
+    GPRX_HIP(hipMemsetAsync(flag.p, 0, sizeof(int), s));
+    GPRX_HIP(hipMemsetAsync(A.p, 0, sizeof(T) * np * np, s));
+    GPRX_HIP(hipMemsetD32Async((hipDeviceptr_t)info.p, INT_MAX, 1, s));
+    launch_pair_features<T>(K, dx.as<T>(), n, d, dx.as<T>(), false, fu.as<T>(), np, s, flag.as<int>());
+    launch_pair_features<T>(K, dx.as<T>(), n, d, dx.as<T>(), true, fv.as<T>(), np, s);
+    GPRX_HIP(hipMemcpyAsync(kd.p, &K, sizeof(KCanon<T>), hipMemcpyHostToDevice, s));
+    const T sig = (T)sigma, sigma2 = sig * sig;
+    if (path == 0) {
+        TileBuild<T> tb = pairs_tile_build<T>(K, kd.as<KCanon<T>>(), fu.as<T>(), fv.as<T>(), np, d, n, sigma2,
+                                              flag.as<int>());
+        GPRX_REQUIRE(tb.mode != 0, GPRX_ERR_ARG,
+                     "gprx_dev_build_matrix: the fused build carries sum-of-exp-leaf trees only (path 1 for others)");
+        potrf_tiles<T>(A.as<T>(), np, np, np, Li.as<T>(), info.as<int>(), ctx->ex, &tb, 0, true);
+    } else {
+        launch_kbuild_mma<T>(K, kd.as<KCanon<T>>(), fu.as<T>(), fv.as<T>(), np, d, A.as<T>(), np, n, sigma2,
+                             flag.as<int>(), s);
+    }
+    std::vector<T> h((size_t)np * n);
+    download(h.data(), A.p, sizeof(T) * np * n, s);
+    int hf = 0, hinfo = 0;
+    download(&hf, flag.p, sizeof(int), s);
+    download(&hinfo, info.p, sizeof(int), s);
+    check_sched(hinfo);
+    T* out = reinterpret_cast<T*>(Kout);
+    for (int64_t j = 0; j < n; j++)
+        for (int64_t i = j; i < n; i++) {
+            const T v = h[(size_t)j * np + i];  // column-major, lower triangle
+            out[(size_t)i * n + j] = v;
+            out[(size_t)j * n + i] = v;
+        }
+    if (hf)
+        throw Error{GPRX_ERR_NONFINITE,
+                    "GaussianProcess::ComputeKernelMatrixInternal: kernel matrix contains entries which are not finite."};
+    return GPRX_OK;
+}
+
 // ---------------------------------------------------------------------------------------
 // sparse GP (subset of regressors), SparseGaussianProcess::PreComputeRegression
 // (include/SparseGaussianProcess.h:274-313):
@@ -819,22 +989,22 @@ static gprx_status sparse_fit_impl(gprx_ctx* ctx, const gprx_kernel_desc* desc, 
     // the inducing points once, of each dense chunk per chunk, both centred on Xm's first row
     const bool mma = pairs_mma_supported<T>(K, 1);
     const int64_t chunk128 = round_up(chunk, GT);
+    dflag.ensure(sizeof(int));
+    GPRX_HIP(hipMemsetAsync(dflag.p, 0, sizeof(int), s));
     if (mma) {
         const int64_t fc = pairs_feature_cols<T>(K, d);
         dKd.ensure(sizeof(KCanon<T>));
         GPRX_HIP(hipMemcpyAsync(dKd.p, &K, sizeof(KCanon<T>), hipMemcpyHostToDevice, s));
         dFU.ensure(sizeof(T) * Mp * fc);
         dFV.ensure(sizeof(T) * chunk128 * fc);
-        launch_pair_features<T>(K, dXm.as<T>(), M, d, dXm.as<T>(), false, dFU.as<T>(), Mp, s);
+        launch_pair_features<T>(K, dXm.as<T>(), M, d, dXm.as<T>(), false, dFU.as<T>(), Mp, s, dflag.as<int>());
     }
     if (K.nper > 0) {
         dtm.ensure(sizeof(T) * 2 * K.nper * M * d);  // Kmm below
         launch_sincos_tables<T>(K, dXm.as<T>(), M, d, dtm.as<T>(), s);
         if (!mma) dtx.ensure(sizeof(T) * 2 * K.nper * chunk * d);  // per-chunk tables of the dense rows
     }
-    dflag.ensure(sizeof(int));
     dinfo.ensure(sizeof(int));
-    GPRX_HIP(hipMemsetAsync(dflag.p, 0, sizeof(int), s));
     // ---- accumulate sigma^-2 [Kmn ; Y^T][Kmn ; Y^T]^T over the dense rows (lower part) ----
     // split-K partials: tiles x partials workgroups in whole rounds of the chip's slots (one
     // tile-mainloop workgroup per CU).  M = 2048: 152 tiles; P = 5 fills 3 rounds to 99% (an
@@ -871,7 +1041,8 @@ static gprx_status sparse_fit_impl(gprx_ctx* ctx, const gprx_kernel_desc* desc, 
         if (nc < chunk || off == 0) GPRX_HIP(hipMemsetAsync(dA.p, 0, sizeof(T) * ld * acols, s));
         if (mma) {
             const int64_t nc128 = round_up(nc, GT);
-            launch_pair_features<T>(K, dX.as<T>() + off * d, nc, d, dXm.as<T>(), true, dFV.as<T>(), nc128, s);
+            launch_pair_features<T>(K, dX.as<T>() + off * d, nc, d, dXm.as<T>(), true, dFV.as<T>(), nc128, s,
+                                    dflag.as<int>());
             launch_kcross_mma<T>(K, dKd.as<KCanon<T>>(), dFU.as<T>(), Mp, M, dFV.as<T>(), nc128, nc, d, dA.as<T>(), ld,
                                  dflag.as<int>(), s, fused ? dY.as<T>() + off : nullptr,
                                  fused ? dKY.as<T>() : nullptr);
@@ -1052,7 +1223,7 @@ gprx_status gprx_model_set_data(gprx_model* M, const void* X, const void* Y, int
     GPRX_REQUIRE(M && X && Y, GPRX_ERR_ARG, "gprx_model_set_data: NULL argument");
     GPRX_REQUIRE(n > 0, GPRX_ERR_STATE, "GaussianProcess::Initialize: no input samples defined during initialization");
     GPRX_REQUIRE(d > 0 && m > 0, GPRX_ERR_DIM, "gprx_model_set_data: input and output dimensions must be positive");
-    std::lock_guard<std::mutex> lk(M->mu);
+    ModelLock lk(M);
     GPRX_HIP(hipSetDevice(ctx->device));
     const size_t es = esize(M->dt);
     M->X.ensure(es * n * d);
@@ -1074,9 +1245,16 @@ gprx_status gprx_model_set_kernel(gprx_model* M, const gprx_kernel_desc* k) {
     gprx_ctx* ctx = M ? M->ctx : nullptr;
     API_BEGIN
     GPRX_REQUIRE(M && k, GPRX_ERR_ARG, "gprx_model_set_kernel: NULL argument");
-    std::lock_guard<std::mutex> lk(M->mu);
+    ModelLock lk(M);
     std::string e = (M->dt == GPRX_F64) ? canonicalize<double>(*k, M->kd) : canonicalize<float>(*k, M->kf);
     GPRX_REQUIRE(e.empty(), GPRX_ERR_ARG, e);
+    if (M->dt == GPRX_F32) {  // the fp64 form of the fp32 tree (its parameters rounded to float)
+        gprx_kernel_desc k32 = *k;
+        for (int i = 0; i < k32.n_nodes && i < GPRX_MAX_KNODES; i++)
+            for (int q = 0; q < 3; q++) k32.node[i].p[q] = (double)(float)k32.node[i].p[q];
+        e = canonicalize<double>(k32, M->kd);
+        GPRX_REQUIRE(e.empty(), GPRX_ERR_ARG, e);
+    }
     M->desc = *k;
     M->has_kernel = true;
     M->fitted = false;
@@ -1090,7 +1268,7 @@ gprx_status gprx_model_set_noise(gprx_model* M, double sigma) {
     gprx_ctx* ctx = M ? M->ctx : nullptr;
     API_BEGIN
     GPRX_REQUIRE(M, GPRX_ERR_ARG, "gprx_model_set_noise: NULL model");
-    std::lock_guard<std::mutex> lk(M->mu);
+    ModelLock lk(M);
     M->sigma = sigma;
     M->fitted = false;
     M->has_alpha = false;
@@ -1102,9 +1280,9 @@ gprx_status gprx_model_set_noise(gprx_model* M, double sigma) {
 gprx_status gprx_model_fit(gprx_model* M, uint32_t flags, gprx_fit_info* info) {
     gprx_ctx* ctx = M ? M->ctx : nullptr;
     API_BEGIN
-    ProfBind pb_(ctx);
     GPRX_REQUIRE(M, GPRX_ERR_ARG, "gprx_model_fit: NULL model");
-    std::lock_guard<std::mutex> lk(M->mu);
+    ModelLock lk(M);
+    ProfBind pb_(ctx);  // after the lock: resolved (streams drained) before it is released
     return M->dt == GPRX_F64 ? model_fit<double>(M, flags, info) : model_fit<float>(M, flags, info);
     API_END(ctx)
 }
@@ -1113,7 +1291,7 @@ gprx_status gprx_model_get_alpha(gprx_model* M, void* alpha) {
     gprx_ctx* ctx = M ? M->ctx : nullptr;
     API_BEGIN
     GPRX_REQUIRE(M && alpha, GPRX_ERR_ARG, "gprx_model_get_alpha: NULL argument");
-    std::lock_guard<std::mutex> lk(M->mu);
+    ModelLock lk(M);
     GPRX_REQUIRE(M->has_alpha, GPRX_ERR_STATE, "gprx: model is not fitted");
     GPRX_HIP(hipSetDevice(ctx->device));
     GPRX_HIP(hipMemcpy(alpha, M->alpha.p, esize(M->dt) * M->n * M->m, hipMemcpyDeviceToHost));
@@ -1125,7 +1303,7 @@ gprx_status gprx_model_set_alpha(gprx_model* M, const void* alpha) {
     gprx_ctx* ctx = M ? M->ctx : nullptr;
     API_BEGIN
     GPRX_REQUIRE(M && alpha, GPRX_ERR_ARG, "gprx_model_set_alpha: NULL argument");
-    std::lock_guard<std::mutex> lk(M->mu);
+    ModelLock lk(M);
     GPRX_REQUIRE(M->has_data && M->has_kernel, GPRX_ERR_STATE, "gprx_model_set_alpha: set data and kernel first");
     GPRX_HIP(hipSetDevice(ctx->device));
     const size_t es = esize(M->dt);
@@ -1149,10 +1327,10 @@ gprx_status gprx_model_set_alpha(gprx_model* M, const void* alpha) {
 gprx_status gprx_model_predict(gprx_model* M, const void* Xq, int64_t q, void* mean, void* deriv) {
     gprx_ctx* ctx = M ? M->ctx : nullptr;
     API_BEGIN
-    ProfBind pb_(ctx);
     GPRX_REQUIRE(M && Xq && mean, GPRX_ERR_ARG, "gprx_model_predict: NULL argument");
     if (q == 0) return GPRX_OK;
-    std::lock_guard<std::mutex> lk(M->mu);
+    ModelLock lk(M);
+    ProfBind pb_(ctx);  // after the lock: resolved (streams drained) before it is released
     GPRX_HIP(hipSetDevice(ctx->device));
     return M->dt == GPRX_F64 ? model_predict<double>(M, Xq, q, mean, deriv)
                              : model_predict<float>(M, Xq, q, mean, deriv);
@@ -1162,10 +1340,10 @@ gprx_status gprx_model_predict(gprx_model* M, const void* Xq, int64_t q, void* m
 gprx_status gprx_model_posterior_cov(gprx_model* M, const void* Xa, const void* Xb, int64_t q, void* out) {
     gprx_ctx* ctx = M ? M->ctx : nullptr;
     API_BEGIN
-    ProfBind pb_(ctx);
     GPRX_REQUIRE(M && Xa && Xb && out, GPRX_ERR_ARG, "gprx_model_posterior_cov: NULL argument");
     if (q == 0) return GPRX_OK;
-    std::lock_guard<std::mutex> lk(M->mu);
+    ModelLock lk(M);
+    ProfBind pb_(ctx);  // after the lock: resolved (streams drained) before it is released
     GPRX_HIP(hipSetDevice(ctx->device));
     return M->dt == GPRX_F64 ? model_posterior_cov<double>(M, Xa, Xb, q, out)
                              : model_posterior_cov<float>(M, Xa, Xb, q, out);
@@ -1175,9 +1353,9 @@ gprx_status gprx_model_posterior_cov(gprx_model* M, const void* Xa, const void* 
 gprx_status gprx_model_core_matrix(gprx_model* M, void* C) {
     gprx_ctx* ctx = M ? M->ctx : nullptr;
     API_BEGIN
-    ProfBind pb_(ctx);
     GPRX_REQUIRE(M && C, GPRX_ERR_ARG, "gprx_model_core_matrix: NULL argument");
-    std::lock_guard<std::mutex> lk(M->mu);
+    ModelLock lk(M);
+    ProfBind pb_(ctx);  // after the lock: resolved (streams drained) before it is released
     GPRX_HIP(hipSetDevice(ctx->device));
     return M->dt == GPRX_F64 ? model_core_matrix<double>(M, C) : model_core_matrix<float>(M, C);
     API_END(ctx)
@@ -1187,9 +1365,9 @@ gprx_status gprx_model_lml(gprx_model* M, uint32_t flags, double* value, double*
                            double* logdet) {
     gprx_ctx* ctx = M ? M->ctx : nullptr;
     API_BEGIN
-    ProfBind pb_(ctx);
     GPRX_REQUIRE(M, GPRX_ERR_ARG, "gprx_model_lml: NULL model");
-    std::lock_guard<std::mutex> lk(M->mu);
+    ModelLock lk(M);
+    ProfBind pb_(ctx);  // after the lock: resolved (streams drained) before it is released
     GPRX_HIP(hipSetDevice(ctx->device));
     return M->dt == GPRX_F64 ? model_lml<double>(M, flags, value, grad, nparams, logdet)
                              : model_lml<float>(M, flags, value, grad, nparams, logdet);
@@ -1199,9 +1377,9 @@ gprx_status gprx_model_lml(gprx_model* M, uint32_t flags, double* value, double*
 gprx_status gprx_kernel_matrix(gprx_ctx* ctx, gprx_dtype dt, const gprx_kernel_desc* k, const void* X, int64_t n,
                                int32_t d, void* K) {
     API_BEGIN
-    ProfBind pb_(ctx);
     GPRX_REQUIRE(ctx && k && X && K, GPRX_ERR_ARG, "gprx_kernel_matrix: NULL argument");
     std::lock_guard<std::mutex> lk(ctx->mu);
+    ProfBind pb_(ctx);  // after the lock: resolved (streams drained) before it is released
     GPRX_HIP(hipSetDevice(ctx->device));
     return dt == GPRX_F64 ? kernel_matrix_impl<double>(ctx, k, X, n, d, K, false)
                           : kernel_matrix_impl<float>(ctx, k, X, n, d, K, false);
@@ -1211,9 +1389,9 @@ gprx_status gprx_kernel_matrix(gprx_ctx* ctx, gprx_dtype dt, const gprx_kernel_d
 gprx_status gprx_deriv_matrix(gprx_ctx* ctx, gprx_dtype dt, const gprx_kernel_desc* k, const void* X, int64_t n,
                               int32_t d, void* D) {
     API_BEGIN
-    ProfBind pb_(ctx);
     GPRX_REQUIRE(ctx && k && X && D, GPRX_ERR_ARG, "gprx_deriv_matrix: NULL argument");
     std::lock_guard<std::mutex> lk(ctx->mu);
+    ProfBind pb_(ctx);  // after the lock: resolved (streams drained) before it is released
     GPRX_HIP(hipSetDevice(ctx->device));
     return dt == GPRX_F64 ? kernel_matrix_impl<double>(ctx, k, X, n, d, D, true)
                           : kernel_matrix_impl<float>(ctx, k, X, n, d, D, true);
@@ -1223,9 +1401,9 @@ gprx_status gprx_deriv_matrix(gprx_ctx* ctx, gprx_dtype dt, const gprx_kernel_de
 gprx_status gprx_cross_matrix(gprx_ctx* ctx, gprx_dtype dt, const gprx_kernel_desc* k, const void* A, int64_t na,
                               const void* B, int64_t nb, int32_t d, void* K) {
     API_BEGIN
-    ProfBind pb_(ctx);
     GPRX_REQUIRE(ctx && k && A && B && K, GPRX_ERR_ARG, "gprx_cross_matrix: NULL argument");
     std::lock_guard<std::mutex> lk(ctx->mu);
+    ProfBind pb_(ctx);  // after the lock: resolved (streams drained) before it is released
     GPRX_HIP(hipSetDevice(ctx->device));
     return dt == GPRX_F64 ? cross_matrix_impl<double>(ctx, k, A, na, B, nb, d, K)
                           : cross_matrix_impl<float>(ctx, k, A, na, B, nb, d, K);
@@ -1234,9 +1412,9 @@ gprx_status gprx_cross_matrix(gprx_ctx* ctx, gprx_dtype dt, const gprx_kernel_de
 
 gprx_status gprx_cholesky(gprx_ctx* ctx, gprx_dtype dt, void* A, int64_t n, int32_t* info) {
     API_BEGIN
-    ProfBind pb_(ctx);
     GPRX_REQUIRE(ctx && A && n > 0, GPRX_ERR_ARG, "gprx_cholesky: bad argument");
     std::lock_guard<std::mutex> lk(ctx->mu);
+    ProfBind pb_(ctx);  // after the lock: resolved (streams drained) before it is released
     GPRX_HIP(hipSetDevice(ctx->device));
     gprx_status st = dt == GPRX_F64 ? cholesky_impl<double>(ctx, A, n, info, false)
                                     : cholesky_impl<float>(ctx, A, n, info, false);
@@ -1247,9 +1425,9 @@ gprx_status gprx_cholesky(gprx_ctx* ctx, gprx_dtype dt, void* A, int64_t n, int3
 
 gprx_status gprx_spd_inverse(gprx_ctx* ctx, gprx_dtype dt, void* A, int64_t n, int32_t* info) {
     API_BEGIN
-    ProfBind pb_(ctx);
     GPRX_REQUIRE(ctx && A && n > 0, GPRX_ERR_ARG, "gprx_spd_inverse: bad argument");
     std::lock_guard<std::mutex> lk(ctx->mu);
+    ProfBind pb_(ctx);  // after the lock: resolved (streams drained) before it is released
     GPRX_HIP(hipSetDevice(ctx->device));
     return dt == GPRX_F64 ? cholesky_impl<double>(ctx, A, n, info, true) : cholesky_impl<float>(ctx, A, n, info, true);
     API_END(ctx)
@@ -1264,6 +1442,7 @@ static const char* kclass_name(int c) {
 gprx_status gprx_ctx_set_stats(gprx_ctx* ctx, int32_t enable) {
     API_BEGIN
     GPRX_REQUIRE(ctx, GPRX_ERR_ARG, "gprx_ctx_set_stats: NULL ctx");
+    std::lock_guard<std::mutex> lk(ctx->mu);
     ctx->prof.on = enable != 0;
     ctx->prof.reset();
     return GPRX_OK;
@@ -1273,6 +1452,7 @@ gprx_status gprx_ctx_set_stats(gprx_ctx* ctx, int32_t enable) {
 gprx_status gprx_ctx_get_stats(gprx_ctx* ctx, gprx_kstat* out, int32_t max, int32_t* count) {
     API_BEGIN
     GPRX_REQUIRE(ctx, GPRX_ERR_ARG, "gprx_ctx_get_stats: NULL ctx");
+    std::lock_guard<std::mutex> lk(ctx->mu);
     int k = 0;
     for (int c = 0; c < KC_COUNT; c++) {
         const Prof::Acc& a = ctx->prof.acc[c];
@@ -1302,6 +1482,18 @@ gprx_status gprx_dev_bench(gprx_ctx* ctx, gprx_dtype dtype, int32_t what, int64_
     gprx_status st = gprx_dev_bench_impl(dtype, what, M, N, K, iters, ms, &ctx->ex);
     if (st != GPRX_OK) return fail(ctx, st, "gprx_dev_bench failed");
     return GPRX_OK;
+    API_END(ctx)
+}
+
+gprx_status gprx_dev_build_matrix(gprx_ctx* ctx, gprx_dtype dt, const gprx_kernel_desc* k, const void* X, int64_t n,
+                                  int32_t d, double sigma, int32_t path, void* K) {
+    API_BEGIN
+    GPRX_REQUIRE(ctx && k && X && K, GPRX_ERR_ARG, "gprx_dev_build_matrix: NULL argument");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ProfBind pb_(ctx);
+    GPRX_HIP(hipSetDevice(ctx->device));
+    return dt == GPRX_F64 ? dev_build_impl<double>(ctx, k, X, n, d, sigma, path, K)
+                          : dev_build_impl<float>(ctx, k, X, n, d, sigma, path, K);
     API_END(ctx)
 }
 
@@ -1340,9 +1532,9 @@ gprx_status gprx_sparse_fit(gprx_ctx* ctx, gprx_dtype dtype, const gprx_kernel_d
                             const void* Y, int64_t n, int32_t d, int32_t m, const void* Xm, int64_t M, double sigma,
                             double jitter, void* Kinv, void* RV, void* RM) {
     API_BEGIN
-    ProfBind pb_(ctx);
     GPRX_REQUIRE(ctx && kernel && Xm && (X || n == 0) && (Y || n == 0), GPRX_ERR_ARG, "gprx_sparse_fit: NULL argument");
     std::lock_guard<std::mutex> lk(ctx->mu);
+    ProfBind pb_(ctx);  // after the lock: resolved (streams drained) before it is released
     return dtype == GPRX_F64 ? sparse_fit_impl<double>(ctx, kernel, X, Y, n, d, m, Xm, M, sigma, jitter, Kinv, RV, RM)
                              : sparse_fit_impl<float>(ctx, kernel, X, Y, n, d, m, Xm, M, sigma, jitter, Kinv, RV, RM);
     API_END(ctx)

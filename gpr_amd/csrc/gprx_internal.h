@@ -286,9 +286,10 @@ template <typename T>
 bool pairs_mma_supported(const KCanon<T>& K, int m);
 template <typename T>
 int64_t pairs_feature_cols(const KCanon<T>& K, int d);
+// flag (optional): set when an input sample has a non-finite coordinate (the fit's check)
 template <typename T>
 void launch_pair_features(const KCanon<T>& K, const T* X, int64_t n, int d, const T* center, bool right, T* F,
-                          int64_t np, hipStream_t s);
+                          int64_t np, hipStream_t s, int* flag = nullptr);
 // Kd: a device copy of K (the kernels read the tree from memory)
 template <typename T>
 void launch_kbuild_mma(const KCanon<T>& K, const KCanon<T>* Kd, const T* FU, const T* FV, int64_t nf, int d, T* A,
@@ -384,9 +385,10 @@ TileBuild<T> pairs_tile_build(const KCanon<T>& K, const KCanon<T>* Kd, const T* 
 // ni > 0: the last ni row blocks of the nrows are the identity, set up here, and leave as
 // L^{-T} (upper triangular, ni = np / 128): the inverse factor riding along as extra rows,
 // each identity block updated only from its own column block on.
+// build_only: run the BUILD tasks alone (the covariance tiles, no factorisation; parity hook).
 template <typename T>
 void potrf_tiles(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info, Exec& ex,
-                 const TileBuild<T>* build = nullptr, int ni = 0);
+                 const TileBuild<T>* build = nullptr, int ni = 0, bool build_only = false);
 // C (lower) = A B^T where both operands vanish left of their row (LAUUM shape), k_potrf.hip
 template <typename T>
 void launch_gemm_nt_kskip(T* C, int64_t ldc, const T* A, int64_t lda, const T* B, int64_t ldb, int64_t M, int64_t N,
@@ -442,5 +444,13 @@ void launch_fit_reductions(const T* A, int64_t ld, int64_t n, int64_t np, int m,
 template <typename T>
 void launch_predict(const KCanon<T>& K, const T* X, const T* tabX, int64_t n, int d, int m, const T* alpha,
                     const T* Xq, const T* tabQ, int64_t q, T* mean, T* deriv, T* Z, T* out, hipStream_t s);
+
+// fp64 iterative refinement of an fp32 fit (k_refine.hip)
+template <typename S, typename D>
+void launch_convert(const S* in, D* out, int64_t n, hipStream_t s);
+void launch_residual_rows(const double* Y, const double* Kx, const double* a, double s2, int64_t n, int m, float* A,
+                          int64_t ld, int64_t row0, int64_t ncols, int mp, hipStream_t s);
+void launch_refine_accumulate(const float* delta, double* a, float* alpha, int64_t e, unsigned long long* nrm,
+                              hipStream_t s);
 
 }  // namespace gprx

@@ -101,11 +101,19 @@ __device__ __forceinline__ void block_stats(const T* FU, int64_t nu, int64_t i0,
     }
 }
 
+// max(x, 0) that keeps NaN: a non-finite input sample must give a non-finite kernel value,
+// as the reference's direct differences do (its (M - M) == (M - M) check then throws,
+// lib/GaussianProcess.cpp:399-401); fmax(NaN, 0) would return 0, a finite value.
+template <typename T>
+__device__ __forceinline__ T clamp0(T x) {
+    return x < T(0) ? T(0) : x;
+}
+
 // (r2, S) of one pair from the tile products and the per-sample norms (hd = d / 2)
 template <typename T, int NPER, bool R2>
 __device__ __forceinline__ void pair_stats(T pr2, T pper, T nu, T nv, T hd, T& r2, T& sp) {
-    r2 = R2 ? fmax(nu + nv + pr2, T(0)) : T(0);
-    sp = NPER ? fmax(fma(T(-0.5), pper, hd), T(0)) : T(0);
+    r2 = R2 ? clamp0(nu + nv + pr2) : T(0);
+    sp = NPER ? clamp0(fma(T(-0.5), pper, hd)) : T(0);
 }
 
 // Tile (i0, j0) of K(X, X) (+ sigma2 on the diagonal, identity beyond n) into A
@@ -319,7 +327,7 @@ __device__ __forceinline__ bool build_tile_sum(const KCanon<T>* __restrict__ Kd,
 #pragma unroll
             for (int y = 0; y < 4; y++) {
                 const int64_t gi = i0 + wr * 64 + y * 16 + lr;
-                r2[y] = gi == gj ? T(0) : fmax(nu[y] + nv + ar[x][y][reg], T(0));
+                r2[y] = gi == gj ? T(0) : clamp0(nu[y] + nv + ar[x][y][reg]);
                 v[y] = 0;
             }
             leaves_of_class<T, 4, false>(Kd, r2, v);
@@ -344,7 +352,7 @@ __device__ __forceinline__ bool build_tile_sum(const KCanon<T>* __restrict__ Kd,
 #pragma unroll
             for (int y = 0; y < 4; y++) {
                 const int64_t gi = i0 + wr * 64 + y * 16 + lr;
-                sp[y] = gi == gj ? T(0) : fmax(fma(T(-0.5), ap[x][y][reg], hd), T(0));
+                sp[y] = gi == gj ? T(0) : clamp0(fma(T(-0.5), ap[x][y][reg], hd));
             }
             leaves_of_class<T, 4, true>(Kd, sp, v);
         }

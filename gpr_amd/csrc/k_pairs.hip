@@ -27,12 +27,22 @@ namespace pr {
 
 // F (np x (Kr + Kp + 1), column-major, ld np): the left (U) or right (V) features of n
 // samples, then their squared norms |x~|^2.  Padding rows are all zero.
+// flag (may be NULL): set when a live sample has a non-finite coordinate.  Every kernel this
+// path evaluates is then non-finite on that sample's row (x - x = NaN in the reference's
+// direct differences), which the reference rejects (lib/GaussianProcess.cpp:399-401); the
+// feature expansion alone would hide it on the diagonal, where r2 = S = 0 is exact.
 template <typename T>
 __global__ void features_kernel(const T* __restrict__ X, int64_t n, int d, const T* __restrict__ center, T b,
-                                int need_r2, int nper, int right, T* __restrict__ F, int64_t np, int Kr, int Kp) {
+                                int need_r2, int nper, int right, T* __restrict__ F, int64_t np, int Kr, int Kp,
+                                int* __restrict__ flag) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= np) return;
     const bool live = i < n;
+    if (flag && live) {
+        bool bad = false;
+        for (int k = 0; k < d; k++) bad |= !isfinite(X[i * d + k]);
+        if (bad) atomicOr(flag, 1);
+    }
     T nrm = 0;
     if (need_r2) {
         for (int k = 0; k < d; k++) {
@@ -323,7 +333,7 @@ __global__ __launch_bounds__(NT) void grad_mma_kernel(const KCanon<T>* __restric
             const T nv = FV[(int64_t)(Kr + Kp) * nf + gj];
 #pragma unroll
             for (int y = 0; y < 4; y++)
-                ar[x][y][reg] = gi_of(y) == gj ? T(0) : fmax(nu[y] + nv + ar[x][y][reg], T(0));
+                ar[x][y][reg] = gi_of(y) == gj ? T(0) : clamp0(nu[y] + nv + ar[x][y][reg]);
         });
         // one element loop per leaf type, with the leaf's constants hoisted (the formulas of
         // leaf_grad, gprx_internal.h, rearranged: one exp per pair, no per-pair division
@@ -391,7 +401,7 @@ __global__ __launch_bounds__(NT) void grad_mma_kernel(const KCanon<T>* __restric
             const int64_t gj = gj_of(x, reg);
 #pragma unroll
             for (int y = 0; y < 4; y++) {
-                const T sp = gi_of(y) == gj ? T(0) : fmax(fma(T(-0.5), ar[x][y][reg], hd), T(0));
+                const T sp = gi_of(y) == gj ? T(0) : clamp0(fma(T(-0.5), ar[x][y][reg], hd));
                 T we = wt[x][y][reg] * exp(c1 * sp);
                 // pinned here: sunk past the next product (to its use), S and the weights
                 // stayed live across it and spilled
@@ -457,10 +467,10 @@ int64_t pairs_feature_cols(const KCanon<T>& K, int d) {
 
 template <typename T>
 void launch_pair_features(const KCanon<T>& K, const T* X, int64_t n, int d, const T* center, bool right, T* F,
-                          int64_t np, hipStream_t s) {
+                          int64_t np, hipStream_t s, int* flag) {
     const int Kr = pr::kr_of(K, d), Kp = pr::kp_of(K, d);
     hipLaunchKernelGGL(pr::features_kernel<T>, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, s, X, n, d, center,
-                       K.nper ? K.b[0] : T(0), K.need_r2 ? 1 : 0, K.nper, right ? 1 : 0, F, np, Kr, Kp);
+                       K.nper ? K.b[0] : T(0), K.need_r2 ? 1 : 0, K.nper, right ? 1 : 0, F, np, Kr, Kp, flag);
 }
 
 template <typename T>
@@ -611,7 +621,7 @@ TileBuild<T> pairs_tile_build(const KCanon<T>& K, const KCanon<T>* Kd, const T* 
     template bool pairs_mma_supported<T>(const KCanon<T>&, int);                                              \
     template int64_t pairs_feature_cols<T>(const KCanon<T>&, int);                                            \
     template void launch_pair_features<T>(const KCanon<T>&, const T*, int64_t, int, const T*, bool, T*, int64_t, \
-                                          hipStream_t);                                                       \
+                                          hipStream_t, int*);                                                 \
     template void launch_kbuild_mma<T>(const KCanon<T>&, const KCanon<T>*, const T*, const T*, int64_t, int, T*,    \
                                        int64_t, int64_t, T, int*, hipStream_t);                               \
     template void launch_kcross_mma<T>(const KCanon<T>&, const KCanon<T>*, const T*, int64_t, int64_t, const T*,  \

@@ -870,7 +870,7 @@ __global__ void pt_init_identity_rows(T* __restrict__ A, int64_t ld, int64_t row
 
 template <typename T>
 void potrf_tiles(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info, Exec& ex, const TileBuild<T>* build,
-                 int ni) {
+                 int ni, bool build_only) {
     using namespace pt;
     if (!ex.pt) ex.pt = new PtState();
     PtState& st = *ex.pt;
@@ -885,11 +885,20 @@ void potrf_tiles(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info
     const int nc = (int)(np / DB), nr = (int)(nrows / GT);
     const bool fused = build && build->mode != 0;
     GPRX_REQUIRE(ni >= 0 && ni <= nr - nc, GPRX_ERR_ARG, "potrf_tiles: bad identity row blocks");
-    auto key = std::make_tuple(nc, nr, fused, ni);
+    GPRX_REQUIRE(!build_only || fused, GPRX_ERR_ARG, "potrf_tiles: build_only needs a fused build");
+    // build_only (a parity hook, gprx_dev_build_matrix): the ticket list holds the BUILD tasks
+    // alone, so the launch writes exactly the covariance tiles the fused factorisation starts from
+    auto key = std::make_tuple(nc, nr, fused, build_only ? -1 : ni);
     auto it = st.sched.find(key);
     if (it == st.sched.end()) {
         const Params& pr = params();
-        Schedule S = make_schedule(nc, nr, pr.W, pr.near_for(nc), st.ncu, pr.cm, fused, ni);
+        Schedule S;
+        if (build_only) {
+            for (int i = 0; i < nc; i++)
+                for (int j = 0; j <= i; j++) S.list.push_back(make_int4(T_BUILD, i, j, 0));
+        } else {
+            S = make_schedule(nc, nr, pr.W, pr.near_for(nc), st.ncu, pr.cm, fused, ni);
+        }
         PtState::Dev d;
         d.n = (int64_t)S.list.size();
         d.est_us = S.est_us;
@@ -991,7 +1000,8 @@ int64_t potrf_tiles_schedule_stats(int nc, int nr, int P, bool build, double* es
 }
 
 template void potrf_tiles<double>(double*, int64_t, int64_t, int64_t, double*, int*, Exec&, const TileBuild<double>*,
-                                  int);
-template void potrf_tiles<float>(float*, int64_t, int64_t, int64_t, float*, int*, Exec&, const TileBuild<float>*, int);
+                                  int, bool);
+template void potrf_tiles<float>(float*, int64_t, int64_t, int64_t, float*, int*, Exec&, const TileBuild<float>*, int,
+                                 bool);
 
 }  // namespace gprx

@@ -23,6 +23,7 @@ UNIQUE_ID_BYTES = 128
 FIT_DEFAULT = 0
 FIT_NO_LU_FALLBACK = 1
 FIT_DISTRIBUTED = 2
+FIT_F32_NO_REFINE = 4
 LML_GRAD = 1
 LML_COMPAT = 2
 
@@ -64,7 +65,8 @@ class KStat(ctypes.Structure):
 class FitInfo(ctypes.Structure):
     _fields_ = [("logdet", ctypes.c_double), ("datafit", ctypes.c_double), ("info", ctypes.c_int32),
                 ("method", ctypes.c_int32), ("ms_build", ctypes.c_double), ("ms_factor", ctypes.c_double),
-                ("ms_solve", ctypes.c_double)]
+                ("ms_solve", ctypes.c_double), ("ms_refine", ctypes.c_double), ("refine_delta", ctypes.c_double),
+                ("refine_steps", ctypes.c_int32), ("pad", ctypes.c_int32)]
 
 
 _lib = None
@@ -117,6 +119,10 @@ def lib():
         L.gprx_ctx_set_stats.argtypes = [ctypes.c_void_p, ctypes.c_int32]
         L.gprx_ctx_get_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(KStat), ctypes.c_int32,
                                          ctypes.POINTER(ctypes.c_int32)]
+        # developer / parity hooks (include/gprx_dev.h)
+        L.gprx_dev_build_matrix.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(KernelDesc),
+                                            ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_double,
+                                            ctypes.c_int32, ctypes.c_void_p]
         _lib = L
     return _lib
 
@@ -227,6 +233,17 @@ class Context:
         K = np.empty((A.shape[0], B.shape[0]), dtype)
         self._c(lib().gprx_cross_matrix(self.h, _dt(dtype), ctypes.byref(kernel_desc(kernel)), _ptr(A), A.shape[0],
                                         _ptr(B), B.shape[0], A.shape[1], _ptr(K)))
+        return K
+
+    def build_matrix(self, kernel, X, sigma, path=0, dtype=np.float64):
+        """K(X, X) + sigma^2 I exactly as the fit's MFMA pair-statistics build writes it
+        (gprx_dev_build_matrix: path 0 = the fused BUILD tasks of the tile factorisation,
+        path 1 = the stand-alone kbuild_mma_kernel)."""
+        X = np.ascontiguousarray(X, dtype)
+        n, d = X.shape
+        K = np.empty((n, n), dtype)
+        self._c(lib().gprx_dev_build_matrix(self.h, _dt(dtype), ctypes.byref(kernel_desc(kernel)), _ptr(X), n, d,
+                                            float(sigma), path, _ptr(K)))
         return K
 
     def cholesky(self, A):

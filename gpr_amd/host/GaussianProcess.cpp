@@ -124,7 +124,7 @@ void GaussianProcess<T>::FitDevice(gprx_fit_info* info) {
 // by Load, or computed by Initialize) keeps predicting with them, as the reference does:
 // the refit's alpha is replaced by m_RegressionVectors.
 template <class T>
-void GaussianProcess<T>::EnsureFactor() {
+void GaussianProcess<T>::EnsureFactor() {  // m_DevMu held
     if (m_DeviceFactor) return;
     FitDevice();
     if (m_Initialized && m_RegressionVectors.rows() == m_SampleVectors.size())
@@ -153,6 +153,7 @@ void GaussianProcess<T>::Initialize() {
 template <class T>
 const typename GaussianProcess<T>::MatrixType& GaussianProcess<T>::GetCoreMatrix() {
     Initialize();
+    std::lock_guard<std::mutex> lk(m_DevMu);
     if (!m_CoreValid) {
         EnsureFactor();
         const std::size_t n = m_SampleVectors.size();
@@ -170,6 +171,7 @@ typename GaussianProcess<T>::VectorType GaussianProcess<T>::Predict(const Vector
     Initialize();
     CheckInputDimension(x, "GaussianProcess::Predict: ");
     VectorType mean(m_OutputDimension);
+    std::lock_guard<std::mutex> lk(m_DevMu);  // not inside another thread's lazy refit
     ThrowIfFailed(gprx_model_predict(m_Model, x.data(), 1, mean.data(), nullptr), DefaultContext());
     return mean;
 }
@@ -179,6 +181,7 @@ typename GaussianProcess<T>::MatrixType GaussianProcess<T>::PredictBatch(const M
     Initialize();
     if (Xq.cols() != m_InputDimension) throw std::string("GaussianProcess::PredictBatch: dimension mismatch");
     MatrixType out(Xq.rows(), m_OutputDimension);
+    std::lock_guard<std::mutex> lk(m_DevMu);
     ThrowIfFailed(gprx_model_predict(m_Model, Xq.data(), (int64_t)Xq.rows(), out.data(), nullptr), DefaultContext());
     return out;
 }
@@ -190,6 +193,7 @@ typename GaussianProcess<T>::VectorType GaussianProcess<T>::PredictDerivative(co
     CheckInputDimension(x, "GaussianProcess::PredictDerivative: ");
     VectorType mean(m_OutputDimension);
     D.resize(m_InputDimension, m_OutputDimension);
+    std::lock_guard<std::mutex> lk(m_DevMu);
     ThrowIfFailed(gprx_model_predict(m_Model, x.data(), 1, mean.data(), D.data()), DefaultContext());
     return mean;
 }
@@ -200,6 +204,7 @@ T GaussianProcess<T>::operator()(const VectorType& x, const VectorType& y) {
     Initialize();
     CheckInputDimension(x, "GaussianProcess::(): ");
     CheckInputDimension(y, "GaussianProcess::(): ");
+    std::lock_guard<std::mutex> lk(m_DevMu);
     EnsureFactor();
     m_CoreSize = m_SampleVectors.size();  // :95-97 builds the core matrix on demand
     T out = 0;
@@ -221,6 +226,7 @@ T GaussianProcess<T>::GetCredibleInterval(const VectorType& x) {
 template <class T>
 std::vector<T> GaussianProcess<T>::CredibleIntervalBatch(const MatrixType& Xq) {
     Initialize();
+    std::lock_guard<std::mutex> lk(m_DevMu);
     EnsureFactor();
     std::vector<T> c(Xq.rows());
     ThrowIfFailed(gprx_model_posterior_cov(m_Model, Xq.data(), Xq.data(), (int64_t)Xq.rows(), c.data()),

@@ -13,6 +13,11 @@
 // Initialize; operator()/GetCredibleInterval use the factor (k - |L^{-1}k|^2) instead of
 // Kx^T C Ky.  The InversionMethod is recorded for API compatibility; the device always
 // factorises with Cholesky (LU fallback when K is not numerically positive definite).
+//
+// Threading (reference: tests/PosteriorProcessTest.cpp:120-134 calls Predict and operator()
+// concurrently after Initialize): the read-only calls may run concurrently; the lazy device
+// refit behind operator()/GetCoreMatrix after Load is guarded by m_DevMu, and libgprx
+// serialises the device calls of one context.
 #pragma once
 
 #include <memory>
@@ -116,6 +121,7 @@ protected:
     bool debug;
 
     gprx_model* m_Model = nullptr;
+    std::mutex m_DevMu;           // guards the lazy refit (EnsureFactor), m_CoreMatrix/m_CoreSize
     bool m_DeviceFactor = false;  // device holds the Cholesky factor of the current state
     bool m_CoreValid = false;     // m_CoreMatrix holds the materialised core matrix
     std::size_t m_CoreSize = 0;   // the reference's m_CoreMatrix.diagonalSize(): n once the
@@ -128,6 +134,7 @@ protected:
     void UploadState();            // samples, kernel, noise -> device
     void FitDevice(gprx_fit_info* info = nullptr);
     void EnsureFactor();           // factor for operator()/core; keeps the regression vectors
+                                   // (caller holds m_DevMu)
 
     friend class Likelihood<TScalarType>;
 };

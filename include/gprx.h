@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define GPRX_ABI_VERSION 1
+#define GPRX_ABI_VERSION 2
 
 typedef enum gprx_status {
     GPRX_OK = 0,
@@ -98,6 +98,10 @@ typedef struct gprx_fit_info {
     double ms_build;     /* device time of the covariance build (HIP events) */
     double ms_factor;    /* device time of the factorisation */
     double ms_solve;     /* device time of the regression-vector solve */
+    double ms_refine;    /* fp32 models: device time of the fp64 iterative refinement */
+    double refine_delta; /* fp32 models: |last correction|_inf / |alpha|_inf (0 if not refined) */
+    int32_t refine_steps;/* fp32 models: refinement steps taken */
+    int32_t pad;
 } gprx_fit_info;
 
 /* ---- library / context ---------------------------------------------------------- */
@@ -147,6 +151,10 @@ gprx_status gprx_model_set_noise(gprx_model* model, double sigma);
 #define GPRX_FIT_NO_LU_FALLBACK 1u /* reserved: the device path always reports NOT_SPD (no LU) */
 #define GPRX_FIT_DISTRIBUTED 2u    /* multi-GPU factorisation on a gprx_ctx_create_dist context
                                       (implied when world > 1; forces the path at world = 1) */
+#define GPRX_FIT_F32_NO_REFINE 4u  /* fp32 models: skip the fp64 iterative refinement of alpha.  By
+                                      default an fp32 fit factorises in fp32 and refines alpha in
+                                      fp64 until it agrees with the double solve: the reference
+                                      inverts fp32 GPs in double (include/LAPACKUtils.h:85-97) */
 /* Initialize (lib/GaussianProcess.cpp:118-130) = ComputeRegressionVectors (:642-672):
  * kernel matrix (:384-402) + noise (:375-381) + factorisation (replaces the default
  * lapack::lu_invert dgetrf_+dgetri_, include/LAPACKUtils.h:38-56,85-97) + regression

@@ -37,6 +37,15 @@ int64_t gprx_dev_pt_trace(int32_t* tasks, int64_t* times, int64_t max);
 /* GPRX_BS_TRACE=1: per block of the last back substitution {start, non-critical tiles done,
  * alpha_{k+1} seen, alpha_k published} (100 MHz wall clock); returns blocks. */
 int64_t gprx_dev_bs_trace(int64_t* times, int64_t max_blocks);
+/* Parity hook for the PRODUCTION covariance build (the fit never materialises K on its own):
+ * K(X, X) + sigma^2 I of n samples (row-major host X, n x d) as the fit's MFMA pair-statistics
+ * path writes it, returned as the full symmetric n x n row-major matrix.
+ *   path 0: the BUILD tasks of the fused tile factorisation (potrf_tiles_kernel, the
+ *           default fit path for sum-of-exp-leaf trees), launched with no other task;
+ *   path 1: the stand-alone kbuild_mma_kernel (trees the fused build does not carry).
+ * GPRX_ERR_ARG when the tree is not covered by that path; GPRX_ERR_NONFINITE as the fit. */
+gprx_status gprx_dev_build_matrix(gprx_ctx* ctx, gprx_dtype dtype, const gprx_kernel_desc* kernel, const void* X,
+                                  int64_t n, int32_t d, double sigma, int32_t path, void* K);
 #ifdef __cplusplus
 }
 #endif

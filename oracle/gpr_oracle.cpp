@@ -56,6 +56,10 @@ typedef void (*getri_t)(int*, double*, int*, int*, double*, int*, int*);
 typedef void (*potrf_t)(char*, int*, double*, int*, int*);
 typedef void (*potri_t)(char*, int*, double*, int*, int*);
 typedef int (*ilaenv_t)(int*, char*, char*, int*, int*, int*, int*);
+typedef void (*dgemm_t)(const char*, const char*, const int*, const int*, const int*, const double*, const double*,
+                        const int*, const double*, const int*, const double*, double*, const int*);
+typedef void (*sgemm_t)(const char*, const char*, const int*, const int*, const int*, const float*, const float*,
+                        const int*, const float*, const int*, const float*, float*, const int*);
 
 struct Lapack {
     getrf_t getrf = nullptr;
@@ -63,6 +67,8 @@ struct Lapack {
     potrf_t potrf = nullptr;
     potri_t potri = nullptr;
     ilaenv_t ilaenv = nullptr;
+    dgemm_t dgemm = nullptr;  // BLAS GEMM for the oracle's Eigen products (optional)
+    sgemm_t sgemm = nullptr;
     std::string name = "none (partial-pivot fallback)";
     bool ok() const { return getrf && getri && potrf && potri && ilaenv; }
 };
@@ -85,6 +91,8 @@ static Lapack load_lapack() {
         T.potrf = (potrf_t)dlsym(h, "dpotrf_");
         T.potri = (potri_t)dlsym(h, "dpotri_");
         T.ilaenv = (ilaenv_t)dlsym(h, "ilaenv_");
+        T.dgemm = (dgemm_t)dlsym(h, "dgemm_");
+        T.sgemm = (sgemm_t)dlsym(h, "sgemm_");
         if (T.ok()) {
             typedef int (*setlayer_t)(int);
             if (auto f = (setlayer_t)dlsym(h, "MKL_Set_Threading_Layer")) f(3 /* MKL_THREADING_GNU */);
@@ -545,9 +553,27 @@ static void deriv_matrix(const Node<T>& k, const T* X, int n, int d, T* M) {
     }
 }
 
+// Column-major BLAS GEMM in T (C = alpha op(A) op(B) + beta C); false when the runtime
+// library has none (the callers then loop).  Eigen's products (the reference's) are blocked
+// GEMMs in T with an unspecified summation order, as BLAS's are.
+static bool blas_gemm(char ta, char tb, int m, int n, int k, double alpha, const double* A, int lda, const double* B,
+                      int ldb, double beta, double* C, int ldc) {
+    if (!lapack().dgemm) return false;
+    lapack().dgemm(&ta, &tb, &m, &n, &k, &alpha, A, &lda, B, &ldb, &beta, C, &ldc);
+    return true;
+}
+static bool blas_gemm(char ta, char tb, int m, int n, int k, float alpha, const float* A, int lda, const float* B,
+                      int ldb, float beta, float* C, int ldc) {
+    if (!lapack().sgemm) return false;
+    lapack().sgemm(&ta, &tb, &m, &n, &k, &alpha, A, &lda, B, &ldb, &beta, C, &ldc);
+    return true;
+}
+
 // Eigen-style row-major GEMM in T: C(r x c) = A(r x k) * B(k x c)
 template <class T>
 static void gemm(const T* A, const T* B, T* C, int r, int kk, int c) {
+    // row-major C = A B is column-major C^T = B^T A^T
+    if (blas_gemm('N', 'N', c, r, kk, T(1), B, c, A, kk, T(0), C, c)) return;
 #pragma omp parallel for schedule(static)
     for (int i = 0; i < r; i++) {
         for (int j = 0; j < c; j++) C[(size_t)i * c + j] = 0;
@@ -784,7 +810,7 @@ int orc_num_threads() { return omp_get_max_threads(); }
                                                                                      i < n; i++) { \
                     T row = 0;                                                                     \
                     for (int j = 0; j < n; j++)                                                    \
-                        row += (alpha[i] * alpha[j] - C[(size_t)i * n + j]) * Dp[(size_t)j * n + i]; \
+                        row += (alpha[i] * alpha[j] - C[(size_t)i * n + j]) * Dp[(size_t)i * n + j]; /* D_p symmetric */ \
                     tr += row;                                                                     \
                 }                                                                                  \
                 grad[p] = 0.5 * tr;                                                                \
@@ -809,21 +835,27 @@ int orc_num_threads() { return omp_get_max_threads(); }
                                                                                     j < M; j++)    \
             Knm[(size_t)i * M + j] = keval(*k, X + (size_t)i * d, Xm + (size_t)j * d, d);          \
         T is2 = 1.0 / (sigma * sigma);                                                             \
-        std::vector<T> S(K);                                                                       \
-        _Pragma("omp parallel for schedule(static)") for (int a = 0; a < M; a++) for (int b = 0;   \
+        /* S = K + is2 Knm^T Knm (:298-299); Knm row-major n x M is column-major Knm^T */         \
+        std::vector<T> S((size_t)M * M), KtY((size_t)M * m);                                       \
+        if (!blas_gemm('N', 'T', M, M, n, T(1), Knm.data(), M, Knm.data(), M, T(0), S.data(), M)) { \
+            _Pragma("omp parallel for schedule(static)") for (int a = 0; a < M; a++) for (int b = 0; \
                                                                                     b < M; b++) {  \
-            T s = 0;                                                                               \
-            for (int i = 0; i < n; i++) s += Knm[(size_t)i * M + a] * Knm[(size_t)i * M + b];      \
-            S[(size_t)a * M + b] = K[(size_t)a * M + b] + is2 * s;                                 \
-        }                                                                                          \
-        std::vector<T> Sig = invert<T>(S, M, FullPivotLU, stable);                                 \
-        std::vector<T> KtY((size_t)M * m);                                                         \
-        for (int a = 0; a < M; a++)                                                                \
-            for (int c = 0; c < m; c++) {                                                          \
                 T s = 0;                                                                           \
-                for (int i = 0; i < n; i++) s += Knm[(size_t)i * M + a] * Y[(size_t)i * m + c];    \
-                KtY[(size_t)a * m + c] = s;                                                        \
+                for (int i = 0; i < n; i++) s += Knm[(size_t)i * M + a] * Knm[(size_t)i * M + b];  \
+                S[(size_t)a * M + b] = s;                                                          \
             }                                                                                      \
+        }                                                                                          \
+        for (size_t e = 0; e < S.size(); e++) S[e] = K[e] + is2 * S[e];                            \
+        std::vector<T> Sig = invert<T>(S, M, FullPivotLU, stable);                                 \
+        /* Knm^T Y (:303): column-major (Knm^T Y)^T = Y^T Knm */                                   \
+        if (!blas_gemm('N', 'T', m, M, n, T(1), Y, m, Knm.data(), M, T(0), KtY.data(), m)) {       \
+            for (int a = 0; a < M; a++)                                                            \
+                for (int c = 0; c < m; c++) {                                                      \
+                    T s = 0;                                                                       \
+                    for (int i = 0; i < n; i++) s += Knm[(size_t)i * M + a] * Y[(size_t)i * m + c]; \
+                    KtY[(size_t)a * m + c] = s;                                                    \
+                }                                                                                  \
+        } /* column-major m x M (ld m) is the row-major M x m layout */                             \
         std::vector<T> A((size_t)M * M), B((size_t)M * M), t1((size_t)M * m), t2((size_t)M * m);   \
         gemm(K.data(), Sig.data(), A.data(), M, M, M);                                             \
         gemm(A.data(), KtY.data(), t1.data(), M, M, m);                                            \

@@ -8,6 +8,8 @@
 #include <functional>
 #include <iostream>
 #include <sstream>
+#include <thread>
+#include <vector>
 
 #include "gpr/GaussianProcess.h"
 #include "gpr/Kernel.h"
@@ -321,6 +323,98 @@ static void sparse_test() {
     check(err < 0.05, "sparse predict error " + num(err));
 }
 
+// PosteriorProcessTest Test1 (tests/PosteriorProcessTest.cpp:51-95): the credible interval
+// is exactly 2 sqrt(gp(x, x)), sigma = 1e-5, 20 sinus samples.
+static void posterior_test1() {
+    typedef GP<double> G;
+    auto gp = std::make_shared<G>(std::make_shared<GaussianKernel<double>>(0.5));
+    gp->SetSigma(0.00001);
+    for (unsigned i = 0; i < 20; i++) {
+        G::VectorType x(1), y(1);
+        x(0) = i * 2 * M_PI / 20;
+        y(0) = std::sin(x(0));
+        gp->AddSample(x, y);
+    }
+    gp->Initialize();
+    for (unsigned i = 0; i < 50; i++) {
+        G::VectorType x(1);
+        x(0) = i * 2 * M_PI / 50 * 1.3;
+        const double c = 2 * std::sqrt((*gp)(x, x)) - gp->GetCredibleInterval(x);
+        check(c == 0, "credible interval not correct at x = " + num(x(0)) + " (gp(x,x) = " + num((*gp)(x, x)) + ")");
+    }
+}
+
+// PosteriorProcessTest Test2 (tests/PosteriorProcessTest.cpp:97-165): the posterior kernel
+// matrix over [0, 5) of a noise-free GP through 4 landmarks, its rows filled by Predict and
+// operator() running CONCURRENTLY (the reference's omp parallel for, :120-134; here 8
+// std::threads).  The reference then samples the posterior (Eigen eigensolver, absent here)
+// and checks every sample equals the mean at the landmarks (|r - mean| <= 1e-9): that holds
+// iff the posterior covariance vanishes on the landmark rows, which is checked directly.
+// Run on a fresh GP and on one restored by Load, whose factor is rebuilt lazily by the first
+// operator() -- the refit that must not race the concurrent Predict calls.
+static void posterior_test2_on(GP<double>& gp) {
+    typedef GP<double> G;
+    const unsigned ns = 50;
+    std::vector<double> mean(ns), K(ns * ns, 0.0);
+    std::vector<std::string> errs(8);
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < 8; t++)
+        th.emplace_back([&, t]() {
+            try {
+                for (unsigned i = t; i < ns; i += 8) {
+                    G::VectorType x1(1);
+                    x1(0) = i * 5.0 / ns;
+                    mean[i] = gp.Predict(x1)(0);
+                    for (unsigned j = i; j < ns; j++) {
+                        G::VectorType x2(1);
+                        x2(0) = j * 5.0 / ns;
+                        K[i * ns + j] = K[j * ns + i] = gp(x1, x2);
+                    }
+                }
+            } catch (const std::string& e) {
+                errs[t] = e;
+            }
+        });
+    for (auto& x : th) x.join();
+    for (auto& e : errs) check(e.empty(), "concurrent call failed: " + e);
+    for (unsigned l : {10u, 20u, 30u, 40u}) {
+        for (unsigned j = 0; j < ns; j++)
+            check(std::fabs(K[l * ns + j]) <= 1e-9, "posterior covariance at landmark " + num(l) + ", " + num(j) +
+                                                     " = " + num(K[l * ns + j]));
+        const double y = (l == 10) ? 0.0 : (l == 30 ? 0.5 : 1.0);
+        check(std::fabs(mean[l] - y) <= 1e-9, "mean at landmark " + num(l) + " = " + num(mean[l]));
+    }
+    for (unsigned i = 0; i < ns; i++) check(K[i * ns + i] >= -1e-9, "negative posterior variance");
+}
+
+static std::shared_ptr<GP<double>> landmark_gp() {
+    typedef GP<double> G;
+    auto gp = std::make_shared<G>(std::make_shared<GaussianKernel<double>>(1));
+    gp->SetSigma(0);
+    const double xs[4] = {1, 2, 3, 4}, ys[4] = {0, 1, 0.5, 1};
+    for (int i = 0; i < 4; i++) {
+        G::VectorType x(1), y(1);
+        x(0) = xs[i];
+        y(0) = ys[i];
+        gp->AddSample(x, y);
+    }
+    gp->Initialize();
+    return gp;
+}
+
+static void posterior_test2() {
+    auto gp = landmark_gp();
+    posterior_test2_on(*gp);
+}
+
+static void posterior_test2_loaded() {
+    auto gp = landmark_gp();
+    gp->Save("/tmp/gpr_amd_post_test-");
+    auto rd = std::make_shared<GP<double>>(std::make_shared<GaussianKernel<double>>(3));
+    rd->Load("/tmp/gpr_amd_post_test-");
+    posterior_test2_on(*rd);
+}
+
 int main() {
     run("GaussianProcessTest1", gp_test1);
     run("GaussianProcessTest2", gp_test2);
@@ -334,5 +428,8 @@ int main() {
     run("IOTest3", io_test3);
     run("LikelihoodGradient", lik_test);
     run("SparseRegression", sparse_test);
+    run("PosteriorProcessTest1", posterior_test1);
+    run("PosteriorProcessTest2", posterior_test2);
+    run("PosteriorProcessTest2Loaded", posterior_test2_loaded);
     return g_fail;
 }

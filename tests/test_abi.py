@@ -32,14 +32,14 @@ def test_python_binding_lists_all_abi_symbols():
 
 
 def test_abi_version():
-    assert gpr_amd.lib().gprx_abi_version() == 1
+    assert gpr_amd.lib().gprx_abi_version() == 2
 
 
 def test_struct_layouts_match_header():
     # gprx_knode: int32 op, int32 pad, double p[3] -> 32 bytes; desc: 8 + 32*32
     assert ctypes.sizeof(gprx.KNode) == 32
     assert ctypes.sizeof(gprx.KernelDesc) == 8 + 32 * gprx.MAX_KNODES
-    assert ctypes.sizeof(gprx.FitInfo) == 8 * 2 + 4 * 2 + 8 * 3
+    assert ctypes.sizeof(gprx.FitInfo) == 8 * 2 + 4 * 2 + 8 * 3 + 8 * 2 + 4 * 2
     assert ctypes.sizeof(gprx.KStat) == 32 + 8 * 4
 
 

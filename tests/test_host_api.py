@@ -5,8 +5,9 @@ KernelFactory<T>, Likelihood<T>, MatrixIO — driven through its two test execut
 * host_cpu_test: kernels / factory / file format on the host, and that a GaussianProcess
   throws when no GPU is visible (no CPU fallback).
 * gp_host_test (-m gpu): the reference's GaussianProcessTest 1-7 and IOTest 1-3 with the
-  reference's thresholds, plus a likelihood gradient consistency check, all running their
-  fits on the GPU through libgprx."""
+  reference's thresholds, plus a likelihood gradient consistency check, the sparse GP and
+  PosteriorProcessTest 1-2 (Predict / operator() from 8 threads at once, on a fresh and on a
+  loaded GP), all running their fits on the GPU through libgprx."""
 import os
 import subprocess
 
@@ -44,4 +45,4 @@ def test_host_cpu():
 def test_host_gpu_reference_scenarios():
     rc, lines, out = _run("gp_host_test")
     assert rc == 0, out
-    assert len(lines) == 12 and all(l.startswith("PASS") for l in lines), out
+    assert len(lines) == 15 and all(l.startswith("PASS") for l in lines), out
