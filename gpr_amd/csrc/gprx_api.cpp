@@ -247,6 +247,11 @@ struct gprx_model {
     // fp32 models: fp64 iterative refinement state (k_refine.hip).  kd then holds the tree in
     // double with the parameters rounded to float first (the reference stores them in T).
     DevBuf Xd, Yd, ad, kxd, fud, fvd, kdev64, tabd, zd, outd, delta, nrm;
+    // LU fallback state (k_getrf.hip), double for both scalar types: the factored matrix,
+    // pivots, the 128-block inverses of L and U, and scratch
+    int method = 0;  // factor of the current fit: 0 Cholesky (A, Linv), 1 LU (lu, ipiv, luL, luU)
+    DevBuf lu, ipiv, luL, luU, luT1, luUt, luB, lured;
+    double lu_sign = 1;  // sign of det(K + sigma^2 I) from the LU
     std::mutex mu;
 };
 
@@ -384,6 +389,102 @@ static void refine_f32(gprx_model* M, gprx_fit_info* out) {
         out->refine_delta = rel;
         out->refine_steps = taken;
     }
+}
+
+// ---------------------------------------------------------------------------------------
+// LU fallback (k_getrf.hip): K + sigma^2 I rebuilt in full, factored with partial pivoting in
+// double, alpha = A^{-1} Y by the two triangular solves.  The reference's default inversion
+// is exactly this LU (dgetrf_ on the matrix cast to double, include/LAPACKUtils.h:38-56,
+// 85-97); it reaches here only when the Cholesky met a non-positive pivot.
+// ---------------------------------------------------------------------------------------
+template <typename T>
+static void lu_build_matrix(gprx_model* M) {
+    hipStream_t s = M->ctx->stream;
+    const KCanon<T>& K = kcanon<T>(M);
+    const int64_t n = M->n, np = M->np;
+    const T sig = (T)M->sigma;
+    const T sigma2 = sig * sig;  // in T, as the reference (lib/GaussianProcess.cpp:379)
+    M->lu.ensure(sizeof(double) * np * np);
+    GPRX_HIP(hipMemsetAsync(M->flag.p, 0, sizeof(int), s));
+    if constexpr (std::is_same<T, double>::value) {
+        launch_kbuild<double>(K, M->X.as<double>(), M->tab.as<double>(), n, M->X.as<double>(), M->tab.as<double>(), n,
+                              M->d, M->lu.as<double>(), np, np, true, sigma2, M->flag.as<int>(), s);
+    } else {  // K evaluated in float (the reference's T), then widened: lu_invert<float> casts to double
+        M->A.ensure(sizeof(float) * np * np);
+        launch_kbuild<float>(K, M->X.as<float>(), M->tab.as<float>(), n, M->X.as<float>(), M->tab.as<float>(), n,
+                             M->d, M->A.as<float>(), np, np, true, sigma2, M->flag.as<int>(), s);
+        launch_convert<float, double>(M->A.as<float>(), M->lu.as<double>(), np * np, s);
+    }
+    launch_sym_fill<double>(M->lu.as<double>(), np, np, s);
+}
+
+template <typename T>
+static void lu_fit(gprx_model* M, gprx_fit_info* out) {
+    gprx_ctx* ctx = M->ctx;
+    hipStream_t s = ctx->stream;
+    const int64_t n = M->n, np = M->np;
+    const int m = M->m;
+    GPRX_HIP(hipEventRecord(ctx->ev[0], s));
+    lu_build_matrix<T>(M);
+    M->ipiv.ensure(sizeof(int) * np);
+    M->luL.ensure(sizeof(double) * np * DB);
+    M->luU.ensure(sizeof(double) * np * DB);
+    M->luT1.ensure(sizeof(double) * np * DB);
+    M->luUt.ensure(sizeof(double) * np * DB);
+    M->luB.ensure(sizeof(double) * np * m);
+    M->lured.ensure(sizeof(double) * 4);
+    GPRX_HIP(hipMemsetD32Async((hipDeviceptr_t)M->info.p, INT_MAX, 1, s));
+    GPRX_HIP(hipEventRecord(ctx->ev[1], s));
+    lu_factor(M->lu.as<double>(), np, np, M->ipiv.as<int>(), M->info.as<int>(), M->luL.as<double>(),
+              M->luU.as<double>(), M->luT1.as<double>(), M->luUt.as<double>(), s);
+    GPRX_HIP(hipEventRecord(ctx->ev[2], s));
+    lu_rhs_from_rows<T>(M->Y.as<T>(), n, m, M->luB.as<double>(), np, np, s);
+    lu_solve(M->lu.as<double>(), np, np, M->ipiv.as<int>(), M->luL.as<double>(), M->luU.as<double>(),
+             M->luB.as<double>(), np, m, s);
+    M->alpha.ensure(sizeof(T) * np * m);
+    lu_rows_from_rhs<T>(M->luB.as<double>(), np, n, m, M->alpha.as<T>(), s);
+    lu_logdet(M->lu.as<double>(), np, n, M->ipiv.as<int>(), M->lured.as<double>(), s);
+    GPRX_HIP(hipEventRecord(ctx->ev[3], s));
+    int hflag = 0, hinfo = 0;
+    double red[3];
+    download(&hflag, M->flag.p, sizeof(int), s);
+    download(&hinfo, M->info.p, sizeof(int), s);
+    download(red, M->lured.p, sizeof(red), s);
+    if (hflag)
+        throw Error{GPRX_ERR_NONFINITE,
+                    "GaussianProcess::ComputeKernelMatrixInternal: kernel matrix contains entries which are not finite."};
+    if (hinfo != INT_MAX)
+        throw Error{GPRX_ERR_SINGULAR, "gprx: kernel matrix is singular (LU pivot " + std::to_string(hinfo) +
+                                           " is zero; the reference's dgetrf_ fails there too)"};
+    // data fit y^T (K + s^2 I)^{-1} y from alpha (the host copies are small next to the factor)
+    std::vector<T> ha((size_t)n * m), hy((size_t)n * m);
+    download(ha.data(), M->alpha.p, sizeof(T) * n * m, s);
+    download(hy.data(), M->Y.p, sizeof(T) * n * m, s);
+    double df = 0;
+    for (size_t e = 0; e < ha.size(); e++) df += (double)hy[e] * (double)ha[e];
+    M->method = 1;
+    M->lu_sign = red[1];
+    M->fitted = true;
+    M->has_alpha = true;
+    M->inv_ready = false;
+    if (out) {
+        float t01 = 0, t12 = 0, t23 = 0;
+        hipEventElapsedTime(&t01, ctx->ev[0], ctx->ev[1]);
+        hipEventElapsedTime(&t12, ctx->ev[1], ctx->ev[2]);
+        hipEventElapsedTime(&t23, ctx->ev[2], ctx->ev[3]);
+        out->ms_build += t01;
+        out->ms_factor += t12;
+        out->ms_solve += t23;
+        out->logdet = red[0];  // log |det|; the sign is the model's lu_sign
+        out->datafit = df;
+        out->method = 1;
+    }
+}
+
+// A^{-1} B for m right-hand sides already in M->luB-shaped column-major storage (np x m)
+static void lu_solve_model(gprx_model* M, double* B, int m) {
+    lu_solve(M->lu.as<double>(), M->np, M->np, M->ipiv.as<int>(), M->luL.as<double>(), M->luU.as<double>(), B, M->np,
+             m, M->ctx->stream);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -536,9 +637,17 @@ static gprx_status model_fit(gprx_model* M, uint32_t flags, gprx_fit_info* out) 
         throw Error{GPRX_ERR_NONFINITE,
                     "GaussianProcess::ComputeKernelMatrixInternal: kernel matrix contains entries which are not finite."};
     check_sched(hinfo);
-    if (hinfo != INT_MAX)
+    if (hinfo != INT_MAX) {
+        // the reference's default inversion is an LU (lib/GaussianProcess.cpp:545-559): refactor
+        // the same matrix with partial pivoting instead of rejecting it
+        if (!(flags & GPRX_FIT_NO_LU_FALLBACK) && !dist) {
+            lu_fit<T>(M, out);
+            return GPRX_OK;
+        }
         throw Error{GPRX_ERR_NOT_SPD, "gprx: kernel matrix is not positive definite (Cholesky pivot " +
                                           std::to_string(hinfo) + " <= 0)"};
+    }
+    M->method = 0;
     M->fitted = true;
     M->has_alpha = true;
     M->inv_ready = want_inv;
@@ -643,6 +752,34 @@ static gprx_status model_posterior_cov(gprx_model* M, const void* Xa, const void
         launch_sincos_tables<T>(K, da.as<T>(), q, d, ta.as<T>(), s);
         launch_sincos_tables<T>(K, db.as<T>(), q, d, tb.as<T>(), s);
     }
+    if (M->method == 1) {  // LU factors: k(x,y) - K(X,x)^T A^{-1} K(X,y), the reference's formula (:84-99)
+        const int64_t np = M->np;
+        DevBuf Kt, Wd, Kad;
+        Wd.ensure(sizeof(double) * np * q);
+        Kad.ensure(sizeof(double) * np * q);
+        auto cross = [&](const T* Xq, const T* tq, double* dst) {  // K(X, Xq): np x q column-major
+            T* buf;
+            if constexpr (std::is_same<T, double>::value) {
+                buf = dst;
+            } else {
+                Kt.ensure(sizeof(T) * np * q);
+                buf = Kt.as<T>();
+            }
+            GPRX_HIP(hipMemsetAsync(buf, 0, sizeof(T) * np * q, s));
+            launch_kbuild<T>(K, M->X.as<T>(), M->tab.as<T>(), M->n, Xq, tq, q, d, buf, np, 0, false, T(0),
+                             M->flag.as<int>(), s);
+            if constexpr (!std::is_same<T, double>::value) launch_convert<T, double>(buf, dst, np * q, s);
+        };
+        cross(db.as<T>(), tb.as<T>(), Wd.as<double>());
+        lu_solve_model(M, Wd.as<double>(), (int)q);
+        cross(da.as<T>(), ta.as<T>(), Kad.as<double>());
+        kab.ensure(sizeof(T) * q);
+        res.ensure(sizeof(T) * q);
+        launch_pair_kernel<T>(K, da.as<T>(), db.as<T>(), q, d, kab.as<T>(), s);
+        lu_coldot<T>(Kad.as<double>(), Wd.as<double>(), np, M->n, q, kab.as<T>(), res.as<T>(), s);
+        download(out, res.p, sizeof(T) * q, s);
+        return GPRX_OK;
+    }
     Ra.ensure(sizeof(T) * qp * M->np);
     Rb.ensure(sizeof(T) * qp * M->np);
     solve_rows_for<T>(M, da.as<T>(), ta.as<T>(), q, qp, Ra.as<T>());
@@ -655,10 +792,33 @@ static gprx_status model_posterior_cov(gprx_model* M, const void* Xa, const void
     return GPRX_OK;
 }
 
+// the explicit inverse from the LU factors (A^{-1} I, double, np x np column-major in luC)
+static void lu_inverse(gprx_model* M, DevBuf& luC) {
+    const int64_t np = M->np;
+    luC.ensure(sizeof(double) * np * np);
+    GPRX_HIP(hipMemsetAsync(luC.p, 0, sizeof(double) * np * np, M->ctx->stream));
+    launch_set_identity_pad<double>(luC.as<double>(), np, 0, np, M->ctx->stream);
+    lu_solve_model(M, luC.as<double>(), (int)np);
+}
+
 template <typename T>
 static gprx_status model_core_matrix(gprx_model* M, void* Cout) {
     GPRX_REQUIRE(M->fitted, GPRX_ERR_STATE, "gprx: model is not fitted");
     hipStream_t s = M->ctx->stream;
+    if (M->method == 1) {  // dgetri_'s inverse (include/LAPACKUtils.h:49) from the LU factors
+        DevBuf luC;
+        lu_inverse(M, luC);
+        const int64_t n = M->n, np = M->np;
+        std::vector<double> h((size_t)n * n);
+        GPRX_HIP(hipStreamSynchronize(s));
+        GPRX_HIP(hipGetLastError());
+        GPRX_HIP(hipMemcpy2D(h.data(), sizeof(double) * n, luC.p, sizeof(double) * np, sizeof(double) * n, n,
+                             hipMemcpyDeviceToHost));
+        T* C = reinterpret_cast<T*>(Cout);
+        for (int64_t j = 0; j < n; j++)
+            for (int64_t i = 0; i < n; i++) C[(size_t)i * n + j] = (T)h[(size_t)j * n + i];
+        return GPRX_OK;
+    }
     model_inverse<T>(M);
     const int64_t n = M->n, np = M->np;
     std::vector<T> h((size_t)n * n);
@@ -687,7 +847,9 @@ static gprx_status model_lml(gprx_model* M, uint32_t flags, double* value, doubl
     M->want_inv = grad && (flags & GPRX_LML_GRAD);
     gprx_status st;
     try {
-        st = model_fit<T>(M, GPRX_FIT_NO_LU_FALLBACK, &fi);
+        // the likelihood inverts with the GP's method too (include/Likelihood.h:77-79 ->
+        // ComputeCoreMatrixWithDeterminant): a matrix the Cholesky rejects takes the LU
+        st = model_fit<T>(M, GPRX_FIT_DEFAULT, &fi);
     } catch (...) {
         M->want_inv = false;
         throw;
@@ -699,10 +861,12 @@ static gprx_status model_lml(gprx_model* M, uint32_t flags, double* value, doubl
     const T df = (T)(-0.5 * fi.datafit);
     const T ct = (T)(-n / 2.0 * std::log(2 * M_PI));  // include/Likelihood.h:192
     double v;
-    if (flags & GPRX_LML_COMPAT) {
+    // LU fits can have det <= 0: the reference's clamp (:180-188) applies in both modes
+    const double det_sign = (M->method == 1) ? M->lu_sign : 1.0;
+    if ((flags & GPRX_LML_COMPAT) || det_sign <= 0) {
         // include/Likelihood.h:77-79 narrows the long-double determinant to T, :180-188 clamps
         typedef long double HP;
-        const HP det_ld = std::exp((HP)fi.logdet);
+        const HP det_ld = (HP)det_sign * std::exp((HP)fi.logdet);
         const HP det = (HP)(T)det_ld;
         HP cp;
         if (det <= std::numeric_limits<HP>::min()) cp = -0.5L * std::log(std::numeric_limits<HP>::min());
@@ -719,7 +883,18 @@ static gprx_status model_lml(gprx_model* M, uint32_t flags, double* value, doubl
     if (nparams) *nparams = K.nparams;
     if (grad && (flags & GPRX_LML_GRAD)) {
         hipStream_t s = M->ctx->stream;
-        if (!M->inv_ready) model_inverse<T>(M);
+        if (M->method == 1) {  // C from the LU factors, in the model's T (the reference casts back)
+            DevBuf luC;
+            lu_inverse(M, luC);
+            M->C.ensure(sizeof(T) * M->np * M->np);
+            if constexpr (std::is_same<T, double>::value)
+                GPRX_HIP(hipMemcpyAsync(M->C.p, luC.p, sizeof(double) * M->np * M->np, hipMemcpyDeviceToDevice, s));
+            else
+                launch_convert<double, T>(luC.as<double>(), M->C.as<T>(), M->np * M->np, s);
+            GPRX_HIP(hipStreamSynchronize(s));
+        } else if (!M->inv_ready) {
+            model_inverse<T>(M);
+        }
         M->grad.ensure(sizeof(double) * MAX_LEAF * 3);
         GPRX_HIP(hipMemsetAsync(M->grad.p, 0, sizeof(double) * MAX_LEAF * 3, s));
         static const bool direct_grad =

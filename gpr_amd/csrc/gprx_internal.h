@@ -445,6 +445,26 @@ template <typename T>
 void launch_predict(const KCanon<T>& K, const T* X, const T* tabX, int64_t n, int d, int m, const T* alpha,
                     const T* Xq, const T* tabQ, int64_t q, T* mean, T* deriv, T* Z, T* out, hipStream_t s);
 
+// LU with partial pivoting, always in double (k_getrf.hip): the fallback when the Cholesky
+// reports a non-positive pivot, as the reference's default LU inverse (include/LAPACKUtils.h
+// :38-56, 85-97).  A: np x np column-major (np a multiple of 128, identity padding); Li, Ui:
+// np/128 inverses of the 128-blocks of L (unit lower) and U; T1, Ut: np x 128 scratch each.
+void lu_factor(double* A, int64_t ld, int64_t np, int* ipiv, int* info, double* Li, double* Ui, double* T1,
+               double* Ut, hipStream_t s);
+// B (np x m, column-major, ldb) <- A^{-1} B
+void lu_solve(const double* A, int64_t ld, int64_t np, const int* ipiv, const double* Li, const double* Ui, double* B,
+              int64_t ldb, int m, hipStream_t s);
+template <typename T>
+void lu_rhs_from_rows(const T* Y, int64_t n, int m, double* B, int64_t ldb, int64_t np, hipStream_t s);
+template <typename T>
+void lu_rows_from_rhs(const double* B, int64_t ldb, int64_t n, int m, T* X, hipStream_t s);
+// out[0] = sum log|U_ii| (i < n), out[1] = sign of det, out[2] = 1 if a U_ii is zero
+void lu_logdet(const double* A, int64_t ld, int64_t n, const int* ipiv, double* out, hipStream_t s);
+// out[c] = kab[c] - sum_{j<n} Ka[j, c] W[j, c]
+template <typename T>
+void lu_coldot(const double* Ka, const double* W, int64_t ld, int64_t n, int64_t q, const T* kab, T* out,
+               hipStream_t s);
+
 // fp64 iterative refinement of an fp32 fit (k_refine.hip)
 template <typename S, typename D>
 void launch_convert(const S* in, D* out, int64_t n, hipStream_t s);

@@ -11,8 +11,10 @@
 // Differences (documented in DESIGN.md): the core matrix C = (K + sigma^2 I)^{-1} is
 // materialised lazily from the device factor (Save, GetCoreMatrix), not at every
 // Initialize; operator()/GetCredibleInterval use the factor (k - |L^{-1}k|^2) instead of
-// Kx^T C Ky.  The InversionMethod is recorded for API compatibility; the device always
-// factorises with Cholesky (LU fallback when K is not numerically positive definite).
+// Kx^T C Ky.  The InversionMethod is recorded for API compatibility; the device factorises
+// with Cholesky and, when K + sigma^2 I is not numerically positive definite, falls back to
+// a partial-pivot LU in double (the reference's default FullPivotLU = dgetrf_,
+// include/LAPACKUtils.h:38-56; gpr_amd/csrc/k_getrf.hip).
 //
 // Threading (reference: tests/PosteriorProcessTest.cpp:120-134 calls Predict and operator()
 // concurrently after Initialize): the read-only calls may run concurrently; the lazy device

@@ -93,8 +93,8 @@ typedef struct gprx_model gprx_model;
 typedef struct gprx_fit_info {
     double logdet;       /* log det(K + sigma^2 I) = 2 sum log L_ii (exact, not clamped) */
     double datafit;      /* sum over outputs of y^T (K + sigma^2 I)^{-1} y */
-    int32_t info;        /* 0, or the 1-based column of the first non-positive pivot */
-    int32_t method;      /* 0 = Cholesky (potrf/potrs), 1 = LU fallback */
+    int32_t info;        /* 0, or the 1-based column of the first non-positive Cholesky pivot */
+    int32_t method;      /* 0 = Cholesky (potrf/potrs), 1 = LU fallback (the Cholesky failed) */
     double ms_build;     /* device time of the covariance build (HIP events) */
     double ms_factor;    /* device time of the factorisation */
     double ms_solve;     /* device time of the regression-vector solve */
@@ -148,7 +148,13 @@ gprx_status gprx_model_set_kernel(gprx_model* model, const gprx_kernel_desc* ker
 gprx_status gprx_model_set_noise(gprx_model* model, double sigma);
 
 #define GPRX_FIT_DEFAULT 0u
-#define GPRX_FIT_NO_LU_FALLBACK 1u /* reserved: the device path always reports NOT_SPD (no LU) */
+#define GPRX_FIT_NO_LU_FALLBACK 1u /* report NOT_SPD instead of refactoring with LU.  By default a
+                                      fit whose Cholesky meets a non-positive pivot is redone with
+                                      a partial-pivot LU in double (the reference's default
+                                      FullPivotLU = dgetrf_, include/LAPACKUtils.h:38-56,85-97);
+                                      gprx_fit_info.method = 1 then.  An exactly singular matrix
+                                      gives GPRX_ERR_SINGULAR (the reference returns non-finite
+                                      regression vectors there) */
 #define GPRX_FIT_DISTRIBUTED 2u    /* multi-GPU factorisation on a gprx_ctx_create_dist context
                                       (implied when world > 1; forces the path at world = 1) */
 #define GPRX_FIT_F32_NO_REFINE 4u  /* fp32 models: skip the fp64 iterative refinement of alpha.  By
