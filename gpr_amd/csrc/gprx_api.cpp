@@ -250,7 +250,7 @@ struct gprx_model {
     // LU fallback state (k_getrf.hip), double for both scalar types: the factored matrix,
     // pivots, the 128-block inverses of L and U, and scratch
     int method = 0;  // factor of the current fit: 0 Cholesky (A, Linv), 1 LU (lu, ipiv, luL, luU)
-    DevBuf lu, ipiv, luL, luU, luT1, luUt, luB, lured;
+    DevBuf lu, ipiv, luUt, luB, lured;
     double lu_sign = 1;  // sign of det(K + sigma^2 I) from the LU
     std::mutex mu;
 };
@@ -427,20 +427,15 @@ static void lu_fit(gprx_model* M, gprx_fit_info* out) {
     GPRX_HIP(hipEventRecord(ctx->ev[0], s));
     lu_build_matrix<T>(M);
     M->ipiv.ensure(sizeof(int) * np);
-    M->luL.ensure(sizeof(double) * np * DB);
-    M->luU.ensure(sizeof(double) * np * DB);
-    M->luT1.ensure(sizeof(double) * np * DB);
     M->luUt.ensure(sizeof(double) * np * DB);
     M->luB.ensure(sizeof(double) * np * m);
     M->lured.ensure(sizeof(double) * 4);
     GPRX_HIP(hipMemsetD32Async((hipDeviceptr_t)M->info.p, INT_MAX, 1, s));
     GPRX_HIP(hipEventRecord(ctx->ev[1], s));
-    lu_factor(M->lu.as<double>(), np, np, M->ipiv.as<int>(), M->info.as<int>(), M->luL.as<double>(),
-              M->luU.as<double>(), M->luT1.as<double>(), M->luUt.as<double>(), s);
+    lu_factor(M->lu.as<double>(), np, np, M->ipiv.as<int>(), M->info.as<int>(), M->luUt.as<double>(), s);
     GPRX_HIP(hipEventRecord(ctx->ev[2], s));
     lu_rhs_from_rows<T>(M->Y.as<T>(), n, m, M->luB.as<double>(), np, np, s);
-    lu_solve(M->lu.as<double>(), np, np, M->ipiv.as<int>(), M->luL.as<double>(), M->luU.as<double>(),
-             M->luB.as<double>(), np, m, s);
+    lu_solve(M->lu.as<double>(), np, np, M->ipiv.as<int>(), M->luB.as<double>(), np, m, s);
     M->alpha.ensure(sizeof(T) * np * m);
     lu_rows_from_rhs<T>(M->luB.as<double>(), np, n, m, M->alpha.as<T>(), s);
     lu_logdet(M->lu.as<double>(), np, n, M->ipiv.as<int>(), M->lured.as<double>(), s);
@@ -483,8 +478,7 @@ static void lu_fit(gprx_model* M, gprx_fit_info* out) {
 
 // A^{-1} B for m right-hand sides already in M->luB-shaped column-major storage (np x m)
 static void lu_solve_model(gprx_model* M, double* B, int m) {
-    lu_solve(M->lu.as<double>(), M->np, M->np, M->ipiv.as<int>(), M->luL.as<double>(), M->luU.as<double>(), B, M->np,
-             m, M->ctx->stream);
+    lu_solve(M->lu.as<double>(), M->np, M->np, M->ipiv.as<int>(), B, M->np, m, M->ctx->stream);
 }
 
 // ---------------------------------------------------------------------------------------

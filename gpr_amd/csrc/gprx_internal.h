@@ -447,13 +447,11 @@ void launch_predict(const KCanon<T>& K, const T* X, const T* tabX, int64_t n, in
 
 // LU with partial pivoting, always in double (k_getrf.hip): the fallback when the Cholesky
 // reports a non-positive pivot, as the reference's default LU inverse (include/LAPACKUtils.h
-// :38-56, 85-97).  A: np x np column-major (np a multiple of 128, identity padding); Li, Ui:
-// np/128 inverses of the 128-blocks of L (unit lower) and U; T1, Ut: np x 128 scratch each.
-void lu_factor(double* A, int64_t ld, int64_t np, int* ipiv, int* info, double* Li, double* Ui, double* T1,
-               double* Ut, hipStream_t s);
+// :38-56, 85-97).  A: np x np column-major (np a multiple of 128, identity padding); Ut: np x
+// 128 scratch.
+void lu_factor(double* A, int64_t ld, int64_t np, int* ipiv, int* info, double* Ut, hipStream_t s);
 // B (np x m, column-major, ldb) <- A^{-1} B
-void lu_solve(const double* A, int64_t ld, int64_t np, const int* ipiv, const double* Li, const double* Ui, double* B,
-              int64_t ldb, int m, hipStream_t s);
+void lu_solve(const double* A, int64_t ld, int64_t np, const int* ipiv, double* B, int64_t ldb, int m, hipStream_t s);
 template <typename T>
 void lu_rhs_from_rows(const T* Y, int64_t n, int m, double* B, int64_t ldb, int64_t np, hipStream_t s);
 template <typename T>

@@ -13,15 +13,14 @@
 // Blocked right-looking getrf, panel width 128 (the MFMA gemm tile):
 //   panel    one workgroup factors the (np - k0) x 128 panel column by column: pivot search
 //            (max |a|, lowest row on ties, as idamax), row swap inside the panel, scaling by
-//            the reciprocal pivot (dgetf2), rank-1 update of the panel's remaining columns;
-//            then the inverses of its unit-lower L11 and upper U11 blocks (used by the solves
-//            and by the U12 step)
+//            the reciprocal pivot (dgetf2), rank-1 update of the panel's remaining columns
 //   laswp    the panel's swaps applied to every other column
-//   U12      = L11^{-1} A12, A22 -= L21 U12 on the MFMA gemm (launch_gemm_nt, through
-//            transposed copies of A12 / U12)
-// Solves with m right-hand sides (column-major B): B = P B, then per 128-block
-//   B_k = L_kk^{-1} B_k, B_>k -= L_>k,k B_k (forward) and B_k = U_kk^{-1} B_k,
-//   B_<k -= U_<k,k B_k (backward).
+//   U12      = L11^{-1} A12 by substitution (dtrsm), A22 -= L21 U12 on the MFMA gemm
+//            (launch_gemm_nt, through a transposed copy of U12)
+// Solves with m right-hand sides (column-major B): B = P B, then per 128-block a
+// substitution with the diagonal block and a block update of the rest (forward with the
+// unit-lower L, backward with U) -- no explicit block inverses anywhere, so the solve keeps
+// LU's backward stability on the near-singular matrices this fallback is for.
 #include "gprx_internal.h"
 
 namespace gprx {
@@ -30,15 +29,12 @@ namespace lu {
 
 constexpr int NB = 128;       // panel width = diagonal block edge
 constexpr int PT = 1024;      // panel workgroup
-constexpr int SLD = NB + 1;   // LDS row stride of the 128 x 128 block image
 
 // One panel: columns k0 .. k0 + NB of A (np x np, column-major, ld), rows k0 .. np.
 // ipiv[j] = the (0-based) row swapped with row j; info: first column with a zero pivot
-// (1-based, atomicMin).  Li, Ui: NB x NB column-major inverses of the unit-lower L11 and the
-// upper U11 of the factored top block.
+// (1-based, atomicMin).
 __global__ __launch_bounds__(PT) void panel_kernel(double* __restrict__ A, int64_t ld, int64_t np, int64_t k0,
-                                                   int* __restrict__ ipiv, int* __restrict__ info,
-                                                   double* __restrict__ Li, double* __restrict__ Ui) {
+                                                   int* __restrict__ ipiv, int* __restrict__ info) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     double* sU = reinterpret_cast<double*>(smem_raw);        // pivot row segment (NB)
     double* sv = sU + NB;                                    // per-wave maxima (PT / 64)
@@ -110,34 +106,6 @@ __global__ __launch_bounds__(PT) void panel_kernel(double* __restrict__ A, int64
             }
         }
         __syncthreads();
-    }
-    // ---- inverses of L11 (unit lower) and U11 (upper), NB x NB column-major --------------
-    double(*sB)[SLD] = reinterpret_cast<double(*)[SLD]>(smem_raw);  // sB[col][row]
-    for (int e = t; e < NB * NB; e += PT) {
-        const int r = e & (NB - 1), c = e >> 7;
-        sB[c][r] = A[k0 + r + (k0 + c) * ld];
-    }
-    __syncthreads();
-    if (t < NB) {  // column c of L11^{-1}: x_c = 1, x_i = -sum_{c<=k<i} L_ik x_k
-        const int c = t;
-        double* x = Li + (int64_t)c * NB;
-        for (int i = 0; i < c; i++) x[i] = 0.0;
-        x[c] = 1.0;
-        for (int i = c + 1; i < NB; i++) {
-            double s = 0.0;
-            for (int k = c; k < i; k++) s = fma(sB[k][i], x[k], s);
-            x[i] = -s;
-        }
-    } else if (t < 2 * NB) {  // column c of U11^{-1}: x_c = 1/U_cc, x_i = -(sum_{i<k<=c} U_ik x_k)/U_ii
-        const int c = t - NB;
-        double* x = Ui + (int64_t)c * NB;
-        for (int i = c + 1; i < NB; i++) x[i] = 0.0;
-        x[c] = 1.0 / sB[c][c];
-        for (int i = c - 1; i >= 0; i--) {
-            double s = 0.0;
-            for (int k = i + 1; k <= c; k++) s = fma(sB[k][i], x[k], s);
-            x[i] = -s / sB[i][i];
-        }
     }
 }
 
@@ -226,27 +194,47 @@ __global__ void apply_pivots_kernel(double* __restrict__ B, int64_t ldb, int64_t
 
 constexpr int SC = 8;  // right-hand sides per workgroup in the solve kernels
 
-// B[r0 .. r0 + NB, :] = Tinv (NB x NB) B[r0 .. r0 + NB, :]
-__global__ __launch_bounds__(256) void tri_apply_kernel(const double* __restrict__ Tinv, double* __restrict__ B,
-                                                        int64_t ldb, int64_t r0, int m) {
-    __shared__ double sb[SC][NB];
-    const int t = threadIdx.x, c0 = blockIdx.x * SC;
-    for (int e = t; e < SC * NB; e += 256) {
-        const int cc = e / NB, r = e % NB;
-        sb[cc][r] = (c0 + cc < m) ? B[r0 + r + (int64_t)(c0 + cc) * ldb] : 0.0;
+// B[r0 .. r0 + NB, :] <- T^{-1} B[r0 .. r0 + NB, :] by substitution with the diagonal block
+// T = A[r0 .., r0 ..] (upper: U with its diagonal; else unit lower L), as dtrsm does: explicit
+// inverses of the blocks would lose backward stability when U is ill conditioned (the
+// singular-kernel fits this fallback exists for).  One thread per row, SC right-hand sides
+// per workgroup; each step publishes one solved row through LDS.
+__global__ __launch_bounds__(NB) void tri_solve_kernel(const double* __restrict__ A, int64_t ld, int64_t r0,
+                                                       double* __restrict__ B, int64_t ldb, int m, int upper) {
+    __shared__ double sx[SC];
+    const int k = threadIdx.x, c0 = blockIdx.x * SC;
+    double b[SC];
+    for (int u = 0; u < SC; u++) b[u] = (c0 + u < m) ? B[r0 + k + (int64_t)(c0 + u) * ldb] : 0.0;
+    const double* Ad = A + r0 + r0 * ld;  // the diagonal block, column-major
+    if (upper) {
+        const double ukk = Ad[k + (int64_t)k * ld];
+        for (int i = NB - 1; i >= 0; i--) {
+            if (k == i)
+                for (int u = 0; u < SC; u++) {
+                    b[u] = b[u] / ukk;
+                    sx[u] = b[u];
+                }
+            __syncthreads();
+            if (k < i) {
+                const double a = Ad[k + (int64_t)i * ld];
+                for (int u = 0; u < SC; u++) b[u] = fma(-a, sx[u], b[u]);
+            }
+            __syncthreads();
+        }
+    } else {
+        for (int i = 0; i < NB; i++) {
+            if (k == i)
+                for (int u = 0; u < SC; u++) sx[u] = b[u];
+            __syncthreads();
+            if (k > i) {
+                const double a = Ad[k + (int64_t)i * ld];
+                for (int u = 0; u < SC; u++) b[u] = fma(-a, sx[u], b[u]);
+            }
+            __syncthreads();
+        }
     }
-    __syncthreads();
-    const int i = t & (NB - 1), ch = t >> 7;  // row i, columns ch, ch + 2, ...
-    double acc[SC / 2];
-    for (int u = 0; u < SC / 2; u++) acc[u] = 0.0;
-    for (int k = 0; k < NB; k++) {
-        const double a = Tinv[i + k * NB];
-        for (int u = 0; u < SC / 2; u++) acc[u] = fma(a, sb[ch + 2 * u][k], acc[u]);
-    }
-    for (int u = 0; u < SC / 2; u++) {
-        const int cc = c0 + ch + 2 * u;
-        if (cc < m) B[r0 + i + (int64_t)cc * ldb] = acc[u];
-    }
+    for (int u = 0; u < SC; u++)
+        if (c0 + u < m) B[r0 + k + (int64_t)(c0 + u) * ldb] = b[u];
 }
 
 // B[r, :] -= sum_k A[r, c0 + k] B[c0 + k, :] for r in [rb, re)
@@ -326,37 +314,28 @@ __global__ __launch_bounds__(256) void coldot_kernel(const double* __restrict__ 
 
 }  // namespace lu
 
-static size_t lu_panel_lds() { return sizeof(double) * (size_t)lu::NB * lu::SLD + 256; }
+static size_t lu_panel_lds() { return sizeof(double) * (lu::NB + lu::PT / 64) + sizeof(int) * (lu::PT / 64 + 4); }
 
 // In-place LU with partial pivoting of the np x np column-major A (np a multiple of 128,
-// padding rows/columns the identity).  Li, Ui: np/128 blocks of 128 x 128; T1, Ut: scratch of
-// np x 128 each.  info: device int (INT_MAX = no zero pivot).
-void lu_factor(double* A, int64_t ld, int64_t np, int* ipiv, int* info, double* Li, double* Ui, double* T1,
-               double* Ut, hipStream_t s) {
+// padding rows/columns the identity).  Ut: np x 128 scratch.  info: device int (INT_MAX = no
+// zero pivot).
+void lu_factor(double* A, int64_t ld, int64_t np, int* ipiv, int* info, double* Ut, hipStream_t s) {
     using namespace lu;
     GPRX_REQUIRE(np % NB == 0, GPRX_ERR_ARG, "lu_factor: np must be a multiple of 128");
-    static bool attr = false;
-    if (!attr) {
-        GPRX_HIP(hipFuncSetAttribute((const void*)panel_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     (int)lu_panel_lds()));
-        attr = true;
-    }
     ProfScope ps(KC_OTHER, s, 2.0 / 3.0 * (double)np * np * np, 0.0);
     for (int64_t k0 = 0; k0 < np; k0 += NB) {
-        const int64_t kb = k0 / NB;
-        hipLaunchKernelGGL(panel_kernel, dim3(1), dim3(PT), lu_panel_lds(), s, A, ld, np, k0, ipiv, info,
-                           Li + kb * NB * NB, Ui + kb * NB * NB);
+        hipLaunchKernelGGL(panel_kernel, dim3(1), dim3(PT), lu_panel_lds(), s, A, ld, np, k0, ipiv, info);
         if (np > NB)
             hipLaunchKernelGGL(laswp_kernel, dim3((unsigned)((np - NB + 255) / 256)), dim3(256), 0, s, A, ld, np, k0,
                                (const int*)ipiv);
         const int64_t rest = np - k0 - NB;
         if (rest <= 0) continue;
-        // U12 = L11^{-1} A12 as its transpose Ut = A12^T L11^{-T} (gemm_nt: C = A B^T)
+        // U12 = L11^{-1} A12 in place (substitution, as dgetrf's dtrsm), then its transpose Ut
+        // as the gemm_nt operand: A22 -= L21 U12 = L21 Ut^T on the MFMA tile gemm
+        hipLaunchKernelGGL(tri_solve_kernel, dim3((unsigned)((rest + SC - 1) / SC)), dim3(NB), 0, s, (const double*)A,
+                           ld, k0, A + (k0 + NB) * ld, ld, (int)rest, 0);
         const dim3 tg((unsigned)(NB / 32), (unsigned)((rest + 31) / 32));
-        hipLaunchKernelGGL(transpose_block_kernel, tg, dim3(256), 0, s, A, ld, k0, k0 + NB, rest, T1, rest, 0);
-        launch_gemm_nt<double>(Ut, rest, T1, rest, Li + kb * NB * NB, NB, rest, NB, NB, 1.0, 0.0, false, s);
-        hipLaunchKernelGGL(transpose_block_kernel, tg, dim3(256), 0, s, A, ld, k0, k0 + NB, rest, Ut, rest, 1);
-        // A22 -= L21 U12 = L21 Ut^T
+        hipLaunchKernelGGL(transpose_block_kernel, tg, dim3(256), 0, s, A, ld, k0, k0 + NB, rest, Ut, rest, 0);
         launch_gemm_nt<double>(A + (k0 + NB) + (k0 + NB) * ld, ld, A + (k0 + NB) + k0 * ld, ld, Ut, rest, rest, rest,
                                NB, -1.0, 1.0, false, s);
     }
@@ -364,8 +343,7 @@ void lu_factor(double* A, int64_t ld, int64_t np, int* ipiv, int* info, double* 
 }
 
 // B (np x m, column-major, ldb) <- A^{-1} B with the factors of lu_factor
-void lu_solve(const double* A, int64_t ld, int64_t np, const int* ipiv, const double* Li, const double* Ui, double* B,
-              int64_t ldb, int m, hipStream_t s) {
+void lu_solve(const double* A, int64_t ld, int64_t np, const int* ipiv, double* B, int64_t ldb, int m, hipStream_t s) {
     using namespace lu;
     if (m <= 0) return;
     hipLaunchKernelGGL(apply_pivots_kernel, dim3((unsigned)((m + 63) / 64)), dim3(64), 0, s, B, ldb, np, m, ipiv);
@@ -373,7 +351,7 @@ void lu_solve(const double* A, int64_t ld, int64_t np, const int* ipiv, const do
     const int64_t nbk = np / NB;
     for (int64_t kb = 0; kb < nbk; kb++) {
         const int64_t r0 = kb * NB;
-        hipLaunchKernelGGL(tri_apply_kernel, dim3(gc), dim3(256), 0, s, Li + kb * NB * NB, B, ldb, r0, m);
+        hipLaunchKernelGGL(tri_solve_kernel, dim3(gc), dim3(NB), 0, s, A, ld, r0, B, ldb, m, 0);
         const int64_t rb = r0 + NB;
         if (rb < np)
             hipLaunchKernelGGL(block_update_kernel, dim3((unsigned)((np - rb + 255) / 256), gc), dim3(256), 0, s, A, ld,
@@ -381,7 +359,7 @@ void lu_solve(const double* A, int64_t ld, int64_t np, const int* ipiv, const do
     }
     for (int64_t kb = nbk - 1; kb >= 0; kb--) {
         const int64_t r0 = kb * NB;
-        hipLaunchKernelGGL(tri_apply_kernel, dim3(gc), dim3(256), 0, s, Ui + kb * NB * NB, B, ldb, r0, m);
+        hipLaunchKernelGGL(tri_solve_kernel, dim3(gc), dim3(NB), 0, s, A, ld, r0, B, ldb, m, 1);
         if (r0 > 0)
             hipLaunchKernelGGL(block_update_kernel, dim3((unsigned)((r0 + 255) / 256), gc), dim3(256), 0, s, A, ld, B,
                                ldb, (int64_t)0, r0, r0, m);

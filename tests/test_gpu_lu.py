@@ -33,7 +33,7 @@ def _model(ctx, ks, X, Y, sigma, dtype=np.float64):
     return M
 
 
-@pytest.mark.parametrize("n,d,m", [(700, 3, 2), (1500, 3, 1), (130, 3, 1)])
+@pytest.mark.parametrize("n,d,m", [(700, 3, 2), (1500, 3, 1), (260, 3, 1)])
 def test_lu_fallback_indefinite_f64(ctx, n, d, m):
     sigma = 0.3
     X, Y = make_data(n, d, m)
@@ -116,8 +116,9 @@ def test_lu_after_cholesky_model_switches_back(ctx):
 @pytest.mark.parametrize("N", [50, 200])
 def test_lu_fallback_singular_sigma0(ctx, N):
     """tests/GaussianProcessTest.cpp:35-76 at N = 50 and 200 (sigma = 0, Gaussian(2.889)):
-    the Cholesky of the numerically singular K fails, the LU solves it with a backward error
-    of order eps, as the reference's dgetrf_ does (its own alpha satisfies the same bound)."""
+    the Cholesky of the numerically singular K fails and the LU solves it with a normwise
+    backward error of order eps, as dgetrf_ + dgetrs_ guarantee (scipy's LU reaches 1e-17
+    here; the reference's own route, the explicit dgetri_ inverse times Y, only 1e-11)."""
     ks = "GaussianKernel(2.889,1,)"
     x = np.array([[i * 2 * np.pi / N] for i in range(N)])
     y = np.sin(x)
@@ -126,19 +127,17 @@ def test_lu_fallback_singular_sigma0(ctx, N):
     assert info.method == 1
     a = M.alpha()
     K = O.kernel_matrix(ks, x)
-    bound = lambda al: np.max(np.abs(K @ al - y)) / (np.max(np.abs(K).sum(1)) * np.max(np.abs(al)))
-    assert bound(a) <= 1e-13
-    a_ref, _ = O.fit(ks, x, y, 0.0)
-    assert bound(a_ref) <= 1e-13
+    berr = np.max(np.abs(K @ a - y)) / (np.max(np.abs(K).sum(1)) * np.max(np.abs(a)))
+    assert berr <= 1e-15, berr
     M.close()
 
 
 def test_exactly_singular_raises(ctx):
-    """Duplicated samples with sigma = 0: identical rows give an exact zero pivot."""
+    """A zero kernel (RationalQuadraticKernel with scale 0, no validation in the reference)
+    and sigma = 0: K = 0, the LU's first pivot is exactly zero."""
     import gpr_amd
     X, Y = make_data(150, 2, 1)
-    X[77] = X[12]
-    M = _model(ctx, "GaussianKernel(0.7,1,)", X, Y, 0.0)
+    M = _model(ctx, "RationalQuadraticKernel(0,1,1,)", X, Y, 0.0)
     with pytest.raises(gpr_amd.GprxError) as e:
         M.fit()
     assert e.value.status == 3  # SINGULAR
