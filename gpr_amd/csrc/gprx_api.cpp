@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <chrono>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -14,6 +15,7 @@
 #include <type_traits>
 #include <vector>
 
+#include "gprx_dist.h"
 #include "gprx_internal.h"
 #include "../../include/gprx_dev.h"
 
@@ -202,6 +204,7 @@ static void check_sched(int hinfo) {
 struct gprx_ctx {
     int device = 0;
     int rank = 0, world = 1;
+    bool virt = false;          // gprx_ctx_create_virtual: world virtual ranks in this process
     ncclComm_t comm = nullptr;  // RCCL communicator (gprx_ctx_create_dist), world > 1
     hipStream_t stream = nullptr;
     hipStream_t aux = nullptr;  // look-ahead stream of the factorisation
@@ -252,7 +255,12 @@ struct gprx_model {
     int method = 0;  // factor of the current fit: 0 Cholesky (A, Linv), 1 LU (lu, ipiv, luL, luU)
     DevBuf lu, ipiv, luUt, luB, lured;
     double lu_sign = 1;  // sign of det(K + sigma^2 I) from the LU
+    // distributed fit (gprx_dist.cpp): the engine (per-rank buffers, schedules) and whether
+    // the current fit is one (its factor is held in tiles per rank: alpha and predict only)
+    DistEngineBase* dist_engine = nullptr;
+    bool dist_fitted = false;
     std::mutex mu;
+    ~gprx_model() { dist_engine_free(dist_engine); }
 };
 
 // Every model call holds its context's mutex, then the model's (always in that order): the
@@ -482,6 +490,73 @@ static void lu_solve_model(gprx_model* M, double* B, int m) {
 }
 
 // ---------------------------------------------------------------------------------------
+// distributed fit (gprx_dist.cpp): row blocks dealt over the ranks, one persistent tile
+// launch per rank, RCCL broadcast of each diagonal inverse and full-mesh panel exchange
+// ---------------------------------------------------------------------------------------
+template <typename T>
+static gprx_status model_fit_dist(gprx_model* M, gprx_fit_info* out) {
+    gprx_ctx* ctx = M->ctx;
+    hipStream_t s = ctx->stream;
+    const KCanon<T>& K = kcanon<T>(M);
+    const int64_t n = M->n, np = round_up(n, DB);
+    M->np = np;
+    M->mp = GT;
+    M->ld = 0;
+    M->fitted = M->has_alpha = M->inv_ready = M->dist_fitted = false;
+    M->alpha.ensure(sizeof(T) * np * M->m);
+    M->flag.ensure(sizeof(int));
+    GPRX_HIP(hipMemsetAsync(M->flag.p, 0, sizeof(int), s));
+    const T sig = (T)M->sigma;
+    const T sigma2 = sig * sig;  // m_Sigma*m_Sigma in T (lib/GaussianProcess.cpp:379)
+    TileBuild<T> tb;
+    std::memset(&tb, 0, sizeof(tb));
+    if (pairs_mma_supported<T>(K, 1)) {  // the fused MFMA build: features of all n samples on every rank
+        const int64_t kf = pairs_feature_cols<T>(K, M->d);
+        M->featU.ensure(sizeof(T) * np * kf);
+        M->featV.ensure(sizeof(T) * np * kf);
+        launch_pair_features<T>(K, M->X.as<T>(), n, M->d, M->X.as<T>(), false, M->featU.as<T>(), np, s,
+                                M->flag.as<int>());
+        launch_pair_features<T>(K, M->X.as<T>(), n, M->d, M->X.as<T>(), true, M->featV.as<T>(), np, s);
+        M->kdev.ensure(sizeof(KCanon<T>));
+        GPRX_HIP(hipMemcpyAsync(M->kdev.p, &K, sizeof(KCanon<T>), hipMemcpyHostToDevice, s));
+        tb = pairs_tile_build<T>(K, M->kdev.as<KCanon<T>>(), M->featU.as<T>(), M->featV.as<T>(), np, M->d, n, sigma2,
+                                 M->flag.as<int>());
+    }
+    GPRX_HIP(hipStreamSynchronize(s));  // the ranks' streams read the features
+    int hflag = 0;
+    GPRX_HIP(hipMemcpy(&hflag, M->flag.p, sizeof(int), hipMemcpyDeviceToHost));
+    DistContext C;
+    C.device = ctx->device;
+    C.rank = ctx->rank;
+    C.world = ctx->world;
+    C.virt = ctx->virt;
+    C.comm = ctx->comm;
+    C.stream = s;
+    DistFitIn<T> in{K, M->X.as<T>(), M->Y.as<T>(), n, M->d, M->m, sigma2, tb};
+    DistFitOut o;
+    const auto t0 = std::chrono::steady_clock::now();
+    dist_fit<T>(M->dist_engine, C, in, o, M->alpha.as<T>(), ctx->ex);
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (out) {
+        std::memset(out, 0, sizeof(*out));
+        out->logdet = o.logdet;
+        out->datafit = o.datafit;
+        out->info = (o.info == INT_MAX || o.info < 0) ? 0 : o.info;
+        out->ms_factor = ms;  // host wall time of the whole distributed fit
+    }
+    if (hflag || o.flag)
+        throw Error{GPRX_ERR_NONFINITE,
+                    "GaussianProcess::ComputeKernelMatrixInternal: kernel matrix contains entries which are not finite."};
+    check_sched(o.info);
+    if (o.info != INT_MAX)
+        throw Error{GPRX_ERR_NOT_SPD, "gprx: kernel matrix is not positive definite (Cholesky pivot " +
+                                          std::to_string(o.info) + " <= 0; no LU fallback on the distributed path)"};
+    M->method = 0;
+    M->fitted = M->has_alpha = M->dist_fitted = true;
+    return GPRX_OK;
+}
+
+// ---------------------------------------------------------------------------------------
 // fit
 // ---------------------------------------------------------------------------------------
 template <typename T>
@@ -492,14 +567,18 @@ static gprx_status model_fit(gprx_model* M, uint32_t flags, gprx_fit_info* out) 
     GPRX_HIP(hipSetDevice(ctx->device));
     hipStream_t s = ctx->stream;
     const KCanon<T>& K = kcanon<T>(M);
-    // multi-GPU factorisation on an RCCL context (GPRX_FIT_DISTRIBUTED forces the same code
-    // path on a one-rank communicator)
-    const bool dist = (ctx->comm && ctx->world > 1) || ((flags & GPRX_FIT_DISTRIBUTED) && ctx->comm);
-    GPRX_REQUIRE(!(flags & GPRX_FIT_DISTRIBUTED) || ctx->comm, GPRX_ERR_STATE,
+    // multi-GPU factorisation: an RCCL context with world > 1, a virtual-rank context, or
+    // GPRX_FIT_DISTRIBUTED (the same code path on a one-rank communicator)
+    GPRX_REQUIRE(!(flags & GPRX_FIT_DISTRIBUTED) || ctx->comm || ctx->virt, GPRX_ERR_STATE,
                  "gprx_model_fit: GPRX_FIT_DISTRIBUTED needs a context from gprx_ctx_create_dist");
-    const int64_t n = M->n, np = round_up(n, dist ? (int64_t)outer_block() : (int64_t)DB), mp = round_up(M->m, GT);
+    if ((ctx->comm && ctx->world > 1) || ctx->virt || (flags & GPRX_FIT_DISTRIBUTED)) {
+        GPRX_REQUIRE(!M->want_inv, GPRX_ERR_STATE, "gprx: the log-likelihood gradient is not available on a distributed fit");
+        return model_fit_dist<T>(M, out);
+    }
+    M->dist_fitted = false;
+    const int64_t n = M->n, np = round_up(n, (int64_t)DB), mp = round_up(M->m, GT);
     // the explicit inverse rides along in the tile factorisation as np identity rows
-    const bool want_inv = M->want_inv && !dist && potrf_uses_tiles();
+    const bool want_inv = M->want_inv && potrf_uses_tiles();
     const int64_t ld = np + mp + (want_inv ? np : 0);
     M->inv_ready = false;
     M->np = np;
@@ -528,7 +607,7 @@ static gprx_status model_fit(gprx_model* M, uint32_t flags, gprx_fit_info* out) 
         std::getenv("GPRX_KBUILD") && std::string(std::getenv("GPRX_KBUILD")) == "separate";
     TileBuild<T> tb;
     std::memset(&tb, 0, sizeof(tb));
-    if ((!dist || ctx->world == 1) && !direct_build && pairs_mma_supported<T>(K, 1)) {
+    if (!direct_build && pairs_mma_supported<T>(K, 1)) {
         // pair statistics on the MFMA units from per-sample features (k_pairs.hip)
         const int64_t kf = pairs_feature_cols<T>(K, M->d);
         M->featU.ensure(sizeof(T) * np * kf);
@@ -538,56 +617,20 @@ static gprx_status model_fit(gprx_model* M, uint32_t flags, gprx_fit_info* out) 
         launch_pair_features<T>(K, M->X.as<T>(), n, M->d, M->X.as<T>(), true, M->featV.as<T>(), np, s);
         M->kdev.ensure(sizeof(KCanon<T>));
         GPRX_HIP(hipMemcpyAsync(M->kdev.p, &K, sizeof(KCanon<T>), hipMemcpyHostToDevice, s));
-        if (!dist && !separate_build && potrf_uses_tiles())
+        if (!separate_build && potrf_uses_tiles())
             tb = pairs_tile_build<T>(K, M->kdev.as<KCanon<T>>(), M->featU.as<T>(), M->featV.as<T>(), np, M->d, n, sigma2,
                                      M->flag.as<int>());
         if (!tb.mode)
             launch_kbuild_mma<T>(K, M->kdev.as<KCanon<T>>(), M->featU.as<T>(), M->featV.as<T>(), np, M->d, M->A.as<T>(),
                                  ld, n, sigma2, M->flag.as<int>(), s);
         launch_aug_rows<T>(M->Y.as<T>(), n, M->m, M->A.as<T>(), ld, np, mp, s);
-    } else if (!dist || ctx->world == 1) {
+    } else {
         launch_kbuild<T>(K, M->X.as<T>(), M->tab.as<T>(), n, M->X.as<T>(), M->tab.as<T>(), n, M->d, M->A.as<T>(), ld,
                          np, true, sigma2, M->flag.as<int>(), s);
         launch_aug_rows<T>(M->Y.as<T>(), n, M->m, M->A.as<T>(), ld, np, mp, s);
-    } else {
-        // sharded build: each rank builds only the column panels it owns (rows c0.. of the
-        // lower triangle, the diagonal noise/padding and the label rows)
-        const int64_t NBO = outer_block(), d = M->d;
-        DevBuf tr, tc;
-        for (int64_t Kp = ctx->rank; Kp * NBO < np; Kp += ctx->world) {
-            const int64_t c0 = Kp * NBO;
-            T* Ap = M->A.as<T>() + c0 * ld;
-            GPRX_HIP(hipMemset2DAsync(Ap + c0, sizeof(T) * ld, 0, sizeof(T) * (ld - c0), NBO, s));
-            const int64_t nr = std::max<int64_t>(0, n - c0), nc = std::min<int64_t>(NBO, nr);
-            if (nc > 0) {
-                const T* tabr = nullptr;
-                const T* tabc = nullptr;
-                if (K.nper > 0) {
-                    tr.ensure(sizeof(T) * 2 * K.nper * nr * d);
-                    tc.ensure(sizeof(T) * 2 * K.nper * nc * d);
-                    launch_sincos_tables<T>(K, M->X.as<T>() + c0 * d, nr, (int)d, tr.as<T>(), s);
-                    launch_sincos_tables<T>(K, M->X.as<T>() + c0 * d, nc, (int)d, tc.as<T>(), s);
-                    tabr = tr.as<T>();
-                    tabc = tc.as<T>();
-                }
-                launch_kbuild<T>(K, M->X.as<T>() + c0 * d, tabr, nr, M->X.as<T>() + c0 * d, tabc, nc, (int)d, Ap + c0,
-                                 ld, 0, false, T(0), M->flag.as<int>(), s);
-            }
-            launch_diag_fix<T>(M->A.as<T>(), ld, c0, NBO, n, sigma2, s);
-            launch_label_rows<T>(M->Y.as<T>() + c0 * M->m, nc, M->m, Ap, ld, np, NBO, mp, s);
-            if (K.nper > 0) GPRX_HIP(hipStreamSynchronize(s));  // tr/tc reused next panel
-        }
     }
     GPRX_HIP(hipEventRecord(ctx->ev[1], s));
-    if (dist) {
-        M->pack.ensure(sizeof(T) * ld * outer_block());
-        potrf_dist<T>(M->A.as<T>(), ld, np, ld, M->Linv.as<T>(), M->info.as<int>(), ctx->ex, ctx->comm, ctx->rank,
-                      ctx->world, M->pack.as<T>());
-        if (ctx->world > 1) {  // the non-finite flag of every rank's panels
-            const ncclResult_t r = ncclAllReduce(M->flag.p, M->flag.p, 1, ncclInt32, ncclMax, ctx->comm, s);
-            if (r != ncclSuccess) throw Error{GPRX_ERR_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(r)};
-        }
-    } else if (tb.mode || want_inv) {
+    if (tb.mode || want_inv) {
         potrf_tiles<T>(M->A.as<T>(), ld, np, ld, M->Linv.as<T>(), M->info.as<int>(), ctx->ex, tb.mode ? &tb : nullptr,
                        want_inv ? (int)(np / GT) : 0);
     } else {
@@ -634,7 +677,7 @@ static gprx_status model_fit(gprx_model* M, uint32_t flags, gprx_fit_info* out) 
     if (hinfo != INT_MAX) {
         // the reference's default inversion is an LU (lib/GaussianProcess.cpp:545-559): refactor
         // the same matrix with partial pivoting instead of rejecting it
-        if (!(flags & GPRX_FIT_NO_LU_FALLBACK) && !dist) {
+        if (!(flags & GPRX_FIT_NO_LU_FALLBACK)) {
             lu_fit<T>(M, out);
             return GPRX_OK;
         }
@@ -648,9 +691,8 @@ static gprx_status model_fit(gprx_model* M, uint32_t flags, gprx_fit_info* out) 
     if constexpr (std::is_same<T, float>::value) {
         // the reference inverts fp32 GPs in double (include/LAPACKUtils.h:85-97): refine alpha
         // in fp64 against the fp32 factor.  Not for the LML's fit (its value and gradient come
-        // from the factor and its inverse) nor the distributed path (replicated factor, local
-        // solve: a refinement there is a later step).
-        if (!(flags & GPRX_FIT_F32_NO_REFINE) && !want_inv && !dist) refine_f32(M, out);
+        // from the factor and its inverse).
+        if (!(flags & GPRX_FIT_F32_NO_REFINE) && !want_inv) refine_f32(M, out);
     }
     return GPRX_OK;
 }
@@ -733,6 +775,8 @@ static void solve_rows_for(gprx_model* M, const T* dXq, const T* dtabQ, int64_t 
 template <typename T>
 static gprx_status model_posterior_cov(gprx_model* M, const void* Xa, const void* Xb, int64_t q, void* out) {
     GPRX_REQUIRE(M->fitted, GPRX_ERR_STATE, "GaussianProcess::ComputeKernelVectorInternal: gaussian process is not initialized.");
+    GPRX_REQUIRE(!M->dist_fitted, GPRX_ERR_STATE,
+                 "gprx: the posterior covariance needs a single-GPU fit (a distributed fit keeps its factor in tiles)");
     hipStream_t s = M->ctx->stream;
     const KCanon<T>& K = kcanon<T>(M);
     const int d = M->d;
@@ -798,6 +842,8 @@ static void lu_inverse(gprx_model* M, DevBuf& luC) {
 template <typename T>
 static gprx_status model_core_matrix(gprx_model* M, void* Cout) {
     GPRX_REQUIRE(M->fitted, GPRX_ERR_STATE, "gprx: model is not fitted");
+    GPRX_REQUIRE(!M->dist_fitted, GPRX_ERR_STATE,
+                 "gprx: the core matrix needs a single-GPU fit (a distributed fit keeps its factor in tiles)");
     hipStream_t s = M->ctx->stream;
     if (M->method == 1) {  // dgetri_'s inverse (include/LAPACKUtils.h:49) from the LU factors
         DevBuf luC;
@@ -1674,6 +1720,18 @@ gprx_status gprx_dist_unique_id(void* out) {
     const ncclResult_t r = ncclGetUniqueId(&id);
     if (r != ncclSuccess) throw Error{GPRX_ERR_RCCL, std::string("ncclGetUniqueId: ") + ncclGetErrorString(r)};
     std::memcpy(out, &id, sizeof(id));
+    return GPRX_OK;
+    API_END(nullptr)
+}
+
+gprx_status gprx_ctx_create_virtual(int device, int world, gprx_ctx** out) {
+    API_BEGIN
+    GPRX_REQUIRE(out, GPRX_ERR_ARG, "gprx_ctx_create_virtual: NULL argument");
+    GPRX_REQUIRE(world >= 1 && world <= 8, GPRX_ERR_ARG, "gprx_ctx_create_virtual: world must be 1..8");
+    gprx_ctx* ctx = ctx_new(device);
+    ctx->virt = true;
+    ctx->world = world;
+    *out = ctx;
     return GPRX_OK;
     API_END(nullptr)
 }

@@ -1,0 +1,641 @@
+// gprx_dist.cpp — the storage-sharded multi-GPU fit (north_star: "the N x N matrix shards
+// row-block across the GPUs with a broadcast of the diagonal panel at each potrf step").
+//
+// Replaces the same reference step as the single-GPU fit -- GaussianProcess::Initialize ->
+// ComputeRegressionVectors, kernel matrix + lapack::lu_invert + C Y (lib/GaussianProcess.cpp
+// :118-130, 642-672; include/LAPACKUtils.h:38-56) -- for a matrix dealt over g ranks:
+//
+//   storage   row block i (128 rows) lives on rank i mod g: N^2/g of the lower factor per
+//             rank, plus the tiles of other ranks' rows it receives (each rank ends with the
+//             whole factor, in tiles, so the solve runs locally everywhere)
+//   compute   each rank runs the persistent tile-dataflow launch (k_ptiles.hip,
+//             potrf_tiles_kernel<T, true>) over its own row blocks: covariance BUILD tasks,
+//             DIAGX (the diagonal 128-block chain), TRSM and UPD tasks, in the order of a list
+//             schedule simulated over all ranks (potrf_dist_schedule)
+//   exchange  per diagonal step k two transport steps, issued by this host thread as the
+//             device reports its pieces ready (host-visible flags the kernel stores):
+//             bcast(k)  Linv_k, the inverse of the factored diagonal block, from its rank to
+//                       all (RCCL ncclBroadcast over xGMI): the only exchange on the chain
+//             panel(k)  every final tile L_ik (i > k) from its rank to every other rank, one
+//                       message per (rank, peer) pair fused in an RCCL group: the full-mesh
+//                       all-gather of the panel, off the chain
+//             each followed by a stream write of a counter the kernel polls (uncached memory)
+//   reduce    log det (each rank's diagonal blocks) and the non-finite / pivot flags: one
+//             RCCL all-reduce each at the end
+//
+// A second transport runs g "virtual ranks" in one process on one GPU (gprx_ctx_create_virtual,
+// include/gprx_dev.h): the same kernels, buffers and issue loop, with device copies in place
+// of RCCL -- the distributed algorithm, exchange protocol and deadlock freedom testable on a
+// single GPU (tests/test_gpu_dist.py).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <chrono>
+#include <climits>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "gprx_dist.h"
+
+namespace gprx {
+
+namespace {
+
+template <typename T>
+ncclDataType_t nccl_t();
+template <>
+ncclDataType_t nccl_t<double>() {
+    return ncclFloat64;
+}
+template <>
+ncclDataType_t nccl_t<float>() {
+    return ncclFloat32;
+}
+
+void rccl_ok(ncclResult_t r, const char* what) {
+    if (r != ncclSuccess) throw Error{GPRX_ERR_RCCL, std::string(what) + ": " + ncclGetErrorString(r)};
+}
+
+// one device allocation, optionally fine-grained / uncached
+struct DMem {
+    void* p = nullptr;
+    size_t bytes = 0;
+    unsigned flags = 0;
+    void ensure(size_t b, unsigned fl = 0) {
+        if (p && b <= bytes && fl == flags) return;
+        release();
+        if (b == 0) return;
+        if (fl) GPRX_HIP(hipExtMallocWithFlags(&p, b, fl));
+        else GPRX_HIP(hipMalloc(&p, b));
+        bytes = b;
+        flags = fl;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    template <typename U>
+    U* as() const {
+        return reinterpret_cast<U*>(p);
+    }
+    ~DMem() { release(); }
+};
+
+struct HMem {  // coherent host memory the device stores to (kernel -> issue loop)
+    void* p = nullptr;
+    size_t bytes = 0;
+    void ensure(size_t b) {
+        if (p && b <= bytes) return;
+        release();
+        GPRX_HIP(hipHostMalloc(&p, b, hipHostMallocCoherent | hipHostMallocMapped));
+        bytes = b;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    unsigned* u() const { return reinterpret_cast<unsigned*>(p); }
+    ~HMem() { release(); }
+};
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------
+// layout: which rank holds which tile, where the send slots and received tiles live
+// ---------------------------------------------------------------------------------------
+struct DistLayout {
+    int g = 1, nc = 0, nr = 0;
+    int owner(int i) const { return i % g; }
+    int loc(int i) const { return i / g; }
+    int nloc(int q) const { return (nr - q + g - 1) / g; }
+    int first(int q, int b) const {  // first row block > b owned by q
+        int i = b + 1;
+        i += ((q - i % g) + g) % g;
+        return i;
+    }
+    int cnt(int q, int b) const {  // row blocks in (b, nr) owned by q
+        const int f = first(q, b);
+        return f >= nr ? 0 : (nr - 1 - f) / g + 1;
+    }
+    int pos(int q, int i, int b) const { return (i - first(q, b)) / g; }
+    // send slot offsets (tiles) of rank q: panel b after all earlier panels
+    std::vector<std::vector<int64_t>> soff;             // [q][b]
+    std::vector<std::vector<std::vector<int64_t>>> roff;  // [r][b][q]: rank r's received chunk from q
+    std::vector<int64_t> stot, rtot;
+    void init(int g_, int nc_, int nr_) {
+        g = g_;
+        nc = nc_;
+        nr = nr_;
+        soff.assign(g, std::vector<int64_t>(nc + 1, 0));
+        stot.assign(g, 0);
+        for (int q = 0; q < g; q++) {
+            int64_t o = 0;
+            for (int b = 0; b < nc; b++) {
+                soff[q][b] = o;
+                o += cnt(q, b);
+            }
+            soff[q][nc] = o;
+            stot[q] = o;
+        }
+        roff.assign(g, std::vector<std::vector<int64_t>>(nc, std::vector<int64_t>(g, -1)));
+        rtot.assign(g, 0);
+        for (int r = 0; r < g; r++) {
+            int64_t o = 0;
+            for (int b = 0; b < nc; b++)
+                for (int q = 0; q < g; q++) {
+                    if (q == r) continue;
+                    roff[r][b][q] = o;
+                    o += cnt(q, b);
+                }
+            rtot[r] = o;
+        }
+    }
+};
+
+// one rank's buffers and launch state
+template <typename T>
+struct DistRank {
+    int r = 0;
+    hipStream_t s = nullptr;  // compute stream
+    bool own_stream = false;
+    DMem A, Linv, send, recv, ctr, info, flag, pd, loc, tptr, sptr, drecv, tiles, tld, red, alpha, tab, list;
+    HMem hdiag, hslot;
+    int64_t ld = 0;
+    int ntasks = 0;
+    hipEvent_t done = nullptr;
+    ~DistRank() {
+        if (done) (void)hipEventDestroy(done);
+        if (own_stream && s) (void)hipStreamDestroy(s);
+    }
+};
+
+struct DistEngineBase {
+    virtual ~DistEngineBase() {}
+};
+
+template <typename T>
+struct DistEngine : DistEngineBase {
+    int g = 1;
+    bool virt = false;
+    int device = 0;
+    std::vector<std::unique_ptr<DistRank<T>>> ranks;  // virtual: all g; RCCL: this rank only
+    ncclComm_t commB = nullptr, commP = nullptr;       // RCCL: broadcast / panel communicators
+    bool own_commP = false;
+    hipStream_t sB = nullptr, sP = nullptr;            // transport streams
+    DistLayout L;
+    int64_t key_n = -1;
+    int key_m = -1;
+    bool key_fused = false;
+    int P = 0;
+    double est_us = 0;
+    std::vector<std::vector<int4>> lists;
+    ~DistEngine() override {
+        ranks.clear();
+        if (sB) (void)hipStreamDestroy(sB);
+        if (sP) (void)hipStreamDestroy(sP);
+        if (own_commP && commP) (void)ncclCommDestroy(commP);
+    }
+};
+
+// ---------------------------------------------------------------------------------------
+// small kernels
+// ---------------------------------------------------------------------------------------
+namespace {
+
+template <typename T>
+__global__ void diag_fix_local_kernel(T* __restrict__ A, int64_t ld, int64_t row0, int64_t c0, int64_t n, T s2) {
+    const int t = threadIdx.x;
+    if (t >= DB) return;
+    const int64_t gi = c0 + t;
+    T* p = A + row0 + t + gi * ld;
+    *p = (gi < n) ? *p + s2 : T(1);
+}
+
+// out[0] = sum of 2 log L_ii over this rank's diagonal blocks (global index < n),
+// out[1] = sum of z^2 over the label tiles (from the tile table, every rank has them all)
+template <typename T>
+__global__ __launch_bounds__(256) void dist_reduce_kernel(const T* __restrict__ A, int64_t ld, const int* __restrict__ loc,
+                                                          int g, int r, int nc, int64_t n, int m,
+                                                          const uint64_t* __restrict__ tiles,
+                                                          const int64_t* __restrict__ tld, double* __restrict__ out) {
+    __shared__ double s0[256], s1[256];
+    const int t = threadIdx.x;
+    double a = 0, b = 0;
+    for (int k = r; k < nc; k += g) {  // this rank's diagonal blocks
+        const int64_t gi = (int64_t)k * DB + (t & (DB - 1));
+        if (t < DB && gi < n) a += 2.0 * log((double)A[(int64_t)loc[k] * DB + t + gi * ld]);
+    }
+    const int64_t lz = tld[nc];
+    for (int k = 0; k < nc; k++) {
+        const T* z = reinterpret_cast<const T*>(tiles[(int64_t)nc * nc + k]);
+        for (int e = t; e < m * DB; e += 256) {
+            const int rr = e % m, c = e / m;
+            if ((int64_t)k * DB + c < n) {
+                const double v = (double)z[rr + (int64_t)c * lz];
+                b += v * v;
+            }
+        }
+    }
+    s0[t] = a;
+    s1[t] = b;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (t < o) {
+            s0[t] += s0[t + o];
+            s1[t] += s1[t + o];
+        }
+        __syncthreads();
+    }
+    if (t == 0) {
+        out[0] = s0[0];
+        out[1] = s1[0];
+    }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------
+// engine setup (per shape): layout, buffers, tables, schedule
+// ---------------------------------------------------------------------------------------
+template <typename T>
+static void setup(DistEngine<T>& E, const DistContext& C, int64_t n, int m, bool fused) {
+    const int64_t np = (n + DB - 1) / DB * DB;
+    const int nc = (int)(np / DB), nr = nc + 1;  // + the label row block
+    if (E.key_n == n && E.key_m == m && E.key_fused == fused && !E.ranks.empty()) return;
+    GPRX_REQUIRE(m <= GT, GPRX_ERR_DIM, "distributed fit: at most 128 label columns");
+    E.g = C.world;
+    E.virt = C.virt;
+    E.device = C.device;
+    E.L.init(E.g, nc, nr);
+    int ncu = 0;
+    GPRX_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, C.device));
+    // CUs left free for the transport kernels (RCCL, copies, stream writes): a persistent
+    // launch on every CU would starve them (one workgroup per CU by LDS)
+    int reserve = 8;
+    if (const char* e = std::getenv("GPRX_DIST_RESERVE_CU")) reserve = std::max(1, std::atoi(e));
+    const int nloc_ranks = E.virt ? E.g : 1;
+    E.P = std::max(1, (ncu - reserve) / nloc_ranks);
+    if (const char* e = std::getenv("GPRX_DIST_P")) E.P = std::max(1, std::atoi(e));
+    E.lists = potrf_dist_schedule(nc, nr, E.P, E.g, fused, &E.est_us);
+    if (!E.sB) {
+        int lo = 0, hi = 0;
+        GPRX_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        GPRX_HIP(hipStreamCreateWithPriority(&E.sB, hipStreamNonBlocking, hi));
+        GPRX_HIP(hipStreamCreateWithPriority(&E.sP, hipStreamNonBlocking, lo));
+    }
+    if (!E.virt && !E.commP) {
+        E.commB = C.comm;
+        if (E.g > 1) {  // a second communicator: the two transport streams progress independently
+            rccl_ok(ncclCommSplit(C.comm, 0, C.rank, &E.commP, nullptr), "ncclCommSplit");
+            E.own_commP = true;
+        } else {
+            E.commP = C.comm;
+        }
+    }
+    E.ranks.clear();
+    const int nranks = E.virt ? E.g : 1;
+    const int64_t DB2 = (int64_t)DB * DB;
+    for (int v = 0; v < nranks; v++) {
+        auto R = std::make_unique<DistRank<T>>();
+        R->r = E.virt ? v : C.rank;
+        const int r = R->r;
+        if (E.virt) {
+            GPRX_HIP(hipStreamCreateWithFlags(&R->s, hipStreamNonBlocking));
+            R->own_stream = true;
+        } else {
+            R->s = C.stream;
+        }
+        GPRX_HIP(hipEventCreateWithFlags(&R->done, hipEventDisableTiming));
+        const int nl = E.L.nloc(r);
+        R->ld = (int64_t)nl * DB;
+        R->A.ensure(sizeof(T) * R->ld * np);
+        R->Linv.ensure(sizeof(T) * nc * DB2, hipDeviceMallocFinegrained);
+        R->send.ensure(sizeof(T) * std::max<int64_t>(1, E.L.stot[r]) * DB2);
+        R->recv.ensure(sizeof(T) * std::max<int64_t>(1, E.L.rtot[r]) * DB2, hipDeviceMallocFinegrained);
+        R->ctr.ensure(sizeof(int) * ((size_t)C_NCTL_DIST + nr + (size_t)nr * nc));
+        R->info.ensure(sizeof(int));
+        R->flag.ensure(sizeof(int));
+        R->drecv.ensure(2 * sizeof(unsigned), hipDeviceMallocUncached);
+        R->red.ensure(2 * sizeof(double));
+        R->alpha.ensure(sizeof(T) * np * m);
+        R->hdiag.ensure(sizeof(unsigned) * nc);
+        R->hslot.ensure(sizeof(unsigned) * (size_t)nr * nc);
+        // tables
+        std::vector<int> loc(nr);
+        std::vector<uint64_t> tptr((size_t)nr * nc, 0), sptr((size_t)nr * nc, 0), tiles((size_t)nr * nc, 0);
+        std::vector<int64_t> tld(nr);
+        T* Ab = R->A.template as<T>();
+        for (int i = 0; i < nr; i++) {
+            const int q = E.L.owner(i);
+            loc[i] = (q == r) ? E.L.loc(i) : -1;
+            tld[i] = (q == r) ? R->ld : (int64_t)DB;
+            for (int b = 0; b < std::min(i, nc); b++) {
+                if (q == r) {
+                    sptr[(size_t)i * nc + b] =
+                        (uint64_t)(R->send.template as<T>() + (E.L.soff[r][b] + E.L.pos(r, i, b)) * DB2);
+                    tiles[(size_t)i * nc + b] = (uint64_t)(Ab + (int64_t)loc[i] * DB + (int64_t)b * DB * R->ld);
+                } else {
+                    const uint64_t p = (uint64_t)(R->recv.template as<T>() + (E.L.roff[r][b][q] + E.L.pos(q, i, b)) * DB2);
+                    tptr[(size_t)i * nc + b] = p;
+                    tiles[(size_t)i * nc + b] = p;
+                }
+            }
+        }
+        R->loc.ensure(sizeof(int) * nr);
+        R->tptr.ensure(sizeof(uint64_t) * tptr.size());
+        R->sptr.ensure(sizeof(uint64_t) * sptr.size());
+        R->tiles.ensure(sizeof(uint64_t) * tiles.size());
+        R->tld.ensure(sizeof(int64_t) * nr);
+        GPRX_HIP(hipMemcpy(R->loc.p, loc.data(), sizeof(int) * nr, hipMemcpyHostToDevice));
+        GPRX_HIP(hipMemcpy(R->tptr.p, tptr.data(), sizeof(uint64_t) * tptr.size(), hipMemcpyHostToDevice));
+        GPRX_HIP(hipMemcpy(R->sptr.p, sptr.data(), sizeof(uint64_t) * sptr.size(), hipMemcpyHostToDevice));
+        GPRX_HIP(hipMemcpy(R->tiles.p, tiles.data(), sizeof(uint64_t) * tiles.size(), hipMemcpyHostToDevice));
+        GPRX_HIP(hipMemcpy(R->tld.p, tld.data(), sizeof(int64_t) * nr, hipMemcpyHostToDevice));
+        PtDist<T> pd;
+        pd.g = E.g;
+        pd.r = r;
+        pd.loc = R->loc.template as<int>();
+        pd.tptr = reinterpret_cast<const T* const*>(R->tptr.p);
+        pd.sptr = reinterpret_cast<T* const*>(R->sptr.p);
+        unsigned *hd = nullptr, *hs = nullptr;
+        GPRX_HIP(hipHostGetDevicePointer((void**)&hd, R->hdiag.p, 0));
+        GPRX_HIP(hipHostGetDevicePointer((void**)&hs, R->hslot.p, 0));
+        pd.hdiag = hd;
+        pd.hslot = hs;
+        pd.drecv = R->drecv.template as<unsigned>();
+        pd.precv = R->drecv.template as<unsigned>() + 1;
+        R->pd.ensure(sizeof(PtDist<T>));
+        GPRX_HIP(hipMemcpy(R->pd.p, &pd, sizeof(pd), hipMemcpyHostToDevice));
+        const std::vector<int4>& lst = E.lists[r];
+        R->ntasks = (int)lst.size();
+        R->list.ensure(sizeof(int4) * std::max<size_t>(1, lst.size()));
+        if (!lst.empty()) GPRX_HIP(hipMemcpy(R->list.p, lst.data(), sizeof(int4) * lst.size(), hipMemcpyHostToDevice));
+        E.ranks.push_back(std::move(R));
+    }
+    E.key_n = n;
+    E.key_m = m;
+    E.key_fused = fused;
+}
+
+// ---------------------------------------------------------------------------------------
+// transport steps
+// ---------------------------------------------------------------------------------------
+template <typename T>
+static void issue_bcast(DistEngine<T>& E, int k) {
+    const int64_t DB2 = (int64_t)DB * DB;
+    const int root = E.L.owner(k);
+    if (E.virt) {
+        const DistRank<T>& Rt = *E.ranks[root];
+        for (auto& R : E.ranks)
+            if (R->r != root)
+                GPRX_HIP(hipMemcpyAsync(R->Linv.template as<T>() + k * DB2, Rt.Linv.template as<T>() + k * DB2,
+                                        sizeof(T) * DB2, hipMemcpyDeviceToDevice, E.sB));
+        for (auto& R : E.ranks) GPRX_HIP(hipStreamWriteValue32(E.sB, R->drecv.p, (uint32_t)(k + 1), 0));
+    } else {
+        DistRank<T>& R = *E.ranks[0];
+        T* p = R.Linv.template as<T>() + k * DB2;
+        if (E.g > 1) rccl_ok(ncclBroadcast(p, p, (size_t)DB2, nccl_t<T>(), root, E.commB, E.sB), "ncclBroadcast");
+        GPRX_HIP(hipStreamWriteValue32(E.sB, R.drecv.p, (uint32_t)(k + 1), 0));
+    }
+}
+
+template <typename T>
+static void issue_panel(DistEngine<T>& E, int b) {
+    const int64_t DB2 = (int64_t)DB * DB;
+    if (E.virt) {
+        for (auto& R : E.ranks)
+            for (auto& Q : E.ranks) {
+                if (Q->r == R->r) continue;
+                const int64_t c = E.L.cnt(Q->r, b);
+                if (c == 0) continue;
+                GPRX_HIP(hipMemcpyAsync(R->recv.template as<T>() + E.L.roff[R->r][b][Q->r] * DB2,
+                                        Q->send.template as<T>() + E.L.soff[Q->r][b] * DB2, sizeof(T) * c * DB2,
+                                        hipMemcpyDeviceToDevice, E.sP));
+            }
+        for (auto& R : E.ranks)
+            GPRX_HIP(hipStreamWriteValue32(E.sP, R->drecv.template as<unsigned>() + 1, (uint32_t)(b + 1), 0));
+    } else {
+        DistRank<T>& R = *E.ranks[0];
+        const int r = R.r;
+        if (E.g > 1) {
+            rccl_ok(ncclGroupStart(), "ncclGroupStart");
+            const int64_t cs = E.L.cnt(r, b);
+            for (int q = 0; q < E.g; q++) {
+                if (q == r) continue;
+                if (cs > 0)
+                    rccl_ok(ncclSend(R.send.template as<T>() + E.L.soff[r][b] * DB2, (size_t)(cs * DB2), nccl_t<T>(), q,
+                                     E.commP, E.sP),
+                            "ncclSend");
+                const int64_t cq = E.L.cnt(q, b);
+                if (cq > 0)
+                    rccl_ok(ncclRecv(R.recv.template as<T>() + E.L.roff[r][b][q] * DB2, (size_t)(cq * DB2), nccl_t<T>(),
+                                     q, E.commP, E.sP),
+                            "ncclRecv");
+            }
+            rccl_ok(ncclGroupEnd(), "ncclGroupEnd");
+        }
+        GPRX_HIP(hipStreamWriteValue32(E.sP, R.drecv.template as<unsigned>() + 1, (uint32_t)(b + 1), 0));
+    }
+}
+
+// this host's ranks have every tile of panel b in its send slot
+template <typename T>
+static bool panel_ready(const DistEngine<T>& E, int b) {
+    for (auto& R : E.ranks) {
+        const unsigned* hs = R->hslot.u();
+        for (int i = E.L.first(R->r, b); i < E.L.nr; i += E.g)
+            if (__atomic_load_n(hs + (size_t)i * E.L.nc + b, __ATOMIC_ACQUIRE) == 0) return false;
+    }
+    return true;
+}
+
+template <typename T>
+static bool bcast_ready(const DistEngine<T>& E, int k) {
+    const int root = E.L.owner(k);
+    for (auto& R : E.ranks)
+        if (R->r == root) return __atomic_load_n(R->hdiag.u() + k, __ATOMIC_ACQUIRE) != 0;
+    return true;  // another process's rank: RCCL waits for it on the device
+}
+
+// ---------------------------------------------------------------------------------------
+// the fit
+// ---------------------------------------------------------------------------------------
+template <typename T>
+void dist_fit(DistEngineBase*& eng, const DistContext& C, const DistFitIn<T>& in, DistFitOut& out, T* alpha_dev,
+              Exec& ex) {
+    if (!eng) eng = new DistEngine<T>();
+    DistEngine<T>& E = *static_cast<DistEngine<T>*>(eng);
+    const bool fused = in.tb.mode != 0;
+    setup<T>(E, C, in.n, in.m, fused);
+    const int nc = E.L.nc, nr = E.L.nr;
+    const int64_t np = (int64_t)nc * DB, n = in.n;
+    const int64_t DB2 = (int64_t)DB * DB;
+    DistRank<T>& R0 = *E.ranks[0];
+    // ---- per rank: reset, build, launch -----------------------------------------------------
+    auto ts = std::chrono::steady_clock::now();
+    for (auto& Rp : E.ranks) {
+        DistRank<T>& R = *Rp;
+        const int r = R.r;
+        hipStream_t s = R.s;
+        std::memset(R.hdiag.p, 0, R.hdiag.bytes);
+        std::memset(R.hslot.p, 0, R.hslot.bytes);
+        const size_t nctr = (size_t)C_NCTL_DIST + nr + (size_t)nr * nc;
+        GPRX_HIP(hipMemsetAsync(R.ctr.p, 0, sizeof(int) * nctr, s));
+        GPRX_HIP(hipMemsetAsync(R.drecv.p, 0, 2 * sizeof(unsigned), s));
+        GPRX_HIP(hipMemsetD32Async((hipDeviceptr_t)R.info.p, INT_MAX, 1, s));
+        GPRX_HIP(hipMemsetAsync(R.flag.p, 0, sizeof(int), s));
+        T* A = R.A.template as<T>();
+        if (fused) {
+            // BUILD tasks write the lower tiles: ver = -1 until built (rows of the matrix only)
+            GPRX_HIP(hipMemsetAsync(R.ctr.template as<int>() + C_NCTL_DIST + nr, 0xff, sizeof(int) * (size_t)nc * nc, s));
+        } else {
+            // the direct build: each owned row block against the columns up to its diagonal
+            GPRX_HIP(hipMemsetAsync(A, 0, sizeof(T) * R.ld * np, s));
+            for (int i = r; i < nc; i += E.g) {
+                const int64_t r0 = (int64_t)i * DB, rows = std::min<int64_t>(DB, n - r0), cols = std::min<int64_t>(r0 + DB, n);
+                T* Ai = A + (int64_t)E.L.loc(i) * DB;
+                if (rows > 0) {
+                    const T *tabr = nullptr, *tabc = nullptr;
+                    if (in.K.nper > 0) {  // sin/cos tables of the block's rows and of its columns
+                        const size_t slot = (size_t)2 * in.K.nper * in.d;
+                        R.tab.ensure(sizeof(T) * slot * ((size_t)DB + (size_t)n));
+                        T* tr = R.tab.template as<T>();
+                        T* tc = tr + slot * DB;
+                        launch_sincos_tables<T>(in.K, in.X + r0 * in.d, rows, in.d, tr, s);
+                        launch_sincos_tables<T>(in.K, in.X, cols, in.d, tc, s);
+                        tabr = tr;
+                        tabc = tc;
+                    }
+                    launch_kbuild<T>(in.K, in.X + r0 * in.d, tabr, rows, in.X, tabc, cols, in.d, Ai, R.ld, 0, false,
+                                     T(0), R.flag.template as<int>(), s);
+                }
+                hipLaunchKernelGGL(diag_fix_local_kernel<T>, dim3(1), dim3(DB), 0, s, A, R.ld,
+                                   (int64_t)E.L.loc(i) * DB, r0, n, in.sigma2);
+            }
+        }
+        if (E.L.owner(nc) == r)  // the label rows: Y^T as row block nc
+            launch_label_rows<T>(in.Y, n, in.m, A, R.ld, (int64_t)E.L.loc(nc) * DB, np, GT, s);
+        TileBuild<T> tbl = in.tb;
+        tbl.flag = R.flag.template as<int>();
+        void* tbdev = nullptr;
+        if (fused) {
+            R.red.ensure(std::max<size_t>(R.red.bytes, sizeof(TileBuild<T>) + 64));
+            tbdev = static_cast<char*>(R.red.p) + 64;  // after the reduction doubles
+            GPRX_HIP(hipMemcpyAsync(tbdev, &tbl, sizeof(tbl), hipMemcpyHostToDevice, s));
+        }
+        DistLaunch<T> Lc;
+        Lc.A = A;
+        Lc.ld = R.ld;
+        Lc.Linv = R.Linv.template as<T>();
+        Lc.info = R.info.template as<int>();
+        Lc.list = R.list.template as<int4>();
+        Lc.ntasks = R.ntasks;
+        Lc.nc = nc;
+        Lc.nr = nr;
+        Lc.ctr = R.ctr.template as<int>();
+        Lc.tb_dev = reinterpret_cast<const TileBuild<T>*>(tbdev);
+        Lc.dist_dev = R.pd.template as<PtDist<T>>();
+        Lc.tlimit = (long long)(1e8 * (2.0 + 20.0 * E.est_us * 1e-6));
+        Lc.P = E.P;
+        Lc.s = s;
+        potrf_tiles_dist_launch<T>(Lc);
+        GPRX_HIP(hipEventRecord(R.done, s));
+    }
+    // ---- issue loop: transport steps as their inputs become ready --------------------------
+    int kb = 0, kp = 0;
+    bool flush = false;
+    const double limit_s = 4.0 + 40.0 * E.est_us * 1e-6;
+    while (kb < nc || kp < nc) {
+        bool progress = false;
+        if (kb < nc && (flush || bcast_ready(E, kb))) {
+            issue_bcast(E, kb++);
+            progress = true;
+        }
+        if (kp < nc && kp < kb + 1 && (flush || panel_ready(E, kp))) {
+            issue_panel(E, kp++);
+            progress = true;
+        }
+        if (progress || flush) continue;
+        // stalled: kernels ended early (a timed-out wait drained them) or out of time -> issue
+        // the rest (their data is stale, the fit reports the error) so peers are not left
+        // waiting inside RCCL
+        bool all_done = true;
+        for (auto& R : E.ranks) all_done &= hipEventQuery(R->done) == hipSuccess;
+        const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - ts).count();
+        if (all_done || el > limit_s) flush = true;
+        else std::this_thread::yield();
+    }
+    for (auto& R : E.ranks) GPRX_HIP(hipStreamSynchronize(R->s));
+    GPRX_HIP(hipStreamSynchronize(E.sB));
+    GPRX_HIP(hipStreamSynchronize(E.sP));
+    GPRX_HIP(hipGetLastError());
+    // ---- reductions, back substitution (every rank holds every tile) -------------------------
+    double logdet = 0, datafit = 0;
+    int info = INT_MAX, flag = 0;
+    for (auto& Rp : E.ranks) {
+        DistRank<T>& R = *Rp;
+        hipLaunchKernelGGL(dist_reduce_kernel<T>, dim3(1), dim3(256), 0, R.s, R.A.template as<T>(), R.ld,
+                           R.loc.template as<int>(), E.g, R.r, nc, n, in.m, R.tiles.template as<uint64_t>(),
+                           R.tld.template as<int64_t>(), R.red.template as<double>());
+        double red[2];
+        int hi = 0, hf = 0;
+        GPRX_HIP(hipMemcpyAsync(red, R.red.p, sizeof(red), hipMemcpyDeviceToHost, R.s));
+        GPRX_HIP(hipMemcpyAsync(&hi, R.info.p, sizeof(int), hipMemcpyDeviceToHost, R.s));
+        GPRX_HIP(hipMemcpyAsync(&hf, R.flag.p, sizeof(int), hipMemcpyDeviceToHost, R.s));
+        GPRX_HIP(hipStreamSynchronize(R.s));
+        logdet += red[0];
+        datafit = red[1];
+        info = std::min(info, hi);
+        flag = std::max(flag, hf);
+    }
+    if (!E.virt && E.g > 1) {  // combine over the ranks: sum of log det, min info, max flag
+        DMem dv;
+        dv.ensure(sizeof(double) + 2 * sizeof(int));
+        double* dl = dv.as<double>();
+        int* di = reinterpret_cast<int*>(dl + 1);
+        GPRX_HIP(hipMemcpyAsync(dl, &logdet, sizeof(double), hipMemcpyHostToDevice, R0.s));
+        GPRX_HIP(hipMemcpyAsync(di, &info, sizeof(int), hipMemcpyHostToDevice, R0.s));
+        GPRX_HIP(hipMemcpyAsync(di + 1, &flag, sizeof(int), hipMemcpyHostToDevice, R0.s));
+        rccl_ok(ncclGroupStart(), "ncclGroupStart");
+        rccl_ok(ncclAllReduce(dl, dl, 1, ncclFloat64, ncclSum, E.commB, R0.s), "ncclAllReduce");
+        rccl_ok(ncclAllReduce(di, di, 1, ncclInt32, ncclMin, E.commB, R0.s), "ncclAllReduce");
+        rccl_ok(ncclAllReduce(di + 1, di + 1, 1, ncclInt32, ncclMax, E.commB, R0.s), "ncclAllReduce");
+        rccl_ok(ncclGroupEnd(), "ncclGroupEnd");
+        GPRX_HIP(hipMemcpyAsync(&logdet, dl, sizeof(double), hipMemcpyDeviceToHost, R0.s));
+        GPRX_HIP(hipMemcpyAsync(&info, di, sizeof(int), hipMemcpyDeviceToHost, R0.s));
+        GPRX_HIP(hipMemcpyAsync(&flag, di + 1, sizeof(int), hipMemcpyDeviceToHost, R0.s));
+        GPRX_HIP(hipStreamSynchronize(R0.s));
+    }
+    out.logdet = logdet;
+    out.datafit = datafit;
+    out.info = info;
+    out.flag = flag;
+    out.est_us = E.est_us;
+    out.P = E.P;
+    if (info < 0 || info != INT_MAX || flag) return;  // the caller reports it
+    // alpha = L^{-T} z on rank 0 of this process (the factor is complete on every rank)
+    GPRX_HIP(hipMemsetD32Async((hipDeviceptr_t)R0.info.p, INT_MAX, 1, R0.s));
+    launch_backsolve_chain<T>(nullptr, 0, np, in.m, R0.Linv.template as<T>(), alpha_dev, R0.info.template as<int>(), ex,
+                              R0.s, R0.tiles.template as<uint64_t>(), R0.tld.template as<int64_t>());
+    int hi = 0;
+    GPRX_HIP(hipMemcpyAsync(&hi, R0.info.p, sizeof(int), hipMemcpyDeviceToHost, R0.s));
+    GPRX_HIP(hipStreamSynchronize(R0.s));
+    if (hi != INT_MAX) out.info = hi;
+    (void)DB2;
+}
+
+void dist_engine_free(DistEngineBase* e) { delete e; }
+
+template void dist_fit<double>(DistEngineBase*&, const DistContext&, const DistFitIn<double>&, DistFitOut&, double*,
+                               Exec&);
+template void dist_fit<float>(DistEngineBase*&, const DistContext&, const DistFitIn<float>&, DistFitOut&, float*, Exec&);
+
+}  // namespace gprx

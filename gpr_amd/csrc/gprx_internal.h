@@ -364,6 +364,47 @@ struct TileBuild {
     int* flag;
     int mode;
 };
+// Distributed tile factorisation (k_ptiles.hip, potrf_tiles_kernel<T, true>): this rank's
+// view of a factorisation whose row blocks are dealt cyclically over g ranks (row block i on
+// rank i mod g).  Device copy, read per task.  Tiles of rows owned elsewhere arrive packed
+// (128 x 128, ld DB) through the panel exchange; the inverse diagonal blocks through the
+// broadcast.  Counters the host reads (hdiag, hsend) are in coherent host memory, those the
+// transport writes (drecv, precv) in uncached device memory.  The kernel only stores to the
+// host-visible words (no atomics over PCIe).
+template <typename T>
+struct PtDist {
+    int g, r;
+    const int* loc;          // [nr] local row block of row block i, -1 if owned elsewhere
+    const T* const* tptr;    // [nr * nc] received tile (i, b) of a row owned elsewhere
+    T* const* sptr;          // [nr * nc] send slot of this rank's final tile (i, b)
+    unsigned* hdiag;         // [nc] set to 1 when Linv_k (slot k of Linv) is final here
+    unsigned* hslot;         // [nr * nc] set to 1 when tile (i, b) is in its send slot
+    const unsigned* drecv;   // Linv_k present for every k < *drecv
+    const unsigned* precv;   // every tile of panels b < *precv received
+};
+
+// One rank's launch of the distributed tile factorisation (k_ptiles.hip).  ctr: C_NCTL +
+// nr + nr * nc ints, zeroed (ver = -1 for the tiles the launch builds) by the caller.
+template <typename T>
+struct DistLaunch {
+    T* A;
+    int64_t ld;
+    T* Linv;
+    int* info;
+    const int4* list;
+    int ntasks, nc, nr;
+    int* ctr;
+    const TileBuild<T>* tb_dev;
+    const PtDist<T>* dist_dev;
+    long long tlimit;  // wall-clock ticks (100 MHz) a single wait may take
+    int P;             // workgroups (one per CU)
+    hipStream_t s;
+};
+// Per-rank ticket lists of the distributed factorisation (row block i on rank i mod g).
+std::vector<std::vector<int4>> potrf_dist_schedule(int nc, int nr, int P, int g, bool build, double* est_us);
+template <typename T>
+void potrf_tiles_dist_launch(const DistLaunch<T>& L);
+
 // LML gradient on the MFMA units (k_pairs.hip): trees it covers, the extra feature columns
 // it needs per sample set, and the launch (partials of ntiles * 3 MAX_LEAF doubles, reduced
 // in a fixed order into acc[3 l + q]).
@@ -430,9 +471,11 @@ void launch_backsolve(const T* A, int64_t ld, int64_t np, int m, const T* Linv, 
 
 // Same solve in one launch: one workgroup per 128-block, chained by flags (k_bsolve.hip).
 // z is read from the label rows np..np+m-1 of A (ld).  A timed-out wait sets *info = -1.
+// tiles/tld (optional, the distributed factor): tile (j, k) at tiles[j * (np/128) + k] with
+// leading dimension tld[j], the label rows as row block np/128; A and ld unused then.
 template <typename T>
 void launch_backsolve_chain(const T* A, int64_t ld, int64_t np, int m, const T* Linv, T* alpha, int* info, Exec& ex,
-                            hipStream_t s);
+                            hipStream_t s, const uint64_t* tiles = nullptr, const int64_t* tld = nullptr);
 
 // logdet partial = 2 sum log L_ii over i < n, datafit = sum of squares of the augmented
 // rows; results accumulated in double on the device (out[0], out[1]).

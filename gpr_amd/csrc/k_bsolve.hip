@@ -100,7 +100,22 @@ struct Args {
     int* info;        // set to -1 (atomicMin) when a wait timed out
     long long tlimit; // wall-clock ticks (100 MHz) per wait
     long long* trace; // GPRX_BS_TRACE: per block {start, non-critical done, alpha_{k+1} seen, published}
+    // distributed factor (optional): tile (j, k) of the factor at tiles[j * nb + k] with leading
+    // dimension tld[j] (j = nb: the label rows z^T); A and ld are then unused
+    const uint64_t* tiles;
+    const int64_t* tld;
 };
+
+// tile (j, k) of the factor (j = nb: the label rows) and its leading dimension
+template <typename T>
+__device__ __forceinline__ const T* bs_tile(const Args<T>& a, int j, int k, int nb, int64_t& ld) {
+    if (a.tiles) {
+        ld = a.tld[j];
+        return reinterpret_cast<const T*>(a.tiles[(int64_t)j * nb + k]);
+    }
+    ld = a.ld;
+    return a.A + (int64_t)j * DB + (int64_t)k * DB * a.ld;
+}
 
 // Wait until *f != 0; false on timeout or another workgroup's error (every wave polls on its
 // own: the caller agrees through LDS before the next barrier).
@@ -166,7 +181,11 @@ __global__ __launch_bounds__(NT) void backsolve_chain_kernel(Args<T> a) {
         for (int e = t; e < DB * DB; e += NT) s_linv[(e / DB) * LDL + (e % DB)] = Lk[e];
     }
     T t1[QR];
-    if (has1) load_run<T>(a.A + (int64_t)(k + 1) * DB + (r0 + c) * a.ld + QR * q, t1);
+    if (has1) {
+        int64_t l1;
+        const T* p1 = bs_tile<T>(a, k + 1, k, nb, l1);
+        load_run<T>(p1 + (int64_t)c * l1 + QR * q, t1);
+    }
     // one alpha block into s_alpha, then every thread's partial of (L^T alpha)_c over its rows
     auto apply = [&](const T(&x)[QR], const T* alpha_j, int r) {
         if (t < DB) s_alpha[t] = ld_sc1(alpha_j + (int64_t)t * a.m + r);
@@ -194,7 +213,9 @@ __global__ __launch_bounds__(NT) void backsolve_chain_kernel(Args<T> a) {
         for (int cc = 0; cc < CPW; cc++) p[cc] = 0;
         for (int j = nb - 1; j > k + 1 && ok; j--) {
             TileRows<T> tr;
-            tr.load(a.A + (int64_t)j * DB + r0 * a.ld, a.ld, w, lane);
+            int64_t lj;
+            const T* pj = bs_tile<T>(a, j, k, nb, lj);
+            tr.load(pj, lj, w, lane);
             ok = wait_flag(fl + j, a.ctl, t0, a.tlimit);
             if (!ok) break;
             const int64_t rj = (int64_t)j * DB + 2 * lane;
@@ -207,7 +228,12 @@ __global__ __launch_bounds__(NT) void backsolve_chain_kernel(Args<T> a) {
             const T sum = wave_reduce_cols<T>(p, lane, col);
             if ((lane & 3) == 0) s_other[CPW * w + col] = sum;
         }
-        const T zc = a.A[a.np + r + (r0 + c) * a.ld];  // label row r of block k (z^T)
+        T zc;  // label row r of block k (z^T)
+        {
+            int64_t lz;
+            const T* pz = bs_tile<T>(a, nb, k, nb, lz);
+            zc = pz[r + (int64_t)c * lz];
+        }
         if (a.trace && r == 0 && t == 0) a.trace[4 * k + 1] = wall_clock64();
         // ---- critical path ----
         T crit = 0;
@@ -253,7 +279,7 @@ int64_t bs_trace_copy(long long* out, int64_t max_blocks) {
 
 template <typename T>
 void launch_backsolve_chain(const T* A, int64_t ld, int64_t np, int m, const T* Linv, T* alpha, int* info,
-                            Exec& ex, hipStream_t s) {
+                            Exec& ex, hipStream_t s, const uint64_t* tiles, const int64_t* tld) {
     using namespace bs;
     const int nb = (int)(np / DB);
     const size_t need = (size_t)C_NCTL + (size_t)nb * m;
@@ -272,6 +298,8 @@ void launch_backsolve_chain(const T* A, int64_t ld, int64_t np, int m, const T* 
     a.info = info;
     a.tlimit = (long long)(1e8 * 4.0);
     a.trace = nullptr;
+    a.tiles = tiles;
+    a.tld = tld;
     static const bool tracing = std::getenv("GPRX_BS_TRACE") != nullptr;
     if (tracing) {
         if (g_bs_trace_n < nb) {
@@ -294,8 +322,8 @@ void launch_backsolve_chain(const T* A, int64_t ld, int64_t np, int m, const T* 
 }
 
 template void launch_backsolve_chain<double>(const double*, int64_t, int64_t, int, const double*, double*, int*,
-                                             Exec&, hipStream_t);
+                                             Exec&, hipStream_t, const uint64_t*, const int64_t*);
 template void launch_backsolve_chain<float>(const float*, int64_t, int64_t, int, const float*, float*, int*, Exec&,
-                                            hipStream_t);
+                                            hipStream_t, const uint64_t*, const int64_t*);
 
 }  // namespace gprx

@@ -93,10 +93,13 @@ __device__ __forceinline__ void wait_vm() {
 // (a multiple of BKS: 0 = idle, K = all; the rest of B is zero for it), but every wave takes
 // part in the staging and the barriers of all K.  A, B: 128 rows x K, column-major (lda,
 // ldb), 16-B aligned.
+// Bpan (optional): B given per 128-column panel -- column c of B at Bpan[c / 128] + (c % 128)
+// ldb (the distributed factorisation's received tiles: one packed 128 x 128 tile per panel,
+// ldb = 128, each panel in its own receive buffer).
 template <typename T>
 __device__ __forceinline__ void tile_mma(typename Mfma<T>::acc_t (&acc)[2][4], const T* __restrict__ A, int64_t lda,
                                          const T* __restrict__ B, int64_t ldb, int K, int kact, T* smem,
-                                         const int t) {
+                                         const int t, const uint64_t* Bpan = nullptr) {
     typedef Mfma<T> Tr;
     typedef typename Tr::acc_t acc_t;
     typedef Stage<T> S;
@@ -113,7 +116,14 @@ __device__ __forceinline__ void tile_mma(typename Mfma<T>::acc_t (&acc)[2][4], c
             const bool isB = g >= S::GRP;
             const int gg = isB ? g - S::GRP : g;
             const int64_t col = (int64_t)st * BKS + gg * S::CPI + lcol;
-            const T* src = isB ? (B + lrow + col * ldb) : (A + lrow + col * lda);
+            const T* src;
+            if (isB && Bpan) {  // the stage's 16 columns lie in one 128-column panel
+                // (addresses as integers: a pointer-to-pointer operand crashed hipcc 7.2)
+                const T* pb = reinterpret_cast<const T*>((uint64_t)__builtin_amdgcn_readfirstlane((long long)Bpan[(st * BKS) >> 7]));
+                src = pb + lrow + (col & (GT - 1)) * ldb;
+            } else {
+                src = isB ? (B + lrow + col * ldb) : (A + lrow + col * lda);
+            }
             __builtin_amdgcn_global_load_lds((const void*)src,
                                              (__attribute__((address_space(3))) void*)(buf + g * S::SRP), 16, 0, 0);
         }

@@ -37,6 +37,7 @@
 // Tile GEMM: 512 threads = 8 waves of 64x32 (v_mfma_f64_16x16x4f64 / _f32_16x16x4f32),
 // operands staged 32-deep through LDS, double-buffered; 147 KB of LDS per workgroup also
 // keeps the launch at one workgroup per CU, so the critical DIAGX step has a whole CU.
+#include "gprx_dist.h"
 #include "gprx_internal.h"
 #include "k_pairs.h"
 
@@ -55,6 +56,7 @@ namespace gprx {
 namespace pt {
 
 using namespace mm;
+static_assert(C_NCTL == C_NCTL_DIST, "counter block layout shared with gprx_dist.cpp");
 
 // ------------------------------------------------------------------------------------------
 // One 128x128 tile:  C = A B^T (UPDATE = false)  or  C -= A B^T (UPDATE = true), K deep.
@@ -63,10 +65,13 @@ using namespace mm;
 // lower triangular (K = 128, a diagonal-block inverse): output columns 32 wc .. 32 wc + 31
 // need only k < 32 wc + 32, the waves skip the MFMAs of the zero part.
 // ------------------------------------------------------------------------------------------
+// Bpan: B by 128-column panels (tile_mma); C2 (optional, TRSM only): a second copy of the
+// result, packed 128 x 128 (ld DB) -- the distributed factorisation's send slot.
 template <typename T, bool UPDATE>
 __device__ __forceinline__ void tile_gemm(T* __restrict__ C, int64_t ldc, const T* __restrict__ A, int64_t lda,
                                           const T* __restrict__ B, int64_t ldb, int K, bool lower, T* smem,
-                                          const int t, bool tri = false) {
+                                          const int t, bool tri = false, const uint64_t* Bpan = nullptr,
+                                          T* __restrict__ C2 = nullptr) {
     typedef Mfma<T> Tr;
     typedef typename Tr::acc_t acc_t;
     const int lane = t & 63, w = t >> 6;
@@ -89,7 +94,7 @@ __device__ __forceinline__ void tile_gemm(T* __restrict__ C, int64_t ldc, const 
             }
     }
     acc_t acc[2][4];
-    tile_mma<T>(acc, A, lda, B, ldb, K, !active ? 0 : (tri ? 32 * (wc + 1) : K), smem, t);
+    tile_mma<T>(acc, A, lda, B, ldb, K, !active ? 0 : (tri ? 32 * (wc + 1) : K), smem, t, Bpan);
     if (!active) return;
 #pragma unroll
     for (int x = 0; x < 2; x++) {
@@ -107,6 +112,7 @@ __device__ __forceinline__ void tile_gemm(T* __restrict__ C, int64_t ldc, const 
                     st_sc1(ccol + il, (lower && il < jl) ? cv[x][y][reg] : cv[x][y][reg] - acc[x][y][reg]);
                 else if (!lower || il >= jl)
                     st_sc1(ccol + il, acc[x][y][reg]);
+                if (!UPDATE && C2) st_sc1(C2 + il + (int64_t)jl * DB, acc[x][y][reg]);
             }
         }
     }
@@ -392,6 +398,7 @@ struct Args {
     const TileBuild<T>* tb;  // BUILD tasks: covariance tiles from pair statistics (device copy,
                              // read per task: as kernel arguments they stayed live in SGPRs and
                              // pushed the whole kernel into spills)
+    const PtDist<T>* dist;   // distributed factorisation (potrf_tiles_kernel<T, true> only)
 };
 
 
@@ -399,8 +406,12 @@ struct Args {
 // values are made wave-uniform, so the loop is a scalar loop with no divergence).  Returns
 // false on timeout or when another workgroup raised the error flag.
 __device__ __forceinline__ int ld_uni(const int* p) { return __builtin_amdgcn_readfirstlane(ld_agent(p)); }
+// counters written by the transport (stream memory ops into uncached memory): system scope
+__device__ __forceinline__ int ld_sys_uni(const unsigned* p) {
+    return __builtin_amdgcn_readfirstlane((int)__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+}
 
-template <typename T>
+template <typename T, bool DIST>
 __device__ bool wait_inputs(const Args<T>& a, int type, int i, int j, int b0, int nb) {
     const int* vp;
     int vwant;
@@ -410,6 +421,9 @@ __device__ bool wait_inputs(const Args<T>& a, int type, int i, int j, int b0, in
     int lwant1;
     const int* lp2;
     int lwant2;
+    // DIST: one dependency may be data of another rank, a transport counter instead
+    const unsigned* rp = nullptr;
+    int rwant = 0;
     if (type == T_DIAGX && i == 0) {  // the first diagonal tile is built
         vp = a.ver;
         vwant = 0;
@@ -430,6 +444,14 @@ __device__ bool wait_inputs(const Args<T>& a, int type, int i, int j, int b0, in
         lwant1 = i;
         lp2 = lp1;
         lwant2 = lwant1;
+        if constexpr (DIST) {
+            if ((i - 1) % a.dist->g != a.dist->r) {  // Linv_{i-1} is broadcast
+                lp1 = lp2 = a.lcnt + i;
+                lwant1 = lwant2 = 0;
+                rp = a.dist->drecv;
+                rwant = i;
+            }
+        }
     } else if (type == T_TRSM) {
         vp = a.ver + (int64_t)i * a.nc + j;
         vwant = j;
@@ -439,6 +461,14 @@ __device__ bool wait_inputs(const Args<T>& a, int type, int i, int j, int b0, in
         lwant1 = j + 1;
         lp2 = lp1;
         lwant2 = lwant1;
+        if constexpr (DIST) {
+            if (j % a.dist->g != a.dist->r) {  // Linv_j is broadcast
+                lp1 = lp2 = a.lcnt + i;
+                lwant1 = lwant2 = 0;
+                rp = a.dist->drecv;
+                rwant = j + 1;
+            }
+        }
     } else {
         vp = a.ver + (int64_t)i * a.nc + j;
         vwant = b0;
@@ -448,12 +478,22 @@ __device__ bool wait_inputs(const Args<T>& a, int type, int i, int j, int b0, in
         lwant1 = b0 + nb;
         lp2 = a.lcnt + j;
         lwant2 = b0 + nb;
+        if constexpr (DIST) {
+            if (j % a.dist->g != a.dist->r) {  // row j's tiles arrive with the panels
+                lp2 = lp1;
+                rp = a.dist->precv;
+                rwant = b0 + nb;
+            }
+        }
     }
     const long long t0 = wall_clock64();
     for (;;) {
         // bitwise: all four loads are issued before any compare resolves
-        const int ok = int(ld_uni(vp) == vwant) & int(ld_uni(vp2) == vwant2) & int(ld_uni(lp1) >= lwant1) &
-                       int(ld_uni(lp2) >= lwant2);
+        int ok = int(ld_uni(vp) == vwant) & int(ld_uni(vp2) == vwant2) & int(ld_uni(lp1) >= lwant1) &
+                 int(ld_uni(lp2) >= lwant2);
+        if constexpr (DIST) {
+            if (rp) ok &= int(ld_sys_uni(rp) >= rwant);
+        }
         if (ok) return true;
         if (ld_uni(a.ctl + C_ERR)) return false;
         if (wall_clock64() - t0 > a.tlimit) {
@@ -464,7 +504,19 @@ __device__ bool wait_inputs(const Args<T>& a, int type, int i, int j, int b0, in
     }
 }
 
-template <typename T>
+// DIST: a host-visible flag = 1 after every wave's stores (sc1 or plain) reached memory
+// (system-scope release: the transport reads them from another agent)
+__device__ __forceinline__ void publish_host(unsigned* p) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (wave_id() == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+template <typename T, bool DIST>
 __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     // ONE __shared__ array (a second __shared__ object can make hipcc drain the LDS-DMA
@@ -492,7 +544,7 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
         const int i = __builtin_amdgcn_readfirstlane(tk.y), j = __builtin_amdgcn_readfirstlane(tk.z),
                   b0 = __builtin_amdgcn_readfirstlane(tk.w);
         dbg_mark(a.dbg, q, 1 + 10 * type, i, j);
-        const bool ok = wait_inputs<T>(a, type, i, j, b0, nb);  // every wave, uniform
+        const bool ok = wait_inputs<T, DIST>(a, type, i, j, b0, nb);  // every wave, uniform
         if (!ok) break;
         if (wv == 0 && !(a.variant & 32)) {  // wave 0 acquires for the workgroup (invalidates this CU's L1)
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -506,40 +558,68 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
         // task instead of hoisted (and held in registers) across the whole task loop
         int tid = t;
         asm volatile("" : "+v"(tid));
-        T* Ci = a.A + (int64_t)i * GT;  // row block i, column 0
+        // row block i of this rank's storage (DIST: only the rank's own row blocks are stored)
+        int li = i;
+        if constexpr (DIST) li = __builtin_amdgcn_readfirstlane(a.dist->loc[i]);
+        T* Ci = a.A + (int64_t)li * GT;  // row block i, column 0
         if (type == T_BUILD) {
             // ver[i][j] goes from -1 (not built) to 0; the tile's values go out write-through
             const TileBuild<T>& b = *a.tb;
             bool bad;
             // one instantiation for every mode: an absent statistic has a zero-depth product
-            // (its accumulators stay 0) and no leaves of its class
-            bad = pr::build_tile_sum<T, 1, true>(b.Kd, b.FU, b.FV, b.nf, b.Kr, b.Kp, b.hd, a.A, ld, b.n, b.sigma2,
-                                                 (int64_t)i * GT, (int64_t)j * GT, smem, tid);
+            // (its accumulators stay 0) and no leaves of its class.  The features are indexed by
+            // the global row, the storage by the local one.
+            bad = pr::build_tile_sum<T, 1, true>(b.Kd, b.FU, b.FV, b.nf, b.Kr, b.Kp, b.hd,
+                                                 a.A + (int64_t)(li - i) * GT, ld, b.n, b.sigma2, (int64_t)i * GT,
+                                                 (int64_t)j * GT, smem, tid);
             if (__builtin_amdgcn_readfirstlane(__any(bad))) atomicOr(b.flag, 1);  // wave-uniform branch
             publish(a.ver + (int64_t)i * a.nc + j, 0, false);
         } else if (type == T_UPD) {
             // variant 64 (timing experiment, wrong results): every update streams the same
             // L2-resident operands, to separate memory-feed from MFMA limits
-            const int64_t oa = (a.variant & 64) ? 0 : (int64_t)i * GT + (int64_t)b0 * GT * ld;
-            const int64_t ob = (a.variant & 64) ? GT : (int64_t)j * GT + (int64_t)b0 * GT * ld;
-            if (!(a.variant & 2)) tile_gemm<T, true>(Ci + (int64_t)j * GT * ld, ld, a.A + oa, ld, a.A + ob, ld, nb * GT,
-                                                     i == j, smem, tid);
+            const int64_t oa = (a.variant & 64) ? 0 : (int64_t)li * GT + (int64_t)b0 * GT * ld;
+            if constexpr (DIST) {
+                // row j of this rank: its stored tiles; of another rank: its received tiles, one
+                // per panel (one call site: two inlined mainloops crashed hipcc 7.2)
+                const int lj = __builtin_amdgcn_readfirstlane(a.dist->loc[j]);
+                const bool loc = lj >= 0;
+                const T* Bop = loc ? a.A + (int64_t)lj * GT + (int64_t)b0 * GT * ld : nullptr;
+                const uint64_t* bp = loc ? nullptr : reinterpret_cast<const uint64_t*>(a.dist->tptr) + (int64_t)j * a.nc + b0;
+                tile_gemm<T, true>(Ci + (int64_t)j * GT * ld, ld, a.A + oa, ld, Bop, loc ? ld : (int64_t)DB, nb * GT,
+                                   i == j, smem, tid, false, bp);
+            } else {
+                const int64_t ob = (a.variant & 64) ? GT : (int64_t)j * GT + (int64_t)b0 * GT * ld;
+                if (!(a.variant & 2))
+                    tile_gemm<T, true>(Ci + (int64_t)j * GT * ld, ld, a.A + oa, ld, a.A + ob, ld, nb * GT, i == j,
+                                       smem, tid);
+            }
             publish(a.ver + (int64_t)i * a.nc + j, b0 + nb, false);
         } else if (type == T_TRSM) {
             T* Cik = Ci + (int64_t)j * GT * ld;
+            T* send = nullptr;
+            if constexpr (DIST) send = a.dist->sptr[(int64_t)i * a.nc + j];
             if (!(a.variant & 1))
-                tile_gemm<T, false>(Cik, ld, Cik, ld, a.Linv + (int64_t)j * DB * DB, DB, GT, false, smem, tid, true);
+                tile_gemm<T, false>(Cik, ld, Cik, ld, a.Linv + (int64_t)j * DB * DB, DB, GT, false, smem, tid, true,
+                                    nullptr, send);
             publish(a.lcnt + i, j + 1, false);
+            if constexpr (DIST) {
+                if (send) publish_host(a.dist->hslot + (int64_t)i * a.nc + j);
+            }
         } else {  // DIAGX(k = i)
             const int k = i;
             T* Akk = Ci + (int64_t)k * GT * ld;
             long long dt[4] = {0, 0, 0, 0};
             if (k > 0) {
                 T* Akm = Ci + (int64_t)(k - 1) * GT * ld;
+                T* send = nullptr;
+                if constexpr (DIST) send = a.dist->sptr[(int64_t)k * a.nc + (k - 1)];
                 tile_gemm<T, false>(Akm, ld, Akm, ld, a.Linv + (int64_t)(k - 1) * DB * DB, DB, GT, false, smem, tid,
-                                    true);
+                                    true, nullptr, send);
                 if (a.trace) dt[0] = wall_clock64();
                 publish(a.lcnt + k, k, false);  // L_{k,k-1} final: unblocks the updates of column k
+                if constexpr (DIST) {
+                    if (send) publish_host(a.dist->hslot + (int64_t)k * a.nc + (k - 1));
+                }
                 if (a.trace) dt[1] = wall_clock64();
                 tile_gemm<T, true>(Akk, ld, Akm, ld, Akm, ld, GT, true, smem, tid);
                 local_sync();
@@ -549,6 +629,7 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
                            a.trace ? a.trace + 4 * (int64_t)(a.ntasks + a.nc) + 4 * (int64_t)k : nullptr);
             if (a.trace) dt[3] = wall_clock64();
             publish(a.lcnt + k, k + 1, true);  // diag_factor stores are plain
+            if constexpr (DIST) publish_host(a.dist->hdiag + k);
             if (a.trace && wv == 0) {
                 long long* dp = a.trace + 4 * (int64_t)a.ntasks + 4 * (int64_t)k;
                 for (int u = 0; u < 4; u++) dp[u] = dt[u];
@@ -777,6 +858,203 @@ static Schedule make_schedule(int nc, int nr, int W, int near, int P, const Cost
     return S;
 }
 
+// ------------------------------------------------------------------------------------------
+// Distributed schedule: the same task DAG with row block i on rank i mod g, plus the two
+// transport steps of every panel as timed nodes that occupy no worker:
+//   bcast(k)  Linv_k from DIAGX(k)'s rank to all ranks (its consumers elsewhere: TRSM(., k),
+//             DIAGX(k + 1)); after bcast(k - 1) (one broadcast stream)
+//   panel(b)  every final tile L_ib (i > b) to every other rank (consumers: updates of tiles
+//             (i', i) on other ranks); after all its producers on all ranks and panel(b - 1)
+// A task whose input lives on another rank depends on the transport node instead of the
+// producer.  Simulated on g x P workers (each task on its rank's P); each rank's ticket list
+// is its tasks in start order.  The simulation order is one topological order of the whole
+// DAG, transport included, so on every rank the smallest unfinished ticket can proceed once
+// the transport has delivered what precedes it: the single-GPU deadlock argument, extended.
+// ------------------------------------------------------------------------------------------
+struct DistSchedule {
+    std::vector<std::vector<int4>> lists;  // per rank
+    double est_us = 0;
+};
+
+static DistSchedule make_schedule_dist(int nc, int nr, int W, int near, int P, int g, const Cost& cm, bool build,
+                                       double bcast_us, double tile_us) {
+    std::vector<Task> tasks;
+    std::vector<int> rank_of;  // -1: transport node
+    tasks.reserve((size_t)nr * nc * 2);
+    auto add = [&](int type, int i, int j, int b0, int nb, double dur, int rk) {
+        Task tk;
+        tk.type = type;
+        tk.i = i;
+        tk.j = j;
+        tk.b0 = b0;
+        tk.nb = nb;
+        tk.dur = dur;
+        tasks.push_back(std::move(tk));
+        rank_of.push_back(rk);
+        return (int)tasks.size() - 1;
+    };
+    auto own = [&](int i) { return i % g; };
+    std::vector<int> diagx(nc, -1), bcast(nc, -1), panel(nc, -1);
+    std::vector<int> trsm((size_t)nr * nc, -1), last_upd((size_t)nr * nc, -1);
+    std::vector<std::vector<int>> deps, edeps;
+    auto dep = [&](int tsk, int on, bool early = false) {
+        if (on < 0) return;
+        auto& d = early ? edeps : deps;
+        if ((int)d.size() <= tsk) d.resize(tsk + 1);
+        d[tsk].push_back(on);
+    };
+    auto prodL = [&](int i, int b, bool& early) -> int {
+        early = i < nc && b == i - 1;
+        if (i < nc && (b == i || b == i - 1)) return diagx[i];
+        return trsm[(size_t)i * nc + b];
+    };
+    // Linv_k as seen from rank rk
+    auto linv = [&](int k, int rk) { return own(k) == rk ? diagx[k] : bcast[k]; };
+    struct Chunk {
+        int i, j, b0, nb;
+    };
+    std::vector<std::vector<Chunk>> by_last(nc);
+    {
+        std::vector<std::pair<int, int>> ch;
+        for (int j = 1; j < nc; j++)
+            for (int i = j; i < nr; i++) {
+                tile_chunks(i, j, W, near, ch, 0);
+                for (auto& c : ch) by_last[c.first + c.second - 1].push_back(Chunk{i, j, c.first, c.second});
+            }
+    }
+    auto make_diagx = [&](int k) {
+        const int id = add(T_DIAGX, k, k, 0, 0, (k == 0) ? cm.diag0 : cm.diagx, own(k));
+        diagx[k] = id;
+        if (k >= 1) {
+            dep(id, linv(k - 1, own(k)));
+            dep(id, last_upd[(size_t)k * nc + (k - 1)]);
+            dep(id, last_upd[(size_t)k * nc + k]);
+        }
+        const int b = add(-1, k, k, 0, 0, bcast_us, -1);  // bcast(k)
+        bcast[k] = b;
+        dep(b, id);
+        if (k >= 1) dep(b, bcast[k - 1]);
+    };
+    if (build)
+        for (int i = 0; i < nc; i++)
+            for (int j = 0; j <= i; j++) last_upd[(size_t)i * nc + j] = add(T_BUILD, i, j, 0, 0, cm.build, own(i));
+    make_diagx(0);
+    dep(diagx[0], last_upd[0]);
+    for (int k = 0; k < nc; k++) {
+        for (int i = k + 1; i < nr; i++) {
+            if (i == k + 1 && i < nc) continue;  // inside DIAGX(k+1)
+            const int id = add(T_TRSM, i, k, 0, 0, cm.trsm, own(i));
+            trsm[(size_t)i * nc + k] = id;
+            dep(id, linv(k, own(i)));
+            dep(id, last_upd[(size_t)i * nc + k]);
+        }
+        if (k + 1 < nc) make_diagx(k + 1);
+        {  // panel(k): every tile L_ik, i > k, delivered everywhere
+            const int ntile = nr - k - 1;
+            const int pn = add(-2, k, k, 0, 0, ntile > 0 ? tile_us * ntile : 0.0, -1);
+            panel[k] = pn;
+            for (int i = k + 1; i < nr; i++) {
+                bool e;
+                const int p = prodL(i, k, e);
+                dep(pn, p, e);
+            }
+            if (k >= 1) dep(pn, panel[k - 1]);
+        }
+        for (const Chunk& c : by_last[k]) {
+            const int rk = own(c.i);
+            const double dur = cm.ovh + c.nb * cm.k128 * (c.i == c.j ? cm.diagf : 1.0);
+            const int id = add(T_UPD, c.i, c.j, c.b0, c.nb, dur, rk);
+            dep(id, last_upd[(size_t)c.i * nc + c.j]);
+            bool e1, e2;
+            const int p1 = prodL(c.i, k, e1);
+            dep(id, p1, e1);
+            if (own(c.j) == rk) {
+                const int p2 = prodL(c.j, k, e2);
+                dep(id, p2, e2);
+            } else {
+                dep(id, panel[k]);
+            }
+            last_upd[(size_t)c.i * nc + c.j] = id;
+        }
+    }
+    const int nt = (int)tasks.size();
+    deps.resize(nt);
+    edeps.resize(nt);
+    for (int id = 0; id < nt; id++) {
+        auto& d = deps[id];
+        auto& ed = edeps[id];
+        std::sort(d.begin(), d.end());
+        d.erase(std::unique(d.begin(), d.end()), d.end());
+        std::sort(ed.begin(), ed.end());
+        ed.erase(std::unique(ed.begin(), ed.end()), ed.end());
+        for (int on : d) {
+            if (on >= id) throw Error{GPRX_ERR_ARG, "potrf dist schedule: producer created after consumer"};
+            tasks[on].succ.push_back(id);
+        }
+        int ne = 0;
+        for (int on : ed) {
+            if (on >= id) throw Error{GPRX_ERR_ARG, "potrf dist schedule: producer created after consumer"};
+            if (std::binary_search(d.begin(), d.end(), on)) continue;
+            tasks[on].esucc.push_back(id);
+            ne++;
+        }
+        tasks[id].ndep = (int)d.size() + ne;
+    }
+    for (int id = nt - 1; id >= 0; id--) {
+        double m = 0;
+        for (int s2 : tasks[id].succ) m = std::max(m, tasks[s2].bl);
+        for (int s2 : tasks[id].esucc) m = std::max(m, tasks[s2].bl - (tasks[id].dur - cm.early));
+        tasks[id].bl = tasks[id].dur + m;
+    }
+    typedef std::pair<double, int> PQ;
+    std::vector<std::priority_queue<PQ>> ready(g);
+    std::priority_queue<PQ, std::vector<PQ>, std::greater<PQ>> running;
+    std::vector<int> indeg(nt), freew(g, P);
+    DistSchedule S;
+    S.lists.resize(g);
+    double now = 0;
+    int started = 0;
+    auto make_ready = [&](int id) {
+        if (rank_of[id] < 0) {  // transport: starts at once, no worker
+            running.push({now + tasks[id].dur, id});
+            started++;
+        } else {
+            ready[rank_of[id]].push({tasks[id].bl, id});
+        }
+    };
+    for (int id = 0; id < nt; id++) {
+        indeg[id] = tasks[id].ndep;
+        if (indeg[id] == 0) make_ready(id);
+    }
+    while (started < nt || !running.empty()) {
+        for (int rk = 0; rk < g; rk++)
+            while (freew[rk] > 0 && !ready[rk].empty()) {
+                const int id = ready[rk].top().second;
+                ready[rk].pop();
+                const Task& tk = tasks[id];
+                S.lists[rk].push_back(make_int4(tk.type | (tk.nb << 8), tk.i, tk.j, tk.b0));
+                running.push({now + tk.dur, id});
+                if (!tk.esucc.empty()) running.push({now + std::min(cm.early, tk.dur), -1 - id});
+                freew[rk]--;
+                started++;
+            }
+        if (running.empty()) throw Error{GPRX_ERR_ARG, "potrf dist schedule: dependency cycle"};
+        const PQ f = running.top();
+        running.pop();
+        now = f.first;
+        if (f.second < 0) {
+            for (int s2 : tasks[-1 - f.second].esucc)
+                if (--indeg[s2] == 0) make_ready(s2);
+            continue;
+        }
+        if (rank_of[f.second] >= 0) freew[rank_of[f.second]]++;
+        for (int s2 : tasks[f.second].succ)
+            if (--indeg[s2] == 0) make_ready(s2);
+    }
+    S.est_us = now;
+    return S;
+}
+
 struct Params {
     // r01i sweep (scripts/sched_sweep.sh): at N = 16384 W = 64 with no single-panel tail is
     // 1.6-2.0% faster than W = 32, near = 1; at N = 4096 (chain-bound) near = 1 stays 6% faster
@@ -937,6 +1215,7 @@ void potrf_tiles(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info
     a.ver = st.ctr + C_NCTL + nr;
     a.info = info;
     a.tb = nullptr;
+    a.dist = nullptr;
     if (fused) {
         GPRX_REQUIRE(build->nf == np, GPRX_ERR_ARG, "potrf_tiles: build features must have np rows");
         if (!st.tb) GPRX_HIP(hipMalloc(&st.tb, sizeof(TileBuild<double>)));
@@ -974,19 +1253,64 @@ void potrf_tiles(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info
     const size_t lds = lds_of(pt_lds_bytes<T>());
     static bool attr = false;
     if (!attr) {
-        GPRX_HIP(hipFuncSetAttribute((const void*)potrf_tiles_kernel<double>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     (int)lds_of(pt_lds_bytes<double>())));
-        GPRX_HIP(hipFuncSetAttribute((const void*)potrf_tiles_kernel<float>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     (int)lds_of(pt_lds_bytes<float>())));
+        GPRX_HIP(hipFuncSetAttribute((const void*)potrf_tiles_kernel<double, false>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_of(pt_lds_bytes<double>())));
+        GPRX_HIP(hipFuncSetAttribute((const void*)potrf_tiles_kernel<float, false>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_of(pt_lds_bytes<float>())));
         attr = true;
     }
     const double nn = (double)np;
     ProfScope ps(KC_TILES, s,
                  nn * nn * nn / 3.0 + (double)(nrows - np - (int64_t)ni * GT) * nn * nn + (ni ? nn * nn * nn / 3.0 : 0.0),
                  0.0);
-    hipLaunchKernelGGL(potrf_tiles_kernel<T>, dim3((unsigned)st.ncu), dim3(NT), lds, s, a);
+    hipLaunchKernelGGL((potrf_tiles_kernel<T, false>), dim3((unsigned)st.ncu), dim3(NT), lds, s, a);
     GPRX_HIP(hipGetLastError());
 }
+
+// ---- distributed factorisation: per-rank ticket lists and one rank's launch ------------------
+std::vector<std::vector<int4>> potrf_dist_schedule(int nc, int nr, int P, int g, bool build, double* est_us) {
+    const pt::Params& pr = pt::params();
+    double bcast_us = 15.0, tile_us = 0.3;  // transport estimates: a broadcast's latency, one tile
+    if (const char* e = std::getenv("GPRX_DIST_BCAST_US")) bcast_us = std::atof(e);
+    if (const char* e = std::getenv("GPRX_DIST_TILE_US")) tile_us = std::atof(e);
+    pt::DistSchedule S = pt::make_schedule_dist(nc, nr, pr.W, pr.near_for(nc), P, g, pr.cm, build, bcast_us, tile_us);
+    if (est_us) *est_us = S.est_us;
+    return S.lists;
+}
+
+template <typename T>
+void potrf_tiles_dist_launch(const DistLaunch<T>& L) {
+    using namespace pt;
+    Args<T> a;
+    std::memset(&a, 0, sizeof(a));
+    a.A = L.A;
+    a.ld = L.ld;
+    a.Linv = L.Linv;
+    a.tasks = L.list;
+    a.ntasks = L.ntasks;
+    a.nc = L.nc;
+    a.ctl = L.ctr;
+    a.lcnt = L.ctr + C_NCTL;
+    a.ver = L.ctr + C_NCTL + L.nr;
+    a.info = L.info;
+    a.tlimit = L.tlimit;
+    a.tb = L.tb_dev;
+    a.dist = L.dist_dev;
+    auto lds_of = [](size_t b) { return std::max<size_t>(b + 16, 96 * 1024); };
+    const size_t lds = lds_of(pt_lds_bytes<T>());
+    static bool attr = false;
+    if (!attr) {
+        GPRX_HIP(hipFuncSetAttribute((const void*)potrf_tiles_kernel<double, true>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_of(pt_lds_bytes<double>())));
+        GPRX_HIP(hipFuncSetAttribute((const void*)potrf_tiles_kernel<float, true>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_of(pt_lds_bytes<float>())));
+        attr = true;
+    }
+    hipLaunchKernelGGL((potrf_tiles_kernel<T, true>), dim3((unsigned)L.P), dim3(NT), lds, L.s, a);
+    GPRX_HIP(hipGetLastError());
+}
+template void potrf_tiles_dist_launch<double>(const DistLaunch<double>&);
+template void potrf_tiles_dist_launch<float>(const DistLaunch<float>&);
 
 // Host-only schedule statistics (no device work): tasks, predicted makespan, and a check
 // that every task's producers come earlier in the ticket order.

@@ -120,6 +120,7 @@ def lib():
         L.gprx_ctx_get_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(KStat), ctypes.c_int32,
                                          ctypes.POINTER(ctypes.c_int32)]
         # developer / parity hooks (include/gprx_dev.h)
+        L.gprx_ctx_create_virtual.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
         L.gprx_dev_build_matrix.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(KernelDesc),
                                             ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_double,
                                             ctypes.c_int32, ctypes.c_void_p]
@@ -175,9 +176,13 @@ def unique_id():
 class Context:
     """One per process per GPU (gprx_ctx)."""
 
-    def __init__(self, device=0, dist=None):
+    def __init__(self, device=0, dist=None, virtual=0):
+        """dist = (rank, world, unique_id): one RCCL rank per process; virtual = g: g virtual
+        ranks of the distributed fit in this process on one GPU (gprx_ctx_create_virtual)."""
         h = ctypes.c_void_p()
-        if dist is None:
+        if virtual:
+            _check(lib().gprx_ctx_create_virtual(device, int(virtual), ctypes.byref(h)))
+        elif dist is None:
             _check(lib().gprx_ctx_create(device, ctypes.byref(h)))
         else:
             rank, world, uid = dist

@@ -155,8 +155,14 @@ gprx_status gprx_model_set_noise(gprx_model* model, double sigma);
                                       gprx_fit_info.method = 1 then.  An exactly singular matrix
                                       gives GPRX_ERR_SINGULAR (the reference returns non-finite
                                       regression vectors there) */
-#define GPRX_FIT_DISTRIBUTED 2u    /* multi-GPU factorisation on a gprx_ctx_create_dist context
-                                      (implied when world > 1; forces the path at world = 1) */
+#define GPRX_FIT_DISTRIBUTED 2u    /* multi-GPU fit on a gprx_ctx_create_dist context (implied when
+                                      world > 1; forces the path at world = 1): row blocks dealt
+                                      cyclically over the ranks (N^2/world of the factor per GPU),
+                                      one persistent tile launch per rank, RCCL broadcast of each
+                                      diagonal-block inverse and exchange of each factored panel.
+                                      Afterwards alpha, predict and the LML value are available;
+                                      the posterior covariance, core matrix and LML gradient need a
+                                      single-GPU fit */
 #define GPRX_FIT_F32_NO_REFINE 4u  /* fp32 models: skip the fp64 iterative refinement of alpha.  By
                                       default an fp32 fit factorises in fp32 and refines alpha in
                                       fp64 until it agrees with the double solve: the reference

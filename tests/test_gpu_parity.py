@@ -212,9 +212,9 @@ def test_set_alpha_restores_predict(ctx, ks):
 @pytest.mark.parametrize("dtype", DTYPES)
 @pytest.mark.parametrize("n", [700, 1536])
 def test_distributed_fit_one_rank(dtype, n):
-    """The multi-GPU factorisation (potrf_dist: panel-cyclic ownership, look-ahead, RCCL
-    broadcast of factored panels) on a one-rank RCCL communicator, forced by
-    GPRX_FIT_DISTRIBUTED: same alpha / predictions / logdet as the single-GPU path."""
+    """The multi-GPU fit (gprx_dist.cpp: row-cyclic sharded storage, per-rank tile launch,
+    RCCL transport) on a one-rank RCCL communicator, forced by GPRX_FIT_DISTRIBUTED: same
+    alpha / predictions / logdet as the single-GPU path."""
     import gpr_amd
     from gpr_amd import gprx
     ks = KERNELS[4]
