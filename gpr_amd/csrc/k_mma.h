@@ -119,7 +119,11 @@ __device__ __forceinline__ void tile_mma(typename Mfma<T>::acc_t (&acc)[2][4], c
             const T* src;
             if (isB && Bpan) {  // the stage's 16 columns lie in one 128-column panel
                 // (addresses as integers: a pointer-to-pointer operand crashed hipcc 7.2)
-                const T* pb = reinterpret_cast<const T*>((uint64_t)__builtin_amdgcn_readfirstlane((long long)Bpan[(st * BKS) >> 7]));
+                // (__builtin_amdgcn_readfirstlane is 32-bit: the halves separately)
+                const uint64_t pv = Bpan[(st * BKS) >> 7];
+                const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)pv);
+                const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(pv >> 32));
+                const T* pb = reinterpret_cast<const T*>(((uint64_t)hi << 32) | lo);
                 src = pb + lrow + (col & (GT - 1)) * ldb;
             } else {
                 src = isB ? (B + lrow + col * ldb) : (A + lrow + col * lda);
