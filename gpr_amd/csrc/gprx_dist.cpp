@@ -577,6 +577,29 @@ void dist_fit(DistEngineBase*& eng, const DistContext& C, const DistFitIn<T>& in
     GPRX_HIP(hipStreamSynchronize(E.sB));
     GPRX_HIP(hipStreamSynchronize(E.sP));
     GPRX_HIP(hipGetLastError());
+    static const bool dbg = std::getenv("GPRX_DIST_DEBUG") != nullptr;
+    if (dbg || flush) {  // the state the issue loop ended in (flush: a stall)
+        for (auto& Rp : E.ranks) {
+            DistRank<T>& R = *Rp;
+            unsigned rc[2] = {0, 0};
+            int ctl[2] = {0, 0};
+            GPRX_HIP(hipMemcpy(rc, R.drecv.p, sizeof(rc), hipMemcpyDeviceToHost));
+            GPRX_HIP(hipMemcpy(ctl, R.ctr.p, sizeof(ctl), hipMemcpyDeviceToHost));
+            int nd = 0, ns = 0, nsw = 0;
+            for (int k = 0; k < nc; k++) nd += R.hdiag.u()[k] != 0;
+            for (int i = 0; i < nr; i++)
+                for (int b = 0; b < std::min(i, nc); b++)
+                    if (E.L.owner(i) == R.r) {
+                        nsw++;
+                        ns += R.hslot.u()[(size_t)i * nc + b] != 0;
+                    }
+            std::fprintf(stderr,
+                         "gprx dist rank %d/%d: P %d tickets %d/%d err %d | diag flags %d/%d (own) send slots %d/%d | "
+                         "drecv %u precv %u | issued bcast %d panel %d of %d%s\n",
+                         R.r, E.g, E.P, ctl[0], R.ntasks, ctl[1], nd, (nc - R.r + E.g - 1) / E.g, ns, nsw, rc[0], rc[1],
+                         kb, kp, nc, flush ? " (flushed)" : "");
+        }
+    }
     // ---- reductions, back substitution (every rank holds every tile) -------------------------
     double logdet = 0, datafit = 0;
     int info = INT_MAX, flag = 0;
