@@ -167,7 +167,8 @@ struct DistRank {
     hipStream_t s = nullptr;  // compute stream
     bool own_stream = false;
     DMem A, Linv, send, recv, ctr, info, flag, pd, loc, tptr, sptr, drecv, tiles, tld, red, alpha, tab, list;
-    HMem hdiag, hslot;
+    HMem hdiag, hslot, dbg;
+    std::vector<int4> hlist;
     int64_t ld = 0;
     int ntasks = 0;
     hipEvent_t done = nullptr;
@@ -375,6 +376,7 @@ static void setup(DistEngine<T>& E, const DistContext& C, int64_t n, int m, bool
         R->pd.ensure(sizeof(PtDist<T>));
         GPRX_HIP(hipMemcpy(R->pd.p, &pd, sizeof(pd), hipMemcpyHostToDevice));
         const std::vector<int4>& lst = E.lists[r];
+        R->hlist = lst;
         R->ntasks = (int)lst.size();
         R->list.ensure(sizeof(int4) * std::max<size_t>(1, lst.size()));
         if (!lst.empty()) GPRX_HIP(hipMemcpy(R->list.p, lst.data(), sizeof(int4) * lst.size(), hipMemcpyHostToDevice));
@@ -546,6 +548,13 @@ void dist_fit(DistEngineBase*& eng, const DistContext& C, const DistFitIn<T>& in
         Lc.tlimit = (long long)(1e8 * (2.0 + 20.0 * E.est_us * 1e-6));
         Lc.P = E.P;
         Lc.s = s;
+        Lc.dbg = nullptr;
+        static const bool dbgw = std::getenv("GPRX_DIST_DEBUG") != nullptr;
+        if (dbgw) {
+            R.dbg.ensure(sizeof(int) * 4 * E.P);
+            std::memset(R.dbg.p, 0xff, sizeof(int) * 4 * E.P);
+            GPRX_HIP(hipHostGetDevicePointer((void**)&Lc.dbg, R.dbg.p, 0));
+        }
         potrf_tiles_dist_launch<T>(Lc);
         GPRX_HIP(hipEventRecord(R.done, s));
     }
@@ -570,6 +579,24 @@ void dist_fit(DistEngineBase*& eng, const DistContext& C, const DistFitIn<T>& in
         bool all_done = true;
         for (auto& R : E.ranks) all_done &= hipEventQuery(R->done) == hipSuccess;
         const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - ts).count();
+        static const bool dbgw = std::getenv("GPRX_DIST_DEBUG") != nullptr;
+        if (dbgw && !flush && el > 1.0) {  // a stall: where every workgroup waits
+            for (auto& Rp : E.ranks) {
+                const int* w = reinterpret_cast<const int*>(Rp->dbg.p);
+                std::fprintf(stderr, "gprx dist stall rank %d (issued bcast %d panel %d, %.2f s):", Rp->r, kb, kp, el);
+                for (int x = 0; x < E.P; x++) {
+                    const int q = __atomic_load_n(w + 4 * x, __ATOMIC_ACQUIRE), ph = w[4 * x + 1];
+                    if (q < 0 || q >= (int)Rp->hlist.size() || ph % 10 != 1) continue;
+                    const int4 t = Rp->hlist[q];
+                    std::fprintf(stderr, " [t%d %s(%d,%d,b0 %d,nb %d)]", q,
+                                 (t.x & 255) == 0 ? "DIAGX" : (t.x & 255) == 1 ? "TRSM" : (t.x & 255) == 2 ? "UPD" : "BUILD",
+                                 t.y, t.z, t.w, t.x >> 8);
+                }
+                std::fprintf(stderr, "\n");
+            }
+            flush = true;
+            continue;
+        }
         if (all_done || el > limit_s) flush = true;
         else std::this_thread::yield();
     }

@@ -399,6 +399,7 @@ struct DistLaunch {
     long long tlimit;  // wall-clock ticks (100 MHz) a single wait may take
     int P;             // workgroups (one per CU)
     hipStream_t s;
+    int* dbg;          // optional: per-workgroup {ticket, phase, i, j} in coherent host memory
 };
 // Per-rank ticket lists of the distributed factorisation (row block i on rank i mod g).
 std::vector<std::vector<int4>> potrf_dist_schedule(int nc, int nr, int P, int g, bool build, double* est_us);

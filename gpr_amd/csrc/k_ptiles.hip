@@ -1296,6 +1296,7 @@ void potrf_tiles_dist_launch(const DistLaunch<T>& L) {
     a.tlimit = L.tlimit;
     a.tb = L.tb_dev;
     a.dist = L.dist_dev;
+    a.dbg = L.dbg;
     auto lds_of = [](size_t b) { return std::max<size_t>(b + 16, 96 * 1024); };
     const size_t lds = lds_of(pt_lds_bytes<T>());
     static bool attr = false;
