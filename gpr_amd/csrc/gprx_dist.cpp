@@ -481,8 +481,8 @@ void dist_fit(DistEngineBase*& eng, const DistContext& C, const DistFitIn<T>& in
     const int64_t np = (int64_t)nc * DB, n = in.n;
     const int64_t DB2 = (int64_t)DB * DB;
     DistRank<T>& R0 = *E.ranks[0];
-    // ---- per rank: reset, build, launch -----------------------------------------------------
-    auto ts = std::chrono::steady_clock::now();
+    // ---- per rank: reset, build; then the launches -------------------------------------------
+    std::vector<DistLaunch<T>> launches(E.ranks.size());
     for (auto& Rp : E.ranks) {
         DistRank<T>& R = *Rp;
         const int r = R.r;
@@ -531,9 +531,12 @@ void dist_fit(DistEngineBase*& eng, const DistContext& C, const DistFitIn<T>& in
         if (fused) {
             R.red.ensure(std::max<size_t>(R.red.bytes, sizeof(TileBuild<T>) + 64));
             tbdev = static_cast<char*>(R.red.p) + 64;  // after the reduction doubles
-            GPRX_HIP(hipMemcpyAsync(tbdev, &tbl, sizeof(tbl), hipMemcpyHostToDevice, s));
+            // synchronous, before any rank's persistent launch: a pageable copy queued behind
+            // one could wait for it (and the virtual ranks' launches must be co-resident)
+            GPRX_HIP(hipStreamSynchronize(s));
+            GPRX_HIP(hipMemcpy(tbdev, &tbl, sizeof(tbl), hipMemcpyHostToDevice));
         }
-        DistLaunch<T> Lc;
+        DistLaunch<T>& Lc = launches[&Rp - &E.ranks[0]];
         Lc.A = A;
         Lc.ld = R.ld;
         Lc.Linv = R.Linv.template as<T>();
@@ -555,21 +558,30 @@ void dist_fit(DistEngineBase*& eng, const DistContext& C, const DistFitIn<T>& in
             std::memset(R.dbg.p, 0xff, sizeof(int) * 4 * E.P);
             GPRX_HIP(hipHostGetDevicePointer((void**)&Lc.dbg, R.dbg.p, 0));
         }
-        potrf_tiles_dist_launch<T>(Lc);
-        GPRX_HIP(hipEventRecord(R.done, s));
+    }
+    // every rank's persistent launch back to back, nothing that could block in between
+    for (size_t v = 0; v < E.ranks.size(); v++) {
+        potrf_tiles_dist_launch<T>(launches[v]);
+        GPRX_HIP(hipEventRecord(E.ranks[v]->done, E.ranks[v]->s));
     }
     // ---- issue loop: transport steps as their inputs become ready --------------------------
+    const auto ts = std::chrono::steady_clock::now();
     int kb = 0, kp = 0;
     bool flush = false;
+    double issue_s = 0;  // host time spent inside the transport calls (diagnostics)
     const double limit_s = 4.0 + 40.0 * E.est_us * 1e-6;
     while (kb < nc || kp < nc) {
         bool progress = false;
         if (kb < nc && (flush || bcast_ready(E, kb))) {
+            const auto t0 = std::chrono::steady_clock::now();
             issue_bcast(E, kb++);
+            issue_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
             progress = true;
         }
         if (kp < nc && kp < kb + 1 && (flush || panel_ready(E, kp))) {
+            const auto t0 = std::chrono::steady_clock::now();
             issue_panel(E, kp++);
+            issue_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
             progress = true;
         }
         if (progress || flush) continue;
@@ -580,10 +592,14 @@ void dist_fit(DistEngineBase*& eng, const DistContext& C, const DistFitIn<T>& in
         for (auto& R : E.ranks) all_done &= hipEventQuery(R->done) == hipSuccess;
         const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - ts).count();
         static const bool dbgw = std::getenv("GPRX_DIST_DEBUG") != nullptr;
-        if (dbgw && !flush && el > 1.0) {  // a stall: where every workgroup waits
+        if (dbgw && !flush && el > 0.5) {  // a stall: where every workgroup waits
             for (auto& Rp : E.ranks) {
                 const int* w = reinterpret_cast<const int*>(Rp->dbg.p);
-                std::fprintf(stderr, "gprx dist stall rank %d (issued bcast %d panel %d, %.2f s):", Rp->r, kb, kp, el);
+                unsigned rc[2] = {9999, 9999};
+                (void)hipMemcpy(rc, Rp->drecv.p, sizeof(rc), hipMemcpyDeviceToHost);
+                std::fprintf(stderr, "gprx dist stall rank %d (issued bcast %d panel %d, %.3f s; device drecv %u precv %u; "
+                                     "issue calls took %.3f s):",
+                             Rp->r, kb, kp, el, rc[0], rc[1], issue_s);
                 for (int x = 0; x < E.P; x++) {
                     const int q = __atomic_load_n(w + 4 * x, __ATOMIC_ACQUIRE), ph = w[4 * x + 1];
                     if (q < 0 || q >= (int)Rp->hlist.size() || ph % 10 != 1) continue;
