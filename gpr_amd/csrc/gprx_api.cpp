@@ -506,6 +506,10 @@ static gprx_status model_fit_dist(gprx_model* M, gprx_fit_info* out) {
     M->alpha.ensure(sizeof(T) * np * M->m);
     M->flag.ensure(sizeof(int));
     GPRX_HIP(hipMemsetAsync(M->flag.p, 0, sizeof(int), s));
+    if (K.nper > 0) {  // per-sample sin/cos tables: the direct predict path reads them
+        M->tab.ensure(sizeof(T) * 2 * K.nper * n * M->d);
+        launch_sincos_tables<T>(K, M->X.as<T>(), n, M->d, M->tab.as<T>(), s);
+    }
     const T sig = (T)M->sigma;
     const T sigma2 = sig * sig;  // m_Sigma*m_Sigma in T (lib/GaussianProcess.cpp:379)
     TileBuild<T> tb;

@@ -276,21 +276,39 @@ static void setup(DistEngine<T>& E, const DistContext& C, int64_t n, int m, bool
     E.virt = C.virt;
     E.device = C.device;
     E.L.init(E.g, nc, nr);
-    int ncu = 0;
+    // CU partition.  The transport kernels (RCCL, copies) and every (virtual) rank's
+    // persistent launch run on streams whose CU masks are disjoint: a persistent launch can
+    // never starve the transport of CUs, nor one virtual rank another.  Without the masks
+    // the transport stalled behind the persistent launches (measured: 2 x 124 workgroups,
+    // the copies waited until the launches timed out).  Mask bit b selects logical CU b / X
+    // of XCC b % X (tools/cu_mask_probe.hip, gfx950; an XCC without a bit is unrestricted,
+    // so every mask covers every XCC): a CU "slot" is one CU on each XCC.
+    int ncu = 0, nxcc = 1;
     GPRX_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, C.device));
-    // CUs left free for the transport kernels (RCCL, copies, stream writes): a persistent
-    // launch on every CU would starve them (one workgroup per CU by LDS)
-    int reserve = 8;
+    if (hipDeviceGetAttribute(&nxcc, hipDeviceAttributeNumberOfXccs, C.device) != hipSuccess || nxcc < 1) nxcc = 1;
+    const int cu_xcc = std::max(1, ncu / nxcc);
+    int reserve = 1;  // transport slots
     if (const char* e = std::getenv("GPRX_DIST_RESERVE_CU")) reserve = std::max(1, std::atoi(e));
     const int nloc_ranks = E.virt ? E.g : 1;
-    E.P = std::max(1, (ncu - reserve) / nloc_ranks);
+    GPRX_REQUIRE(cu_xcc - reserve >= nloc_ranks, GPRX_ERR_ARG, "distributed fit: too many virtual ranks for the CUs");
+    const int per = (cu_xcc - reserve) / nloc_ranks;  // compute slots per rank
+    E.P = nxcc * per;  // one workgroup per CU (LDS)
     if (const char* e = std::getenv("GPRX_DIST_P")) E.P = std::max(1, std::atoi(e));
+    auto masked_stream = [&](int slot0, int nslot) {
+        std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+        for (int c = slot0; c < slot0 + nslot; c++)
+            for (int x = 0; x < nxcc; x++) {
+                const int b = c * nxcc + x;
+                if (b < ncu) mask[b / 32] |= 1u << (b % 32);
+            }
+        hipStream_t st = nullptr;
+        GPRX_HIP(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()));
+        return st;
+    };
     E.lists = potrf_dist_schedule(nc, nr, E.P, E.g, fused, &E.est_us);
     if (!E.sB) {
-        int lo = 0, hi = 0;
-        GPRX_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
-        GPRX_HIP(hipStreamCreateWithPriority(&E.sB, hipStreamNonBlocking, hi));
-        GPRX_HIP(hipStreamCreateWithPriority(&E.sP, hipStreamNonBlocking, lo));
+        E.sB = masked_stream(0, reserve);
+        E.sP = masked_stream(0, reserve);
     }
     if (!E.virt && !E.commP) {
         E.commB = C.comm;
@@ -308,12 +326,8 @@ static void setup(DistEngine<T>& E, const DistContext& C, int64_t n, int m, bool
         auto R = std::make_unique<DistRank<T>>();
         R->r = E.virt ? v : C.rank;
         const int r = R->r;
-        if (E.virt) {
-            GPRX_HIP(hipStreamCreateWithFlags(&R->s, hipStreamNonBlocking));
-            R->own_stream = true;
-        } else {
-            R->s = C.stream;
-        }
+        R->s = masked_stream(reserve + v * per, per);  // this rank's CUs
+        R->own_stream = true;
         GPRX_HIP(hipEventCreateWithFlags(&R->done, hipEventDisableTiming));
         const int nl = E.L.nloc(r);
         R->ld = (int64_t)nl * DB;
@@ -569,6 +583,7 @@ void dist_fit(DistEngineBase*& eng, const DistContext& C, const DistFitIn<T>& in
     int kb = 0, kp = 0;
     bool flush = false;
     double issue_s = 0;  // host time spent inside the transport calls (diagnostics)
+    double dbg_next = 0.25;
     const double limit_s = 4.0 + 40.0 * E.est_us * 1e-6;
     while (kb < nc || kp < nc) {
         bool progress = false;
@@ -592,26 +607,36 @@ void dist_fit(DistEngineBase*& eng, const DistContext& C, const DistFitIn<T>& in
         for (auto& R : E.ranks) all_done &= hipEventQuery(R->done) == hipSuccess;
         const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - ts).count();
         static const bool dbgw = std::getenv("GPRX_DIST_DEBUG") != nullptr;
-        if (dbgw && !flush && el > 0.5) {  // a stall: where every workgroup waits
+        if (dbgw && !flush && el > dbg_next) {  // a stall: where every workgroup is
+            dbg_next += 0.5;
             for (auto& Rp : E.ranks) {
                 const int* w = reinterpret_cast<const int*>(Rp->dbg.p);
                 unsigned rc[2] = {9999, 9999};
                 (void)hipMemcpy(rc, Rp->drecv.p, sizeof(rc), hipMemcpyDeviceToHost);
-                std::fprintf(stderr, "gprx dist stall rank %d (issued bcast %d panel %d, %.3f s; device drecv %u precv %u; "
-                                     "issue calls took %.3f s):",
-                             Rp->r, kb, kp, el, rc[0], rc[1], issue_s);
+                int nun = 0, nwait = 0, nwork = 0, nend = 0;
                 for (int x = 0; x < E.P; x++) {
+                    const int ph = __atomic_load_n(w + 4 * x + 1, __ATOMIC_ACQUIRE);
+                    nun += ph < 0;
+                    nwait += ph >= 0 && ph % 10 == 1;
+                    nwork += ph >= 0 && ph % 10 == 2;
+                    nend += ph == 9;
+                }
+                std::fprintf(stderr,
+                             "gprx dist stall rank %d (issued bcast %d panel %d, %.3f s; device drecv %u precv %u; "
+                             "issue calls took %.3f s; workgroups unstarted %d waiting %d working %d ended %d; hdiag0 %u):",
+                             Rp->r, kb, kp, el, rc[0], rc[1], issue_s, nun, nwait, nwork, nend, Rp->hdiag.u()[0]);
+                int shown = 0;
+                for (int x = 0; x < E.P && shown < 16; x++) {
                     const int q = __atomic_load_n(w + 4 * x, __ATOMIC_ACQUIRE), ph = w[4 * x + 1];
                     if (q < 0 || q >= (int)Rp->hlist.size() || ph % 10 != 1) continue;
                     const int4 t = Rp->hlist[q];
+                    shown++;
                     std::fprintf(stderr, " [t%d %s(%d,%d,b0 %d,nb %d)]", q,
                                  (t.x & 255) == 0 ? "DIAGX" : (t.x & 255) == 1 ? "TRSM" : (t.x & 255) == 2 ? "UPD" : "BUILD",
                                  t.y, t.z, t.w, t.x >> 8);
                 }
                 std::fprintf(stderr, "\n");
             }
-            flush = true;
-            continue;
         }
         if (all_done || el > limit_s) flush = true;
         else std::this_thread::yield();

@@ -7,7 +7,7 @@ import pytest
 # next to two transport streams: every stream needs a hardware queue of its own, or a
 # transport command queued behind a persistent launch on a shared queue could never run
 # (HIP's default is 4 queues per process; gpurun allows up to 32).  Set before HIP starts.
-os.environ["GPU_MAX_HW_QUEUES"] = "16"
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:

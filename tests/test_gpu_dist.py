@@ -45,6 +45,8 @@ def test_virtual_ranks_f64(g, ks, n, m):
         assert relerr(M.predict(Xq), O.predict(ks, X, a_ref, Xq)) <= 1e-6
         K = O.kernel_matrix(ks, X) + sigma * sigma * np.eye(n)
         assert abs(info.logdet - np.linalg.slogdet(K)[1]) <= 1e-9 * max(1.0, abs(info.logdet))
+        df_ref = float(np.sum(Y.reshape(n, m) * a_ref.reshape(n, m)))  # trace(Y^T K^-1 Y) = z^T z
+        assert abs(info.datafit - df_ref) <= 1e-8 * abs(df_ref)
         M.close()
     finally:
         vctx.close()
@@ -80,7 +82,14 @@ def test_virtual_ranks_repeat_and_lml_value():
         assert np.array_equal(a1, M.alpha())  # fixed schedules and summation orders: bit-identical
         v, _, logdet = M.lml(grad=False)
         vr, _, _, ldr = O.lml(C3K, X, Y, sigma, with_grad=False)
-        assert abs(v - vr) <= 1e-6 * abs(vr)
+        assert abs(logdet - ldr) <= 1e-9 * abs(ldr)
+        # the exact value from its pieces (include/Likelihood.h:166-202) ...
+        a_ref, _ = O.fit(C3K, X, Y, sigma, want_core=False)
+        v_exact = -0.5 * float(Y.reshape(-1) @ a_ref.reshape(-1)) - 0.5 * ldr - n / 2 * np.log(2 * np.pi)
+        assert abs(v - v_exact) <= 1e-8 * abs(v_exact)
+        # ... and the reference's value, whose determinant underflows double here (clamped)
+        vc, _, _ = M.lml(grad=False, compat=True)
+        assert abs(vc - vr) <= 1e-6 * abs(vr)
         with pytest.raises(gpr_amd.GprxError):
             M.posterior_cov(X[:3], X[:3])
         M.close()
