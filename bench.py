@@ -9,11 +9,15 @@ Cholesky factorisation + regression-vector solve (the reference's
 GaussianProcess<double>::Initialize, lib/GaussianProcess.cpp:118-130), inputs resident in
 HBM before the timed region.
 
-Multi-GPU: launched by torch.distributed.run, one process per GPU.  Default (--mode
-replicas): each rank fits its own independent GP (weak scaling): value = fits completed by
-all ranks / max-over-ranks time -- the throughput metric of BASELINE.json.  --mode dist:
-one fit whose factorisation is split over the ranks (panel-cyclic, RCCL broadcasts of the
-factored panels, gpr_amd/csrc/k_potrf.hip potrf_dist; strong scaling).
+Multi-GPU: launched by torch.distributed.run, one process per GPU.  The headline (--mode
+dist, the default for N > 1) is ONE fit per step whose matrix is sharded over the ranks:
+row blocks dealt cyclically (each GPU stores ~N^2/(2g) of the lower triangle and builds only
+its own tiles), each rank runs the persistent tile-dataflow factorisation on its rows, the
+diagonal-block inverses go out by RCCL broadcast and the factored panels by a full-mesh
+grouped send/recv (gpr_amd/csrc/gprx_dist.cpp; strong scaling: value = fits/s of the
+job).  The same run also measures --mode replicas (every rank fits its own GP, weak
+scaling) and reports it under "replicas"; `--mode replicas` makes that the headline.
+Predict is query-sharded over the ranks (X and alpha replicated).
 
 Prints ONE JSON line on rank 0 (plus human-readable detail on stderr).
 """
@@ -93,9 +97,11 @@ def main():
     ap.add_argument("--lml", type=int, default=1, help="also time one log-marginal likelihood + gradient "
                                                         "(BASELINE.json configs[2]); 0 = skip")
     ap.add_argument("--cpu-n", type=int, default=16384, help="N of the CPU-baseline sample (0 = skip)")
-    ap.add_argument("--mode", choices=["replicas", "dist"], default="replicas",
-                    help="N>1: independent fits per GPU (replicas, weak scaling) or one fit whose "
-                         "factorisation is split over the GPUs (dist, strong scaling, RCCL broadcasts)")
+    ap.add_argument("--mode", choices=["replicas", "dist"], default="dist",
+                    help="N>1 headline: one fit whose matrix is sharded over the GPUs (dist, strong "
+                         "scaling) or independent fits per GPU (replicas, weak scaling); both are measured")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="testing: run the sharded-fit leg (and make it the headline) even at N = 1")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -119,21 +125,14 @@ def main():
         cfg["d"] = args.d
     n, d, m = cfg["n"], cfg["d"], cfg["m"]
 
-    distributed_fit = args.mode == "dist" and world > 1
-    if distributed_fit:
-        uid = [gpr_amd.unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        ctx = gpr_amd.Context(local_rank, dist=(rank, world, uid[0]))
-    else:
-        ctx = gpr_amd.Context(local_rank)
     X, Y = make_data(n, d, m)
-    model = gpr_amd.Model(ctx, np.float64)
-    model.set_data(X, Y)
-    model.set_kernel(cfg["kernel"])
-    model.set_noise(cfg["sigma"])
 
-    for _ in range(args.warmup):
-        model.fit()
+    def make_model(c):
+        mdl = gpr_amd.Model(c, np.float64)
+        mdl.set_data(X, Y)
+        mdl.set_kernel(cfg["kernel"])
+        mdl.set_noise(cfg["sigma"])
+        return mdl
 
     def barrier_sync():
         if dist is not None:
@@ -141,41 +140,87 @@ def main():
             dist.barrier()
             torch.cuda.synchronize()
 
-    ctx.set_stats(True)
-    barrier_sync()
-    t0 = time.perf_counter()
-    infos = [model.fit() for _ in range(args.steps)]
-    barrier_sync()
-    elapsed = time.perf_counter() - t0
-    stats = ctx.stats()
-    ctx.set_stats(False)
-
-    if dist is not None:
+    def max_over_ranks(x):
+        if dist is None:
+            return x
         import torch
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([x], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        return float(t.item())
 
-    fits = args.steps * (1 if distributed_fit else world)
-    value = fits / elapsed
-    ms_per_step = 1e3 * elapsed / args.steps
+    def timed_fits(mdl, c, flags=0):
+        """W untimed warmup fits, then exactly K fits between barrier + synchronize; max over ranks."""
+        for _ in range(args.warmup):
+            mdl.fit(flags)
+        c.set_stats(True)
+        barrier_sync()
+        t0 = time.perf_counter()
+        infos = [mdl.fit(flags) for _ in range(args.steps)]
+        barrier_sync()
+        el = time.perf_counter() - t0
+        st = c.stats()
+        c.set_stats(False)
+        return max_over_ranks(el), infos, st
 
-    # prediction throughput (device time of the fused predict kernels, mean only)
+    # ---- the sharded fit over all ranks (the N > 1 headline) -------------------------------
+    dres, dist_error = None, None
+    if world > 1 or args.force_dist:
+        try:
+            uid = [gpr_amd.unique_id() if rank == 0 else None]
+            if dist is not None:
+                dist.broadcast_object_list(uid, src=0)
+            dctx = gpr_amd.Context(local_rank, dist=(rank, world, uid[0]))
+            dmodel = make_model(dctx)
+            el, infos, st = timed_fits(dmodel, dctx, gpr_amd.gprx.FIT_DISTRIBUTED)
+            dres = {"elapsed": el, "infos": infos}
+            dmodel.close()
+            dctx.close()
+        except Exception as e:  # reported; the replicas line stands in
+            dist_error = repr(e)
+            log("distributed fit failed:", dist_error)
+
+    # ---- one independent fit per GPU (the N = 1 headline; the replicas extra for N > 1) -----
+    ctx = gpr_amd.Context(local_rank)
+    model = make_model(ctx)
+    el_r, infos_r, stats = timed_fits(model, ctx)
+    replicas = {"value": world * args.steps / el_r, "ms_per_step": 1e3 * el_r / args.steps,
+                "scaling": "weak", "fits_per_step": world}
+
+    headline_dist = dres is not None and args.mode == "dist" and (world > 1 or args.force_dist)
+    if headline_dist:
+        value = args.steps / dres["elapsed"]
+        ms_per_step = 1e3 * dres["elapsed"] / args.steps
+    else:
+        value, ms_per_step = replicas["value"], replicas["ms_per_step"]
+
+    # prediction throughput, query-sharded over the ranks (X and alpha replicated): each rank
+    # predicts its contiguous slice of the Q queries; device time of the fused predict
+    # kernels, max over ranks
     pred = None
     if args.predict_q > 0:
         Xq = make_queries(args.predict_q, d)
+        lo, hi = gpr_amd.query_shard(args.predict_q, rank, world)
+        model.predict(Xq[lo:hi])
         ctx.set_stats(True)
+        barrier_sync()
         tq0 = time.perf_counter()
-        model.predict(Xq)
-        tq = time.perf_counter() - tq0
+        model.predict(Xq[lo:hi])
+        tq = max_over_ranks(time.perf_counter() - tq0)
         ps = ctx.stats().get("predict")
         ctx.set_stats(False)
-        pred = {"q": args.predict_q, "pts_per_s_device": args.predict_q / (ps["ms"] * 1e-3) if ps else None,
-                "pts_per_s_wall_incl_pcie": args.predict_q / tq}
+        pms = max_over_ranks(ps["ms"]) if ps else None
+        pred = {"q": args.predict_q, "sharded_over": world,
+                "pts_per_s_device": args.predict_q / (pms * 1e-3) if pms else None,
+                "pts_per_s_wall_incl_pcie": args.predict_q / tq,
+                # SURVEY.md 8(d): F_pred = Q N (2d + 2m) flop
+                "roofline": ({"bound": "mfma", "achieved": args.predict_q * n * (2.0 * d + 2.0 * m)
+                              / (pms * 1e-3) / 1e12 / world, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
+                              "frac": args.predict_q * n * (2.0 * d + 2.0 * m) / (pms * 1e-3) / 1e12 / world
+                              / PEAK_FP64_TFLOPS} if pms else None)}
 
     # log-marginal likelihood + gradient (refit, explicit inverse, fused gradient pass)
     lml = None
-    if args.lml and not distributed_fit:
+    if args.lml:
         model.lml(grad=True)
         ctx.set_stats(True)
         tl0 = time.perf_counter()
@@ -188,18 +233,29 @@ def main():
     # dominant kernel: the persistent tile-dataflow factorisation, one launch per fit (with
     # the covariance build fused in as BUILD tasks for sum-of-exp-leaf kernel trees).
     # Algorithmic work per launch = n^3/3 (Cholesky) + m n^2 (forward solve of the label
-    # rows); the build's work is not counted, so `achieved` understates the launch.
-    fac = stats.get("potrf_tiles", {"ms": 0, "flops": 0, "launches": 0})
+    # rows); the build's work is not counted, so `achieved` understates the launch.  For the
+    # sharded fit the launch is each rank's potrf_tiles_kernel<double, true> (device time by
+    # HIP events on its stream, max over ranks) and the peak is g GPUs'.
     alg_flops = n ** 3 / 3.0 + m * float(n) ** 2
-    avg_ms = (fac["ms"] / fac["launches"]) if fac["launches"] else 0.0
+    if headline_dist:
+        avg_ms = max_over_ranks(float(np.mean([i.ms_factor for i in dres["infos"]])))
+        infos = dres["infos"]
+        kname = "potrf_tiles_kernel<double, true> (one per rank: sharded tile-dataflow build + Cholesky, k_ptiles.hip)"
+    else:
+        fac = stats.get("potrf_tiles", {"ms": 0, "flops": 0, "launches": 0})
+        avg_ms = (fac["ms"] / fac["launches"]) if fac["launches"] else 0.0
+        infos = infos_r
+        kname = "potrf_tiles_kernel<double> (persistent tile-dataflow covariance build + Cholesky + forward solve, k_ptiles.hip)"
+    peak = PEAK_FP64_TFLOPS * (world if headline_dist else 1)
     achieved = (alg_flops / (avg_ms * 1e-3) / 1e12) if avg_ms > 0 else 0.0
     phases = {k: {"ms_per_fit": v["ms"] / args.steps, "launches_per_fit": v["launches"] / args.steps,
                   "tflops": (v["flops"] / (v["ms"] * 1e-3) / 1e12) if v["ms"] and v["flops"] else None,
                   "gbs": (v["bytes"] / (v["ms"] * 1e-3) / 1e9) if v["ms"] and v["bytes"] else None}
               for k, v in stats.items()}
-    t_roof = fit_roofline_ms(n, d, m)
-    traffic = traffic_from_profile()
-    fit_ms = np.median([i.ms_build + i.ms_factor + i.ms_solve for i in infos])
+    g_roof = world if headline_dist else 1
+    t_roof = fit_roofline_ms(n, d, m, g_roof)
+    traffic = traffic_from_profile() if not headline_dist else None
+    fit_ms = float(np.median([i.ms_build + i.ms_factor + i.ms_solve for i in infos]))
 
     if rank == 0:
         cpu = None
@@ -217,26 +273,28 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
-            "scaling": "strong" if distributed_fit else "weak",
+            "scaling": "strong" if headline_dist else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (SplitMix64 seed 0x47505231, gpr_amd/synth.py)",
             "config": {"workload": "C3: GP fit N=16384 d=32 m=1 Sum(Gaussian(2,0.15)+Periodic(0.1,pi,1)) "
                                    "sigma=1.0 fp64 (BASELINE.json configs[2])",
                        "n": n, "d": d, "m": m, "kernel": cfg["kernel"],
-                       "parallelism": (f"panel-cyclic factorisation over {world} GPUs (RCCL)" if distributed_fit
+                       "parallelism": (f"sharded: row blocks cyclic over {world} GPUs, tile-dataflow per rank, "
+                                       "RCCL broadcast + full-mesh panel exchange" if headline_dist
                                        else ("replicas" if world > 1 else "single-gpu"))},
-            "roofline": {"bound": "mfma", "kernel": "potrf_tiles_kernel<double> (persistent tile-dataflow "
-                                                      "covariance build + Cholesky + forward solve, k_ptiles.hip)",
-                         "achieved": achieved, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / PEAK_FP64_TFLOPS,
+            "roofline": {"bound": "mfma", "kernel": kname,
+                         "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+                         "frac": achieved / peak,
                          "avg_launch_us": 1e3 * avg_ms if avg_ms else None,
                          "algorithmic_flops_per_launch": alg_flops,
                          # HBM bytes per launch from the committed PMC passes (FETCH_SIZE x 2 +
                          # WRITE_SIZE, MI355X_MICROARCH.md), null if none is committed
                          "traffic": (traffic["bytes_per_launch"] if traffic else None),
                          "traffic_source": (traffic["source"] if traffic else None)},
-            "fit_roofline": {"t_roof_ms": t_roof, "t_fit_device_ms": fit_ms, "frac": t_roof / fit_ms},
+            "fit_roofline": {"t_roof_ms": t_roof, "gpus": g_roof, "t_fit_device_ms": fit_ms, "frac": t_roof / fit_ms},
+            "replicas": replicas if world > 1 else None,
+            "dist_error": dist_error,
             "phases": phases,
             "predict": pred,
             "lml_grad": lml,

@@ -546,7 +546,10 @@ static gprx_status model_fit_dist(gprx_model* M, gprx_fit_info* out) {
         out->logdet = o.logdet;
         out->datafit = o.datafit;
         out->info = (o.info == INT_MAX || o.info < 0) ? 0 : o.info;
-        out->ms_factor = ms;  // host wall time of the whole distributed fit
+        out->ms_factor = o.ms_kernel;  // device time of this process's persistent launch(es)
+        out->ms_solve = o.ms_solve;
+        out->refine_delta = 0;
+        (void)ms;  // host wall time of the whole distributed fit (GPRX_DIST_TRACE prints it)
     }
     if (hflag || o.flag)
         throw Error{GPRX_ERR_NONFINITE,

@@ -172,8 +172,12 @@ struct DistRank {
     int64_t ld = 0;
     int ntasks = 0;
     hipEvent_t done = nullptr;
+    hipEvent_t t0 = nullptr, t1 = nullptr, t2 = nullptr;  // launch start / end, back-solve end
     ~DistRank() {
         if (done) (void)hipEventDestroy(done);
+        if (t0) (void)hipEventDestroy(t0);
+        if (t1) (void)hipEventDestroy(t1);
+        if (t2) (void)hipEventDestroy(t2);
         if (own_stream && s) (void)hipStreamDestroy(s);
     }
 };
@@ -329,6 +333,9 @@ static void setup(DistEngine<T>& E, const DistContext& C, int64_t n, int m, bool
         R->s = masked_stream(reserve + v * per, per);  // this rank's CUs
         R->own_stream = true;
         GPRX_HIP(hipEventCreateWithFlags(&R->done, hipEventDisableTiming));
+        GPRX_HIP(hipEventCreate(&R->t0));
+        GPRX_HIP(hipEventCreate(&R->t1));
+        GPRX_HIP(hipEventCreate(&R->t2));
         const int nl = E.L.nloc(r);
         R->ld = (int64_t)nl * DB;
         R->A.ensure(sizeof(T) * R->ld * np);
@@ -575,8 +582,10 @@ void dist_fit(DistEngineBase*& eng, const DistContext& C, const DistFitIn<T>& in
     }
     // every rank's persistent launch back to back, nothing that could block in between
     for (size_t v = 0; v < E.ranks.size(); v++) {
+        GPRX_HIP(hipEventRecord(E.ranks[v]->t0, E.ranks[v]->s));
         potrf_tiles_dist_launch<T>(launches[v]);
         GPRX_HIP(hipEventRecord(E.ranks[v]->done, E.ranks[v]->s));
+        GPRX_HIP(hipEventRecord(E.ranks[v]->t1, E.ranks[v]->s));
     }
     // ---- issue loop: transport steps as their inputs become ready --------------------------
     const auto ts = std::chrono::steady_clock::now();
@@ -585,16 +594,21 @@ void dist_fit(DistEngineBase*& eng, const DistContext& C, const DistFitIn<T>& in
     double issue_s = 0;  // host time spent inside the transport calls (diagnostics)
     double dbg_next = 0.25;
     const double limit_s = 4.0 + 40.0 * E.est_us * 1e-6;
+    static const bool trace = std::getenv("GPRX_DIST_TRACE") != nullptr;
+    std::vector<double> tb_issue(trace ? nc : 0), tp_issue(trace ? nc : 0);
+    auto now_us = [&]() { return 1e6 * std::chrono::duration<double>(std::chrono::steady_clock::now() - ts).count(); };
     while (kb < nc || kp < nc) {
         bool progress = false;
         if (kb < nc && (flush || bcast_ready(E, kb))) {
             const auto t0 = std::chrono::steady_clock::now();
+            if (trace) tb_issue[kb] = now_us();
             issue_bcast(E, kb++);
             issue_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
             progress = true;
         }
         if (kp < nc && kp < kb + 1 && (flush || panel_ready(E, kp))) {
             const auto t0 = std::chrono::steady_clock::now();
+            if (trace) tp_issue[kp] = now_us();
             issue_panel(E, kp++);
             issue_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
             progress = true;
@@ -642,6 +656,15 @@ void dist_fit(DistEngineBase*& eng, const DistContext& C, const DistFitIn<T>& in
         else std::this_thread::yield();
     }
     for (auto& R : E.ranks) GPRX_HIP(hipStreamSynchronize(R->s));
+    if (trace) {  // host times of the transport issues (us from the launches)
+        const double tend = now_us();
+        std::fprintf(stderr, "gprx dist trace g %d P %d nc %d: end %.0f us, issue calls %.0f us\n", E.g, E.P, nc, tend,
+                     1e6 * issue_s);
+        for (int k = 0; k < nc; k++)
+            if (k < 8 || k % 16 == 0 || k >= nc - 4)
+                std::fprintf(stderr, "  k %4d bcast %9.1f panel %9.1f  (bcast step %7.1f)\n", k, tb_issue[k], tp_issue[k],
+                             k ? tb_issue[k] - tb_issue[k - 1] : tb_issue[k]);
+    }
     GPRX_HIP(hipStreamSynchronize(E.sB));
     GPRX_HIP(hipStreamSynchronize(E.sP));
     GPRX_HIP(hipGetLastError());
@@ -711,15 +734,23 @@ void dist_fit(DistEngineBase*& eng, const DistContext& C, const DistFitIn<T>& in
     out.flag = flag;
     out.est_us = E.est_us;
     out.P = E.P;
+    out.ms_kernel = 0;
+    for (auto& Rp : E.ranks) {  // the persistent launches' device time (the slowest rank)
+        float ms = 0;
+        if (hipEventElapsedTime(&ms, Rp->t0, Rp->t1) == hipSuccess) out.ms_kernel = std::max(out.ms_kernel, (double)ms);
+    }
     if (info < 0 || info != INT_MAX || flag) return;  // the caller reports it
     // alpha = L^{-T} z on rank 0 of this process (the factor is complete on every rank)
     GPRX_HIP(hipMemsetD32Async((hipDeviceptr_t)R0.info.p, INT_MAX, 1, R0.s));
     launch_backsolve_chain<T>(nullptr, 0, np, in.m, R0.Linv.template as<T>(), alpha_dev, R0.info.template as<int>(), ex,
                               R0.s, R0.tiles.template as<uint64_t>(), R0.tld.template as<int64_t>());
+    GPRX_HIP(hipEventRecord(R0.t2, R0.s));
     int hi = 0;
     GPRX_HIP(hipMemcpyAsync(&hi, R0.info.p, sizeof(int), hipMemcpyDeviceToHost, R0.s));
     GPRX_HIP(hipStreamSynchronize(R0.s));
     if (hi != INT_MAX) out.info = hi;
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, R0.t1, R0.t2) == hipSuccess) out.ms_solve = ms;
     (void)DB2;
 }
 

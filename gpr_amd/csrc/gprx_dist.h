@@ -29,6 +29,7 @@ struct DistFitIn {
 
 struct DistFitOut {
     double logdet = 0, datafit = 0, est_us = 0;
+    double ms_kernel = 0, ms_solve = 0;  // device time: persistent launch (slowest local rank), back-solve
     int info = 0, flag = 0, P = 0;
 };
 

@@ -173,6 +173,14 @@ def unique_id():
     return buf.raw
 
 
+def query_shard(q, rank, world):
+    """Rows [lo, hi) of Q queries that `rank` of `world` predicts (SURVEY.md 8(e) "Predict:
+    shard queries; replicate X, alpha"): contiguous, sizes differing by at most one."""
+    if world < 1 or not (0 <= rank < world) or q < 0:
+        raise ValueError("query_shard: need 0 <= rank < world and q >= 0")
+    return (q * rank) // world, (q * (rank + 1)) // world
+
+
 class Context:
     """One per process per GPU (gprx_ctx)."""
 
