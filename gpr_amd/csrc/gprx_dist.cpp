@@ -5,9 +5,10 @@
 // ComputeRegressionVectors, kernel matrix + lapack::lu_invert + C Y (lib/GaussianProcess.cpp
 // :118-130, 642-672; include/LAPACKUtils.h:38-56) -- for a matrix dealt over g ranks:
 //
-//   storage   row block i (128 rows) lives on rank i mod g: N^2/g of the lower factor per
-//             rank, plus the tiles of other ranks' rows it receives (each rank ends with the
-//             whole factor, in tiles, so the solve runs locally everywhere)
+//   storage   row block i (128 rows) lives on rank (i / gb) mod g (groups of gb blocks dealt
+//             cyclically; gb from the simulated makespan): N^2/g of the lower factor per rank,
+//             plus the tiles of other ranks' rows it receives (each rank ends with the whole
+//             factor, in tiles, so the solve runs locally everywhere)
 //   compute   each rank runs the persistent tile-dataflow launch (k_ptiles.hip,
 //             potrf_tiles_kernel<T, true>) over its own row blocks: covariance BUILD tasks,
 //             DIAGX (the diagonal 128-block chain), TRSM and UPD tasks, in the order of a list
@@ -34,6 +35,7 @@
 #include <chrono>
 #include <climits>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -112,28 +114,37 @@ struct HMem {  // coherent host memory the device stores to (kernel -> issue loo
 // layout: which rank holds which tile, where the send slots and received tiles live
 // ---------------------------------------------------------------------------------------
 struct DistLayout {
-    int g = 1, nc = 0, nr = 0;
-    int owner(int i) const { return i % g; }
-    int loc(int i) const { return i / g; }
-    int nloc(int q) const { return (nr - q + g - 1) / g; }
-    int first(int q, int b) const {  // first row block > b owned by q
-        int i = b + 1;
-        i += ((q - i % g) + g) % g;
-        return i;
+    // Row block i (128 rows; i = nc is the label block) lives on rank (i / gb) mod g: groups
+    // of gb consecutive blocks dealt cyclically.  gb > 1 keeps gb - 1 of every gb diagonal
+    // steps on one rank (the chain DIAGX(k) -> DIAGX(k + 1) then needs no broadcast hop).
+    int g = 1, gb = 1, nc = 0, nr = 0;
+    std::vector<int> own, lidx;          // per row block: owner rank, index in its rows
+    std::vector<std::vector<int>> rows;  // per rank: owned row blocks, ascending
+    int owner(int i) const { return own[i]; }
+    int loc(int i) const { return lidx[i]; }
+    int nloc(int q) const { return (int)rows[q].size(); }
+    int firstpos(int q, int b) const {  // index in rows[q] of the first row block > b
+        return (int)(std::upper_bound(rows[q].begin(), rows[q].end(), b) - rows[q].begin());
     }
-    int cnt(int q, int b) const {  // row blocks in (b, nr) owned by q
-        const int f = first(q, b);
-        return f >= nr ? 0 : (nr - 1 - f) / g + 1;
-    }
-    int pos(int q, int i, int b) const { return (i - first(q, b)) / g; }
+    int cnt(int q, int b) const { return nloc(q) - firstpos(q, b); }  // row blocks in (b, nr) on q
+    int pos(int q, int i, int b) const { return lidx[i] - firstpos(q, b); }
     // send slot offsets (tiles) of rank q: panel b after all earlier panels
     std::vector<std::vector<int64_t>> soff;             // [q][b]
     std::vector<std::vector<std::vector<int64_t>>> roff;  // [r][b][q]: rank r's received chunk from q
     std::vector<int64_t> stot, rtot;
-    void init(int g_, int nc_, int nr_) {
+    void init(int g_, int gb_, int nc_, int nr_) {
         g = g_;
+        gb = std::max(1, gb_);
         nc = nc_;
         nr = nr_;
+        own.assign(nr, 0);
+        lidx.assign(nr, 0);
+        rows.assign(g, std::vector<int>());
+        for (int i = 0; i < nr; i++) {
+            own[i] = (i / gb) % g;
+            lidx[i] = (int)rows[own[i]].size();
+            rows[own[i]].push_back(i);
+        }
         soff.assign(g, std::vector<int64_t>(nc + 1, 0));
         stot.assign(g, 0);
         for (int q = 0; q < g; q++) {
@@ -166,7 +177,7 @@ struct DistRank {
     int r = 0;
     hipStream_t s = nullptr;  // compute stream
     bool own_stream = false;
-    DMem A, Linv, send, recv, ctr, info, flag, pd, loc, tptr, sptr, drecv, tiles, tld, red, alpha, tab, list;
+    DMem A, Linv, send, recv, ctr, info, flag, pd, loc, tptr, sptr, drecv, tiles, tld, red, alpha, tab, list, trace;
     HMem hdiag, hslot, dbg;
     std::vector<int4> hlist;
     int64_t ld = 0;
@@ -234,7 +245,8 @@ __global__ __launch_bounds__(256) void dist_reduce_kernel(const T* __restrict__ 
     __shared__ double s0[256], s1[256];
     const int t = threadIdx.x;
     double a = 0, b = 0;
-    for (int k = r; k < nc; k += g) {  // this rank's diagonal blocks
+    for (int k = 0; k < nc; k++) {  // this rank's diagonal blocks
+        if (loc[k] < 0) continue;
         const int64_t gi = (int64_t)k * DB + (t & (DB - 1));
         if (t < DB && gi < n) a += 2.0 * log((double)A[(int64_t)loc[k] * DB + t + gi * ld]);
     }
@@ -279,7 +291,6 @@ static void setup(DistEngine<T>& E, const DistContext& C, int64_t n, int m, bool
     E.g = C.world;
     E.virt = C.virt;
     E.device = C.device;
-    E.L.init(E.g, nc, nr);
     // CU partition.  The transport kernels (RCCL, copies) and every (virtual) rank's
     // persistent launch run on streams whose CU masks are disjoint: a persistent launch can
     // never starve the transport of CUs, nor one virtual rank another.  Without the masks
@@ -291,7 +302,9 @@ static void setup(DistEngine<T>& E, const DistContext& C, int64_t n, int m, bool
     GPRX_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, C.device));
     if (hipDeviceGetAttribute(&nxcc, hipDeviceAttributeNumberOfXccs, C.device) != hipSuccess || nxcc < 1) nxcc = 1;
     const int cu_xcc = std::max(1, ncu / nxcc);
-    int reserve = 1;  // transport slots
+    // transport slots: one CU per XCC for the virtual ranks' copies; two for RCCL, whose
+    // kernels run one workgroup per channel
+    int reserve = E.virt ? 1 : 2;
     if (const char* e = std::getenv("GPRX_DIST_RESERVE_CU")) reserve = std::max(1, std::atoi(e));
     const int nloc_ranks = E.virt ? E.g : 1;
     GPRX_REQUIRE(cu_xcc - reserve >= nloc_ranks, GPRX_ERR_ARG, "distributed fit: too many virtual ranks for the CUs");
@@ -309,7 +322,24 @@ static void setup(DistEngine<T>& E, const DistContext& C, int64_t n, int m, bool
         GPRX_HIP(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()));
         return st;
     };
-    E.lists = potrf_dist_schedule(nc, nr, E.P, E.g, fused, &E.est_us);
+    // row-block grouping: the simulated makespan picks gb (GPRX_DIST_GROUP forces it)
+    int gb = 1;
+    if (const char* e = std::getenv("GPRX_DIST_GROUP")) {
+        gb = std::max(1, std::atoi(e));
+        E.lists = potrf_dist_schedule(nc, nr, E.P, E.g, gb, fused, &E.est_us);
+    } else {
+        E.lists = potrf_dist_schedule(nc, nr, E.P, E.g, 1, fused, &E.est_us);
+        for (int cand = 2; E.g > 1 && cand <= 8 && nc >= 2 * cand * E.g; cand *= 2) {
+            double est = 0;
+            auto l = potrf_dist_schedule(nc, nr, E.P, E.g, cand, fused, &est);
+            if (est < E.est_us) {
+                E.est_us = est;
+                E.lists = std::move(l);
+                gb = cand;
+            }
+        }
+    }
+    E.L.init(E.g, gb, nc, nr);
     if (!E.sB) {
         E.sB = masked_stream(0, reserve);
         E.sP = masked_stream(0, reserve);
@@ -474,8 +504,9 @@ template <typename T>
 static bool panel_ready(const DistEngine<T>& E, int b) {
     for (auto& R : E.ranks) {
         const unsigned* hs = R->hslot.u();
-        for (int i = E.L.first(R->r, b); i < E.L.nr; i += E.g)
-            if (__atomic_load_n(hs + (size_t)i * E.L.nc + b, __ATOMIC_ACQUIRE) == 0) return false;
+        const std::vector<int>& rw = E.L.rows[R->r];
+        for (int x = E.L.firstpos(R->r, b); x < (int)rw.size(); x++)
+            if (__atomic_load_n(hs + (size_t)rw[x] * E.L.nc + b, __ATOMIC_ACQUIRE) == 0) return false;
     }
     return true;
 }
@@ -522,7 +553,8 @@ void dist_fit(DistEngineBase*& eng, const DistContext& C, const DistFitIn<T>& in
         } else {
             // the direct build: each owned row block against the columns up to its diagonal
             GPRX_HIP(hipMemsetAsync(A, 0, sizeof(T) * R.ld * np, s));
-            for (int i = r; i < nc; i += E.g) {
+            for (int i : E.L.rows[r]) {
+                if (i >= nc) continue;
                 const int64_t r0 = (int64_t)i * DB, rows = std::min<int64_t>(DB, n - r0), cols = std::min<int64_t>(r0 + DB, n);
                 T* Ai = A + (int64_t)E.L.loc(i) * DB;
                 if (rows > 0) {
@@ -573,6 +605,13 @@ void dist_fit(DistEngineBase*& eng, const DistContext& C, const DistFitIn<T>& in
         Lc.P = E.P;
         Lc.s = s;
         Lc.dbg = nullptr;
+        Lc.trace = nullptr;
+        static const char* tdir = std::getenv("GPRX_DIST_TRACE_DEV");  // directory for per-rank task traces
+        if (tdir) {
+            R.trace.ensure(sizeof(long long) * 4 * ((size_t)R.ntasks + 2 * (size_t)nc));
+            GPRX_HIP(hipMemsetAsync(R.trace.p, 0, R.trace.bytes, s));
+            Lc.trace = R.trace.template as<long long>();
+        }
         static const bool dbgw = std::getenv("GPRX_DIST_DEBUG") != nullptr;
         if (dbgw) {
             R.dbg.ensure(sizeof(int) * 4 * E.P);
@@ -656,6 +695,20 @@ void dist_fit(DistEngineBase*& eng, const DistContext& C, const DistFitIn<T>& in
         else std::this_thread::yield();
     }
     for (auto& R : E.ranks) GPRX_HIP(hipStreamSynchronize(R->s));
+    if (const char* tdir = std::getenv("GPRX_DIST_TRACE_DEV")) {  // raw per-rank task traces
+        for (auto& Rp : E.ranks) {
+            std::vector<long long> tr(4 * ((size_t)Rp->ntasks + 2 * (size_t)nc));
+            GPRX_HIP(hipMemcpy(tr.data(), Rp->trace.p, sizeof(long long) * tr.size(), hipMemcpyDeviceToHost));
+            const std::string path = std::string(tdir) + "/rank" + std::to_string(Rp->r) + ".bin";
+            if (FILE* f = std::fopen(path.c_str(), "wb")) {
+                const int hdr[4] = {Rp->ntasks, nc, E.g, E.L.gb};
+                std::fwrite(hdr, sizeof(int), 4, f);
+                std::fwrite(Rp->hlist.data(), sizeof(int4), Rp->hlist.size(), f);
+                std::fwrite(tr.data(), sizeof(long long), tr.size(), f);
+                std::fclose(f);
+            }
+        }
+    }
     if (trace) {  // host times of the transport issues (us from the launches)
         const double tend = now_us();
         std::fprintf(stderr, "gprx dist trace g %d P %d nc %d: end %.0f us, issue calls %.0f us\n", E.g, E.P, nc, tend,
@@ -687,7 +740,7 @@ void dist_fit(DistEngineBase*& eng, const DistContext& C, const DistFitIn<T>& in
             std::fprintf(stderr,
                          "gprx dist rank %d/%d: P %d tickets %d/%d err %d | diag flags %d/%d (own) send slots %d/%d | "
                          "drecv %u precv %u | issued bcast %d panel %d of %d%s\n",
-                         R.r, E.g, E.P, ctl[0], R.ntasks, ctl[1], nd, (nc - R.r + E.g - 1) / E.g, ns, nsw, rc[0], rc[1],
+                         R.r, E.g, E.P, ctl[0], R.ntasks, ctl[1], nd, E.L.cnt(R.r, -1) - (E.L.owner(nc) == R.r), ns, nsw, rc[0], rc[1],
                          kb, kp, nc, flush ? " (flushed)" : "");
         }
     }

@@ -400,9 +400,10 @@ struct DistLaunch {
     int P;             // workgroups (one per CU)
     hipStream_t s;
     int* dbg;          // optional: per-workgroup {ticket, phase, i, j} in coherent host memory
+    long long* trace;  // optional: 4 * (ntasks + 2 nc) words, as GPRX_PT_TRACE (k_ptiles.hip)
 };
-// Per-rank ticket lists of the distributed factorisation (row block i on rank i mod g).
-std::vector<std::vector<int4>> potrf_dist_schedule(int nc, int nr, int P, int g, bool build, double* est_us);
+// Per-rank ticket lists of the distributed factorisation (row block i on rank (i / gb) mod g).
+std::vector<std::vector<int4>> potrf_dist_schedule(int nc, int nr, int P, int g, int gb, bool build, double* est_us);
 template <typename T>
 void potrf_tiles_dist_launch(const DistLaunch<T>& L);
 

@@ -402,9 +402,9 @@ struct Args {
 };
 
 
-// Every wave waits until the task's inputs are final (all lanes load the same words; the
-// values are made wave-uniform, so the loop is a scalar loop with no divergence).  Returns
-// false on timeout or when another workgroup raised the error flag.
+// Wave 0 waits until the task's inputs are final (all lanes load the same words; the values
+// are made wave-uniform, so the loop is a scalar loop with no divergence).  Returns false on
+// timeout or when another workgroup raised the error flag.
 __device__ __forceinline__ int ld_uni(const int* p) { return __builtin_amdgcn_readfirstlane(ld_agent(p)); }
 // counters written by the transport (stream memory ops into uncached memory): system scope
 __device__ __forceinline__ int ld_sys_uni(const unsigned* p) {
@@ -445,7 +445,7 @@ __device__ bool wait_inputs(const Args<T>& a, int type, int i, int j, int b0, in
         lp2 = lp1;
         lwant2 = lwant1;
         if constexpr (DIST) {
-            if ((i - 1) % a.dist->g != a.dist->r) {  // Linv_{i-1} is broadcast
+            if (__builtin_amdgcn_readfirstlane(a.dist->loc[i - 1]) < 0) {  // Linv_{i-1} is broadcast
                 lp1 = lp2 = a.lcnt + i;
                 lwant1 = lwant2 = 0;
                 rp = a.dist->drecv;
@@ -462,7 +462,7 @@ __device__ bool wait_inputs(const Args<T>& a, int type, int i, int j, int b0, in
         lp2 = lp1;
         lwant2 = lwant1;
         if constexpr (DIST) {
-            if (j % a.dist->g != a.dist->r) {  // Linv_j is broadcast
+            if (__builtin_amdgcn_readfirstlane(a.dist->loc[j]) < 0) {  // Linv_j is broadcast
                 lp1 = lp2 = a.lcnt + i;
                 lwant1 = lwant2 = 0;
                 rp = a.dist->drecv;
@@ -479,7 +479,7 @@ __device__ bool wait_inputs(const Args<T>& a, int type, int i, int j, int b0, in
         lp2 = a.lcnt + j;
         lwant2 = b0 + nb;
         if constexpr (DIST) {
-            if (j % a.dist->g != a.dist->r) {  // row j's tiles arrive with the panels
+            if (__builtin_amdgcn_readfirstlane(a.dist->loc[j]) < 0) {  // row j's tiles arrive with the panels
                 lp2 = lp1;
                 rp = a.dist->precv;
                 rwant = b0 + nb;
@@ -522,6 +522,7 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
     // ONE __shared__ array (a second __shared__ object can make hipcc drain the LDS-DMA
     // pipeline with vmcnt(0)); the ticket word sits after the largest per-task image
     int& s_q = *reinterpret_cast<int*>(smem_raw + pt_lds_bytes<T>());
+    int& s_ok = *reinterpret_cast<int*>(smem_raw + pt_lds_bytes<T>() + sizeof(int));
     T* smem = reinterpret_cast<T*>(smem_raw);
     const int t = threadIdx.x;
     const int wv = wave_id();
@@ -544,13 +545,20 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
         const int i = __builtin_amdgcn_readfirstlane(tk.y), j = __builtin_amdgcn_readfirstlane(tk.z),
                   b0 = __builtin_amdgcn_readfirstlane(tk.w);
         dbg_mark(a.dbg, q, 1 + 10 * type, i, j);
-        const bool ok = wait_inputs<T, DIST>(a, type, i, j, b0, nb);  // every wave, uniform
-        if (!ok) break;
-        if (wv == 0 && !(a.variant & 32)) {  // wave 0 acquires for the workgroup (invalidates this CU's L1)
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // wave 0 alone polls the task's counters (the other waves sleep in the barrier: eight
+        // times fewer loads on the counters -- hundreds of workgroups polling the transport's
+        // uncached words measured 10x slower distributed fits), then acquires for the
+        // workgroup (invalidates this CU's L1).  All of wave 0's lanes store the same word.
+        if (wv == 0) {
+            const bool ok0 = wait_inputs<T, DIST>(a, type, i, j, b0, nb);
+            if (ok0 && !(a.variant & 32)) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            s_ok = ok0 ? 1 : 0;
         }
         __syncthreads();
+        if (!__builtin_amdgcn_readfirstlane(s_ok)) break;
         const long long tr1 = a.trace ? wall_clock64() : 0;
         const long long tc1 = a.trace ? (long long)__builtin_amdgcn_s_memtime() : 0;
         dbg_mark(a.dbg, q, 2 + 10 * type, i, j);
@@ -859,7 +867,7 @@ static Schedule make_schedule(int nc, int nr, int W, int near, int P, const Cost
 }
 
 // ------------------------------------------------------------------------------------------
-// Distributed schedule: the same task DAG with row block i on rank i mod g, plus the two
+// Distributed schedule: the same task DAG with row block i on rank (i / gb) mod g, plus the two
 // transport steps of every panel as timed nodes that occupy no worker:
 //   bcast(k)  Linv_k from DIAGX(k)'s rank to all ranks (its consumers elsewhere: TRSM(., k),
 //             DIAGX(k + 1)); after bcast(k - 1) (one broadcast stream)
@@ -876,8 +884,8 @@ struct DistSchedule {
     double est_us = 0;
 };
 
-static DistSchedule make_schedule_dist(int nc, int nr, int W, int near, int P, int g, const Cost& cm, bool build,
-                                       double bcast_us, double tile_us) {
+static DistSchedule make_schedule_dist(int nc, int nr, int W, int near, int P, int g, int gb, const Cost& cm,
+                                       bool build, double bcast_us, double tile_us) {
     std::vector<Task> tasks;
     std::vector<int> rank_of;  // -1: transport node
     tasks.reserve((size_t)nr * nc * 2);
@@ -893,7 +901,7 @@ static DistSchedule make_schedule_dist(int nc, int nr, int W, int near, int P, i
         rank_of.push_back(rk);
         return (int)tasks.size() - 1;
     };
-    auto own = [&](int i) { return i % g; };
+    auto own = [&](int i) { return (i / gb) % g; };  // gprx_dist.cpp DistLayout
     std::vector<int> diagx(nc, -1), bcast(nc, -1), panel(nc, -1);
     std::vector<int> trsm((size_t)nr * nc, -1), last_upd((size_t)nr * nc, -1);
     std::vector<std::vector<int>> deps, edeps;
@@ -1268,12 +1276,13 @@ void potrf_tiles(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info
 }
 
 // ---- distributed factorisation: per-rank ticket lists and one rank's launch ------------------
-std::vector<std::vector<int4>> potrf_dist_schedule(int nc, int nr, int P, int g, bool build, double* est_us) {
+std::vector<std::vector<int4>> potrf_dist_schedule(int nc, int nr, int P, int g, int gb, bool build, double* est_us) {
     const pt::Params& pr = pt::params();
-    double bcast_us = 15.0, tile_us = 0.3;  // transport estimates: a broadcast's latency, one tile
+    double bcast_us = 30.0, tile_us = 0.5;  // transport estimates: a broadcast's latency, one tile
     if (const char* e = std::getenv("GPRX_DIST_BCAST_US")) bcast_us = std::atof(e);
     if (const char* e = std::getenv("GPRX_DIST_TILE_US")) tile_us = std::atof(e);
-    pt::DistSchedule S = pt::make_schedule_dist(nc, nr, pr.W, pr.near_for(nc), P, g, pr.cm, build, bcast_us, tile_us);
+    pt::DistSchedule S =
+        pt::make_schedule_dist(nc, nr, pr.W, pr.near_for(nc), P, g, std::max(1, gb), pr.cm, build, bcast_us, tile_us);
     if (est_us) *est_us = S.est_us;
     return S.lists;
 }
@@ -1297,6 +1306,7 @@ void potrf_tiles_dist_launch(const DistLaunch<T>& L) {
     a.tb = L.tb_dev;
     a.dist = L.dist_dev;
     a.dbg = L.dbg;
+    a.trace = L.trace;
     auto lds_of = [](size_t b) { return std::max<size_t>(b + 16, 96 * 1024); };
     const size_t lds = lds_of(pt_lds_bytes<T>());
     static bool attr = false;

@@ -52,6 +52,27 @@ def test_virtual_ranks_f64(g, ks, n, m):
         vctx.close()
 
 
+@pytest.mark.parametrize("g,gb", [(2, 3), (3, 2)])
+def test_virtual_ranks_grouped(g, gb, monkeypatch):
+    """Row blocks dealt in groups of gb consecutive blocks (GPRX_DIST_GROUP forces the group
+    size the simulated makespan otherwise picks): ownership, local storage, send slots and the
+    remote-input checks all follow the ownership table."""
+    import gpr_amd
+    monkeypatch.setenv("GPRX_DIST_GROUP", str(gb))
+    n, d, m, sigma = 1700, 4, 2, 0.5
+    X, Y = make_data(n, d, m)
+    vctx = gpr_amd.Context(0, virtual=g)
+    try:
+        M, info = _fit(vctx, C3K, X, Y, sigma, np.float64)
+        a_ref, _ = O.fit(C3K, X, Y, sigma, want_core=False)
+        assert relerr(M.alpha(), a_ref) <= 1e-6
+        K = O.kernel_matrix(C3K, X) + sigma * sigma * np.eye(n)
+        assert abs(info.logdet - np.linalg.slogdet(K)[1]) <= 1e-9 * max(1.0, abs(info.logdet))
+        M.close()
+    finally:
+        vctx.close()
+
+
 @pytest.mark.parametrize("g", [2, 4])
 def test_virtual_ranks_f32(g):
     import gpr_amd
