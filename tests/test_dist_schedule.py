@@ -1,6 +1,9 @@
-"""World-size-2 gloo test of the multi-GPU fit schedule (tests/dist_schedule.py restates
-potrf_dist / the sharded build): every rank ends with the full factor and the forward-solved
-label rows, identical to a single-process Cholesky."""
+"""World-size-2 gloo test of the storage-sharded multi-GPU fit and of the distributed LML
+gradient reduction (tests/dist_schedule.py restates gprx_dist.cpp / potrf_tiles_kernel<T,
+true> and model_lml on a distributed context): each rank stores only its row blocks, the
+diagonal inverses are broadcast and the panels exchanged, and every rank ends with alpha,
+log det and data fit equal to a single-process solve; the per-rank gradient partials
+all-reduce to the full gradient."""
 import os
 import socket
 
@@ -18,49 +21,74 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, n, NBO, out):
+def _gauss(X, sig, sc):
+    r2 = np.sum((X[:, None, :] - X[None, :, :]) ** 2, axis=-1)
+    e = np.exp(-0.5 * r2 / sig ** 2)
+    K = sc * sc * e
+    # d/d sigma, d/d scale (include/Kernel.h:471-479 order)
+    return K, [sc * sc * r2 / sig ** 3 * e, 2.0 * sc * e]
+
+
+def _worker(rank, world, port, n, B, gb, out):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import torch
-    from tests.dist_schedule import build_owned, potrf_dist
-    from oracle import oracle as O
+    from tests.dist_schedule import assemble_L, grad_partial, sharded_fit
     from gpr_amd.synth import make_data
-    ks = "SumKernel(GaussianKernel(2,0.15,),PeriodicKernel(0.1,3.141592653589793,1,))"
-    X, Y = make_data(n, 4, 2)
-    Kfull = O.kernel_matrix(ks, X)
-    np_ = -(-n // NBO) * NBO
-    ld = np_ + 128
-    A = build_owned(Kfull, Y, 0.5, n, np_, ld, NBO, rank, world)
+    X, Y = make_data(n, 3, 2)
+    K, dK = _gauss(X, 0.9, 1.1)
 
     def bcast(buf, root):
         t = torch.from_numpy(buf)
         dist.broadcast(t, src=root)
         buf[:] = t.numpy()
 
-    A = potrf_dist(A, np_, NBO, rank, world, bcast)
-    L = np.tril(A[:n, :n])
-    Z = A[np_:np_ + 2, :n]
-    np.save(out + f"_L{rank}.npy", L)
-    np.save(out + f"_Z{rank}.npy", Z)
+    def allgather_obj(obj):
+        res = [None] * world
+        dist.all_gather_object(res, obj)
+        return res
+
+    def allreduce_sum(a):
+        t = torch.from_numpy(np.array(a, dtype=np.float64, copy=True))  # all_reduce is in place
+        dist.all_reduce(t)
+        return t.numpy()
+
+    alpha, logdet, datafit, tiles, Linv, np_ = sharded_fit(K, Y, 0.5, n, B, rank, world, gb, bcast,
+                                                           allgather_obj, allreduce_sum)
+    L = assemble_L(tiles, Linv, np_ // B, B)
+    Wi = np.linalg.inv(L)
+    C = Wi.T @ Wi
+    part = grad_partial(alpha[:, :1], C, dK, n, B, rank, world, gb)
+    grad = 0.5 * allreduce_sum(part)
+    np.savez(out + f"_{rank}.npz", alpha=alpha, logdet=logdet, datafit=datafit, grad=grad, part=part)
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n,NBO", [(300, 64), (513, 128)])
-def test_panel_cyclic_factor_world2(tmp_path, n, NBO):
+@pytest.mark.parametrize("n,B,gb", [(300, 64, 1), (513, 64, 2), (400, 32, 3)])
+def test_sharded_fit_world2(tmp_path, n, B, gb):
     world = 2
     out = str(tmp_path / "res")
-    mp.spawn(_worker, args=(world, _free_port(), n, NBO, out), nprocs=world, join=True)
-    from oracle import oracle as O
+    mp.spawn(_worker, args=(world, _free_port(), n, B, gb, out), nprocs=world, join=True)
     from gpr_amd.synth import make_data
-    ks = "SumKernel(GaussianKernel(2,0.15,),PeriodicKernel(0.1,3.141592653589793,1,))"
-    X, Y = make_data(n, 4, 2)
-    K = O.kernel_matrix(ks, X) + 0.25 * np.eye(n)
-    Lref = np.linalg.cholesky(K)
-    Zref = np.linalg.solve(Lref, Y).T
+    X, Y = make_data(n, 3, 2)
+    K, dK = _gauss(X, 0.9, 1.1)
+    Kn = K + 0.25 * np.eye(n)
+    aref = np.linalg.solve(Kn, Y)
+    ldref = np.linalg.slogdet(Kn)[1]
+    dfref = float(np.sum(Y * aref))
+    C = np.linalg.inv(Kn)
+    a1 = aref[:, 0]
+    gref = np.array([0.5 * np.trace((np.outer(a1, a1) - C) @ D) for D in dK])
+    parts = []
     for r in range(world):
-        L = np.load(out + f"_L{r}.npy")
-        Z = np.load(out + f"_Z{r}.npy")
-        assert np.max(np.abs(L - Lref)) <= 1e-10 * np.max(np.abs(Lref))
-        assert np.max(np.abs(Z - Zref)) <= 1e-10 * np.max(np.abs(Zref))
+        z = np.load(out + f"_{r}.npz")
+        assert np.max(np.abs(z["alpha"] - aref)) <= 1e-10 * np.max(np.abs(aref))
+        assert abs(float(z["logdet"]) - ldref) <= 1e-10 * abs(ldref)
+        assert abs(float(z["datafit"]) - dfref) <= 1e-10 * abs(dfref)
+        assert np.max(np.abs(z["grad"] - gref)) <= 1e-9 * np.max(np.abs(gref))
+        parts.append(z["part"])
+    # each rank's partial covers only its row blocks: the two differ and sum to the gradient
+    assert np.max(np.abs(parts[0] - parts[1])) > 0
+    assert np.max(np.abs(0.5 * (parts[0] + parts[1]) - gref)) <= 1e-9 * np.max(np.abs(gref))
