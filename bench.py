@@ -173,6 +173,12 @@ def main():
             dmodel = make_model(dctx)
             el, infos, st = timed_fits(dmodel, dctx, gpr_amd.gprx.FIT_DISTRIBUTED)
             dres = {"elapsed": el, "infos": infos}
+            if args.lml:  # LML + gradient on the sharded factor (row-block partials, one all-reduce)
+                dmodel.lml(grad=True, distributed=True)
+                barrier_sync()
+                tl0 = time.perf_counter()
+                dmodel.lml(grad=True, distributed=True)
+                dres["lml_ms_wall"] = 1e3 * max_over_ranks(time.perf_counter() - tl0)
             dmodel.close()
             dctx.close()
         except Exception as e:  # reported; the replicas line stands in
@@ -298,6 +304,7 @@ def main():
             "phases": phases,
             "predict": pred,
             "lml_grad": lml,
+            "lml_grad_sharded_ms_wall": (dres or {}).get("lml_ms_wall"),
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -494,6 +494,9 @@ static void lu_solve_model(gprx_model* M, double* B, int m) {
 // launch per rank, RCCL broadcast of each diagonal inverse and full-mesh panel exchange
 // ---------------------------------------------------------------------------------------
 template <typename T>
+static void model_inverse(gprx_model* M);
+
+template <typename T>
 static gprx_status model_fit_dist(gprx_model* M, gprx_fit_info* out) {
     gprx_ctx* ctx = M->ctx;
     hipStream_t s = ctx->stream;
@@ -560,6 +563,17 @@ static gprx_status model_fit_dist(gprx_model* M, gprx_fit_info* out) {
                                           std::to_string(o.info) + " <= 0; no LU fallback on the distributed path)"};
     M->method = 0;
     M->fitted = M->has_alpha = M->dist_fitted = true;
+    if (M->want_inv) {
+        // the LML gradient: C = (K + s^2 I)^{-1} on this process from the dense factor every
+        // rank can assemble from its tiles (replicated potri); the gradient
+        // is then reduced over the ranks' row blocks (model_lml)
+        M->ld = np;
+        M->A.ensure(sizeof(T) * np * np);
+        M->Linv.ensure(sizeof(T) * np * DB);
+        dist_assemble_factor<T>(M->dist_engine, M->A.as<T>(), np, M->Linv.as<T>(), s);
+        model_inverse<T>(M);
+        M->inv_ready = true;
+    }
     return GPRX_OK;
 }
 
@@ -578,10 +592,7 @@ static gprx_status model_fit(gprx_model* M, uint32_t flags, gprx_fit_info* out) 
     // GPRX_FIT_DISTRIBUTED (the same code path on a one-rank communicator)
     GPRX_REQUIRE(!(flags & GPRX_FIT_DISTRIBUTED) || ctx->comm || ctx->virt, GPRX_ERR_STATE,
                  "gprx_model_fit: GPRX_FIT_DISTRIBUTED needs a context from gprx_ctx_create_dist");
-    if ((ctx->comm && ctx->world > 1) || ctx->virt || (flags & GPRX_FIT_DISTRIBUTED)) {
-        GPRX_REQUIRE(!M->want_inv, GPRX_ERR_STATE, "gprx: the log-likelihood gradient is not available on a distributed fit");
-        return model_fit_dist<T>(M, out);
-    }
+    if ((ctx->comm && ctx->world > 1) || ctx->virt || (flags & GPRX_FIT_DISTRIBUTED)) return model_fit_dist<T>(M, out);
     M->dist_fitted = false;
     const int64_t n = M->n, np = round_up(n, (int64_t)DB), mp = round_up(M->m, GT);
     // the explicit inverse rides along in the tile factorisation as np identity rows
@@ -896,7 +907,7 @@ static gprx_status model_lml(gprx_model* M, uint32_t flags, double* value, doubl
     try {
         // the likelihood inverts with the GP's method too (include/Likelihood.h:77-79 ->
         // ComputeCoreMatrixWithDeterminant): a matrix the Cholesky rejects takes the LU
-        st = model_fit<T>(M, GPRX_FIT_DEFAULT, &fi);
+        st = model_fit<T>(M, (flags & GPRX_LML_DISTRIBUTED) ? GPRX_FIT_DISTRIBUTED : GPRX_FIT_DEFAULT, &fi);
     } catch (...) {
         M->want_inv = false;
         throw;
@@ -960,9 +971,34 @@ static gprx_status model_lml(gprx_model* M, uint32_t flags, double* value, doubl
             M->scratch2.ensure(sizeof(T) * np * std::max<int64_t>(kg, 1));
             const int64_t nt = np / GT;
             M->pack.ensure(sizeof(double) * MAX_LEAF * 3 * nt * (nt + 1) / 2);
-            launch_lml_grad_mma<T>(K, M->kdev.as<KCanon<T>>(), M->X.as<T>(), M->n, M->d, M->featU.as<T>(),
-                                   M->featV.as<T>(), M->scratch1.as<T>(), M->scratch2.as<T>(), np, M->alpha.as<T>(),
-                                   M->C.as<T>(), M->np, M->pack.as<double>(), M->grad.as<double>(), s);
+            if (M->dist_fitted) {
+                // distributed context: each rank sums the tiles of its own row blocks and one
+                // all-reduce of the partials gives the gradient; virtual
+                // ranks (all in this process) add their partials here
+                int g = 1, gb = 1, r0 = 0;
+                bool virt = false;
+                dist_layout(M->dist_engine, &g, &gb, &r0, &virt);
+                double tot[MAX_LEAF * 3] = {0};
+                for (int r = virt ? 0 : r0; r < (virt ? g : r0 + 1); r++) {
+                    launch_lml_grad_mma<T>(K, M->kdev.as<KCanon<T>>(), M->X.as<T>(), M->n, M->d, M->featU.as<T>(),
+                                           M->featV.as<T>(), M->scratch1.as<T>(), M->scratch2.as<T>(), np,
+                                           M->alpha.as<T>(), M->C.as<T>(), M->np, M->pack.as<double>(),
+                                           M->grad.as<double>(), s, g, r, gb);
+                    if (!virt) {
+                        dist_allreduce_sum(M->dist_engine, M->grad.as<double>(), MAX_LEAF * 3, s);
+                        break;
+                    }
+                    double part[MAX_LEAF * 3];
+                    download(part, M->grad.p, sizeof(part), s);
+                    for (int q = 0; q < MAX_LEAF * 3; q++) tot[q] += part[q];
+                }
+                if (virt) upload<double>(M->grad, tot, sizeof(tot), s);
+            } else {
+                launch_lml_grad_mma<T>(K, M->kdev.as<KCanon<T>>(), M->X.as<T>(), M->n, M->d, M->featU.as<T>(),
+                                       M->featV.as<T>(), M->scratch1.as<T>(), M->scratch2.as<T>(), np,
+                                       M->alpha.as<T>(), M->C.as<T>(), M->np, M->pack.as<double>(),
+                                       M->grad.as<double>(), s);
+            }
         } else {
             launch_lml_grad<T>(K, M->X.as<T>(), M->tab.as<T>(), M->n, M->d, M->alpha.as<T>(), M->C.as<T>(), M->np,
                                M->grad.as<double>(), s);

@@ -809,6 +809,72 @@ void dist_fit(DistEngineBase*& eng, const DistContext& C, const DistFitIn<T>& in
 
 void dist_engine_free(DistEngineBase* e) { delete e; }
 
+namespace {
+template <typename T>
+__global__ __launch_bounds__(256) void assemble_tiles_kernel(const uint64_t* __restrict__ tiles,
+                                                             const int64_t* __restrict__ tld, int nc, T* __restrict__ A,
+                                                             int64_t ld) {
+    const int i = blockIdx.x, j = blockIdx.y;  // tile (i, j), i > j
+    if (j >= i) return;
+    const T* src = reinterpret_cast<const T*>(tiles[(int64_t)i * nc + j]);
+    const int64_t sl = tld[i];
+    T* dst = A + (int64_t)i * DB + (int64_t)j * DB * ld;
+    for (int e = threadIdx.x; e < DB * DB; e += 256) {
+        const int r = e & (DB - 1), c = e >> 7;
+        dst[r + (int64_t)c * ld] = src[r + (int64_t)c * sl];
+    }
+}
+}  // namespace
+
+template <typename T>
+void dist_assemble_factor(DistEngineBase* eng, T* A, int64_t ld, T* Linv, hipStream_t s) {
+    GPRX_REQUIRE(eng, GPRX_ERR_STATE, "distributed fit: no factor");
+    DistEngine<T>& E = *static_cast<DistEngine<T>*>(eng);
+    GPRX_REQUIRE(!E.ranks.empty(), GPRX_ERR_STATE, "distributed fit: no factor");
+    const DistRank<T>& R0 = *E.ranks[0];
+    const int nc = E.L.nc;
+    GPRX_HIP(hipMemsetAsync(A, 0, sizeof(T) * (size_t)ld * nc * DB, s));
+    if (nc > 1)
+        hipLaunchKernelGGL(assemble_tiles_kernel<T>, dim3((unsigned)nc, (unsigned)nc), dim3(256), 0, s,
+                           R0.tiles.template as<uint64_t>(), R0.tld.template as<int64_t>(), nc, A, ld);
+    GPRX_HIP(hipMemcpyAsync(Linv, R0.Linv.p, sizeof(T) * (size_t)nc * DB * DB, hipMemcpyDeviceToDevice, s));
+    GPRX_HIP(hipStreamSynchronize(s));
+}
+template void dist_assemble_factor<double>(DistEngineBase*, double*, int64_t, double*, hipStream_t);
+template void dist_assemble_factor<float>(DistEngineBase*, float*, int64_t, float*, hipStream_t);
+
+template <typename T>
+static bool layout_of(DistEngineBase* eng, int* g, int* gb, int* rank, bool* virt) {
+    auto* E = dynamic_cast<DistEngine<T>*>(eng);
+    if (!E || E->ranks.empty()) return false;
+    *g = E->g;
+    *gb = E->L.gb;
+    *rank = E->ranks[0]->r;
+    *virt = E->virt;
+    return true;
+}
+
+void dist_layout(DistEngineBase* eng, int* g, int* gb, int* rank, bool* virt) {
+    GPRX_REQUIRE(eng && (layout_of<double>(eng, g, gb, rank, virt) || layout_of<float>(eng, g, gb, rank, virt)),
+                 GPRX_ERR_STATE, "distributed fit: no layout");
+}
+
+template <typename T>
+static bool allreduce_of(DistEngineBase* eng, double* dev, int count, hipStream_t s) {
+    auto* E = dynamic_cast<DistEngine<T>*>(eng);
+    if (!E) return false;
+    if (!E->virt && E->g > 1) {
+        rccl_ok(ncclAllReduce(dev, dev, (size_t)count, ncclFloat64, ncclSum, E->commB, s), "ncclAllReduce");
+        GPRX_HIP(hipStreamSynchronize(s));
+    }
+    return true;
+}
+
+void dist_allreduce_sum(DistEngineBase* eng, double* dev, int count, hipStream_t s) {
+    GPRX_REQUIRE(eng && (allreduce_of<double>(eng, dev, count, s) || allreduce_of<float>(eng, dev, count, s)),
+                 GPRX_ERR_STATE, "distributed fit: no engine");
+}
+
 template void dist_fit<double>(DistEngineBase*&, const DistContext&, const DistFitIn<double>&, DistFitOut&, double*,
                                Exec&);
 template void dist_fit<float>(DistEngineBase*&, const DistContext&, const DistFitIn<float>&, DistFitOut&, float*, Exec&);

@@ -41,4 +41,16 @@ void dist_fit(DistEngineBase*& eng, const DistContext& C, const DistFitIn<T>& in
               Exec& ex);
 void dist_engine_free(DistEngineBase* e);
 
+// After a successful dist_fit: the dense factor on this process (every rank holds every
+// off-diagonal tile and every diagonal inverse): the strictly-lower blocks of L into A
+// (np x np, column-major, ld) and Linv (nc blocks of DB x DB), on `s` (synchronised).
+template <typename T>
+void dist_assemble_factor(DistEngineBase* eng, T* A, int64_t ld, T* Linv, hipStream_t s);
+// The layout of the last fit: ranks, row-block group size, this process's first rank, and
+// whether its ranks are virtual (all in this process).
+void dist_layout(DistEngineBase* eng, int* g, int* gb, int* rank, bool* virt);
+// In-place sum over the ranks of `count` doubles in device memory (RCCL; no-op for virtual
+// ranks and one-rank communicators).
+void dist_allreduce_sum(DistEngineBase* eng, double* dev, int count, hipStream_t s);
+
 }  // namespace gprx

@@ -417,7 +417,7 @@ int64_t pairs_grad_feature_cols(const KCanon<T>& K, int d);
 template <typename T>
 void launch_lml_grad_mma(const KCanon<T>& K, const KCanon<T>* Kd, const T* X, int64_t n, int d, const T* FU,
                          const T* FV, T* GU, T* GV, int64_t nf, const T* alpha, const T* C, int64_t ldc, double* part,
-                         double* acc, hipStream_t s);
+                         double* acc, hipStream_t s, int og = 1, int orank = 0, int ogb = 1);  // og > 1: rank orank's rows
 // The BUILD description of K(X, X) + sigma2 I from the features of launch_pair_features
 // (k_pairs.hip; the same trees as launch_kbuild_mma).
 template <typename T>

@@ -259,7 +259,8 @@ __global__ __launch_bounds__(NT) void grad_mma_kernel(const KCanon<T>* __restric
                                                       const T* __restrict__ FV, const T* __restrict__ GU,
                                                       const T* __restrict__ GV, int64_t nf, int Kr, int Kp, int Kf,
                                                       T hd, const T* __restrict__ alpha, const T* __restrict__ C,
-                                                      int64_t ldc, int64_t n, double* __restrict__ part) {
+                                                      int64_t ldc, int64_t n, double* __restrict__ part, int og,
+                                                      int orank, int ogb) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     T* smem = reinterpret_cast<T*>(smem_raw);
     double* sacc = reinterpret_cast<double*>(smem_raw + gemm_lds<T>());  // [8 waves][MAX_LEAF * 3]
@@ -272,6 +273,12 @@ __global__ __launch_bounds__(NT) void grad_mma_kernel(const KCanon<T>* __restric
         while (i * (i + 1) / 2 > b) i--;
         ti = i;
         tj = b - i * (i + 1) / 2;
+    }
+    // a distributed context's share: only the tiles of row blocks rank `orank` owns (row block
+    // i on rank (i / ogb) mod og, gprx_dist.cpp); the others contribute zero
+    if (og > 1 && (ti / ogb) % og != orank) {
+        if (threadIdx.x < MAX_LEAF * 3) part[(int64_t)blockIdx.x * MAX_LEAF * 3 + threadIdx.x] = 0.0;
+        return;
     }
     const int64_t i0 = ti * GT, j0 = tj * GT;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -561,7 +568,7 @@ int64_t pairs_grad_feature_cols(const KCanon<T>& K, int d) {
 template <typename T>
 void launch_lml_grad_mma(const KCanon<T>& K, const KCanon<T>* Kd, const T* X, int64_t n, int d, const T* FU,
                          const T* FV, T* GU, T* GV, int64_t nf, const T* alpha, const T* C, int64_t ldc, double* part,
-                         double* acc, hipStream_t s) {
+                         double* acc, hipStream_t s, int og, int orank, int ogb) {
     const int Kr = pr::kr_of(K, d), Kp = pr::kp_of(K, d), Kf = (int)pairs_grad_feature_cols(K, d);
     if (K.nper) {
         const dim3 g((unsigned)((nf + 255) / 256));
@@ -576,7 +583,7 @@ void launch_lml_grad_mma(const KCanon<T>& K, const KCanon<T>* Kd, const T* X, in
     auto go = [&](auto kfn) {
         GPRX_HIP(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         hipLaunchKernelGGL(kfn, grid, dim3(mm::NT), lds, s, Kd, FU, FV, (const T*)GU, (const T*)GV, nf, Kr, Kp, Kf,
-                           T(0.5) * T(d), alpha, C, ldc, n, part);
+                           T(0.5) * T(d), alpha, C, ldc, n, part, og, orank, ogb > 1 ? ogb : 1);
     };
     if (K.nper && K.need_r2) go(pr::grad_mma_kernel<T, 1, true>);
     else if (K.nper) go(pr::grad_mma_kernel<T, 1, false>);
@@ -615,7 +622,7 @@ TileBuild<T> pairs_tile_build(const KCanon<T>& K, const KCanon<T>* Kd, const T* 
     template int64_t pairs_grad_feature_cols<T>(const KCanon<T>&, int);                                       \
     template void launch_lml_grad_mma<T>(const KCanon<T>&, const KCanon<T>*, const T*, int64_t, int, const T*, \
                                          const T*, T*, T*, int64_t, const T*, const T*, int64_t, double*,     \
-                                         double*, hipStream_t);                                               \
+                                         double*, hipStream_t, int, int, int);                                \
     template TileBuild<T> pairs_tile_build<T>(const KCanon<T>&, const KCanon<T>*, const T*, const T*, int64_t, int, \
                                               int64_t, T, int*);                                              \
     template bool pairs_mma_supported<T>(const KCanon<T>&, int);                                              \

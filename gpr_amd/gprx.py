@@ -26,6 +26,7 @@ FIT_DISTRIBUTED = 2
 FIT_F32_NO_REFINE = 4
 LML_GRAD = 1
 LML_COMPAT = 2
+LML_DISTRIBUTED = 4
 
 STATUS = {0: "OK", 1: "NONFINITE", 2: "NOT_SPD", 3: "SINGULAR", 4: "DIM", 5: "HIP", 6: "RCCL", 7: "OOM",
           8: "ARG", 9: "STATE", 10: "NO_DEVICE"}
@@ -371,8 +372,8 @@ class Model:
         self._c(lib().gprx_model_core_matrix(self.h, _ptr(C)))
         return C
 
-    def lml(self, grad=True, compat=False):
-        flags = (LML_GRAD if grad else 0) | (LML_COMPAT if compat else 0)
+    def lml(self, grad=True, compat=False, distributed=False):
+        flags = (LML_GRAD if grad else 0) | (LML_COMPAT if compat else 0) | (LML_DISTRIBUTED if distributed else 0)
         v = ctypes.c_double()
         g = np.zeros(MAX_KPARAMS, np.float64)
         npar = ctypes.c_int32()

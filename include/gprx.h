@@ -160,9 +160,9 @@ gprx_status gprx_model_set_noise(gprx_model* model, double sigma);
                                       cyclically over the ranks (N^2/world of the factor per GPU),
                                       one persistent tile launch per rank, RCCL broadcast of each
                                       diagonal-block inverse and exchange of each factored panel.
-                                      Afterwards alpha, predict and the LML value are available;
-                                      the posterior covariance, core matrix and LML gradient need a
-                                      single-GPU fit */
+                                      Afterwards alpha and predict are available, and the LML
+                                      (value and gradient, GPRX_LML_DISTRIBUTED) runs on it; the
+                                      posterior covariance and core matrix need a single-GPU fit */
 #define GPRX_FIT_F32_NO_REFINE 4u  /* fp32 models: skip the fp64 iterative refinement of alpha.  By
                                       default an fp32 fit factorises in fp32 and refines alpha in
                                       fp64 until it agrees with the double solve: the reference
@@ -196,6 +196,11 @@ gprx_status gprx_model_core_matrix(gprx_model* model, void* C);
 #define GPRX_LML_GRAD 1u   /* also compute the hyper-parameter gradient */
 #define GPRX_LML_COMPAT 2u /* reproduce the reference's determinant narrowing + clamps
                               (include/Likelihood.h:77-79, 240-257); otherwise exact */
+#define GPRX_LML_DISTRIBUTED 4u /* refit with GPRX_FIT_DISTRIBUTED (implied on a multi-rank or
+                              virtual context): log det = sum of the ranks' diagonal blocks,
+                              C from the factor every rank assembles from its tiles (replicated
+                              potri), each rank's gradient partial over its own row blocks
+                              combined by one all-reduce of the P partials */
 /* GaussianLogLikelihood::operator() / GetValueAndParameterDerivatives
  * (include/Likelihood.h:166-285) for m = 1: value = -1/2 y^T C y - 1/2 log det - N/2 log 2pi,
  * grad_p = 1/2 tr((alpha alpha^T - C) dK/dp).  Refits from scratch like the reference.

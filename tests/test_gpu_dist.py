@@ -158,3 +158,52 @@ def test_virtual_ranks_not_spd_and_nonfinite():
         M.close()
     finally:
         vctx.close()
+
+
+PRODK = "ProductKernel(GaussianKernel(1.2,0.8,),RationalQuadraticKernel(1,0.7,2,))"
+
+
+@pytest.mark.parametrize("g", [1, 2, 3])
+@pytest.mark.parametrize("ks", [C3K, RQK, PRODK])
+def test_virtual_ranks_lml_grad(g, ks):
+    """LML value + gradient on a distributed context (row-block partials of the gradient
+    summed over the ranks; C from the factor assembled from the tiles) vs the oracle."""
+    import gpr_amd
+    n, d, sigma = 900, 3, 0.4
+    X, Y = make_data(n, d, 1)
+    vctx = gpr_amd.Context(0, virtual=g)
+    try:
+        M = gpr_amd.Model(vctx, np.float64)
+        M.set_data(X, Y)
+        M.set_kernel(ks)
+        M.set_noise(sigma)
+        v, grad, logdet = M.lml(grad=True)
+        vr, gr, _, ldr = O.lml(ks, X, Y, sigma)
+        assert abs(logdet - ldr) <= 1e-9 * abs(ldr)
+        assert relerr(grad, gr) <= 1e-6
+        vc, _, _ = M.lml(grad=False, compat=True)
+        assert abs(vc - vr) <= 1e-6 * max(1.0, abs(vr))
+        M.close()
+    finally:
+        vctx.close()
+
+
+def test_rccl_one_rank_lml_grad():
+    """The same on a one-rank RCCL communicator (GPRX_LML_DISTRIBUTED): the all-reduce of the
+    gradient partials runs through RCCL."""
+    import gpr_amd
+    n, d, sigma = 700, 4, 0.5
+    X, Y = make_data(n, d, 1)
+    dctx = gpr_amd.Context(0, dist=(0, 1, gpr_amd.unique_id()))
+    try:
+        M = gpr_amd.Model(dctx, np.float64)
+        M.set_data(X, Y)
+        M.set_kernel(C3K)
+        M.set_noise(sigma)
+        v, grad, logdet = M.lml(grad=True, distributed=True)
+        vr, gr, _, ldr = O.lml(C3K, X, Y, sigma)
+        assert abs(logdet - ldr) <= 1e-9 * abs(ldr)
+        assert relerr(grad, gr) <= 1e-6
+        M.close()
+    finally:
+        dctx.close()
