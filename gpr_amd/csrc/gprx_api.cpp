@@ -259,6 +259,10 @@ struct gprx_model {
     // the current fit is one (its factor is held in tiles per rank: alpha and predict only)
     DistEngineBase* dist_engine = nullptr;
     bool dist_fitted = false;
+    // a kernel with no device form: the caller evaluated K (n x n, row-major, T) -- the
+    // reference's virtual Kernel<T>::operator() (include/Kernel.h:52-59); see k_hostk.hip
+    bool host_k = false;
+    DevBuf Kext;
     std::mutex mu;
     ~gprx_model() { dist_engine_free(dist_engine); }
 };
@@ -414,6 +418,16 @@ static void lu_build_matrix(gprx_model* M) {
     const T sigma2 = sig * sig;  // in T, as the reference (lib/GaussianProcess.cpp:379)
     M->lu.ensure(sizeof(double) * np * np);
     GPRX_HIP(hipMemsetAsync(M->flag.p, 0, sizeof(int), s));
+    if (M->host_k) {  // the caller's K, widened to double like lu_invert<float> (LAPACKUtils.h:85-97)
+        if constexpr (std::is_same<T, double>::value) {
+            launch_kext_build<double>(M->Kext.as<double>(), n, M->lu.as<double>(), np, np, sigma2, M->flag.as<int>(), s);
+        } else {
+            M->A.ensure(sizeof(float) * np * np);
+            launch_kext_build<float>(M->Kext.as<float>(), n, M->A.as<float>(), np, np, sigma2, M->flag.as<int>(), s);
+            launch_convert<float, double>(M->A.as<float>(), M->lu.as<double>(), np * np, s);
+        }
+        return;
+    }
     if constexpr (std::is_same<T, double>::value) {
         launch_kbuild<double>(K, M->X.as<double>(), M->tab.as<double>(), n, M->X.as<double>(), M->tab.as<double>(), n,
                               M->d, M->lu.as<double>(), np, np, true, sigma2, M->flag.as<int>(), s);
@@ -499,6 +513,7 @@ static void model_inverse(gprx_model* M);
 template <typename T>
 static gprx_status model_fit_dist(gprx_model* M, gprx_fit_info* out) {
     gprx_ctx* ctx = M->ctx;
+    GPRX_REQUIRE(!M->host_k, GPRX_ERR_STATE, "gprx: a caller-evaluated kernel matrix needs a single-GPU fit");
     hipStream_t s = ctx->stream;
     const KCanon<T>& K = kcanon<T>(M);
     const int64_t n = M->n, np = round_up(n, DB);
@@ -625,7 +640,10 @@ static gprx_status model_fit(gprx_model* M, uint32_t flags, gprx_fit_info* out) 
         std::getenv("GPRX_KBUILD") && std::string(std::getenv("GPRX_KBUILD")) == "separate";
     TileBuild<T> tb;
     std::memset(&tb, 0, sizeof(tb));
-    if (!direct_build && pairs_mma_supported<T>(K, 1)) {
+    if (M->host_k) {  // the caller's K (k_hostk.hip)
+        launch_kext_build<T>(M->Kext.as<T>(), n, M->A.as<T>(), ld, np, sigma2, M->flag.as<int>(), s);
+        launch_aug_rows<T>(M->Y.as<T>(), n, M->m, M->A.as<T>(), ld, np, mp, s);
+    } else if (!direct_build && pairs_mma_supported<T>(K, 1)) {
         // pair statistics on the MFMA units from per-sample features (k_pairs.hip)
         const int64_t kf = pairs_feature_cols<T>(K, M->d);
         M->featU.ensure(sizeof(T) * np * kf);
@@ -710,7 +728,8 @@ static gprx_status model_fit(gprx_model* M, uint32_t flags, gprx_fit_info* out) 
         // the reference inverts fp32 GPs in double (include/LAPACKUtils.h:85-97): refine alpha
         // in fp64 against the fp32 factor.  Not for the LML's fit (its value and gradient come
         // from the factor and its inverse).
-        if (!(flags & GPRX_FIT_F32_NO_REFINE) && !want_inv) refine_f32(M, out);
+        // (a caller-evaluated kernel has no fp64 form to refine against)
+        if (!(flags & GPRX_FIT_F32_NO_REFINE) && !want_inv && !M->host_k) refine_f32(M, out);
     }
     return GPRX_OK;
 }
@@ -743,6 +762,7 @@ static void download(void* host, const void* dev, size_t bytes, hipStream_t s) {
 template <typename T>
 static gprx_status model_predict(gprx_model* M, const void* Xq, int64_t q, void* mean, void* deriv) {
     GPRX_REQUIRE(M->has_alpha, GPRX_ERR_STATE, "GaussianProcess::ComputeKernelVectorInternal: gaussian process is not initialized.");
+    GPRX_REQUIRE(!M->host_k, GPRX_ERR_STATE, "gprx: a caller-evaluated kernel predicts through gprx_model_predict_kx");
     hipStream_t s = M->ctx->stream;
     const KCanon<T>& K = kcanon<T>(M);
     const int d = M->d, m = M->m;
@@ -795,6 +815,7 @@ static gprx_status model_posterior_cov(gprx_model* M, const void* Xa, const void
     GPRX_REQUIRE(M->fitted, GPRX_ERR_STATE, "GaussianProcess::ComputeKernelVectorInternal: gaussian process is not initialized.");
     GPRX_REQUIRE(!M->dist_fitted, GPRX_ERR_STATE,
                  "gprx: the posterior covariance needs a single-GPU fit (a distributed fit keeps its factor in tiles)");
+    GPRX_REQUIRE(!M->host_k, GPRX_ERR_STATE, "gprx: a caller-evaluated kernel uses gprx_model_posterior_cov_kx");
     hipStream_t s = M->ctx->stream;
     const KCanon<T>& K = kcanon<T>(M);
     const int d = M->d;
@@ -901,6 +922,8 @@ static gprx_status model_lml(gprx_model* M, uint32_t flags, double* value, doubl
     GPRX_REQUIRE(M->m == 1, GPRX_ERR_DIM,
                  "GaussianLogLikelihood: only one output dimension is supported (the reference's data-fit term is "
                  "m x m, include/Likelihood.h:175)");
+    GPRX_REQUIRE(!(M->host_k && grad && (flags & GPRX_LML_GRAD)), GPRX_ERR_STATE,
+                 "gprx: a caller-evaluated kernel takes its derivative matrices through gprx_model_lml_dk");
     gprx_fit_info fi;
     M->want_inv = grad && (flags & GPRX_LML_GRAD);
     gprx_status st;
@@ -1011,6 +1034,101 @@ static gprx_status model_lml(gprx_model* M, uint32_t flags, double* value, doubl
             for (int q = 0; q < np; q++) grad[K.param_base[l] + q] = 0.5 * acc[l * 3 + q];
         }
     }
+    return GPRX_OK;
+}
+
+// ---------------------------------------------------------------------------------------
+// caller-evaluated kernels (k_hostk.hip): predict, posterior covariance and the LML gradient
+// from the caller's kernel vectors / derivative matrices
+// ---------------------------------------------------------------------------------------
+template <typename T>
+static gprx_status model_predict_kx(gprx_model* M, const void* Kx, const void* Xq, int64_t q, void* mean, void* deriv) {
+    GPRX_REQUIRE(M->has_alpha, GPRX_ERR_STATE, "GaussianProcess::ComputeKernelVectorInternal: gaussian process is not initialized.");
+    GPRX_REQUIRE(!deriv || Xq, GPRX_ERR_ARG, "gprx_model_predict_kx: the derivative needs the query points");
+    hipStream_t s = M->ctx->stream;
+    const int d = M->d, m = M->m;
+    const int64_t n = M->n;
+    DevBuf dk, dq, dmean, dder;
+    upload<T>(dk, Kx, sizeof(T) * q * n, s);
+    if (deriv) {
+        upload<T>(dq, Xq, sizeof(T) * q * d, s);
+        dder.ensure(sizeof(T) * q * d * m);
+    }
+    dmean.ensure(sizeof(T) * q * m);
+    launch_kx_predict<T>(dk.as<T>(), deriv ? dq.as<T>() : nullptr, M->X.as<T>(), q, n, d, M->alpha.as<T>(), m,
+                         dmean.as<T>(), deriv ? dder.as<T>() : nullptr, s);
+    download(mean, dmean.p, sizeof(T) * q * m, s);
+    if (deriv) download(deriv, dder.p, sizeof(T) * q * d * m, s);
+    return GPRX_OK;
+}
+
+template <typename T>
+static gprx_status model_posterior_cov_kx(gprx_model* M, const void* Kxa, const void* Kxb, const void* kab, int64_t q,
+                                          void* out) {
+    GPRX_REQUIRE(M->fitted, GPRX_ERR_STATE, "GaussianProcess::ComputeKernelVectorInternal: gaussian process is not initialized.");
+    GPRX_REQUIRE(!M->dist_fitted, GPRX_ERR_STATE, "gprx: the posterior covariance needs a single-GPU fit");
+    hipStream_t s = M->ctx->stream;
+    const int64_t n = M->n, np = M->np, qp = round_up(q, GT);
+    DevBuf dkab, res;
+    upload<T>(dkab, kab, sizeof(T) * q, s);
+    res.ensure(sizeof(T) * q);
+    const T* ka = reinterpret_cast<const T*>(Kxa);
+    const T* kb = reinterpret_cast<const T*>(Kxb);
+    if (M->method == 1) {  // LU: k(x,y) - K(X,x)^T A^{-1} K(X,y) (lib/GaussianProcess.cpp:84-99)
+        std::vector<double> ha((size_t)np * q, 0.0), hb((size_t)np * q, 0.0);  // np x q column-major
+        for (int64_t j = 0; j < q; j++)
+            for (int64_t i = 0; i < n; i++) {
+                ha[(size_t)j * np + i] = (double)ka[j * n + i];
+                hb[(size_t)j * np + i] = (double)kb[j * n + i];
+            }
+        DevBuf Wd, Kad;
+        upload<double>(Wd, hb.data(), sizeof(double) * np * q, s);
+        upload<double>(Kad, ha.data(), sizeof(double) * np * q, s);
+        lu_solve_model(M, Wd.as<double>(), (int)q);
+        lu_coldot<T>(Kad.as<double>(), Wd.as<double>(), np, n, q, dkab.as<T>(), res.as<T>(), s);
+    } else {  // Cholesky: k(x,y) - (L^{-1} kx) . (L^{-1} ky), rows qp x np (ld qp)
+        std::vector<T> ha((size_t)qp * np, T(0)), hb((size_t)qp * np, T(0));
+        for (int64_t j = 0; j < q; j++)
+            for (int64_t i = 0; i < n; i++) {
+                ha[(size_t)i * qp + j] = ka[j * n + i];
+                hb[(size_t)i * qp + j] = kb[j * n + i];
+            }
+        DevBuf Ra, Rb;
+        upload<T>(Ra, ha.data(), sizeof(T) * qp * np, s);
+        upload<T>(Rb, hb.data(), sizeof(T) * qp * np, s);
+        trsm_rows<T>(M->A.as<T>(), M->ld, np, M->Linv.as<T>(), Ra.as<T>(), qp, qp, s);
+        trsm_rows<T>(M->A.as<T>(), M->ld, np, M->Linv.as<T>(), Rb.as<T>(), qp, qp, s);
+        launch_rowdot<T>(Ra.as<T>(), Rb.as<T>(), qp, q, np, dkab.as<T>(), res.as<T>(), s);
+    }
+    download(out, res.p, sizeof(T) * q, s);
+    return GPRX_OK;
+}
+
+template <typename T>
+static gprx_status model_lml_dk(gprx_model* M, uint32_t flags, const void* dK, int32_t P, double* value, double* grad,
+                                double* logdet) {
+    GPRX_REQUIRE(P >= 0 && (P == 0 || dK), GPRX_ERR_ARG, "gprx_model_lml_dk: bad derivative matrices");
+    gprx_status st = model_lml<T>(M, flags & ~GPRX_LML_GRAD, value, nullptr, nullptr, logdet);
+    if (st != GPRX_OK || !grad || P == 0) return st;
+    hipStream_t s = M->ctx->stream;
+    const int64_t n = M->n, np = M->np;
+    if (M->method == 1) {  // C from the LU factors, in T (the reference casts back)
+        DevBuf luC;
+        lu_inverse(M, luC);
+        M->C.ensure(sizeof(T) * np * np);
+        if constexpr (std::is_same<T, double>::value)
+            GPRX_HIP(hipMemcpyAsync(M->C.p, luC.p, sizeof(double) * np * np, hipMemcpyDeviceToDevice, s));
+        else
+            launch_convert<double, T>(luC.as<double>(), M->C.as<T>(), np * np, s);
+        GPRX_HIP(hipStreamSynchronize(s));
+    } else {
+        model_inverse<T>(M);
+    }
+    DevBuf ddk, g;
+    upload<T>(ddk, dK, sizeof(T) * (size_t)P * n * n, s);
+    g.ensure(sizeof(double) * P);
+    launch_dk_grad<T>(ddk.as<T>(), P, n, M->alpha.as<T>(), M->C.as<T>(), np, g.as<double>(), s);
+    download(grad, g.p, sizeof(double) * P, s);
     return GPRX_OK;
 }
 
@@ -1515,6 +1633,7 @@ gprx_status gprx_model_set_kernel(gprx_model* M, const gprx_kernel_desc* k) {
     }
     M->desc = *k;
     M->has_kernel = true;
+    M->host_k = false;
     M->fitted = false;
     M->has_alpha = false;
     M->inv_ready = false;
@@ -1629,6 +1748,67 @@ gprx_status gprx_model_lml(gprx_model* M, uint32_t flags, double* value, double*
     GPRX_HIP(hipSetDevice(ctx->device));
     return M->dt == GPRX_F64 ? model_lml<double>(M, flags, value, grad, nparams, logdet)
                              : model_lml<float>(M, flags, value, grad, nparams, logdet);
+    API_END(ctx)
+}
+
+gprx_status gprx_model_set_kernel_matrix(gprx_model* M, const void* K) {
+    gprx_ctx* ctx = M ? M->ctx : nullptr;
+    API_BEGIN
+    GPRX_REQUIRE(M && K, GPRX_ERR_ARG, "gprx_model_set_kernel_matrix: NULL argument");
+    ModelLock lk(M);
+    GPRX_REQUIRE(M->has_data, GPRX_ERR_STATE, "gprx_model_set_kernel_matrix: set the data first");
+    GPRX_HIP(hipSetDevice(ctx->device));
+    const size_t es = esize(M->dt);
+    M->Kext.ensure(es * M->n * M->n);
+    GPRX_HIP(hipStreamSynchronize(ctx->stream));
+    GPRX_HIP(hipMemcpy(M->Kext.p, K, es * M->n * M->n, hipMemcpyHostToDevice));
+    std::memset(&M->kd, 0, sizeof(M->kd));  // no device form: nothing else reads the tree
+    std::memset(&M->kf, 0, sizeof(M->kf));
+    std::memset(&M->desc, 0, sizeof(M->desc));
+    M->host_k = true;
+    M->has_kernel = true;
+    M->fitted = false;
+    M->has_alpha = false;
+    M->inv_ready = false;
+    return GPRX_OK;
+    API_END(ctx)
+}
+
+gprx_status gprx_model_predict_kx(gprx_model* M, const void* Kx, const void* Xq, int64_t q, void* mean, void* deriv) {
+    gprx_ctx* ctx = M ? M->ctx : nullptr;
+    API_BEGIN
+    GPRX_REQUIRE(M && Kx && mean, GPRX_ERR_ARG, "gprx_model_predict_kx: NULL argument");
+    if (q == 0) return GPRX_OK;
+    ModelLock lk(M);
+    GPRX_HIP(hipSetDevice(ctx->device));
+    return M->dt == GPRX_F64 ? model_predict_kx<double>(M, Kx, Xq, q, mean, deriv)
+                             : model_predict_kx<float>(M, Kx, Xq, q, mean, deriv);
+    API_END(ctx)
+}
+
+gprx_status gprx_model_posterior_cov_kx(gprx_model* M, const void* Kxa, const void* Kxb, const void* kab, int64_t q,
+                                        void* out) {
+    gprx_ctx* ctx = M ? M->ctx : nullptr;
+    API_BEGIN
+    GPRX_REQUIRE(M && Kxa && Kxb && kab && out, GPRX_ERR_ARG, "gprx_model_posterior_cov_kx: NULL argument");
+    if (q == 0) return GPRX_OK;
+    ModelLock lk(M);
+    GPRX_HIP(hipSetDevice(ctx->device));
+    return M->dt == GPRX_F64 ? model_posterior_cov_kx<double>(M, Kxa, Kxb, kab, q, out)
+                             : model_posterior_cov_kx<float>(M, Kxa, Kxb, kab, q, out);
+    API_END(ctx)
+}
+
+gprx_status gprx_model_lml_dk(gprx_model* M, uint32_t flags, const void* dK, int32_t P, double* value, double* grad,
+                              double* logdet) {
+    gprx_ctx* ctx = M ? M->ctx : nullptr;
+    API_BEGIN
+    GPRX_REQUIRE(M, GPRX_ERR_ARG, "gprx_model_lml_dk: NULL model");
+    ModelLock lk(M);
+    ProfBind pb_(ctx);
+    GPRX_HIP(hipSetDevice(ctx->device));
+    return M->dt == GPRX_F64 ? model_lml_dk<double>(M, flags, dK, P, value, grad, logdet)
+                             : model_lml_dk<float>(M, flags, dK, P, value, grad, logdet);
     API_END(ctx)
 }
 

@@ -279,6 +279,15 @@ void launch_kbuild(const KCanon<T>& K, const T* Xa, const T* tabA, int64_t na, c
                    int64_t nb, int d, T* A, int64_t ld, int64_t npad, bool lower, T sigma2, int* flag,
                    hipStream_t s);
 
+// Kernels with no device form, evaluated by the caller (k_hostk.hip)
+template <typename T>
+void launch_kext_build(const T* Kx, int64_t n, T* A, int64_t ld, int64_t np, T sigma2, int* flag, hipStream_t s);
+template <typename T>
+void launch_kx_predict(const T* Kx, const T* Xq, const T* X, int64_t q, int64_t n, int d, const T* alpha, int m,
+                       T* mean, T* D, hipStream_t s);
+template <typename T>
+void launch_dk_grad(const T* dK, int P, int64_t n, const T* alpha, const T* C, int64_t ldc, double* out, hipStream_t s);
+
 // MFMA pair statistics (k_pairs.hip): kernels without White leaves and with at most one
 // periodic frequency build their covariance / predict their mean from per-sample feature
 // matrices (np rows x pairs_feature_cols columns, column-major) and 128x128 MFMA tiles.

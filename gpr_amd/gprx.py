@@ -40,6 +40,7 @@ EXPORTED = [
     "gprx_model_predict", "gprx_model_posterior_cov", "gprx_model_core_matrix", "gprx_model_lml",
     "gprx_kernel_matrix", "gprx_cross_matrix", "gprx_deriv_matrix", "gprx_cholesky", "gprx_spd_inverse",
     "gprx_sparse_fit", "gprx_ctx_set_stats", "gprx_ctx_get_stats",
+    "gprx_model_set_kernel_matrix", "gprx_model_predict_kx", "gprx_model_posterior_cov_kx", "gprx_model_lml_dk",
 ]
 
 
@@ -102,6 +103,14 @@ def lib():
         L.gprx_model_core_matrix.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         L.gprx_model_lml.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_double),
                                      ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_double)]
+        L.gprx_model_set_kernel_matrix.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        L.gprx_model_predict_kx.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                            ctypes.c_void_p, ctypes.c_void_p]
+        L.gprx_model_posterior_cov_kx.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                  ctypes.c_int64, ctypes.c_void_p]
+        L.gprx_model_lml_dk.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_int32,
+                                        ctypes.POINTER(ctypes.c_double), ctypes.c_void_p,
+                                        ctypes.POINTER(ctypes.c_double)]
         for f in ("gprx_kernel_matrix", "gprx_deriv_matrix"):
             getattr(L, f).argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(KernelDesc), ctypes.c_void_p,
                                       ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p]
@@ -302,6 +311,7 @@ class Model:
         self.h = h
         self.n = self.d = self.m = 0
         self.kernel = None
+        self._Xh = None
 
     def close(self):
         if self.h:
@@ -325,10 +335,30 @@ class Model:
         n, d = X.shape
         self._c(lib().gprx_model_set_data(self.h, _ptr(X), _ptr(Y), n, d, Y.shape[1]))
         self.n, self.d, self.m = n, d, Y.shape[1]
+        self._Xh = X  # host copy: a kernel with no device form is evaluated against it
+        if self._host_kernel():
+            self._set_host_kernel()
 
     def set_kernel(self, kernel):
+        """A kernel string / node (evaluated on the device), or an object with no device form:
+        callable k(Xa, Xb) -> na x nb matrix, optionally with .gradient(Xa, Xb) -> P x na x nb
+        (the reference's virtual Kernel::operator() / GetDerivative, include/Kernel.h:52-59).
+        The latter is evaluated here on the host; the factorisation and solves stay on the
+        device (gprx_model_set_kernel_matrix and the *_kx entry points)."""
+        if callable(kernel) and not isinstance(kernel, str) and not hasattr(kernel, "op"):
+            self.kernel = kernel
+            if self._Xh is not None:  # else set_data evaluates it
+                self._set_host_kernel()
+            return
         self.kernel = as_node(kernel)
         self._c(lib().gprx_model_set_kernel(self.h, ctypes.byref(kernel_desc(self.kernel))))
+
+    def _host_kernel(self):
+        return self.kernel is not None and callable(self.kernel) and not hasattr(self.kernel, "op")
+
+    def _set_host_kernel(self):
+        K = np.ascontiguousarray(self.kernel(self._Xh, self._Xh), self.dtype)
+        self._c(lib().gprx_model_set_kernel_matrix(self.h, _ptr(K)))
 
     def set_noise(self, sigma):
         self._c(lib().gprx_model_set_noise(self.h, float(sigma)))
@@ -352,14 +382,25 @@ class Model:
         q = Xq.shape[0]
         mean = np.empty((q, self.m), self.dtype)
         D = np.empty((q, self.d, self.m), self.dtype) if deriv else None
-        self._c(lib().gprx_model_predict(self.h, _ptr(Xq), q, _ptr(mean), _ptr(D)))
+        if self._host_kernel():
+            Kx = np.ascontiguousarray(self.kernel(Xq, self._Xh), self.dtype)
+            self._c(lib().gprx_model_predict_kx(self.h, _ptr(Kx), _ptr(Xq), q, _ptr(mean), _ptr(D)))
+        else:
+            self._c(lib().gprx_model_predict(self.h, _ptr(Xq), q, _ptr(mean), _ptr(D)))
         return (mean, D) if deriv else mean
 
     def posterior_cov(self, Xa, Xb):
         Xa = np.ascontiguousarray(Xa, self.dtype)
         Xb = np.ascontiguousarray(Xb, self.dtype)
         out = np.empty(Xa.shape[0], self.dtype)
-        self._c(lib().gprx_model_posterior_cov(self.h, _ptr(Xa), _ptr(Xb), Xa.shape[0], _ptr(out)))
+        if self._host_kernel():
+            Ka = np.ascontiguousarray(self.kernel(Xa, self._Xh), self.dtype)
+            Kb = np.ascontiguousarray(self.kernel(Xb, self._Xh), self.dtype)
+            kab = np.ascontiguousarray([self.kernel(Xa[i:i + 1], Xb[i:i + 1])[0, 0] for i in range(Xa.shape[0])],
+                                       self.dtype)
+            self._c(lib().gprx_model_posterior_cov_kx(self.h, _ptr(Ka), _ptr(Kb), _ptr(kab), Xa.shape[0], _ptr(out)))
+        else:
+            self._c(lib().gprx_model_posterior_cov(self.h, _ptr(Xa), _ptr(Xb), Xa.shape[0], _ptr(out)))
         return out
 
     def credible_interval(self, Xq):
@@ -374,6 +415,14 @@ class Model:
 
     def lml(self, grad=True, compat=False, distributed=False):
         flags = (LML_GRAD if grad else 0) | (LML_COMPAT if compat else 0) | (LML_DISTRIBUTED if distributed else 0)
+        if self._host_kernel():
+            dK = np.ascontiguousarray(self.kernel.gradient(self._Xh, self._Xh), self.dtype) if grad else None
+            P = dK.shape[0] if grad else 0
+            v, ld = ctypes.c_double(), ctypes.c_double()
+            g = np.zeros(max(P, 1), np.float64)
+            self._c(lib().gprx_model_lml_dk(self.h, flags & ~LML_GRAD, _ptr(dK), P, ctypes.byref(v),
+                                            _ptr(g) if grad else None, ctypes.byref(ld)))
+            return v.value, (g[:P].copy() if grad else None), ld.value
         v = ctypes.c_double()
         g = np.zeros(MAX_KPARAMS, np.float64)
         npar = ctypes.c_int32()

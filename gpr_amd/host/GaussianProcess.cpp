@@ -15,6 +15,7 @@
 #include <limits>
 #include <sstream>
 #include <sys/stat.h>
+#include <thread>
 
 #include "../../include/gpr/MatrixIO.h"
 
@@ -102,7 +103,35 @@ void GaussianProcess<T>::UploadState() {
     }
     ThrowIfFailed(gprx_model_set_data(Model(), X.data(), Y.data(), (int64_t)n, (int32_t)d, (int32_t)m), ctx);
     std::vector<gprx_knode> prog;
-    m_Kernel->Describe(prog);
+    try {
+        m_Kernel->Describe(prog);
+        m_HostKernel = false;
+    } catch (const std::string&) {
+        // no device form: K through the virtual operator() (lib/GaussianProcess.cpp:384-402),
+        // the upper triangle mirrored, evaluated over the rows by the host's threads
+        m_HostKernel = true;
+        std::vector<T> K(n * n);
+        const unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+        std::vector<std::thread> th;
+        std::exception_ptr err = nullptr;
+        std::mutex emu;
+        for (unsigned w = 0; w < nt; w++)
+            th.emplace_back([&, w]() {
+                try {
+                    for (std::size_t i = w; i < n; i += nt)
+                        for (std::size_t j = 0; j <= i; j++)
+                            K[i * n + j] = K[j * n + i] = (*m_Kernel)(m_SampleVectors[i], m_SampleVectors[j]);
+                } catch (...) {
+                    std::lock_guard<std::mutex> l(emu);
+                    if (!err) err = std::current_exception();
+                }
+            });
+        for (auto& t : th) t.join();
+        if (err) std::rethrow_exception(err);
+        ThrowIfFailed(gprx_model_set_kernel_matrix(m_Model, K.data()), ctx);
+        ThrowIfFailed(gprx_model_set_noise(m_Model, (double)m_Sigma), ctx);
+        return;
+    }
     if (prog.size() > GPRX_MAX_KNODES) throw std::string("GaussianProcess: kernel has too many nodes for the device");
     gprx_kernel_desc desc{};
     desc.n_nodes = (int32_t)prog.size();
@@ -129,6 +158,33 @@ void GaussianProcess<T>::EnsureFactor() {  // m_DevMu held
     FitDevice();
     if (m_Initialized && m_RegressionVectors.rows() == m_SampleVectors.size())
         ThrowIfFailed(gprx_model_set_alpha(m_Model, m_RegressionVectors.data()), DefaultContext());
+}
+
+template <class T>
+std::vector<T> GaussianProcess<T>::HostKernelRows(const T* Xq, std::size_t q) const {
+    const std::size_t n = m_SampleVectors.size(), d = m_InputDimension;
+    std::vector<T> R(q * n);
+    VectorType x(d);
+    for (std::size_t a = 0; a < q; a++) {
+        for (std::size_t k = 0; k < d; k++) x[k] = Xq[a * d + k];
+        for (std::size_t i = 0; i < n; i++) R[a * n + i] = (*m_Kernel)(x, m_SampleVectors[i]);
+    }
+    return R;
+}
+
+// dK/dp for every parameter p (GetDerivative order), P x n x n
+template <class T>
+std::vector<T> GaussianProcess<T>::HostDerivativeMatrices(int32_t& P) const {
+    const std::size_t n = m_SampleVectors.size();
+    P = (int32_t)m_Kernel->GetNumberOfParameters();
+    std::vector<T> D((std::size_t)P * n * n);
+    for (std::size_t i = 0; i < n; i++)
+        for (std::size_t j = 0; j <= i; j++) {
+            const VectorType g = m_Kernel->GetDerivative(m_SampleVectors[i], m_SampleVectors[j]);
+            if ((int32_t)g.size() != P) throw std::string("GaussianProcess: kernel derivative has the wrong size");
+            for (int32_t p = 0; p < P; p++) D[(std::size_t)p * n * n + i * n + j] = D[(std::size_t)p * n * n + j * n + i] = g[p];
+        }
+    return D;
 }
 
 // lib/GaussianProcess.cpp:118-130, 642-672
@@ -172,6 +228,11 @@ typename GaussianProcess<T>::VectorType GaussianProcess<T>::Predict(const Vector
     CheckInputDimension(x, "GaussianProcess::Predict: ");
     VectorType mean(m_OutputDimension);
     std::lock_guard<std::mutex> lk(m_DevMu);  // not inside another thread's lazy refit
+    if (m_HostKernel) {
+        const std::vector<T> kx = HostKernelRows(x.data(), 1);
+        ThrowIfFailed(gprx_model_predict_kx(m_Model, kx.data(), x.data(), 1, mean.data(), nullptr), DefaultContext());
+        return mean;
+    }
     ThrowIfFailed(gprx_model_predict(m_Model, x.data(), 1, mean.data(), nullptr), DefaultContext());
     return mean;
 }
@@ -182,6 +243,12 @@ typename GaussianProcess<T>::MatrixType GaussianProcess<T>::PredictBatch(const M
     if (Xq.cols() != m_InputDimension) throw std::string("GaussianProcess::PredictBatch: dimension mismatch");
     MatrixType out(Xq.rows(), m_OutputDimension);
     std::lock_guard<std::mutex> lk(m_DevMu);
+    if (m_HostKernel) {
+        const std::vector<T> kx = HostKernelRows(Xq.data(), Xq.rows());
+        ThrowIfFailed(gprx_model_predict_kx(m_Model, kx.data(), Xq.data(), (int64_t)Xq.rows(), out.data(), nullptr),
+                      DefaultContext());
+        return out;
+    }
     ThrowIfFailed(gprx_model_predict(m_Model, Xq.data(), (int64_t)Xq.rows(), out.data(), nullptr), DefaultContext());
     return out;
 }
@@ -194,6 +261,11 @@ typename GaussianProcess<T>::VectorType GaussianProcess<T>::PredictDerivative(co
     VectorType mean(m_OutputDimension);
     D.resize(m_InputDimension, m_OutputDimension);
     std::lock_guard<std::mutex> lk(m_DevMu);
+    if (m_HostKernel) {
+        const std::vector<T> kx = HostKernelRows(x.data(), 1);
+        ThrowIfFailed(gprx_model_predict_kx(m_Model, kx.data(), x.data(), 1, mean.data(), D.data()), DefaultContext());
+        return mean;
+    }
     ThrowIfFailed(gprx_model_predict(m_Model, x.data(), 1, mean.data(), D.data()), DefaultContext());
     return mean;
 }
@@ -208,6 +280,12 @@ T GaussianProcess<T>::operator()(const VectorType& x, const VectorType& y) {
     EnsureFactor();
     m_CoreSize = m_SampleVectors.size();  // :95-97 builds the core matrix on demand
     T out = 0;
+    if (m_HostKernel) {
+        const std::vector<T> ka = HostKernelRows(x.data(), 1), kb = HostKernelRows(y.data(), 1);
+        const T kab = (*m_Kernel)(x, y);
+        ThrowIfFailed(gprx_model_posterior_cov_kx(m_Model, ka.data(), kb.data(), &kab, 1, &out), DefaultContext());
+        return out;
+    }
     ThrowIfFailed(gprx_model_posterior_cov(m_Model, x.data(), y.data(), 1, &out), DefaultContext());
     return out;
 }
@@ -229,8 +307,16 @@ std::vector<T> GaussianProcess<T>::CredibleIntervalBatch(const MatrixType& Xq) {
     std::lock_guard<std::mutex> lk(m_DevMu);
     EnsureFactor();
     std::vector<T> c(Xq.rows());
-    ThrowIfFailed(gprx_model_posterior_cov(m_Model, Xq.data(), Xq.data(), (int64_t)Xq.rows(), c.data()),
-                  DefaultContext());
+    if (m_HostKernel) {
+        const std::vector<T> kx = HostKernelRows(Xq.data(), Xq.rows());
+        std::vector<T> kk(Xq.rows());
+        for (std::size_t a = 0; a < Xq.rows(); a++) kk[a] = (*m_Kernel)(Xq.row(a), Xq.row(a));
+        ThrowIfFailed(gprx_model_posterior_cov_kx(m_Model, kx.data(), kx.data(), kk.data(), (int64_t)Xq.rows(), c.data()),
+                      DefaultContext());
+    } else {
+        ThrowIfFailed(gprx_model_posterior_cov(m_Model, Xq.data(), Xq.data(), (int64_t)Xq.rows(), c.data()),
+                      DefaultContext());
+    }
     for (auto& v : c) v = 2 * std::sqrt(std::max(static_cast<T>(0.0), v));
     return c;
 }

@@ -8,6 +8,12 @@
 // resident in HBM; the host keeps the sample lists (for Save / ==) and a copy of the
 // regression vectors (m_RegressionVectors, as the reference).
 //
+// Kernels with no device form (a user Kernel<T> subclass that does not override Describe):
+// K, the query kernel vectors and the derivative matrices are evaluated on the host through
+// the virtual operator() / GetDerivative, as the reference does for every kernel; the
+// factorisation, solves and reductions still run on the device (gprx_model_set_kernel_matrix
+// and the *_kx entry points of include/gprx.h).
+//
 // Differences (documented in DESIGN.md): the core matrix C = (K + sigma^2 I)^{-1} is
 // materialised lazily from the device factor (Save, GetCoreMatrix), not at every
 // Initialize; operator()/GetCredibleInterval use the factor (k - |L^{-1}k|^2) instead of
@@ -125,6 +131,9 @@ protected:
     gprx_model* m_Model = nullptr;
     std::mutex m_DevMu;           // guards the lazy refit (EnsureFactor), m_CoreMatrix/m_CoreSize
     bool m_DeviceFactor = false;  // device holds the Cholesky factor of the current state
+    bool m_HostKernel = false;    // the kernel has no device form (Describe throws): K and the
+                                  // kernel vectors are evaluated here through the virtual
+                                  // operator() (include/Kernel.h:52-59), the rest on the device
     bool m_CoreValid = false;     // m_CoreMatrix holds the materialised core matrix
     std::size_t m_CoreSize = 0;   // the reference's m_CoreMatrix.diagonalSize(): n once the
                                   // core exists (Initialize w/o efficient storage, operator(),
@@ -137,6 +146,9 @@ protected:
     void FitDevice(gprx_fit_info* info = nullptr);
     void EnsureFactor();           // factor for operator()/core; keeps the regression vectors
                                    // (caller holds m_DevMu)
+    // host-evaluated kernel rows K(x, X) of q queries (rows of Xq, or one vector), row-major
+    std::vector<TScalarType> HostKernelRows(const TScalarType* Xq, std::size_t q) const;
+    std::vector<TScalarType> HostDerivativeMatrices(int32_t& P) const;  // P x n x n
 
     friend class Likelihood<TScalarType>;
 };

@@ -62,8 +62,17 @@ protected:
         int32_t np = 0;
         e.grad.resize(GPRX_MAX_KNODES * 3);
         uint32_t flags = (compat ? GPRX_LML_COMPAT : 0u) | (grad ? GPRX_LML_GRAD : 0u);
-        ThrowIfFailed(gprx_model_lml(gp->m_Model, flags, &e.value, grad ? e.grad.data() : nullptr, &np, &e.logdet),
-                      DefaultContext());
+        if (gp->m_HostKernel) {  // no device form: the derivative matrices through GetDerivative
+            std::vector<TScalarType> dK;
+            if (grad) dK = gp->HostDerivativeMatrices(np);
+            if ((int32_t)e.grad.size() < np) e.grad.resize(np);
+            ThrowIfFailed(gprx_model_lml_dk(gp->m_Model, flags & ~GPRX_LML_GRAD, grad ? dK.data() : nullptr,
+                                            grad ? np : 0, &e.value, grad ? e.grad.data() : nullptr, &e.logdet),
+                          DefaultContext());
+        } else {
+            ThrowIfFailed(gprx_model_lml(gp->m_Model, flags, &e.value, grad ? e.grad.data() : nullptr, &np, &e.logdet),
+                          DefaultContext());
+        }
         gp->m_DeviceFactor = true;
         gp->m_CoreValid = false;
         // the likelihood does not change the gp's regression vectors (the reference only

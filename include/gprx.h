@@ -208,6 +208,28 @@ gprx_status gprx_model_core_matrix(gprx_model* model, void* C);
 gprx_status gprx_model_lml(gprx_model* model, uint32_t flags, double* value, double* grad, int32_t* nparams,
                            double* logdet);
 
+/* ---- kernels with no device form ----------------------------------------------------
+ * The reference dispatches every pair through the virtual Kernel<T>::operator() /
+ * GetDerivative (include/Kernel.h:52-59), so a user subclass works with the GP unchanged.
+ * A kernel that cannot be lowered to gprx_kernel_desc is evaluated by the CALLER and handed
+ * over as matrices (row-major, model dtype); the factorisation, solves, inverse and
+ * reductions stay on the device.  gpr::GaussianProcess does this automatically for kernels
+ * whose Describe() throws. */
+/* K(X, X) (n x n, without the noise) in place of gprx_model_set_kernel; set the data first. */
+gprx_status gprx_model_set_kernel_matrix(gprx_model* model, const void* K);
+/* Predict / PredictDerivative from Kx = K(Xq, X) (q x n): mean q x m; deriv (optional,
+ * needs Xq, q x d) q x d x m with the reference's D(:,c) = -Xd^T (Kx o alpha_c). */
+gprx_status gprx_model_predict_kx(gprx_model* model, const void* Kx, const void* Xq, int64_t q, void* mean,
+                                  void* deriv);
+/* operator()(a_j, b_j) = kab_j - Kxa_j^T C Kxb_j for q pairs, Kxa = K(Xa, X), Kxb = K(Xb, X)
+ * (q x n), kab = k(a_j, b_j) (q). */
+gprx_status gprx_model_posterior_cov_kx(gprx_model* model, const void* Kxa, const void* Kxb, const void* kab,
+                                        int64_t q, void* out);
+/* gprx_model_lml with the gradient from the caller's derivative matrices dK (P x n x n,
+ * dK_p = d K / d p_p, the reference's GetDerivative order). */
+gprx_status gprx_model_lml_dk(gprx_model* model, uint32_t flags, const void* dK, int32_t P, double* value,
+                              double* grad, double* logdet);
+
 /* ---- building blocks (host buffers; used by parity tests) --------------------------- */
 /* ComputeKernelMatrixInternal (lib/GaussianProcess.cpp:384-402): K = [k(x_i,x_j)], N x N. */
 gprx_status gprx_kernel_matrix(gprx_ctx* ctx, gprx_dtype dtype, const gprx_kernel_desc* kernel, const void* X,

@@ -415,6 +415,81 @@ static void posterior_test2_loaded() {
     posterior_test2_on(*rd);
 }
 
+// A user Kernel<T> subclass without a device form (no Describe override): the GP evaluates
+// it through the virtual operator() / GetDerivative, as the reference does for every kernel
+// (include/Kernel.h:52-59), and factors / solves / reduces on the device.  Same Gaussian
+// function as the built-in kernel: identical predictions, intervals and likelihood.
+template <class T>
+class UserGaussian : public Kernel<T> {
+public:
+    typedef typename Kernel<T>::VectorType VectorType;
+    typedef typename Kernel<T>::ParameterVectorType ParameterVectorType;
+    UserGaussian(T sigma, T scale) : s(sigma), c(scale) {
+        this->m_Parameters = {sigma, scale};
+        this->m_StringParameters = {this->P2S(sigma), this->P2S(scale)};
+    }
+    T operator()(const VectorType& x, const VectorType& y) const override {
+        const T r = (x - y).norm();
+        return c * c * std::exp(-0.5 * r * r / (s * s));
+    }
+    VectorType GetDerivative(const VectorType& x, const VectorType& y) const override {
+        const T r = (x - y).norm(), f = std::exp(-0.5 * r * r / (s * s));
+        VectorType D(2);
+        D[0] = c * c * r * r / (s * s * s) * f;
+        D[1] = 2 * c * f;
+        return D;
+    }
+    std::string ToString() const override { return "UserGaussian(" + this->ParametersToString(this->m_StringParameters) + ")"; }
+    unsigned GetNumberOfParameters() const override { return 2; }
+    void SetParameters(const ParameterVectorType& p) override {
+        s = p[0];
+        c = p[1];
+        this->m_Parameters = p;
+    }
+
+private:
+    T s, c;
+};
+
+static void host_kernel_test() {
+    typedef GP<double> G;
+    auto gu = std::make_shared<G>(std::make_shared<UserGaussian<double>>(0.7, 1.3));
+    auto gd = std::make_shared<G>(std::make_shared<GaussianKernel<double>>(0.7, 1.3));
+    for (auto& gp : {gu, gd}) {
+        gp->SetSigma(0.1);
+        for (unsigned i = 0; i < 60; i++) {
+            G::VectorType x(2), y(1);
+            x(0) = std::sin(0.37 * i);
+            x(1) = std::cos(1.3 * i);
+            y(0) = std::sin(2 * x(0)) + 0.5 * x(1);
+            gp->AddSample(x, y);
+        }
+        gp->Initialize();
+    }
+    for (unsigned i = 0; i < 20; i++) {
+        G::VectorType x(2), x2(2);
+        x(0) = 0.05 * i - 0.5;
+        x(1) = 0.3 - 0.02 * i;
+        x2(0) = x(1);
+        x2(1) = x(0);
+        G::MatrixType Du, Dd;
+        const double mu = gu->PredictDerivative(x, Du)(0), md = gd->PredictDerivative(x, Dd)(0);
+        check(std::fabs(mu - md) <= 1e-9 * std::max(1.0, std::fabs(md)), "mean " + num(mu) + " vs " + num(md));
+        for (unsigned k = 0; k < 2; k++)
+            check(std::fabs(Du(k, 0) - Dd(k, 0)) <= 1e-8 * std::max(1.0, std::fabs(Dd(k, 0))), "derivative");
+        const double cu = (*gu)(x, x2), cd = (*gd)(x, x2);
+        check(std::fabs(cu - cd) <= 1e-9, "posterior covariance " + num(cu) + " vs " + num(cd));
+        check(std::fabs(gu->GetCredibleInterval(x) - gd->GetCredibleInterval(x)) <= 1e-7, "credible interval");
+    }
+    GaussianLogLikelihood<double> lik;
+    auto vu = lik.GetValueAndParameterDerivatives(gu), vd = lik.GetValueAndParameterDerivatives(gd);
+    check(std::fabs(vu.first(0) - vd.first(0)) <= 1e-8 * std::fabs(vd.first(0)),
+          "likelihood " + num(vu.first(0)) + " vs " + num(vd.first(0)));
+    for (unsigned p = 0; p < 2; p++)
+        check(std::fabs(vu.second(p) - vd.second(p)) <= 1e-7 * std::max(1.0, std::fabs(vd.second(p))),
+              "likelihood gradient " + num(vu.second(p)) + " vs " + num(vd.second(p)));
+}
+
 int main() {
     run("GaussianProcessTest1", gp_test1);
     run("GaussianProcessTest2", gp_test2);
@@ -431,5 +506,6 @@ int main() {
     run("PosteriorProcessTest1", posterior_test1);
     run("PosteriorProcessTest2", posterior_test2);
     run("PosteriorProcessTest2Loaded", posterior_test2_loaded);
+    run("HostEvaluatedKernel", host_kernel_test);
     return g_fail;
 }

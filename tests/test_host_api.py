@@ -7,7 +7,8 @@ KernelFactory<T>, Likelihood<T>, MatrixIO — driven through its two test execut
 * gp_host_test (-m gpu): the reference's GaussianProcessTest 1-7 and IOTest 1-3 with the
   reference's thresholds, plus a likelihood gradient consistency check, the sparse GP and
   PosteriorProcessTest 1-2 (Predict / operator() from 8 threads at once, on a fresh and on a
-  loaded GP), all running their fits on the GPU through libgprx."""
+  loaded GP), and a user Kernel<T> subclass with no device form (host-evaluated through its
+  virtual operator(), factored on the device), all running their fits on the GPU."""
 import os
 import subprocess
 
@@ -45,4 +46,4 @@ def test_host_cpu():
 def test_host_gpu_reference_scenarios():
     rc, lines, out = _run("gp_host_test")
     assert rc == 0, out
-    assert len(lines) == 15 and all(l.startswith("PASS") for l in lines), out
+    assert len(lines) == 16 and all(l.startswith("PASS") for l in lines), out
