@@ -263,6 +263,11 @@ struct gprx_model {
     // reference's virtual Kernel<T>::operator() (include/Kernel.h:52-59); see k_hostk.hip
     bool host_k = false;
     DevBuf Kext;
+    // a sparse GP's variance state (gprx_model_set_sparse_cov): the model holds the inducing
+    // points and W = Kmm^{-1} - RM (padded np x np, column-major) for
+    // operator()(x,y) = k(x,y) - Kx^T W Ky (include/SparseGaussianProcess.h:94-106)
+    bool sparse_cov = false;
+    DevBuf sparseW;
     std::mutex mu;
     ~gprx_model() { dist_engine_free(dist_engine); }
 };
@@ -812,7 +817,8 @@ static void solve_rows_for(gprx_model* M, const T* dXq, const T* dtabQ, int64_t 
 
 template <typename T>
 static gprx_status model_posterior_cov(gprx_model* M, const void* Xa, const void* Xb, int64_t q, void* out) {
-    GPRX_REQUIRE(M->fitted, GPRX_ERR_STATE, "GaussianProcess::ComputeKernelVectorInternal: gaussian process is not initialized.");
+    GPRX_REQUIRE(M->fitted || M->sparse_cov, GPRX_ERR_STATE,
+                 "GaussianProcess::ComputeKernelVectorInternal: gaussian process is not initialized.");
     GPRX_REQUIRE(!M->dist_fitted, GPRX_ERR_STATE,
                  "gprx: the posterior covariance needs a single-GPU fit (a distributed fit keeps its factor in tiles)");
     GPRX_REQUIRE(!M->host_k, GPRX_ERR_STATE, "gprx: a caller-evaluated kernel uses gprx_model_posterior_cov_kx");
@@ -828,6 +834,26 @@ static gprx_status model_posterior_cov(gprx_model* M, const void* Xa, const void
         tb.ensure(sizeof(T) * 2 * K.nper * q * d);
         launch_sincos_tables<T>(K, da.as<T>(), q, d, ta.as<T>(), s);
         launch_sincos_tables<T>(K, db.as<T>(), q, d, tb.as<T>(), s);
+    }
+    if (M->sparse_cov) {  // k(x,y) - Kx^T W Ky over the inducing points, batched on the device
+        const int64_t Mp = round_up(M->n, GT);
+        DevBuf Z;
+        Ra.ensure(sizeof(T) * qp * Mp);
+        Rb.ensure(sizeof(T) * qp * Mp);
+        Z.ensure(sizeof(T) * qp * Mp);
+        GPRX_HIP(hipMemsetAsync(Ra.p, 0, sizeof(T) * qp * Mp, s));
+        GPRX_HIP(hipMemsetAsync(Rb.p, 0, sizeof(T) * qp * Mp, s));
+        launch_kbuild<T>(K, da.as<T>(), ta.as<T>(), q, M->X.as<T>(), M->tab.as<T>(), M->n, d, Ra.as<T>(), qp, 0, false,
+                         T(0), M->flag.as<int>(), s);
+        launch_kbuild<T>(K, db.as<T>(), tb.as<T>(), q, M->X.as<T>(), M->tab.as<T>(), M->n, d, Rb.as<T>(), qp, 0, false,
+                         T(0), M->flag.as<int>(), s);
+        launch_gemm_nt<T>(Z.as<T>(), qp, Rb.as<T>(), qp, M->sparseW.as<T>(), Mp, qp, Mp, Mp, T(1), T(0), false, s);
+        kab.ensure(sizeof(T) * q);
+        res.ensure(sizeof(T) * q);
+        launch_pair_kernel<T>(K, da.as<T>(), db.as<T>(), q, d, kab.as<T>(), s);
+        launch_rowdot<T>(Ra.as<T>(), Z.as<T>(), qp, q, Mp, kab.as<T>(), res.as<T>(), s);
+        download(out, res.p, sizeof(T) * q, s);
+        return GPRX_OK;
     }
     if (M->method == 1) {  // LU factors: k(x,y) - K(X,x)^T A^{-1} K(X,y), the reference's formula (:84-99)
         const int64_t np = M->np;
@@ -1439,7 +1465,7 @@ static gprx_status sparse_fit_impl(gprx_ctx* ctx, const gprx_kernel_desc* desc, 
         launch_syrk_splitk<T>(dS.as<T>(), ld, sstride, dA.as<T>(), ld, fused ? Mp : ld, Mp, kpart, Pc, is2, s);
     }
     launch_sum_partials<T>(dS.as<T>(), sstride, P, s);  // dS[0] += dS[1..P-1]
-    if (ctx->comm && ctx->world > 1) {
+    if (ctx->comm) {  // rows sharded over the ranks: sum the partial normal equations
         const ncclResult_t r =
             ncclAllReduce(dS.p, dS.p, (size_t)(ld * Mp), nccl_type<T>(), ncclSum, ctx->comm, s);
         if (r != ncclSuccess) throw Error{GPRX_ERR_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(r)};
@@ -1610,6 +1636,7 @@ gprx_status gprx_model_set_data(gprx_model* M, const void* X, const void* Y, int
     M->d = d;
     M->m = m;
     M->has_data = true;
+    M->sparse_cov = false;
     M->fitted = false;
     M->has_alpha = false;
     M->inv_ready = false;
@@ -1748,6 +1775,39 @@ gprx_status gprx_model_lml(gprx_model* M, uint32_t flags, double* value, double*
     GPRX_HIP(hipSetDevice(ctx->device));
     return M->dt == GPRX_F64 ? model_lml<double>(M, flags, value, grad, nparams, logdet)
                              : model_lml<float>(M, flags, value, grad, nparams, logdet);
+    API_END(ctx)
+}
+
+gprx_status gprx_model_set_sparse_cov(gprx_model* M, const void* W) {
+    gprx_ctx* ctx = M ? M->ctx : nullptr;
+    API_BEGIN
+    GPRX_REQUIRE(M && W, GPRX_ERR_ARG, "gprx_model_set_sparse_cov: NULL argument");
+    ModelLock lk(M);
+    GPRX_REQUIRE(M->has_data && M->has_kernel && !M->host_k, GPRX_ERR_STATE,
+                 "gprx_model_set_sparse_cov: set the inducing points and the kernel first");
+    GPRX_HIP(hipSetDevice(ctx->device));
+    const int64_t n = M->n, Mp = round_up(n, GT);
+    const size_t es = esize(M->dt);
+    std::vector<unsigned char> h(es * Mp * Mp, 0);  // padded, column-major
+    for (int64_t i = 0; i < n; i++)
+        for (int64_t j = 0; j < n; j++)
+            std::memcpy(&h[es * (i + j * Mp)], static_cast<const unsigned char*>(W) + es * (i * n + j), es);
+    M->sparseW.ensure(h.size());
+    GPRX_HIP(hipStreamSynchronize(ctx->stream));
+    GPRX_HIP(hipMemcpy(M->sparseW.p, h.data(), h.size(), hipMemcpyHostToDevice));
+    const int nper = M->dt == GPRX_F64 ? M->kd.nper : M->kf.nper;
+    if (nper > 0) {  // the inducing points' sin/cos tables
+        M->tab.ensure(es * 2 * nper * n * M->d);
+        if (M->dt == GPRX_F64)
+            launch_sincos_tables<double>(M->kd, M->X.as<double>(), n, M->d, M->tab.as<double>(), ctx->stream);
+        else
+            launch_sincos_tables<float>(M->kf, M->X.as<float>(), n, M->d, M->tab.as<float>(), ctx->stream);
+    }
+    M->flag.ensure(sizeof(int));
+    GPRX_HIP(hipMemsetAsync(M->flag.p, 0, sizeof(int), ctx->stream));
+    GPRX_HIP(hipStreamSynchronize(ctx->stream));
+    M->sparse_cov = true;
+    return GPRX_OK;
     API_END(ctx)
 }
 

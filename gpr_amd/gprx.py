@@ -41,6 +41,7 @@ EXPORTED = [
     "gprx_kernel_matrix", "gprx_cross_matrix", "gprx_deriv_matrix", "gprx_cholesky", "gprx_spd_inverse",
     "gprx_sparse_fit", "gprx_ctx_set_stats", "gprx_ctx_get_stats",
     "gprx_model_set_kernel_matrix", "gprx_model_predict_kx", "gprx_model_posterior_cov_kx", "gprx_model_lml_dk",
+    "gprx_model_set_sparse_cov",
 ]
 
 
@@ -104,6 +105,7 @@ def lib():
         L.gprx_model_lml.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_double),
                                      ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_double)]
         L.gprx_model_set_kernel_matrix.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        L.gprx_model_set_sparse_cov.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         L.gprx_model_predict_kx.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                                             ctypes.c_void_p, ctypes.c_void_p]
         L.gprx_model_posterior_cov_kx.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
@@ -402,6 +404,12 @@ class Model:
         else:
             self._c(lib().gprx_model_posterior_cov(self.h, _ptr(Xa), _ptr(Xb), Xa.shape[0], _ptr(out)))
         return out
+
+    def set_sparse_cov(self, W):
+        """Make W = Kmm^{-1} - RM resident: posterior_cov then gives the sparse GP's operator()
+        (include/SparseGaussianProcess.h:94-106); the model's data are the inducing points."""
+        W = np.ascontiguousarray(W, self.dtype)
+        self._c(lib().gprx_model_set_sparse_cov(self.h, _ptr(W)))
 
     def credible_interval(self, Xq):
         """GetCredibleInterval (lib/GaussianProcess.cpp:102-114): 2 sqrt(max(0, gp(x,x)))."""

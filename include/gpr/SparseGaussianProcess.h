@@ -63,31 +63,15 @@ public:
         return mean;
     }
 
-    // include/SparseGaussianProcess.h:94-106: k(x,y) - Kx^T Kinv Ky + Kx^T RM Ky
+    // include/SparseGaussianProcess.h:94-106: k(x,y) - Kx^T Kinv Ky + Kx^T RM Ky, on the
+    // device against the resident W = Kinv - RM (gprx_model_set_sparse_cov)
     TScalarType operator()(const VectorType& x, const VectorType& y) override {
         Initialize();
         this->CheckInputDimension(x, "SparseGaussianProcess::(): ");
         this->CheckInputDimension(y, "SparseGaussianProcess::(): ");
-        const std::size_t M = m_InducingSampleVectors.size();
-        std::vector<TScalarType> Xm = Pack(m_InducingSampleVectors), kx(M), ky(M);
-        gprx_kernel_desc kd = Desc();
-        ThrowIfFailed(gprx_cross_matrix(DefaultContext(), Dtype(), &kd, x.data(), 1, Xm.data(), (int64_t)M,
-                                        (int32_t)x.size(), kx.data()),
-                      DefaultContext());
-        ThrowIfFailed(gprx_cross_matrix(DefaultContext(), Dtype(), &kd, y.data(), 1, Xm.data(), (int64_t)M,
-                                        (int32_t)y.size(), ky.data()),
-                      DefaultContext());
-        TScalarType a = 0, b = 0;
-        for (std::size_t i = 0; i < M; i++) {
-            TScalarType ti = 0, ri = 0;
-            for (std::size_t j = 0; j < M; j++) {
-                ti += m_Kinv[i * M + j] * ky[j];
-                ri += m_RM[i * M + j] * ky[j];
-            }
-            a += kx[i] * ti;
-            b += kx[i] * ri;
-        }
-        return (*this->m_Kernel)(x, y) - a + b;
+        TScalarType out = 0;
+        ThrowIfFailed(gprx_model_posterior_cov(m_Sparse, x.data(), y.data(), 1, &out), DefaultContext());
+        return out;
     }
 
     // include/SparseGaussianProcess.h:108-128
@@ -122,6 +106,9 @@ public:
                       DefaultContext());
         ThrowIfFailed(gprx_model_set_kernel(m_Sparse, &kd), DefaultContext());
         ThrowIfFailed(gprx_model_set_alpha(m_Sparse, m_RegressionVectors.data()), DefaultContext());
+        std::vector<TScalarType> W(M * M);
+        for (std::size_t i = 0; i < M * M; i++) W[i] = m_Kinv[i] - m_RM[i];
+        ThrowIfFailed(gprx_model_set_sparse_cov(m_Sparse, W.data()), DefaultContext());
         m_SparseInitialized = true;
     }
 

@@ -208,6 +208,13 @@ gprx_status gprx_model_core_matrix(gprx_model* model, void* C);
 gprx_status gprx_model_lml(gprx_model* model, uint32_t flags, double* value, double* grad, int32_t* nparams,
                            double* logdet);
 
+/* SparseGaussianProcess::operator()(x,y) = k(x,y) - Kx^T Kmm^{-1} Ky + Kx^T RM Ky
+ * (include/SparseGaussianProcess.h:94-106) on a model whose data are the inducing points:
+ * W = Kmm^{-1} - RM (M x M, row-major, from gprx_sparse_fit) becomes resident, and
+ * gprx_model_posterior_cov then evaluates q pairs on the device (two cross-kernel blocks, one
+ * GEMM, one row dot). */
+gprx_status gprx_model_set_sparse_cov(gprx_model* model, const void* W);
+
 /* ---- kernels with no device form ----------------------------------------------------
  * The reference dispatches every pair through the virtual Kernel<T>::operator() /
  * GetDerivative (include/Kernel.h:52-59), so a user subclass works with the GP unchanged.

@@ -90,3 +90,46 @@ def test_sparse_fit_multi_tile(ctx, monkeypatch, ks):
     assert relerr(RV, RV_r) <= tol
     assert relerr(RM, RM_r) <= tol
     assert np.array_equal(Kinv, Kinv.T) and np.array_equal(RM, RM.T)
+
+
+@pytest.mark.parametrize("ks", [CASES[0][0], CASES[1][0]])
+def test_sparse_operator_on_device(ctx, ks):
+    """SparseGaussianProcess::operator()(x,y) = k(x,y) - Kx^T Kinv Ky + Kx^T RM Ky
+    (include/SparseGaussianProcess.h:94-106) from the resident W = Kinv - RM
+    (gprx_model_set_sparse_cov), batched over q pairs, vs the oracle's matrices in numpy."""
+    import gpr_amd
+    n, d, M, m = 900, 3, 60, 1
+    X, Y, Xm = _inputs(n, d, M, m, np.float64)
+    Kinv, RV, RM = ctx.sparse_fit(ks, X, Y, Xm, 0.3, 1e-4)
+    Ki_r, RV_r, RM_r = O.sparse_fit(ks, X, Y, Xm, 0.3, 1e-4)
+    S = gpr_amd.Model(ctx, np.float64)
+    S.set_data(Xm, Y[:: n // M][:M])
+    S.set_kernel(ks)
+    S.set_alpha(RV)
+    S.set_sparse_cov(Kinv - RM)
+    Xa, Xb = make_queries(150, d), make_queries(150, d)[::-1].copy()
+    cov = S.posterior_cov(Xa, Xb)
+    Ka, Kb = O.cross_matrix(ks, Xa, Xm), O.cross_matrix(ks, Xb, Xm)
+    kab = np.array([O.cross_matrix(ks, Xa[i:i + 1], Xb[i:i + 1])[0, 0] for i in range(150)])
+    ref = kab - np.sum(Ka * ((Ki_r - RM_r) @ Kb.T).T, axis=1)
+    assert np.max(np.abs(cov - ref)) <= 1e-8 * max(1.0, np.max(np.abs(ref)))
+    S.close()
+
+
+def test_sparse_fit_rccl_one_rank():
+    """gprx_sparse_fit on an RCCL context: the dense rows are the rank's shard and the partial
+    normal equations [Kmn; Y^T][Kmn; Y^T]^T are summed by ncclAllReduce (SURVEY.md 8(e)
+    "Sparse fit"); on one rank the result equals the local fit."""
+    import gpr_amd
+    ks = CASES[0][0]
+    n, d, M, m = 800, 3, 48, 1
+    X, Y, Xm = _inputs(n, d, M, m, np.float64)
+    lctx = gpr_amd.Context(0)
+    dctx = gpr_amd.Context(0, dist=(0, 1, gpr_amd.unique_id()))
+    try:
+        Kl, RVl, RMl = lctx.sparse_fit(ks, X, Y, Xm, 0.3, 1e-4)
+        Kd, RVd, RMd = dctx.sparse_fit(ks, X, Y, Xm, 0.3, 1e-4)
+        assert relerr(RVd, RVl) <= 1e-12 and relerr(RMd, RMl) <= 1e-12 and relerr(Kd, Kl) <= 1e-12
+    finally:
+        dctx.close()
+        lctx.close()
