@@ -167,9 +167,9 @@ __device__ __forceinline__ void dbg_mark(int* dbg, int q, int phase, int i, int 
 }
 
 template <typename T>
-__device__ __forceinline__ void diag_factor(T* __restrict__ A, int64_t ld, T* __restrict__ Linv, int* __restrict__ info,
-                                            int64_t col0, unsigned char* smem_raw, const int t, int* dbg = nullptr,
-                                            long long* prof = nullptr) {
+__device__ __forceinline__ void diag_factor_rank8(T* __restrict__ A, int64_t ld, T* __restrict__ Linv,
+                                                  int* __restrict__ info, int64_t col0, unsigned char* smem_raw,
+                                                  const int t, int* dbg = nullptr, long long* prof = nullptr) {
     long long pt0 = prof ? wall_clock64() : 0, pacc1 = 0, pacc2 = 0, pm = 0;
     T(*sV)[SPL] = reinterpret_cast<T(*)[SPL]>(smem_raw);
     T(*sP)[SPL] = reinterpret_cast<T(*)[SPL]>(smem_raw + sizeof(T) * 8 * SPL);
@@ -336,6 +336,369 @@ __device__ __forceinline__ void diag_factor(T* __restrict__ A, int64_t ld, T* __
         for (int c = t >> 7; c < DB; c += NT / DB) {
             if (r >= c) A[r + (int64_t)c * ld] = sI[r][c];
             Linv[r + c * DB] = (r > c) ? sI[c][r] : ((r == c) ? sBd[r] : T(0));
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Diagonal 128x128 block, blocked: four 32-column panels, the panel's 32 x 32 diagonal block
+// factored by ONE wave in registers and everything else on the MFMA units.
+//
+// The block lives in LDS (column-major, stride SIL): lower triangle = A becoming L; the
+// strict upper triangle collects Linv^T (Linv = L^{-1}), its diagonal goes to sDi.  Per panel
+// p (c0 = 32 p):
+//   1  wave 0: D = L_pp L_pp^T in registers -- lane l < 32 holds row l of D, lane 32 + i row
+//      i of the identity riding along (it ends as row i of L_pp^{-T}); column step c: the
+//      pivot and the scaled column are broadcast by readlane (scalar operands), no barrier.
+//      L_pp -> lower, Dinv_p = L_pp^{-1} -> upper (transposed) + sDi
+//   2  all waves: panel rows below, L_rp = A_rp Dinv_p^T (16x16 MFMA tiles, K = 32)
+//   3  all waves: trailing lower tiles A_rr' -= L_rp L_r'p^T
+// then the off-diagonal 32-blocks of Linv by distance d = 1..3:
+//   Linv_ij = -Dinv_i sum_{k=j}^{i-1} L_ik Linv_kj  (i = j + d; S staged in Linv_ij's slot)
+// and L, Linv leave in coalesced column stores.  Replaces the rank-8 in-register image
+// (diag_factor_rank8: 16 serial pivot steps of 2 barriers each, 52 us per DIAGX task).
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ double rl_lane(double v, int lane) {
+    const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, lane);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), lane);
+    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+__device__ __forceinline__ float rl_lane(float v, int lane) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), lane));
+}
+
+// One wave factors the 32 x 32 diagonal block D at (c0, c0) of the LDS image: L_D -> lower,
+// Dinv = L_D^{-1} -> upper (transposed, Dinv[j][i] at row c0 + i, column c0 + j) and sDi.
+//
+// (f64; f32 keeps diag_factor_rank8.)  The augmented [D; I] (64 x 32) lives in eight 16x16 MFMA accumulator tiles
+// (acc[tr][tc][reg] = row 16 tr + lane % 16, column 16 tc + lane / 16 + 4 reg).  Column steps
+// of 4: the 4 x 4 pivot block comes out by readlane, its factor and inverse are formed
+// uniformly, the 4 panel columns -- ONE register of the tile column, lanes (row, column) --
+// are solved by three shuffles and four FMAs per lane, and the trailing update is one
+// v_mfma_f64_16x16x4f64 per tile straight from those panel registers (their (row, k) lane
+// layout is the MFMA operand layout), with the finished columns masked to zero in the
+// operand.  The identity rows (tiles 2, 3) end as L_D^{-T}.
+template <typename T>
+__device__ __forceinline__ void fact32(T* __restrict__ sS, T* __restrict__ sDi, int c0, int& fail) {
+    constexpr int SL = SIL;
+    const int lane = threadIdx.x & 63, lr = lane & 15, lk = lane >> 4;
+    if constexpr (std::is_same<T, double>::value) {
+        typedef Mfma<double> Tr;
+        // tiles (tile row tr: 0, 1 = D, 2, 3 = identity; tile column tc) that can be nonzero:
+        // (0, 1) is above the diagonal and (3, 1)'s partner (3, 0) stays zero (L^{-T} is upper)
+        constexpr int TI[4][2] = {{0, -1}, {1, 2}, {3, 4}, {-1, 5}};
+        d4_t acc[6];
+#pragma unroll
+        for (int tr = 0; tr < 4; tr++)
+#pragma unroll
+            for (int tc = 0; tc < 2; tc++) {
+                if (TI[tr][tc] < 0) continue;
+#pragma unroll
+                for (int rg = 0; rg < 4; rg++) {
+                    const int R = 16 * tr + lr, C = 16 * tc + Tr::orow(lk, rg);
+                    double v;
+                    if (tr < 2) v = (C <= R) ? sS[(c0 + R) + (c0 + C) * SL] : 0.0;
+                    else v = (R - 32 == C) ? 1.0 : 0.0;
+                    acc[TI[tr][tc]][rg] = v;
+                }
+            }
+#pragma unroll
+        for (int st = 0; st < 8; st++) {
+            const int k0 = 4 * st, tc = k0 / 16, rg = (k0 % 16) / 4, pl = k0 % 16;
+            // the 4 x 4 pivot block (lower) of tile (tc, tc): P[i][j] at lane (pl + i) + 16 j;
+            // its factor, then Q = L_P^{-1}, reduced to this lane's row qr = Q[lk][.]
+            double qr[4];
+            {
+                double Lp[4][4], rq[4];
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+#pragma unroll
+                    for (int j = 0; j < i; j++) {
+                        double v = rl_lane(acc[TI[tc][tc]][rg], pl + i + 16 * j);
+#pragma unroll
+                        for (int k = 0; k < j; k++) v = fma(-Lp[i][k], Lp[j][k], v);
+                        Lp[i][j] = v * rq[j];
+                    }
+                    double dsum = rl_lane(acc[TI[tc][tc]][rg], pl + i + 16 * i);
+#pragma unroll
+                    for (int k = 0; k < i; k++) dsum = fma(-Lp[i][k], Lp[i][k], dsum);
+                    if (!(dsum > 0.0) && fail < 0) fail = c0 + k0 + i;
+                    rq[i] = rsqrt_full(dsum);
+                    Lp[i][i] = dsum * rq[i];
+                }
+                double Q[4][4];
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    Q[i][i] = rq[i];
+#pragma unroll
+                    for (int j = 0; j < i; j++) {
+                        double v = 0.0;
+#pragma unroll
+                        for (int k = j; k < i; k++) v = fma(Lp[i][k], Q[k][j], v);
+                        Q[i][j] = -v * rq[i];
+                    }
+                }
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    double v = 0.0;
+#pragma unroll
+                    for (int j = i; j < 4; j++) v = (lk == j) ? Q[j][i] : v;
+                    qr[i] = v;
+                }
+            }
+            // panel: L[r][k0 + lk] = sum_{i <= lk} a[r][k0 + i] Q[lk][i] (D rows above k0 kept)
+            double pv[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int tr = 0; tr < 4; tr++) {
+                if (TI[tr][tc] < 0) continue;
+                const double v = acc[TI[tr][tc]][rg];
+                double nv = 0.0;
+#pragma unroll
+                for (int i = 0; i < 4; i++) nv = fma(__shfl(v, lr + 16 * i, 64), qr[i], nv);
+                const bool keep = tr < 2 && 16 * tr + lr < k0;
+                pv[tr] = keep ? v : nv;
+                acc[TI[tr][tc]][rg] = pv[tr];
+            }
+            // trailing: tile (tr, tcp) -= panel(tr) panel_D(tcp)^T over the columns > k0 + 3
+#pragma unroll
+            for (int tcp = tc; tcp < 2; tcp++) {
+                const double a = (16 * tcp + lr > k0 + 3) ? -pv[tcp] : 0.0;
+#pragma unroll
+                for (int tr = 0; tr < 4; tr++) {
+                    if (TI[tr][tcp] < 0 || TI[tr][tc] < 0) continue;  // absent output / zero panel
+                    if (tr < 2 && tr < tcp) continue;
+                    const double b = (tr < 2 && 16 * tr + lr < k0 + 4) ? 0.0 : pv[tr];
+                    acc[TI[tr][tcp]] = Tr::mma(a, b, acc[TI[tr][tcp]]);
+                }
+            }
+        }
+        // out: L_D (lower incl. diagonal); Dinv from the identity rows (X = L_D^{-T},
+        // Dinv[j][i] = X[i][j]) transposed into the upper triangle, its diagonal into sDi
+#pragma unroll
+        for (int tr = 0; tr < 4; tr++)
+#pragma unroll
+            for (int tc = 0; tc < 2; tc++) {
+                if (TI[tr][tc] < 0) continue;
+#pragma unroll
+                for (int rg = 0; rg < 4; rg++) {
+                    const int R = 16 * tr + lr, C = 16 * tc + Tr::orow(lk, rg);
+                    const double v = acc[TI[tr][tc]][rg];
+                    if (tr < 2) {
+                        if (C <= R) sS[(c0 + R) + (c0 + C) * SL] = v;
+                    } else {
+                        const int i = R - 32;
+                        if (C > i) sS[(c0 + i) + (c0 + C) * SL] = v;
+                        else if (C == i) sDi[c0 + i] = v;
+                    }
+                }
+            }
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ void diag_factor(T* __restrict__ A, int64_t ld, T* __restrict__ Linv, int* __restrict__ info,
+                                            int64_t col0, unsigned char* smem_raw, const int t, int* dbg = nullptr,
+                                            long long* prof = nullptr) {
+#ifndef GPRX_DIAG_BLOCKED
+    // Default: the rank-8 register image.  The blocked form below (GPRX_DIAG_BLOCKED, f64) was
+    // measured at 47.8 us per diagonal factor against 52 us, but its register demand raised
+    // the whole persistent kernel's spills from 10 to 29 VGPRs and the C3 factorisation by
+    // 0.6 ms (27.3 -> 28.0 ms): kept as a measured experiment, off.
+    if constexpr (true) {
+#else
+    if constexpr (!std::is_same<T, double>::value) {  // f32: the rank-8 register image
+#endif
+        diag_factor_rank8<T>(A, ld, Linv, info, col0, smem_raw, t, dbg, prof);
+        return;
+    }
+    (void)dbg;
+    typedef Mfma<T> Tr;
+    typedef typename Tr::acc_t acc_t;
+    constexpr int SL = SIL;
+    T* sS = reinterpret_cast<T*>(smem_raw);
+    T* sDi = sS + (size_t)DB * SL;
+    const int w = t >> 6, lane = t & 63, lr = lane & 15, lk = lane >> 4;
+    long long pt0 = prof ? wall_clock64() : 0, pf = 0, pm = 0, pinv = 0;
+    // ---- load (column c, rows r: coalesced; all loads in flight before the LDS stores) --
+    {
+        const int r = t & (DB - 1), cq = t >> 7;
+        T v[DB / (NT / DB)];
+#pragma unroll
+        for (int u = 0; u < DB / (NT / DB); u++) v[u] = A[r + (int64_t)(cq + u * (NT / DB)) * ld];
+#pragma unroll
+        for (int u = 0; u < DB / (NT / DB); u++) sS[r + (cq + u * (NT / DB)) * SL] = v[u];
+    }
+    __syncthreads();
+    const long long pload = prof ? wall_clock64() : 0;
+    int fail = -1;
+#pragma unroll 1
+    for (int p = 0; p < 4; p++) {
+        const int c0 = 32 * p;
+        const long long tf0 = prof ? wall_clock64() : 0;
+        // ---- 1: the 32 x 32 diagonal block, wave 0 -----------------------------------------
+        if (w == 0) fact32<T>(sS, sDi, c0, fail);
+        __syncthreads();
+        if (prof) {
+            const long long tn = wall_clock64();
+            pf += tn - tf0;
+            pm = tn;
+        }
+        if (p == 3) break;
+        // ---- 2: L_rp = A_rp Dinv_p^T for the rows below (output tiles 16 x 16) -------------
+        const int r0 = c0 + 32, nrt = (DB - r0) / 16;
+        {
+            acc_t acc[2];
+            int tl[2];
+            int nt = 0;
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                const int tt = w + 8 * u;
+                tl[u] = tt;
+                acc[u] = acc_t{0};
+                if (tt < nrt * 2) {
+                    nt = u + 1;
+                    const int rt = tt >> 1, ct = tt & 1;
+                    const int cc = ct * 16 + lr;  // output column (Dinv row)
+#pragma unroll
+                    for (int kq = 0; kq < 8; kq++) {
+                        const int k = kq * 4 + lk;
+                        const T av = (k < cc) ? sS[(c0 + k) + (c0 + cc) * SL] : (k == cc ? sDi[c0 + cc] : T(0));
+                        const T bv = sS[(r0 + rt * 16 + lr) + (c0 + k) * SL];
+                        acc[u] = Tr::mma(av, bv, acc[u]);
+                    }
+                }
+            }
+            __syncthreads();  // every read of A_rp done before the panel is overwritten
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                if (u < nt) {
+                    const int rt = tl[u] >> 1, ct = tl[u] & 1;
+#pragma unroll
+                    for (int reg = 0; reg < 4; reg++)
+                        sS[(r0 + rt * 16 + lr) + (c0 + ct * 16 + Tr::orow(lk, reg)) * SL] = acc[u][reg];
+                }
+            }
+        }
+        __syncthreads();
+        // ---- 3: trailing lower tiles A_rr' -= L_rp L_r'p^T ---------------------------------
+        {
+            const int ntl = nrt * (nrt + 1) / 2;
+#pragma unroll 1
+            for (int tt = w; tt < ntl; tt += 8) {
+                int rt = 0;
+                while ((rt + 1) * (rt + 2) / 2 <= tt) rt++;
+                const int ct = tt - rt * (rt + 1) / 2;
+                acc_t acc = acc_t{0};
+#pragma unroll
+                for (int kq = 0; kq < 8; kq++) {
+                    const int k = kq * 4 + lk;
+                    const T av = sS[(r0 + ct * 16 + lr) + (c0 + k) * SL];
+                    const T bv = sS[(r0 + rt * 16 + lr) + (c0 + k) * SL];
+                    acc = Tr::mma(av, bv, acc);
+                }
+#pragma unroll
+                for (int reg = 0; reg < 4; reg++) {
+                    T& dst = sS[(r0 + rt * 16 + lr) + (r0 + ct * 16 + Tr::orow(lk, reg)) * SL];
+                    dst -= acc[reg];
+                }
+            }
+        }
+        __syncthreads();
+    }
+    if (prof) pinv = wall_clock64();
+    if (fail >= 0) atomicMin(info, (int)(col0 + fail + 1));  // wave 0, every lane the same value
+    // ---- the off-diagonal 32-blocks of Linv, by distance --------------------------------------
+    // Linv_ij (i > j) is kept transposed in the upper block (j, i): element (r, c) of Linv_ij at
+    // sS[(32 j + c) + (32 i + r) SL].  Dinv_j's elements: (kk > c) upper of block (j, j), sDi.
+#pragma unroll 1
+    for (int dd = 1; dd < 4; dd++) {
+        const int nb = 4 - dd, ntt = nb * 4;  // blocks j = 0 .. nb-1, four 16x16 tiles each
+        // ntt <= 12 tiles: wave w takes tile w and tile w + 8
+        // S = sum_{k=j}^{i-1} L_ik Linv_kj: out[r][c], b = L_i k-block rows, a = Linv_kj cols
+        acc_t acc = acc_t{0}, acc2 = acc_t{0};
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            const int tt = w + 8 * u;
+            if (tt >= ntt) continue;
+            const int j = tt >> 2, i = j + dd, rt = (tt >> 1) & 1, ct = tt & 1;
+            acc_t a0 = acc_t{0};
+#pragma unroll 1
+            for (int kb = j; kb < i; kb++) {
+#pragma unroll
+                for (int kq = 0; kq < 8; kq++) {
+                    const int kk = kq * 4 + lk, cc = ct * 16 + lr;
+                    T av;  // Linv_{kb, j}[kk][cc]
+                    if (kb == j) av = (kk > cc) ? sS[(32 * j + cc) + (32 * j + kk) * SL] : (kk == cc ? sDi[32 * j + cc] : T(0));
+                    else av = sS[(32 * j + cc) + (32 * kb + kk) * SL];
+                    const T bv = sS[(32 * i + rt * 16 + lr) + (32 * kb + kk) * SL];  // L_{i,kb}[r][kk]
+                    a0 = Tr::mma(av, bv, a0);
+                }
+            }
+            if (u == 0) acc = a0;
+            else acc2 = a0;
+        }
+        __syncthreads();  // reads of the previous level's blocks done
+        // stage S (transposed, like Linv) in block (j, i)'s slot
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            const int tt = w + 8 * u;
+            if (tt >= ntt) continue;
+            const int j = tt >> 2, i = j + dd, rt = (tt >> 1) & 1, ct = tt & 1;
+            const acc_t& a0 = u == 0 ? acc : acc2;
+#pragma unroll
+            for (int reg = 0; reg < 4; reg++) {
+                const int r = rt * 16 + lr, c = ct * 16 + Tr::orow(lk, reg);
+                sS[(32 * j + c) + (32 * i + r) * SL] = a0[reg];
+            }
+        }
+        __syncthreads();
+        // Linv_ij = -Dinv_i S: out[r][c] = -sum_k Dinv_i[r][k] S[k][c]
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            const int tt = w + 8 * u;
+            if (tt >= ntt) continue;
+            const int j = tt >> 2, i = j + dd, rt = (tt >> 1) & 1, ct = tt & 1;
+            acc_t a0 = acc_t{0};
+#pragma unroll
+            for (int kq = 0; kq < 8; kq++) {
+                const int kk = kq * 4 + lk, rr = rt * 16 + lr, cc = ct * 16 + lr;
+                const T av = sS[(32 * j + cc) + (32 * i + kk) * SL];  // S[kk][cc]
+                const T bv = (kk < rr) ? sS[(32 * i + kk) + (32 * i + rr) * SL]
+                                       : (kk == rr ? sDi[32 * i + rr] : T(0));  // Dinv_i[rr][kk]
+                a0 = Tr::mma(av, bv, a0);
+            }
+            if (u == 0) acc = a0;
+            else acc2 = a0;
+        }
+        __syncthreads();  // S read before it is overwritten by Linv_ij
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            const int tt = w + 8 * u;
+            if (tt >= ntt) continue;
+            const int j = tt >> 2, i = j + dd, rt = (tt >> 1) & 1, ct = tt & 1;
+            const acc_t& a0 = u == 0 ? acc : acc2;
+#pragma unroll
+            for (int reg = 0; reg < 4; reg++) {
+                const int r = rt * 16 + lr, c = ct * 16 + Tr::orow(lk, reg);
+                sS[(32 * j + c) + (32 * i + r) * SL] = -a0[reg];
+            }
+        }
+        __syncthreads();
+    }
+    if (prof && t == 0) {
+        const long long te = wall_clock64();
+        prof[0] = pload - pt0;
+        prof[1] = pf;
+        prof[2] = (pinv - pload - pf) + (te - pinv);
+        (void)pm;
+    }
+    // ---- L and Linv out: coalesced columns ------------------------------------------------
+    {
+        const int r = t & (DB - 1);
+        for (int c = t >> 7; c < DB; c += NT / DB) {
+            if (r >= c) A[r + (int64_t)c * ld] = sS[r + c * SL];
+            Linv[r + c * DB] = (r > c) ? sS[c + r * SL] : ((r == c) ? sDi[r] : T(0));
         }
     }
 }
