@@ -614,6 +614,23 @@ static gprx_status model_fit(gprx_model* M, uint32_t flags, gprx_fit_info* out) 
                  "gprx_model_fit: GPRX_FIT_DISTRIBUTED needs a context from gprx_ctx_create_dist");
     if ((ctx->comm && ctx->world > 1) || ctx->virt || (flags & GPRX_FIT_DISTRIBUTED)) return model_fit_dist<T>(M, out);
     M->dist_fitted = false;
+    if (flags & GPRX_FIT_FORCE_LU) {  // the SVD inversion methods' stand-in: LU in double directly
+        const int64_t np0 = round_up(M->n, (int64_t)DB);
+        M->np = np0;
+        M->mp = round_up(M->m, GT);
+        M->ld = np0;
+        M->inv_ready = false;
+        M->info.ensure(sizeof(int));
+        M->flag.ensure(sizeof(int));
+        M->alpha.ensure(sizeof(T) * np0 * M->m);
+        if (K.nper > 0) {
+            M->tab.ensure(sizeof(T) * 2 * K.nper * M->n * M->d);
+            launch_sincos_tables<T>(K, M->X.as<T>(), M->n, M->d, M->tab.as<T>(), s);
+        }
+        if (out) std::memset(out, 0, sizeof(*out));
+        lu_fit<T>(M, out);
+        return GPRX_OK;
+    }
     const int64_t n = M->n, np = round_up(n, (int64_t)DB), mp = round_up(M->m, GT);
     // the explicit inverse rides along in the tile factorisation as np identity rows
     const bool want_inv = M->want_inv && potrf_uses_tiles();
@@ -956,7 +973,10 @@ static gprx_status model_lml(gprx_model* M, uint32_t flags, double* value, doubl
     try {
         // the likelihood inverts with the GP's method too (include/Likelihood.h:77-79 ->
         // ComputeCoreMatrixWithDeterminant): a matrix the Cholesky rejects takes the LU
-        st = model_fit<T>(M, (flags & GPRX_LML_DISTRIBUTED) ? GPRX_FIT_DISTRIBUTED : GPRX_FIT_DEFAULT, &fi);
+        st = model_fit<T>(M,
+                          ((flags & GPRX_LML_DISTRIBUTED) ? GPRX_FIT_DISTRIBUTED : 0u) |
+                              ((flags & GPRX_LML_FORCE_LU) ? GPRX_FIT_FORCE_LU : 0u),
+                          &fi);
     } catch (...) {
         M->want_inv = false;
         throw;

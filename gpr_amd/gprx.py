@@ -23,10 +23,12 @@ UNIQUE_ID_BYTES = 128
 FIT_DEFAULT = 0
 FIT_NO_LU_FALLBACK = 1
 FIT_DISTRIBUTED = 2
+FIT_FORCE_LU = 8
 FIT_F32_NO_REFINE = 4
 LML_GRAD = 1
 LML_COMPAT = 2
 LML_DISTRIBUTED = 4
+LML_FORCE_LU = 8
 
 STATUS = {0: "OK", 1: "NONFINITE", 2: "NOT_SPD", 3: "SINGULAR", 4: "DIM", 5: "HIP", 6: "RCCL", 7: "OOM",
           8: "ARG", 9: "STATE", 10: "NO_DEVICE"}
@@ -421,8 +423,9 @@ class Model:
         self._c(lib().gprx_model_core_matrix(self.h, _ptr(C)))
         return C
 
-    def lml(self, grad=True, compat=False, distributed=False):
-        flags = (LML_GRAD if grad else 0) | (LML_COMPAT if compat else 0) | (LML_DISTRIBUTED if distributed else 0)
+    def lml(self, grad=True, compat=False, distributed=False, force_lu=False):
+        flags = ((LML_GRAD if grad else 0) | (LML_COMPAT if compat else 0) | (LML_DISTRIBUTED if distributed else 0)
+                 | (LML_FORCE_LU if force_lu else 0))
         if self._host_kernel():
             dK = np.ascontiguousarray(self.kernel.gradient(self._Xh, self._Xh), self.dtype) if grad else None
             P = dK.shape[0] if grad else 0

@@ -144,7 +144,11 @@ template <class T>
 void GaussianProcess<T>::FitDevice(gprx_fit_info* info) {
     UploadState();
     gprx_fit_info fi;
-    ThrowIfFailed(gprx_model_fit(m_Model, GPRX_FIT_DEFAULT, &fi), DefaultContext());
+    // lib/GaussianProcess.cpp:531-618: FullPivotLU (default) and SelfAdjointEigenSolver take
+    // the Cholesky with the LU fallback; the SVD methods (the exact inverse V S^-1 U^T) take
+    // the LU in double directly (include/gprx.h GPRX_FIT_FORCE_LU)
+    const uint32_t flags = (m_InvMethod == JacobiSVD || m_InvMethod == BDCSVD) ? GPRX_FIT_FORCE_LU : GPRX_FIT_DEFAULT;
+    ThrowIfFailed(gprx_model_fit(m_Model, flags, &fi), DefaultContext());
     if (info) *info = fi;
     m_DeviceFactor = true;
 }

@@ -17,10 +17,11 @@
 // Differences (documented in DESIGN.md): the core matrix C = (K + sigma^2 I)^{-1} is
 // materialised lazily from the device factor (Save, GetCoreMatrix), not at every
 // Initialize; operator()/GetCredibleInterval use the factor (k - |L^{-1}k|^2) instead of
-// Kx^T C Ky.  The InversionMethod is recorded for API compatibility; the device factorises
-// with Cholesky and, when K + sigma^2 I is not numerically positive definite, falls back to
-// a partial-pivot LU in double (the reference's default FullPivotLU = dgetrf_,
-// include/LAPACKUtils.h:38-56; gpr_amd/csrc/k_getrf.hip).
+// Kx^T C Ky.  InversionMethod (lib/GaussianProcess.cpp:531-618): FullPivotLU (default) and
+// SelfAdjointEigenSolver factorise with Cholesky and, when K + sigma^2 I is not numerically
+// positive definite, fall back to a partial-pivot LU in double (FullPivotLU = dgetrf_,
+// include/LAPACKUtils.h:38-56; gpr_amd/csrc/k_getrf.hip); JacobiSVD / BDCSVD, whose formula is
+// the exact inverse V S^{-1} U^T, factorise with that LU directly (no SVD is formed).
 //
 // Threading (reference: tests/PosteriorProcessTest.cpp:120-134 calls Predict and operator()
 // concurrently after Initialize): the read-only calls may run concurrently; the lazy device

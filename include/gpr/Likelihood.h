@@ -62,6 +62,8 @@ protected:
         int32_t np = 0;
         e.grad.resize(GPRX_MAX_KNODES * 3);
         uint32_t flags = (compat ? GPRX_LML_COMPAT : 0u) | (grad ? GPRX_LML_GRAD : 0u);
+        typedef GaussianProcess<TScalarType> GPT;
+        if (gp->m_InvMethod == GPT::JacobiSVD || gp->m_InvMethod == GPT::BDCSVD) flags |= GPRX_LML_FORCE_LU;
         if (gp->m_HostKernel) {  // no device form: the derivative matrices through GetDerivative
             std::vector<TScalarType> dK;
             if (grad) dK = gp->HostDerivativeMatrices(np);

@@ -167,6 +167,14 @@ gprx_status gprx_model_set_noise(gprx_model* model, double sigma);
                                       default an fp32 fit factorises in fp32 and refines alpha in
                                       fp64 until it agrees with the double solve: the reference
                                       inverts fp32 GPs in double (include/LAPACKUtils.h:85-97) */
+#define GPRX_FIT_FORCE_LU 8u       /* factor with the partial-pivot LU in double directly (no
+                                      Cholesky first).  The reference's JacobiSVD / BDCSVD methods
+                                      (lib/GaussianProcess.cpp:564-592) form V S^{-1} U^T with every
+                                      singular value inverted, i.e. the exact inverse of a
+                                      nonsingular K: no SVD is built here, the LU gives the same
+                                      matrix to cond(K) eps (gpr::GaussianProcess maps those two
+                                      methods to this flag; SelfAdjointEigenSolver is the
+                                      reference's chol_invert, :594-612, the default path) */
 /* Initialize (lib/GaussianProcess.cpp:118-130) = ComputeRegressionVectors (:642-672):
  * kernel matrix (:384-402) + noise (:375-381) + factorisation (replaces the default
  * lapack::lu_invert dgetrf_+dgetri_, include/LAPACKUtils.h:38-56,85-97) + regression
@@ -196,6 +204,7 @@ gprx_status gprx_model_core_matrix(gprx_model* model, void* C);
 #define GPRX_LML_GRAD 1u   /* also compute the hyper-parameter gradient */
 #define GPRX_LML_COMPAT 2u /* reproduce the reference's determinant narrowing + clamps
                               (include/Likelihood.h:77-79, 240-257); otherwise exact */
+#define GPRX_LML_FORCE_LU 8u /* refit with GPRX_FIT_FORCE_LU (the SVD inversion methods) */
 #define GPRX_LML_DISTRIBUTED 4u /* refit with GPRX_FIT_DISTRIBUTED (implied on a multi-rank or
                               virtual context): log det = sum of the ranks' diagonal blocks,
                               C from the factor every rank assembles from its tiles (replicated

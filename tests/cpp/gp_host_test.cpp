@@ -490,6 +490,33 @@ static void host_kernel_test() {
               "likelihood gradient " + num(vu.second(p)) + " vs " + num(vd.second(p)));
 }
 
+// SetInversionMethod (lib/GaussianProcess.cpp:531-618): the SVD methods' exact inverse and the
+// self-adjoint (Cholesky) branch give the default method's regression to rounding.
+static void inversion_methods_test() {
+    typedef GP<double> G;
+    std::vector<std::shared_ptr<G>> gps;
+    for (int meth = 0; meth < 4; meth++) {
+        auto gp = std::make_shared<G>(std::make_shared<GaussianKernel<double>>(1.1, 0.9));
+        gp->SetSigma(0.05);
+        gp->SetInversionMethod(static_cast<G::InversionMethod>(meth));
+        for (unsigned i = 0; i < 80; i++) {
+            G::VectorType x(1), y(1);
+            x(0) = i * 0.1;
+            y(0) = std::sin(x(0));
+            gp->AddSample(x, y);
+        }
+        gp->Initialize();
+        gps.push_back(gp);
+    }
+    for (unsigned i = 0; i < 30; i++) {
+        G::VectorType x(1);
+        x(0) = 0.27 * i;
+        const double m0 = gps[0]->Predict(x)(0);
+        for (int meth = 1; meth < 4; meth++)
+            check(std::fabs(gps[meth]->Predict(x)(0) - m0) <= 1e-8, "method " + num(meth) + " prediction");
+    }
+}
+
 int main() {
     run("GaussianProcessTest1", gp_test1);
     run("GaussianProcessTest2", gp_test2);
@@ -507,5 +534,6 @@ int main() {
     run("PosteriorProcessTest2", posterior_test2);
     run("PosteriorProcessTest2Loaded", posterior_test2_loaded);
     run("HostEvaluatedKernel", host_kernel_test);
+    run("InversionMethods", inversion_methods_test);
     return g_fail;
 }

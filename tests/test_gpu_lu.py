@@ -142,3 +142,28 @@ def test_exactly_singular_raises(ctx):
         M.fit()
     assert e.value.status == 3  # SINGULAR
     M.close()
+
+
+def test_svd_inversion_methods(ctx):
+    """JacobiSVD / BDCSVD (lib/GaussianProcess.cpp:564-592) form core = V S^{-1} U^T, the exact
+    inverse of a nonsingular K; GPRX_FIT_FORCE_LU produces that matrix through the LU in double.
+    Restated with numpy's SVD (LAPACK gesdd) on an ill-conditioned K."""
+    from gpr_amd import gprx
+    n, d, sigma = 400, 2, 1e-3
+    ks = "GaussianKernel(0.9,1.0,)"
+    X, Y = make_data(n, d, 1)
+    K = O.kernel_matrix(ks, X) + sigma * sigma * np.eye(n)
+    U, S, Vt = np.linalg.svd(K)
+    core = Vt.T @ np.diag(1.0 / S) @ U.T
+    a_svd = core @ Y
+    M = _model(ctx, ks, X, Y, sigma)
+    info = M.fit(gprx.FIT_FORCE_LU)
+    assert info.method == 1
+    cond = S[0] / S[-1]
+    tol = max(1e-9, 50 * cond * np.finfo(np.float64).eps)
+    assert relerr(M.alpha(), a_svd) <= tol
+    Xq = make_queries(30, d)
+    assert relerr(M.predict(Xq), O.cross_matrix(ks, Xq, X) @ a_svd) <= tol
+    v, g, ld = M.lml(grad=True, force_lu=True)
+    assert abs(ld - np.linalg.slogdet(K)[1]) <= 1e-8 * abs(ld)
+    M.close()
