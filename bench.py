@@ -69,7 +69,7 @@ def cpu_baseline(cfg, n_cpu):
     }
 
 
-def traffic_from_profile(kernel="potrf_tiles_kernel<double>"):
+def traffic_from_profile(kernels=("potrf_tiles_kernel<double, false>", "potrf_tiles_kernel<double>")):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC passes
     (profiles/*_pmc_traffic.json, written by scripts/pmc_traffic.py: FETCH_SIZE x 2 (gfx950
     wide-read correction, MI355X_MICROARCH.md §HBM) + WRITE_SIZE, averaged over launches)."""
@@ -78,7 +78,8 @@ def traffic_from_profile(kernel="potrf_tiles_kernel<double>"):
     for path in reversed(files):
         try:
             with open(path) as f:
-                k = json.load(f)["kernels"].get(kernel)
+                ks = json.load(f)["kernels"]
+            k = next((ks[n] for n in kernels if n in ks), None)
         except Exception:
             continue
         if k is not None:
