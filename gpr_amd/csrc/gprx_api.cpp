@@ -379,8 +379,8 @@ static void refine_f32(gprx_model* M, gprx_fit_info* out) {
         }
         launch_residual_rows(M->Yd.as<double>(), M->kxd.as<double>(), M->ad.as<double>(), s2, n, m,
                              M->A.as<float>(), ld, np, np, (int)mp, s);
-        trsm_rows<float>(M->A.as<float>(), ld, np, M->Linv.as<float>(), M->A.as<float>() + np, ld, mp, s);
         GPRX_HIP(hipMemsetD32Async((hipDeviceptr_t)M->info.p, INT_MAX, 1, s));
+        launch_forward_chain<float>(M->A.as<float>(), ld, np, m, M->Linv.as<float>(), M->info.as<int>(), ctx->ex, s);
         launch_backsolve_chain<float>(M->A.as<float>(), ld, np, m, M->Linv.as<float>(), M->delta.as<float>(),
                                       M->info.as<int>(), ctx->ex, s);
         launch_refine_accumulate(M->delta.as<float>(), M->ad.as<double>(), M->alpha.as<float>(), n * m,

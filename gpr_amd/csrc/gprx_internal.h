@@ -75,8 +75,8 @@ __host__ __device__ inline T leaf_value(const KLeaf<T>& L, T r2, T s0, T s1) {
             return L.c0 * exp(L.c1 * r2);
         case L_WHITE:
             return (r2 == T(0)) ? L.c0 : T(0);
-        case L_RQ:
-            return L.c0 * exp(-L.c2 * log1p(L.c1 * r2));
+        case L_RQ:  // alpha = 1: std::pow(b, -1) = 1 / b
+            return (L.c2 == T(1)) ? L.c0 / (T(1) + L.c1 * r2) : L.c0 * exp(-L.c2 * log1p(L.c1 * r2));
         case L_PERIODIC:
             return L.c0 * exp(L.c1 * (L.pslot == 0 ? s0 : s1));
     }
@@ -487,6 +487,9 @@ void launch_backsolve(const T* A, int64_t ld, int64_t np, int m, const T* Linv, 
 template <typename T>
 void launch_backsolve_chain(const T* A, int64_t ld, int64_t np, int m, const T* Linv, T* alpha, int* info, Exec& ex,
                             hipStream_t s, const uint64_t* tiles = nullptr, const int64_t* tld = nullptr);
+// Forward substitution z = L^{-1} r in place in the label rows (A + np, ld), one chained launch
+template <typename T>
+void launch_forward_chain(T* A, int64_t ld, int64_t np, int m, const T* Linv, int* info, Exec& ex, hipStream_t s);
 
 // logdet partial = 2 sum log L_ii over i < n, datafit = sum of squares of the augmented
 // rows; results accumulated in double on the device (out[0], out[1]).

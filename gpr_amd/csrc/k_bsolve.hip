@@ -21,6 +21,7 @@
 #include "gprx_internal.h"
 
 #include <algorithm>
+#include <cstring>
 
 namespace gprx {
 
@@ -264,6 +265,99 @@ __global__ __launch_bounds__(NT) void backsolve_chain_kernel(Args<T> a) {
     if (t == 0 && ld_uni(a.ctl + C_ERR)) atomicMin(a.info, -1);
 }
 
+// ---------------------------------------------------------------------------------------
+// Forward substitution z = L^{-1} r in ONE launch, in place in the label rows of the factor
+// (rows np .. np + m - 1 hold r^T, then z^T): the correction solve of the fp32 refinement
+// (gprx_api.cpp refine_f32; the reference inverts fp32 GPs in double, LAPACKUtils.h:85-97).
+//     z_k = Linv_k ( r_k - sum_{j < k} L_kj z_j )                (128-row blocks k)
+// Block k = ticket (first block first): it waits only on blocks claimed before it.  Lanes own
+// rows (2 per lane), wave w columns 16 w .. 16 w + 15 of each tile: a tile's loads go out
+// before its z_j is waited for, z_j comes in as wave-uniform sc1 loads, and the eight waves'
+// row partials meet in LDS once per block.  Replaces 2 GEMM launches per block (trsm_rows).
+template <typename T>
+__global__ __launch_bounds__(NT) void forward_chain_kernel(Args<T> a) {
+    __shared__ T s_part[8][DB];
+    __shared__ T s_v[DB];
+    __shared__ int s_int[2];
+    const int t = threadIdx.x, w = __builtin_amdgcn_readfirstlane(t >> 6), lane = t & 63;
+    const int nb = (int)(a.np / DB);
+    int* flags = a.ctl + C_NCTL;
+    if (w == 0) {
+        const int v = __hip_atomic_fetch_add(a.ctl + C_TICKET, (t == 0) ? 1 : 0, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+        s_int[0] = __builtin_amdgcn_readfirstlane(v);
+    }
+    __syncthreads();
+    const int k = __builtin_amdgcn_readfirstlane(s_int[0]);
+    if (k >= nb) return;
+    T* zrows = const_cast<T*>(a.A) + a.np;  // label rows: element (rhs r, sample i) at zrows[r + i ld]
+    typedef T v2 __attribute__((ext_vector_type(2)));
+    bool ok = true;
+    for (int r = 0; r < a.m && ok; r++) {
+        int* fl = flags + (int64_t)r * nb;
+        const long long t0 = wall_clock64();
+        T p0 = 0, p1 = 0;  // rows 2 lane, 2 lane + 1 of block k
+        for (int j = 0; j < k && ok; j++) {
+            const T* tile = a.A + (int64_t)k * DB + (int64_t)j * DB * a.ld;  // L_kj
+            v2 x[CPW];
+#pragma unroll
+            for (int cc = 0; cc < CPW; cc++)
+                x[cc] = *reinterpret_cast<const v2*>(tile + (int64_t)(w * CPW + cc) * a.ld + 2 * lane);
+            ok = wait_flag(fl + j, a.ctl, t0, a.tlimit);
+            if (!ok) break;
+#pragma unroll
+            for (int cc = 0; cc < CPW; cc++) {
+                const T zc = ld_sc1(zrows + r + ((int64_t)j * DB + w * CPW + cc) * a.ld);
+                p0 = fma(x[cc][0], zc, p0);
+                p1 = fma(x[cc][1], zc, p1);
+            }
+        }
+        // agree on a failed wait (each wave polled on its own)
+        if (t == 0) s_int[1] = 0;
+        __syncthreads();
+        if (!ok && lane == 0) s_int[1] = 1;
+        s_part[w][2 * lane] = p0;
+        s_part[w][2 * lane + 1] = p1;
+        __syncthreads();
+        if (s_int[1]) {
+            ok = false;
+            break;
+        }
+        if (t < DB) {
+            T acc = 0;
+#pragma unroll
+            for (int ww = 0; ww < 8; ww++) acc += s_part[ww][t];
+            s_v[t] = zrows[r + ((int64_t)k * DB + t) * a.ld] - acc;
+        }
+        __syncthreads();
+        // z_k = Linv_k v
+        {
+            const T* Lk = a.Linv + (int64_t)k * DB * DB;
+            T q0 = 0, q1 = 0;
+#pragma unroll
+            for (int cc = 0; cc < CPW; cc++) {
+                const v2 x = *reinterpret_cast<const v2*>(Lk + (int64_t)(w * CPW + cc) * DB + 2 * lane);
+                const T vc = s_v[w * CPW + cc];
+                q0 = fma(x[0], vc, q0);
+                q1 = fma(x[1], vc, q1);
+            }
+            s_part[w][2 * lane] = q0;
+            s_part[w][2 * lane + 1] = q1;
+        }
+        __syncthreads();
+        if (t < DB) {
+            T acc = 0;
+#pragma unroll
+            for (int ww = 0; ww < 8; ww++) acc += s_part[ww][t];
+            st_sc1(zrows + r + ((int64_t)k * DB + t) * a.ld, acc);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (w == 0) __hip_atomic_store(fl + k, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (t == 0 && ld_uni(a.ctl + C_ERR)) atomicMin(a.info, -1);
+}
+
 }  // namespace bs
 
 // GPRX_BS_TRACE timeline of the last launch (per block, 100 MHz wall clock)
@@ -320,6 +414,31 @@ void launch_backsolve_chain(const T* A, int64_t ld, int64_t np, int m, const T* 
     hipLaunchKernelGGL(backsolve_chain_kernel<T>, dim3((unsigned)nb), dim3(NT), bs_lds<T>(), s, a);
     GPRX_HIP(hipGetLastError());
 }
+
+template <typename T>
+void launch_forward_chain(T* A, int64_t ld, int64_t np, int m, const T* Linv, int* info, Exec& ex, hipStream_t s) {
+    using namespace bs;
+    const int nb = (int)(np / DB);
+    const size_t need = (size_t)C_NCTL + (size_t)nb * m;
+    GPRX_REQUIRE(np % DB == 0 && ld % 2 == 0, GPRX_ERR_ARG, "launch_forward_chain: bad sizes");
+    int* scratch = ex.scratch_ints(need);
+    ProfScope ps(KC_BACKSOLVE, s, 2.0 * (double)np * np * m / 2.0, (double)sizeof(T) * np * (np + 1) / 2.0);
+    GPRX_HIP(hipMemsetAsync(scratch, 0, sizeof(int) * need, s));
+    Args<T> a;
+    std::memset(&a, 0, sizeof(a));
+    a.A = A;
+    a.ld = ld;
+    a.np = np;
+    a.m = m;
+    a.Linv = Linv;
+    a.ctl = scratch;
+    a.info = info;
+    a.tlimit = (long long)(1e8 * 4.0);
+    hipLaunchKernelGGL(forward_chain_kernel<T>, dim3((unsigned)nb), dim3(NT), 0, s, a);
+    GPRX_HIP(hipGetLastError());
+}
+template void launch_forward_chain<double>(double*, int64_t, int64_t, int, const double*, int*, Exec&, hipStream_t);
+template void launch_forward_chain<float>(float*, int64_t, int64_t, int, const float*, int*, Exec&, hipStream_t);
 
 template void launch_backsolve_chain<double>(const double*, int64_t, int64_t, int, const double*, double*, int*,
                                              Exec&, hipStream_t, const uint64_t*, const int64_t*);

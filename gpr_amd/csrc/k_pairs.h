@@ -45,10 +45,18 @@ __device__ __forceinline__ void leaf_into(const KLeaf<T>* __restrict__ L, const 
             p[e] = MUL ? p[e] * f : p[e] + f;
         }
     } else if (ty == L_RQ) {
+        if (c2 == T(1)) {  // alpha = 1: pow(b, -1) is 1 / b (the reference's std::pow, :794-797)
 #pragma unroll
-        for (int e = 0; e < E; e++) {
-            const T f = c0 * exp(-c2 * log1p(c1 * r2[e]));
-            p[e] = MUL ? p[e] * f : p[e] + f;
+            for (int e = 0; e < E; e++) {
+                const T f = c0 / (T(1) + c1 * r2[e]);
+                p[e] = MUL ? p[e] * f : p[e] + f;
+            }
+        } else {
+#pragma unroll
+            for (int e = 0; e < E; e++) {
+                const T f = c0 * exp(-c2 * log1p(c1 * r2[e]));
+                p[e] = MUL ? p[e] * f : p[e] + f;
+            }
         }
     } else {  // L_GAUSS, L_GAUSS_EXP
 #pragma unroll
