@@ -97,6 +97,7 @@ def main():
     ap.add_argument("--predict-q", type=int, default=65536)
     ap.add_argument("--lml", type=int, default=1, help="also time one log-marginal likelihood + gradient "
                                                         "(BASELINE.json configs[2]); 0 = skip")
+    ap.add_argument("--build-iters", type=int, default=3, help="time the covariance build alone (0 = skip)")
     ap.add_argument("--cpu-n", type=int, default=16384, help="N of the CPU-baseline sample (0 = skip)")
     ap.add_argument("--mode", choices=["replicas", "dist"], default="dist",
                     help="N>1 headline: one fit whose matrix is sharded over the GPUs (dist, strong "
@@ -237,6 +238,22 @@ def main():
         ctx.set_stats(False)
         lml = {"ms_wall": 1e3 * tl, "phases_ms": {k: v["ms"] for k, v in ls.items()}}
 
+    # the covariance build alone (north_star asks for its HBM GB/s; in the fit it is fused into
+    # the factorisation launch as BUILD tasks): the same BUILD tasks with no other task in the
+    # ticket list, features resident, device time by HIP events.  Algorithmic bytes per build
+    # (SURVEY.md 8(d)): 8 (n d + n (n + 1) / 2) -- X read once, the lower triangle written once.
+    build = None
+    if args.build_iters > 0:
+        try:
+            bms = max_over_ranks(ctx.build_time(cfg["kernel"], X, cfg["sigma"], path=0, iters=args.build_iters))
+            bbytes = 8.0 * (n * d + n * (n + 1) / 2)
+            build = {"ms": bms, "algorithmic_bytes": bbytes, "gbs": bbytes / (bms * 1e-3) / 1e9,
+                     "frac_hbm": bbytes / (bms * 1e-3) / 1e9 / PEAK_HBM_GBS,
+                     "entries_per_s": n * (n + 1) / 2 / (bms * 1e-3),
+                     "kernel": "potrf_tiles_kernel<double, false> with BUILD tasks only (k_ptiles.hip)"}
+        except Exception as e:
+            log("build timing failed:", e)
+
     # dominant kernel: the persistent tile-dataflow factorisation, one launch per fit (with
     # the covariance build fused in as BUILD tasks for sum-of-exp-leaf kernel trees).
     # Algorithmic work per launch = n^3/3 (Cholesky) + m n^2 (forward solve of the label
@@ -305,6 +322,7 @@ def main():
             "phases": phases,
             "predict": pred,
             "lml_grad": lml,
+            "build": build,
             "lml_grad_sharded_ms_wall": (dres or {}).get("lml_ms_wall"),
             "cpu_baseline": cpu,
         }

@@ -1299,7 +1299,7 @@ static gprx_status cholesky_impl(gprx_ctx* ctx, void* Ahost, int64_t n, int32_t*
 // gprx_dev_build_matrix: the fit's covariance tiles, written alone (include/gprx_dev.h)
 template <typename T>
 static gprx_status dev_build_impl(gprx_ctx* ctx, const gprx_kernel_desc* desc, const void* X, int64_t n, int d,
-                                  double sigma, int path, void* Kout) {
+                                  double sigma, int path, void* Kout, int iters = 0, double* ms = nullptr) {
     KCanon<T> K;
     std::string e = canonicalize<T>(*desc, K);
     GPRX_REQUIRE(e.empty(), GPRX_ERR_ARG, e);
@@ -1324,16 +1324,41 @@ static gprx_status dev_build_impl(gprx_ctx* ctx, const gprx_kernel_desc* desc, c
     launch_pair_features<T>(K, dx.as<T>(), n, d, dx.as<T>(), true, fv.as<T>(), np, s);
     GPRX_HIP(hipMemcpyAsync(kd.p, &K, sizeof(KCanon<T>), hipMemcpyHostToDevice, s));
     const T sig = (T)sigma, sigma2 = sig * sig;
+    TileBuild<T> tb{};
     if (path == 0) {
-        TileBuild<T> tb = pairs_tile_build<T>(K, kd.as<KCanon<T>>(), fu.as<T>(), fv.as<T>(), np, d, n, sigma2,
-                                              flag.as<int>());
+        tb = pairs_tile_build<T>(K, kd.as<KCanon<T>>(), fu.as<T>(), fv.as<T>(), np, d, n, sigma2, flag.as<int>());
         GPRX_REQUIRE(tb.mode != 0, GPRX_ERR_ARG,
                      "gprx_dev_build_matrix: the fused build carries sum-of-exp-leaf trees only (path 1 for others)");
-        potrf_tiles<T>(A.as<T>(), np, np, np, Li.as<T>(), info.as<int>(), ctx->ex, &tb, 0, true);
-    } else {
-        launch_kbuild_mma<T>(K, kd.as<KCanon<T>>(), fu.as<T>(), fv.as<T>(), np, d, A.as<T>(), np, n, sigma2,
-                             flag.as<int>(), s);
     }
+    auto launch = [&] {
+        if (path == 0)
+            potrf_tiles<T>(A.as<T>(), np, np, np, Li.as<T>(), info.as<int>(), ctx->ex, &tb, 0, true);
+        else
+            launch_kbuild_mma<T>(K, kd.as<KCanon<T>>(), fu.as<T>(), fv.as<T>(), np, d, A.as<T>(), np, n, sigma2,
+                                 flag.as<int>(), s);
+    };
+    if (ms) {  // gprx_dev_build_time: device time of the build alone (features resident)
+        launch();  // warm (schedule cached, code loaded)
+        hipStream_t ls = path == 0 ? ctx->ex.s0 : s;
+        GPRX_HIP(hipStreamSynchronize(s));
+        hipEvent_t e0, e1;
+        GPRX_HIP(hipEventCreate(&e0));
+        GPRX_HIP(hipEventCreate(&e1));
+        GPRX_HIP(hipEventRecord(e0, ls));
+        for (int it = 0; it < iters; it++) launch();
+        GPRX_HIP(hipEventRecord(e1, ls));
+        GPRX_HIP(hipEventSynchronize(e1));
+        float t = 0;
+        GPRX_HIP(hipEventElapsedTime(&t, e0, e1));
+        GPRX_HIP(hipEventDestroy(e0));
+        GPRX_HIP(hipEventDestroy(e1));
+        *ms = (double)t / std::max(1, iters);
+        int hinfo = 0;
+        download(&hinfo, info.p, sizeof(int), s);
+        check_sched(hinfo);
+        return GPRX_OK;
+    }
+    launch();
     std::vector<T> h((size_t)np * n);
     download(h.data(), A.p, sizeof(T) * np * n, s);
     int hf = 0, hinfo = 0;
@@ -2012,6 +2037,18 @@ gprx_status gprx_dev_build_matrix(gprx_ctx* ctx, gprx_dtype dt, const gprx_kerne
     GPRX_HIP(hipSetDevice(ctx->device));
     return dt == GPRX_F64 ? dev_build_impl<double>(ctx, k, X, n, d, sigma, path, K)
                           : dev_build_impl<float>(ctx, k, X, n, d, sigma, path, K);
+    API_END(ctx)
+}
+
+gprx_status gprx_dev_build_time(gprx_ctx* ctx, gprx_dtype dt, const gprx_kernel_desc* k, const void* X, int64_t n,
+                                int32_t d, double sigma, int32_t path, int32_t iters, double* ms) {
+    API_BEGIN
+    GPRX_REQUIRE(ctx && k && X && ms && iters > 0, GPRX_ERR_ARG, "gprx_dev_build_time: bad argument");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ProfBind pb_(ctx);
+    GPRX_HIP(hipSetDevice(ctx->device));
+    return dt == GPRX_F64 ? dev_build_impl<double>(ctx, k, X, n, d, sigma, path, nullptr, iters, ms)
+                          : dev_build_impl<float>(ctx, k, X, n, d, sigma, path, nullptr, iters, ms);
     API_END(ctx)
 }
 

@@ -138,6 +138,9 @@ def lib():
         L.gprx_dev_build_matrix.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(KernelDesc),
                                             ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_double,
                                             ctypes.c_int32, ctypes.c_void_p]
+        L.gprx_dev_build_time.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(KernelDesc),
+                                          ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_double,
+                                          ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(ctypes.c_double)]
         _lib = L
     return _lib
 
@@ -272,6 +275,15 @@ class Context:
         self._c(lib().gprx_dev_build_matrix(self.h, _dt(dtype), ctypes.byref(kernel_desc(kernel)), _ptr(X), n, d,
                                             float(sigma), path, _ptr(K)))
         return K
+
+    def build_time(self, kernel, X, sigma, path=0, iters=5, dtype=np.float64):
+        """Mean device ms of that build alone, features resident (gprx_dev_build_time)."""
+        X = np.ascontiguousarray(X, dtype)
+        n, d = X.shape
+        ms = ctypes.c_double(0)
+        self._c(lib().gprx_dev_build_time(self.h, _dt(dtype), ctypes.byref(kernel_desc(kernel)), _ptr(X), n, d,
+                                          float(sigma), path, iters, ctypes.byref(ms)))
+        return ms.value
 
     def cholesky(self, A):
         A = np.array(A, copy=True, order="C")

@@ -46,6 +46,10 @@ int64_t gprx_dev_bs_trace(int64_t* times, int64_t max_blocks);
  * GPRX_ERR_ARG when the tree is not covered by that path; GPRX_ERR_NONFINITE as the fit. */
 gprx_status gprx_dev_build_matrix(gprx_ctx* ctx, gprx_dtype dtype, const gprx_kernel_desc* kernel, const void* X,
                                   int64_t n, int32_t d, double sigma, int32_t path, void* K);
+/* Device time (mean over `iters` launches, HIP events on the launch's stream) of the same
+ * build alone, features already resident: bench.py reports the build's GB/s from it. */
+gprx_status gprx_dev_build_time(gprx_ctx* ctx, gprx_dtype dtype, const gprx_kernel_desc* kernel, const void* X,
+                                int64_t n, int32_t d, double sigma, int32_t path, int32_t iters, double* ms);
 /* Test context for the distributed fit: `world` VIRTUAL ranks in this process, all on one
  * GPU -- each runs its own persistent tile launch over its row blocks (a share of the CUs),
  * with device copies in place of the RCCL broadcast / panel exchange (gprx_dist.cpp).  Models

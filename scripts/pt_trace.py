@@ -68,6 +68,11 @@ for t in (0, 1, 2, 3):
             md = m & diag
             if md.any():
                 res[key]["diagtile_exec_us_mean"] = float(ex[md].mean())
+# worker time per task type, in ms of the whole chip (sum of exec / workers)
+res["chip_ms_by_type"] = {names[t]: round(float(ex[typ == t].sum() / P / 1e3), 3) for t in (0, 1, 2, 3)}
+res["chip_ms_wait"] = round(float(wt.sum() / P / 1e3), 3)
+res["chip_ms_idle"] = round(float(span / 1e3 - (ex.sum() + wt.sum()) / P / 1e3), 3)
+res["upd_panels"] = int(nb[typ == 2].sum())
 # DIAGX chain
 d = np.where(typ == 0)[0]
 order = np.argsort(tasks[d, 1])

@@ -80,6 +80,14 @@ def test_build_c3_shapes(ctx, n, d):
     assert relerr(ctx.build_matrix(ks, X, 1.0, 0), _ref(ks, X, 1.0)) <= 1e-12
 
 
+@pytest.mark.parametrize("path", [0, 1])
+def test_build_time_hook(ctx, path):
+    """gprx_dev_build_time (bench.py's build GB/s) runs the same launches and reports time."""
+    X, _ = make_data(1000, 32)
+    ms = ctx.build_time(FUSED[3], X, 1.0, path, iters=2)
+    assert 0.0 < ms < 1e3
+
+
 def test_build_breathing_raw_scale(ctx):
     """The reference's own 1-D breathing signal (tests/data/breathing1D.mat) at its raw
     amplitude, as sample coordinates: time-delay embedding x_i = (s_i, s_{i+1}, s_{i+2})."""
