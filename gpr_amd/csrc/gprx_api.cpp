@@ -1413,11 +1413,25 @@ static void download_sym(void* out, const DevBuf& C, int64_t ldc, int64_t n, hip
     GPRX_HIP(hipStreamSynchronize(s));
 }
 
+// Device state of the sparse GP's normal equations (shared by the fit and the likelihood).
 template <typename T>
-static gprx_status sparse_fit_impl(gprx_ctx* ctx, const gprx_kernel_desc* desc, const void* Xh, const void* Yh,
-                                   int64_t n, int d, int m, const void* Xmh, int64_t M, double sigma, double jitter,
-                                   void* Kinv, void* RV, void* RM) {
+struct SparseNE {
     KCanon<T> K{};
+    int64_t Mp = 0, mp = 0, ld = 0, chunk = 0, chunk128 = 0;
+    bool mma = false;
+    T is2 = 0;
+    DevBuf dXm, dtm, dX, dtx, dY, dS, dA, dK, dLinv, dLinvK, dinfo, dflag, dz, dalpha, dV, dC, dFU, dFV, dKd;
+};
+
+// SparseGaussianProcess::PreComputeRegression (include/SparseGaussianProcess.h:274-313) up to
+// the factorisation: S = Kmm + jitter I + sigma^-2 Kmn Knm with b = sigma^-2 Kmn Y riding
+// along as extra rows (Kmn streamed in row chunks through the GPU, never held whole), S = L L^T
+// (b becomes L^{-1} b in place), and Kmm + jitter I built (unfactored) in dK.
+template <typename T>
+static void sparse_normal_eq(gprx_ctx* ctx, SparseNE<T>& st, const gprx_kernel_desc* desc, const void* Xh,
+                             const void* Yh, int64_t n, int d, int m, const void* Xmh, int64_t M, double sigma,
+                             double jitter) {
+    KCanon<T>& K = st.K;
     const std::string e = canonicalize<T>(*desc, K);
     GPRX_REQUIRE(e.empty(), GPRX_ERR_ARG, e);
     GPRX_REQUIRE(M > 0 && d > 0 && m > 0 && n >= 0, GPRX_ERR_DIM, "gprx_sparse_fit: bad dimensions");
@@ -1425,10 +1439,16 @@ static gprx_status sparse_fit_impl(gprx_ctx* ctx, const gprx_kernel_desc* desc, 
     GPRX_HIP(hipSetDevice(ctx->device));
     hipStream_t s = ctx->stream;
     const int64_t Mp = round_up(M, DB), mp = round_up(m, GT), ld = Mp + mp;
+    st.Mp = Mp;
+    st.mp = mp;
+    st.ld = ld;
     int64_t cmax = 32768;  // dense rows per streamed block (GPRX_SPARSE_CHUNK overrides, for tests)
     if (const char* ev = std::getenv("GPRX_SPARSE_CHUNK")) cmax = std::max<int64_t>(64, round_up(std::atoll(ev), 64));
     const int64_t chunk = std::max<int64_t>(BT, std::min<int64_t>(round_up(std::max<int64_t>(n, 1), 64), cmax));
-    DevBuf dXm, dtm, dX, dtx, dY, dS, dA, dK, dLinv, dLinvK, dinfo, dflag, dz, dalpha, dV, dC, dFU, dFV, dKd;
+    DevBuf &dXm = st.dXm, &dtm = st.dtm, &dX = st.dX, &dtx = st.dtx, &dY = st.dY, &dS = st.dS, &dA = st.dA,
+           &dK = st.dK, &dLinv = st.dLinv, &dinfo = st.dinfo, &dflag = st.dflag, &dFU = st.dFU, &dFV = st.dFV,
+           &dKd = st.dKd;
+    st.chunk = chunk;
     upload<T>(dXm, Xmh, sizeof(T) * M * d, s);
     upload<T>(dX, Xh, sizeof(T) * std::max<int64_t>(n, 1) * d, s);
     upload<T>(dY, Yh, sizeof(T) * std::max<int64_t>(n, 1) * m, s);
@@ -1436,6 +1456,8 @@ static gprx_status sparse_fit_impl(gprx_ctx* ctx, const gprx_kernel_desc* desc, 
     // the inducing points once, of each dense chunk per chunk, both centred on Xm's first row
     const bool mma = pairs_mma_supported<T>(K, 1);
     const int64_t chunk128 = round_up(chunk, GT);
+    st.mma = mma;
+    st.chunk128 = chunk128;
     dflag.ensure(sizeof(int));
     GPRX_HIP(hipMemsetAsync(dflag.p, 0, sizeof(int), s));
     if (mma) {
@@ -1481,6 +1503,7 @@ static gprx_status sparse_fit_impl(gprx_ctx* ctx, const gprx_kernel_desc* desc, 
     const int64_t acols = chunk + 16 * 16;  // slack: the P <= 16 split-K slices may overhang ncp (zeros)
     dA.ensure(sizeof(T) * ld * acols);
     const T is2 = T(1) / (T(sigma) * T(sigma));  // inverse_sigma2 in T (:285)
+    st.is2 = is2;
     DevBuf dKY;
     if (fused) dKY.ensure(sizeof(T) * (chunk128 / GT) * Mp);
     for (int64_t off = 0; off < n; off += chunk) {
@@ -1536,6 +1559,33 @@ static gprx_status sparse_fit_impl(gprx_ctx* ctx, const gprx_kernel_desc* desc, 
     if (hinfo != INT_MAX)
         throw Error{GPRX_ERR_NOT_SPD, "gprx_sparse_fit: K + sigma^-2 Knm^T Knm is not positive definite (pivot " +
                                           std::to_string(hinfo) + ")"};
+}
+
+// Kmm + jitter I = L L^T in place (dK, ld Mp); Linv blocks into dLinvK.
+template <typename T>
+static void sparse_factor_kmm(gprx_ctx* ctx, SparseNE<T>& st) {
+    hipStream_t s = ctx->stream;
+    const int64_t Mp = st.Mp;
+    int hinfo = 0;
+    st.dLinvK.ensure(sizeof(T) * Mp * DB);
+    GPRX_HIP(hipMemsetD32Async((hipDeviceptr_t)st.dinfo.p, INT_MAX, 1, s));
+    potrf_auto<T>(st.dK.template as<T>(), Mp, Mp, Mp, st.dLinvK.template as<T>(), st.dinfo.template as<int>(), ctx->ex);
+    download(&hinfo, st.dinfo.p, sizeof(int), s);
+    check_sched(hinfo);
+    if (hinfo != INT_MAX)
+        throw Error{GPRX_ERR_NOT_SPD,
+                    "gprx_sparse_fit: Kmm + jitter I is not positive definite (pivot " + std::to_string(hinfo) + ")"};
+}
+
+template <typename T>
+static gprx_status sparse_fit_impl(gprx_ctx* ctx, const gprx_kernel_desc* desc, const void* Xh, const void* Yh,
+                                   int64_t n, int d, int m, const void* Xmh, int64_t M, double sigma, double jitter,
+                                   void* Kinv, void* RV, void* RM) {
+    SparseNE<T> st;
+    sparse_normal_eq<T>(ctx, st, desc, Xh, Yh, n, d, m, Xmh, M, sigma, jitter);
+    hipStream_t s = ctx->stream;
+    const int64_t Mp = st.Mp, ld = st.ld;
+    DevBuf &dS = st.dS, &dK = st.dK, &dLinv = st.dLinv, &dz = st.dz, &dalpha = st.dalpha, &dV = st.dV, &dC = st.dC;
     if (RV) {
         dz.ensure(sizeof(T) * m * Mp);
         dalpha.ensure(sizeof(T) * Mp * m);
@@ -1550,16 +1600,202 @@ static gprx_status sparse_fit_impl(gprx_ctx* ctx, const gprx_kernel_desc* desc, 
     }
     // ---- Kinv ------------------------------------------------------------------------------
     if (Kinv) {
-        dLinvK.ensure(sizeof(T) * Mp * DB);
-        GPRX_HIP(hipMemsetD32Async((hipDeviceptr_t)dinfo.p, INT_MAX, 1, s));
-        potrf_auto<T>(dK.as<T>(), Mp, Mp, Mp, dLinvK.as<T>(), dinfo.as<int>(), ctx->ex);
-        download(&hinfo, dinfo.p, sizeof(int), s);
-        check_sched(hinfo);
-    if (hinfo != INT_MAX)
-            throw Error{GPRX_ERR_NOT_SPD, "gprx_sparse_fit: Kmm + jitter I is not positive definite (pivot " +
-                                              std::to_string(hinfo) + ")"};
-        launch_spd_inverse_from_factor<T>(dK.as<T>(), Mp, Mp, dLinvK.as<T>(), dV.as<T>(), dC.as<T>(), s);
+        sparse_factor_kmm<T>(ctx, st);
+        launch_spd_inverse_from_factor<T>(dK.as<T>(), Mp, Mp, st.dLinvK.template as<T>(), dV.as<T>(), dC.as<T>(), s);
         download_sym<T>(Kinv, dC, Mp, M, s);
+    }
+    return GPRX_OK;
+}
+
+// SparseGaussianLogLikelihood::GetValueAndParameterDerivatives (include/SparseLikelihood.h:
+// 231-344) without the reference's N x N matrices.  With B = Kmm + jitter I +
+// sigma^-2 Kmn Knm (the fit's S), Sigma = B^{-1}, u = sigma^-2 Sigma Kmn y (= RV) and
+// Woodbury on C = sigma^2 I + Knm Kmm^{-1} Kmn:
+//   y^T C^{-1} y = sigma^-2 y^T y - |L_B^{-1} b|^2                 (b = sigma^-2 Kmn y)
+//   log|C|       = N log sigma^2 + log|B| - log|Kmm + jitter I|    (EfficientDeterminant, :132-145)
+// and the derivative of C, A_p = D_p W^T + W D_p^T - W E_p W^T (W = Knm Kmm^{-1}, D_p = dKnm/dp,
+// E_p = dKmm/dp, :246-252), collapses to
+//   grad_p = sum_{i,a} D_p,ia Omega_ia + 1/2 sum_{a,b} E_p,ab (Kmm^{-1} - Sigma - u u^T)_ab,
+//   Omega  = sigma^-2 [(y - Knm u) u^T - Knm Sigma]     (the data-fit and complexity terms, :255-273)
+// so the N x M part needs one GEMM Knm Sigma per row chunk (2 N M^2 flops) and a weighted
+// derivative sum over the chunk's pairs; the M x M part is the dense LML's gradient pass on the
+// inducing points.  Rows shard over an RCCL context like the fit (one all-reduce of the
+// partials).  compat: the reference's long-double product det(Kmm^{-1}) * sigma^{2N} * det(B)
+// and its clamps (:148-158, 305-314), evaluated from the three log-determinants.
+template <typename T>
+static gprx_status sparse_lml_impl(gprx_ctx* ctx, const gprx_kernel_desc* desc, const void* Xh, const void* Yh,
+                                   int64_t n, int d, int m, const void* Xmh, int64_t M, double sigma, double jitter,
+                                   uint32_t flags, double* value, double* grad, int32_t* nparams, double* logdet) {
+    GPRX_REQUIRE(M > 0, GPRX_ERR_DIM,
+                 "SparseLikelihood::GetValueAndParameterDerivative: there are no inducing samples specified");
+    GPRX_REQUIRE(m == 1, GPRX_ERR_DIM,
+                 "SparseGaussianLogLikelihood: only one output dimension is supported (the reference's data-fit term "
+                 "is m x m, include/SparseLikelihood.h:303)");
+    GPRX_REQUIRE(n > 0, GPRX_ERR_DIM, "SparseGaussianProcess::ComputeCoreMatrices: empty sample set.");
+    SparseNE<T> st;
+    sparse_normal_eq<T>(ctx, st, desc, Xh, Yh, n, d, m, Xmh, M, sigma, jitter);
+    sparse_factor_kmm<T>(ctx, st);
+    hipStream_t s = ctx->stream;
+    const KCanon<T>& K = st.K;
+    const int64_t Mp = st.Mp, ld = st.ld, chunk = st.chunk, c128 = st.chunk128;
+    const T is2 = st.is2;
+    // [0] log|B|, [1] |L_B^{-1} b|^2, [2] log|Kmm + jitter|, [4] y^T y, partials after
+    DevBuf red;
+    red.ensure(sizeof(double) * (8 + 2 * (Mp / 128 + 2)));
+    double* dred = red.as<double>();
+    launch_fit_reductions<T>(st.dS.template as<T>(), ld, M, Mp, 1, dred + 8, s);
+    GPRX_HIP(hipMemcpyAsync(dred, dred + 8, 2 * sizeof(double), hipMemcpyDeviceToDevice, s));
+    launch_fit_reductions<T>(st.dK.template as<T>(), Mp, M, Mp, 0, dred + 8, s);
+    GPRX_HIP(hipMemcpyAsync(dred + 2, dred + 8, sizeof(double), hipMemcpyDeviceToDevice, s));
+    launch_sq_sum<T>(st.dY.template as<T>(), n, dred + 4, s);
+    double h[5];
+    download(h, dred, sizeof(h), s);
+    double yty = h[4], nn = (double)n;
+    const bool want_grad = grad && (flags & GPRX_LML_GRAD);
+    double acc_x[MAX_LEAF * 3] = {0}, acc_m[MAX_LEAF * 3] = {0};
+    if (want_grad) {
+        // u = Sigma b (the fit's RV), Sigma (full symmetric), H = Kmm^{-1} - Sigma (lower)
+        st.dz.ensure(sizeof(T) * Mp);
+        st.dalpha.ensure(sizeof(T) * Mp);
+        launch_backsolve<T>(st.dS.template as<T>(), ld, Mp, 1, st.dLinv.template as<T>(), st.dz.template as<T>(), st.dalpha.template as<T>(), s);
+        const T* u = st.dalpha.template as<T>();
+        DevBuf dSig, dH;
+        st.dV.ensure(sizeof(T) * Mp * Mp);
+        dSig.ensure(sizeof(T) * Mp * Mp);
+        dH.ensure(sizeof(T) * Mp * Mp);
+        launch_spd_inverse_from_factor<T>(st.dS.template as<T>(), ld, Mp, st.dLinv.template as<T>(), st.dV.template as<T>(), dSig.as<T>(), s);
+        launch_sym_fill<T>(dSig.as<T>(), Mp, Mp, s);
+        launch_spd_inverse_from_factor<T>(st.dK.template as<T>(), Mp, Mp, st.dLinvK.template as<T>(), st.dV.template as<T>(), dH.as<T>(), s);
+        launch_sub<T>(dH.as<T>(), dSig.as<T>(), dH.as<T>(), Mp * Mp, s);
+        // ---- N x M part, chunk by chunk: A_t = K(Xc, Xm), r = sigma^-2 (y_c - A_t u),
+        // G = sigma^-2 A_t Sigma, then sum (r_i u_a - G_ia) dk(x_i, xm_a)/dp ----
+        const bool gmma = st.mma && pairs_grad_supported<T>(K);
+        DevBuf dAt, dG, dr, dFUc, dFVm, dGU, dGV, part, acc;
+        dAt.ensure(sizeof(T) * c128 * Mp);
+        dG.ensure(sizeof(T) * c128 * Mp);
+        dr.ensure(sizeof(T) * c128);
+        acc.ensure(sizeof(double) * MAX_LEAF * 3);
+        const int64_t fc = pairs_feature_cols<T>(K, d), kg = std::max<int64_t>(1, pairs_grad_feature_cols<T>(K, d));
+        if (st.mma) {
+            dFUc.ensure(sizeof(T) * c128 * fc);
+            dFVm.ensure(sizeof(T) * Mp * fc);
+            launch_pair_features<T>(K, st.dXm.template as<T>(), M, d, st.dXm.template as<T>(), true, dFVm.as<T>(), Mp, s,
+                                    st.dflag.template as<int>());
+        }
+        if (gmma) {
+            dGU.ensure(sizeof(T) * c128 * kg);
+            dGV.ensure(sizeof(T) * Mp * kg);
+            part.ensure(sizeof(double) * MAX_LEAF * 3 * (c128 / GT) * (Mp / GT));
+        } else {
+            GPRX_HIP(hipMemsetAsync(acc.p, 0, sizeof(double) * MAX_LEAF * 3, s));
+        }
+        for (int64_t off = 0; off < n; off += chunk) {
+            const int64_t nc = std::min(chunk, n - off), nc128 = round_up(nc, GT);
+            const T* Xc = st.dX.template as<T>() + off * d;
+            if (nc < chunk || off == 0) GPRX_HIP(hipMemsetAsync(dAt.p, 0, sizeof(T) * c128 * Mp, s));
+            const T* tabc = nullptr;
+            if (st.mma) {
+                launch_pair_features<T>(K, Xc, nc, d, st.dXm.template as<T>(), false, dFUc.as<T>(), nc128, s,
+                                        st.dflag.template as<int>());
+                launch_kcross_mma<T>(K, st.dKd.template as<KCanon<T>>(), dFUc.as<T>(), nc128, nc, dFVm.as<T>(), Mp, M, d,
+                                     dAt.as<T>(), c128, st.dflag.template as<int>(), s, nullptr, nullptr);
+            } else {
+                if (K.nper > 0) {
+                    launch_sincos_tables<T>(K, Xc, nc, d, st.dtx.template as<T>(), s);
+                    tabc = st.dtx.template as<T>();
+                }
+                launch_kbuild<T>(K, Xc, tabc, nc, st.dXm.template as<T>(), st.dtm.template as<T>(), M, d, dAt.as<T>(), c128, 0, false,
+                                 T(0), st.dflag.template as<int>(), s);
+            }
+            launch_sparse_resid<T>(dAt.as<T>(), c128, nc, M, u, st.dY.template as<T>() + off, is2, dr.as<T>(), s);
+            launch_gemm_nt<T>(dG.as<T>(), c128, dAt.as<T>(), c128, dSig.as<T>(), Mp, nc128, Mp, Mp, is2, T(0), false,
+                              s);
+            if (gmma) {
+                launch_lml_grad_mma_cross<T>(K, st.dKd.template as<KCanon<T>>(), Xc, nc, st.dXm.template as<T>(), M, st.dXm.template as<T>(), d,
+                                             dFUc.as<T>(), nc128, dFVm.as<T>(), Mp, dGU.as<T>(), dGV.as<T>(), dr.as<T>(),
+                                             u, dG.as<T>(), c128, part.as<double>(), acc.as<double>(), s);
+                double a[MAX_LEAF * 3];
+                download(a, acc.p, sizeof(a), s);
+                for (int q = 0; q < MAX_LEAF * 3; q++) acc_x[q] += a[q];  // chunk order: deterministic
+            } else {
+                launch_lml_grad_cross<T>(K, Xc, tabc, nc, st.dXm.template as<T>(), st.dtm.template as<T>(), M, d, dr.as<T>(), u,
+                                         dG.as<T>(), c128, acc.as<double>(), s);
+            }
+        }
+        if (!gmma) download(acc_x, acc.p, sizeof(acc_x), s);
+        // ---- M x M part: sum (u_a u_b - H_ab) dKmm_ab/dp (the dense LML's pass, weights
+        // alpha alpha^T - C with alpha = u, C = H) ----
+        const int64_t ntm = Mp / GT;
+        if (gmma) {
+            DevBuf dFUm, dFVm2, dGUm, dGVm, partm;
+            dFUm.ensure(sizeof(T) * Mp * fc);
+            dFVm2.ensure(sizeof(T) * Mp * fc);
+            dGUm.ensure(sizeof(T) * Mp * kg);
+            dGVm.ensure(sizeof(T) * Mp * kg);
+            partm.ensure(sizeof(double) * MAX_LEAF * 3 * ntm * (ntm + 1) / 2);
+            launch_pair_features<T>(K, st.dXm.template as<T>(), M, d, st.dXm.template as<T>(), false, dFUm.as<T>(), Mp, s);
+            launch_pair_features<T>(K, st.dXm.template as<T>(), M, d, st.dXm.template as<T>(), true, dFVm2.as<T>(), Mp, s);
+            launch_lml_grad_mma<T>(K, st.dKd.template as<KCanon<T>>(), st.dXm.template as<T>(), M, d, dFUm.as<T>(), dFVm2.as<T>(),
+                                   dGUm.as<T>(), dGVm.as<T>(), Mp, u, dH.as<T>(), Mp, partm.as<double>(),
+                                   acc.as<double>(), s);
+        } else {
+            GPRX_HIP(hipMemsetAsync(acc.p, 0, sizeof(double) * MAX_LEAF * 3, s));
+            launch_lml_grad<T>(K, st.dXm.template as<T>(), st.dtm.template as<T>(), M, d, u, dH.as<T>(), Mp, acc.as<double>(), s);
+        }
+        download(acc_m, acc.p, sizeof(acc_m), s);
+    }
+    int hflag = 0;
+    download(&hflag, st.dflag.p, sizeof(int), s);
+    if (hflag)
+        throw Error{GPRX_ERR_NONFINITE,
+                    "GaussianProcess::ComputeKernelMatrixInternal: kernel matrix contains entries which are not finite."};
+    if (ctx->comm) {  // rows sharded over the ranks: the data terms and the N x M gradient partials
+        // (the M x M part is the same on every rank: added once, after the reduction)
+        double loc[MAX_LEAF * 3 + 2];
+        for (int q = 0; q < MAX_LEAF * 3; q++) loc[q] = acc_x[q];
+        loc[MAX_LEAF * 3] = yty;
+        loc[MAX_LEAF * 3 + 1] = nn;
+        DevBuf dl;
+        upload<double>(dl, loc, sizeof(loc), s);
+        const ncclResult_t r = ncclAllReduce(dl.p, dl.p, MAX_LEAF * 3 + 2, ncclFloat64, ncclSum, ctx->comm, s);
+        if (r != ncclSuccess) throw Error{GPRX_ERR_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(r)};
+        download(loc, dl.p, sizeof(loc), s);
+        for (int q = 0; q < MAX_LEAF * 3; q++) acc_x[q] = loc[q];
+        yty = loc[MAX_LEAF * 3];
+        nn = loc[MAX_LEAF * 3 + 1];
+    }
+    for (int q = 0; q < MAX_LEAF * 3; q++) acc_x[q] -= 0.5 * acc_m[q];  // replicated M x M part, once
+    const double logdet_b = h[0], zz = h[1], logdet_k = h[2];
+    const T s2 = T(sigma) * T(sigma);
+    const double ld_c = nn * std::log((double)s2) + logdet_b - logdet_k;
+    const T df = (T)(-0.5 * ((double)is2 * yty - zz));
+    const T ct = (T)(-(nn / 2.0) * std::log(2 * M_PI));  // include/SparseLikelihood.h:198 (N dense samples)
+    double v;
+    if (flags & GPRX_LML_COMPAT) {
+        typedef long double HP;
+        HP det_b = std::exp(-(HP)logdet_k);  // det(Kmm^{-1}) (:138-141, inf clamped to max)
+        if (std::isinf(det_b)) det_b = std::numeric_limits<HP>::max();
+        const HP prod_a = std::exp((HP)nn * std::log((HP)s2));  // prod of the N noise entries
+        const HP det = det_b * prod_a * std::exp((HP)logdet_b);
+        HP cp;
+        if (det <= std::numeric_limits<HP>::min() || std::isnan(det)) cp = -0.5L * std::log(std::numeric_limits<HP>::min());
+        else if (det > std::numeric_limits<HP>::max()) cp = -0.5L * std::log(std::numeric_limits<HP>::max());
+        else cp = -0.5L * std::log(det);
+        v = (double)(T)(df + (T)(cp + (HP)ct));
+    } else {
+        v = (double)df - 0.5 * ld_c + (double)ct;
+    }
+    if (std::isnan(v))
+        throw Error{GPRX_ERR_NONFINITE, "SparseLikelihood::GetValueAndParameterDerivative: likelihood value is not a number."};
+    if (value) *value = v;
+    if (logdet) *logdet = ld_c;
+    if (nparams) *nparams = K.nparams;
+    if (want_grad) {
+        for (int l = 0; l < K.nleaf; l++) {
+            const int t = K.leaf[l].type;
+            const int npl = (t == L_WHITE) ? 1 : ((t == L_GAUSS || t == L_GAUSS_EXP) ? 2 : 3);
+            for (int q = 0; q < npl; q++) grad[K.param_base[l] + q] = acc_x[l * 3 + q];
+        }
     }
     return GPRX_OK;
 }
@@ -2104,6 +2340,23 @@ gprx_status gprx_sparse_fit(gprx_ctx* ctx, gprx_dtype dtype, const gprx_kernel_d
     ProfBind pb_(ctx);  // after the lock: resolved (streams drained) before it is released
     return dtype == GPRX_F64 ? sparse_fit_impl<double>(ctx, kernel, X, Y, n, d, m, Xm, M, sigma, jitter, Kinv, RV, RM)
                              : sparse_fit_impl<float>(ctx, kernel, X, Y, n, d, m, Xm, M, sigma, jitter, Kinv, RV, RM);
+    API_END(ctx)
+}
+
+gprx_status gprx_sparse_lml(gprx_ctx* ctx, gprx_dtype dtype, const gprx_kernel_desc* kernel, const void* X,
+                            const void* Y, int64_t n, int32_t d, int32_t m, const void* Xm, int64_t M, double sigma,
+                            double jitter, uint32_t flags, double* value, double* grad, int32_t* nparams,
+                            double* logdet) {
+    API_BEGIN
+    GPRX_REQUIRE(M > 0, GPRX_ERR_DIM,
+                 "SparseLikelihood::GetValueAndParameterDerivative: there are no inducing samples specified");
+    GPRX_REQUIRE(ctx && kernel && Xm && X && Y, GPRX_ERR_ARG, "gprx_sparse_lml: NULL argument");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ProfBind pb_(ctx);
+    return dtype == GPRX_F64 ? sparse_lml_impl<double>(ctx, kernel, X, Y, n, d, m, Xm, M, sigma, jitter, flags, value,
+                                                       grad, nparams, logdet)
+                             : sparse_lml_impl<float>(ctx, kernel, X, Y, n, d, m, Xm, M, sigma, jitter, flags, value,
+                                                      grad, nparams, logdet);
     API_END(ctx)
 }
 

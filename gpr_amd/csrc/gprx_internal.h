@@ -427,6 +427,29 @@ template <typename T>
 void launch_lml_grad_mma(const KCanon<T>& K, const KCanon<T>* Kd, const T* X, int64_t n, int d, const T* FU,
                          const T* FV, T* GU, T* GV, int64_t nf, const T* alpha, const T* C, int64_t ldc, double* part,
                          double* acc, hipStream_t s, int og = 1, int orank = 0, int ogb = 1);  // og > 1: rank orank's rows
+// Rectangular form for the sparse likelihood (k_pairs.hip): acc[3 l + q] = sum over the
+// na x nb pairs (xa_i, xb_j) of (a_i b_j - C_ij) d leaf_l / d p_q.
+template <typename T>
+void launch_lml_grad_mma_cross(const KCanon<T>& K, const KCanon<T>* Kd, const T* Xa, int64_t na, const T* Xb,
+                               int64_t nb, const T* center, int d, const T* FU, int64_t nfu, const T* FV, int64_t nfv,
+                               T* GU, T* GV, const T* a, const T* b, const T* C, int64_t ldc, double* part, double* acc,
+                               hipStream_t s);
+// VALU form of the same sum for every tree (k_lml.hip); acc is accumulated into (atomics).
+template <typename T>
+void launch_lml_grad_cross(const KCanon<T>& K, const T* Xa, const T* tabA, int64_t na, const T* Xb, const T* tabB,
+                           int64_t nb, int d, const T* a, const T* b, const T* C, int64_t ldc, double* acc,
+                           hipStream_t s);
+// Sparse likelihood helpers (k_sparse.hip).
+// out[i] = alpha (y[i] - sum_j A[i + j lda] u[j]) for i < n (rows of K(Xc, Xm) u)
+template <typename T>
+void launch_sparse_resid(const T* A, int64_t lda, int64_t n, int64_t M, const T* u, const T* y, T alpha, T* out,
+                         hipStream_t s);
+// out[0] = sum_i y[i]^2 (fixed order, double)
+template <typename T>
+void launch_sq_sum(const T* y, int64_t n, double* out, hipStream_t s);
+// Z = X - Y elementwise (e entries)
+template <typename T>
+void launch_sub(const T* X, const T* Y, T* Z, int64_t e, hipStream_t s);
 // The BUILD description of K(X, X) + sigma2 I from the features of launch_pair_features
 // (k_pairs.hip; the same trees as launch_kbuild_mma).
 template <typename T>

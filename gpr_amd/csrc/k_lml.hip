@@ -124,13 +124,25 @@ struct GradSmem {
     double red[256];
 };
 
-template <typename T, int NPER>
+// CROSS: rows from X (n), columns from Xb (nb), every tile (ntr row tiles), weights
+// alpha_i beta_j - C_ij without doubling (the sparse likelihood, include/SparseLikelihood.h:317-340).
+template <typename T, int NPER, bool CROSS = false>
 __global__ __launch_bounds__(256) void lml_grad_kernel(KCanon<T> K, const T* __restrict__ X, const T* __restrict__ tab,
                                                        int64_t n, int d, const T* __restrict__ alpha,
-                                                       const T* __restrict__ C, int64_t ldc, double* __restrict__ gout) {
+                                                       const T* __restrict__ C, int64_t ldc, double* __restrict__ gout,
+                                                       const T* __restrict__ Xb = nullptr,
+                                                       const T* __restrict__ tabB = nullptr, int64_t nb = 0,
+                                                       const T* __restrict__ beta = nullptr, int64_t ntr = 1) {
     __shared__ __attribute__((aligned(16))) GradSmem<T, NPER> sm;
+    const T* __restrict__ Xc = CROSS ? Xb : X;
+    const T* __restrict__ tc = CROSS ? tabB : tab;
+    const T* __restrict__ bv = CROSS ? beta : alpha;
+    const int64_t ncol = CROSS ? nb : n;
     int64_t ti, tj;
-    {
+    if (CROSS) {
+        ti = blockIdx.x % ntr;
+        tj = blockIdx.x / ntr;
+    } else {
         const int64_t b = blockIdx.x;
         int64_t i = (int64_t)((sqrt(8.0 * (double)b + 1.0) - 1.0) * 0.5);
         while ((i + 1) * (i + 2) / 2 <= b) i++;
@@ -149,14 +161,15 @@ __global__ __launch_bounds__(256) void lml_grad_kernel(KCanon<T> K, const T* __r
         for (int b = 0; b < 4; b++) r2[a][b] = s0[a][b] = s1[a][b] = f0[a][b] = f1[a][b] = T(0);
     const int64_t nd = n * (int64_t)d;
     for (int k0 = 0; k0 < d; k0 += DC) {
+        const int64_t ndc = ncol * (int64_t)d;
         stage_chunk<T>(sm.xa, X, i0, n, d, k0);
-        stage_chunk<T>(sm.xb, X, j0, n, d, k0);
+        stage_chunk<T>(sm.xb, Xc, j0, ncol, d, k0);
 #pragma unroll
         for (int p = 0; p < NPER; p++) {
             stage_chunk<T>(sm.per[4 * p + 0], tab + (2 * p) * nd, i0, n, d, k0);
             stage_chunk<T>(sm.per[4 * p + 1], tab + (2 * p + 1) * nd, i0, n, d, k0);
-            stage_chunk<T>(sm.per[4 * p + 2], tab + (2 * p) * nd, j0, n, d, k0);
-            stage_chunk<T>(sm.per[4 * p + 3], tab + (2 * p + 1) * nd, j0, n, d, k0);
+            stage_chunk<T>(sm.per[4 * p + 2], tc + (2 * p) * ndc, j0, ncol, d, k0);
+            stage_chunk<T>(sm.per[4 * p + 3], tc + (2 * p + 1) * ndc, j0, ncol, d, k0);
         }
         __syncthreads();
         const int kmax = min(DC, d - k0);
@@ -216,8 +229,8 @@ __global__ __launch_bounds__(256) void lml_grad_kernel(KCanon<T> K, const T* __r
 #pragma unroll
         for (int b = 0; b < 4; b++) {
             const int64_t gj = j0 + ty * 4 + b;
-            if (gi >= n || gj >= n || gi < gj) continue;
-            const T w = (alpha[gi] * alpha[gj] - C[gi + gj * ldc]) * (gi == gj ? T(1) : T(2));
+            if (gi >= n || gj >= ncol || (!CROSS && gi < gj)) continue;
+            const T w = (alpha[gi] * bv[gj] - C[gi + gj * ldc]) * ((CROSS || gi == gj) ? T(1) : T(2));
             T lv[MAX_LEAF];
 #pragma unroll
             for (int l = 0; l < MAX_LEAF; l++)
@@ -266,14 +279,40 @@ void launch_lml_grad(const KCanon<T>& K, const T* X, const T* tab, int64_t n, in
     const unsigned grid = (unsigned)(nt * (nt + 1) / 2);
     ProfScope ps(KC_LML_GRAD, s, 0.0, (double)sizeof(T) * ((double)n * (n + 1) / 2 + (double)n * d));
     if (K.nper == 0)
-        hipLaunchKernelGGL((lml_grad_kernel<T, 0>), dim3(grid), dim3(256), 0, s, K, X, tab, n, d, alpha, C, ldc, acc);
+        hipLaunchKernelGGL((lml_grad_kernel<T, 0>), dim3(grid), dim3(256), 0, s, K, X, tab, n, d, alpha, C, ldc, acc,
+                           X, tab, n, alpha, (int64_t)1);
     else if (K.nper == 1)
-        hipLaunchKernelGGL((lml_grad_kernel<T, 1>), dim3(grid), dim3(256), 0, s, K, X, tab, n, d, alpha, C, ldc, acc);
+        hipLaunchKernelGGL((lml_grad_kernel<T, 1>), dim3(grid), dim3(256), 0, s, K, X, tab, n, d, alpha, C, ldc, acc,
+                           X, tab, n, alpha, (int64_t)1);
     else
-        hipLaunchKernelGGL((lml_grad_kernel<T, 2>), dim3(grid), dim3(256), 0, s, K, X, tab, n, d, alpha, C, ldc, acc);
+        hipLaunchKernelGGL((lml_grad_kernel<T, 2>), dim3(grid), dim3(256), 0, s, K, X, tab, n, d, alpha, C, ldc, acc,
+                           X, tab, n, alpha, (int64_t)1);
+}
+
+template <typename T>
+void launch_lml_grad_cross(const KCanon<T>& K, const T* Xa, const T* tabA, int64_t na, const T* Xb, const T* tabB,
+                           int64_t nb, int d, const T* a, const T* b, const T* C, int64_t ldc, double* acc,
+                           hipStream_t s) {
+    const int64_t ntr = (na + BT - 1) / BT, ntc = (nb + BT - 1) / BT;
+    if (ntr * ntc == 0) return;
+    const unsigned grid = (unsigned)(ntr * ntc);
+    ProfScope ps(KC_LML_GRAD, s, 0.0, (double)sizeof(T) * ((double)na * nb + (double)(na + nb) * d));
+    if (K.nper == 0)
+        hipLaunchKernelGGL((lml_grad_kernel<T, 0, true>), dim3(grid), dim3(256), 0, s, K, Xa, tabA, na, d, a, C, ldc,
+                           acc, Xb, tabB, nb, b, ntr);
+    else if (K.nper == 1)
+        hipLaunchKernelGGL((lml_grad_kernel<T, 1, true>), dim3(grid), dim3(256), 0, s, K, Xa, tabA, na, d, a, C, ldc,
+                           acc, Xb, tabB, nb, b, ntr);
+    else
+        hipLaunchKernelGGL((lml_grad_kernel<T, 2, true>), dim3(grid), dim3(256), 0, s, K, Xa, tabA, na, d, a, C, ldc,
+                           acc, Xb, tabB, nb, b, ntr);
+    GPRX_HIP(hipGetLastError());
 }
 
 #define GPRX_INST(T)                                                                                            \
+    template void launch_lml_grad_cross<T>(const KCanon<T>&, const T*, const T*, int64_t, const T*, const T*,  \
+                                           int64_t, int, const T*, const T*, const T*, int64_t, double*,      \
+                                           hipStream_t);                                                       \
     template void launch_set_identity_pad<T>(T*, int64_t, int64_t, int64_t, hipStream_t);                      \
     template void launch_gemm_add_lower<T>(T*, int64_t, const T*, int64_t, int64_t, hipStream_t);              \
     template void launch_sym_fill<T>(T*, int64_t, int64_t, hipStream_t);                                       \

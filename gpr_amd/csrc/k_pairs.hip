@@ -254,19 +254,26 @@ __global__ void grad_features_kernel(const T* __restrict__ X, int64_t n, int d, 
 // accumulator set: r2 (its leaves' derivatives summed at once), then S, where the periodic
 // leaf's w e and w e S are summed and w e is kept in place of S, then F (sum of w e F).
 // At most one periodic leaf (pairs_grad_supported).
-template <typename T, int NPER, bool R2>
+// CROSS: every tile of a rectangular pair block (rows: the U features, nf rows, nrow live;
+// columns: the V features, nfv rows, ncol live) with weights w_ij = alpha_i beta_j - C_ij and
+// no diagonal (the sparse likelihood's sum over K(X, Xm), include/SparseLikelihood.h:317-340).
+template <typename T, int NPER, bool R2, bool CROSS = false>
 __global__ __launch_bounds__(NT) void grad_mma_kernel(const KCanon<T>* __restrict__ Kd, const T* __restrict__ FU,
                                                       const T* __restrict__ FV, const T* __restrict__ GU,
                                                       const T* __restrict__ GV, int64_t nf, int Kr, int Kp, int Kf,
                                                       T hd, const T* __restrict__ alpha, const T* __restrict__ C,
                                                       int64_t ldc, int64_t n, double* __restrict__ part, int og,
-                                                      int orank, int ogb) {
+                                                      int orank, int ogb, int64_t nfv = 0, int64_t ncol = 0,
+                                                      const T* __restrict__ beta = nullptr) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     T* smem = reinterpret_cast<T*>(smem_raw);
     double* sacc = reinterpret_cast<double*>(smem_raw + gemm_lds<T>());  // [8 waves][MAX_LEAF * 3]
     typedef Mfma<T> Tr;
     int64_t ti, tj;
-    {
+    if (CROSS) {
+        ti = blockIdx.x % (nf / GT);
+        tj = blockIdx.x / (nf / GT);
+    } else {
         const int64_t b = blockIdx.x;
         int64_t i = (int64_t)((sqrt(8.0 * (double)b + 1.0) - 1.0) * 0.5);
         while ((i + 1) * (i + 2) / 2 <= b) i++;
@@ -274,9 +281,11 @@ __global__ __launch_bounds__(NT) void grad_mma_kernel(const KCanon<T>* __restric
         ti = i;
         tj = b - i * (i + 1) / 2;
     }
+    const int64_t nv_ = CROSS ? nfv : nf, ncol_ = CROSS ? ncol : n;
+    const T* __restrict__ bvec = CROSS ? beta : alpha;
     // a distributed context's share: only the tiles of row blocks rank `orank` owns (row block
     // i on rank (i / ogb) mod og, gprx_dist.cpp); the others contribute zero
-    if (og > 1 && (ti / ogb) % og != orank) {
+    if (!CROSS && og > 1 && (ti / ogb) % og != orank) {
         if (threadIdx.x < MAX_LEAF * 3) part[(int64_t)blockIdx.x * MAX_LEAF * 3 + threadIdx.x] = 0.0;
         return;
     }
@@ -308,10 +317,10 @@ __global__ __launch_bounds__(NT) void grad_mma_kernel(const KCanon<T>* __restric
 #pragma unroll
             for (int y = 0; y < 4; y++) {
                 const int64_t gi = gi_of(y);
-                const bool in = gi < n && gj < n && gi >= gj;
+                const bool in = gi < n && gj < ncol_ && (CROSS || gi >= gj);
                 const int64_t ci = in ? gi : 0, cj = in ? gj : 0;
-                const T v = alpha[ci] * alpha[cj] - C[ci + cj * ldc];
-                wt[x][y][reg] = in ? v * (gi == gj ? T(1) : T(2)) : T(0);
+                const T v = alpha[ci] * bvec[cj] - C[ci + cj * ldc];
+                wt[x][y][reg] = in ? (CROSS ? v : v * (gi == gj ? T(1) : T(2))) : T(0);
             }
         });
     };
@@ -329,7 +338,7 @@ __global__ __launch_bounds__(NT) void grad_mma_kernel(const KCanon<T>* __restric
     __syncthreads();
     typename Tr::acc_t ar[2][4];
     if (R2) {
-        tile_mma<T>(ar, FU + i0, nf, FV + j0, nf, Kr, Kr, smem, t);
+        tile_mma<T>(ar, FU + i0, nf, FV + j0, nv_, Kr, Kr, smem, t);
         load_weights();
         T nu[4];
 #pragma unroll
@@ -337,10 +346,10 @@ __global__ __launch_bounds__(NT) void grad_mma_kernel(const KCanon<T>* __restric
         each([&](auto cc) {
             constexpr int x = decltype(cc)::value >> 2, reg = decltype(cc)::value & 3;
             const int64_t gj = gj_of(x, reg);
-            const T nv = FV[(int64_t)(Kr + Kp) * nf + gj];
+            const T nv = FV[(int64_t)(Kr + Kp) * nv_ + gj];
 #pragma unroll
             for (int y = 0; y < 4; y++)
-                ar[x][y][reg] = gi_of(y) == gj ? T(0) : clamp0(nu[y] + nv + ar[x][y][reg]);
+                ar[x][y][reg] = (!CROSS && gi_of(y) == gj) ? T(0) : clamp0(nu[y] + nv + ar[x][y][reg]);
         });
         // one element loop per leaf type, with the leaf's constants hoisted (the formulas of
         // leaf_grad, gprx_internal.h, rearranged: one exp per pair, no per-pair division
@@ -400,7 +409,7 @@ __global__ __launch_bounds__(NT) void grad_mma_kernel(const KCanon<T>* __restric
         const KLeaf<T>& L = Kd->leaf[lp];
         const T sc = L.p[0], sig = L.p[2], c1 = L.c1;
         if (R2) __syncthreads();  // the staging ring is reused
-        tile_mma<T>(ar, FU + (int64_t)Kr * nf + i0, nf, FV + (int64_t)Kr * nf + j0, nf, Kp, Kp, smem, t);
+        tile_mma<T>(ar, FU + (int64_t)Kr * nf + i0, nf, FV + (int64_t)Kr * nv_ + j0, nv_, Kp, Kp, smem, t);
         load_weights();
         double a0 = 0, a2 = 0;
         each([&](auto cc) {
@@ -408,7 +417,7 @@ __global__ __launch_bounds__(NT) void grad_mma_kernel(const KCanon<T>* __restric
             const int64_t gj = gj_of(x, reg);
 #pragma unroll
             for (int y = 0; y < 4; y++) {
-                const T sp = gi_of(y) == gj ? T(0) : clamp0(fma(T(-0.5), ar[x][y][reg], hd));
+                const T sp = (!CROSS && gi_of(y) == gj) ? T(0) : clamp0(fma(T(-0.5), ar[x][y][reg], hd));
                 T we = wt[x][y][reg] * exp(c1 * sp);
                 // pinned here: sunk past the next product (to its use), S and the weights
                 // stayed live across it and spilled
@@ -420,13 +429,14 @@ __global__ __launch_bounds__(NT) void grad_mma_kernel(const KCanon<T>* __restric
         });
         __syncthreads();
         typename Tr::acc_t af[2][4];
-        tile_mma<T>(af, GU + i0, nf, GV + j0, nf, Kf, Kf, smem, t);
+        tile_mma<T>(af, GU + i0, nf, GV + j0, nv_, Kf, Kf, smem, t);
         double a1 = 0;
         each([&](auto cc) {
             constexpr int x = decltype(cc)::value >> 2, reg = decltype(cc)::value & 3;
             const int64_t gj = gj_of(x, reg);
 #pragma unroll
-            for (int y = 0; y < 4; y++) a1 += (double)(ar[x][y][reg] * (gi_of(y) == gj ? T(0) : af[x][y][reg]));
+            for (int y = 0; y < 4; y++)
+                a1 += (double)(ar[x][y][reg] * ((!CROSS && gi_of(y) == gj) ? T(0) : af[x][y][reg]));
         });
         // d/d(scale) = 2 sc e, d/db = -0.5 sc^2 e F / sigma^2, d/dsigma = sc^2 e S / sigma^3
         flush(lp, (double)(T(2) * sc) * a0, (double)(T(-0.5) * sc * sc / (sig * sig)) * a1,
@@ -583,11 +593,48 @@ void launch_lml_grad_mma(const KCanon<T>& K, const KCanon<T>* Kd, const T* X, in
     auto go = [&](auto kfn) {
         GPRX_HIP(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         hipLaunchKernelGGL(kfn, grid, dim3(mm::NT), lds, s, Kd, FU, FV, (const T*)GU, (const T*)GV, nf, Kr, Kp, Kf,
-                           T(0.5) * T(d), alpha, C, ldc, n, part, og, orank, ogb > 1 ? ogb : 1);
+                           T(0.5) * T(d), alpha, C, ldc, n, part, og, orank, ogb > 1 ? ogb : 1, nf, n, alpha);
     };
     if (K.nper && K.need_r2) go(pr::grad_mma_kernel<T, 1, true>);
     else if (K.nper) go(pr::grad_mma_kernel<T, 1, false>);
     else go(pr::grad_mma_kernel<T, 0, true>);
+    hipLaunchKernelGGL(pr::grad_reduce_kernel, dim3(MAX_LEAF * 3), dim3(256), 0, s, (const double*)part, ntiles, acc);
+    GPRX_HIP(hipGetLastError());
+}
+
+// Cross form: acc[3 l + q] = sum_{i < na, j < nb} (a_i b_j - C_ij) d leaf_l(xa_i, xb_j) / d p_q
+// (no doubling, no diagonal).  FU: left features of Xa (nfu rows), FV: right features of Xb
+// (nfv rows), both centred on `center`; GU, GV (nfu / nfv rows) are computed here.
+template <typename T>
+void launch_lml_grad_mma_cross(const KCanon<T>& K, const KCanon<T>* Kd, const T* Xa, int64_t na, const T* Xb,
+                               int64_t nb, const T* center, int d, const T* FU, int64_t nfu, const T* FV, int64_t nfv,
+                               T* GU, T* GV, const T* a, const T* b, const T* C, int64_t ldc, double* part, double* acc,
+                               hipStream_t s) {
+    GPRX_REQUIRE(nfu % GT == 0 && nfv % GT == 0 && na <= nfu && nb <= nfv && ldc >= nfu, GPRX_ERR_ARG,
+                 "launch_lml_grad_mma_cross: feature rows must be multiples of 128 covering the samples");
+    const int Kr = pr::kr_of(K, d), Kp = pr::kp_of(K, d), Kf = (int)pairs_grad_feature_cols(K, d);
+    if (K.nper) {
+        hipLaunchKernelGGL(pr::grad_features_kernel<T>, dim3((unsigned)((nfu + 255) / 256)), dim3(256), 0, s, Xa, na,
+                           d, center, K.b[0], 0, GU, nfu, Kf);
+        hipLaunchKernelGGL(pr::grad_features_kernel<T>, dim3((unsigned)((nfv + 255) / 256)), dim3(256), 0, s, Xb, nb,
+                           d, center, K.b[0], 1, GV, nfv, Kf);
+    }
+    const int64_t ntiles = (nfu / GT) * (nfv / GT);
+    if (ntiles == 0) {
+        GPRX_HIP(hipMemsetAsync(acc, 0, sizeof(double) * MAX_LEAF * 3, s));
+        return;
+    }
+    ProfScope ps(KC_LML_GRAD, s, 2.0 * (double)GT * GT * (Kr + Kp + Kf) * ntiles,
+                 (double)sizeof(T) * ((double)na * nb + (double)(na + nb) * d));
+    const size_t lds = mm::gemm_lds<T>() + sizeof(double) * 8 * MAX_LEAF * 3;
+    auto go = [&](auto kfn) {
+        GPRX_HIP(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        hipLaunchKernelGGL(kfn, dim3((unsigned)ntiles), dim3(mm::NT), lds, s, Kd, FU, FV, (const T*)GU, (const T*)GV,
+                           nfu, Kr, Kp, Kf, T(0.5) * T(d), a, C, ldc, na, part, 1, 0, 1, nfv, nb, b);
+    };
+    if (K.nper && K.need_r2) go(pr::grad_mma_kernel<T, 1, true, true>);
+    else if (K.nper) go(pr::grad_mma_kernel<T, 1, false, true>);
+    else go(pr::grad_mma_kernel<T, 0, true, true>);
     hipLaunchKernelGGL(pr::grad_reduce_kernel, dim3(MAX_LEAF * 3), dim3(256), 0, s, (const double*)part, ntiles, acc);
     GPRX_HIP(hipGetLastError());
 }
@@ -620,6 +667,10 @@ TileBuild<T> pairs_tile_build(const KCanon<T>& K, const KCanon<T>* Kd, const T* 
 #define GPRX_PAIRS_INST(T)                                                                                    \
     template bool pairs_grad_supported<T>(const KCanon<T>&);                                                  \
     template int64_t pairs_grad_feature_cols<T>(const KCanon<T>&, int);                                       \
+    template void launch_lml_grad_mma_cross<T>(const KCanon<T>&, const KCanon<T>*, const T*, int64_t, const T*,  \
+                                               int64_t, const T*, int, const T*, int64_t, const T*, int64_t, T*,  \
+                                               T*, const T*, const T*, const T*, int64_t, double*, double*,        \
+                                               hipStream_t);                                                      \
     template void launch_lml_grad_mma<T>(const KCanon<T>&, const KCanon<T>*, const T*, int64_t, int, const T*, \
                                          const T*, T*, T*, int64_t, const T*, const T*, int64_t, double*,     \
                                          double*, hipStream_t, int, int, int);                                \

@@ -43,7 +43,7 @@ EXPORTED = [
     "gprx_kernel_matrix", "gprx_cross_matrix", "gprx_deriv_matrix", "gprx_cholesky", "gprx_spd_inverse",
     "gprx_sparse_fit", "gprx_ctx_set_stats", "gprx_ctx_get_stats",
     "gprx_model_set_kernel_matrix", "gprx_model_predict_kx", "gprx_model_posterior_cov_kx", "gprx_model_lml_dk",
-    "gprx_model_set_sparse_cov",
+    "gprx_model_set_sparse_cov", "gprx_sparse_lml",
 ]
 
 
@@ -128,6 +128,11 @@ def lib():
                                       ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
                                       ctypes.c_void_p, ctypes.c_int64, ctypes.c_double, ctypes.c_double,
                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        L.gprx_sparse_lml.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(KernelDesc), ctypes.c_void_p,
+                                      ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
+                                      ctypes.c_void_p, ctypes.c_int64, ctypes.c_double, ctypes.c_double,
+                                      ctypes.c_uint32, ctypes.POINTER(ctypes.c_double), ctypes.c_void_p,
+                                      ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_double)]
         L.gprx_dist_unique_id.argtypes = [ctypes.c_void_p]
         L.gprx_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
         L.gprx_ctx_set_stats.argtypes = [ctypes.c_void_p, ctypes.c_int32]
@@ -314,6 +319,26 @@ class Context:
         self._c(lib().gprx_sparse_fit(self.h, _dt(dtype), ctypes.byref(kernel_desc(kernel)), _ptr(X), _ptr(Y), n, d,
                                       m, _ptr(Xm), M, sigma, jitter, _ptr(Kinv), _ptr(RV), _ptr(RM)))
         return Kinv, RV, RM
+
+    def sparse_lml(self, kernel, X, Y, Xm, sigma, jitter, dtype=np.float64, grad=True, compat=False):
+        """SparseGaussianLogLikelihood (include/SparseLikelihood.h:231-344) -> (value, grad, logdet)."""
+        X = np.ascontiguousarray(X, dtype)
+        Y = np.ascontiguousarray(Y, dtype)
+        if Y.ndim == 1:
+            Y = Y[:, None]
+        Xm = np.ascontiguousarray(Xm, dtype)
+        n, d = X.shape
+        m = Y.shape[1]
+        M = Xm.shape[0]
+        flags = (LML_GRAD if grad else 0) | (LML_COMPAT if compat else 0)
+        v = ctypes.c_double()
+        ld = ctypes.c_double()
+        npar = ctypes.c_int32()
+        g = np.zeros(3 * MAX_KNODES, np.float64)
+        self._c(lib().gprx_sparse_lml(self.h, _dt(dtype), ctypes.byref(kernel_desc(kernel)), _ptr(X), _ptr(Y), n, d,
+                                      m, _ptr(Xm), M, sigma, jitter, flags, ctypes.byref(v), _ptr(g),
+                                      ctypes.byref(npar), ctypes.byref(ld)))
+        return v.value, (g[:npar.value].copy() if grad else None), ld.value
 
 
 class Model:

@@ -112,6 +112,37 @@ public:
         m_SparseInitialized = true;
     }
 
+    // SparseGaussianLogLikelihood (include/SparseLikelihood.h:231-344) on the device: one
+    // gprx_sparse_lml call over the current dense and inducing samples (SparseLikelihood.h in
+    // this directory is the reference's class surface over it).  grad receives the kernel
+    // parameters' derivatives (GetParameters order).
+    void EvaluateLogLikelihood(bool want_grad, bool compat, double* value, std::vector<double>* grad,
+                               double* logdet) const {
+        if (m_InducingSampleVectors.empty())
+            throw std::string("SparseLikelihood::GetValueAndParameterDerivative: there are no inducing samples specified");
+        if (this->m_SampleVectors.empty())
+            throw std::string("SparseGaussianProcess::ComputeCoreMatrices: empty sample set.");
+        const std::size_t M = m_InducingSampleVectors.size(), n = this->m_SampleVectors.size();
+        if (!(M <= n))
+            throw std::string(
+                "SparseGaussianProcess::ComputeKernelVectorMatrix: number of dense samples must be higher than the "
+                "number of sparse samples");
+        if (this->m_OutputDimension != 1)
+            throw std::string("SparseGaussianLogLikelihood: device likelihood supports one output dimension");
+        const unsigned d = this->m_InputDimension;
+        std::vector<TScalarType> X = Pack(this->m_SampleVectors), Y = Pack(this->m_LabelVectors),
+                                 Xm = Pack(m_InducingSampleVectors);
+        gprx_kernel_desc kd = Desc();
+        std::vector<double> g(3 * GPRX_MAX_KNODES, 0.0);
+        int32_t np = 0;
+        const uint32_t flags = (want_grad ? GPRX_LML_GRAD : 0u) | (compat ? GPRX_LML_COMPAT : 0u);
+        ThrowIfFailed(gprx_sparse_lml(DefaultContext(), Dtype(), &kd, X.data(), Y.data(), (int64_t)n, (int32_t)d, 1,
+                                      Xm.data(), (int64_t)M, (double)this->m_Sigma, (double)m_Jitter, flags, value,
+                                      want_grad ? g.data() : nullptr, &np, logdet),
+                      DefaultContext());
+        if (grad) grad->assign(g.begin(), g.begin() + np);
+    }
+
     const MatrixType& GetRegressionVectors() const { return m_RegressionVectors; }
     const std::vector<TScalarType>& GetInducingInvertedKernelMatrix() const { return m_Kinv; }  // row-major M x M
     const std::vector<TScalarType>& GetRegressionMatrix() const { return m_RM; }               // row-major M x M

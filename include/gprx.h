@@ -273,6 +273,19 @@ gprx_status gprx_sparse_fit(gprx_ctx* ctx, gprx_dtype dtype, const gprx_kernel_d
                             const void* Y, int64_t n, int32_t d, int32_t m, const void* Xm, int64_t M,
                             double sigma, double jitter, void* Kinv, void* RV, void* RM);
 
+/* SparseGaussianLogLikelihood::operator() / GetValueAndParameterDerivatives
+ * (include/SparseLikelihood.h:113-344) for m = 1, in O(N M^2) (Woodbury on the Nystrom
+ * covariance sigma^2 I + Knm Kmm^{-1} Kmn; the reference's N x N C_inv and derivative stacks
+ * are never formed): value = -1/2 y^T C^{-1} y - 1/2 log|C| - N/2 log 2pi, grad_p over the
+ * kernel parameters (the noise is not differentiated, as in the reference).  flags:
+ * GPRX_LML_GRAD, GPRX_LML_COMPAT (the reference's long-double determinant product and its
+ * clamps, :132-158, 305-314; otherwise exact).  logdet receives log|C|.  On an RCCL context
+ * each rank passes its share of the dense rows (as gprx_sparse_fit). */
+gprx_status gprx_sparse_lml(gprx_ctx* ctx, gprx_dtype dtype, const gprx_kernel_desc* kernel, const void* X,
+                            const void* Y, int64_t n, int32_t d, int32_t m, const void* Xm, int64_t M, double sigma,
+                            double jitter, uint32_t flags, double* value, double* grad, int32_t* nparams,
+                            double* logdet);
+
 #ifdef __cplusplus
 }
 #endif

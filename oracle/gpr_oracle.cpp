@@ -22,6 +22,7 @@
 //    * Gaussian log likelihood .......... include/Likelihood.h:77-79, 166-344
 //    * sparse PreComputeRegression ...... include/SparseGaussianProcess.h:174-313
 //                                          (without the N x N core matrix, :309-311)
+//    * sparse log likelihood ............ include/SparseLikelihood.h:129-145, 231-344
 //  Parity pinning: see tests/test_oracle_kats.py (the reference's own deterministic
 //  known-answer tests) and tests/test_oracle_numpy.py (independent numpy/scipy check).
 // =====================================================================================
@@ -627,6 +628,137 @@ static std::vector<T> core_matrix(const Node<T>& k, const T* X, int n, int d, T 
     return C;
 }
 
+// SparseGaussianLogLikelihood::GetValueAndParameterDerivatives, include/SparseLikelihood.h:
+// 231-344, with its N x N matrices (small n only): ComputeCoreMatrices
+// (include/SparseGaussianProcess.h:323-350), EfficientInversion (SparseLikelihood.h:129-135),
+// the derivative stacks (SparseGaussianProcess.h:237-264, 380+), A_p (:246-252), the data-fit
+// and complexity gradients (:255-273), EfficientDeterminant (:138-145) with the clamps
+// (:305-314) and the constant term (:325).  Y is n x 1.  det_out: the long-double
+// determinant; logdet_out: log of its three factors summed (exact).
+template <class T>
+static void sparse_lml(const Node<T>& k, const T* X, const T* Y, int n, int d, const T* Xm, int M, T sigma, T jitter,
+                       T* value, T* grad, double* det_out, double* logdet_out) {
+    typedef long double HP;
+    if (M == 0)
+        throw std::string("SparseLikelihood::GetValueAndParameterDerivative: there are no inducing samples specified");
+    const bool stable = (jitter < std::numeric_limits<T>::min()) ? true : false;
+    // ComputeKernelMatrixWithJitter (SparseGaussianProcess.h:174-180), InvertKernelMatrix
+    std::vector<T> K((size_t)M * M);
+    kernel_matrix(k, Xm, M, d, K.data());
+    for (int i = 0; i < M; i++) K[(size_t)i * M + i] += jitter;
+    std::vector<T> Kinv = invert<T>(K, M, FullPivotLU, stable);
+    if (!(M <= n))
+        throw std::string("SparseGaussianProcess::ComputeKernelVectorMatrix: number of dense samples must be higher than the number of sparse samples");
+    std::vector<T> Knm((size_t)n * M);
+#pragma omp parallel for schedule(static)
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j < M; j++) Knm[(size_t)i * M + j] = keval(k, X + (size_t)i * d, Xm + (size_t)j * d, d);
+    if (sigma <= 0) throw std::string("SparseGaussianProcess::ComputeCoreMatrices: sigma must be positive.");
+    if (n == 0) throw std::string("SparseGaussianProcess::ComputeCoreMatrices: empty sample set.");
+    const T s2 = sigma * sigma;  // I_sigma diagonal (GetSigmaSquared)
+    const T ainv = T(1.0) / s2;  // A_inv = 1 / A.diagonal()
+    // EfficientInversion: inner = B_inv + X^T A_inv X = K + Knm^T A_inv Knm; C_inv = A_inv - A_inv X inner^-1 X^T A_inv
+    std::vector<T> inner((size_t)M * M, T(0));
+#pragma omp parallel for schedule(static)
+    for (int a = 0; a < M; a++)
+        for (int b = 0; b < M; b++) {
+            T acc = 0;
+            for (int i = 0; i < n; i++) acc += Knm[(size_t)i * M + a] * ainv * Knm[(size_t)i * M + b];
+            inner[(size_t)a * M + b] = K[(size_t)a * M + b] + acc;
+        }
+    std::vector<T> inner_inv = invert<T>(inner, M, FullPivotLU, false);  // GetInverseMatrix (SparseLikelihood.h:100-102)
+    std::vector<T> Z((size_t)n * M);  // X inner^-1
+    gemm(Knm.data(), inner_inv.data(), Z.data(), n, M, M);
+    std::vector<T> Cinv((size_t)n * n);
+#pragma omp parallel for schedule(static)
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j < n; j++) {
+            T acc = 0;
+            for (int a = 0; a < M; a++) acc += Z[(size_t)i * M + a] * Knm[(size_t)j * M + a];
+            Cinv[(size_t)i * n + j] = (i == j ? ainv : T(0)) - ainv * acc * ainv;
+        }
+    // data fit (:301-302): -0.5 Y^T C_inv Y
+    std::vector<T> v(n);  // C_inv Y
+    for (int i = 0; i < n; i++) {
+        T acc = 0;
+        for (int j = 0; j < n; j++) acc += Cinv[(size_t)i * n + j] * Y[j];
+        v[i] = acc;
+    }
+    T df = 0;
+    for (int i = 0; i < n; i++) df += Y[i] * v[i];
+    df = -0.5 * df;
+    // EfficientDeterminant: |A + X B X'| = |B| |A| |inv(B) + X' inv(A) X|, B = K_inv
+    HP det_B = det_long_double(Kinv, M);
+    if (std::isinf(det_B)) det_B = std::numeric_limits<HP>::max();
+    HP prodA = 1;
+    for (int i = 0; i < n; i++) prodA *= (HP)s2;
+    const HP det_inner = det_long_double(inner, M);
+    const HP determinant = det_B * prodA * det_inner;
+    if (det_out) *det_out = (double)determinant;
+    if (logdet_out)
+        *logdet_out = (double)(std::log(std::fabs(det_long_double(Kinv, M))) + (HP)n * std::log((HP)s2) +
+                               std::log(std::fabs(det_inner)));
+    HP cp;
+    if (determinant <= std::numeric_limits<HP>::min() || std::isnan(determinant))
+        cp = -0.5 * std::log(std::numeric_limits<HP>::min());
+    else if (determinant > std::numeric_limits<HP>::max())
+        cp = -0.5 * std::log(std::numeric_limits<HP>::max());
+    else
+        cp = -0.5 * std::log(determinant);
+    const T ct = -(n / 2.0) * std::log(2 * M_PI);
+    const T val = df + (T)(cp + ct);
+    if (std::isnan(val))
+        throw std::string("SparseLikelihood::GetValueAndParameterDerivative: likelihood value is not a number.");
+    *value = val;
+    if (!grad) return;
+    // Kmm_d (P stacked M x M, no jitter) and Knm_d (P stacked n x M)
+    const int P = k.nparams();
+    std::vector<T> Kmm_d((size_t)P * M * M), Knm_d((size_t)P * n * M);
+    deriv_matrix(k, Xm, M, d, Kmm_d.data());
+#pragma omp parallel for schedule(static)
+    for (int i = 0; i < n; i++) {
+        std::vector<T> g;
+        for (int j = 0; j < M; j++) {
+            g.clear();
+            kgrad(k, X + (size_t)i * d, Xm + (size_t)j * d, d, g);
+            for (int p = 0; p < P; p++) Knm_d[((size_t)p * n + i) * M + j] = g[p];
+        }
+    }
+    std::vector<T> W((size_t)n * M);  // Knm K_inv
+    gemm(Knm.data(), Kinv.data(), W.data(), n, M, M);
+    std::vector<T> Ap((size_t)n * n), T1((size_t)n * M), T2((size_t)M * M), Q((size_t)n * M);
+    for (int p = 0; p < P; p++) {
+        const T* Dp = Knm_d.data() + (size_t)p * n * M;
+        const T* Ep = Kmm_d.data() + (size_t)p * M * M;
+        gemm(Dp, Kinv.data(), T1.data(), n, M, M);  // Knm_d K_inv
+        gemm(Ep, Kinv.data(), T2.data(), M, M, M);  // Kmm_d K_inv
+        gemm(W.data(), T2.data(), Q.data(), n, M, M);  // Knm K_inv Kmm_d K_inv
+#pragma omp parallel for schedule(static)
+        for (int i = 0; i < n; i++)
+            for (int j = 0; j < n; j++) {
+                T a = 0, b = 0, c = 0;
+                for (int l = 0; l < M; l++) {
+                    a += T1[(size_t)i * M + l] * Knm[(size_t)j * M + l];  // Knm_d K_inv Knm^T
+                    b += Q[(size_t)i * M + l] * Knm[(size_t)j * M + l];   // Knm K_inv Kmm_d K_inv Knm^T
+                    c += W[(size_t)i * M + l] * Dp[(size_t)j * M + l];    // Knm K_inv Knm_d^T
+                }
+                Ap[(size_t)i * n + j] = a - b + c;
+            }
+        // 0.5 Y^T C_inv A_p C_inv Y (C_inv symmetric: v^T A_p v) and -0.5 tr(C_inv A_p)
+        T dt = 0, tr = 0;
+        for (int i = 0; i < n; i++) {
+            T r = 0, q = 0;
+            for (int j = 0; j < n; j++) {
+                r += Ap[(size_t)i * n + j] * v[j];
+                q += Cinv[(size_t)i * n + j] * Ap[(size_t)j * n + i];
+            }
+            dt += v[i] * r;
+            tr += q;
+        }
+        grad[p] = 0.5 * dt - 0.5 * tr;
+    }
+}
+
 }  // namespace orc
 
 using namespace orc;
@@ -867,6 +999,16 @@ int orc_num_threads() { return omp_get_max_threads(); }
         std::copy(Ki.begin(), Ki.end(), Kinv);                                                     \
         ORC_CATCH                                                                                  \
     }
+
+#define ORC_DEFINE_SPARSE_LML(SUF, T)                                                              \
+    int orc_sparse_lml_##SUF(const char* ks, const T* X, const T* Y, int n, int d, const T* Xm, int M, \
+                             T sigma, T jitter, T* value, T* grad, double* det_out, double* logdet_out) { \
+        ORC_TRY auto k = kernel_from<T>(ks);                                                       \
+        sparse_lml(*k, X, Y, n, d, Xm, M, sigma, jitter, value, grad, det_out, logdet_out);        \
+        ORC_CATCH                                                                                  \
+    }
+ORC_DEFINE_SPARSE_LML(f64, double)
+ORC_DEFINE_SPARSE_LML(f32, float)
 
 ORC_DEFINE(f64, double)
 ORC_DEFINE(f32, float)

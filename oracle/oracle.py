@@ -196,3 +196,18 @@ def sparse_fit(kstr, X, Y, Xm, sigma, jitter, dtype=np.float64):
     _call(f"orc_sparse_fit_{suf}", kstr.encode(), _p(X), _p(Y), n, d, m, _p(Xm), M, ct(sigma), ct(jitter),
           _p(Kinv), _p(RV), _p(RM))
     return Kinv, RV, RM
+
+
+def sparse_lml(kstr, X, Y, Xm, sigma, jitter, dtype=np.float64, with_grad=True):
+    """SparseGaussianLogLikelihood value (+ gradient), N x N restatement (small n).
+    Returns (value, grad, det, logdet)."""
+    suf, ct = _dt(dtype)
+    X, Y, Xm = _c(X, dtype), _c(Y, dtype).reshape(-1), _c(Xm, dtype)
+    n, d = X.shape
+    val = np.zeros(1, dtype)
+    g = np.zeros(kernel_nparams(kstr, dtype), dtype) if with_grad else None
+    det = ctypes.c_double()
+    ld = ctypes.c_double()
+    _call(f"orc_sparse_lml_{suf}", kstr.encode(), _p(X), _p(Y), n, d, _p(Xm), Xm.shape[0], ct(sigma), ct(jitter),
+          _p(val), _p(g), ctypes.byref(det), ctypes.byref(ld))
+    return val[0], g, det.value, ld.value

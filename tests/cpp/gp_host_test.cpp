@@ -16,6 +16,7 @@
 #include "gpr/Likelihood.h"
 #include "gpr/MatrixIO.h"
 #include "gpr/SparseGaussianProcess.h"
+#include "gpr/SparseLikelihood.h"
 
 using namespace gpr;
 
@@ -323,6 +324,58 @@ static void sparse_test() {
     check(err < 0.05, "sparse predict error " + num(err));
 }
 
+// SparseGaussianLogLikelihood (include/SparseLikelihood.h:231-344): value and gradient on a
+// sparse GP (every 8th dense sample inducing) vs central differences of the value; operator(),
+// GetValueAndParameterDerivatives and GetValueAndJacobian agree; a dense GP is rejected with
+// the reference's cast message.
+static void sparse_lik_test() {
+    typedef SparseGaussianProcess<double> S;
+    auto k = std::make_shared<GaussianKernel<double>>(0.9, 1.2);
+    auto gp = std::make_shared<S>(k, 1e-3);
+    gp->SetSigma(0.2);
+    for (unsigned i = 0; i < 320; i++) {
+        S::VectorType x(1), y(1);
+        x(0) = -3 + 6.0 * i / 319;
+        y(0) = std::sin(2 * x(0)) + 0.1 * std::cos(7 * x(0));
+        gp->AddSample(x, y);
+        if (i % 16 == 0) gp->AddInducingSample(x, y);
+    }
+    SparseGaussianLogLikelihood<double> lik;
+    auto vg = lik.GetValueAndParameterDerivatives(gp);
+    check(std::isfinite(vg.first(0)), "sparse likelihood not finite");
+    check(lik(gp)(0) == vg.first(0), "operator() vs GetValueAndParameterDerivatives");
+    auto vj = lik.GetValueAndJacobian(gp);
+    check(vj.second.rows() == 1 && vj.second.cols() == vg.second.size(), "Jacobian shape");
+    auto p = k->GetParameters();
+    for (std::size_t i = 0; i < p.size(); i++) {
+        check(vj.second(0, i) == vg.second(i), "Jacobian row vs gradient");
+        // Richardson-extrapolated central differences (cond(Kmm + jitter I) ~ 1e4 limits plain
+        // differences at small steps to ~1e-4)
+        auto cd = [&](double h) {
+            auto pp = p, pm = p;
+            pp[i] += h;
+            pm[i] -= h;
+            k->SetParameters(pp);
+            const double vp = lik(gp)(0);
+            k->SetParameters(pm);
+            const double vm = lik(gp)(0);
+            return (vp - vm) / (2 * h);
+        };
+        const double fd = (4 * cd(5e-4) - cd(1e-3)) / 3;
+        check(std::fabs(fd - vg.second(i)) <= 1e-4 * std::max(1.0, std::fabs(fd)),
+              "sparse grad " + num(vg.second(i)) + " vs fd " + num(fd));
+    }
+    k->SetParameters(p);
+    auto dense = std::make_shared<GP<double>>(k);
+    bool threw = false;
+    try {
+        lik(dense);
+    } catch (std::string& e) {
+        threw = e == "SparseGaussianLogLikelihood: cannot cast to SparseGaussianProcess";
+    }
+    check(threw, "dense GP must be rejected");
+}
+
 // PosteriorProcessTest Test1 (tests/PosteriorProcessTest.cpp:51-95): the credible interval
 // is exactly 2 sqrt(gp(x, x)), sigma = 1e-5, 20 sinus samples.
 static void posterior_test1() {
@@ -530,6 +583,7 @@ int main() {
     run("IOTest3", io_test3);
     run("LikelihoodGradient", lik_test);
     run("SparseRegression", sparse_test);
+    run("SparseLogLikelihood", sparse_lik_test);
     run("PosteriorProcessTest1", posterior_test1);
     run("PosteriorProcessTest2", posterior_test2);
     run("PosteriorProcessTest2Loaded", posterior_test2_loaded);

@@ -145,3 +145,35 @@ def test_sparse_fit_numpy():
     assert relerr(Kinv, np.linalg.inv(Kmm)) < 1e-8
     assert relerr(RV, Sig @ Knm.T @ Y / s ** 2) < 1e-6
     assert relerr(RM, Sig) < 1e-6
+
+
+@pytest.mark.parametrize("ks,ref", [CASES[0], CASES[4], CASES[2]])
+def test_sparse_lml_numpy(ks, ref):
+    """The oracle's literal SparseGaussianLogLikelihood (include/SparseLikelihood.h:231-344)
+    against an independent numpy evaluation of the Nystrom likelihood
+    log N(y | 0, sigma^2 I + Knm Kmm^-1 Kmn) (dense solve, slogdet) and central differences of
+    it in every kernel parameter (the reference differentiates the kernel parameters only)."""
+    n, M, s, jit = 150, 15, 0.4, 1e-3
+    X, Y = make_data(n, 3)
+    Xm = X[:: n // M][:M].copy()
+    y = Y[:, 0]
+    v, g, det, ld = O.sparse_lml(ks, X, y, Xm, s, jit)
+
+    def lml_np(kstr):
+        Kmm = O.kernel_matrix(kstr, Xm) + jit * np.eye(M)
+        Knm = O.cross_matrix(kstr, X, Xm)
+        C = s * s * np.eye(n) + Knm @ np.linalg.solve(Kmm, Knm.T)
+        sign, lgd = np.linalg.slogdet(C)
+        return -0.5 * y @ np.linalg.solve(C, y) - 0.5 * lgd - n / 2 * np.log(2 * np.pi), lgd
+
+    v_np, ld_np = lml_np(ks)
+    assert abs(v - v_np) < 1e-8 * max(1, abs(v_np))
+    assert abs(ld - ld_np) < 1e-8 * max(1, abs(ld_np))
+    P = np.array(__import__("gpr_amd").parse_kernel(ks).parameters())
+    for p in range(len(P)):
+        h = 1e-5 * max(1.0, abs(P[p]))
+        Pp, Pm = P.copy(), P.copy()
+        Pp[p] += h
+        Pm[p] -= h
+        fd = (lml_np(_with_params(ks, Pp))[0] - lml_np(_with_params(ks, Pm))[0]) / (2 * h)
+        assert abs(fd - g[p]) < 1e-5 * max(1, abs(fd)), (p, fd, g[p])
