@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--d", type=int, default=64)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--lml", type=int, default=1, help="also time the sparse log likelihood + gradient")
     args = ap.parse_args()
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -69,6 +70,26 @@ def main():
         print(json.dumps({"metric": "sparse GP fit (M inducing, N dense)", "n": n, "M": M, "d": d, "n_gpus": world,
                           "ms_per_fit": dt * 1e3, "fits_per_s": 1.0 / dt, "tflops_effective": flops / dt / 1e12,
                           "note": "wall time incl. host->device upload of the rank's rows and host outputs"}))
+    if args.lml:  # SparseGaussianLogLikelihood value + gradient (gprx_sparse_lml)
+        ctx.sparse_lml(ks, Xl, Yl, Xm, 0.1, 1e-4)
+        if dist:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            v, g, ld = ctx.sparse_lml(ks, Xl, Yl, Xm, 0.1, 1e-4)
+        dt = (time.perf_counter() - t0) / args.steps
+        if dist:
+            import torch
+            t = torch.tensor([dt], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t[0])
+        # fit's normal equations + the gradient pass's GEMM K(Xc, Xm) Sigma (2 N M^2) + M^3 inverses
+        lflops = flops + 2.0 * n * M * M + 2.0 * M ** 3
+        if rank == 0:
+            print(json.dumps({"metric": "sparse GP log likelihood + gradient", "n": n, "M": M, "d": d,
+                              "n_gpus": world, "ms_per_eval": dt * 1e3, "value": v, "grad": list(g),
+                              "tflops_effective": lflops / dt / 1e12,
+                              "note": "wall time incl. host->device upload of the rank's rows"}))
     ctx.close()
 
 

@@ -133,3 +133,21 @@ def test_sparse_fit_rccl_one_rank():
     finally:
         dctx.close()
         lctx.close()
+
+
+def test_sparse_lml_rccl_one_rank():
+    """gprx_sparse_lml on an RCCL context (rows sharded; normal equations, data terms and the
+    N x M gradient partials all-reduced): on one rank it equals the local call."""
+    import gpr_amd
+    ks = CASES[1][0]
+    n, d, M, m = 800, 3, 48, 1
+    X, Y, Xm = _inputs(n, d, M, m, np.float64)
+    lctx = gpr_amd.Context(0)
+    dctx = gpr_amd.Context(0, dist=(0, 1, gpr_amd.unique_id()))
+    try:
+        vl, gl, ldl = lctx.sparse_lml(ks, X, Y, Xm, 0.5, 1e-3)
+        vd, gd, ldd = dctx.sparse_lml(ks, X, Y, Xm, 0.5, 1e-3)
+        assert vd == vl and ldd == ldl and np.array_equal(gd, gl)
+    finally:
+        dctx.close()
+        lctx.close()
