@@ -90,18 +90,23 @@ void GaussianProcess<T>::AddSample(const VectorType& x, const VectorType& y) {
     m_SampleVectors.push_back(x);
     m_LabelVectors.push_back(y);
     m_Initialized = false;
+    m_DataUploaded = false;
 }
 
 template <class T>
 void GaussianProcess<T>::UploadState() {
     gprx_ctx* ctx = DefaultContext();
-    const std::size_t n = m_SampleVectors.size(), d = m_InputDimension, m = m_OutputDimension;
-    std::vector<T> X(n * d), Y(n * m);
-    for (std::size_t i = 0; i < n; i++) {
-        for (std::size_t k = 0; k < d; k++) X[i * d + k] = m_SampleVectors[i][k];
-        for (std::size_t c = 0; c < m; c++) Y[i * m + c] = m_LabelVectors[i][c];
+    const std::size_t n = m_SampleVectors.size();
+    if (!m_DataUploaded || !m_Model) {
+        const std::size_t d = m_InputDimension, m = m_OutputDimension;
+        std::vector<T> X(n * d), Y(n * m);
+        for (std::size_t i = 0; i < n; i++) {
+            for (std::size_t k = 0; k < d; k++) X[i * d + k] = m_SampleVectors[i][k];
+            for (std::size_t c = 0; c < m; c++) Y[i * m + c] = m_LabelVectors[i][c];
+        }
+        ThrowIfFailed(gprx_model_set_data(Model(), X.data(), Y.data(), (int64_t)n, (int32_t)d, (int32_t)m), ctx);
+        m_DataUploaded = true;
     }
-    ThrowIfFailed(gprx_model_set_data(Model(), X.data(), Y.data(), (int64_t)n, (int32_t)d, (int32_t)m), ctx);
     std::vector<gprx_knode> prog;
     try {
         m_Kernel->Describe(prog);

@@ -136,6 +136,9 @@ protected:
                                   // kernel vectors are evaluated here through the virtual
                                   // operator() (include/Kernel.h:52-59), the rest on the device
     bool m_CoreValid = false;     // m_CoreMatrix holds the materialised core matrix
+    bool m_DataUploaded = false;  // the device model holds the current samples (AddSample clears
+                                  // it): an optimiser loop re-evaluating the likelihood under new
+                                  // kernel parameters re-sends only the kernel
     std::size_t m_CoreSize = 0;   // the reference's m_CoreMatrix.diagonalSize(): n once the
                                   // core exists (Initialize w/o efficient storage, operator(),
                                   // Load), 0 when efficient storage dropped it

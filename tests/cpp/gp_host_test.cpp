@@ -17,6 +17,7 @@
 #include "gpr/MatrixIO.h"
 #include "gpr/SparseGaussianProcess.h"
 #include "gpr/SparseLikelihood.h"
+#include "gpr/GaussianProcessInference.h"
 
 using namespace gpr;
 
@@ -376,6 +377,76 @@ static void sparse_lik_test() {
     check(threw, "dense GP must be rejected");
 }
 
+// MaximumLikelihoodTest2 Test1 (tests/MaximumLikelihoodTest2.cpp:36-117): GaussianExp kernel
+// hyper-parameters by GaussianProcessInference::Optimize (100 Gauss-Newton steps of 0.1) on
+// 200 noisy samples of (0.5 sin(11x) + sin(4x)) x^2, then the exp'd parameters in a Gaussian
+// kernel; mean absolute prediction error over 1000 points <= 2 (the reference's bar).  The
+// reference draws its noise from boost's normal_distribution seeded with time(0); here a fixed
+// LCG + Box-Muller (sd 0.1).
+static void ml_test1() {
+    typedef GP<double> G;
+    const unsigned n = 200;
+    const double noise = 0.1;
+    auto f = [](double x) { return (0.5 * std::sin(x + 10 * x) + std::sin(4 * x)) * x * x; };
+    unsigned long long st = 0x9E3779B97F4A7C15ull;
+    auto unif = [&]() {
+        st = st * 6364136223846793005ull + 1442695040888963407ull;
+        return ((st >> 11) + 0.5) * (1.0 / 9007199254740992.0);
+    };
+    const double start = -5, stop = 10;
+    auto gk = std::make_shared<GaussianExpKernel<double>>(1, 1);
+    auto gp = std::make_shared<G>(gk);
+    gp->SetSigma(noise);
+    for (unsigned i = 0; i < n; i++) {
+        const double x = start + i * (stop - start) / n;
+        const double r = noise * std::sqrt(-2 * std::log(unif())) * std::cos(2 * M_PI * unif());
+        G::VectorType xv(1), yv(1);
+        xv(0) = x;
+        yv(0) = f(x) + r;
+        gp->AddSample(xv, yv);
+    }
+    auto lh = std::make_shared<GaussianLogLikelihood<double>>();
+    GaussianProcessInference<double> gpi(lh, gp, 1e-1, 100);
+    gpi.Optimize(false, true);
+    auto parameters = gpi.GetParameters();
+    for (auto& p : parameters) p = std::exp(p);
+    auto k = std::make_shared<GaussianKernel<double>>(1, 1);
+    k->SetParameters(parameters);
+    gp->SetKernel(k);
+    double error = 0;
+    const unsigned gt_n = 1000;
+    for (unsigned i = 0; i < gt_n; i++) {
+        const double x = start + i * (stop - start) / gt_n;
+        G::VectorType xv(1);
+        xv(0) = x;
+        error += std::fabs(gp->Predict(xv)(0) - f(x));
+    }
+    check(error / gt_n <= 2, "ML Test1 mean error " + num(error / gt_n));
+}
+
+// SparseInferenceTest-style loop: Optimize2 (Gauss-Newton on J^T J) of a sparse GP's kernel
+// parameters with SparseGaussianLogLikelihood; the likelihood must not decrease.
+static void sparse_ml_test() {
+    typedef SparseGaussianProcess<double> S;
+    auto k = std::make_shared<GaussianKernel<double>>(2.0, 1.0);
+    auto gp = std::make_shared<S>(k, 1e-3);
+    gp->SetSigma(0.1);
+    for (unsigned i = 0; i < 400; i++) {
+        S::VectorType x(1), y(1);
+        x(0) = -3 + 6.0 * i / 399;
+        y(0) = std::sin(2 * x(0));
+        gp->AddSample(x, y);
+        if (i % 16 == 0) gp->AddInducingSample(x, y);
+    }
+    auto lh = std::make_shared<SparseGaussianLogLikelihood<double>>();
+    const double v0 = (*lh)(gp)(0);
+    GaussianProcessInference<double> gpi(lh, gp, 1e-2, 20);
+    gpi.Optimize2(false, false);
+    k->SetParameters(gpi.GetParameters());
+    const double v1 = (*lh)(gp)(0);
+    check(std::isfinite(v1) && v1 >= v0, "sparse inference: likelihood " + num(v0) + " -> " + num(v1));
+}
+
 // PosteriorProcessTest Test1 (tests/PosteriorProcessTest.cpp:51-95): the credible interval
 // is exactly 2 sqrt(gp(x, x)), sigma = 1e-5, 20 sinus samples.
 static void posterior_test1() {
@@ -584,6 +655,8 @@ int main() {
     run("LikelihoodGradient", lik_test);
     run("SparseRegression", sparse_test);
     run("SparseLogLikelihood", sparse_lik_test);
+    run("MaximumLikelihoodTest1", ml_test1);
+    run("SparseInferenceOptimize2", sparse_ml_test);
     run("PosteriorProcessTest1", posterior_test1);
     run("PosteriorProcessTest2", posterior_test2);
     run("PosteriorProcessTest2Loaded", posterior_test2_loaded);

@@ -10,6 +10,7 @@
 #include <sstream>
 
 #include "gpr/GaussianProcess.h"
+#include "gpr/GaussianProcessInference.h"
 #include "gpr/Kernel.h"
 #include "gpr/MatrixIO.h"
 
@@ -125,7 +126,56 @@ static void dim_test() {
     check(threw, "dimension mismatch message");
 }
 
+// pinv (include/Prior.h:38-55 restated in gpr/GaussianProcessInference.h): Moore-Penrose
+// conditions on a full-rank and a rank-deficient matrix, and the rank-1 g g^T of Optimize,
+// whose pseudo-inverse times g is g / |g|^2.
+static void pinv_test() {
+    typedef GaussianProcess<double>::MatrixType MT;
+    auto mul = [](const MT& a, const MT& b) {
+        MT c(a.rows(), b.cols());
+        for (std::size_t i = 0; i < a.rows(); i++)
+            for (std::size_t j = 0; j < b.cols(); j++) {
+                double s = 0;
+                for (std::size_t k = 0; k < a.cols(); k++) s += a(i, k) * b(k, j);
+                c(i, j) = s;
+            }
+        return c;
+    };
+    auto maxdiff = [](const MT& a, const MT& b) {
+        double m = 0;
+        for (std::size_t i = 0; i < a.rows(); i++)
+            for (std::size_t j = 0; j < a.cols(); j++) m = std::max(m, std::fabs(a(i, j) - b(i, j)));
+        return m;
+    };
+    MT A(5, 5), R(5, 5);
+    unsigned st = 12345;
+    for (std::size_t i = 0; i < 5; i++)
+        for (std::size_t j = 0; j < 5; j++) {
+            st = st * 1103515245u + 12345u;
+            A(i, j) = ((st >> 8) % 1000) / 500.0 - 1.0;
+        }
+    for (std::size_t i = 0; i < 5; i++)  // rank 3: rows 3, 4 are combinations of rows 0-2
+        for (std::size_t j = 0; j < 5; j++) R(i, j) = i < 3 ? A(i, j) : A(0, j) * (i - 2.0) + A(1, j);
+    for (const MT* M : {&A, &R}) {
+        const MT P = pinv<MT>(*M);
+        check(maxdiff(mul(mul(*M, P), *M), *M) < 1e-12, "pinv: A P A != A");
+        check(maxdiff(mul(mul(P, *M), P), P) < 1e-10, "pinv: P A P != P");
+    }
+    const double g[3] = {0.3, -2.0, 0.7};
+    MT G(3, 3);
+    for (int a = 0; a < 3; a++)
+        for (int b = 0; b < 3; b++) G(a, b) = g[a] * g[b];
+    const MT P = pinv<MT>(G);
+    const double g2 = 0.09 + 4.0 + 0.49;
+    for (int a = 0; a < 3; a++) {
+        double u = 0;
+        for (int b = 0; b < 3; b++) u += P(a, b) * g[b];
+        check(std::fabs(u - g[a] / g2) < 1e-12, "pinv(g g^T) g != g / |g|^2");
+    }
+}
+
 int main(int argc, char** argv) {
+    run("PseudoInverse", pinv_test);
     run("KernelDerivatives", deriv_test);
     run("KernelFactoryRoundTrip", factory_test);
     run("MatrixIO", io_test);

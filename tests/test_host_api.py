@@ -39,11 +39,11 @@ def test_host_cpu():
     args = [] if _gpu_visible() else ["--no-device"]
     rc, lines, out = _run("host_cpu_test", *args)
     assert rc == 0, out
-    assert len(lines) == 4 + len(args), out
+    assert len(lines) == 5 + len(args), out
 
 
 @pytest.mark.gpu
 def test_host_gpu_reference_scenarios():
     rc, lines, out = _run("gp_host_test")
     assert rc == 0, out
-    assert len(lines) == 18 and all(l.startswith("PASS") for l in lines), out
+    assert len(lines) == 20 and all(l.startswith("PASS") for l in lines), out
