@@ -95,6 +95,7 @@ def main():
     ap.add_argument("--n", type=int, default=None)
     ap.add_argument("--d", type=int, default=None)
     ap.add_argument("--predict-q", type=int, default=65536)
+    ap.add_argument("--variance-q", type=int, default=4096, help="posterior-variance queries (0 = skip)")
     ap.add_argument("--lml", type=int, default=1, help="also time one log-marginal likelihood + gradient "
                                                         "(BASELINE.json configs[2]); 0 = skip")
     ap.add_argument("--build-iters", type=int, default=3, help="time the covariance build alone (0 = skip)")
@@ -226,6 +227,24 @@ def main():
                               "frac": args.predict_q * n * (2.0 * d + 2.0 * m) / (pms * 1e-3) / 1e12 / world
                               / PEAK_FP64_TFLOPS} if pms else None)}
 
+    # posterior variance (GetCredibleInterval, lib/GaussianProcess.cpp:102-114): k(x,x) - |L^{-1} k_x|^2
+    # for Qv queries, query-sharded; the forward solve with Qv right-hand sides on the tile GEMM
+    # (Qv N^2 flop) dominates.  Wall time of the call (queries up, variances down: small)
+    var = None
+    if args.variance_q > 0:
+        Xv = make_queries(args.variance_q, d)
+        lo, hi = gpr_amd.query_shard(args.variance_q, rank, world)
+        model.posterior_cov(Xv[lo:hi], Xv[lo:hi])
+        barrier_sync()
+        tv0 = time.perf_counter()
+        model.posterior_cov(Xv[lo:hi], Xv[lo:hi])
+        tv = max_over_ranks(time.perf_counter() - tv0)
+        fl = float(args.variance_q) * n * n
+        var = {"q": args.variance_q, "sharded_over": world, "pts_per_s_wall": args.variance_q / tv,
+               "ms": 1e3 * tv, "roofline": {"bound": "mfma", "achieved": fl / tv / 1e12 / world,
+                                            "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
+                                            "frac": fl / tv / 1e12 / world / PEAK_FP64_TFLOPS}}
+
     # log-marginal likelihood + gradient (refit, explicit inverse, fused gradient pass)
     lml = None
     if args.lml:
@@ -321,6 +340,7 @@ def main():
             "dist_error": dist_error,
             "phases": phases,
             "predict": pred,
+            "variance": var,
             "lml_grad": lml,
             "build": build,
             "lml_grad_sharded_ms_wall": (dres or {}).get("lml_ms_wall"),

@@ -900,14 +900,18 @@ static gprx_status model_posterior_cov(gprx_model* M, const void* Xa, const void
         download(out, res.p, sizeof(T) * q, s);
         return GPRX_OK;
     }
+    // the variance (GetCredibleInterval, :102-114, pairs (x, x)): one solve, |L^{-1} k_x|^2
+    const bool same = (Xa == Xb) || std::memcmp(Xa, Xb, sizeof(T) * q * d) == 0;
     Ra.ensure(sizeof(T) * qp * M->np);
-    Rb.ensure(sizeof(T) * qp * M->np);
     solve_rows_for<T>(M, da.as<T>(), ta.as<T>(), q, qp, Ra.as<T>());
-    solve_rows_for<T>(M, db.as<T>(), tb.as<T>(), q, qp, Rb.as<T>());
+    if (!same) {
+        Rb.ensure(sizeof(T) * qp * M->np);
+        solve_rows_for<T>(M, db.as<T>(), tb.as<T>(), q, qp, Rb.as<T>());
+    }
     kab.ensure(sizeof(T) * q);
     res.ensure(sizeof(T) * q);
     launch_pair_kernel<T>(K, da.as<T>(), db.as<T>(), q, d, kab.as<T>(), s);
-    launch_rowdot<T>(Ra.as<T>(), Rb.as<T>(), qp, q, M->np, kab.as<T>(), res.as<T>(), s);
+    launch_rowdot<T>(Ra.as<T>(), same ? Ra.as<T>() : Rb.as<T>(), qp, q, M->np, kab.as<T>(), res.as<T>(), s);
     download(out, res.p, sizeof(T) * q, s);
     return GPRX_OK;
 }

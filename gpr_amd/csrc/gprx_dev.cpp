@@ -17,6 +17,10 @@ template <typename T>
 void launch_diag_public(T* Akk, int64_t ld, T* Lk, int* info, int64_t col0, hipStream_t s, int ph = 3);
 template <typename T>
 void launch_diag_prof(T* Akk, int64_t ld, T* Lk, int* info, long long* prof, hipStream_t s);
+namespace pt {
+template <typename T>
+void launch_diag_bench(int variant, T* A, int64_t ld, T* Linv, int* info, long long* prof, int reps, hipStream_t s);
+}
 }  // namespace gprx
 
 using namespace gprx;
@@ -51,7 +55,30 @@ static gprx_status bench_impl(int what, int64_t M, int64_t N, int64_t K, int ite
     int* info = (int*)alloc(sizeof(int));
     float tms = 0;
     try {
-        if (what == 6) {  // in-kernel phase ticks of the diagonal kernel: ms[0..4] per launch
+        if (what == 11 || what == 12) {  // tile-engine diagonal factor (k_ptiles.hip), variant what - 11:
+            // ms[0] = us per factor (events), ms[1..5] = per-factor phase ticks (100 MHz)
+            const int reps = std::max(1, iters);
+            T* A = (T*)alloc(sizeof(T) * DB * DB * (size_t)reps);
+            T* L = (T*)alloc(sizeof(T) * DB * DB);
+            long long* pr = (long long*)alloc(sizeof(long long) * 8);
+            for (int it = 0; it < reps; it++)
+                hipLaunchKernelGGL(dev_fill_spd<T>, dim3((DB * DB + 255) / 256), dim3(256), 0, s, A + (size_t)it * DB * DB,
+                                   (int64_t)DB, (int64_t)DB, (uint64_t)it);
+            (void)hipMemsetAsync(info, 0x7f, sizeof(int), s);
+            pt::launch_diag_bench<T>(what - 11, A, DB, L, info, pr, 1, s);  // warm (factors block 0 in place)
+            for (int it = 0; it < 1; it++)
+                hipLaunchKernelGGL(dev_fill_spd<T>, dim3((DB * DB + 255) / 256), dim3(256), 0, s, A, (int64_t)DB,
+                                   (int64_t)DB, (uint64_t)0);
+            (void)hipEventRecord(e0, s);
+            pt::launch_diag_bench<T>(what - 11, A, DB, L, info, pr, reps, s);
+            (void)hipEventRecord(e1, s);
+            (void)hipEventSynchronize(e1);
+            (void)hipEventElapsedTime(&tms, e0, e1);
+            long long h[8];
+            (void)hipMemcpy(h, pr, sizeof(h), hipMemcpyDeviceToHost);
+            ms[0] = 1e3 * tms / reps;
+            for (int i = 0; i < 5; i++) ms[1 + i] = (double)h[i] / reps;
+        } else if (what == 6) {  // in-kernel phase ticks of the diagonal kernel: ms[0..4] per launch
             T* A = (T*)alloc(sizeof(T) * DB * DB * (size_t)iters);
             T* L = (T*)alloc(sizeof(T) * DB * DB);
             long long* pr = (long long*)alloc(sizeof(long long) * 8);

@@ -89,6 +89,31 @@ __device__ __forceinline__ void wait_vm() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// Output block (wr, wc) of wave w (64 x 32 outputs at rows 64 wr, columns 32 wc).  Waves w and
+// w + 4 share a SIMD (and its MFMA unit), so a shape whose blocks carry unequal work is mapped
+// with each SIMD's pair summing to the same work:
+//   MAP 0: wr = w & 1, wc = w >> 1 (every block a full 128-deep product);
+//   MAP 1: triangular B (TRSM, k < 32 (wc + 1)): pairs take wc {0, 3} or {1, 2} -- 160 of the
+//          512 k-columns per SIMD instead of 128/128/192/192;
+//   MAP 2: lower (diagonal) tile, 16 x 16 tiles strictly above the diagonal skipped: per SIMD
+//          8/8/10/10 of the 36 live tiles instead of 7/15/3/11 (or two full waves).
+template <int MAP>
+__device__ __forceinline__ void wave_block(int w, int& wr, int& wc) {
+    if (MAP == 1) {
+        wr = w & 1;
+        wc = (w < 4) ? (w >> 1) : 3 - ((w - 4) >> 1);
+    } else if (MAP == 2) {
+        // w: 0 (1,0)  1 (1,1)  2 (0,0)  3 (1,2)  4 (0,2)  5 (0,3)  6 (1,3)  7 (0,1)
+        constexpr unsigned RW = 0b01001011u;          // wr bit per wave
+        constexpr unsigned CW = 0x13322010u;          // 4-bit wc per wave: 0,1,0,2,2,3,3,1
+        wr = (RW >> w) & 1;
+        wc = (CW >> (4 * w)) & 15;
+    } else {
+        wr = w & 1;
+        wc = w >> 1;
+    }
+}
+
 // acc = A B^T over K (multiple of BKS); this wave multiplies only the first kact k-columns
 // (a multiple of BKS: 0 = idle, K = all; the rest of B is zero for it), but every wave takes
 // part in the staging and the barriers of all K.  A, B: 128 rows x K, column-major (lda,
@@ -96,7 +121,7 @@ __device__ __forceinline__ void wait_vm() {
 // Bpan (optional): B given per 128-column panel -- column c of B at Bpan[c / 128] + (c % 128)
 // ldb (the distributed factorisation's received tiles: one packed 128 x 128 tile per panel,
 // ldb = 128, each panel in its own receive buffer).
-template <typename T>
+template <typename T, int MAP = 0>
 __device__ __forceinline__ void tile_mma(typename Mfma<T>::acc_t (&acc)[2][4], const T* __restrict__ A, int64_t lda,
                                          const T* __restrict__ B, int64_t ldb, int K, int kact, T* smem,
                                          const int t, const uint64_t* Bpan = nullptr) {
@@ -104,7 +129,8 @@ __device__ __forceinline__ void tile_mma(typename Mfma<T>::acc_t (&acc)[2][4], c
     typedef typename Tr::acc_t acc_t;
     typedef Stage<T> S;
     const int lane = t & 63, w = t >> 6;
-    const int wr = w & 1, wc = w >> 1;
+    int wr, wc;
+    wave_block<MAP>(w, wr, wc);
     const int lr = lane & 15, lk = lane >> 4;
     const int lcol = lane / S::LPC, lrow = (lane % S::LPC) * S::E;
 
@@ -188,7 +214,9 @@ __device__ __forceinline__ void tile_mma(typename Mfma<T>::acc_t (&acc)[2][4], c
 #pragma unroll
                 for (int x = 0; x < 2; x++)
 #pragma unroll
-                    for (int y = 0; y < 4; y++) acc[x][y] = Tr::mma(fb[kq & 1][x], fa[kq & 1][y], acc[x][y]);
+                    for (int y = 0; y < 4; y++)
+                        if (MAP != 2 || 4 * wr + y >= 2 * wc + x)  // (MAP 2: wave-uniform tile skip)
+                            acc[x][y] = Tr::mma(fb[kq & 1][x], fa[kq & 1][y], acc[x][y]);
             }
         }
         st0 = nmf;

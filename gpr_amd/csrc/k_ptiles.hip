@@ -67,7 +67,8 @@ static_assert(C_NCTL == C_NCTL_DIST, "counter block layout shared with gprx_dist
 // ------------------------------------------------------------------------------------------
 // Bpan: B by 128-column panels (tile_mma); C2 (optional, TRSM only): a second copy of the
 // result, packed 128 x 128 (ld DB) -- the distributed factorisation's send slot.
-template <typename T, bool UPDATE>
+// MAP: the wave -> output-block map (k_mma.h wave_block): 1 for triangular B, 2 for lower.
+template <typename T, bool UPDATE, int MAP = 0>
 __device__ __forceinline__ void tile_gemm(T* __restrict__ C, int64_t ldc, const T* __restrict__ A, int64_t lda,
                                           const T* __restrict__ B, int64_t ldb, int K, bool lower, T* smem,
                                           const int t, bool tri = false, const uint64_t* Bpan = nullptr,
@@ -75,7 +76,8 @@ __device__ __forceinline__ void tile_gemm(T* __restrict__ C, int64_t ldc, const 
     typedef Mfma<T> Tr;
     typedef typename Tr::acc_t acc_t;
     const int lane = t & 63, w = t >> 6;
-    const int wr = w & 1, wc = w >> 1;
+    int wr, wc;
+    wave_block<MAP>(w, wr, wc);
     const int lr = lane & 15, lk = lane >> 4;
     const bool active = !(lower && wr == 0 && wc >= 2);
     // UPDATE: the whole C tile is fetched into registers up front (its latency hides under the
@@ -94,7 +96,7 @@ __device__ __forceinline__ void tile_gemm(T* __restrict__ C, int64_t ldc, const 
             }
     }
     acc_t acc[2][4];
-    tile_mma<T>(acc, A, lda, B, ldb, K, !active ? 0 : (tri ? 32 * (wc + 1) : K), smem, t, Bpan);
+    tile_mma<T, MAP>(acc, A, lda, B, ldb, K, !active ? 0 : (tri ? 32 * (wc + 1) : K), smem, t, Bpan);
     if (!active) return;
 #pragma unroll
     for (int x = 0; x < 2; x++) {
@@ -497,22 +499,9 @@ __device__ __forceinline__ void fact32(T* __restrict__ sS, T* __restrict__ sDi, 
 }
 
 template <typename T>
-__device__ __forceinline__ void diag_factor(T* __restrict__ A, int64_t ld, T* __restrict__ Linv, int* __restrict__ info,
-                                            int64_t col0, unsigned char* smem_raw, const int t, int* dbg = nullptr,
-                                            long long* prof = nullptr) {
-#ifndef GPRX_DIAG_BLOCKED
-    // Default: the rank-8 register image.  The blocked form below (GPRX_DIAG_BLOCKED, f64) was
-    // measured at 47.8 us per diagonal factor against 52 us, but its register demand raised
-    // the whole persistent kernel's spills from 10 to 29 VGPRs and the C3 factorisation by
-    // 0.6 ms (27.3 -> 28.0 ms): kept as a measured experiment, off.
-    if constexpr (true) {
-#else
-    if constexpr (!std::is_same<T, double>::value) {  // f32: the rank-8 register image
-#endif
-        diag_factor_rank8<T>(A, ld, Linv, info, col0, smem_raw, t, dbg, prof);
-        return;
-    }
-    (void)dbg;
+__device__ __forceinline__ void diag_factor_blocked(T* __restrict__ A, int64_t ld, T* __restrict__ Linv,
+                                                    int* __restrict__ info, int64_t col0, unsigned char* smem_raw,
+                                                    const int t, long long* prof = nullptr) {
     typedef Mfma<T> Tr;
     typedef typename Tr::acc_t acc_t;
     constexpr int SL = SIL;
@@ -690,7 +679,8 @@ __device__ __forceinline__ void diag_factor(T* __restrict__ A, int64_t ld, T* __
         const long long te = wall_clock64();
         prof[0] = pload - pt0;
         prof[1] = pf;
-        prof[2] = (pinv - pload - pf) + (te - pinv);
+        prof[2] = pinv - pload - pf;
+        prof[3] = te - pinv;
         (void)pm;
     }
     // ---- L and Linv out: coalesced columns ------------------------------------------------
@@ -702,6 +692,62 @@ __device__ __forceinline__ void diag_factor(T* __restrict__ A, int64_t ld, T* __
         }
     }
 }
+
+template <typename T>
+__device__ __forceinline__ void diag_factor(T* __restrict__ A, int64_t ld, T* __restrict__ Linv, int* __restrict__ info,
+                                            int64_t col0, unsigned char* smem_raw, const int t, int* dbg = nullptr,
+                                            long long* prof = nullptr) {
+#ifdef GPRX_DIAG_BLOCKED
+    if constexpr (std::is_same<T, double>::value) {
+        diag_factor_blocked<T>(A, ld, Linv, info, col0, smem_raw, t, prof);
+        return;
+    }
+#endif
+    // Default: the rank-8 register image.  The blocked form (GPRX_DIAG_BLOCKED, f64) was
+    // measured at 47.8 us per diagonal factor against 52 us, but its register demand raised
+    // the whole persistent kernel's spills from 10 to 29 VGPRs and the C3 factorisation by
+    // 0.6 ms (27.3 -> 28.0 ms): kept as a measured experiment, off.
+    diag_factor_rank8<T>(A, ld, Linv, info, col0, smem_raw, t, dbg, prof);
+}
+
+// Developer microbenchmark (gprx_dev_bench what 11 / 12): one workgroup factors `reps` fresh
+// 128 x 128 blocks (A + r * DB * ld) back to back with variant V (0 rank-8, 1 blocked); prof
+// accumulates the variant's phase ticks (wall clock, 100 MHz) over the reps.
+template <typename T, int V>
+__global__ __launch_bounds__(NT) void diag_bench_kernel(T* A, int64_t ld, T* Linv, int* info, long long* prof,
+                                                        int reps) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    long long acc[5] = {0, 0, 0, 0, 0};
+    long long ph[4] = {0, 0, 0, 0};
+    for (int r = 0; r < reps; r++) {
+        const long long t0 = wall_clock64();
+        if (V == 0) diag_factor_rank8<T>(A + (int64_t)r * DB * ld, ld, Linv, info, 0, smem_raw, threadIdx.x, nullptr, ph);
+        else diag_factor_blocked<T>(A + (int64_t)r * DB * ld, ld, Linv, info, 0, smem_raw, threadIdx.x, ph);
+        __syncthreads();
+        const long long t1 = wall_clock64();
+        acc[0] += ph[0];
+        acc[1] += ph[1];
+        acc[2] += ph[2];
+        acc[3] += ph[3];
+        acc[4] += t1 - t0;
+    }
+    if (threadIdx.x == 0)
+        for (int u = 0; u < 5; u++) prof[u] = acc[u];
+}
+
+template <typename T>
+void launch_diag_bench(int variant, T* A, int64_t ld, T* Linv, int* info, long long* prof, int reps, hipStream_t s) {
+    const size_t lds = diag_lds<T>() + 64;
+    auto go = [&](auto kfn) {
+        GPRX_HIP(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        hipLaunchKernelGGL(kfn, dim3(1), dim3(NT), lds, s, A, ld, Linv, info, prof, reps);
+    };
+    if (variant == 0 || !std::is_same<T, double>::value) go(diag_bench_kernel<T, 0>);
+    else go(diag_bench_kernel<T, 1>);
+    GPRX_HIP(hipGetLastError());
+}
+template void launch_diag_bench<double>(int, double*, int64_t, double*, int*, long long*, int, hipStream_t);
+template void launch_diag_bench<float>(int, float*, int64_t, float*, int*, long long*, int, hipStream_t);
 
 // ------------------------------------------------------------------------------------------
 // Hand-off helpers
@@ -970,8 +1016,8 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
             T* send = nullptr;
             if constexpr (DIST) send = a.dist->sptr[(int64_t)i * a.nc + j];
             if (!(a.variant & 1))
-                tile_gemm<T, false>(Cik, ld, Cik, ld, a.Linv + (int64_t)j * DB * DB, DB, GT, false, smem, tid, true,
-                                    nullptr, send);
+                tile_gemm<T, false, 1>(Cik, ld, Cik, ld, a.Linv + (int64_t)j * DB * DB, DB, GT, false, smem, tid, true,
+                                       nullptr, send);
             publish(a.lcnt + i, j + 1, false);
             if constexpr (DIST) {
                 if (send) publish_host(a.dist->hslot + (int64_t)i * a.nc + j);
@@ -984,15 +1030,15 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
                 T* Akm = Ci + (int64_t)(k - 1) * GT * ld;
                 T* send = nullptr;
                 if constexpr (DIST) send = a.dist->sptr[(int64_t)k * a.nc + (k - 1)];
-                tile_gemm<T, false>(Akm, ld, Akm, ld, a.Linv + (int64_t)(k - 1) * DB * DB, DB, GT, false, smem, tid,
-                                    true, nullptr, send);
+                tile_gemm<T, false, 1>(Akm, ld, Akm, ld, a.Linv + (int64_t)(k - 1) * DB * DB, DB, GT, false, smem,
+                                       tid, true, nullptr, send);
                 if (a.trace) dt[0] = wall_clock64();
                 publish(a.lcnt + k, k, false);  // L_{k,k-1} final: unblocks the updates of column k
                 if constexpr (DIST) {
                     if (send) publish_host(a.dist->hslot + (int64_t)k * a.nc + (k - 1));
                 }
                 if (a.trace) dt[1] = wall_clock64();
-                tile_gemm<T, true>(Akk, ld, Akm, ld, Akm, ld, GT, true, smem, tid);
+                tile_gemm<T, true, 2>(Akk, ld, Akm, ld, Akm, ld, GT, true, smem, tid);
                 local_sync();
             }
             if (a.trace) dt[2] = wall_clock64();
