@@ -39,6 +39,11 @@ __global__ void dev_fill_spd(T* A, int64_t ld, int64_t n, uint64_t seed) {
     A[e] = v;
 }
 
+__global__ void dev_fexp_kernel(const double* __restrict__ x, int64_t n, double* __restrict__ y) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) y[i] = fexp(x[i]);
+}
+
 template <typename T>
 static gprx_status bench_impl(int what, int64_t M, int64_t N, int64_t K, int iters, double* ms, Exec& ex) {
     hipStream_t s = ex.s0;
@@ -244,3 +249,17 @@ gprx_status gprx_dev_bench_impl(gprx_dtype dtype, int32_t what, int64_t M, int64
                              : bench_impl<float>(what, M, N, K, iters, ms, *ex);
 }
 }  // namespace gprx
+
+extern "C" gprx_status gprx_dev_fexp(gprx_ctx* ctx, const double* x, int64_t n, double* y) {
+    (void)ctx;
+    if (n <= 0) return GPRX_OK;
+    double *dx = nullptr, *dy = nullptr;
+    if (hipMalloc(&dx, sizeof(double) * n) != hipSuccess || hipMalloc(&dy, sizeof(double) * n) != hipSuccess)
+        return GPRX_ERR_OOM;
+    (void)hipMemcpy(dx, x, sizeof(double) * n, hipMemcpyHostToDevice);
+    hipLaunchKernelGGL(dev_fexp_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, dx, n, dy);
+    const hipError_t e = hipMemcpy(y, dy, sizeof(double) * n, hipMemcpyDeviceToHost);
+    (void)hipFree(dx);
+    (void)hipFree(dy);
+    return e == hipSuccess ? GPRX_OK : GPRX_ERR_HIP;
+}

@@ -161,6 +161,42 @@ __host__ __device__ inline T kernel_value(const KCanon<T>& K, T r2, T s0, T s1) 
     return v;
 }
 
+// exp for f64 in the pair-statistics epilogues (k_pairs.h leaf_into): x = (64 k + j) ln2/64 + r,
+// |r| <= ln2/128, exp(x) = 2^k 2^{j/64} (1 + expm1(r)) with a 64-entry table of 2^{j/64}
+// (correctly rounded) and a degree-5 polynomial for expm1 (truncation r^6/720 < 4e-17): 11 f64
+// operations against the 17 of the library's degree-11 sequence -- the epilogue's f64 VALU work
+// is serial with the tile's f64 MFMAs.  Error < 1 ulp + the final rounding;
+// x < -745 gives 0 (the library's underflow), NaN stays NaN.
+__device__ __constant__ const double kExp2Tab64[64] = {
+    1.0, 1.0108892860517005, 1.0218971486541166, 1.0330248790212284,
+    1.0442737824274138, 1.0556451783605572, 1.0671404006768237, 1.0787607977571199,
+    1.0905077326652577, 1.102382583307841, 1.1143867425958924, 1.1265216186082418,
+    1.1387886347566916, 1.1511892299529827, 1.1637248587775775, 1.1763969916502812,
+    1.189207115002721, 1.202156731452703, 1.215247359980469, 1.22848053610687,
+    1.241857812073484, 1.255380757024691, 1.2690509571917332, 1.2828700160787783,
+    1.2968395546510096, 1.3109612115247644, 1.3252366431597413, 1.339667524053303,
+    1.3542555469368927, 1.3690024229745905, 1.383909881963832, 1.3989796725383112,
+    1.4142135623730951, 1.42961333839197, 1.4451808069770467, 1.460917794180647,
+    1.4768261459394993, 1.4929077282912648, 1.5091644275934228, 1.5255981507445384,
+    1.5422108254079407, 1.559004400237837, 1.5759808451078865, 1.593142151342267,
+    1.6104903319492543, 1.6280274218573478, 1.645755478153965, 1.6636765803267364,
+    1.681792830507429, 1.7001063537185235, 1.718619298122478, 1.7373338352737062,
+    1.7562521603732995, 1.7753764925265212, 1.7947090750031072, 1.8142521755003989,
+    1.8340080864093424, 1.8539791250833855, 1.8741676341103, 1.8945759815869656,
+    1.9152065613971474, 1.9360617934922943, 1.9571441241754002, 1.978456026387951,
+};
+__device__ __forceinline__ double fexp(double x) {
+    const double kd = __builtin_rint(x * 92.33248261689366);  // 64 / ln2
+    double r = fma(-kd, 0.01083042469326756, x);             // ln2/64, high part (exact product)
+    r = fma(-kd, 2.9815858269852933e-12, r);                   // low part
+    const int n = (int)kd;
+    const double t = kExp2Tab64[n & 63];
+    const double p = fma(r * r, fma(r, fma(r, fma(r, 1.0 / 120.0, 1.0 / 24.0), 1.0 / 6.0), 0.5), r);
+    const double v = __builtin_ldexp(fma(t, p, t), n >> 6);
+    return x < -745.5 ? 0.0 : v;
+}
+__device__ __forceinline__ float fexp(float x) { return expf(x); }
+
 // sincos for both scalar types
 __device__ inline void gsincos(double x, double* s, double* c) { sincos(x, s, c); }
 __device__ inline void gsincos(float x, float* s, float* c) { sincosf(x, s, c); }

@@ -55,6 +55,9 @@ gprx_status gprx_dev_build_time(gprx_ctx* ctx, gprx_dtype dtype, const gprx_kern
  * with device copies in place of the RCCL broadcast / panel exchange (gprx_dist.cpp).  Models
  * of this context fit with the multi-GPU algorithm end to end on a single device. */
 gprx_status gprx_ctx_create_virtual(int device, int world, gprx_ctx** out);
+/* The pair-statistics epilogues' f64 exp (gprx_internal.h fexp) on n host values (accuracy
+ * test against the C library). */
+gprx_status gprx_dev_fexp(gprx_ctx* ctx, const double* x, int64_t n, double* y);
 #ifdef __cplusplus
 }
 #endif

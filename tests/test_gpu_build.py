@@ -150,3 +150,25 @@ def test_sparse_rejects_nonfinite_inputs(ctx):
     with pytest.raises(Exception) as e:
         ctx.sparse_fit("GaussianKernel(1,1,)", X, Y, X[::10].copy() + 0.01, 0.1, 1e-4)
     assert "not finite" in str(e.value)
+
+
+def test_fexp_accuracy(ctx):
+    """The epilogues' table-driven f64 exp (gprx_internal.h fexp) against numpy's exp: <= 2 ulp
+    over the arguments the kernels produce (c r2, c S <= 0, down to the underflow), 0 below
+    -745.5, NaN kept."""
+    import ctypes
+    from gpr_amd.gprx import lib
+    L = lib()
+    L.gprx_dev_fexp.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
+    rng = np.random.default_rng(7)
+    x = np.concatenate([-np.abs(rng.standard_normal(200000)) * 3, -rng.random(200000) * 745.0,
+                        rng.random(20000) * 20, np.linspace(-708.5, -700, 5000), [0.0, -0.0, -1e-300, -746.0, np.nan]])
+    y = np.empty_like(x)
+    assert L.gprx_dev_fexp(ctx.h, x.ctypes.data, x.size, y.ctypes.data) == 0
+    ref = np.exp(x)
+    fin = np.isfinite(x) & (x > -708)  # normal results: error in ulps of the reference
+    ulp = np.abs(y[fin] - ref[fin]) / np.spacing(ref[fin])
+    assert ulp.max() <= 2.0, ulp.max()
+    sub = np.isfinite(x) & (x <= -708) & (x >= -745.0)  # subnormal range: absolute error
+    assert np.max(np.abs(y[sub] - ref[sub])) <= 4 * np.spacing(0.0)
+    assert y[-2] == 0.0 and np.isnan(y[-1])
