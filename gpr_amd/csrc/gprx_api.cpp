@@ -259,6 +259,7 @@ struct gprx_model {
     // the current fit is one (its factor is held in tiles per rank: alpha and predict only)
     DistEngineBase* dist_engine = nullptr;
     bool dist_fitted = false;
+    bool dist_dense = false;  // the tiles of a distributed fit assembled into A (ld np) and Linv
     // a kernel with no device form: the caller evaluated K (n x n, row-major, T) -- the
     // reference's virtual Kernel<T>::operator() (include/Kernel.h:52-59); see k_hostk.hip
     bool host_k = false;
@@ -525,7 +526,7 @@ static gprx_status model_fit_dist(gprx_model* M, gprx_fit_info* out) {
     M->np = np;
     M->mp = GT;
     M->ld = 0;
-    M->fitted = M->has_alpha = M->inv_ready = M->dist_fitted = false;
+    M->fitted = M->has_alpha = M->inv_ready = M->dist_fitted = M->dist_dense = false;
     M->alpha.ensure(sizeof(T) * np * M->m);
     M->flag.ensure(sizeof(int));
     GPRX_HIP(hipMemsetAsync(M->flag.p, 0, sizeof(int), s));
@@ -591,10 +592,25 @@ static gprx_status model_fit_dist(gprx_model* M, gprx_fit_info* out) {
         M->A.ensure(sizeof(T) * np * np);
         M->Linv.ensure(sizeof(T) * np * DB);
         dist_assemble_factor<T>(M->dist_engine, M->A.as<T>(), np, M->Linv.as<T>(), s);
+        M->dist_dense = true;
         model_inverse<T>(M);
         M->inv_ready = true;
     }
     return GPRX_OK;
+}
+
+// The dense factor of a distributed fit on this process, for the calls that solve with the
+// whole factor (posterior covariance, core matrix): every rank holds every tile after the fit
+// (its own and the received ones), assembled once per fit into A (ld np) and Linv.
+template <typename T>
+static void ensure_dense_factor(gprx_model* M) {
+    if (!M->dist_fitted || M->dist_dense) return;
+    const int64_t np = M->np;
+    M->ld = np;
+    M->A.ensure(sizeof(T) * np * np);
+    M->Linv.ensure(sizeof(T) * np * DB);
+    dist_assemble_factor<T>(M->dist_engine, M->A.as<T>(), np, M->Linv.as<T>(), M->ctx->stream);
+    M->dist_dense = true;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -836,9 +852,8 @@ template <typename T>
 static gprx_status model_posterior_cov(gprx_model* M, const void* Xa, const void* Xb, int64_t q, void* out) {
     GPRX_REQUIRE(M->fitted || M->sparse_cov, GPRX_ERR_STATE,
                  "GaussianProcess::ComputeKernelVectorInternal: gaussian process is not initialized.");
-    GPRX_REQUIRE(!M->dist_fitted, GPRX_ERR_STATE,
-                 "gprx: the posterior covariance needs a single-GPU fit (a distributed fit keeps its factor in tiles)");
     GPRX_REQUIRE(!M->host_k, GPRX_ERR_STATE, "gprx: a caller-evaluated kernel uses gprx_model_posterior_cov_kx");
+    ensure_dense_factor<T>(M);
     hipStream_t s = M->ctx->stream;
     const KCanon<T>& K = kcanon<T>(M);
     const int d = M->d;
@@ -928,8 +943,7 @@ static void lu_inverse(gprx_model* M, DevBuf& luC) {
 template <typename T>
 static gprx_status model_core_matrix(gprx_model* M, void* Cout) {
     GPRX_REQUIRE(M->fitted, GPRX_ERR_STATE, "gprx: model is not fitted");
-    GPRX_REQUIRE(!M->dist_fitted, GPRX_ERR_STATE,
-                 "gprx: the core matrix needs a single-GPU fit (a distributed fit keeps its factor in tiles)");
+    ensure_dense_factor<T>(M);
     hipStream_t s = M->ctx->stream;
     if (M->method == 1) {  // dgetri_'s inverse (include/LAPACKUtils.h:49) from the LU factors
         DevBuf luC;

@@ -91,7 +91,7 @@ def test_virtual_ranks_f32(g):
 
 def test_virtual_ranks_repeat_and_lml_value():
     """Several fits on one engine (counters, flags and receive buffers reset per fit), the
-    LML value from the distributed factor, and the factor-based calls refused."""
+    LML value from the distributed factor, and a factor-based call after them."""
     import gpr_amd
     n, d, sigma = 900, 3, 0.4
     X, Y = make_data(n, d, 1)
@@ -111,8 +111,10 @@ def test_virtual_ranks_repeat_and_lml_value():
         # ... and the reference's value, whose determinant underflows double here (clamped)
         vc, _, _ = M.lml(grad=False, compat=True)
         assert abs(vc - vr) <= 1e-6 * abs(vr)
-        with pytest.raises(gpr_amd.GprxError):
-            M.posterior_cov(X[:3], X[:3])
+        # the factor-based calls assemble the tiles (test_virtual_ranks_posterior_and_core):
+        # at the training points the posterior variance is at most the noise-free prior
+        pv = M.posterior_cov(X[:3], X[:3])
+        assert np.all(np.isfinite(pv)) and np.all(pv >= -1e-10)
         M.close()
     finally:
         vctx.close()
@@ -207,3 +209,27 @@ def test_rccl_one_rank_lml_grad():
         M.close()
     finally:
         dctx.close()
+
+
+@pytest.mark.parametrize("g", [2, 3])
+def test_virtual_ranks_posterior_and_core(g):
+    """operator()(x,y) / GetCredibleInterval (lib/GaussianProcess.cpp:84-114) and the core
+    matrix (:513-528) on a distributed fit: the factor every rank holds as tiles (its own and the
+    received ones) is assembled once into a dense factor, then the single-GPU solves run."""
+    import gpr_amd
+    n, d, sigma = 900, 4, 0.5
+    X, Y = make_data(n, d, 1)
+    vctx = gpr_amd.Context(0, virtual=g)
+    try:
+        M, _ = _fit(vctx, C3K, X, Y, sigma, np.float64)
+        _, C_ref = O.fit(C3K, X, Y, sigma)
+        Xa, Xb = make_queries(40, d), make_queries(40, d)[::-1].copy()
+        assert relerr(M.posterior_cov(Xa, Xb), O.posterior_cov(C3K, X, C_ref, Xa, Xb)) <= 1e-6
+        var = M.posterior_cov(Xa, Xa)
+        assert relerr(var, O.posterior_cov(C3K, X, C_ref, Xa, Xa)) <= 1e-6
+        assert relerr(M.core_matrix(), C_ref) <= 1e-6
+        M.fit()  # a refit drops the assembled factor; the next call assembles the new one
+        assert relerr(M.posterior_cov(Xa, Xa), var) <= 1e-12
+        M.close()
+    finally:
+        vctx.close()
