@@ -60,7 +60,7 @@ static gprx_status bench_impl(int what, int64_t M, int64_t N, int64_t K, int ite
     int* info = (int*)alloc(sizeof(int));
     float tms = 0;
     try {
-        if (what == 11 || what == 12) {  // tile-engine diagonal factor (k_ptiles.hip), variant what - 11:
+        if (what == 11 || what == 12 || what == 13) {  // tile-engine diagonal factor (k_ptiles.hip), variant what - 11:
             // ms[0] = us per factor (events), ms[1..5] = per-factor phase ticks (100 MHz)
             const int reps = std::max(1, iters);
             T* A = (T*)alloc(sizeof(T) * DB * DB * (size_t)reps);
@@ -262,4 +262,33 @@ extern "C" gprx_status gprx_dev_fexp(gprx_ctx* ctx, const double* x, int64_t n, 
     (void)hipFree(dx);
     (void)hipFree(dy);
     return e == hipSuccess ? GPRX_OK : GPRX_ERR_HIP;
+}
+
+extern "C" gprx_status gprx_dev_diag_factor(gprx_ctx* ctx, int32_t variant, const double* A, double* L, double* Linv,
+                                            int32_t* info_out) {
+    (void)ctx;
+    if (variant < 0 || variant > 2 || !A || !L || !Linv || !info_out) return GPRX_ERR_ARG;
+    double *dA = nullptr, *dLi = nullptr;
+    int* di = nullptr;
+    long long* pr = nullptr;
+    const size_t b = sizeof(double) * DB * DB;
+    gprx_status st = GPRX_OK;
+    if (hipMalloc(&dA, b) != hipSuccess || hipMalloc(&dLi, b) != hipSuccess || hipMalloc(&di, sizeof(int)) != hipSuccess ||
+        hipMalloc(&pr, sizeof(long long) * 8) != hipSuccess) {
+        st = GPRX_ERR_OOM;
+    } else {
+        const int big = 0x7fffffff;
+        (void)hipMemcpy(dA, A, b, hipMemcpyHostToDevice);
+        (void)hipMemcpy(di, &big, sizeof(int), hipMemcpyHostToDevice);
+        pt::launch_diag_bench<double>(variant, dA, DB, dLi, di, pr, 1, 0);
+        if (hipMemcpy(L, dA, b, hipMemcpyDeviceToHost) != hipSuccess ||
+            hipMemcpy(Linv, dLi, b, hipMemcpyDeviceToHost) != hipSuccess ||
+            hipMemcpy(info_out, di, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
+            st = GPRX_ERR_HIP;
+    }
+    (void)hipFree(dA);
+    (void)hipFree(dLi);
+    (void)hipFree(di);
+    (void)hipFree(pr);
+    return st;
 }

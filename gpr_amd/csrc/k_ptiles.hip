@@ -138,12 +138,13 @@ __device__ __forceinline__ void tile_gemm(T* __restrict__ C, int64_t ldc, const 
 constexpr int SPL = DB + 4;
 constexpr int SIL = DB + 2;
 
+// v_rsq_f64 (relative error ~2^-23) refined by ONE Halley step, y (1 + e/2 + 3e^2/8) with
+// e = 1 - x y^2 (cubic convergence: error ~2^-69 before rounding): 4 dependent f64 operations
+// after the rsq against the 6 of two Newton steps -- the pivot chain is latency-bound
 __device__ __forceinline__ double rsqrt_full(double x) {
-    double y = __builtin_amdgcn_rsq(x);
-    const double h = 0.5 * x;
-    y = y * fma(-h * y, y, 1.5);
-    y = y * fma(-h * y, y, 1.5);
-    return y;
+    const double y = __builtin_amdgcn_rsq(x);
+    const double e = fma(-x * y, y, 1.0);
+    return fma(y * e, fma(e, 0.375, 0.5), y);
 }
 __device__ __forceinline__ float rsqrt_full(float x) {
     float y = __builtin_amdgcn_rsqf(x);
@@ -154,8 +155,10 @@ __device__ __forceinline__ float rsqrt_full(float x) {
 
 template <typename T>
 constexpr size_t diag_lds() {
-    return sizeof(T) * ((size_t)DB * SIL + DB) > sizeof(T) * (2 * 8 * SPL + 144) ? sizeof(T) * ((size_t)DB * SIL + DB)
-                                                                              : sizeof(T) * (2 * 8 * SPL + 144);
+    // (DB + 2 diagonal words: diag_factor_la keeps a zero after sDi)
+    return sizeof(T) * ((size_t)DB * SIL + DB + 2) > sizeof(T) * (2 * 8 * SPL + 144)
+               ? sizeof(T) * ((size_t)DB * SIL + DB + 2)
+               : sizeof(T) * (2 * 8 * SPL + 144);
 }
 
 __device__ __forceinline__ void dbg_mark(int* dbg, int q, int phase, int i, int j) {
@@ -411,6 +414,7 @@ __device__ __forceinline__ void fact32(T* __restrict__ sS, T* __restrict__ sDi, 
             // the 4 x 4 pivot block (lower) of tile (tc, tc): P[i][j] at lane (pl + i) + 16 j;
             // its factor, then Q = L_P^{-1}, reduced to this lane's row qr = Q[lk][.]
             double qr[4];
+            double lpv = 0.0;  // this lane's entry of L_P when it holds a pivot row
             {
                 double Lp[4][4], rq[4];
 #pragma unroll
@@ -428,6 +432,16 @@ __device__ __forceinline__ void fact32(T* __restrict__ sS, T* __restrict__ sDi, 
                     if (!(dsum > 0.0) && fail < 0) fail = c0 + k0 + i;
                     rq[i] = rsqrt_full(dsum);
                     Lp[i][i] = dsum * rq[i];
+                }
+                {  // lpv = L_P[lr - pl][lk] (0 above the diagonal): a two-level select
+                    double cv[4];
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        cv[j] = 0.0;
+#pragma unroll
+                        for (int i = j; i < 4; i++) cv[j] = (lr - pl == i) ? Lp[i][j] : cv[j];
+                    }
+                    lpv = (lk == 0) ? cv[0] : (lk == 1) ? cv[1] : (lk == 2) ? cv[2] : cv[3];
                 }
                 double Q[4][4];
 #pragma unroll
@@ -449,7 +463,9 @@ __device__ __forceinline__ void fact32(T* __restrict__ sS, T* __restrict__ sDi, 
                     qr[i] = v;
                 }
             }
-            // panel: L[r][k0 + lk] = sum_{i <= lk} a[r][k0 + i] Q[lk][i] (D rows above k0 kept)
+            // panel: L[r][k0 + lk] = sum_{i <= lk} a[r][k0 + i] Q[lk][i] (D rows above k0 kept; the
+            // pivot rows take L_P itself -- recomputing them as A_P Q^T costs accuracy on
+            // ill-conditioned blocks)
             double pv[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
             for (int tr = 0; tr < 4; tr++) {
@@ -460,7 +476,10 @@ __device__ __forceinline__ void fact32(T* __restrict__ sS, T* __restrict__ sDi, 
                 for (int i = 0; i < 4; i++) nv = fma(__shfl(v, lr + 16 * i, 64), qr[i], nv);
                 const bool keep = tr < 2 && 16 * tr + lr < k0;
                 pv[tr] = keep ? v : nv;
-                acc[TI[tr][tc]][rg] = pv[tr];
+                // (the trailing update masks the pivot rows out of both operands, so their
+                // exact L_P values are off the critical path)
+                const bool piv = tr == tc && lr >= pl && lr < pl + 4;
+                acc[TI[tr][tc]][rg] = piv ? lpv : pv[tr];
             }
             // trailing: tile (tr, tcp) -= panel(tr) panel_D(tcp)^T over the columns > k0 + 3
 #pragma unroll
@@ -693,25 +712,307 @@ __device__ __forceinline__ void diag_factor_blocked(T* __restrict__ A, int64_t l
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// Diagonal 128x128 block, blocked with LOOK-AHEAD (f64): the same LDS image and 32-column
+// panels as diag_factor_blocked, but only the critical chain stays serial.  Per panel p
+// (c0 = 32 p), 16 x 16 tile indices R, C = 0..7:
+//   F(p)   wave 0: fact32 (the 32 x 32 diagonal block: L_pp, Dinv_p)
+//          waves 1-7 meanwhile: the far trailing tiles of panel p-1 (C >= 2p + 2) and Linv's
+//          row block p-1 (Linv_{p-1,j} = -Dinv_{p-1} sum_{k=j}^{p-2} L_{p-1,k} Linv_kj, one wave
+//          per (j, 16-column) unit: S staged in the unit's own slot, wave-private, no barrier)
+//   P(p)   all waves: L_rp = A_rp Dinv_p^T for the rows below
+//   Ua(p)  all waves: the trailing tiles of the NEXT panel's columns only (C = 2p+2, 2p+3)
+// so F(p+1) starts after a panel solve and a 32-column update instead of the whole trailing
+// update and the Linv assembly.  Linv's last row block follows F(3).  Every region a phase
+// writes is disjoint from what the concurrent waves read or write (see the phase comments).
+// ------------------------------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ T linv_at(const T* __restrict__ sS, const T* __restrict__ sDi, int R, int C) {
+    // Linv[R][C] of the LDS image: strict lower part kept transposed in the upper triangle, the
+    // diagonal in sDi (= sS + DB SIL), a zero in sDi[DB].  One unconditional load from a selected
+    // address: a conditional load compiles to an exec-masked branch per element.
+    (void)sDi;
+    const int idx = (R > C) ? C + R * SIL : DB * SIL + (R == C ? R : DB);
+    return sS[idx];
+}
+
+// one 16 x 16 lower tile (R, C) of the trailing matrix: A_RC -= L_{R,panel} L_{C,panel}^T (K = 32)
+template <typename T>
+__device__ __forceinline__ void la_trail_tile(T* __restrict__ sS, int c0, int R, int C, int lr, int lk) {
+    typedef Mfma<T> Tr;
+    typename Tr::acc_t acc = typename Tr::acc_t{0};
+#pragma unroll
+    for (int kq = 0; kq < 8; kq++) {
+        const int k = c0 + kq * 4 + lk;
+        acc = Tr::mma(sS[(16 * C + lr) + k * SIL], sS[(16 * R + lr) + k * SIL], acc);
+    }
+#pragma unroll
+    for (int reg = 0; reg < 4; reg++) sS[(16 * R + lr) + (16 * C + Tr::orow(lk, reg)) * SIL] -= acc[reg];
+}
+
+// Linv row block p, column block j, 16-column half ct (rows 32 p .. 32 p + 31): one wave.
+// S = sum_{kb_lo <= kb < kb_hi} L_{p,kb} Linv_{kb,j} (LA_LOAD: plus the partial S staged by an
+// earlier call), staged transposed in the unit's own Linv slot; LA_FINISH: Linv_pj = -Dinv_p S.
+enum { LA_LOAD = 1, LA_FINISH = 2 };
+template <typename T>
+__device__ __forceinline__ void la_linv_unit(T* __restrict__ sS, const T* __restrict__ sDi, int p, int j, int ct,
+                                             int kb_lo, int kb_hi, int mode, int lr, int lk) {
+    typedef Mfma<T> Tr;
+    typedef typename Tr::acc_t acc_t;
+    acc_t s0 = acc_t{0}, s1 = acc_t{0};
+    const int cc = 32 * j + 16 * ct + lr;  // Linv column this lane feeds
+    if (mode & LA_LOAD) {
+#pragma unroll
+        for (int reg = 0; reg < 4; reg++) {
+            const int c = 32 * j + 16 * ct + Tr::orow(lk, reg);
+            s0[reg] = sS[c + (32 * p + lr) * SIL];
+            s1[reg] = sS[c + (32 * p + 16 + lr) * SIL];
+        }
+    }
+#pragma unroll 1
+    for (int kb = kb_lo; kb < kb_hi; kb++) {
+#pragma unroll
+        for (int kq = 0; kq < 8; kq++) {
+            const int kk = 32 * kb + kq * 4 + lk;
+            const T av = linv_at(sS, sDi, kk, cc);  // Linv[kk][cc]
+            s0 = Tr::mma(av, sS[(32 * p + lr) + kk * SIL], s0);
+            s1 = Tr::mma(av, sS[(32 * p + 16 + lr) + kk * SIL], s1);
+        }
+    }
+    // stage S (rows 32p + r, columns 32j + 16ct + c) transposed in the unit's own Linv slot
+#pragma unroll
+    for (int reg = 0; reg < 4; reg++) {
+        const int c = 32 * j + 16 * ct + Tr::orow(lk, reg);
+        sS[c + (32 * p + lr) * SIL] = s0[reg];
+        sS[c + (32 * p + 16 + lr) * SIL] = s1[reg];
+    }
+    if (!(mode & LA_FINISH)) return;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // Linv_pj = -Dinv_p S
+    acc_t o0 = acc_t{0}, o1 = acc_t{0};
+#pragma unroll
+    for (int kq = 0; kq < 8; kq++) {
+        const int kk = kq * 4 + lk;
+        const T av = sS[cc + (32 * p + kk) * SIL];  // S[kk][cc]
+        o0 = Tr::mma(av, linv_at(sS, sDi, 32 * p + lr, 32 * p + kk), o0);
+        o1 = Tr::mma(av, linv_at(sS, sDi, 32 * p + 16 + lr, 32 * p + kk), o1);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int reg = 0; reg < 4; reg++) {
+        const int c = 32 * j + 16 * ct + Tr::orow(lk, reg);
+        sS[c + (32 * p + lr) * SIL] = -o0[reg];
+        sS[c + (32 * p + 16 + lr) * SIL] = -o1[reg];
+    }
+}
+
+// global stores of finished pieces, spread over the threads tid0 .. tid0 + nth - 1:
+// L's panel q (rows 32 q .. 127, columns 32 q .. 32 q + 31) and Linv's row block q (all columns)
+template <typename T>
+__device__ __forceinline__ void la_store_lpanel(T* __restrict__ A, int64_t ld, const T* __restrict__ sS, int q, int tid,
+                                                int nth) {
+    const int nr = DB - 32 * q;
+    for (int e = tid; e < 32 * nr; e += nth) {
+        const int c = 32 * q + e / nr, r = 32 * q + e % nr;
+        A[r + (int64_t)c * ld] = sS[r + c * SIL];
+    }
+}
+template <typename T>
+__device__ __forceinline__ void la_store_linv_rows(T* __restrict__ Linv, const T* __restrict__ sS,
+                                                   const T* __restrict__ sDi, int q, int tid, int nth) {
+    for (int e = tid; e < 32 * DB; e += nth) {
+        const int c = e >> 5, r = 32 * q + (e & 31);
+        Linv[r + c * DB] = linv_at(sS, sDi, r, c);
+    }
+}
+
+// F(p)'s side phase, waves wlo..7: the stores of what panel p-1 finished (L panel p-1, Linv
+// row block p-2), then the jobs -- Linv row block p-1 (2 (p-1) units), at p = 3 also the
+// partial sums of Linv row block 3 over kb < 2 (4 units), then the far trailing tiles of panel
+// p-1 (C >= 2p + 2, R >= C)
+template <typename T>
+__device__ __forceinline__ void la_side(T* __restrict__ A, int64_t ld, T* __restrict__ Linv, T* __restrict__ sS,
+                                        const T* __restrict__ sDi, int p, int t, int w, int wlo, int lr, int lk) {
+    const int nth = NT - 64 * wlo, tid = t - 64 * wlo;
+    la_store_lpanel<T>(A, ld, sS, p - 1, tid, nth);
+    if (p >= 2) la_store_linv_rows<T>(Linv, sS, sDi, p - 2, tid, nth);
+    const int pl = p - 1, nl = 2 * pl, np3 = (p == 3) ? 4 : 0;
+    const int cmin = 2 * p + 2, nc = 8 - cmin, nt = nc > 0 ? nc * (nc + 1) / 2 : 0;
+    const int nw = 8 - wlo;
+#pragma unroll 1
+    for (int job = w - wlo; job < nl + np3 + nt; job += nw) {
+        if (job < nl) {
+            la_linv_unit<T>(sS, sDi, pl, job >> 1, job & 1, job >> 1, pl, LA_FINISH, lr, lk);
+        } else if (job < nl + np3) {
+            const int u = job - nl;
+            la_linv_unit<T>(sS, sDi, 3, u >> 1, u & 1, u >> 1, 2, 0, lr, lk);
+        } else {
+            const int tt = job - nl - np3;  // lower tiles of the C >= cmin square, row-major
+            int rr = 0;
+            while ((rr + 1) * (rr + 2) / 2 <= tt) rr++;
+            const int cc = tt - rr * (rr + 1) / 2;
+            la_trail_tile<T>(sS, 32 * pl, cmin + rr, cmin + cc, lr, lk);
+        }
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ void diag_factor_la(T* __restrict__ A, int64_t ld, T* __restrict__ Linv,
+                                               int* __restrict__ info, int64_t col0, unsigned char* smem_raw,
+                                               const int t, long long* prof = nullptr) {
+    typedef Mfma<T> Tr;
+    typedef typename Tr::acc_t acc_t;
+    constexpr int SL = SIL;
+    T* sS = reinterpret_cast<T*>(smem_raw);
+    T* sDi = sS + (size_t)DB * SL;
+    const int w = t >> 6, lane = t & 63, lr = lane & 15, lk = lane >> 4;
+    long long pt0 = prof ? wall_clock64() : 0, pf = 0, pside = 0, pfw = 0;
+    {
+        const int r = t & (DB - 1), cq = t >> 7;
+        T v[DB / (NT / DB)];
+#pragma unroll
+        for (int u = 0; u < DB / (NT / DB); u++) v[u] = A[r + (int64_t)(cq + u * (NT / DB)) * ld];
+#pragma unroll
+        for (int u = 0; u < DB / (NT / DB); u++) sS[r + (cq + u * (NT / DB)) * SL] = v[u];
+        if (t == 0) sDi[DB] = T(0);  // linv_at's zero
+    }
+    __syncthreads();
+    const long long pload = prof ? wall_clock64() : 0;
+    int fail = -1;
+#pragma unroll 1
+    for (int p = 0; p < 4; p++) {
+        const int c0 = 32 * p;
+        const long long tf0 = prof ? wall_clock64() : 0;
+        // ---- F(p): wave 0 factors the diagonal block; the others finish panel p-1's side work
+        // (fact32 touches block (p, p) only; the far trailing tiles have C >= 2p + 2; the Linv
+        // units write rows 32 (p - 1) .. 32 p - 1 (p = 3: also 96 .. 127) of columns < 32 (p - 1),
+        // transposed: LDS columns >= 32 (p - 1), rows < 32 (p - 1); the stores only read)
+        if (w == 0) {
+            fact32<T>(sS, sDi, c0, fail);
+            if (prof) pfw += wall_clock64() - tf0;
+        } else if (p > 0) {
+            la_side<T>(A, ld, Linv, sS, sDi, p, t, w, 1, lr, lk);
+        }
+        __syncthreads();
+        if (prof) {
+            const long long tn = wall_clock64();
+            pf += tn - tf0;
+        }
+        if (p == 3) break;
+        const long long ts0 = prof ? wall_clock64() : 0;
+        // ---- P(p): L_rp = A_rp Dinv_p^T for the rows below; one 16-row tile per wave (both of
+        // its 16-column halves), so a wave overwrites only what it read: no barrier inside.
+        // The explicit inverse alone is not backward stable when L_pp is ill-conditioned (a
+        // sparse-GP normal matrix with cond 1.5e13 lost positive definiteness at pivot 35):
+        // one step of refinement, X += (A - X L_pp^T) Dinv_p^T, restores the substitution's
+        // accuracy (numpy emulation: residual 5.8e-10 against 4.7e-10 for dtrsm).
+        const int r0 = c0 + 32, nrt = (DB - r0) / 16;
+        if (w < nrt) {
+            acc_t a0 = acc_t{0}, a1 = acc_t{0};
+            const int rr = r0 + w * 16 + lr;
+            T av0[4], av1[4];
+#pragma unroll
+            for (int reg = 0; reg < 4; reg++) {  // A_rp in the accumulator layout (for the residual)
+                av0[reg] = sS[rr + (c0 + Tr::orow(lk, reg)) * SL];
+                av1[reg] = sS[rr + (c0 + 16 + Tr::orow(lk, reg)) * SL];
+            }
+#pragma unroll
+            for (int kq = 0; kq < 8; kq++) {
+                const int k = kq * 4 + lk;
+                const T bv = sS[rr + (c0 + k) * SL];
+                a0 = Tr::mma(linv_at(sS, sDi, c0 + lr, c0 + k), bv, a0);
+                a1 = Tr::mma(linv_at(sS, sDi, c0 + 16 + lr, c0 + k), bv, a1);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int reg = 0; reg < 4; reg++) {  // X0 (kept in a0, a1) through LDS to the operand layout
+                sS[rr + (c0 + Tr::orow(lk, reg)) * SL] = a0[reg];
+                sS[rr + (c0 + 16 + Tr::orow(lk, reg)) * SL] = a1[reg];
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            acc_t q0 = acc_t{0}, q1 = acc_t{0};  // X0 L_pp^T
+#pragma unroll
+            for (int kq = 0; kq < 8; kq++) {
+                const int k = kq * 4 + lk;
+                const T xv = sS[rr + (c0 + k) * SL];
+                const T l0v = sS[(c0 + lr) + (c0 + k) * SL], l1v = sS[(c0 + 16 + lr) + (c0 + k) * SL];
+                const T l0 = (lr >= k) ? l0v : T(0), l1 = (16 + lr >= k) ? l1v : T(0);  // above: Dinv
+                q0 = Tr::mma(l0, xv, q0);
+                q1 = Tr::mma(l1, xv, q1);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int reg = 0; reg < 4; reg++) {  // R = A - X0 L^T, to the operand layout
+                sS[rr + (c0 + Tr::orow(lk, reg)) * SL] = av0[reg] - q0[reg];
+                sS[rr + (c0 + 16 + Tr::orow(lk, reg)) * SL] = av1[reg] - q1[reg];
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int kq = 0; kq < 8; kq++) {
+                const int k = kq * 4 + lk;
+                const T rv = sS[rr + (c0 + k) * SL];
+                a0 = Tr::mma(linv_at(sS, sDi, c0 + lr, c0 + k), rv, a0);
+                a1 = Tr::mma(linv_at(sS, sDi, c0 + 16 + lr, c0 + k), rv, a1);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int reg = 0; reg < 4; reg++) {
+                sS[rr + (c0 + Tr::orow(lk, reg)) * SL] = a0[reg];
+                sS[rr + (c0 + 16 + Tr::orow(lk, reg)) * SL] = a1[reg];
+            }
+        }
+        __syncthreads();
+        // ---- Ua(p): the next panel's columns (C = 2p+2, 2p+3; R >= C), all waves -------------
+        {
+            const int Cn = 2 * p + 2, n0 = 8 - Cn, ntl = n0 + (n0 - 1);
+#pragma unroll 1
+            for (int tt = w; tt < ntl; tt += 8) {
+                const int C = tt < n0 ? Cn : Cn + 1;
+                const int R = tt < n0 ? Cn + tt : Cn + 1 + (tt - n0);
+                la_trail_tile<T>(sS, c0, R, C, lr, lk);
+            }
+        }
+        __syncthreads();
+        if (prof) pside += wall_clock64() - ts0;
+    }
+    if (fail >= 0) atomicMin(info, (int)(col0 + fail + 1));  // wave 0, every lane the same value
+    // Linv's last row block: the kb = 2 term and -Dinv_3 S (6 units, waves 0-5); the stores of
+    // L panel 3 and Linv row block 2 by waves 6-7 meanwhile
+    if (w < 6) {
+        const int j = w >> 1;
+        la_linv_unit<T>(sS, sDi, 3, j, w & 1, 2, 3, (j < 2 ? LA_LOAD : 0) | LA_FINISH, lr, lk);
+    } else {
+        la_store_lpanel<T>(A, ld, sS, 3, t - 384, 128);
+        la_store_linv_rows<T>(Linv, sS, sDi, 2, t - 384, 128);
+    }
+    __syncthreads();
+    la_store_linv_rows<T>(Linv, sS, sDi, 3, t, NT);
+    if (prof && t == 0) {  // load, F phases (barrier to barrier), P + Ua phases, fact32 alone
+        prof[0] = pload - pt0;
+        prof[1] = pf;
+        prof[2] = pside;
+        prof[3] = pfw;
+    }
+}
+
 template <typename T>
 __device__ __forceinline__ void diag_factor(T* __restrict__ A, int64_t ld, T* __restrict__ Linv, int* __restrict__ info,
                                             int64_t col0, unsigned char* smem_raw, const int t, int* dbg = nullptr,
                                             long long* prof = nullptr) {
-#ifdef GPRX_DIAG_BLOCKED
+#ifndef GPRX_DIAG_RANK8
+    // f64: the blocked factor with look-ahead (diag_factor_la: 38 us per block in isolation
+    // against 50.6 for the rank-8 image, scripts/diag_bench.py)
     if constexpr (std::is_same<T, double>::value) {
-        diag_factor_blocked<T>(A, ld, Linv, info, col0, smem_raw, t, prof);
+        diag_factor_la<T>(A, ld, Linv, info, col0, smem_raw, t, prof);
         return;
     }
 #endif
-    // Default: the rank-8 register image.  The blocked form (GPRX_DIAG_BLOCKED, f64) was
-    // measured at 47.8 us per diagonal factor against 52 us, but its register demand raised
-    // the whole persistent kernel's spills from 10 to 29 VGPRs and the C3 factorisation by
-    // 0.6 ms (27.3 -> 28.0 ms): kept as a measured experiment, off.
+    // f32 (and GPRX_DIAG_RANK8): the rank-8 register image
     diag_factor_rank8<T>(A, ld, Linv, info, col0, smem_raw, t, dbg, prof);
 }
 
 // Developer microbenchmark (gprx_dev_bench what 11 / 12): one workgroup factors `reps` fresh
-// 128 x 128 blocks (A + r * DB * ld) back to back with variant V (0 rank-8, 1 blocked); prof
+// 128 x 128 blocks (A + r * DB * ld) back to back with variant V (0 rank-8, 1 blocked, 2 look-ahead); prof
 // accumulates the variant's phase ticks (wall clock, 100 MHz) over the reps.
 template <typename T, int V>
 __global__ __launch_bounds__(NT) void diag_bench_kernel(T* A, int64_t ld, T* Linv, int* info, long long* prof,
@@ -722,7 +1023,8 @@ __global__ __launch_bounds__(NT) void diag_bench_kernel(T* A, int64_t ld, T* Lin
     for (int r = 0; r < reps; r++) {
         const long long t0 = wall_clock64();
         if (V == 0) diag_factor_rank8<T>(A + (int64_t)r * DB * ld, ld, Linv, info, 0, smem_raw, threadIdx.x, nullptr, ph);
-        else diag_factor_blocked<T>(A + (int64_t)r * DB * ld, ld, Linv, info, 0, smem_raw, threadIdx.x, ph);
+        else if (V == 1) diag_factor_blocked<T>(A + (int64_t)r * DB * ld, ld, Linv, info, 0, smem_raw, threadIdx.x, ph);
+        else diag_factor_la<T>(A + (int64_t)r * DB * ld, ld, Linv, info, 0, smem_raw, threadIdx.x, ph);
         __syncthreads();
         const long long t1 = wall_clock64();
         acc[0] += ph[0];
@@ -743,7 +1045,8 @@ void launch_diag_bench(int variant, T* A, int64_t ld, T* Linv, int* info, long l
         hipLaunchKernelGGL(kfn, dim3(1), dim3(NT), lds, s, A, ld, Linv, info, prof, reps);
     };
     if (variant == 0 || !std::is_same<T, double>::value) go(diag_bench_kernel<T, 0>);
-    else go(diag_bench_kernel<T, 1>);
+    else if (variant == 1) go(diag_bench_kernel<T, 1>);
+    else go(diag_bench_kernel<T, 2>);
     GPRX_HIP(hipGetLastError());
 }
 template void launch_diag_bench<double>(int, double*, int64_t, double*, int*, long long*, int, hipStream_t);
@@ -1006,8 +1309,11 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
                                    i == j, smem, tid, false, bp);
             } else {
                 const int64_t ob = (a.variant & 64) ? GT : (int64_t)j * GT + (int64_t)b0 * GT * ld;
+                // variant 128 (timing experiment, wrong results): operand stride 0 along k, every
+                // k-slice of the update re-reads the same 1 KB column -- a truly cache-resident feed
+                const int64_t lop = (a.variant & 128) ? 0 : ld;
                 if (!(a.variant & 2))
-                    tile_gemm<T, true>(Ci + (int64_t)j * GT * ld, ld, a.A + oa, ld, a.A + ob, ld, nb * GT, i == j,
+                    tile_gemm<T, true>(Ci + (int64_t)j * GT * ld, ld, a.A + oa, lop, a.A + ob, lop, nb * GT, i == j,
                                        smem, tid);
             }
             publish(a.ver + (int64_t)i * a.nc + j, b0 + nb, false);

@@ -16,7 +16,9 @@ extern "C" {
  *           s_memtime ticks per launch of (load, solve phases, update phases, store, total),
  *       7 = potrf with look-ahead replayed from a captured hipGraph, 8 = backsolve from a graph,
  *       9 = potrf as one persistent tile-dataflow launch (potrf_tiles),
- *      10 = back substitution as one flag-chained launch (launch_backsolve_chain).
+ *      10 = back substitution as one flag-chained launch (launch_backsolve_chain),
+ *      11 / 12 / 13 = the tile engine's diagonal-block factor, variant what - 11 (rank-8 /
+ *           blocked / look-ahead): ms[0] = us per factor, ms[1..5] = phase ticks (100 MHz).
  * For 1/2: (M, N, K) are the gemm sizes; for 3/4/5: M = n.  Returns the mean device time
  * per call over `iters` calls (HIP events) in *ms. */
 gprx_status gprx_dev_bench(gprx_ctx* ctx, gprx_dtype dtype, int32_t what, int64_t M, int64_t N, int64_t K,
@@ -55,6 +57,12 @@ gprx_status gprx_dev_build_time(gprx_ctx* ctx, gprx_dtype dtype, const gprx_kern
  * with device copies in place of the RCCL broadcast / panel exchange (gprx_dist.cpp).  Models
  * of this context fit with the multi-GPU algorithm end to end on a single device. */
 gprx_status gprx_ctx_create_virtual(int device, int world, gprx_ctx** out);
+/* Parity hook for the tile engine's diagonal-block factor: the 128 x 128 SPD block A (column-
+ * major, host) factored by variant 0 (rank-8 register image), 1 (blocked) or 2 (blocked with
+ * look-ahead): L (lower triangle meaningful, the upper keeps A), Linv = L^{-1} (column-major)
+ * and info (INT_MAX when SPD, else the 1-based first non-positive pivot column). */
+gprx_status gprx_dev_diag_factor(gprx_ctx* ctx, int32_t variant, const double* A, double* L, double* Linv,
+                                 int32_t* info);
 /* The pair-statistics epilogues' f64 exp (gprx_internal.h fexp) on n host values (accuracy
  * test against the C library). */
 gprx_status gprx_dev_fexp(gprx_ctx* ctx, const double* x, int64_t n, double* y);

@@ -1,5 +1,6 @@
-"""Tile-engine diagonal 128x128 factor + inverse in isolation (gprx_dev_bench what 11 / 12:
-rank-8 register image / blocked MFMA form, k_ptiles.hip): us per factor and phase ticks."""
+"""Tile-engine diagonal 128x128 factor + inverse in isolation (gprx_dev_bench what 11 / 12 / 13:
+rank-8 register image / blocked MFMA form / blocked with look-ahead, k_ptiles.hip): us per
+factor and phase ticks."""
 import ctypes
 import json
 import os
@@ -15,8 +16,8 @@ L.gprx_dev_bench.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int32, ctyp
 ctx = gpr_amd.Context(0)
 out = {}
 for dt, name in ((1, "f64"), (0, "f32")):
-    for what, var in ((11, "rank8"), (12, "blocked")):
-        if dt == 0 and what == 12:
+    for what, var in ((11, "rank8"), (12, "blocked"), (13, "lookahead")):
+        if dt == 0 and what >= 12:
             continue
         arr = (ctypes.c_double * 8)()
         st = L.gprx_dev_bench(ctx.h, dt, what, 128, 0, 0, 64, ctypes.cast(arr, ctypes.POINTER(ctypes.c_double)))
