@@ -66,6 +66,7 @@ static gprx_status bench_impl(int what, int64_t M, int64_t N, int64_t K, int ite
             T* A = (T*)alloc(sizeof(T) * DB * DB * (size_t)reps);
             T* L = (T*)alloc(sizeof(T) * DB * DB);
             long long* pr = (long long*)alloc(sizeof(long long) * 8);
+            (void)hipMemsetAsync(pr, 0, sizeof(long long) * 8, s);
             for (int it = 0; it < reps; it++)
                 hipLaunchKernelGGL(dev_fill_spd<T>, dim3((DB * DB + 255) / 256), dim3(256), 0, s, A + (size_t)it * DB * DB,
                                    (int64_t)DB, (int64_t)DB, (uint64_t)it);
@@ -82,7 +83,7 @@ static gprx_status bench_impl(int what, int64_t M, int64_t N, int64_t K, int ite
             long long h[8];
             (void)hipMemcpy(h, pr, sizeof(h), hipMemcpyDeviceToHost);
             ms[0] = 1e3 * tms / reps;
-            for (int i = 0; i < 5; i++) ms[1 + i] = (double)h[i] / reps;
+            for (int i = 0; i < 8; i++) ms[1 + i] = (double)h[i] / reps;
         } else if (what == 6) {  // in-kernel phase ticks of the diagonal kernel: ms[0..4] per launch
             T* A = (T*)alloc(sizeof(T) * DB * DB * (size_t)iters);
             T* L = (T*)alloc(sizeof(T) * DB * DB);

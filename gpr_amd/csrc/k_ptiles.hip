@@ -373,6 +373,22 @@ __device__ __forceinline__ float rl_lane(float v, int lane) {
     return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), lane));
 }
 
+// GPRX_FACT32_PROF (a profiling build only): core-clock split of fact32's steps into the pivot
+// block (readlanes, 4 x 4 factor, its inverse), the panel solve and the trailing MFMAs; each
+// mark first makes the wave wait for the phase's last result (readfirstlane)
+#ifdef GPRX_FACT32_PROF
+#define F32_MARK(acc_, x_)                                                                           \
+    do {                                                                                             \
+        const int d_ = __builtin_amdgcn_readfirstlane((int)__builtin_bit_cast(unsigned long long, (double)(x_))); \
+        asm volatile("" ::"s"(d_) : "memory");                                                       \
+        const long long n_ = (long long)__builtin_amdgcn_s_memtime();                               \
+        acc_ += n_ - f32_t;                                                                          \
+        f32_t = n_;                                                                                  \
+    } while (0)
+#else
+#define F32_MARK(acc_, x_) (void)0
+#endif
+
 // One wave factors the 32 x 32 diagonal block D at (c0, c0) of the LDS image: L_D -> lower,
 // Dinv = L_D^{-1} -> upper (transposed, Dinv[j][i] at row c0 + i, column c0 + j) and sDi.
 //
@@ -385,7 +401,8 @@ __device__ __forceinline__ float rl_lane(float v, int lane) {
 // layout is the MFMA operand layout), with the finished columns masked to zero in the
 // operand.  The identity rows (tiles 2, 3) end as L_D^{-T}.
 template <typename T>
-__device__ __forceinline__ void fact32(T* __restrict__ sS, T* __restrict__ sDi, int c0, int& fail) {
+__device__ __forceinline__ void fact32(T* __restrict__ sS, T* __restrict__ sDi, int c0, int& fail,
+                                       long long* fprof = nullptr) {
     constexpr int SL = SIL;
     const int lane = threadIdx.x & 63, lr = lane & 15, lk = lane >> 4;
     if constexpr (std::is_same<T, double>::value) {
@@ -408,9 +425,33 @@ __device__ __forceinline__ void fact32(T* __restrict__ sS, T* __restrict__ sDi, 
                     acc[TI[tr][tc]][rg] = v;
                 }
             }
+#ifdef GPRX_FACT32_PROF
+        long long f32_t = (long long)__builtin_amdgcn_s_memtime(), f32_piv = 0, f32_pan = 0, f32_trl = 0;
+#endif
+        // Trailing MFMAs of step st: tiles (tr, tcp) for tcp = tc..1 (see f32_mfma_on).  Only the
+        // one that updates the NEXT pivot tile is issued at once; the others are deferred into
+        // the next step's pivot phase, one between each column of its 4 x 4 factor
+        // (sched_barrier): issued back to back they held the wave's in-order issue for ~6 x 64
+        // cycles in front of the pivot chain, the latency-bound critical path of the factor.
+        double pa[2] = {0.0, 0.0}, pb[4] = {0.0, 0.0, 0.0, 0.0};  // the previous step's operands
 #pragma unroll
         for (int st = 0; st < 8; st++) {
             const int k0 = 4 * st, tc = k0 / 16, rg = (k0 % 16) / 4, pl = k0 % 16;
+            // deferred MFMA number m of step st - 1 (compile-time: the loop is unrolled)
+            auto deferred = [&](int m) {
+                if (st == 0) return;
+                const int tcq = (4 * (st - 1)) / 16, tcn = tc;
+                int cnt = 0;
+#pragma unroll
+                for (int tcp = tcq; tcp < 2; tcp++)
+#pragma unroll
+                    for (int tr = 0; tr < 4; tr++) {
+                        if (TI[tr][tcp] < 0 || TI[tr][tcq] < 0) continue;
+                        if (tr < 2 && tr < tcp) continue;
+                        if (tr == tcn && tcp == tcn) continue;  // the critical one, already issued
+                        if (cnt++ == m) acc[TI[tr][tcp]] = Tr::mma(pa[tcp], pb[tr], acc[TI[tr][tcp]]);
+                    }
+            };
             // the 4 x 4 pivot block (lower) of tile (tc, tc): P[i][j] at lane (pl + i) + 16 j;
             // its factor, then Q = L_P^{-1}, reduced to this lane's row qr = Q[lk][.]
             double qr[4];
@@ -419,6 +460,10 @@ __device__ __forceinline__ void fact32(T* __restrict__ sS, T* __restrict__ sDi, 
                 double Lp[4][4], rq[4];
 #pragma unroll
                 for (int i = 0; i < 4; i++) {
+                    __builtin_amdgcn_sched_barrier(0);
+                    deferred(i == 0 ? 0 : i + 1);
+                    if (i == 0) deferred(1);
+                    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                     for (int j = 0; j < i; j++) {
                         double v = rl_lane(acc[TI[tc][tc]][rg], pl + i + 16 * j);
@@ -433,6 +478,7 @@ __device__ __forceinline__ void fact32(T* __restrict__ sS, T* __restrict__ sDi, 
                     rq[i] = rsqrt_full(dsum);
                     Lp[i][i] = dsum * rq[i];
                 }
+                __builtin_amdgcn_sched_barrier(0);
                 {  // lpv = L_P[lr - pl][lk] (0 above the diagonal): a two-level select
                     double cv[4];
 #pragma unroll
@@ -463,6 +509,7 @@ __device__ __forceinline__ void fact32(T* __restrict__ sS, T* __restrict__ sDi, 
                     qr[i] = v;
                 }
             }
+            F32_MARK(f32_piv, qr[0] + qr[1] + qr[2] + qr[3]);
             // panel: L[r][k0 + lk] = sum_{i <= lk} a[r][k0 + i] Q[lk][i] (D rows above k0 kept; the
             // pivot rows take L_P itself -- recomputing them as A_P Q^T costs accuracy on
             // ill-conditioned blocks)
@@ -481,19 +528,35 @@ __device__ __forceinline__ void fact32(T* __restrict__ sS, T* __restrict__ sDi, 
                 const bool piv = tr == tc && lr >= pl && lr < pl + 4;
                 acc[TI[tr][tc]][rg] = piv ? lpv : pv[tr];
             }
-            // trailing: tile (tr, tcp) -= panel(tr) panel_D(tcp)^T over the columns > k0 + 3
+            F32_MARK(f32_pan, pv[0] + pv[1] + pv[2] + pv[3]);
+            // trailing: tile (tr, tcp) -= panel(tr) panel_D(tcp)^T over the columns > k0 + 3:
+            // operands for this step's MFMAs; the next pivot tile's one now, the rest deferred
 #pragma unroll
-            for (int tcp = tc; tcp < 2; tcp++) {
-                const double a = (16 * tcp + lr > k0 + 3) ? -pv[tcp] : 0.0;
+            for (int tcp = 0; tcp < 2; tcp++) pa[tcp] = (16 * tcp + lr > k0 + 3) ? -pv[tcp] : 0.0;
 #pragma unroll
-                for (int tr = 0; tr < 4; tr++) {
-                    if (TI[tr][tcp] < 0 || TI[tr][tc] < 0) continue;  // absent output / zero panel
-                    if (tr < 2 && tr < tcp) continue;
-                    const double b = (tr < 2 && 16 * tr + lr < k0 + 4) ? 0.0 : pv[tr];
-                    acc[TI[tr][tcp]] = Tr::mma(a, b, acc[TI[tr][tcp]]);
-                }
+            for (int tr = 0; tr < 4; tr++) pb[tr] = (tr < 2 && 16 * tr + lr < k0 + 4) ? 0.0 : pv[tr];
+            if (st < 7) {
+                const int tcn = (k0 + 4) / 16;
+                acc[TI[tcn][tcn]] = Tr::mma(pa[tcn], pb[tcn], acc[TI[tcn][tcn]]);
+            } else {  // last step: everything now
+#pragma unroll
+                for (int tcp = tc; tcp < 2; tcp++)
+#pragma unroll
+                    for (int tr = 0; tr < 4; tr++) {
+                        if (TI[tr][tcp] < 0 || TI[tr][tc] < 0) continue;
+                        if (tr < 2 && tr < tcp) continue;
+                        acc[TI[tr][tcp]] = Tr::mma(pa[tcp], pb[tr], acc[TI[tr][tcp]]);
+                    }
             }
         }
+#ifdef GPRX_FACT32_PROF
+        F32_MARK(f32_trl, acc[0][3] + acc[2][3] + acc[5][3]);
+        if (fprof) {
+            fprof[0] += f32_piv;
+            fprof[1] += f32_pan;
+            fprof[2] += f32_trl;
+        }
+#endif
         // out: L_D (lower incl. diagonal); Dinv from the identity rows (X = L_D^{-T},
         // Dinv[j][i] = X[i][j]) transposed into the upper triangle, its diagonal into sDi
 #pragma unroll
@@ -888,7 +951,7 @@ __device__ __forceinline__ void diag_factor_la(T* __restrict__ A, int64_t ld, T*
         // units write rows 32 (p - 1) .. 32 p - 1 (p = 3: also 96 .. 127) of columns < 32 (p - 1),
         // transposed: LDS columns >= 32 (p - 1), rows < 32 (p - 1); the stores only read)
         if (w == 0) {
-            fact32<T>(sS, sDi, c0, fail);
+            fact32<T>(sS, sDi, c0, fail, prof ? prof + 4 : nullptr);
             if (prof) pfw += wall_clock64() - tf0;
         } else if (p > 0) {
             la_side<T>(A, ld, Linv, sS, sDi, p, t, w, 1, lr, lk);
@@ -1019,7 +1082,7 @@ __global__ __launch_bounds__(NT) void diag_bench_kernel(T* A, int64_t ld, T* Lin
                                                         int reps) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     long long acc[5] = {0, 0, 0, 0, 0};
-    long long ph[4] = {0, 0, 0, 0};
+    long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // [4..6]: fact32 core-clock split (GPRX_FACT32_PROF)
     for (int r = 0; r < reps; r++) {
         const long long t0 = wall_clock64();
         if (V == 0) diag_factor_rank8<T>(A + (int64_t)r * DB * ld, ld, Linv, info, 0, smem_raw, threadIdx.x, nullptr, ph);
@@ -1033,8 +1096,10 @@ __global__ __launch_bounds__(NT) void diag_bench_kernel(T* A, int64_t ld, T* Lin
         acc[3] += ph[3];
         acc[4] += t1 - t0;
     }
-    if (threadIdx.x == 0)
+    if (threadIdx.x == 0) {
         for (int u = 0; u < 5; u++) prof[u] = acc[u];
+        for (int u = 0; u < 3; u++) prof[5 + u] = ph[4 + u];
+    }
 }
 
 template <typename T>

@@ -18,7 +18,8 @@ extern "C" {
  *       9 = potrf as one persistent tile-dataflow launch (potrf_tiles),
  *      10 = back substitution as one flag-chained launch (launch_backsolve_chain),
  *      11 / 12 / 13 = the tile engine's diagonal-block factor, variant what - 11 (rank-8 /
- *           blocked / look-ahead): ms[0] = us per factor, ms[1..5] = phase ticks (100 MHz).
+ *           blocked / look-ahead): ms must hold 9 doubles: ms[0] = us per factor, ms[1..5] =
+ *           phase ticks (100 MHz), ms[6..8] = fact32 core cycles (GPRX_FACT32_PROF builds).
  * For 1/2: (M, N, K) are the gemm sizes; for 3/4/5: M = n.  Returns the mean device time
  * per call over `iters` calls (HIP events) in *ms. */
 gprx_status gprx_dev_bench(gprx_ctx* ctx, gprx_dtype dtype, int32_t what, int64_t M, int64_t N, int64_t K,
