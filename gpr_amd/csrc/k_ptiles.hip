@@ -919,10 +919,11 @@ __device__ __forceinline__ void la_side(T* __restrict__ A, int64_t ld, T* __rest
     }
 }
 
+// from_lds: the block is already in the LDS image (diagx_ts left the syrk result there)
 template <typename T>
 __device__ __forceinline__ void diag_factor_la(T* __restrict__ A, int64_t ld, T* __restrict__ Linv,
                                                int* __restrict__ info, int64_t col0, unsigned char* smem_raw,
-                                               const int t, long long* prof = nullptr) {
+                                               const int t, long long* prof = nullptr, bool from_lds = false) {
     typedef Mfma<T> Tr;
     typedef typename Tr::acc_t acc_t;
     constexpr int SL = SIL;
@@ -930,15 +931,15 @@ __device__ __forceinline__ void diag_factor_la(T* __restrict__ A, int64_t ld, T*
     T* sDi = sS + (size_t)DB * SL;
     const int w = t >> 6, lane = t & 63, lr = lane & 15, lk = lane >> 4;
     long long pt0 = prof ? wall_clock64() : 0, pf = 0, pside = 0, pfw = 0;
-    {
+    if (!from_lds) {
         const int r = t & (DB - 1), cq = t >> 7;
         T v[DB / (NT / DB)];
 #pragma unroll
         for (int u = 0; u < DB / (NT / DB); u++) v[u] = A[r + (int64_t)(cq + u * (NT / DB)) * ld];
 #pragma unroll
         for (int u = 0; u < DB / (NT / DB); u++) sS[r + (cq + u * (NT / DB)) * SL] = v[u];
-        if (t == 0) sDi[DB] = T(0);  // linv_at's zero
     }
+    if (t == 0) sDi[DB] = T(0);  // linv_at's zero
     __syncthreads();
     const long long pload = prof ? wall_clock64() : 0;
     int fail = -1;
@@ -1058,18 +1059,22 @@ __device__ __forceinline__ void diag_factor_la(T* __restrict__ A, int64_t ld, T*
     }
 }
 
+#ifndef GPRX_DIAG_RANK8
+constexpr bool DIAG_LA = true;
+#else
+constexpr bool DIAG_LA = false;
+#endif
+// from_lds (f64 look-ahead form only): the block is in the LDS image already (diagx_ts)
 template <typename T>
 __device__ __forceinline__ void diag_factor(T* __restrict__ A, int64_t ld, T* __restrict__ Linv, int* __restrict__ info,
                                             int64_t col0, unsigned char* smem_raw, const int t, int* dbg = nullptr,
-                                            long long* prof = nullptr) {
-#ifndef GPRX_DIAG_RANK8
-    // f64: the blocked factor with look-ahead (diag_factor_la: 38 us per block in isolation
+                                            long long* prof = nullptr, bool from_lds = false) {
+    // f64: the blocked factor with look-ahead (diag_factor_la: 43 us per block in isolation
     // against 50.6 for the rank-8 image, scripts/diag_bench.py)
-    if constexpr (std::is_same<T, double>::value) {
-        diag_factor_la<T>(A, ld, Linv, info, col0, smem_raw, t, prof);
+    if constexpr (std::is_same<T, double>::value && DIAG_LA) {
+        diag_factor_la<T>(A, ld, Linv, info, col0, smem_raw, t, prof, from_lds);
         return;
     }
-#endif
     // f32 (and GPRX_DIAG_RANK8): the rank-8 register image
     diag_factor_rank8<T>(A, ld, Linv, info, col0, smem_raw, t, dbg, prof);
 }
@@ -1293,6 +1298,97 @@ __device__ __forceinline__ void publish_host(unsigned* p) {
     }
 }
 
+// DIAGX(k > 0)'s two products before the diagonal factor, with the result left in the
+// factor's LDS image (f64, diag_factor_la):
+//   T = A_{k,k-1} Linv_{k-1}^T  on the staging ring (triangular B, MAP 1), stored to HBM as
+//       L_{k,k-1} (+ the distributed send slot) AND into the LDS image as an operand;
+//   A_kk - T T^T  with both fragments read from that image (no second HBM round trip, no
+//       ring fill), the diagonal tile's lower 16 x 16 tiles only (MAP 2), accumulated onto
+//       A_kk itself (loaded while T is stored); the result overwrites the image (lower part).
+// Publishes L_{k,k-1} (lcnt[k] = k) between the two, as the two-call form did.
+template <typename T, bool DIST>
+__device__ __forceinline__ long long diagx_ts(T* __restrict__ Akm, T* __restrict__ Akk, int64_t ld,
+                                              const T* __restrict__ Lp, T* __restrict__ send, int* lflag, int k,
+                                              unsigned* hslot, T* smem, const int t, bool mark) {
+    typedef Mfma<T> Tr;
+    typedef typename Tr::acc_t acc_t;
+    const int lane = t & 63, w = t >> 6, lr = lane & 15, lk = lane >> 4;
+    int sr, sc;
+    wave_block<2>(w, sr, sc);
+    acc_t sacc[2][4];  // the S accumulators, started from A_kk (loaded while T is stored)
+    // ---- T on the ring ---------------------------------------------------------------------
+    {
+        int tr_, tc_;
+        wave_block<1>(w, tr_, tc_);
+        acc_t acc[2][4];
+        tile_mma<T, 1>(acc, Akm, ld, Lp, DB, GT, 32 * (tc_ + 1), smem, t);
+        // A_kk into the S accumulators (MAP 2 layout; every element, the upper ones unused):
+        // in flight while T goes out
+#pragma unroll
+        for (int x = 0; x < 2; x++)
+#pragma unroll
+            for (int reg = 0; reg < 4; reg++) {
+                const T* ccol = Akk + (int64_t)(sc * 32 + x * 16 + Tr::orow(lk, reg)) * ld;
+#pragma unroll
+                for (int y = 0; y < 4; y++) sacc[x][y][reg] = ccol[sr * 64 + y * 16 + lr];
+            }
+        __syncthreads();  // every wave done with the ring before the image overwrites it
+#pragma unroll
+        for (int x = 0; x < 2; x++)
+#pragma unroll
+            for (int reg = 0; reg < 4; reg++) {
+                const int jl = tc_ * 32 + x * 16 + Tr::orow(lk, reg);
+#pragma unroll
+                for (int y = 0; y < 4; y++) {
+                    const int il = tr_ * 64 + y * 16 + lr;
+                    st_sc1(Akm + il + (int64_t)jl * ld, acc[x][y][reg]);
+                    if (send) st_sc1(send + il + (int64_t)jl * DB, acc[x][y][reg]);
+                    smem[il + jl * SIL] = acc[x][y][reg];
+                }
+            }
+    }
+    publish(lflag, k, false);  // L_{k,k-1} final: unblocks the updates of column k (also a barrier)
+    if constexpr (DIST) {
+        if (send) publish_host(hslot);
+    }
+    const long long tm = mark ? wall_clock64() : 0;  // (GPRX_PT_TRACE: end of the T phase)
+    // ---- A_kk - T T^T from the image ----------------------------------------------------------
+    // fragments of step kq + 1 are read while the MFMAs of step kq run (as tile_mma)
+    T fb[2][2], fa[2][4];
+    auto frag = [&](int kq, int r) {
+        const int kc = kq * 4 + lk;
+#pragma unroll
+        for (int x = 0; x < 2; x++) fb[r][x] = smem[(sc * 32 + x * 16 + lr) + kc * SIL];
+#pragma unroll
+        for (int y = 0; y < 4; y++) fa[r][y] = smem[(sr * 64 + y * 16 + lr) + kc * SIL];
+    };
+    frag(0, 0);
+#pragma unroll 2
+    for (int kq = 0; kq < GT / 4; kq++) {
+        if (kq + 1 < GT / 4) frag(kq + 1, (kq + 1) & 1);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int x = 0; x < 2; x++)
+#pragma unroll
+            for (int y = 0; y < 4; y++)
+                if (4 * sr + y >= 2 * sc + x) sacc[x][y] = Tr::mma(-fb[kq & 1][x], fa[kq & 1][y], sacc[x][y]);
+    }
+    __syncthreads();  // every read of T done before the image takes the result
+#pragma unroll
+    for (int x = 0; x < 2; x++)
+#pragma unroll
+        for (int reg = 0; reg < 4; reg++) {
+            const int jl = sc * 32 + x * 16 + Tr::orow(lk, reg);
+#pragma unroll
+            for (int y = 0; y < 4; y++) {
+                const int il = sr * 64 + y * 16 + lr;
+                if (4 * sr + y >= 2 * sc + x) smem[il + jl * SIL] = sacc[x][y][reg];
+            }
+        }
+    __syncthreads();
+    return tm;
+}
+
 template <typename T, bool DIST>
 __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
@@ -1397,7 +1493,19 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
             const int k = i;
             T* Akk = Ci + (int64_t)k * GT * ld;
             long long dt[4] = {0, 0, 0, 0};
-            if (k > 0) {
+            constexpr bool fused_ts = std::is_same<T, double>::value && DIAG_LA;
+            if (fused_ts && k > 0) {
+                T* Akm = Ci + (int64_t)(k - 1) * GT * ld;
+                T* send = nullptr;
+                unsigned* hs = nullptr;
+                if constexpr (DIST) {
+                    send = a.dist->sptr[(int64_t)k * a.nc + (k - 1)];
+                    hs = a.dist->hslot + (int64_t)k * a.nc + (k - 1);
+                }
+                dt[0] = diagx_ts<T, DIST>(Akm, Akk, ld, a.Linv + (int64_t)(k - 1) * DB * DB, send, a.lcnt + k, k,
+                                          hs, smem, tid, a.trace != nullptr);
+                dt[1] = dt[0];
+            } else if (k > 0) {
                 T* Akm = Ci + (int64_t)(k - 1) * GT * ld;
                 T* send = nullptr;
                 if constexpr (DIST) send = a.dist->sptr[(int64_t)k * a.nc + (k - 1)];
@@ -1414,7 +1522,8 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
             }
             if (a.trace) dt[2] = wall_clock64();
             diag_factor<T>(Akk, ld, a.Linv + (int64_t)k * DB * DB, a.info, (int64_t)k * DB, smem_raw, tid, a.dbg,
-                           a.trace ? a.trace + 4 * (int64_t)(a.ntasks + a.nc) + 4 * (int64_t)k : nullptr);
+                           a.trace ? a.trace + 4 * (int64_t)(a.ntasks + a.nc) + 4 * (int64_t)k : nullptr,
+                           fused_ts && k > 0);
             if (a.trace) dt[3] = wall_clock64();
             publish(a.lcnt + k, k + 1, true);  // diag_factor stores are plain
             if constexpr (DIST) publish_host(a.dist->hdiag + k);
