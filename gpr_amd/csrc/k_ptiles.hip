@@ -980,19 +980,33 @@ __device__ __forceinline__ void diag_factor_la(T* __restrict__ A, int64_t ld, T*
                 av0[reg] = sS[rr + (c0 + Tr::orow(lk, reg)) * SL];
                 av1[reg] = sS[rr + (c0 + 16 + Tr::orow(lk, reg)) * SL];
             }
+            T dmax = T(0);  // max |Dinv_p| over the entries this lane feeds
 #pragma unroll
             for (int kq = 0; kq < 8; kq++) {
                 const int k = kq * 4 + lk;
                 const T bv = sS[rr + (c0 + k) * SL];
-                a0 = Tr::mma(linv_at(sS, sDi, c0 + lr, c0 + k), bv, a0);
-                a1 = Tr::mma(linv_at(sS, sDi, c0 + 16 + lr, c0 + k), bv, a1);
+                const T d0 = linv_at(sS, sDi, c0 + lr, c0 + k), d1 = linv_at(sS, sDi, c0 + 16 + lr, c0 + k);
+                dmax = fmax(dmax, fmax(fabs(d0), fabs(d1)));
+                a0 = Tr::mma(d0, bv, a0);
+                a1 = Tr::mma(d1, bv, a1);
             }
+            // est = max|Dinv_p| max_i L_ii (<= cond_2(L_pp), within a factor 32^2 of it): a
+            // well-conditioned block skips the refinement -- its explicit-inverse error is then
+            // no larger than that of the 128-block TRSM tasks (which also use explicit inverses)
+            T dimin = sDi[c0 + (lane & 31)];  // 1 / L_ii
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) {
+                dmax = fmax(dmax, __shfl_xor(dmax, off, 64));
+                dimin = fmin(dimin, __shfl_xor(dimin, off, 64));
+            }
+            const bool refine = __builtin_amdgcn_readfirstlane((int)(dmax > T(32) * dimin)) != 0;
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
             for (int reg = 0; reg < 4; reg++) {  // X0 (kept in a0, a1) through LDS to the operand layout
                 sS[rr + (c0 + Tr::orow(lk, reg)) * SL] = a0[reg];
                 sS[rr + (c0 + 16 + Tr::orow(lk, reg)) * SL] = a1[reg];
             }
+            if (refine) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             acc_t q0 = acc_t{0}, q1 = acc_t{0};  // X0 L_pp^T
 #pragma unroll
@@ -1024,6 +1038,7 @@ __device__ __forceinline__ void diag_factor_la(T* __restrict__ A, int64_t ld, T*
                 sS[rr + (c0 + Tr::orow(lk, reg)) * SL] = a0[reg];
                 sS[rr + (c0 + 16 + Tr::orow(lk, reg)) * SL] = a1[reg];
             }
+            }  // refine
         }
         __syncthreads();
         // ---- Ua(p): the next panel's columns (C = 2p+2, 2p+3; R >= C), all waves -------------
