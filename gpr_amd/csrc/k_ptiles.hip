@@ -1320,7 +1320,7 @@ __device__ __forceinline__ void publish_host(unsigned* p) {
 //   A_kk - T T^T  with both fragments read from that image (no second HBM round trip, no
 //       ring fill), the diagonal tile's lower 16 x 16 tiles only (MAP 2), accumulated onto
 //       A_kk itself (loaded while T is stored); the result overwrites the image (lower part).
-// Publishes L_{k,k-1} (lcnt[k] = k) between the two, as the two-call form did.
+// Publishes L_{k,k-1} (lcnt[k] = k) after S (the two-call form published between the two).
 template <typename T, bool DIST>
 __device__ __forceinline__ long long diagx_ts(T* __restrict__ Akm, T* __restrict__ Akk, int64_t ld,
                                               const T* __restrict__ Lp, T* __restrict__ send, int* lflag, int k,
@@ -1330,23 +1330,23 @@ __device__ __forceinline__ long long diagx_ts(T* __restrict__ Akm, T* __restrict
     const int lane = t & 63, w = t >> 6, lr = lane & 15, lk = lane >> 4;
     int sr, sc;
     wave_block<2>(w, sr, sc);
-    acc_t sacc[2][4];  // the S accumulators, started from A_kk (loaded while T is stored)
+    // the S accumulators start from A_kk: its loads are in flight during T's mainloop
+    // (MAP 2 layout; every element, the upper ones unused)
+    acc_t sacc[2][4];
+#pragma unroll
+    for (int x = 0; x < 2; x++)
+#pragma unroll
+        for (int reg = 0; reg < 4; reg++) {
+            const T* ccol = Akk + (int64_t)(sc * 32 + x * 16 + Tr::orow(lk, reg)) * ld;
+#pragma unroll
+            for (int y = 0; y < 4; y++) sacc[x][y][reg] = ccol[sr * 64 + y * 16 + lr];
+        }
     // ---- T on the ring ---------------------------------------------------------------------
     {
         int tr_, tc_;
         wave_block<1>(w, tr_, tc_);
         acc_t acc[2][4];
         tile_mma<T, 1>(acc, Akm, ld, Lp, DB, GT, 32 * (tc_ + 1), smem, t);
-        // A_kk into the S accumulators (MAP 2 layout; every element, the upper ones unused):
-        // in flight while T goes out
-#pragma unroll
-        for (int x = 0; x < 2; x++)
-#pragma unroll
-            for (int reg = 0; reg < 4; reg++) {
-                const T* ccol = Akk + (int64_t)(sc * 32 + x * 16 + Tr::orow(lk, reg)) * ld;
-#pragma unroll
-                for (int y = 0; y < 4; y++) sacc[x][y][reg] = ccol[sr * 64 + y * 16 + lr];
-            }
         __syncthreads();  // every wave done with the ring before the image overwrites it
 #pragma unroll
         for (int x = 0; x < 2; x++)
@@ -1362,10 +1362,7 @@ __device__ __forceinline__ long long diagx_ts(T* __restrict__ Akm, T* __restrict
                 }
             }
     }
-    publish(lflag, k, false);  // L_{k,k-1} final: unblocks the updates of column k (also a barrier)
-    if constexpr (DIST) {
-        if (send) publish_host(hslot);
-    }
+    __syncthreads();  // the image holds T
     const long long tm = mark ? wall_clock64() : 0;  // (GPRX_PT_TRACE: end of the T phase)
     // ---- A_kk - T T^T from the image ----------------------------------------------------------
     // fragments of step kq + 1 are read while the MFMAs of step kq run (as tile_mma)
@@ -1388,7 +1385,12 @@ __device__ __forceinline__ long long diagx_ts(T* __restrict__ Akm, T* __restrict
             for (int y = 0; y < 4; y++)
                 if (4 * sr + y >= 2 * sc + x) sacc[x][y] = Tr::mma(-fb[kq & 1][x], fa[kq & 1][y], sacc[x][y]);
     }
-    __syncthreads();  // every read of T done before the image takes the result
+    // L_{k,k-1} final: unblocks the updates of column k.  Published after S so the HBM stores'
+    // latency hides under S; its barrier is also "every read of T done" for the image below.
+    publish(lflag, k, false);
+    if constexpr (DIST) {
+        if (send) publish_host(hslot);
+    }
 #pragma unroll
     for (int x = 0; x < 2; x++)
 #pragma unroll
@@ -1567,9 +1569,9 @@ struct Cost {  // per-task durations (us, one CU), calibrated from GPRX_PT_TRACE
     double k128 = 17.1;  // per 128-deep slice of a full tile update
     double ovh = 6.5;    // per update task: ticket, waits, fences, C read-modify-write
     double trsm = 16.0;  // TRSM tile (r01i trace: 15.9)
-    double diagx = 96.0;   // DIAGX(k > 0): trsm tile + syrk tile + 128x128 factor/inverse (r01i trace)
-    double diag0 = 70.0;   // DIAGX(0): factor/inverse only
-    double early = 20.0;   // DIAGX(k) publishes L_{k,k-1} after its trsm phase
+    double diagx = 70.0;   // DIAGX(k > 0): trsm + syrk tile + 128x128 factor/inverse (r02f trace, f64)
+    double diag0 = 40.0;   // DIAGX(0): factor/inverse only
+    double early = 31.0;   // DIAGX(k) publishes L_{k,k-1} after its trsm and syrk phases
     double diagf = 0.97;   // diagonal-tile update relative to a full one (2 of 8 waves idle)
     double build = 28.0;   // BUILD tile (pair statistics + kernel values + stores)
 };
