@@ -455,7 +455,6 @@ __device__ __forceinline__ void fact32(T* __restrict__ sS, T* __restrict__ sDi, 
             // the 4 x 4 pivot block (lower) of tile (tc, tc): P[i][j] at lane (pl + i) + 16 j;
             // its factor, then Q = L_P^{-1}, reduced to this lane's row qr = Q[lk][.]
             double qr[4];
-            double lpv = 0.0;  // this lane's entry of L_P when it holds a pivot row
             {
                 double Lp[4][4], rq[4];
 #pragma unroll
@@ -474,20 +473,19 @@ __device__ __forceinline__ void fact32(T* __restrict__ sS, T* __restrict__ sDi, 
                     double dsum = rl_lane(acc[TI[tc][tc]][rg], pl + i + 16 * i);
 #pragma unroll
                     for (int k = 0; k < i; k++) dsum = fma(-Lp[i][k], Lp[i][k], dsum);
-                    if (!(dsum > 0.0) && fail < 0) fail = c0 + k0 + i;
-                    rq[i] = rsqrt_full(dsum);
+                    rq[i] = rsqrt_full(dsum);  // (a non-positive or NaN dsum gives a NaN L_ii: checked at the end)
                     Lp[i][i] = dsum * rq[i];
                 }
                 __builtin_amdgcn_sched_barrier(0);
-                {  // lpv = L_P[lr - pl][lk] (0 above the diagonal): a two-level select
-                    double cv[4];
+                // L_P goes to the image directly (lane 0; the output stage below skips the
+                // diagonal 4 x 4 blocks): the pivot rows' panel values A_P Q^T would cost
+                // accuracy on ill-conditioned blocks, and a per-lane select of L_P cost ~26
+                // instructions on the latency-bound pivot chain
+                if (lane == 0) {
 #pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        cv[j] = 0.0;
+                    for (int i = 0; i < 4; i++)
 #pragma unroll
-                        for (int i = j; i < 4; i++) cv[j] = (lr - pl == i) ? Lp[i][j] : cv[j];
-                    }
-                    lpv = (lk == 0) ? cv[0] : (lk == 1) ? cv[1] : (lk == 2) ? cv[2] : cv[3];
+                        for (int j = 0; j <= i; j++) sS[(c0 + k0 + i) + (c0 + k0 + j) * SL] = Lp[i][j];
                 }
                 double Q[4][4];
 #pragma unroll
@@ -510,9 +508,7 @@ __device__ __forceinline__ void fact32(T* __restrict__ sS, T* __restrict__ sDi, 
                 }
             }
             F32_MARK(f32_piv, qr[0] + qr[1] + qr[2] + qr[3]);
-            // panel: L[r][k0 + lk] = sum_{i <= lk} a[r][k0 + i] Q[lk][i] (D rows above k0 kept; the
-            // pivot rows take L_P itself -- recomputing them as A_P Q^T costs accuracy on
-            // ill-conditioned blocks)
+            // panel: L[r][k0 + lk] = sum_{i <= lk} a[r][k0 + i] Q[lk][i] (D rows above k0 kept)
             double pv[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
             for (int tr = 0; tr < 4; tr++) {
@@ -522,11 +518,8 @@ __device__ __forceinline__ void fact32(T* __restrict__ sS, T* __restrict__ sDi, 
 #pragma unroll
                 for (int i = 0; i < 4; i++) nv = fma(__shfl(v, lr + 16 * i, 64), qr[i], nv);
                 const bool keep = tr < 2 && 16 * tr + lr < k0;
-                pv[tr] = keep ? v : nv;
-                // (the trailing update masks the pivot rows out of both operands, so their
-                // exact L_P values are off the critical path)
-                const bool piv = tr == tc && lr >= pl && lr < pl + 4;
-                acc[TI[tr][tc]][rg] = piv ? lpv : pv[tr];
+                pv[tr] = keep ? v : nv;  // (pivot rows: masked out of the trailing operands)
+                acc[TI[tr][tc]][rg] = pv[tr];
             }
             F32_MARK(f32_pan, pv[0] + pv[1] + pv[2] + pv[3]);
             // trailing: tile (tr, tcp) -= panel(tr) panel_D(tcp)^T over the columns > k0 + 3:
@@ -569,7 +562,7 @@ __device__ __forceinline__ void fact32(T* __restrict__ sS, T* __restrict__ sDi, 
                     const int R = 16 * tr + lr, C = 16 * tc + Tr::orow(lk, rg);
                     const double v = acc[TI[tr][tc]][rg];
                     if (tr < 2) {
-                        if (C <= R) sS[(c0 + R) + (c0 + C) * SL] = v;
+                        if (C <= R && (R >> 2) != (C >> 2)) sS[(c0 + R) + (c0 + C) * SL] = v;  // L_P: above
                     } else {
                         const int i = R - 32;
                         if (C > i) sS[(c0 + i) + (c0 + C) * SL] = v;
@@ -577,6 +570,11 @@ __device__ __forceinline__ void fact32(T* __restrict__ sS, T* __restrict__ sDi, 
                     }
                 }
             }
+        // info: the first column whose pivot was not positive (its L_ii and every later one NaN)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const double dg = sS[(c0 + (lane & 31)) * (SL + 1)];
+        const unsigned long long bad = __ballot(lane < 32 && !(dg > 0.0));
+        if (bad && fail < 0) fail = c0 + (int)__builtin_ctzll(bad);
     }
 }
 
