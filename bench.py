@@ -226,6 +226,17 @@ def main():
                               / (pms * 1e-3) / 1e12 / world, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
                               "frac": args.predict_q * n * (2.0 * d + 2.0 * m) / (pms * 1e-3) / 1e12 / world
                               / PEAK_FP64_TFLOPS} if pms else None)}
+        if pms:
+            # the same bound for THIS kernel tree: per (query, sample) pair the
+            # Gaussian r^2 (d deep) and the periodic statistic (2d deep) on the f64 MFMA units,
+            # 2 * 3d flop, plus on the f64 VALU two exps (fexp, 11 ops each) and ~6 ops of leaf
+            # scaling, sum and the alpha accumulation; MFMA and f64 VALU do not co-issue
+            # (DESIGN.md 4.11), so the two times add.  VALU peak: 78.6 TFLOP/s = 39.3 T FMA/s.
+            pairs = float(args.predict_q) * n / world
+            t_roof = pairs * 6.0 * d / (PEAK_FP64_TFLOPS * 1e12) + pairs * 28.0 / (PEAK_FP64_TFLOPS / 2 * 1e12)
+            pred["roofline_tree"] = {"bound": "mfma+valu (serial)", "t_roof_ms": 1e3 * t_roof,
+                                     "t_device_ms": pms, "frac": 1e3 * t_roof / pms,
+                                     "mfma_flop_per_pair": 6.0 * d, "valu_ops_per_pair": 28.0}
 
     # posterior variance (GetCredibleInterval, lib/GaussianProcess.cpp:102-114): k(x,x) - |L^{-1} k_x|^2
     # for Qv queries, query-sharded; the forward solve with Qv right-hand sides on the tile GEMM
