@@ -281,6 +281,15 @@ def main():
                      "frac_hbm": bbytes / (bms * 1e-3) / 1e9 / PEAK_HBM_GBS,
                      "entries_per_s": n * (n + 1) / 2 / (bms * 1e-3),
                      "kernel": "potrf_tiles_kernel<double, false> with BUILD tasks only (k_ptiles.hip)"}
+            # the build is compute-bound for this tree, not HBM-bound: per 128 x 128 lower tile
+            # the pair statistics are a 128 x 128 x 3d MFMA product (r^2: d deep, periodic: 2d)
+            # and every entry costs two exps (~17 f64 ops each, ocml) plus ~6 ops on the f64
+            # VALU, serial with the MFMAs; the stores at HBM rate on top
+            ntile = (n // 128) * (n // 128 + 1) / 2
+            t_b = (ntile * 2.0 * 128 * 128 * 3 * d / (PEAK_FP64_TFLOPS * 1e12)
+                   + ntile * 128 * 128 * 40.0 / (PEAK_FP64_TFLOPS / 2 * 1e12) + bbytes / (PEAK_HBM_GBS * 1e9))
+            build["roofline_tree"] = {"bound": "mfma+valu (serial) + hbm stores", "t_roof_ms": 1e3 * t_b,
+                                      "frac": 1e3 * t_b / bms}
         except Exception as e:
             log("build timing failed:", e)
 
