@@ -155,24 +155,98 @@ __global__ __launch_bounds__(NT) void predict_mma_kernel(const KCanon<T>* __rest
     T nu[4];
 #pragma unroll
     for (int y = 0; y < 4; y++) nu[y] = R2 ? FU[(int64_t)(Kr + Kp) * nfu + i0 + wr * 64 + y * 16 + lr] : T(0);
-    // column norms of the current block go through LDS (after the staging ring): held in
-    // registers across the two tile products they made this kernel spill
-    T* nvs = smem + gemm_lds<T>() / sizeof(T);
-    T* als = nvs + GT;
-    for (int64_t j0 = 0; j0 < n; j0 += GT) {
-        // column norms and alpha of the current block go through LDS (after the staging ring;
-        // written here, read after tile_mma's barriers): held in registers across the two
-        // tile products they made this kernel spill.  alpha = 0 masks the padding columns.
-        if (t < GT) {
-            if (R2) nvs[t] = FV[(int64_t)(Kr + Kp) * nfv + j0 + t];
-            als[t] = (j0 + t < n) ? alpha[(j0 + t) * m] : T(0);
+    // ONE staging ring over all training blocks: the stage index runs on across blocks, so the
+    // next block's first stages are loading while this block's exp epilogue runs (a fresh
+    // ring per block exposed its fill latency 128 times per workgroup).  Column norms and alpha
+    // of a block go through LDS after the ring, double-buffered by block parity: block jb + 1's
+    // are loaded at the end of block jb's epilogue (alpha = 0 masks the padding columns).
+    typedef Stage<T> S;
+    typedef typename Tr::acc_t acc_t;
+    T* nvs = smem + gemm_lds<T>() / sizeof(T);  // [2][GT]
+    T* als = nvs + 2 * GT;                      // [2][GT]
+    const int nblk = (int)((n + GT - 1) / GT);
+    const int NS1 = __builtin_amdgcn_readfirstlane(Kr) / BKS, NS = NS1 + __builtin_amdgcn_readfirstlane(Kp) / BKS;
+    const int64_t total = (int64_t)nblk * NS;
+    const int lcol = lane / S::LPC, lrow = (lane % S::LPC) * S::E;
+    auto issue = [&](int64_t gs) {  // global stage gs: block gs / NS, k-columns (gs % NS) BKS ..
+        const int jb = (int)(gs / NS), sx = (int)(gs % NS);
+        T* buf = smem + (gs % NBUF) * S::STG;
+        const T* A = FU + i0;
+        const T* B = FV + (int64_t)jb * GT;
+#pragma unroll
+        for (int u = 0; u < S::IPW; u++) {
+            const int g = w * S::IPW + u;
+            const bool isB = g >= S::GRP;
+            const int gg = isB ? g - S::GRP : g;
+            const int64_t col = (int64_t)sx * BKS + gg * S::CPI + lcol;
+            const T* src = isB ? (B + lrow + col * nfv) : (A + lrow + col * nfu);
+            __builtin_amdgcn_global_load_lds((const void*)src,
+                                             (__attribute__((address_space(3))) void*)(buf + g * S::SRP), 16, 0, 0);
         }
-        typename Tr::acc_t ar[2][4], ap[2][4];
-        // opaque thread index: the query-side operand addresses are loop-invariant, and
-        // hoisted out of this loop they stayed live in registers across it (spills)
-        int tid = t;
-        asm volatile("" : "+v"(tid));
-        block_stats<T, NPER, R2>(FU, nfu, i0, FV, nfv, j0, Kr, Kp, smem, tid, ar, ap);
+    };
+    auto load_block_consts = [&](int jb) {  // norms / alpha of block jb into parity jb & 1
+        if (t < GT) {
+            const int64_t j = (int64_t)jb * GT + t;
+            if (R2) nvs[(jb & 1) * GT + t] = FV[(int64_t)(Kr + Kp) * nfv + j];
+            als[(jb & 1) * GT + t] = (j < n) ? alpha[j * m] : T(0);
+        }
+    };
+    load_block_consts(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the ring's counted waits see only its loads)
+#pragma unroll
+    for (int p = 0; p < AHEAD; p++)
+        if (p < total) issue(p);
+    auto stage_sync = [&](int64_t gs) {
+        const int64_t ahead = total - 1 - gs;
+        if (AHEAD >= 3 && ahead >= 2) wait_vm<(AHEAD >= 3 ? 2 : 0) * S::IPW>();
+        else if (AHEAD >= 2 && ahead >= 1) wait_vm<S::IPW>();
+        else wait_vm<0>();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (gs + AHEAD < total) issue(gs + AHEAD);
+    };
+    auto stages = [&](acc_t(&acc)[2][4], int64_t gbeg, int64_t gend) {
+#pragma nounroll
+        for (int64_t gs = gbeg; gs < gend; gs++) {
+            stage_sync(gs);
+            const T* a = smem + (gs % NBUF) * S::STG;
+            const T* b = a + S::GRP * S::SRP;
+            T fa[2][4], fb[2][2];
+            auto frag = [&](int kq, int r) {
+                const int kr = kq * 4 + lk;
+                const int ko = (kr / S::CPI) * S::SRP + (kr % S::CPI) * GT;
+#pragma unroll
+                for (int x = 0; x < 2; x++) fb[r][x] = b[ko + wc * 32 + x * 16 + lr];
+#pragma unroll
+                for (int y = 0; y < 4; y++) fa[r][y] = a[ko + wr * 64 + y * 16 + lr];
+            };
+            frag(0, 0);
+#pragma unroll
+            for (int kq = 0; kq < BKS / 4; kq++) {
+                if (kq + 1 < BKS / 4) frag(kq + 1, (kq + 1) & 1);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int x = 0; x < 2; x++)
+#pragma unroll
+                    for (int y = 0; y < 4; y++) acc[x][y] = Tr::mma(fb[kq & 1][x], fa[kq & 1][y], acc[x][y]);
+            }
+        }
+    };
+#pragma nounroll
+    for (int jb = 0; jb < nblk; jb++) {
+        acc_t ar[2][4], ap[2][4];
+#pragma unroll
+        for (int x = 0; x < 2; x++)
+#pragma unroll
+            for (int y = 0; y < 4; y++) {
+                ar[x][y] = acc_t{0};
+                ap[x][y] = acc_t{0};
+            }
+        const int64_t g0 = (int64_t)jb * NS;
+        stages(ar, g0, g0 + NS1);
+        stages(ap, g0 + NS1, g0 + NS);
+        const T* nvb = nvs + (jb & 1) * GT;
+        const T* alb = als + (jb & 1) * GT;
         auto chunk = [&](auto cc) {  // 4 pairs per thread at a time: column (x, reg), rows y
             constexpr int x = decltype(cc)::value >> 2, reg = decltype(cc)::value & 3;
             const int jl = wc * 32 + x * 16 + Tr::orow(lk, reg);
@@ -180,9 +254,9 @@ __global__ __launch_bounds__(NT) void predict_mma_kernel(const KCanon<T>* __rest
 #pragma unroll
             for (int y = 0; y < 4; y++)
                 pair_stats<T, NPER, R2>(R2 ? ar[x][y][reg] : T(0), NPER ? ap[x][y][reg] : T(0), nu[y],
-                                        R2 ? nvs[jl] : T(0), hd, r2[y], sp[y]);
+                                        R2 ? nvb[jl] : T(0), hd, r2[y], sp[y]);
             pair_values<T, 4>(Kd, r2, sp, v);
-            const T al = als[jl];
+            const T al = alb[jl];
 #pragma unroll
             for (int y = 0; y < 4; y++) racc[0][y] = fma(v[y], al, racc[0][y]);
         };
@@ -194,8 +268,12 @@ __global__ __launch_bounds__(NT) void predict_mma_kernel(const KCanon<T>* __rest
         chunk(std::integral_constant<int, 5>{});
         chunk(std::integral_constant<int, 6>{});
         chunk(std::integral_constant<int, 7>{});
-        __syncthreads();  // the staging ring is refilled by the next block's product
+        if (jb + 1 < nblk) {
+            load_block_consts(jb + 1);  // (read after the next stage barrier)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the prefetched stages landed during the epilogue
+        }
     }
+    __syncthreads();  // the reduction below reuses the ring's LDS
     // rows 64 wr + 16 y + lr: sum over the lane groups lk, then over the 4 column waves (LDS)
     T* red = smem;  // [4 wc][128 rows][PM]
 #pragma unroll
@@ -492,7 +570,7 @@ void launch_pair_features(const KCanon<T>& K, const T* X, int64_t n, int d, cons
 
 template <typename T>
 static size_t pairs_lds() {
-    const size_t a = mm::gemm_lds<T>() + sizeof(T) * 2 * GT, b = sizeof(T) * 4 * GT * pr::PM;  // + norms, alpha
+    const size_t a = mm::gemm_lds<T>() + sizeof(T) * 4 * GT, b = sizeof(T) * 4 * GT * pr::PM;  // + norms, alpha (x2)
     return a > b ? a : b;
 }
 
