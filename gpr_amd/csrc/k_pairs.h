@@ -123,6 +123,15 @@ __device__ __forceinline__ void pair_stats(T pr2, T pper, T nu, T nv, T hd, T& r
     r2 = R2 ? clamp0(nu + nv + pr2) : T(0);
     sp = NPER ? clamp0(fma(T(-0.5), pper, hd)) : T(0);
 }
+// the same without the clamps (predict): a rounding-negative statistic (~1e-16 relative, a
+// query on a training point) only moves a kernel value by that much in every leaf form
+// (exp, 1 / (1 + c r2), log1p), and NaN propagates as before; the clamps were 3 of the ~17
+// f64 VALU instructions per pair outside the exps, which bound the predict epilogue
+template <typename T, int NPER, bool R2>
+__device__ __forceinline__ void pair_stats_nc(T pr2, T pper, T nu, T nv, T hd, T& r2, T& sp) {
+    r2 = R2 ? nu + nv + pr2 : T(0);
+    sp = NPER ? fma(T(-0.5), pper, hd) : T(0);
+}
 
 // Tile (i0, j0) of K(X, X) (+ sigma2 on the diagonal, identity beyond n) into A
 // (column-major), from the features FU, FV (nf rows); plain stores of the lower triangle.

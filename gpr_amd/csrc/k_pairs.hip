@@ -247,27 +247,32 @@ __global__ __launch_bounds__(NT) void predict_mma_kernel(const KCanon<T>* __rest
         stages(ap, g0 + NS1, g0 + NS);
         const T* nvb = nvs + (jb & 1) * GT;
         const T* alb = als + (jb & 1) * GT;
-        auto chunk = [&](auto cc) {  // 4 pairs per thread at a time: column (x, reg), rows y
-            constexpr int x = decltype(cc)::value >> 2, reg = decltype(cc)::value & 3;
-            const int jl = wc * 32 + x * 16 + Tr::orow(lk, reg);
-            T r2[4], sp[4], v[4];
+        // 8 pairs per thread at a time (column group x, registers 2h, 2h + 1; rows y): eight
+        // independent exp chains per wave against four -- only two waves share a SIMD
+        auto chunk = [&](auto cc) {
+            constexpr int x = decltype(cc)::value >> 1, h = decltype(cc)::value & 1;
+            T r2[8], sp[8], v[8];
 #pragma unroll
-            for (int y = 0; y < 4; y++)
-                pair_stats<T, NPER, R2>(R2 ? ar[x][y][reg] : T(0), NPER ? ap[x][y][reg] : T(0), nu[y],
-                                        R2 ? nvb[jl] : T(0), hd, r2[y], sp[y]);
-            pair_values<T, 4>(Kd, r2, sp, v);
-            const T al = alb[jl];
+            for (int u = 0; u < 2; u++) {
+                const int reg = 2 * h + u;
+                const int jl = wc * 32 + x * 16 + Tr::orow(lk, reg);
 #pragma unroll
-            for (int y = 0; y < 4; y++) racc[0][y] = fma(v[y], al, racc[0][y]);
+                for (int y = 0; y < 4; y++)
+                    pair_stats_nc<T, NPER, R2>(R2 ? ar[x][y][reg] : T(0), NPER ? ap[x][y][reg] : T(0), nu[y],
+                                               R2 ? nvb[jl] : T(0), hd, r2[4 * u + y], sp[4 * u + y]);
+            }
+            pair_values<T, 8>(Kd, r2, sp, v);
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                const T al = alb[wc * 32 + x * 16 + Tr::orow(lk, 2 * h + u)];
+#pragma unroll
+                for (int y = 0; y < 4; y++) racc[0][y] = fma(v[4 * u + y], al, racc[0][y]);
+            }
         };
         chunk(std::integral_constant<int, 0>{});
         chunk(std::integral_constant<int, 1>{});
         chunk(std::integral_constant<int, 2>{});
         chunk(std::integral_constant<int, 3>{});
-        chunk(std::integral_constant<int, 4>{});
-        chunk(std::integral_constant<int, 5>{});
-        chunk(std::integral_constant<int, 6>{});
-        chunk(std::integral_constant<int, 7>{});
         if (jb + 1 < nblk) {
             load_block_consts(jb + 1);  // (read after the next stage barrier)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the prefetched stages landed during the epilogue
