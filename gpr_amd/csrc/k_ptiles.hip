@@ -991,13 +991,12 @@ __device__ __forceinline__ void diag_factor_la(T* __restrict__ A, int64_t ld, T*
             // est = max|Dinv_p| max_i L_ii (<= cond_2(L_pp), within a factor 32^2 of it): a
             // well-conditioned block skips the refinement -- its explicit-inverse error is then
             // no larger than that of the 128-block TRSM tasks (which also use explicit inverses)
-            T dimin = sDi[c0 + (lane & 31)];  // 1 / L_ii
+            // (min of the 32 diagonal words by broadcast LDS reads, the max test by one ballot:
+            // two 6-step shuffle reductions cost ~0.45 us per panel on the chain)
+            T dimin = sDi[c0];  // 1 / L_ii
 #pragma unroll
-            for (int off = 32; off >= 1; off >>= 1) {
-                dmax = fmax(dmax, __shfl_xor(dmax, off, 64));
-                dimin = fmin(dimin, __shfl_xor(dimin, off, 64));
-            }
-            const bool refine = __builtin_amdgcn_readfirstlane((int)(dmax > T(32) * dimin)) != 0;
+            for (int i = 1; i < 32; i++) dimin = fmin(dimin, sDi[c0 + i]);
+            const bool refine = __ballot(dmax > T(32) * dimin) != 0;
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
             for (int reg = 0; reg < 4; reg++) {  // X0 (kept in a0, a1) through LDS to the operand layout
