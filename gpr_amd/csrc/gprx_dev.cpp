@@ -293,3 +293,14 @@ extern "C" gprx_status gprx_dev_diag_factor(gprx_ctx* ctx, int32_t variant, cons
     (void)hipFree(pr);
     return st;
 }
+
+extern "C" gprx_status gprx_dev_dist_schedule(int32_t nc, int32_t nr, int32_t P, int32_t g, int32_t gb, int32_t build,
+                                              double* est_us) {
+    if (nc < 1 || nr < nc || P < 1 || g < 1 || gb < 1 || !est_us) return GPRX_ERR_ARG;
+    try {
+        (void)potrf_dist_schedule(nc, nr, P, g, gb, build != 0, est_us);
+    } catch (...) {
+        return GPRX_ERR_ARG;
+    }
+    return GPRX_OK;
+}

@@ -30,6 +30,11 @@ gprx_status gprx_dev_bench(gprx_ctx* ctx, gprx_dtype dtype, int32_t what, int64_
  * and simulated makespan (us).  Throws nothing, needs no
  * device: GPRX_ERR_ARG if the ticket order would violate a dependency. */
 gprx_status gprx_dev_schedule(int32_t nc, int32_t nr, int32_t P, int32_t build, double* est_us, int64_t* ntasks);
+/* Host-only: the distributed factorisation's schedule (g ranks of P workers each, row blocks
+ * grouped by gb, build as above), simulated over all ranks with the transports as timed nodes;
+ * returns the simulated makespan (us) -- the figure gprx_dist.cpp picks gb by. */
+gprx_status gprx_dev_dist_schedule(int32_t nc, int32_t nr, int32_t P, int32_t g, int32_t gb, int32_t build,
+                                   double* est_us);
 /* GPRX_PT_DEBUG=1: copy the per-workgroup status {ticket, phase, i, j} of the running (or last)
  * potrf_tiles launch out of pinned host memory, without synchronising; returns workgroups. */
 int32_t gprx_dev_pt_debug(int32_t* out, int32_t max_wg);

@@ -111,3 +111,35 @@ def test_schedule_more_workers_never_slower():
     _, _, e64 = _sched(96, 97, P=64)
     _, _, e256 = _sched(96, 97, P=256)
     assert e256 <= e64
+
+
+def _dist_sched(nc, nr, P, g, gb, build=True):
+    L = lib()
+    L.gprx_dev_dist_schedule.argtypes = [ctypes.c_int32] * 6 + [ctypes.POINTER(ctypes.c_double)]
+    est = ctypes.c_double()
+    st = L.gprx_dev_dist_schedule(nc, nr, P, g, gb, 1 if build else 0, ctypes.byref(est))
+    return st, est.value
+
+
+def test_dist_schedule_makespan_scales_and_is_chain_bound():
+    # C3 (nc = 128, one label row block) on g ranks of 240 workers (gprx_dist.cpp: two CU
+    # slots per XCC reserved for RCCL): more ranks never simulate slower at the best grouping,
+    # and the makespan stays above the DIAGX chain (nc diagonal steps of the cost model's
+    # 70 us) -- the sharded fit is chain-bound at 8 ranks
+    best = {}
+    for g in (1, 2, 4, 8):
+        ests = []
+        for gb in (1, 2, 4, 8):
+            if g > 1 and 128 < 2 * gb * g:
+                continue
+            st, est = _dist_sched(128, 129, 240, g, gb)
+            assert st == 0 and est > 0
+            ests.append(est)
+        best[g] = min(ests)
+    assert best[2] < best[1] and best[4] < best[2] and best[8] <= best[4]
+    assert best[8] > 128 * 70.0
+
+
+def test_dist_schedule_rejects_bad_arguments():
+    assert _dist_sched(0, 1, 240, 1, 1)[0] != 0
+    assert _dist_sched(4, 3, 240, 1, 1)[0] != 0
