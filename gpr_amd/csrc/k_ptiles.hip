@@ -875,7 +875,7 @@ __device__ __forceinline__ void la_store_lpanel(T* __restrict__ A, int64_t ld, c
     const int nr = DB - 32 * q;
     for (int e = tid; e < 32 * nr; e += nth) {
         const int c = 32 * q + e / nr, r = 32 * q + e % nr;
-        A[r + (int64_t)c * ld] = sS[r + c * SIL];
+        st_sc1(A + r + (int64_t)c * ld, sS[r + c * SIL]);  // write-through: no release fence needed
     }
 }
 template <typename T>
@@ -883,7 +883,7 @@ __device__ __forceinline__ void la_store_linv_rows(T* __restrict__ Linv, const T
                                                    const T* __restrict__ sDi, int q, int tid, int nth) {
     for (int e = tid; e < 32 * DB; e += nth) {
         const int c = e >> 5, r = 32 * q + (e & 31);
-        Linv[r + c * DB] = linv_at(sS, sDi, r, c);
+        st_sc1(Linv + r + c * DB, linv_at(sS, sDi, r, c));
     }
 }
 
@@ -1539,7 +1539,9 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
                            a.trace ? a.trace + 4 * (int64_t)(a.ntasks + a.nc) + 4 * (int64_t)k : nullptr,
                            fused_ts && k > 0);
             if (a.trace) dt[3] = wall_clock64();
-            publish(a.lcnt + k, k + 1, true);  // diag_factor stores are plain
+            // the look-ahead factor (f64) stores write-through (sc1) like the tile tasks; the
+            // rank-8 image (f32) stores plain and needs the release fence
+            publish(a.lcnt + k, k + 1, !(std::is_same<T, double>::value && DIAG_LA));
             if constexpr (DIST) publish_host(a.dist->hdiag + k);
             if (a.trace && wv == 0) {
                 long long* dp = a.trace + 4 * (int64_t)a.ntasks + 4 * (int64_t)k;
