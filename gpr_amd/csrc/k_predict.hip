@@ -208,29 +208,28 @@ void launch_rowdot(const T* Va, const T* Vb, int64_t ld, int64_t q, int64_t n, c
 // Solve V L^T = R in place for the rows of R (qp x np, column-major, ld), given the
 // factor L (column-major, ldA) and its diagonal-block inverses: V = R L^{-T}, i.e. each
 // row of V is (L^{-1} r)^T.
-// Blocked right-looking, in groups of TR_GROUP diagonal blocks: inside a group each block is
-// solved with its inverse and updates the rest of the group; the columns right of the group
-// then take ONE update with K = TR_GROUP * 128 (per-block updates with K = 128 paid the tile
-// mainloop's fill and a launch per 128 columns: the variance path ran at 0.49 of peak).
-constexpr int64_t TR_GROUP = 4;
+// Recursive right-looking: the column range [k0, k1) is solved as its left half, ONE update
+// of the right half by the left (K = the left half's width), then the right half; a single
+// 128-block is solved with its inverse.  The updates' K doubles at each level up (8192 at the
+// top for N = 16384): per-block updates with K = 128 paid the tile mainloop's fill and a launch
+// per 128 columns (0.49 of peak); groups of 4 / 8 / 16 blocks gave 0.59 / 0.61 / 0.62.
+template <typename T>
+static void trsm_rows_rec(const T* A, int64_t ldA, const T* Linv, T* R, int64_t ld, int64_t qp, int64_t k0, int64_t k1,
+                          hipStream_t s) {
+    if (k1 - k0 <= DB) {
+        T* Rk = R + k0 * ld;
+        launch_gemm_nt<T>(Rk, ld, Rk, ld, Linv + (k0 / DB) * (int64_t)DB * DB, DB, qp, DB, DB, T(1), T(0), false, s);
+        return;
+    }
+    const int64_t nb = (k1 - k0) / DB, km = k0 + ((nb + 1) / 2) * DB;
+    trsm_rows_rec<T>(A, ldA, Linv, R, ld, qp, k0, km, s);
+    launch_gemm_nt<T>(R + km * ld, ld, R + k0 * ld, ld, A + km + k0 * ldA, ldA, qp, k1 - km, km - k0, T(-1), T(1), false,
+                      s);
+    trsm_rows_rec<T>(A, ldA, Linv, R, ld, qp, km, k1, s);
+}
 template <typename T>
 void trsm_rows(const T* A, int64_t ldA, int64_t np, const T* Linv, T* R, int64_t ld, int64_t qp, hipStream_t s) {
-    for (int64_t g0 = 0; g0 < np; g0 += TR_GROUP * DB) {
-        const int64_t g1 = std::min(np, g0 + TR_GROUP * DB);
-        for (int64_t k0 = g0; k0 < g1; k0 += DB) {
-            T* Rk = R + k0 * ld;
-            launch_gemm_nt<T>(Rk, ld, Rk, ld, Linv + (k0 / DB) * (int64_t)DB * DB, DB, qp, DB, DB, T(1), T(0), false,
-                              s);
-            const int64_t rem = g1 - (k0 + DB);
-            if (rem > 0)
-                launch_gemm_nt<T>(R + (k0 + DB) * ld, ld, Rk, ld, A + (k0 + DB) + k0 * ldA, ldA, qp, rem, DB, T(-1),
-                                  T(1), false, s);
-        }
-        const int64_t rest = np - g1;
-        if (rest > 0)
-            launch_gemm_nt<T>(R + g1 * ld, ld, R + g0 * ld, ld, A + g1 + g0 * ldA, ldA, qp, rest, g1 - g0, T(-1), T(1),
-                              false, s);
-    }
+    if (np > 0) trsm_rows_rec<T>(A, ldA, Linv, R, ld, qp, 0, np, s);
 }
 
 #define GPRX_INST(T)                                                                                         \
