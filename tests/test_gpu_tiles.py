@@ -126,3 +126,26 @@ def test_c3_full_size_residual(ctx):
     # the Jensen bound of SURVEY.md §8(d) keeps the log-determinant finite and positive
     assert 0.0 < info.logdet <= n * (0.15 ** 2 + 0.1 ** 2) + n * np.log(1.0 + 1e-12) + 1.0
     M.close()
+
+
+@pytest.mark.parametrize("ks", ["SumKernel(GaussianKernel(2,0.15,),PeriodicKernel(0.1,3.141592653589793,1,))",
+                                "GaussianExpKernel(-0.3,0.1,)", "RationalQuadraticKernel(1.1,0.6,1.5,)"])
+def test_predict_at_training_points(ctx, ks):
+    """Queries ON training points (and offset copies of them): the MFMA predict's pair
+    statistics r2 = |x~|^2 + |y~|^2 - 2 x~.y~ and S round to tiny negatives there and are
+    used unclamped (k_pairs.h pair_stats_nc); the predictions must still match the oracle's
+    direct differences (lib/GaussianProcess.cpp:54-61)."""
+    sigma = 0.7
+    n, d = 640, 9
+    X, Y = make_data(n, d, 1)
+    M = gpr_amd.Model(ctx, np.float64)
+    M.set_data(X, Y)
+    M.set_kernel(ks)
+    M.set_noise(sigma)
+    M.fit()
+    a_ref, _ = O.fit(ks, X, Y, sigma, np.float64)
+    Xq = np.concatenate([X[::3], X[:50] + 1e-9])
+    p = M.predict(Xq)
+    assert np.all(np.isfinite(p))
+    assert relerr(p, O.predict(ks, X, a_ref, Xq, np.float64)) <= 1e-6
+    M.close()
