@@ -516,8 +516,31 @@ static void lu_solve_model(gprx_model* M, double* B, int m) {
 template <typename T>
 static void model_inverse(gprx_model* M);
 
+// The LU in double on this process's full copy of the samples (np x np workspace): the
+// GPRX_FIT_FORCE_LU path, and the NOT_SPD fallback of a distributed fit, where every rank
+// computes the same factor from its replicated X, Y.
 template <typename T>
-static gprx_status model_fit_dist(gprx_model* M, gprx_fit_info* out) {
+static void lu_fit_replicated(gprx_model* M, gprx_fit_info* out) {
+    hipStream_t s = M->ctx->stream;
+    const KCanon<T>& K = kcanon<T>(M);
+    const int64_t np0 = round_up(M->n, (int64_t)DB);
+    M->np = np0;
+    M->mp = round_up(M->m, GT);
+    M->ld = np0;
+    M->fitted = M->has_alpha = M->inv_ready = M->dist_fitted = M->dist_dense = false;
+    M->info.ensure(sizeof(int));
+    M->flag.ensure(sizeof(int));
+    M->alpha.ensure(sizeof(T) * np0 * M->m);
+    if (K.nper > 0 && !M->host_k) {
+        M->tab.ensure(sizeof(T) * 2 * K.nper * M->n * M->d);
+        launch_sincos_tables<T>(K, M->X.as<T>(), M->n, M->d, M->tab.as<T>(), s);
+    }
+    if (out) std::memset(out, 0, sizeof(*out));
+    lu_fit<T>(M, out);
+}
+
+template <typename T>
+static gprx_status model_fit_dist(gprx_model* M, uint32_t flags, gprx_fit_info* out) {
     gprx_ctx* ctx = M->ctx;
     GPRX_REQUIRE(!M->host_k, GPRX_ERR_STATE, "gprx: a caller-evaluated kernel matrix needs a single-GPU fit");
     hipStream_t s = ctx->stream;
@@ -579,9 +602,19 @@ static gprx_status model_fit_dist(gprx_model* M, gprx_fit_info* out) {
         throw Error{GPRX_ERR_NONFINITE,
                     "GaussianProcess::ComputeKernelMatrixInternal: kernel matrix contains entries which are not finite."};
     check_sched(o.info);
-    if (o.info != INT_MAX)
-        throw Error{GPRX_ERR_NOT_SPD, "gprx: kernel matrix is not positive definite (Cholesky pivot " +
-                                          std::to_string(o.info) + " <= 0; no LU fallback on the distributed path)"};
+    if (o.info != INT_MAX) {
+        // the reference's default inversion is an LU (lib/GaussianProcess.cpp:545-559) and it
+        // never rejects an indefinite K: every rank refactors the same K + s^2 I with the
+        // partial-pivot LU in double (X and Y are replicated, the LU is deterministic, so the
+        // ranks agree bit for bit).  Replicated, like the reference's own serial getrf: an
+        // indefinite K is the exception path, not the sharded fit's workload.
+        if (flags & GPRX_FIT_NO_LU_FALLBACK)
+            throw Error{GPRX_ERR_NOT_SPD, "gprx: kernel matrix is not positive definite (Cholesky pivot " +
+                                              std::to_string(o.info) + " <= 0)"};
+        lu_fit_replicated<T>(M, out);
+        if (out) out->info = o.info;  // the Cholesky's failing pivot, as on one GPU
+        return GPRX_OK;
+    }
     M->method = 0;
     M->fitted = M->has_alpha = M->dist_fitted = true;
     if (M->want_inv) {
@@ -628,25 +661,15 @@ static gprx_status model_fit(gprx_model* M, uint32_t flags, gprx_fit_info* out) 
     // GPRX_FIT_DISTRIBUTED (the same code path on a one-rank communicator)
     GPRX_REQUIRE(!(flags & GPRX_FIT_DISTRIBUTED) || ctx->comm || ctx->virt, GPRX_ERR_STATE,
                  "gprx_model_fit: GPRX_FIT_DISTRIBUTED needs a context from gprx_ctx_create_dist");
-    if ((ctx->comm && ctx->world > 1) || ctx->virt || (flags & GPRX_FIT_DISTRIBUTED)) return model_fit_dist<T>(M, out);
-    M->dist_fitted = false;
-    if (flags & GPRX_FIT_FORCE_LU) {  // the SVD inversion methods' stand-in: LU in double directly
-        const int64_t np0 = round_up(M->n, (int64_t)DB);
-        M->np = np0;
-        M->mp = round_up(M->m, GT);
-        M->ld = np0;
-        M->inv_ready = false;
-        M->info.ensure(sizeof(int));
-        M->flag.ensure(sizeof(int));
-        M->alpha.ensure(sizeof(T) * np0 * M->m);
-        if (K.nper > 0) {
-            M->tab.ensure(sizeof(T) * 2 * K.nper * M->n * M->d);
-            launch_sincos_tables<T>(K, M->X.as<T>(), M->n, M->d, M->tab.as<T>(), s);
-        }
-        if (out) std::memset(out, 0, sizeof(*out));
-        lu_fit<T>(M, out);
+    // the SVD inversion methods' stand-in: the LU in double directly.  On a distributed
+    // context every rank runs it on its replicated X, Y (as the NOT_SPD fallback below)
+    if (flags & GPRX_FIT_FORCE_LU) {
+        lu_fit_replicated<T>(M, out);
         return GPRX_OK;
     }
+    if ((ctx->comm && ctx->world > 1) || ctx->virt || (flags & GPRX_FIT_DISTRIBUTED))
+        return model_fit_dist<T>(M, flags, out);
+    M->dist_fitted = false;
     const int64_t n = M->n, np = round_up(n, (int64_t)DB), mp = round_up(M->m, GT);
     // the explicit inverse rides along in the tile factorisation as np identity rows
     const bool want_inv = M->want_inv && potrf_uses_tiles();
@@ -991,9 +1014,11 @@ static gprx_status model_lml(gprx_model* M, uint32_t flags, double* value, doubl
     try {
         // the likelihood inverts with the GP's method too (include/Likelihood.h:77-79 ->
         // ComputeCoreMatrixWithDeterminant): a matrix the Cholesky rejects takes the LU
+        // the value and gradient come from the factor (and its inverse), never from alpha:
+        // an fp32 model's fp64 refinement of alpha would be thrown away (GPRX_FIT_F32_NO_REFINE)
         st = model_fit<T>(M,
                           ((flags & GPRX_LML_DISTRIBUTED) ? GPRX_FIT_DISTRIBUTED : 0u) |
-                              ((flags & GPRX_LML_FORCE_LU) ? GPRX_FIT_FORCE_LU : 0u),
+                              ((flags & GPRX_LML_FORCE_LU) ? GPRX_FIT_FORCE_LU : 0u) | GPRX_FIT_F32_NO_REFINE,
                           &fi);
     } catch (...) {
         M->want_inv = false;

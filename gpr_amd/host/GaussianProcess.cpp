@@ -389,9 +389,15 @@ void GaussianProcess<T>::Load(std::string prefix) {
         ls >> ks;
         m_Kernel = KernelFactory<T>::GetKernel(ks);
     }
+    // the sample lists were replaced: whatever the device held (samples, factor, alpha, a
+    // host-evaluated K) belongs to the previous state of this object
+    m_DataUploaded = false;
+    m_DeviceFactor = false;
+    m_HostKernel = false;
+    if (m_RegressionVectors.rows() != m_SampleVectors.size() || m_RegressionVectors.cols() != m_OutputDimension)
+        throw std::string("GaussianProcess::Load: regression vectors do not match the samples");
     UploadState();
     ThrowIfFailed(gprx_model_set_alpha(m_Model, m_RegressionVectors.data()), DefaultContext());
-    m_DeviceFactor = false;
     m_Initialized = true;
 }
 

@@ -55,6 +55,9 @@ protected:
         std::vector<double> grad;
     };
     Eval Evaluate(const GaussianProcessTypePointer gp, bool grad, bool compat = true) const {
+        // the kernel swap, the likelihood's refit and the alpha restore are one step for a
+        // concurrent Predict / operator() on the same gp (they take m_DevMu too)
+        std::lock_guard<std::mutex> lk(gp->m_DevMu);
         gp->UploadState();
         if (gp->m_OutputDimension != 1)
             throw std::string("GaussianLogLikelihood: device likelihood supports one output dimension");

@@ -261,6 +261,47 @@ static void io_test3() {
     }
 }
 
+// Load into a GP that was already fitted on OTHER samples (a different count, both ways): the
+// device must drop the old samples, factor and alpha, and predict / operator() must then match
+// the GP that was saved (the reference's Load replaces every member, lib/GaussianProcess.cpp
+// :184-268).
+static std::shared_ptr<GP<double>> reload_gp(unsigned n, double phase) {
+    auto gp = std::make_shared<GP<double>>(std::make_shared<GaussianKernel<double>>(0.7, 1.3));
+    gp->SetSigma(0.05);
+    for (unsigned i = 0; i < n; i++) {
+        GP<double>::VectorType x(2), y(1);
+        x(0) = i * 6.0 / n;
+        x(1) = std::cos(0.3 * i + phase);
+        y(0) = std::sin(x(0) + phase) + 0.3 * x(1);
+        gp->AddSample(x, y);
+    }
+    gp->Initialize();
+    return gp;
+}
+
+static void io_reload_test() {
+    for (int dir = 0; dir < 2; dir++) {
+        const unsigned ns = dir ? 61 : 23, nt = dir ? 23 : 61;  // saved size, target's own size
+        auto src = reload_gp(ns, 0.4);
+        src->Save("/tmp/gpr_amd_reload_test-");
+        auto dst = reload_gp(nt, 1.9);
+        GP<double>::VectorType x(2);
+        x(0) = 2.2;
+        x(1) = 0.1;
+        (void)dst->Predict(x);
+        (void)(*dst)(x, x);  // the target holds its own factor and alpha on the device
+        dst->Load("/tmp/gpr_amd_reload_test-");
+        for (int q = 0; q < 5; q++) {
+            x(0) = 0.3 + 1.1 * q;
+            x(1) = 0.2 * q - 0.4;
+            const double a = src->Predict(x)(0), b = dst->Predict(x)(0);
+            check(std::fabs(a - b) <= 1e-9 * std::max(1.0, std::fabs(a)), "predict after Load " + num(a) + " vs " + num(b));
+            const double ca = (*src)(x, x), cb = (*dst)(x, x);
+            check(std::fabs(ca - cb) <= 1e-9, "posterior variance after Load " + num(ca) + " vs " + num(cb));
+        }
+    }
+}
+
 // Likelihood: value and gradient through the host classes are finite and the gradient
 // matches a central difference of the value (GaussianLikelihoodTest's consistency idea).
 static void lik_test() {
@@ -652,6 +693,7 @@ int main() {
     run("IOTest1", io_test1);
     run("IOTest2", io_test2);
     run("IOTest3", io_test3);
+    run("IOReloadIntoFittedGP", io_reload_test);
     run("LikelihoodGradient", lik_test);
     run("SparseRegression", sparse_test);
     run("SparseLogLikelihood", sparse_lik_test);

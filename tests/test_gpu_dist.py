@@ -140,16 +140,71 @@ def test_virtual_ranks_c3_shape():
         sctx.close()
 
 
+INDEF = "RationalQuadraticKernel(1.2,2,-1,)"  # K + s^2 I indefinite (tests/test_gpu_lu.py)
+
+
+@pytest.mark.parametrize("g", [2, 3])
+def test_virtual_ranks_lu_fallback(g):
+    """An indefinite K on a distributed context: the sharded Cholesky meets a non-positive
+    pivot and every rank refactors with the partial-pivot LU in double, as the reference's
+    default inversion does (lib/GaussianProcess.cpp:545-559) -- the same fit that succeeds on
+    one GPU succeeds here, with the same alpha, predictions and LML gradient."""
+    import gpr_amd
+    n, d, m, sigma = 700, 3, 2, 0.3
+    X, Y = make_data(n, d, m)
+    vctx = gpr_amd.Context(0, virtual=g)
+    try:
+        M, info = _fit(vctx, INDEF, X, Y, sigma, np.float64)
+        assert info.method == 1 and info.info > 0
+        a_ref, C_ref = O.fit(INDEF, X, Y, sigma)
+        assert relerr(M.alpha(), a_ref) <= 1e-6
+        Xq = make_queries(40, d)
+        assert relerr(M.predict(Xq), O.predict(INDEF, X, a_ref, Xq)) <= 1e-6
+        assert relerr(M.core_matrix(), C_ref) <= 1e-6
+        with pytest.raises(gpr_amd.GprxError) as e:
+            M.fit(gpr_amd.gprx.FIT_NO_LU_FALLBACK)
+        assert e.value.status == 2
+        M.close()
+        Y1 = Y[:, :1].copy()
+        M = gpr_amd.Model(vctx, np.float64)
+        M.set_data(X, Y1)
+        M.set_kernel(INDEF)
+        M.set_noise(sigma)
+        v, grad, logdet = M.lml(grad=True)
+        vr, gr, _, ldr = O.lml(INDEF, X, Y1, sigma)
+        assert relerr(grad, gr) <= 1e-6
+        M.close()
+    finally:
+        vctx.close()
+
+
+def test_virtual_ranks_force_lu():
+    """GPRX_FIT_FORCE_LU (the SVD inversion methods) on a distributed context: the LU on every
+    rank, never a Cholesky that could reject the matrix."""
+    import gpr_amd
+    n, d, sigma = 500, 3, 0.5
+    X, Y = make_data(n, d, 1)
+    vctx = gpr_amd.Context(0, virtual=2)
+    try:
+        M, info = _fit(vctx, C3K, X, Y, sigma, np.float64, flags=gpr_amd.gprx.FIT_FORCE_LU)
+        assert info.method == 1
+        a_ref, _ = O.fit(C3K, X, Y, sigma, want_core=False)
+        assert relerr(M.alpha(), a_ref) <= 1e-6
+        M.close()
+    finally:
+        vctx.close()
+
+
 def test_virtual_ranks_not_spd_and_nonfinite():
     import gpr_amd
     vctx = gpr_amd.Context(0, virtual=2)
     try:
         X, Y = make_data(600, 3, 1)
         M, _ = _fit(vctx, C3K, X, Y, 0.5, np.float64)
-        M.set_kernel("RationalQuadraticKernel(1.2,2,-1,)")  # indefinite (tests/test_gpu_lu.py)
+        M.set_kernel(INDEF)
         M.set_noise(0.3)
         with pytest.raises(gpr_amd.GprxError) as e:
-            M.fit()
+            M.fit(gpr_amd.gprx.FIT_NO_LU_FALLBACK)
         assert e.value.status == 2
         X[100, 1] = np.nan
         M.set_data(X, Y)

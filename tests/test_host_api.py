@@ -46,4 +46,4 @@ def test_host_cpu():
 def test_host_gpu_reference_scenarios():
     rc, lines, out = _run("gp_host_test")
     assert rc == 0, out
-    assert len(lines) == 20 and all(l.startswith("PASS") for l in lines), out
+    assert len(lines) == 21 and all(l.startswith("PASS") for l in lines), out
