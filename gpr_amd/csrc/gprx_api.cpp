@@ -206,6 +206,9 @@ struct gprx_ctx {
     int rank = 0, world = 1;
     bool virt = false;          // gprx_ctx_create_virtual: world virtual ranks in this process
     ncclComm_t comm = nullptr;  // RCCL communicator (gprx_ctx_create_dist), world > 1
+    HostColl* hc = nullptr;     // host collectives of a multi-process context (RCCL or the caller's)
+    bool peer = false;          // gprx_ctx_create_peer: the caller's collective, no RCCL
+    int cu_slot = 0, cu_slots = 1;  // GPRX_DIST_SHARED_GPU: ranks of one GPU split its CUs
     hipStream_t stream = nullptr;
     hipStream_t aux = nullptr;  // look-ahead stream of the factorisation
     hipStream_t aux2 = nullptr;  // second look-ahead stream (next panel's later columns)
@@ -259,7 +262,9 @@ struct gprx_model {
     // the current fit is one (its factor is held in tiles per rank: alpha and predict only)
     DistEngineBase* dist_engine = nullptr;
     bool dist_fitted = false;
-    bool dist_dense = false;  // the tiles of a distributed fit assembled into A (ld np) and Linv
+    bool dist_dense = false;  // the tiles of a distributed fit gathered into A (ld np) and Linv
+    bool dist_inv_tiles = false;  // LML-mode distributed fit: C in the ranks' tiles (dist_lml_grad)
+    DistFitOut dist_stats;        // layout, window and memory of the last distributed fit
     // a kernel with no device form: the caller evaluated K (n x n, row-major, T) -- the
     // reference's virtual Kernel<T>::operator() (include/Kernel.h:52-59); see k_hostk.hip
     bool host_k = false;
@@ -539,6 +544,115 @@ static void lu_fit_replicated(gprx_model* M, gprx_fit_info* out) {
     lu_fit<T>(M, out);
 }
 
+// The dense factor of a distributed fit on this process, for the calls that solve with the
+// whole factor (posterior covariance, core matrix, the VALU gradient's C): gathered once per
+// fit from every rank's packed rows (device reads through the mappings of the mailboxes'
+// storage) into A (ld np) and Linv.  The one place a sharded fit holds N^2 on a process.
+template <typename T>
+static void ensure_dense_factor(gprx_model* M) {
+    if (!M->dist_fitted || M->dist_dense) return;
+    const int64_t np = M->np;
+    M->ld = np;
+    M->A.ensure(sizeof(T) * np * np);
+    M->Linv.ensure(sizeof(T) * np * DB);
+    dist_gather_factor<T>(M->dist_engine, M->A.as<T>(), np, M->Linv.as<T>(), M->ctx->stream);
+    M->dist_dense = true;
+}
+
+// fp64 iterative refinement of a SHARDED fp32 fit (the single-GPU refine_f32 restated over the
+// ranks): each process evaluates the fp64 residual r = Y - (K + s2 I) alpha_d only at the rows
+// its ranks own (pair statistics of those rows against all n samples), the correction
+// (L L^T)^{-1} r runs as the sharded forward + back substitutions (k_dsolve.hip) and arrives on
+// every rank, alpha_d += delta everywhere (identical: no reduction needed).
+static void refine_f32_dist(gprx_model* M, gprx_fit_info* out) {
+    gprx_ctx* ctx = M->ctx;
+    hipStream_t s = ctx->stream;
+    const KCanon<double>& K = M->kd;
+    const int64_t n = M->n, np = M->np;
+    const int d = M->d, m = M->m;
+    int steps = 3;
+    if (const char* e = std::getenv("GPRX_REFINE_STEPS")) steps = std::max(0, std::atoi(e));
+    GPRX_HIP(hipEventRecord(ctx->ev[0], s));
+    // the rows this process's ranks own
+    std::vector<int64_t> idx;
+    for (int b : dist_own_blocks(M->dist_engine))
+        for (int64_t r = (int64_t)b * DB; r < std::min<int64_t>(n, (int64_t)(b + 1) * DB); r++) idx.push_back(r);
+    const int64_t q = (int64_t)idx.size(), qp = round_up(std::max<int64_t>(q, 1), GT);
+    DevBuf didx, Xo, fuo, kxo, rhs;
+    didx.ensure(sizeof(int64_t) * std::max<int64_t>(q, 1));
+    GPRX_HIP(hipStreamSynchronize(s));
+    if (q) GPRX_HIP(hipMemcpy(didx.p, idx.data(), sizeof(int64_t) * q, hipMemcpyHostToDevice));
+    M->Xd.ensure(sizeof(double) * n * d);
+    M->Yd.ensure(sizeof(double) * n * m);
+    M->ad.ensure(sizeof(double) * n * m);
+    M->delta.ensure(sizeof(float) * np * m);
+    M->nrm.ensure(2 * sizeof(unsigned long long));
+    kxo.ensure(sizeof(double) * qp * m);
+    rhs.ensure(sizeof(float) * np * m);
+    launch_convert<float, double>(M->X.as<float>(), M->Xd.as<double>(), n * d, s);
+    launch_convert<float, double>(M->Y.as<float>(), M->Yd.as<double>(), n * m, s);
+    launch_convert<float, double>(M->alpha.as<float>(), M->ad.as<double>(), n * m, s);
+    Xo.ensure(sizeof(double) * std::max<int64_t>(q, 1) * d);
+    launch_gather_rows(M->Xd.as<double>(), didx.as<int64_t>(), q, d, Xo.as<double>(), s);
+    const bool mma = pairs_mma_supported<double>(K, 1);
+    if (mma) {
+        const int64_t kf = pairs_feature_cols<double>(K, d);
+        fuo.ensure(sizeof(double) * qp * kf);
+        M->fvd.ensure(sizeof(double) * np * kf);
+        launch_pair_features<double>(K, Xo.as<double>(), q, d, M->Xd.as<double>(), false, fuo.as<double>(), qp, s);
+        launch_pair_features<double>(K, M->Xd.as<double>(), n, d, M->Xd.as<double>(), true, M->fvd.as<double>(), np, s);
+        M->kdev64.ensure(sizeof(KCanon<double>));
+        GPRX_HIP(hipMemcpyAsync(M->kdev64.p, &K, sizeof(KCanon<double>), hipMemcpyHostToDevice, s));
+    } else {
+        if (K.nper > 0) {
+            M->tabd.ensure(sizeof(double) * 2 * K.nper * n * d);
+            launch_sincos_tables<double>(K, M->Xd.as<double>(), n, d, M->tabd.as<double>(), s);
+            fuo.ensure(sizeof(double) * 2 * K.nper * std::max<int64_t>(q, 1) * d);
+            launch_sincos_tables<double>(K, Xo.as<double>(), q, d, fuo.as<double>(), s);
+        }
+        M->zd.ensure(sizeof(double) * n * m);
+        M->outd.ensure(sizeof(double) * std::max<int64_t>(n, qp) * m);
+    }
+    const float sf = (float)M->sigma;
+    const double s2 = (double)(sf * sf);  // m_Sigma * m_Sigma in T (lib/GaussianProcess.cpp:379)
+    double rel = 0;
+    int taken = 0;
+    for (int it = 0; it < steps; it++) {
+        if (mma) {
+            for (int c = 0; c < m; c++)
+                launch_predict_mma<double>(K, M->kdev64.as<KCanon<double>>(), fuo.as<double>(), qp, M->fvd.as<double>(),
+                                           np, d, M->ad.as<double>() + c, n, m, q, kxo.as<double>() + c, s);
+        } else {
+            launch_predict<double>(K, M->Xd.as<double>(), M->tabd.as<double>(), n, d, m, M->ad.as<double>(),
+                                   Xo.as<double>(), fuo.as<double>(), q, kxo.as<double>(), nullptr, M->zd.as<double>(),
+                                   M->outd.as<double>(), s);
+        }
+        GPRX_HIP(hipMemsetAsync(rhs.p, 0, sizeof(float) * np * m, s));
+        launch_residual_scatter(M->Yd.as<double>(), kxo.as<double>(), M->ad.as<double>(), s2, didx.as<int64_t>(), q, m,
+                                rhs.as<float>(), s);
+        dist_solve<float>(M->dist_engine, rhs.as<float>(), M->delta.as<float>(), s);
+        launch_refine_accumulate(M->delta.as<float>(), M->ad.as<double>(), M->alpha.as<float>(), n * m,
+                                 M->nrm.as<unsigned long long>(), s);
+        unsigned long long h[2];
+        download(h, M->nrm.p, sizeof(h), s);
+        double dn, an;
+        std::memcpy(&dn, &h[0], sizeof(double));
+        std::memcpy(&an, &h[1], sizeof(double));
+        rel = an > 0 ? dn / an : dn;
+        taken = it + 1;
+        if (!(rel > 0x1p-26)) break;  // below fp32 resolution of alpha (NaN: stop too)
+    }
+    GPRX_HIP(hipEventRecord(ctx->ev[1], s));
+    GPRX_HIP(hipEventSynchronize(ctx->ev[1]));
+    if (out) {
+        float ms = 0;
+        hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[1]);
+        out->ms_refine = ms;
+        out->refine_delta = rel;
+        out->refine_steps = taken;
+    }
+}
+
 template <typename T>
 static gprx_status model_fit_dist(gprx_model* M, uint32_t flags, gprx_fit_info* out) {
     gprx_ctx* ctx = M->ctx;
@@ -581,13 +695,16 @@ static gprx_status model_fit_dist(gprx_model* M, uint32_t flags, gprx_fit_info* 
     C.rank = ctx->rank;
     C.world = ctx->world;
     C.virt = ctx->virt;
-    C.comm = ctx->comm;
-    C.stream = s;
-    DistFitIn<T> in{K, M->X.as<T>(), M->Y.as<T>(), n, M->d, M->m, sigma2, tb};
+    C.hc = ctx->hc;
+    C.cu_slot = ctx->cu_slot;
+    C.cu_slots = ctx->cu_slots;
+    // LML mode: the inverse rides along in the sharded launch (identity rows + C tiles) when the
+    // gradient pass can read C tile by tile; other trees take a dense C on every process
+    const bool inv_tiles = M->want_inv && pairs_grad_supported<T>(K);
+    DistFitIn<T> in{K, M->X.as<T>(), M->Y.as<T>(), n, M->d, M->m, sigma2, tb, inv_tiles};
     DistFitOut o;
-    const auto t0 = std::chrono::steady_clock::now();
-    dist_fit<T>(M->dist_engine, C, in, o, M->alpha.as<T>(), ctx->ex);
-    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    dist_fit<T>(M->dist_engine, C, in, o, M->alpha.as<T>());
+    M->dist_stats = o;
     if (out) {
         std::memset(out, 0, sizeof(*out));
         out->logdet = o.logdet;
@@ -596,7 +713,6 @@ static gprx_status model_fit_dist(gprx_model* M, uint32_t flags, gprx_fit_info* 
         out->ms_factor = o.ms_kernel;  // device time of this process's persistent launch(es)
         out->ms_solve = o.ms_solve;
         out->refine_delta = 0;
-        (void)ms;  // host wall time of the whole distributed fit (GPRX_DIST_TRACE prints it)
     }
     if (hflag || o.flag)
         throw Error{GPRX_ERR_NONFINITE,
@@ -617,34 +733,25 @@ static gprx_status model_fit_dist(gprx_model* M, uint32_t flags, gprx_fit_info* 
     }
     M->method = 0;
     M->fitted = M->has_alpha = M->dist_fitted = true;
+    M->dist_inv_tiles = inv_tiles;
     if (M->want_inv) {
-        // the LML gradient: C = (K + s^2 I)^{-1} on this process from the dense factor every
-        // rank can assemble from its tiles (replicated potri); the gradient
-        // is then reduced over the ranks' row blocks (model_lml)
-        M->ld = np;
-        M->A.ensure(sizeof(T) * np * np);
-        M->Linv.ensure(sizeof(T) * np * DB);
-        dist_assemble_factor<T>(M->dist_engine, M->A.as<T>(), np, M->Linv.as<T>(), s);
-        M->dist_dense = true;
-        model_inverse<T>(M);
+        if (!inv_tiles) {
+            // a tree off the MFMA gradient path: its VALU gradient reads a dense C, formed on
+            // every process from the gathered factor (documented N^2 per process)
+            ensure_dense_factor<T>(M);
+            model_inverse<T>(M);
+        }
         M->inv_ready = true;
+    }
+    if constexpr (std::is_same<T, float>::value) {
+        // the reference inverts fp32 GPs in double (include/LAPACKUtils.h:85-97): fp64
+        // refinement of alpha against the sharded fp32 factor, as on one GPU
+        if (!(flags & GPRX_FIT_F32_NO_REFINE) && !M->want_inv) refine_f32_dist(M, out);
     }
     return GPRX_OK;
 }
 
-// The dense factor of a distributed fit on this process, for the calls that solve with the
-// whole factor (posterior covariance, core matrix): every rank holds every tile after the fit
-// (its own and the received ones), assembled once per fit into A (ld np) and Linv.
-template <typename T>
-static void ensure_dense_factor(gprx_model* M) {
-    if (!M->dist_fitted || M->dist_dense) return;
-    const int64_t np = M->np;
-    M->ld = np;
-    M->A.ensure(sizeof(T) * np * np);
-    M->Linv.ensure(sizeof(T) * np * DB);
-    dist_assemble_factor<T>(M->dist_engine, M->A.as<T>(), np, M->Linv.as<T>(), M->ctx->stream);
-    M->dist_dense = true;
-}
+
 
 // ---------------------------------------------------------------------------------------
 // fit
@@ -659,15 +766,15 @@ static gprx_status model_fit(gprx_model* M, uint32_t flags, gprx_fit_info* out) 
     const KCanon<T>& K = kcanon<T>(M);
     // multi-GPU factorisation: an RCCL context with world > 1, a virtual-rank context, or
     // GPRX_FIT_DISTRIBUTED (the same code path on a one-rank communicator)
-    GPRX_REQUIRE(!(flags & GPRX_FIT_DISTRIBUTED) || ctx->comm || ctx->virt, GPRX_ERR_STATE,
-                 "gprx_model_fit: GPRX_FIT_DISTRIBUTED needs a context from gprx_ctx_create_dist");
+    GPRX_REQUIRE(!(flags & GPRX_FIT_DISTRIBUTED) || ctx->hc || ctx->virt, GPRX_ERR_STATE,
+                 "gprx_model_fit: GPRX_FIT_DISTRIBUTED needs a context from gprx_ctx_create_dist / _peer");
     // the SVD inversion methods' stand-in: the LU in double directly.  On a distributed
     // context every rank runs it on its replicated X, Y (as the NOT_SPD fallback below)
     if (flags & GPRX_FIT_FORCE_LU) {
         lu_fit_replicated<T>(M, out);
         return GPRX_OK;
     }
-    if ((ctx->comm && ctx->world > 1) || ctx->virt || (flags & GPRX_FIT_DISTRIBUTED))
+    if ((ctx->hc && ctx->world > 1) || ctx->virt || (flags & GPRX_FIT_DISTRIBUTED))
         return model_fit_dist<T>(M, flags, out);
     M->dist_fitted = false;
     const int64_t n = M->n, np = round_up(n, (int64_t)DB), mp = round_up(M->m, GT);
@@ -1062,7 +1169,8 @@ static gprx_status model_lml(gprx_model* M, uint32_t flags, double* value, doubl
             else
                 launch_convert<double, T>(luC.as<double>(), M->C.as<T>(), M->np * M->np, s);
             GPRX_HIP(hipStreamSynchronize(s));
-        } else if (!M->inv_ready) {
+        } else if (!M->inv_ready || (M->dist_fitted && !M->dist_inv_tiles && !M->dist_dense)) {
+            ensure_dense_factor<T>(M);
             model_inverse<T>(M);
         }
         M->grad.ensure(sizeof(double) * MAX_LEAF * 3);
@@ -1083,28 +1191,13 @@ static gprx_status model_lml(gprx_model* M, uint32_t flags, double* value, doubl
             M->scratch2.ensure(sizeof(T) * np * std::max<int64_t>(kg, 1));
             const int64_t nt = np / GT;
             M->pack.ensure(sizeof(double) * MAX_LEAF * 3 * nt * (nt + 1) / 2);
-            if (M->dist_fitted) {
-                // distributed context: each rank sums the tiles of its own row blocks and one
-                // all-reduce of the partials gives the gradient; virtual
-                // ranks (all in this process) add their partials here
-                int g = 1, gb = 1, r0 = 0;
-                bool virt = false;
-                dist_layout(M->dist_engine, &g, &gb, &r0, &virt);
-                double tot[MAX_LEAF * 3] = {0};
-                for (int r = virt ? 0 : r0; r < (virt ? g : r0 + 1); r++) {
-                    launch_lml_grad_mma<T>(K, M->kdev.as<KCanon<T>>(), M->X.as<T>(), M->n, M->d, M->featU.as<T>(),
-                                           M->featV.as<T>(), M->scratch1.as<T>(), M->scratch2.as<T>(), np,
-                                           M->alpha.as<T>(), M->C.as<T>(), M->np, M->pack.as<double>(),
-                                           M->grad.as<double>(), s, g, r, gb);
-                    if (!virt) {
-                        dist_allreduce_sum(M->dist_engine, M->grad.as<double>(), MAX_LEAF * 3, s);
-                        break;
-                    }
-                    double part[MAX_LEAF * 3];
-                    download(part, M->grad.p, sizeof(part), s);
-                    for (int q = 0; q < MAX_LEAF * 3; q++) tot[q] += part[q];
-                }
-                if (virt) upload<double>(M->grad, tot, sizeof(tot), s);
+            if (M->dist_fitted && M->dist_inv_tiles) {
+                // sharded fit in LML mode: each rank sums (alpha alpha^T - C) o dK/dp over the
+                // lower tiles of its own row blocks, C straight from its packed C tiles (the
+                // sharded potri riding along in the factorisation); one reduction over the ranks
+                dist_lml_grad<T>(M->dist_engine, K, M->kdev.as<KCanon<T>>(), M->X.as<T>(), M->n, M->d,
+                                 M->featU.as<T>(), M->featV.as<T>(), M->scratch1.as<T>(), M->scratch2.as<T>(), np,
+                                 M->alpha.as<T>(), M->pack.as<double>(), M->grad.as<double>(), s);
             } else {
                 launch_lml_grad_mma<T>(K, M->kdev.as<KCanon<T>>(), M->X.as<T>(), M->n, M->d, M->featU.as<T>(),
                                        M->featV.as<T>(), M->scratch1.as<T>(), M->scratch2.as<T>(), np,
@@ -1580,6 +1673,8 @@ static void sparse_normal_eq(gprx_ctx* ctx, SparseNE<T>& st, const gprx_kernel_d
         const ncclResult_t r =
             ncclAllReduce(dS.p, dS.p, (size_t)(ld * Mp), nccl_type<T>(), ncclSum, ctx->comm, s);
         if (r != ncclSuccess) throw Error{GPRX_ERR_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(r)};
+    } else if (ctx->peer && ctx->world > 1) {  // the caller's collective (host round trip)
+        hostcoll_allreduce_dev<T>(ctx->hc, dS.as<T>(), (int)(ld * Mp), s);
     }
     // ---- S = K + accumulated; K separately for Kinv ----------------------------------------
     dK.ensure(sizeof(T) * Mp * Mp);
@@ -1792,7 +1887,7 @@ static gprx_status sparse_lml_impl(gprx_ctx* ctx, const gprx_kernel_desc* desc, 
     if (hflag)
         throw Error{GPRX_ERR_NONFINITE,
                     "GaussianProcess::ComputeKernelMatrixInternal: kernel matrix contains entries which are not finite."};
-    if (ctx->comm) {  // rows sharded over the ranks: the data terms and the N x M gradient partials
+    if (ctx->comm || (ctx->peer && ctx->world > 1)) {  // rows sharded over the ranks: the data terms and the N x M gradient partials
         // (the M x M part is the same on every rank: added once, after the reduction)
         double loc[MAX_LEAF * 3 + 2];
         for (int q = 0; q < MAX_LEAF * 3; q++) loc[q] = acc_x[q];
@@ -1800,8 +1895,12 @@ static gprx_status sparse_lml_impl(gprx_ctx* ctx, const gprx_kernel_desc* desc, 
         loc[MAX_LEAF * 3 + 1] = nn;
         DevBuf dl;
         upload<double>(dl, loc, sizeof(loc), s);
-        const ncclResult_t r = ncclAllReduce(dl.p, dl.p, MAX_LEAF * 3 + 2, ncclFloat64, ncclSum, ctx->comm, s);
-        if (r != ncclSuccess) throw Error{GPRX_ERR_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(r)};
+        if (ctx->comm) {
+            const ncclResult_t r = ncclAllReduce(dl.p, dl.p, MAX_LEAF * 3 + 2, ncclFloat64, ncclSum, ctx->comm, s);
+            if (r != ncclSuccess) throw Error{GPRX_ERR_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(r)};
+        } else {
+            hostcoll_allreduce_dev<double>(ctx->hc, dl.as<double>(), MAX_LEAF * 3 + 2, s);
+        }
         download(loc, dl.p, sizeof(loc), s);
         for (int q = 0; q < MAX_LEAF * 3; q++) acc_x[q] = loc[q];
         yty = loc[MAX_LEAF * 3];
@@ -1919,6 +2018,7 @@ void gprx_ctx_destroy(gprx_ctx* ctx) {
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
     if (ctx->aux2) (void)hipStreamDestroy(ctx->aux2);
+    delete ctx->hc;
     if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
     delete ctx;
 }
@@ -2331,6 +2431,24 @@ gprx_status gprx_dev_build_time(gprx_ctx* ctx, gprx_dtype dt, const gprx_kernel_
     API_END(ctx)
 }
 
+gprx_status gprx_dev_dist_info(gprx_model* M, int64_t* out) {
+    API_BEGIN
+    GPRX_REQUIRE(M && out, GPRX_ERR_ARG, "gprx_dev_dist_info: NULL argument");
+    GPRX_REQUIRE(M->dist_fitted || M->dist_stats.bytes_rank > 0, GPRX_ERR_STATE,
+                 "gprx_dev_dist_info: no distributed fit on this model");
+    const DistFitOut& o = M->dist_stats;
+    out[0] = o.bytes_rank;
+    out[1] = o.bytes_storage;
+    out[2] = o.gb;
+    out[3] = o.ww;
+    out[4] = o.chunk_w;
+    out[5] = o.P;
+    out[6] = (int64_t)o.est_us;
+    out[7] = M->ctx->world;
+    return GPRX_OK;
+    API_END(M ? M->ctx : nullptr)
+}
+
 gprx_status gprx_dist_unique_id(void* out) {
     API_BEGIN
     GPRX_REQUIRE(out, GPRX_ERR_ARG, "gprx_dist_unique_id: out is NULL");
@@ -2368,6 +2486,26 @@ gprx_status gprx_ctx_create_dist(int device, int rank, int world, const void* un
     if (r != ncclSuccess) {
         gprx_ctx_destroy(ctx);
         throw Error{GPRX_ERR_RCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(r)};
+    }
+    ctx->hc = make_rccl_coll(ctx->comm, world, device);
+    *out = ctx;
+    return GPRX_OK;
+    API_END(nullptr)
+}
+
+gprx_status gprx_ctx_create_peer(int device, int rank, int world, gprx_allgather_fn fn, void* user, gprx_ctx** out) {
+    API_BEGIN
+    GPRX_REQUIRE(out && fn, GPRX_ERR_ARG, "gprx_ctx_create_peer: NULL argument");
+    GPRX_REQUIRE(world >= 1 && world <= 32 && rank >= 0 && rank < world, GPRX_ERR_ARG,
+                 "gprx_ctx_create_peer: bad rank/world");
+    gprx_ctx* ctx = ctx_new(device);
+    ctx->rank = rank;
+    ctx->world = world;
+    ctx->peer = true;
+    ctx->hc = make_callback_coll(fn, user, world);
+    if (const char* e = std::getenv("GPRX_DIST_SHARED_GPU"); e && std::atoi(e) != 0) {
+        ctx->cu_slot = rank;
+        ctx->cu_slots = world;
     }
     *out = ctx;
     return GPRX_OK;

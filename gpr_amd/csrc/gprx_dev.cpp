@@ -294,11 +294,18 @@ extern "C" gprx_status gprx_dev_diag_factor(gprx_ctx* ctx, int32_t variant, cons
     return st;
 }
 
-extern "C" gprx_status gprx_dev_dist_schedule(int32_t nc, int32_t nr, int32_t P, int32_t g, int32_t gb, int32_t build,
-                                              double* est_us) {
-    if (nc < 1 || nr < nc || P < 1 || g < 1 || gb < 1 || !est_us) return GPRX_ERR_ARG;
+extern "C" gprx_status gprx_dev_dist_schedule(int32_t nc, int32_t P, int32_t g, int32_t gb, int32_t ww, int32_t flags,
+                                              double* est_us, int32_t* chunk_w, int64_t* ntasks) {
+    if (nc < 1 || P < 1 || g < 1 || g > 32 || gb < 1 || ww < 1 || !est_us) return GPRX_ERR_ARG;
     try {
-        (void)potrf_dist_schedule(nc, nr, P, g, gb, build != 0, est_us);
+        const DistSched S = potrf_dist_schedule(nc, g, gb, ww, P, (flags & 1) != 0, (flags & 2) != 0);
+        *est_us = S.est_us;
+        if (chunk_w) *chunk_w = S.W;
+        if (ntasks) {
+            int64_t t = 0;
+            for (const auto& l : S.lists) t += (int64_t)l.size();
+            *ntasks = t;
+        }
     } catch (...) {
         return GPRX_ERR_ARG;
     }

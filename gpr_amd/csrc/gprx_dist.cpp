@@ -3,31 +3,38 @@
 //
 // Replaces the same reference step as the single-GPU fit -- GaussianProcess::Initialize ->
 // ComputeRegressionVectors, kernel matrix + lapack::lu_invert + C Y (lib/GaussianProcess.cpp
-// :118-130, 642-672; include/LAPACKUtils.h:38-56) -- for a matrix dealt over g ranks:
+// :118-130, 642-672; include/LAPACKUtils.h:38-56) -- and the likelihood's inverse
+// (include/Likelihood.h:204-285) for a matrix dealt over g ranks:
 //
-//   storage   row block i (128 rows) lives on rank (i / gb) mod g (groups of gb blocks dealt
-//             cyclically; gb from the simulated makespan): N^2/g of the lower factor per rank,
-//             plus the tiles of other ranks' rows it receives (each rank ends with the whole
-//             factor, in tiles, so the solve runs locally everywhere)
+//   storage   row block i (128 rows; i = nc is the label block Y^T) lives on rank (i / gb) mod g
+//             (groups of gb blocks dealt cyclically; gb from the simulated makespan).  A rank
+//             keeps only the LOWER tiles of its own row blocks, packed (PtDist,
+//             gprx_internal.h): ~N^2 / (2 g) of the factor.  Tiles of other ranks' rows pass
+//             through a bounded WINDOW of ww panels (flow-controlled, below).
 //   compute   each rank runs the persistent tile-dataflow launch (k_ptiles.hip,
 //             potrf_tiles_kernel<T, true>) over its own row blocks: covariance BUILD tasks,
 //             DIAGX (the diagonal 128-block chain), TRSM and UPD tasks, in the order of a list
 //             schedule simulated over all ranks (potrf_dist_schedule)
-//   exchange  per diagonal step k two transport steps, issued by this host thread as the
-//             device reports its pieces ready (host-visible flags the kernel stores):
-//             bcast(k)  Linv_k, the inverse of the factored diagonal block, from its rank to
-//                       all (RCCL ncclBroadcast over xGMI): the only exchange on the chain
-//             panel(k)  every final tile L_ik (i > k) from its rank to every other rank, one
-//                       message per (rank, peer) pair fused in an RCCL group: the full-mesh
-//                       all-gather of the panel, off the chain
-//             each followed by a stream write of a counter the kernel polls (uncached memory)
-//   reduce    log det (each rank's diagonal blocks) and the non-finite / pivot flags: one
-//             RCCL all-reduce each at the end
+//   exchange  device-initiated, no host thread in the loop: a task that finishes a tile other
+//             ranks read stores it straight into their mailboxes (xGMI peer stores through IPC
+//             mappings; the same process's memory for virtual ranks) and raises their per-tile
+//             flag; DIAGX(k) pushes Linv_k to every rank -- the north star's broadcast of the
+//             diagonal panel, issued by the kernel that produced it
+//   flow      a window slot is refilled with panel p + ww only after every consumer released
+//             panel p (its last window-reading update chunk done), so per-rank memory stays
+//             N^2/(2g) + ww N 128 s + O(N 128 s) at any N
+//   solve     alpha by a distributed back substitution (k_dsolve.hip): partial sums pushed to the
+//             owner of each block, alpha_k pushed to every rank
+//   reduce    log det (each rank's diagonal blocks), data fit, status: one host all-gather of a
+//             few bytes per fit (RCCL, or the caller's collective)
+//   LML mode  the inverse's identity rows ride along on their row's rank (U = L^{-T}) and the
+//             lower C = U U^T accumulates in tiles of the same launch: the sharded potri
+//             (SURVEY.md 8(f) rank 2); the gradient is reduced from each rank's own C tiles
 //
-// A second transport runs g "virtual ranks" in one process on one GPU (gprx_ctx_create_virtual,
-// include/gprx_dev.h): the same kernels, buffers and issue loop, with device copies in place
-// of RCCL -- the distributed algorithm, exchange protocol and deadlock freedom testable on a
-// single GPU (tests/test_gpu_dist.py).
+// A second form runs g "virtual ranks" in one process on one GPU (gprx_ctx_create_virtual,
+// include/gprx_dev.h): the same kernels, each rank on its own share of the CUs, pushing into the
+// other ranks' buffers directly -- the distributed algorithm, exchange protocol and deadlock
+// freedom testable on a single GPU (tests/test_gpu_dist.py).
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -37,10 +44,8 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
-#include <map>
 #include <memory>
 #include <string>
-#include <thread>
 #include <vector>
 
 #include "gprx_dist.h"
@@ -49,34 +54,20 @@ namespace gprx {
 
 namespace {
 
-template <typename T>
-ncclDataType_t nccl_t();
-template <>
-ncclDataType_t nccl_t<double>() {
-    return ncclFloat64;
-}
-template <>
-ncclDataType_t nccl_t<float>() {
-    return ncclFloat32;
-}
-
 void rccl_ok(ncclResult_t r, const char* what) {
     if (r != ncclSuccess) throw Error{GPRX_ERR_RCCL, std::string(what) + ": " + ncclGetErrorString(r)};
 }
 
-// one device allocation, optionally fine-grained / uncached
+// one device allocation, optionally fine-grained (the mailbox: stored into by other GPUs)
 struct DMem {
     void* p = nullptr;
     size_t bytes = 0;
-    unsigned flags = 0;
-    void ensure(size_t b, unsigned fl = 0) {
-        if (p && b <= bytes && fl == flags) return;
+    void alloc(size_t b, bool fine) {
         release();
-        if (b == 0) return;
-        if (fl) GPRX_HIP(hipExtMallocWithFlags(&p, b, fl));
+        if (b == 0) b = 256;
+        if (fine) GPRX_HIP(hipExtMallocWithFlags(&p, b, hipDeviceMallocFinegrained));
         else GPRX_HIP(hipMalloc(&p, b));
         bytes = b;
-        flags = fl;
     }
     void release() {
         if (p) (void)hipFree(p);
@@ -90,84 +81,139 @@ struct DMem {
     ~DMem() { release(); }
 };
 
-struct HMem {  // coherent host memory the device stores to (kernel -> issue loop)
-    void* p = nullptr;
-    size_t bytes = 0;
-    void ensure(size_t b) {
-        if (p && b <= bytes) return;
-        release();
-        GPRX_HIP(hipHostMalloc(&p, b, hipHostMallocCoherent | hipHostMallocMapped));
-        bytes = b;
-    }
-    void release() {
-        if (p) (void)hipHostFree(p);
-        p = nullptr;
-        bytes = 0;
-    }
-    unsigned* u() const { return reinterpret_cast<unsigned*>(p); }
-    ~HMem() { release(); }
-};
+template <typename U>
+void upload_vec(DMem& m, const std::vector<U>& v) {
+    m.alloc(sizeof(U) * std::max<size_t>(1, v.size()), false);
+    if (!v.empty()) GPRX_HIP(hipMemcpy(m.p, v.data(), sizeof(U) * v.size(), hipMemcpyHostToDevice));
+}
+
+int64_t align256(int64_t b) { return (b + 255) / 256 * 256; }
 
 }  // namespace
 
 // ---------------------------------------------------------------------------------------
-// layout: which rank holds which tile, where the send slots and received tiles live
+// host collectives
+// ---------------------------------------------------------------------------------------
+struct RcclColl : HostColl {
+    ncclComm_t comm;
+    int world, device;
+    hipStream_t s = nullptr;
+    DMem sb, rb;
+    RcclColl(ncclComm_t c, int w, int d) : comm(c), world(w), device(d) {
+        GPRX_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    }
+    ~RcclColl() override {
+        if (s) (void)hipStreamDestroy(s);
+    }
+    void allgather(const void* send, size_t bytes, void* recv) override {
+        if (world == 1) {
+            std::memcpy(recv, send, bytes);
+            return;
+        }
+        if (sb.bytes < bytes) sb.alloc(bytes, false);
+        if (rb.bytes < bytes * world) rb.alloc(bytes * world, false);
+        GPRX_HIP(hipMemcpy(sb.p, send, bytes, hipMemcpyHostToDevice));
+        rccl_ok(ncclAllGather(sb.p, rb.p, bytes, ncclUint8, comm, s), "ncclAllGather");
+        GPRX_HIP(hipStreamSynchronize(s));
+        GPRX_HIP(hipMemcpy(recv, rb.p, bytes * world, hipMemcpyDeviceToHost));
+    }
+};
+HostColl* make_rccl_coll(ncclComm_t comm, int world, int device) { return new RcclColl(comm, world, device); }
+
+struct CallbackColl : HostColl {
+    gprx_allgather_fn fn;
+    void* user;
+    int world;
+    CallbackColl(gprx_allgather_fn f, void* u, int w) : fn(f), user(u), world(w) {}
+    void allgather(const void* send, size_t bytes, void* recv) override {
+        if (fn(user, send, bytes, recv) != 0) throw Error{GPRX_ERR_RCCL, "gprx: the caller's all-gather failed"};
+    }
+};
+HostColl* make_callback_coll(gprx_allgather_fn fn, void* user, int world) { return new CallbackColl(fn, user, world); }
+
+template <typename T>
+void hostcoll_allreduce_dev(HostColl* hc, T* dev, int count, hipStream_t s) {
+    std::vector<T> mine(count);
+    GPRX_HIP(hipStreamSynchronize(s));
+    GPRX_HIP(hipMemcpy(mine.data(), dev, sizeof(T) * count, hipMemcpyDeviceToHost));
+    int world = 1;
+    if (auto* r = dynamic_cast<RcclColl*>(hc)) world = r->world;
+    if (auto* c = dynamic_cast<CallbackColl*>(hc)) world = c->world;
+    std::vector<T> all((size_t)count * world);
+    hc->allgather(mine.data(), sizeof(T) * count, all.data());
+    for (int e = 0; e < count; e++) {  // rank order: every rank sums identically
+        T v = 0;
+        for (int q = 0; q < world; q++) v += all[(size_t)q * count + e];
+        mine[e] = v;
+    }
+    GPRX_HIP(hipMemcpy(dev, mine.data(), sizeof(T) * count, hipMemcpyHostToDevice));
+}
+template void hostcoll_allreduce_dev<double>(HostColl*, double*, int, hipStream_t);
+template void hostcoll_allreduce_dev<float>(HostColl*, float*, int, hipStream_t);
+
+// ---------------------------------------------------------------------------------------
+// layout: which rank holds which row block, and where in its packed storage
 // ---------------------------------------------------------------------------------------
 struct DistLayout {
-    // Row block i (128 rows; i = nc is the label block) lives on rank (i / gb) mod g: groups
-    // of gb consecutive blocks dealt cyclically.  gb > 1 keeps gb - 1 of every gb diagonal
-    // steps on one rank (the chain DIAGX(k) -> DIAGX(k + 1) then needs no broadcast hop).
-    int g = 1, gb = 1, nc = 0, nr = 0;
-    std::vector<int> own, lidx;          // per row block: owner rank, index in its rows
-    std::vector<std::vector<int>> rows;  // per rank: owned row blocks, ascending
-    int owner(int i) const { return own[i]; }
-    int loc(int i) const { return lidx[i]; }
-    int nloc(int q) const { return (int)rows[q].size(); }
-    int firstpos(int q, int b) const {  // index in rows[q] of the first row block > b
-        return (int)(std::upper_bound(rows[q].begin(), rows[q].end(), b) - rows[q].begin());
-    }
-    int cnt(int q, int b) const { return nloc(q) - firstpos(q, b); }  // row blocks in (b, nr) on q
-    int pos(int q, int i, int b) const { return lidx[i] - firstpos(q, b); }
-    // send slot offsets (tiles) of rank q: panel b after all earlier panels
-    std::vector<std::vector<int64_t>> soff;             // [q][b]
-    std::vector<std::vector<std::vector<int64_t>>> roff;  // [r][b][q]: rank r's received chunk from q
-    std::vector<int64_t> stot, rtot;
-    void init(int g_, int gb_, int nc_, int nr_) {
+    int g = 1, gb = 1, nc = 0, nr = 0, nci = 0;
+    bool inv = false;
+    std::vector<int> own, loc;            // per row block: owner rank, index among its rows
+    std::vector<std::vector<int>> rows;   // per rank: owned row blocks, ascending
+    std::vector<std::vector<int64_t>> roff;  // per rank: element offset of each own row block
+    std::vector<int64_t> elems;           // per rank: storage elements
+    int ncols(int i) const { return i < nc ? i + 1 : (i == nc ? nc : nc + 1); }
+    void init(int g_, int gb_, int nc_, bool inv_) {
         g = g_;
         gb = std::max(1, gb_);
         nc = nc_;
-        nr = nr_;
+        inv = inv_;
+        nr = nc + 1 + (inv ? nc : 0);
+        nci = inv ? 2 * nc : nc;
         own.assign(nr, 0);
-        lidx.assign(nr, 0);
-        rows.assign(g, std::vector<int>());
+        loc.assign(nr, 0);
+        rows.assign(g, {});
         for (int i = 0; i < nr; i++) {
-            own[i] = (i / gb) % g;
-            lidx[i] = (int)rows[own[i]].size();
+            own[i] = i <= nc ? (i / gb) % g : ((i - nc - 1) / gb) % g;
+            loc[i] = (int)rows[own[i]].size();
             rows[own[i]].push_back(i);
         }
-        soff.assign(g, std::vector<int64_t>(nc + 1, 0));
-        stot.assign(g, 0);
+        roff.assign(g, {});
+        elems.assign(g, 0);
+        const int64_t DB2 = (int64_t)DB * DB;
         for (int q = 0; q < g; q++) {
             int64_t o = 0;
-            for (int b = 0; b < nc; b++) {
-                soff[q][b] = o;
-                o += cnt(q, b);
+            for (int i : rows[q]) {
+                roff[q].push_back(o);
+                o += (int64_t)ncols(i) * DB2;
             }
-            soff[q][nc] = o;
-            stot[q] = o;
+            elems[q] = o;
         }
-        roff.assign(g, std::vector<std::vector<int64_t>>(nc, std::vector<int64_t>(g, -1)));
-        rtot.assign(g, 0);
-        for (int r = 0; r < g; r++) {
-            int64_t o = 0;
-            for (int b = 0; b < nc; b++)
-                for (int q = 0; q < g; q++) {
-                    if (q == r) continue;
-                    roff[r][b][q] = o;
-                    o += cnt(q, b);
-                }
-            rtot[r] = o;
-        }
+    }
+};
+
+// mailbox byte layout (identical on every rank): see PtDist / DSArgs
+struct MailboxLayout {
+    int64_t o_linv = 0, o_win = 0, o_z = 0, o_alpha = 0, o_zf = 0, o_part = 0, o_flags = 0, o_sflags = 0, bytes = 0;
+    void init(int g, int nc, int nr, int ww, int m, size_t s, bool window) {
+        const int64_t DB2 = (int64_t)DB * DB, np = (int64_t)nc * DB;
+        int64_t o = 0;
+        o_linv = o;
+        o = align256(o + (int64_t)nc * DB2 * (int64_t)s);
+        o_win = o;
+        o = align256(o + (window ? (int64_t)ww * nr * DB2 * (int64_t)s : 0));
+        o_z = o;
+        o = align256(o + (int64_t)nc * DB2 * (int64_t)s);
+        o_alpha = o;
+        o = align256(o + np * m * (int64_t)s);
+        o_zf = o;
+        o = align256(o + np * m * (int64_t)s);
+        o_part = o;
+        o = align256(o + (int64_t)g * nc * DB * m * (int64_t)s);
+        o_flags = o;
+        o = align256(o + 4 * (dist_f_rel(nr, nc) + (int64_t)g * nc));
+        o_sflags = o;
+        o = align256(o + 4 * ((int64_t)(2 + g) * nc));
+        bytes = o;
     }
 };
 
@@ -175,21 +221,20 @@ struct DistLayout {
 template <typename T>
 struct DistRank {
     int r = 0;
-    hipStream_t s = nullptr;  // compute stream
-    bool own_stream = false;
-    DMem A, Linv, send, recv, ctr, info, flag, pd, loc, tptr, sptr, drecv, tiles, tld, red, alpha, tab, list, trace;
-    HMem hdiag, hslot, dbg;
-    std::vector<int4> hlist;
-    int64_t ld = 0;
+    hipStream_t s = nullptr;
+    DMem store, mbox, ctr, info, flag, red, sctl, part;
+    DMem t_loc, t_roff, t_own, t_tptr, t_cons, t_need, t_mb, t_orows, t_lastof, t_ctab, pd, list;
+    std::vector<uint64_t> mb;          // every rank's mailbox as mapped here
+    std::vector<uint64_t> st;          // every rank's storage as mapped here
+    std::vector<void*> opened;         // IPC mappings to close
+    std::vector<int> orows;            // own matrix row blocks
     int ntasks = 0;
-    hipEvent_t done = nullptr;
-    hipEvent_t t0 = nullptr, t1 = nullptr, t2 = nullptr;  // launch start / end, back-solve end
+    hipEvent_t t0 = nullptr, t1 = nullptr;
     ~DistRank() {
-        if (done) (void)hipEventDestroy(done);
+        for (void* p : opened) (void)hipIpcCloseMemHandle(p);
         if (t0) (void)hipEventDestroy(t0);
         if (t1) (void)hipEventDestroy(t1);
-        if (t2) (void)hipEventDestroy(t2);
-        if (own_stream && s) (void)hipStreamDestroy(s);
+        if (s) (void)hipStreamDestroy(s);
     }
 };
 
@@ -199,684 +244,675 @@ struct DistEngineBase {
 
 template <typename T>
 struct DistEngine : DistEngineBase {
-    int g = 1;
+    int g = 1, device = 0, P = 0, gb = 1, ww = 2, W = 1;
     bool virt = false;
-    int device = 0;
-    std::vector<std::unique_ptr<DistRank<T>>> ranks;  // virtual: all g; RCCL: this rank only
-    ncclComm_t commB = nullptr, commP = nullptr;       // RCCL: broadcast / panel communicators
-    bool own_commP = false;
-    hipStream_t sB = nullptr, sP = nullptr;            // transport streams
+    HostColl* hc = nullptr;
     DistLayout L;
+    MailboxLayout MB;
+    DistSched S;
     int64_t key_n = -1;
     int key_m = -1;
-    bool key_fused = false;
-    int P = 0;
-    double est_us = 0;
-    std::vector<std::vector<int4>> lists;
-    ~DistEngine() override {
+    bool key_fused = false, key_inv = false;
+    int64_t n = 0, np = 0;
+    int m = 0;
+    unsigned ep = 0, sep = 0;  // epochs of the fits and of the solves (flag values)
+    std::vector<std::unique_ptr<DistRank<T>>> ranks;  // virtual: all g; otherwise this process's rank
+    ~DistEngine() override { teardown(); }
+    void teardown() {
+        if (!virt && hc && !ranks.empty()) {  // every rank unmaps before any rank frees
+            for (auto& R : ranks) {
+                for (void* p : R->opened) (void)hipIpcCloseMemHandle(p);
+                R->opened.clear();
+            }
+            try {
+                int x = 0;
+                std::vector<int> all(g);
+                hc->allgather(&x, sizeof(int), all.data());
+            } catch (...) {
+            }
+        }
         ranks.clear();
-        if (sB) (void)hipStreamDestroy(sB);
-        if (sP) (void)hipStreamDestroy(sP);
-        if (own_commP && commP) (void)ncclCommDestroy(commP);
     }
 };
 
 // ---------------------------------------------------------------------------------------
-// small kernels
+// small kernels: counters, packed-storage initialisation, the factor gather
 // ---------------------------------------------------------------------------------------
 namespace {
 
-template <typename T>
-__global__ void diag_fix_local_kernel(T* __restrict__ A, int64_t ld, int64_t row0, int64_t c0, int64_t n, T s2) {
-    const int t = threadIdx.x;
-    if (t >= DB) return;
-    const int64_t gi = c0 + t;
-    T* p = A + row0 + t + gi * ld;
-    *p = (gi < n) ? *p + s2 : T(1);
+// ver = -1 for the BUILD tiles (matrix rows, j <= i); identity row E_a: lcnt = a, ver[.] = a
+__global__ void dist_init_counters(int* __restrict__ lcnt, int* __restrict__ ver, int nc, int nr, int nci, int build) {
+    const int i = blockIdx.x;
+    if (i >= nr) return;
+    const int a = i > nc ? i - nc - 1 : 0;
+    if (threadIdx.x == 0 && i > nc) lcnt[i] = a;
+    for (int c = threadIdx.x; c < nci; c += blockDim.x) {
+        int v = 0;
+        if (i > nc) v = a;
+        else if (build && i < nc && c <= i) v = -1;
+        ver[(int64_t)i * nci + c] = v;
+    }
 }
 
-// out[0] = sum of 2 log L_ii over this rank's diagonal blocks (global index < n),
-// out[1] = sum of z^2 over the label tiles (from the tile table, every rank has them all)
+// identity row block E_a (packed: columns a..nc-1, then the C tiles): the first tile the
+// identity, everything else 0
 template <typename T>
-__global__ __launch_bounds__(256) void dist_reduce_kernel(const T* __restrict__ A, int64_t ld, const int* __restrict__ loc,
-                                                          int g, int r, int nc, int64_t n, int m,
-                                                          const uint64_t* __restrict__ tiles,
-                                                          const int64_t* __restrict__ tld, double* __restrict__ out) {
-    __shared__ double s0[256], s1[256];
+__global__ void dist_init_identity(T* __restrict__ rowbase, int ntile) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t tot = (int64_t)ntile * DB * DB;
+    if (e >= tot) return;
+    const int64_t r = e % DB, c = (e / DB) % DB, tile = e / ((int64_t)DB * DB);
+    rowbase[e] = (tile == 0 && r == c) ? T(1) : T(0);
+}
+
+// the direct build's diagonal tile: + sigma^2 inside the matrix, identity in the padding
+template <typename T>
+__global__ void dist_diag_fix(T* __restrict__ tile, int64_t r0, int64_t n, T s2) {
     const int t = threadIdx.x;
-    double a = 0, b = 0;
-    for (int k = 0; k < nc; k++) {  // this rank's diagonal blocks
-        if (loc[k] < 0) continue;
-        const int64_t gi = (int64_t)k * DB + (t & (DB - 1));
-        if (t < DB && gi < n) a += 2.0 * log((double)A[(int64_t)loc[k] * DB + t + gi * ld]);
-    }
-    const int64_t lz = tld[nc];
-    for (int k = 0; k < nc; k++) {
-        const T* z = reinterpret_cast<const T*>(tiles[(int64_t)nc * nc + k]);
-        for (int e = t; e < m * DB; e += 256) {
-            const int rr = e % m, c = e / m;
-            if ((int64_t)k * DB + c < n) {
-                const double v = (double)z[rr + (int64_t)c * lz];
-                b += v * v;
-            }
-        }
-    }
-    s0[t] = a;
-    s1[t] = b;
-    __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-        if (t < o) {
-            s0[t] += s0[t + o];
-            s1[t] += s1[t + o];
-        }
-        __syncthreads();
-    }
-    if (t == 0) {
-        out[0] = s0[0];
-        out[1] = s1[0];
+    if (t >= DB) return;
+    T* p = tile + t + (int64_t)t * DB;
+    *p = (r0 + t < n) ? *p + s2 : T(1);
+}
+
+// dense gather: tile (i, j), i > j, of the factor from its rank's storage (src table) into A
+template <typename T>
+__global__ __launch_bounds__(256) void dist_gather_kernel(const uint64_t* __restrict__ src, int nc, T* __restrict__ A,
+                                                          int64_t ld) {
+    const int i = blockIdx.x, j = blockIdx.y;
+    if (j >= i) return;
+    const T* s = reinterpret_cast<const T*>(src[(int64_t)i * nc + j]);
+    T* d = A + (int64_t)i * DB + (int64_t)j * DB * ld;
+    for (int e = threadIdx.x; e < DB * DB; e += 256) {
+        const int r = e & (DB - 1), c = e >> 7;
+        d[r + (int64_t)c * ld] = s[e];
     }
 }
 
 }  // namespace
 
 // ---------------------------------------------------------------------------------------
-// engine setup (per shape): layout, buffers, tables, schedule
+// engine setup (per shape): layout, schedule, buffers, mailbox mappings, tables
 // ---------------------------------------------------------------------------------------
 template <typename T>
-static void setup(DistEngine<T>& E, const DistContext& C, int64_t n, int m, bool fused) {
-    const int64_t np = (n + DB - 1) / DB * DB;
-    const int nc = (int)(np / DB), nr = nc + 1;  // + the label row block
-    if (E.key_n == n && E.key_m == m && E.key_fused == fused && !E.ranks.empty()) return;
+static void setup(DistEngine<T>& E, const DistContext& C, int64_t n, int m, bool fused, bool inv) {
+    if (E.key_n == n && E.key_m == m && E.key_fused == fused && E.key_inv == inv && !E.ranks.empty()) return;
     GPRX_REQUIRE(m <= GT, GPRX_ERR_DIM, "distributed fit: at most 128 label columns");
+    GPRX_REQUIRE(C.world >= 1 && C.world <= 32, GPRX_ERR_ARG, "distributed fit: 1..32 ranks");
+    E.teardown();
+    const int64_t np = (n + DB - 1) / DB * DB;
+    const int nc = (int)(np / DB);
     E.g = C.world;
     E.virt = C.virt;
     E.device = C.device;
-    // CU partition.  The transport kernels (RCCL, copies) and every (virtual) rank's
-    // persistent launch run on streams whose CU masks are disjoint: a persistent launch can
-    // never starve the transport of CUs, nor one virtual rank another.  Without the masks
-    // the transport stalled behind the persistent launches (measured: 2 x 124 workgroups,
-    // the copies waited until the launches timed out).  Mask bit b selects logical CU b / X
-    // of XCC b % X (tools/cu_mask_probe.hip, gfx950; an XCC without a bit is unrestricted,
-    // so every mask covers every XCC): a CU "slot" is one CU on each XCC.
+    E.hc = C.hc;
+    E.n = n;
+    E.np = np;
+    E.m = m;
+    // CU partition.  A real rank has its GPU to itself (one workgroup per CU: nothing else runs
+    // during the fit, the exchange is the kernel's own stores).  Virtual ranks, and processes
+    // sharing one GPU (tests), each take a disjoint slice: every rank's persistent launch must be
+    // resident for the others to progress.  Mask bit b selects logical CU b / X of XCC b % X
+    // (tools/cu_mask_probe.hip, gfx950), so a slice is a range of "slots" of one CU per XCC.
     int ncu = 0, nxcc = 1;
     GPRX_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, C.device));
     if (hipDeviceGetAttribute(&nxcc, hipDeviceAttributeNumberOfXccs, C.device) != hipSuccess || nxcc < 1) nxcc = 1;
     const int cu_xcc = std::max(1, ncu / nxcc);
-    // transport slots: one CU per XCC for the virtual ranks' copies; two for RCCL, whose
-    // kernels run one workgroup per channel
-    int reserve = E.virt ? 1 : 2;
-    if (const char* e = std::getenv("GPRX_DIST_RESERVE_CU")) reserve = std::max(1, std::atoi(e));
-    const int nloc_ranks = E.virt ? E.g : 1;
-    GPRX_REQUIRE(cu_xcc - reserve >= nloc_ranks, GPRX_ERR_ARG, "distributed fit: too many virtual ranks for the CUs");
-    const int per = (cu_xcc - reserve) / nloc_ranks;  // compute slots per rank
-    E.P = nxcc * per;  // one workgroup per CU (LDS)
+    const int nlocal = E.virt ? E.g : 1;
+    const int shares = E.virt ? E.g : std::max(1, C.cu_slots);
+    GPRX_REQUIRE(cu_xcc >= shares, GPRX_ERR_ARG, "distributed fit: too many ranks sharing the GPU's CUs");
+    const int per = cu_xcc / shares;
+    E.P = nxcc * per;
     if (const char* e = std::getenv("GPRX_DIST_P")) E.P = std::max(1, std::atoi(e));
     auto masked_stream = [&](int slot0, int nslot) {
+        hipStream_t st = nullptr;
+        if (shares == 1) {
+            GPRX_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+            return st;
+        }
         std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
         for (int c = slot0; c < slot0 + nslot; c++)
             for (int x = 0; x < nxcc; x++) {
                 const int b = c * nxcc + x;
                 if (b < ncu) mask[b / 32] |= 1u << (b % 32);
             }
-        hipStream_t st = nullptr;
         GPRX_HIP(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()));
         return st;
     };
-    // row-block grouping: the simulated makespan picks gb (GPRX_DIST_GROUP forces it)
-    int gb = 1;
-    if (const char* e = std::getenv("GPRX_DIST_GROUP")) {
-        gb = std::max(1, std::atoi(e));
-        E.lists = potrf_dist_schedule(nc, nr, E.P, E.g, gb, fused, &E.est_us);
+    // row-block grouping and window: the simulated makespan picks them (GPRX_DIST_GROUP /
+    // GPRX_DIST_WINDOW force them).  Every rank runs the same deterministic simulation.
+    int gb = 1, ww = std::min(32, nc);
+    double best = 0;
+    auto sim = [&](int gbc, int wwc) { return potrf_dist_schedule(nc, E.g, gbc, wwc, E.P, fused, inv); };
+    const char* eg = std::getenv("GPRX_DIST_GROUP");
+    const char* ew = std::getenv("GPRX_DIST_WINDOW");
+    if (ew) ww = std::max(2, std::min(nc, std::atoi(ew)));
+    if (E.g == 1) ww = std::max(2, nc);  // nothing goes through a window: chunks as on one GPU
+    if (eg) {
+        gb = std::max(1, std::atoi(eg));
+        E.S = sim(gb, ww);
     } else {
-        E.lists = potrf_dist_schedule(nc, nr, E.P, E.g, 1, fused, &E.est_us);
+        E.S = sim(1, ww);
+        best = E.S.est_us;
         for (int cand = 2; E.g > 1 && cand <= 8 && nc >= 2 * cand * E.g; cand *= 2) {
-            double est = 0;
-            auto l = potrf_dist_schedule(nc, nr, E.P, E.g, cand, fused, &est);
-            if (est < E.est_us) {
-                E.est_us = est;
-                E.lists = std::move(l);
+            DistSched c = sim(cand, ww);
+            if (c.est_us < best) {
+                best = c.est_us;
+                E.S = std::move(c);
                 gb = cand;
             }
         }
     }
-    E.L.init(E.g, gb, nc, nr);
-    if (!E.sB) {
-        E.sB = masked_stream(0, reserve);
-        E.sP = masked_stream(0, reserve);
+    if (!ew && E.g > 1) {  // the smallest window within 2% of the best simulated makespan
+        std::vector<std::pair<int, DistSched>> cands;
+        for (int w : {8, 16, 64})
+            if (w < nc && w != ww) cands.push_back({w, sim(gb, w)});
+        double bw = E.S.est_us;
+        for (auto& c : cands) bw = std::min(bw, c.second.est_us);
+        int pick = ww;
+        double pe = E.S.est_us;
+        for (auto& c : cands)
+            if (c.first < pick && c.second.est_us <= 1.02 * bw) {
+                pick = c.first;
+                pe = c.second.est_us;
+            }
+        if (E.S.est_us > 1.02 * bw && pick == ww)  // a wider window is clearly faster
+            for (auto& c : cands)
+                if (c.second.est_us <= 1.02 * bw && (pick == ww || c.first < pick)) {
+                    pick = c.first;
+                    pe = c.second.est_us;
+                }
+        if (pick != ww)
+            for (auto& c : cands)
+                if (c.first == pick) {
+                    E.S = std::move(c.second);
+                    ww = pick;
+                    break;
+                }
+        (void)pe;
     }
-    if (!E.virt && !E.commP) {
-        E.commB = C.comm;
-        if (E.g > 1) {  // a second communicator: the two transport streams progress independently
-            rccl_ok(ncclCommSplit(C.comm, 0, C.rank, &E.commP, nullptr), "ncclCommSplit");
-            E.own_commP = true;
-        } else {
-            E.commP = C.comm;
-        }
-    }
-    E.ranks.clear();
-    const int nranks = E.virt ? E.g : 1;
+    E.gb = gb;
+    E.ww = ww;
+    E.W = E.S.W;
+    E.L.init(E.g, gb, nc, inv);
+    const int nr = E.L.nr, nci = E.L.nci;
+    E.MB.init(E.g, nc, nr, ww, m, sizeof(T), E.g > 1);
     const int64_t DB2 = (int64_t)DB * DB;
-    for (int v = 0; v < nranks; v++) {
+    // ---- per local rank: buffers -------------------------------------------------------------
+    for (int v = 0; v < nlocal; v++) {
         auto R = std::make_unique<DistRank<T>>();
         R->r = E.virt ? v : C.rank;
         const int r = R->r;
-        R->s = masked_stream(reserve + v * per, per);  // this rank's CUs
-        R->own_stream = true;
-        GPRX_HIP(hipEventCreateWithFlags(&R->done, hipEventDisableTiming));
+        const int slot = E.virt ? v : (shares > 1 ? C.cu_slot : 0);
+        R->s = masked_stream(slot * per, per);
         GPRX_HIP(hipEventCreate(&R->t0));
         GPRX_HIP(hipEventCreate(&R->t1));
-        GPRX_HIP(hipEventCreate(&R->t2));
-        const int nl = E.L.nloc(r);
-        R->ld = (int64_t)nl * DB;
-        R->A.ensure(sizeof(T) * R->ld * np);
-        R->Linv.ensure(sizeof(T) * nc * DB2, hipDeviceMallocFinegrained);
-        R->send.ensure(sizeof(T) * std::max<int64_t>(1, E.L.stot[r]) * DB2);
-        R->recv.ensure(sizeof(T) * std::max<int64_t>(1, E.L.rtot[r]) * DB2, hipDeviceMallocFinegrained);
-        R->ctr.ensure(sizeof(int) * ((size_t)C_NCTL_DIST + nr + (size_t)nr * nc));
-        R->info.ensure(sizeof(int));
-        R->flag.ensure(sizeof(int));
-        R->drecv.ensure(2 * sizeof(unsigned), hipDeviceMallocUncached);
-        R->red.ensure(2 * sizeof(double));
-        R->alpha.ensure(sizeof(T) * np * m);
-        R->hdiag.ensure(sizeof(unsigned) * nc);
-        R->hslot.ensure(sizeof(unsigned) * (size_t)nr * nc);
-        // tables
-        std::vector<int> loc(nr);
-        std::vector<uint64_t> tptr((size_t)nr * nc, 0), sptr((size_t)nr * nc, 0), tiles((size_t)nr * nc, 0);
-        std::vector<int64_t> tld(nr);
-        T* Ab = R->A.template as<T>();
-        for (int i = 0; i < nr; i++) {
-            const int q = E.L.owner(i);
-            loc[i] = (q == r) ? E.L.loc(i) : -1;
-            tld[i] = (q == r) ? R->ld : (int64_t)DB;
-            for (int b = 0; b < std::min(i, nc); b++) {
-                if (q == r) {
-                    sptr[(size_t)i * nc + b] =
-                        (uint64_t)(R->send.template as<T>() + (E.L.soff[r][b] + E.L.pos(r, i, b)) * DB2);
-                    tiles[(size_t)i * nc + b] = (uint64_t)(Ab + (int64_t)loc[i] * DB + (int64_t)b * DB * R->ld);
-                } else {
-                    const uint64_t p = (uint64_t)(R->recv.template as<T>() + (E.L.roff[r][b][q] + E.L.pos(q, i, b)) * DB2);
-                    tptr[(size_t)i * nc + b] = p;
-                    tiles[(size_t)i * nc + b] = p;
+        R->store.alloc(sizeof(T) * (size_t)E.L.elems[r], false);
+        R->mbox.alloc((size_t)E.MB.bytes, true);
+        GPRX_HIP(hipMemset(R->mbox.p, 0, E.MB.bytes));  // flags 0: below every epoch
+        R->ctr.alloc(sizeof(int) * ((size_t)C_NCTL_DIST + nr + (size_t)nr * nci + nc), false);
+        R->info.alloc(sizeof(int), false);
+        R->flag.alloc(sizeof(int), false);
+        R->red.alloc(sizeof(double) * 4 + sizeof(TileBuild<T>) + 64, false);
+        R->sctl.alloc(sizeof(int) * 8, false);
+        R->part.alloc(sizeof(double) * MAX_LEAF * 3 * (size_t)nc * (nc + 1) / 2 + 64, false);
+        E.ranks.push_back(std::move(R));
+    }
+    // ---- every rank's mailbox and storage as mapped in this process ------------------------------
+    for (auto& R : E.ranks) {
+        R->mb.assign(E.g, 0);
+        R->st.assign(E.g, 0);
+    }
+    if (E.virt) {
+        for (auto& R : E.ranks)
+            for (auto& Q : E.ranks) {
+                R->mb[Q->r] = (uint64_t)Q->mbox.p;
+                R->st[Q->r] = (uint64_t)Q->store.p;
+            }
+    } else {
+        DistRank<T>& R = *E.ranks[0];
+        R.mb[R.r] = (uint64_t)R.mbox.p;
+        R.st[R.r] = (uint64_t)R.store.p;
+        if (E.g > 1) {
+            GPRX_REQUIRE(E.hc, GPRX_ERR_STATE, "distributed fit: no host collective");
+            hipIpcMemHandle_t mine[2];
+            GPRX_HIP(hipIpcGetMemHandle(&mine[0], R.mbox.p));
+            GPRX_HIP(hipIpcGetMemHandle(&mine[1], R.store.p));
+            std::vector<hipIpcMemHandle_t> all(2 * (size_t)E.g);
+            E.hc->allgather(mine, sizeof(mine), all.data());
+            for (int q = 0; q < E.g; q++) {
+                if (q == R.r) continue;
+                for (int h = 0; h < 2; h++) {
+                    void* p = nullptr;
+                    GPRX_HIP(hipIpcOpenMemHandle(&p, all[2 * (size_t)q + h], hipIpcMemLazyEnablePeerAccess));
+                    R.opened.push_back(p);
+                    (h == 0 ? R.mb : R.st)[q] = (uint64_t)p;
                 }
             }
         }
-        R->loc.ensure(sizeof(int) * nr);
-        R->tptr.ensure(sizeof(uint64_t) * tptr.size());
-        R->sptr.ensure(sizeof(uint64_t) * sptr.size());
-        R->tiles.ensure(sizeof(uint64_t) * tiles.size());
-        R->tld.ensure(sizeof(int64_t) * nr);
-        GPRX_HIP(hipMemcpy(R->loc.p, loc.data(), sizeof(int) * nr, hipMemcpyHostToDevice));
-        GPRX_HIP(hipMemcpy(R->tptr.p, tptr.data(), sizeof(uint64_t) * tptr.size(), hipMemcpyHostToDevice));
-        GPRX_HIP(hipMemcpy(R->sptr.p, sptr.data(), sizeof(uint64_t) * sptr.size(), hipMemcpyHostToDevice));
-        GPRX_HIP(hipMemcpy(R->tiles.p, tiles.data(), sizeof(uint64_t) * tiles.size(), hipMemcpyHostToDevice));
-        GPRX_HIP(hipMemcpy(R->tld.p, tld.data(), sizeof(int64_t) * nr, hipMemcpyHostToDevice));
-        PtDist<T> pd;
-        pd.g = E.g;
-        pd.r = r;
-        pd.loc = R->loc.template as<int>();
-        pd.tptr = reinterpret_cast<const T* const*>(R->tptr.p);
-        pd.sptr = reinterpret_cast<T* const*>(R->sptr.p);
-        unsigned *hd = nullptr, *hs = nullptr;
-        GPRX_HIP(hipHostGetDevicePointer((void**)&hd, R->hdiag.p, 0));
-        GPRX_HIP(hipHostGetDevicePointer((void**)&hs, R->hslot.p, 0));
-        pd.hdiag = hd;
-        pd.hslot = hs;
-        pd.drecv = R->drecv.template as<unsigned>();
-        pd.precv = R->drecv.template as<unsigned>() + 1;
-        R->pd.ensure(sizeof(PtDist<T>));
-        GPRX_HIP(hipMemcpy(R->pd.p, &pd, sizeof(pd), hipMemcpyHostToDevice));
-        const std::vector<int4>& lst = E.lists[r];
-        R->hlist = lst;
-        R->ntasks = (int)lst.size();
-        R->list.ensure(sizeof(int4) * std::max<size_t>(1, lst.size()));
-        if (!lst.empty()) GPRX_HIP(hipMemcpy(R->list.p, lst.data(), sizeof(int4) * lst.size(), hipMemcpyHostToDevice));
-        E.ranks.push_back(std::move(R));
+    }
+    // ---- tables -------------------------------------------------------------------------------
+    std::vector<int> lastof(E.g, -1);
+    for (int q = 0; q < E.g; q++)
+        for (int i : E.L.rows[q])
+            if (i < nc) lastof[q] = std::max(lastof[q], i);
+    for (auto& Rp : E.ranks) {
+        DistRank<T>& R = *Rp;
+        const int r = R.r;
+        std::vector<int> loc(nr, -1);
+        for (int i = 0; i < nr; i++)
+            if (E.L.own[i] == r) loc[i] = E.L.loc[i];
+        std::vector<uint64_t> tptr((size_t)nr * nc, 0);
+        if (E.g > 1)
+            for (int j = 0; j < nr; j++)
+                for (int b = 0; b < nc; b++)
+                    tptr[(size_t)j * nc + b] =
+                        R.mb[r] + (uint64_t)(E.MB.o_win + ((int64_t)(b % ww) * nr + j) * DB2 * (int64_t)sizeof(T));
+        R.orows.clear();
+        for (int i : E.L.rows[r])
+            if (i < nc) R.orows.push_back(i);
+        upload_vec(R.t_loc, loc);
+        upload_vec(R.t_roff, E.L.roff[r]);
+        upload_vec(R.t_own, E.L.own);
+        upload_vec(R.t_tptr, tptr);
+        upload_vec(R.t_cons, E.S.cons);
+        upload_vec(R.t_need, E.S.need);
+        upload_vec(R.t_mb, R.mb);
+        upload_vec(R.t_orows, R.orows);
+        upload_vec(R.t_lastof, lastof);
+        R.pd.alloc(sizeof(PtDist<T>), false);
+        const std::vector<int4>& lst = E.S.lists[r];
+        R.ntasks = (int)lst.size();
+        upload_vec(R.list, lst);
+        if (inv) {  // C tile (ti, tj) of this rank's identity rows, for the gradient pass
+            std::vector<uint64_t> ctab((size_t)nc * nc, 0);
+            for (int a = 0; a < nc; a++) {
+                const int i = nc + 1 + a;
+                if (E.L.own[i] != r) continue;
+                for (int c = 0; c <= a; c++)
+                    ctab[(size_t)a * nc + c] = (uint64_t)(R.store.template as<T>() + E.L.roff[r][E.L.loc[i]] +
+                                                          (int64_t)(nc - a + c) * DB2);
+            }
+            upload_vec(R.t_ctab, ctab);
+        }
     }
     E.key_n = n;
     E.key_m = m;
     E.key_fused = fused;
-}
-
-// ---------------------------------------------------------------------------------------
-// transport steps
-// ---------------------------------------------------------------------------------------
-template <typename T>
-static void issue_bcast(DistEngine<T>& E, int k) {
-    const int64_t DB2 = (int64_t)DB * DB;
-    const int root = E.L.owner(k);
-    if (E.virt) {
-        const DistRank<T>& Rt = *E.ranks[root];
-        for (auto& R : E.ranks)
-            if (R->r != root)
-                GPRX_HIP(hipMemcpyAsync(R->Linv.template as<T>() + k * DB2, Rt.Linv.template as<T>() + k * DB2,
-                                        sizeof(T) * DB2, hipMemcpyDeviceToDevice, E.sB));
-        for (auto& R : E.ranks) GPRX_HIP(hipStreamWriteValue32(E.sB, R->drecv.p, (uint32_t)(k + 1), 0));
-    } else {
-        DistRank<T>& R = *E.ranks[0];
-        T* p = R.Linv.template as<T>() + k * DB2;
-        if (E.g > 1) rccl_ok(ncclBroadcast(p, p, (size_t)DB2, nccl_t<T>(), root, E.commB, E.sB), "ncclBroadcast");
-        GPRX_HIP(hipStreamWriteValue32(E.sB, R.drecv.p, (uint32_t)(k + 1), 0));
-    }
+    E.key_inv = inv;
 }
 
 template <typename T>
-static void issue_panel(DistEngine<T>& E, int b) {
-    const int64_t DB2 = (int64_t)DB * DB;
-    if (E.virt) {
-        for (auto& R : E.ranks)
-            for (auto& Q : E.ranks) {
-                if (Q->r == R->r) continue;
-                const int64_t c = E.L.cnt(Q->r, b);
-                if (c == 0) continue;
-                GPRX_HIP(hipMemcpyAsync(R->recv.template as<T>() + E.L.roff[R->r][b][Q->r] * DB2,
-                                        Q->send.template as<T>() + E.L.soff[Q->r][b] * DB2, sizeof(T) * c * DB2,
-                                        hipMemcpyDeviceToDevice, E.sP));
-            }
-        for (auto& R : E.ranks)
-            GPRX_HIP(hipStreamWriteValue32(E.sP, R->drecv.template as<unsigned>() + 1, (uint32_t)(b + 1), 0));
-    } else {
-        DistRank<T>& R = *E.ranks[0];
-        const int r = R.r;
-        if (E.g > 1) {
-            rccl_ok(ncclGroupStart(), "ncclGroupStart");
-            const int64_t cs = E.L.cnt(r, b);
-            for (int q = 0; q < E.g; q++) {
-                if (q == r) continue;
-                if (cs > 0)
-                    rccl_ok(ncclSend(R.send.template as<T>() + E.L.soff[r][b] * DB2, (size_t)(cs * DB2), nccl_t<T>(), q,
-                                     E.commP, E.sP),
-                            "ncclSend");
-                const int64_t cq = E.L.cnt(q, b);
-                if (cq > 0)
-                    rccl_ok(ncclRecv(R.recv.template as<T>() + E.L.roff[r][b][q] * DB2, (size_t)(cq * DB2), nccl_t<T>(),
-                                     q, E.commP, E.sP),
-                            "ncclRecv");
-            }
-            rccl_ok(ncclGroupEnd(), "ncclGroupEnd");
-        }
-        GPRX_HIP(hipStreamWriteValue32(E.sP, R.drecv.template as<unsigned>() + 1, (uint32_t)(b + 1), 0));
-    }
-}
-
-// this host's ranks have every tile of panel b in its send slot
-template <typename T>
-static bool panel_ready(const DistEngine<T>& E, int b) {
-    for (auto& R : E.ranks) {
-        const unsigned* hs = R->hslot.u();
-        const std::vector<int>& rw = E.L.rows[R->r];
-        for (int x = E.L.firstpos(R->r, b); x < (int)rw.size(); x++)
-            if (__atomic_load_n(hs + (size_t)rw[x] * E.L.nc + b, __ATOMIC_ACQUIRE) == 0) return false;
-    }
-    return true;
+static PtDist<T> make_ptdist(const DistEngine<T>& E, const DistRank<T>& R) {
+    PtDist<T> pd;
+    std::memset(&pd, 0, sizeof(pd));
+    pd.g = E.g;
+    pd.r = R.r;
+    pd.nc = E.L.nc;
+    pd.nr = E.L.nr;
+    pd.ww = E.ww;
+    pd.nci = E.L.nci;
+    pd.ep = E.ep;
+    pd.loc = R.t_loc.template as<int>();
+    pd.roff = R.t_roff.template as<int64_t>();
+    pd.own = R.t_own.template as<int>();
+    pd.tptr = R.t_tptr.template as<uint64_t>();
+    pd.cons = R.t_cons.template as<unsigned char>();
+    pd.need = R.t_need.template as<int>();
+    pd.ucnt = R.ctr.template as<int>() + C_NCTL_DIST + E.L.nr + (size_t)E.L.nr * E.L.nci;
+    pd.mb = R.t_mb.template as<uint64_t>();
+    pd.o_linv = E.MB.o_linv;
+    pd.o_win = E.MB.o_win;
+    pd.o_z = E.MB.o_z;
+    pd.o_flags = E.MB.o_flags;
+    return pd;
 }
 
 template <typename T>
-static bool bcast_ready(const DistEngine<T>& E, int k) {
-    const int root = E.L.owner(k);
-    for (auto& R : E.ranks)
-        if (R->r == root) return __atomic_load_n(R->hdiag.u() + k, __ATOMIC_ACQUIRE) != 0;
-    return true;  // another process's rank: RCCL waits for it on the device
+static DSArgs<T> make_dsargs(const DistEngine<T>& E, const DistRank<T>& R) {
+    DSArgs<T> a;
+    std::memset(&a, 0, sizeof(a));
+    a.g = E.g;
+    a.r = R.r;
+    a.nc = E.L.nc;
+    a.m = E.m;
+    a.own = R.t_own.template as<int>();
+    a.loc = R.t_loc.template as<int>();
+    a.roff = R.t_roff.template as<int64_t>();
+    a.store = R.store.template as<T>();
+    a.orows = R.t_orows.template as<int>();
+    a.nown = (int)R.orows.size();
+    a.last_of = R.t_lastof.template as<int>();
+    a.last_own = R.orows.empty() ? -1 : R.orows.back();
+    a.Linv = reinterpret_cast<const T*>(R.mbox.template as<char>() + E.MB.o_linv);
+    a.mb = R.t_mb.template as<uint64_t>();
+    a.o_ztile = E.MB.o_z;
+    a.o_alpha = E.MB.o_alpha;
+    a.o_zf = E.MB.o_zf;
+    a.o_part = E.MB.o_part;
+    a.o_fflags = E.MB.o_flags;
+    a.o_sflags = E.MB.o_sflags;
+    a.fit_ep = E.ep;
+    a.sep = E.sep;
+    a.ctl = R.sctl.template as<int>();
+    a.info = R.info.template as<int>();
+    a.tlimit = (long long)(1e8 * 4.0);
+    return a;
 }
 
 // ---------------------------------------------------------------------------------------
 // the fit
 // ---------------------------------------------------------------------------------------
 template <typename T>
-void dist_fit(DistEngineBase*& eng, const DistContext& C, const DistFitIn<T>& in, DistFitOut& out, T* alpha_dev,
-              Exec& ex) {
+void dist_fit(DistEngineBase*& eng, const DistContext& C, const DistFitIn<T>& in, DistFitOut& out, T* alpha_dev) {
     if (!eng) eng = new DistEngine<T>();
-    DistEngine<T>& E = *static_cast<DistEngine<T>*>(eng);
+    DistEngine<T>* Ep = dynamic_cast<DistEngine<T>*>(eng);
+    if (!Ep) {  // the model changed scalar type
+        delete eng;
+        eng = Ep = new DistEngine<T>();
+    }
+    DistEngine<T>& E = *Ep;
     const bool fused = in.tb.mode != 0;
-    setup<T>(E, C, in.n, in.m, fused);
-    const int nc = E.L.nc, nr = E.L.nr;
-    const int64_t np = (int64_t)nc * DB, n = in.n;
+    setup<T>(E, C, in.n, in.m, fused, in.inv);
+    const int nc = E.L.nc, nr = E.L.nr, nci = E.L.nci;
+    const int64_t np = E.np, n = in.n;
     const int64_t DB2 = (int64_t)DB * DB;
-    DistRank<T>& R0 = *E.ranks[0];
-    // ---- per rank: reset, build; then the launches -------------------------------------------
+    E.ep++;
+    // ---- per rank: counters, storage, then the launches ------------------------------------------
     std::vector<DistLaunch<T>> launches(E.ranks.size());
-    for (auto& Rp : E.ranks) {
-        DistRank<T>& R = *Rp;
+    for (size_t v = 0; v < E.ranks.size(); v++) {
+        DistRank<T>& R = *E.ranks[v];
         const int r = R.r;
         hipStream_t s = R.s;
-        std::memset(R.hdiag.p, 0, R.hdiag.bytes);
-        std::memset(R.hslot.p, 0, R.hslot.bytes);
-        const size_t nctr = (size_t)C_NCTL_DIST + nr + (size_t)nr * nc;
+        const size_t nctr = (size_t)C_NCTL_DIST + nr + (size_t)nr * nci + nc;
         GPRX_HIP(hipMemsetAsync(R.ctr.p, 0, sizeof(int) * nctr, s));
-        GPRX_HIP(hipMemsetAsync(R.drecv.p, 0, 2 * sizeof(unsigned), s));
+        int* lcnt = R.ctr.template as<int>() + C_NCTL_DIST;
+        hipLaunchKernelGGL(dist_init_counters, dim3((unsigned)nr), dim3(256), 0, s, lcnt, lcnt + nr, nc, nr, nci,
+                           fused ? 1 : 0);
         GPRX_HIP(hipMemsetD32Async((hipDeviceptr_t)R.info.p, INT_MAX, 1, s));
         GPRX_HIP(hipMemsetAsync(R.flag.p, 0, sizeof(int), s));
-        T* A = R.A.template as<T>();
-        if (fused) {
-            // BUILD tasks write the lower tiles: ver = -1 until built (rows of the matrix only)
-            GPRX_HIP(hipMemsetAsync(R.ctr.template as<int>() + C_NCTL_DIST + nr, 0xff, sizeof(int) * (size_t)nc * nc, s));
-        } else {
-            // the direct build: each owned row block against the columns up to its diagonal
-            GPRX_HIP(hipMemsetAsync(A, 0, sizeof(T) * R.ld * np, s));
-            for (int i : E.L.rows[r]) {
-                if (i >= nc) continue;
+        T* A = R.store.template as<T>();
+        for (int x = 0; x < (int)E.L.rows[r].size(); x++) {
+            const int i = E.L.rows[r][x];
+            T* base = A + E.L.roff[r][x];
+            if (i == nc) {  // the label rows: Y^T as row block nc (DB x np, ld DB)
+                launch_label_rows<T>(in.Y, n, in.m, base, DB, 0, np, GT, s);
+            } else if (i > nc) {  // identity row block of the inverse (LML mode)
+                const int64_t e = (int64_t)E.L.ncols(i) * DB2;
+                hipLaunchKernelGGL(dist_init_identity<T>, dim3((unsigned)((e + 255) / 256)), dim3(256), 0, s, base,
+                                   E.L.ncols(i));
+            } else if (!fused) {  // the direct build: row block i against the columns up to its diagonal
                 const int64_t r0 = (int64_t)i * DB, rows = std::min<int64_t>(DB, n - r0), cols = std::min<int64_t>(r0 + DB, n);
-                T* Ai = A + (int64_t)E.L.loc(i) * DB;
+                GPRX_HIP(hipMemsetAsync(base, 0, sizeof(T) * (size_t)E.L.ncols(i) * DB2, s));
                 if (rows > 0) {
                     const T *tabr = nullptr, *tabc = nullptr;
+                    DMem tab;
                     if (in.K.nper > 0) {  // sin/cos tables of the block's rows and of its columns
                         const size_t slot = (size_t)2 * in.K.nper * in.d;
-                        R.tab.ensure(sizeof(T) * slot * ((size_t)DB + (size_t)n));
-                        T* tr = R.tab.template as<T>();
+                        tab.alloc(sizeof(T) * slot * ((size_t)DB + (size_t)n), false);
+                        T* tr = tab.as<T>();
                         T* tc = tr + slot * DB;
                         launch_sincos_tables<T>(in.K, in.X + r0 * in.d, rows, in.d, tr, s);
                         launch_sincos_tables<T>(in.K, in.X, cols, in.d, tc, s);
                         tabr = tr;
                         tabc = tc;
                     }
-                    launch_kbuild<T>(in.K, in.X + r0 * in.d, tabr, rows, in.X, tabc, cols, in.d, Ai, R.ld, 0, false,
-                                     T(0), R.flag.template as<int>(), s);
+                    launch_kbuild<T>(in.K, in.X + r0 * in.d, tabr, rows, in.X, tabc, cols, in.d, base, DB, 0, false, T(0),
+                                     R.flag.template as<int>(), s);
+                    if (tab.p) GPRX_HIP(hipStreamSynchronize(s));  // before the tables are freed
                 }
-                hipLaunchKernelGGL(diag_fix_local_kernel<T>, dim3(1), dim3(DB), 0, s, A, R.ld,
-                                   (int64_t)E.L.loc(i) * DB, r0, n, in.sigma2);
+                hipLaunchKernelGGL(dist_diag_fix<T>, dim3(1), dim3(DB), 0, s, base + (int64_t)i * DB2, r0, n, in.sigma2);
             }
         }
-        if (E.L.owner(nc) == r)  // the label rows: Y^T as row block nc
-            launch_label_rows<T>(in.Y, n, in.m, A, R.ld, (int64_t)E.L.loc(nc) * DB, np, GT, s);
-        TileBuild<T> tbl = in.tb;
-        tbl.flag = R.flag.template as<int>();
+        const PtDist<T> pd = make_ptdist(E, R);
+        GPRX_HIP(hipMemcpyAsync(R.pd.p, &pd, sizeof(pd), hipMemcpyHostToDevice, s));
         void* tbdev = nullptr;
         if (fused) {
-            R.red.ensure(std::max<size_t>(R.red.bytes, sizeof(TileBuild<T>) + 64));
-            tbdev = static_cast<char*>(R.red.p) + 64;  // after the reduction doubles
-            // synchronous, before any rank's persistent launch: a pageable copy queued behind
-            // one could wait for it (and the virtual ranks' launches must be co-resident)
-            GPRX_HIP(hipStreamSynchronize(s));
-            GPRX_HIP(hipMemcpy(tbdev, &tbl, sizeof(tbl), hipMemcpyHostToDevice));
+            TileBuild<T> tbl = in.tb;
+            tbl.flag = R.flag.template as<int>();
+            tbdev = static_cast<char*>(R.red.p) + 64;
+            GPRX_HIP(hipMemcpyAsync(tbdev, &tbl, sizeof(tbl), hipMemcpyHostToDevice, s));
         }
-        DistLaunch<T>& Lc = launches[&Rp - &E.ranks[0]];
+        GPRX_HIP(hipStreamSynchronize(s));  // pageable copies done before any rank's persistent launch
+        DistLaunch<T>& Lc = launches[v];
         Lc.A = A;
-        Lc.ld = R.ld;
-        Lc.Linv = R.Linv.template as<T>();
+        Lc.Linv = reinterpret_cast<T*>(R.mbox.template as<char>() + E.MB.o_linv);
         Lc.info = R.info.template as<int>();
         Lc.list = R.list.template as<int4>();
         Lc.ntasks = R.ntasks;
         Lc.nc = nc;
         Lc.nr = nr;
+        Lc.nci = nci;
         Lc.ctr = R.ctr.template as<int>();
         Lc.tb_dev = reinterpret_cast<const TileBuild<T>*>(tbdev);
         Lc.dist_dev = R.pd.template as<PtDist<T>>();
-        Lc.tlimit = (long long)(1e8 * (2.0 + 20.0 * E.est_us * 1e-6));
+        Lc.tlimit = (long long)(1e8 * (2.0 + 20.0 * E.S.est_us * 1e-6));
         Lc.P = E.P;
         Lc.s = s;
         Lc.dbg = nullptr;
         Lc.trace = nullptr;
-        static const char* tdir = std::getenv("GPRX_DIST_TRACE_DEV");  // directory for per-rank task traces
-        if (tdir) {
-            R.trace.ensure(sizeof(long long) * 4 * ((size_t)R.ntasks + 2 * (size_t)nc));
-            GPRX_HIP(hipMemsetAsync(R.trace.p, 0, R.trace.bytes, s));
-            Lc.trace = R.trace.template as<long long>();
-        }
-        static const bool dbgw = std::getenv("GPRX_DIST_DEBUG") != nullptr;
-        if (dbgw) {
-            R.dbg.ensure(sizeof(int) * 4 * E.P);
-            std::memset(R.dbg.p, 0xff, sizeof(int) * 4 * E.P);
-            GPRX_HIP(hipHostGetDevicePointer((void**)&Lc.dbg, R.dbg.p, 0));
-        }
     }
     // every rank's persistent launch back to back, nothing that could block in between
     for (size_t v = 0; v < E.ranks.size(); v++) {
         GPRX_HIP(hipEventRecord(E.ranks[v]->t0, E.ranks[v]->s));
         potrf_tiles_dist_launch<T>(launches[v]);
-        GPRX_HIP(hipEventRecord(E.ranks[v]->done, E.ranks[v]->s));
         GPRX_HIP(hipEventRecord(E.ranks[v]->t1, E.ranks[v]->s));
     }
-    // ---- issue loop: transport steps as their inputs become ready --------------------------
-    const auto ts = std::chrono::steady_clock::now();
-    int kb = 0, kp = 0;
-    bool flush = false;
-    double issue_s = 0;  // host time spent inside the transport calls (diagnostics)
-    double dbg_next = 0.25;
-    const double limit_s = 4.0 + 40.0 * E.est_us * 1e-6;
-    static const bool trace = std::getenv("GPRX_DIST_TRACE") != nullptr;
-    std::vector<double> tb_issue(trace ? nc : 0), tp_issue(trace ? nc : 0);
-    auto now_us = [&]() { return 1e6 * std::chrono::duration<double>(std::chrono::steady_clock::now() - ts).count(); };
-    while (kb < nc || kp < nc) {
-        bool progress = false;
-        if (kb < nc && (flush || bcast_ready(E, kb))) {
-            const auto t0 = std::chrono::steady_clock::now();
-            if (trace) tb_issue[kb] = now_us();
-            issue_bcast(E, kb++);
-            issue_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-            progress = true;
-        }
-        if (kp < nc && kp < kb + 1 && (flush || panel_ready(E, kp))) {
-            const auto t0 = std::chrono::steady_clock::now();
-            if (trace) tp_issue[kp] = now_us();
-            issue_panel(E, kp++);
-            issue_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-            progress = true;
-        }
-        if (progress || flush) continue;
-        // stalled: kernels ended early (a timed-out wait drained them) or out of time -> issue
-        // the rest (their data is stale, the fit reports the error) so peers are not left
-        // waiting inside RCCL
-        bool all_done = true;
-        for (auto& R : E.ranks) all_done &= hipEventQuery(R->done) == hipSuccess;
-        const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - ts).count();
-        static const bool dbgw = std::getenv("GPRX_DIST_DEBUG") != nullptr;
-        if (dbgw && !flush && el > dbg_next) {  // a stall: where every workgroup is
-            dbg_next += 0.5;
-            for (auto& Rp : E.ranks) {
-                const int* w = reinterpret_cast<const int*>(Rp->dbg.p);
-                unsigned rc[2] = {9999, 9999};
-                (void)hipMemcpy(rc, Rp->drecv.p, sizeof(rc), hipMemcpyDeviceToHost);
-                int nun = 0, nwait = 0, nwork = 0, nend = 0;
-                for (int x = 0; x < E.P; x++) {
-                    const int ph = __atomic_load_n(w + 4 * x + 1, __ATOMIC_ACQUIRE);
-                    nun += ph < 0;
-                    nwait += ph >= 0 && ph % 10 == 1;
-                    nwork += ph >= 0 && ph % 10 == 2;
-                    nend += ph == 9;
-                }
-                std::fprintf(stderr,
-                             "gprx dist stall rank %d (issued bcast %d panel %d, %.3f s; device drecv %u precv %u; "
-                             "issue calls took %.3f s; workgroups unstarted %d waiting %d working %d ended %d; hdiag0 %u):",
-                             Rp->r, kb, kp, el, rc[0], rc[1], issue_s, nun, nwait, nwork, nend, Rp->hdiag.u()[0]);
-                int shown = 0;
-                for (int x = 0; x < E.P && shown < 16; x++) {
-                    const int q = __atomic_load_n(w + 4 * x, __ATOMIC_ACQUIRE), ph = w[4 * x + 1];
-                    if (q < 0 || q >= (int)Rp->hlist.size() || ph % 10 != 1) continue;
-                    const int4 t = Rp->hlist[q];
-                    shown++;
-                    std::fprintf(stderr, " [t%d %s(%d,%d,b0 %d,nb %d)]", q,
-                                 (t.x & 255) == 0 ? "DIAGX" : (t.x & 255) == 1 ? "TRSM" : (t.x & 255) == 2 ? "UPD" : "BUILD",
-                                 t.y, t.z, t.w, t.x >> 8);
-                }
-                std::fprintf(stderr, "\n");
-            }
-        }
-        if (all_done || el > limit_s) flush = true;
-        else std::this_thread::yield();
-    }
     for (auto& R : E.ranks) GPRX_HIP(hipStreamSynchronize(R->s));
-    if (const char* tdir = std::getenv("GPRX_DIST_TRACE_DEV")) {  // raw per-rank task traces
-        for (auto& Rp : E.ranks) {
-            std::vector<long long> tr(4 * ((size_t)Rp->ntasks + 2 * (size_t)nc));
-            GPRX_HIP(hipMemcpy(tr.data(), Rp->trace.p, sizeof(long long) * tr.size(), hipMemcpyDeviceToHost));
-            const std::string path = std::string(tdir) + "/rank" + std::to_string(Rp->r) + ".bin";
-            if (FILE* f = std::fopen(path.c_str(), "wb")) {
-                const int hdr[4] = {Rp->ntasks, nc, E.g, E.L.gb};
-                std::fwrite(hdr, sizeof(int), 4, f);
-                std::fwrite(Rp->hlist.data(), sizeof(int4), Rp->hlist.size(), f);
-                std::fwrite(tr.data(), sizeof(long long), tr.size(), f);
-                std::fclose(f);
-            }
-        }
-    }
-    if (trace) {  // host times of the transport issues (us from the launches)
-        const double tend = now_us();
-        std::fprintf(stderr, "gprx dist trace g %d P %d nc %d: end %.0f us, issue calls %.0f us\n", E.g, E.P, nc, tend,
-                     1e6 * issue_s);
-        for (int k = 0; k < nc; k++)
-            if (k < 8 || k % 16 == 0 || k >= nc - 4)
-                std::fprintf(stderr, "  k %4d bcast %9.1f panel %9.1f  (bcast step %7.1f)\n", k, tb_issue[k], tp_issue[k],
-                             k ? tb_issue[k] - tb_issue[k - 1] : tb_issue[k]);
-    }
-    GPRX_HIP(hipStreamSynchronize(E.sB));
-    GPRX_HIP(hipStreamSynchronize(E.sP));
     GPRX_HIP(hipGetLastError());
-    static const bool dbg = std::getenv("GPRX_DIST_DEBUG") != nullptr;
-    if (dbg || flush) {  // the state the issue loop ended in (flush: a stall)
-        for (auto& Rp : E.ranks) {
-            DistRank<T>& R = *Rp;
-            unsigned rc[2] = {0, 0};
-            int ctl[2] = {0, 0};
-            GPRX_HIP(hipMemcpy(rc, R.drecv.p, sizeof(rc), hipMemcpyDeviceToHost));
-            GPRX_HIP(hipMemcpy(ctl, R.ctr.p, sizeof(ctl), hipMemcpyDeviceToHost));
-            int nd = 0, ns = 0, nsw = 0;
-            for (int k = 0; k < nc; k++) nd += R.hdiag.u()[k] != 0;
-            for (int i = 0; i < nr; i++)
-                for (int b = 0; b < std::min(i, nc); b++)
-                    if (E.L.owner(i) == R.r) {
-                        nsw++;
-                        ns += R.hslot.u()[(size_t)i * nc + b] != 0;
-                    }
-            std::fprintf(stderr,
-                         "gprx dist rank %d/%d: P %d tickets %d/%d err %d | diag flags %d/%d (own) send slots %d/%d | "
-                         "drecv %u precv %u | issued bcast %d panel %d of %d%s\n",
-                         R.r, E.g, E.P, ctl[0], R.ntasks, ctl[1], nd, E.L.cnt(R.r, -1) - (E.L.owner(nc) == R.r), ns, nsw, rc[0], rc[1],
-                         kb, kp, nc, flush ? " (flushed)" : "");
-        }
-    }
-    // ---- reductions, back substitution (every rank holds every tile) -------------------------
-    double logdet = 0, datafit = 0;
-    int info = INT_MAX, flag = 0;
+    // ---- reductions: log det, data fit, status (one small all-gather over the processes) --------
+    struct Part {
+        double logdet, datafit;
+        int info, flag;
+    };
+    Part tot{0, 0, INT_MAX, 0};
     for (auto& Rp : E.ranks) {
         DistRank<T>& R = *Rp;
-        hipLaunchKernelGGL(dist_reduce_kernel<T>, dim3(1), dim3(256), 0, R.s, R.A.template as<T>(), R.ld,
-                           R.loc.template as<int>(), E.g, R.r, nc, n, in.m, R.tiles.template as<uint64_t>(),
-                           R.tld.template as<int64_t>(), R.red.template as<double>());
+        DSArgs<T> a = make_dsargs(E, R);
+        launch_dist_reduce<T>(a, n, R.red.template as<double>(), R.s);
         double red[2];
         int hi = 0, hf = 0;
         GPRX_HIP(hipMemcpyAsync(red, R.red.p, sizeof(red), hipMemcpyDeviceToHost, R.s));
         GPRX_HIP(hipMemcpyAsync(&hi, R.info.p, sizeof(int), hipMemcpyDeviceToHost, R.s));
         GPRX_HIP(hipMemcpyAsync(&hf, R.flag.p, sizeof(int), hipMemcpyDeviceToHost, R.s));
         GPRX_HIP(hipStreamSynchronize(R.s));
-        logdet += red[0];
-        datafit = red[1];
-        info = std::min(info, hi);
-        flag = std::max(flag, hf);
+        tot.logdet += red[0];
+        tot.datafit += red[1];
+        tot.info = std::min(tot.info, hi);
+        tot.flag = std::max(tot.flag, hf);
     }
-    if (!E.virt && E.g > 1) {  // combine over the ranks: sum of log det, min info, max flag
-        DMem dv;
-        dv.ensure(sizeof(double) + 2 * sizeof(int));
-        double* dl = dv.as<double>();
-        int* di = reinterpret_cast<int*>(dl + 1);
-        GPRX_HIP(hipMemcpyAsync(dl, &logdet, sizeof(double), hipMemcpyHostToDevice, R0.s));
-        GPRX_HIP(hipMemcpyAsync(di, &info, sizeof(int), hipMemcpyHostToDevice, R0.s));
-        GPRX_HIP(hipMemcpyAsync(di + 1, &flag, sizeof(int), hipMemcpyHostToDevice, R0.s));
-        rccl_ok(ncclGroupStart(), "ncclGroupStart");
-        rccl_ok(ncclAllReduce(dl, dl, 1, ncclFloat64, ncclSum, E.commB, R0.s), "ncclAllReduce");
-        rccl_ok(ncclAllReduce(di, di, 1, ncclInt32, ncclMin, E.commB, R0.s), "ncclAllReduce");
-        rccl_ok(ncclAllReduce(di + 1, di + 1, 1, ncclInt32, ncclMax, E.commB, R0.s), "ncclAllReduce");
-        rccl_ok(ncclGroupEnd(), "ncclGroupEnd");
-        GPRX_HIP(hipMemcpyAsync(&logdet, dl, sizeof(double), hipMemcpyDeviceToHost, R0.s));
-        GPRX_HIP(hipMemcpyAsync(&info, di, sizeof(int), hipMemcpyDeviceToHost, R0.s));
-        GPRX_HIP(hipMemcpyAsync(&flag, di + 1, sizeof(int), hipMemcpyDeviceToHost, R0.s));
-        GPRX_HIP(hipStreamSynchronize(R0.s));
+    if (!E.virt && E.g > 1) {  // across the processes (rank order: identical sums everywhere)
+        std::vector<Part> all(E.g);
+        E.hc->allgather(&tot, sizeof(Part), all.data());
+        tot = Part{0, 0, INT_MAX, 0};
+        for (const Part& p : all) {
+            tot.logdet += p.logdet;
+            tot.datafit += p.datafit;
+            tot.info = std::min(tot.info, p.info);
+            tot.flag = std::max(tot.flag, p.flag);
+        }
     }
-    out.logdet = logdet;
-    out.datafit = datafit;
-    out.info = info;
-    out.flag = flag;
-    out.est_us = E.est_us;
+    out.logdet = tot.logdet;
+    out.datafit = tot.datafit;
+    out.info = tot.info;
+    out.flag = tot.flag;
+    out.est_us = E.S.est_us;
     out.P = E.P;
+    out.gb = E.gb;
+    out.ww = E.ww;
+    out.chunk_w = E.W;
     out.ms_kernel = 0;
-    for (auto& Rp : E.ranks) {  // the persistent launches' device time (the slowest rank)
+    out.bytes_rank = 0;
+    out.bytes_storage = 0;
+    for (auto& Rp : E.ranks) {
         float ms = 0;
         if (hipEventElapsedTime(&ms, Rp->t0, Rp->t1) == hipSuccess) out.ms_kernel = std::max(out.ms_kernel, (double)ms);
+        const int64_t b = (int64_t)(Rp->store.bytes + Rp->mbox.bytes + Rp->ctr.bytes + Rp->part.bytes + Rp->t_tptr.bytes +
+                                    Rp->t_cons.bytes + Rp->t_need.bytes + Rp->list.bytes + Rp->t_ctab.bytes);
+        out.bytes_rank = std::max(out.bytes_rank, b);
+        out.bytes_storage = std::max(out.bytes_storage, (int64_t)Rp->store.bytes);
     }
-    if (info < 0 || info != INT_MAX || flag) return;  // the caller reports it
-    // alpha = L^{-T} z on rank 0 of this process (the factor is complete on every rank)
-    GPRX_HIP(hipMemsetD32Async((hipDeviceptr_t)R0.info.p, INT_MAX, 1, R0.s));
-    launch_backsolve_chain<T>(nullptr, 0, np, in.m, R0.Linv.template as<T>(), alpha_dev, R0.info.template as<int>(), ex,
-                              R0.s, R0.tiles.template as<uint64_t>(), R0.tld.template as<int64_t>());
-    GPRX_HIP(hipEventRecord(R0.t2, R0.s));
-    int hi = 0;
-    GPRX_HIP(hipMemcpyAsync(&hi, R0.info.p, sizeof(int), hipMemcpyDeviceToHost, R0.s));
-    GPRX_HIP(hipStreamSynchronize(R0.s));
-    if (hi != INT_MAX) out.info = hi;
-    float ms = 0;
-    if (hipEventElapsedTime(&ms, R0.t1, R0.t2) == hipSuccess) out.ms_solve = ms;
-    (void)DB2;
+    if (tot.info != INT_MAX || tot.flag) return;  // the caller reports it
+    // ---- alpha = L^{-T} z: the distributed back substitution ---------------------------------
+    E.sep++;
+    const auto ts0 = std::chrono::steady_clock::now();
+    for (auto& Rp : E.ranks) {
+        DistRank<T>& R = *Rp;
+        GPRX_HIP(hipMemsetAsync(R.sctl.p, 0, sizeof(int) * 8, R.s));
+        GPRX_HIP(hipMemsetD32Async((hipDeviceptr_t)R.info.p, INT_MAX, 1, R.s));
+    }
+    for (auto& Rp : E.ranks) {
+        DSArgs<T> a = make_dsargs(E, *Rp);
+        a.zmode = 0;
+        launch_dist_back<T>(a, Rp->s);
+    }
+    int hinfo = INT_MAX;
+    for (auto& Rp : E.ranks) {
+        int hi = 0;
+        GPRX_HIP(hipMemcpyAsync(&hi, Rp->info.p, sizeof(int), hipMemcpyDeviceToHost, Rp->s));
+        GPRX_HIP(hipStreamSynchronize(Rp->s));
+        hinfo = std::min(hinfo, hi);
+    }
+    out.ms_solve = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts0).count();
+    if (hinfo != INT_MAX) {
+        out.info = -1;
+        return;
+    }
+    const DistRank<T>& R0 = *E.ranks[0];
+    GPRX_HIP(hipMemcpy(alpha_dev, R0.mbox.template as<char>() + E.MB.o_alpha, sizeof(T) * np * E.m,
+                       hipMemcpyDeviceToDevice));
 }
 
-void dist_engine_free(DistEngineBase* e) { delete e; }
-
-namespace {
+// ---------------------------------------------------------------------------------------
+// solves with the sharded factor (the fp32 refinement's correction)
+// ---------------------------------------------------------------------------------------
 template <typename T>
-__global__ __launch_bounds__(256) void assemble_tiles_kernel(const uint64_t* __restrict__ tiles,
-                                                             const int64_t* __restrict__ tld, int nc, T* __restrict__ A,
-                                                             int64_t ld) {
-    const int i = blockIdx.x, j = blockIdx.y;  // tile (i, j), i > j
-    if (j >= i) return;
-    const T* src = reinterpret_cast<const T*>(tiles[(int64_t)i * nc + j]);
-    const int64_t sl = tld[i];
-    T* dst = A + (int64_t)i * DB + (int64_t)j * DB * ld;
-    for (int e = threadIdx.x; e < DB * DB; e += 256) {
-        const int r = e & (DB - 1), c = e >> 7;
-        dst[r + (int64_t)c * ld] = src[r + (int64_t)c * sl];
+void dist_solve(DistEngineBase* eng, const T* rhs, T* out, hipStream_t s) {
+    auto* Ep = dynamic_cast<DistEngine<T>*>(eng);
+    GPRX_REQUIRE(Ep && !Ep->ranks.empty(), GPRX_ERR_STATE, "distributed solve: no factor");
+    DistEngine<T>& E = *Ep;
+    GPRX_HIP(hipStreamSynchronize(s));  // rhs written on the caller's stream
+    E.sep++;
+    for (auto& Rp : E.ranks) {
+        GPRX_HIP(hipMemsetAsync(Rp->sctl.p, 0, sizeof(int) * 8, Rp->s));
+        GPRX_HIP(hipMemsetD32Async((hipDeviceptr_t)Rp->info.p, INT_MAX, 1, Rp->s));
     }
+    for (auto& Rp : E.ranks) {
+        DSArgs<T> a = make_dsargs(E, *Rp);
+        a.rhs = rhs;
+        launch_dist_forward<T>(a, Rp->s);
+    }
+    for (auto& Rp : E.ranks) GPRX_HIP(hipMemsetAsync(Rp->sctl.p, 0, sizeof(int) * 8, Rp->s));
+    for (auto& Rp : E.ranks) {
+        DSArgs<T> a = make_dsargs(E, *Rp);
+        a.zmode = 1;
+        launch_dist_back<T>(a, Rp->s);
+    }
+    int hinfo = INT_MAX;
+    for (auto& Rp : E.ranks) {
+        int hi = 0;
+        GPRX_HIP(hipMemcpyAsync(&hi, Rp->info.p, sizeof(int), hipMemcpyDeviceToHost, Rp->s));
+        GPRX_HIP(hipStreamSynchronize(Rp->s));
+        hinfo = std::min(hinfo, hi);
+    }
+    if (hinfo != INT_MAX) throw Error{GPRX_ERR_HIP, "gprx: distributed solve timed out (flag wait)"};
+    const DistRank<T>& R0 = *E.ranks[0];
+    GPRX_HIP(hipMemcpy(out, R0.mbox.template as<char>() + E.MB.o_alpha, sizeof(T) * E.np * E.m, hipMemcpyDeviceToDevice));
 }
-}  // namespace
+template void dist_solve<double>(DistEngineBase*, const double*, double*, hipStream_t);
+template void dist_solve<float>(DistEngineBase*, const float*, float*, hipStream_t);
 
+// ---------------------------------------------------------------------------------------
+// the dense factor on this process (posterior covariance, core matrix): a documented gather
+// ---------------------------------------------------------------------------------------
 template <typename T>
-void dist_assemble_factor(DistEngineBase* eng, T* A, int64_t ld, T* Linv, hipStream_t s) {
-    GPRX_REQUIRE(eng, GPRX_ERR_STATE, "distributed fit: no factor");
-    DistEngine<T>& E = *static_cast<DistEngine<T>*>(eng);
-    GPRX_REQUIRE(!E.ranks.empty(), GPRX_ERR_STATE, "distributed fit: no factor");
+void dist_gather_factor(DistEngineBase* eng, T* A, int64_t ld, T* Linv, hipStream_t s) {
+    auto* Ep = dynamic_cast<DistEngine<T>*>(eng);
+    GPRX_REQUIRE(Ep && !Ep->ranks.empty(), GPRX_ERR_STATE, "distributed fit: no factor");
+    DistEngine<T>& E = *Ep;
     const DistRank<T>& R0 = *E.ranks[0];
     const int nc = E.L.nc;
+    const int64_t DB2 = (int64_t)DB * DB;
+    std::vector<uint64_t> src((size_t)nc * nc, 0);
+    for (int i = 0; i < nc; i++) {
+        const int q = E.L.own[i];
+        for (int j = 0; j < i; j++)
+            src[(size_t)i * nc + j] = R0.st[q] + sizeof(T) * (uint64_t)(E.L.roff[q][E.L.loc[i]] + (int64_t)j * DB2);
+    }
+    DMem tab;
+    upload_vec(tab, src);
     GPRX_HIP(hipMemsetAsync(A, 0, sizeof(T) * (size_t)ld * nc * DB, s));
     if (nc > 1)
-        hipLaunchKernelGGL(assemble_tiles_kernel<T>, dim3((unsigned)nc, (unsigned)nc), dim3(256), 0, s,
-                           R0.tiles.template as<uint64_t>(), R0.tld.template as<int64_t>(), nc, A, ld);
-    GPRX_HIP(hipMemcpyAsync(Linv, R0.Linv.p, sizeof(T) * (size_t)nc * DB * DB, hipMemcpyDeviceToDevice, s));
+        hipLaunchKernelGGL(dist_gather_kernel<T>, dim3((unsigned)nc, (unsigned)nc), dim3(256), 0, s,
+                           tab.as<uint64_t>(), nc, A, ld);
+    GPRX_HIP(hipMemcpyAsync(Linv, R0.mbox.template as<char>() + E.MB.o_linv, sizeof(T) * (size_t)nc * DB2,
+                            hipMemcpyDeviceToDevice, s));
     GPRX_HIP(hipStreamSynchronize(s));
+    GPRX_HIP(hipGetLastError());
 }
-template void dist_assemble_factor<double>(DistEngineBase*, double*, int64_t, double*, hipStream_t);
-template void dist_assemble_factor<float>(DistEngineBase*, float*, int64_t, float*, hipStream_t);
+template void dist_gather_factor<double>(DistEngineBase*, double*, int64_t, double*, hipStream_t);
+template void dist_gather_factor<float>(DistEngineBase*, float*, int64_t, float*, hipStream_t);
+
+// ---------------------------------------------------------------------------------------
+// LML gradient from the ranks' C tiles
+// ---------------------------------------------------------------------------------------
+template <typename T>
+void dist_lml_grad(DistEngineBase* eng, const KCanon<T>& K, const KCanon<T>* Kd, const T* X, int64_t n, int d,
+                   const T* FU, const T* FV, T* GU, T* GV, int64_t nf, const T* alpha, double* part, double* acc,
+                   hipStream_t s) {
+    auto* Ep = dynamic_cast<DistEngine<T>*>(eng);
+    GPRX_REQUIRE(Ep && !Ep->ranks.empty() && Ep->key_inv, GPRX_ERR_STATE, "distributed gradient: no LML-mode factor");
+    DistEngine<T>& E = *Ep;
+    double tot[MAX_LEAF * 3] = {0};
+    for (auto& Rp : E.ranks) {
+        launch_lml_grad_mma<T>(K, Kd, X, n, d, FU, FV, GU, GV, nf, alpha, nullptr, 0, part, acc, s,
+                               Rp->t_ctab.template as<uint64_t>());
+        double p[MAX_LEAF * 3];
+        GPRX_HIP(hipStreamSynchronize(s));
+        GPRX_HIP(hipMemcpy(p, acc, sizeof(p), hipMemcpyDeviceToHost));
+        for (int q = 0; q < MAX_LEAF * 3; q++) tot[q] += p[q];
+    }
+    GPRX_HIP(hipMemcpy(acc, tot, sizeof(tot), hipMemcpyHostToDevice));
+    if (!E.virt && E.g > 1) hostcoll_allreduce_dev<double>(E.hc, acc, MAX_LEAF * 3, s);
+}
+template void dist_lml_grad<double>(DistEngineBase*, const KCanon<double>&, const KCanon<double>*, const double*, int64_t,
+                                    int, const double*, const double*, double*, double*, int64_t, const double*,
+                                    double*, double*, hipStream_t);
+template void dist_lml_grad<float>(DistEngineBase*, const KCanon<float>&, const KCanon<float>*, const float*, int64_t,
+                                   int, const float*, const float*, float*, float*, int64_t, const float*, double*,
+                                   double*, hipStream_t);
 
 template <typename T>
-static bool layout_of(DistEngineBase* eng, int* g, int* gb, int* rank, bool* virt) {
+static bool own_blocks_of(DistEngineBase* eng, std::vector<int>& out) {
     auto* E = dynamic_cast<DistEngine<T>*>(eng);
     if (!E || E->ranks.empty()) return false;
-    *g = E->g;
-    *gb = E->L.gb;
-    *rank = E->ranks[0]->r;
-    *virt = E->virt;
+    out.clear();
+    for (auto& R : E->ranks)
+        for (int i : R->orows) out.push_back(i);
+    std::sort(out.begin(), out.end());
     return true;
 }
-
-void dist_layout(DistEngineBase* eng, int* g, int* gb, int* rank, bool* virt) {
-    GPRX_REQUIRE(eng && (layout_of<double>(eng, g, gb, rank, virt) || layout_of<float>(eng, g, gb, rank, virt)),
-                 GPRX_ERR_STATE, "distributed fit: no layout");
+std::vector<int> dist_own_blocks(DistEngineBase* eng) {
+    std::vector<int> v;
+    GPRX_REQUIRE(eng && (own_blocks_of<double>(eng, v) || own_blocks_of<float>(eng, v)), GPRX_ERR_STATE,
+                 "distributed fit: no layout");
+    return v;
 }
 
 template <typename T>
 static bool allreduce_of(DistEngineBase* eng, double* dev, int count, hipStream_t s) {
     auto* E = dynamic_cast<DistEngine<T>*>(eng);
     if (!E) return false;
-    if (!E->virt && E->g > 1) {
-        rccl_ok(ncclAllReduce(dev, dev, (size_t)count, ncclFloat64, ncclSum, E->commB, s), "ncclAllReduce");
-        GPRX_HIP(hipStreamSynchronize(s));
-    }
+    if (!E->virt && E->g > 1) hostcoll_allreduce_dev<double>(E->hc, dev, count, s);
     return true;
 }
-
 void dist_allreduce_sum(DistEngineBase* eng, double* dev, int count, hipStream_t s) {
     GPRX_REQUIRE(eng && (allreduce_of<double>(eng, dev, count, s) || allreduce_of<float>(eng, dev, count, s)),
                  GPRX_ERR_STATE, "distributed fit: no engine");
 }
 
-template void dist_fit<double>(DistEngineBase*&, const DistContext&, const DistFitIn<double>&, DistFitOut&, double*,
-                               Exec&);
-template void dist_fit<float>(DistEngineBase*&, const DistContext&, const DistFitIn<float>&, DistFitOut&, float*, Exec&);
+void dist_engine_free(DistEngineBase* e) { delete e; }
+
+template void dist_fit<double>(DistEngineBase*&, const DistContext&, const DistFitIn<double>&, DistFitOut&, double*);
+template void dist_fit<float>(DistEngineBase*&, const DistContext&, const DistFitIn<float>&, DistFitOut&, float*);
 
 }  // namespace gprx

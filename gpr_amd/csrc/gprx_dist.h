@@ -7,13 +7,31 @@ namespace gprx {
 
 constexpr int C_NCTL_DIST = 16;  // control words at the head of a tile launch's counter block (k_mma.h)
 
-// the process's view of the ranks: one RCCL rank per process, or g virtual ranks on one GPU
+// Small host-side collectives between the processes of a distributed context: exchanging the
+// mailboxes' IPC handles, and the per-fit reductions (log det, status) of a few bytes.  The bulk
+// exchange never goes through here -- it is device-initiated (pushes into the peers' mailboxes).
+struct HostColl {
+    virtual ~HostColl() {}
+    // recv (world * bytes) receives every rank's `send` in rank order
+    virtual void allgather(const void* send, size_t bytes, void* recv) = 0;
+};
+// RCCL (ncclAllGather through a device staging buffer)
+HostColl* make_rccl_coll(ncclComm_t comm, int world, int device);
+// the caller's function (gprx_ctx_create_peer)
+HostColl* make_callback_coll(gprx_allgather_fn fn, void* user, int world);
+
+// sum over the ranks of `count` values in device memory (in place), through the collective
+template <typename T>
+void hostcoll_allreduce_dev(HostColl* hc, T* dev, int count, hipStream_t s);
+
+// the process's view of the ranks: one rank per process (RCCL or caller collectives), or g
+// virtual ranks on one GPU
 struct DistContext {
     int device = 0;
     int rank = 0, world = 1;
-    bool virt = false;           // world virtual ranks in this process (device copies, no RCCL)
-    ncclComm_t comm = nullptr;   // RCCL communicator (not virt)
-    hipStream_t stream = nullptr;  // the rank's compute stream (not virt)
+    bool virt = false;             // world virtual ranks in this process (direct pointers)
+    HostColl* hc = nullptr;        // multi-process collectives (not virt)
+    int cu_slot = 0, cu_slots = 1;  // this process's share of the CUs (ranks sharing one GPU)
 };
 
 template <typename T>
@@ -25,32 +43,74 @@ struct DistFitIn {
     int d, m;
     T sigma2;
     TileBuild<T> tb;  // mode != 0: the fused MFMA build (features of all n samples); else the direct build
+    bool inv;         // LML mode: the inverse's identity rows and C = (K + s^2 I)^{-1} ride along
 };
 
 struct DistFitOut {
     double logdet = 0, datafit = 0, est_us = 0;
     double ms_kernel = 0, ms_solve = 0;  // device time: persistent launch (slowest local rank), back-solve
     int info = 0, flag = 0, P = 0;
+    int gb = 1, ww = 0, chunk_w = 0;     // the layout and window the schedule picked
+    int64_t bytes_rank = 0;              // device bytes the engine holds per rank (max over this process's ranks)
+    int64_t bytes_storage = 0;           // of which the packed own rows
 };
 
 struct DistEngineBase;
-// One distributed fit: alpha_dev (np x m, this process's rank 0) receives the regression
+// One distributed fit: alpha_dev (np x m, row-major, this process) receives the regression
 // vectors when the factorisation succeeds (out.info == INT_MAX, out.flag == 0).
 template <typename T>
-void dist_fit(DistEngineBase*& eng, const DistContext& C, const DistFitIn<T>& in, DistFitOut& out, T* alpha_dev,
-              Exec& ex);
+void dist_fit(DistEngineBase*& eng, const DistContext& C, const DistFitIn<T>& in, DistFitOut& out, T* alpha_dev);
 void dist_engine_free(DistEngineBase* e);
 
-// After a successful dist_fit: the dense factor on this process (every rank holds every
-// off-diagonal tile and every diagonal inverse): the strictly-lower blocks of L into A
-// (np x np, column-major, ld) and Linv (nc blocks of DB x DB), on `s` (synchronised).
+// (L L^T)^{-1} rhs with the sharded factor of the last fit: the forward and back substitutions
+// chained on the devices across the ranks.  rhs: np x m row-major (each rank reads its own row
+// blocks; a virtual context's ranks all read this buffer); out: np x m, every rank.
 template <typename T>
-void dist_assemble_factor(DistEngineBase* eng, T* A, int64_t ld, T* Linv, hipStream_t s);
-// The layout of the last fit: ranks, row-block group size, this process's first rank, and
-// whether its ranks are virtual (all in this process).
-void dist_layout(DistEngineBase* eng, int* g, int* gb, int* rank, bool* virt);
-// In-place sum over the ranks of `count` doubles in device memory (RCCL; no-op for virtual
-// ranks and one-rank communicators).
+void dist_solve(DistEngineBase* eng, const T* rhs, T* out, hipStream_t s);
+// After a successful dist_fit: the dense factor on this process, gathered from every rank's
+// storage (a documented N^2 copy for the calls that need the whole factor: posterior covariance,
+// core matrix): the strictly-lower blocks of L into A (np x np, column-major, ld) and Linv.
+template <typename T>
+void dist_gather_factor(DistEngineBase* eng, T* A, int64_t ld, T* Linv, hipStream_t s);
+// After an LML-mode fit: this process's ranks' gradient partials of
+// sum over the lower tiles of their own row blocks of (alpha alpha^T - C) o dK/dp (k_pairs.hip),
+// summed over the ranks into acc (device, MAX_LEAF * 3 doubles).  C tiles from the storage.
+template <typename T>
+void dist_lml_grad(DistEngineBase* eng, const KCanon<T>& K, const KCanon<T>* Kd, const T* X, int64_t n, int d,
+                   const T* FU, const T* FV, T* GU, T* GV, int64_t nf, const T* alpha, double* part, double* acc,
+                   hipStream_t s);
+// The rows this process's ranks own (row blocks of 128, the label block excluded), ascending.
+std::vector<int> dist_own_blocks(DistEngineBase* eng);
+// Sum over the ranks of `count` doubles in device memory (no-op for virtual ranks).
 void dist_allreduce_sum(DistEngineBase* eng, double* dev, int count, hipStream_t s);
+
+// ---- the sharded solves and reductions (k_dsolve.hip), one launch per rank ----------------
+template <typename T>
+struct DSArgs {
+    int g, r, nc, m;
+    const int* own;        // [nc + 1] owner of each row block (the label block last)
+    const int* loc;        // [nr] local index of an own row block
+    const int64_t* roff;   // [nloc] element offset of local row block li in the packed storage
+    const T* store;        // this rank's packed row blocks (tile (i, k) at roff[loc[i]] + k DB^2)
+    const int* orows;      // this rank's matrix row blocks (< nc), ascending
+    int nown;
+    const int* last_of;    // [g] last matrix row block of each rank (-1: none)
+    int last_own;
+    const T* Linv;         // this rank's diagonal-block inverses (all nc)
+    const uint64_t* mb;    // [g] mailbox bases as mapped here
+    int64_t o_ztile, o_alpha, o_zf, o_part, o_fflags, o_sflags;  // mailbox byte offsets
+    int zmode;             // back substitution's z: 0 the label tiles (fit), 1 the z area (forward solve)
+    const T* rhs;          // forward substitution: np x m, row-major
+    unsigned fit_ep, sep;  // epochs of the fit (label tiles) and of this solve
+    int* ctl;              // [4] ticket, error (zeroed per launch)
+    int* info;             // atomicMin -1 on a timed-out wait
+    long long tlimit;
+};
+template <typename T>
+void launch_dist_back(const DSArgs<T>& a, hipStream_t s);
+template <typename T>
+void launch_dist_forward(const DSArgs<T>& a, hipStream_t s);
+template <typename T>
+void launch_dist_reduce(const DSArgs<T>& a, int64_t n, double* out, hipStream_t s);
 
 }  // namespace gprx

@@ -409,35 +409,56 @@ struct TileBuild {
     int* flag;
     int mode;
 };
-// Distributed tile factorisation (k_ptiles.hip, potrf_tiles_kernel<T, true>): this rank's
-// view of a factorisation whose row blocks are dealt cyclically over g ranks (row block i on
-// rank i mod g).  Device copy, read per task.  Tiles of rows owned elsewhere arrive packed
-// (128 x 128, ld DB) through the panel exchange; the inverse diagonal blocks through the
-// broadcast.  Counters the host reads (hdiag, hsend) are in coherent host memory, those the
-// transport writes (drecv, precv) in uncached device memory.  The kernel only stores to the
-// host-visible words (no atomics over PCIe).
+// Distributed tile factorisation (k_ptiles.hip, potrf_tiles_kernel<T, true>; gprx_dist.cpp):
+// this rank's view of a factorisation whose row blocks are dealt over g ranks in groups of gb
+// (row block i on rank (i / gb) mod g).  Device copy, read per task.
+//
+// Storage: a rank keeps only the LOWER part of its own row blocks, packed -- row block i's
+// tiles (i, j), j = 0..i (the label row block nc: j < nc), contiguous 128 x 128 column-major
+// tiles (ld DB) from element roff[loc[i]]; the identity row blocks of the inverse (LML mode,
+// E_a = nc + 1 + a) keep their tiles (E_a, b), b = a..nc-1, then the C tiles (E_a, E_c), c <= a.
+//
+// Exchange: no host in the loop.  Every rank has a MAILBOX (one device allocation, the same
+// byte offsets on every rank, mapped into every peer: the same process for virtual ranks,
+// hipIpcOpenMemHandle across processes).  A producing task pushes its final tile straight into
+// the window slot of each rank that consumes the row -- slot (b mod ww, row j) -- and raises that
+// rank's per-tile flag; a diagonal task pushes Linv_k into every rank's Linv array.  Flags hold
+// the fit's epoch (no reset between fits).  A window slot is reused for panel b + ww only after
+// every consumer released panel b: a rank counts its completed window-reading updates per panel
+// (ucnt) and, at the last one, stores its release flag into every peer's mailbox.
 template <typename T>
 struct PtDist {
-    int g, r;
-    const int* loc;          // [nr] local row block of row block i, -1 if owned elsewhere
-    const T* const* tptr;    // [nr * nc] received tile (i, b) of a row owned elsewhere
-    T* const* sptr;          // [nr * nc] send slot of this rank's final tile (i, b)
-    unsigned* hdiag;         // [nc] set to 1 when Linv_k (slot k of Linv) is final here
-    unsigned* hslot;         // [nr * nc] set to 1 when tile (i, b) is in its send slot
-    const unsigned* drecv;   // Linv_k present for every k < *drecv
-    const unsigned* precv;   // every tile of panels b < *precv received
+    int g, r, nc, nr, ww;      // ranks, this rank, column blocks, row blocks, window panels
+    int nci;                   // column blocks of the counter array (nc, or 2 nc with C tiles)
+    unsigned ep;               // this fit's epoch (flag value)
+    const int* loc;            // [nr] local index of row block i, -1 if owned elsewhere
+    const int64_t* roff;       // [nloc] element offset of local row block li in the storage
+    const int* own;            // [nr] owner rank of row block i
+    const uint64_t* tptr;      // [nr * nc] window address (this rank) of remote tile (j, b)
+    const unsigned char* cons; // [g * nr] rank q consumes the tiles of row block j
+    const int* need;           // [g * nc] window-reading update chunks of rank q covering panel p
+    int* ucnt;                 // [nc] this rank's completed window-reading chunks per panel (local)
+    const uint64_t* mb;        // [g] mailbox base of every rank (as mapped in this process)
+    // mailbox byte offsets (the same on every rank)
+    int64_t o_linv, o_win, o_z, o_flags;
+    // flag words in the mailbox (unsigned, from o_flags): tile (j, b) received at
+    // [F_TILE + j * nc + b], Linv_k at [F_LINV(nr, nc) + k], panel p released by rank q at
+    // [F_REL(nr, nc) + q * nc + p]
 };
+constexpr int64_t dist_f_tile() { return 0; }
+constexpr int64_t dist_f_linv(int nr, int nc) { return (int64_t)nr * nc; }
+constexpr int64_t dist_f_rel(int nr, int nc) { return (int64_t)nr * nc + nc; }
 
 // One rank's launch of the distributed tile factorisation (k_ptiles.hip).  ctr: C_NCTL +
-// nr + nr * nc ints, zeroed (ver = -1 for the tiles the launch builds) by the caller.
+// nr + nr * nci ints, zeroed (ver = -1 for the tiles the launch builds; the identity rows'
+// counters start at their first column) by the caller.
 template <typename T>
 struct DistLaunch {
-    T* A;
-    int64_t ld;
-    T* Linv;
+    T* A;              // packed storage of this rank's row blocks (ld DB)
+    T* Linv;           // nc diagonal-block inverses (this rank's mailbox)
     int* info;
     const int4* list;
-    int ntasks, nc, nr;
+    int ntasks, nc, nr, nci;
     int* ctr;
     const TileBuild<T>* tb_dev;
     const PtDist<T>* dist_dev;
@@ -447,8 +468,18 @@ struct DistLaunch {
     int* dbg;          // optional: per-workgroup {ticket, phase, i, j} in coherent host memory
     long long* trace;  // optional: 4 * (ntasks + 2 nc) words, as GPRX_PT_TRACE (k_ptiles.hip)
 };
-// Per-rank ticket lists of the distributed factorisation (row block i on rank (i / gb) mod g).
-std::vector<std::vector<int4>> potrf_dist_schedule(int nc, int nr, int P, int g, int gb, bool build, double* est_us);
+// The simulated schedule of a distributed factorisation: per-rank ticket lists (in start
+// order of one list-schedule simulation of all ranks, window flow control included), the
+// window-reading chunks per (rank, panel), and the predicted makespan.  ni > 0: nc identity
+// row blocks ride along (U = L^{-T}) plus the lower C = U U^T tiles (LML mode).
+struct DistSched {
+    std::vector<std::vector<int4>> lists;
+    std::vector<int> need;            // [g * nc]
+    std::vector<unsigned char> cons;  // [g * nr]: rank q reads row block j through its window
+    double est_us = 0;
+    int W = 0;              // update chunk width used
+};
+DistSched potrf_dist_schedule(int nc, int g, int gb, int ww, int P, bool build, bool inv);
 template <typename T>
 void potrf_tiles_dist_launch(const DistLaunch<T>& L);
 
@@ -462,7 +493,8 @@ int64_t pairs_grad_feature_cols(const KCanon<T>& K, int d);
 template <typename T>
 void launch_lml_grad_mma(const KCanon<T>& K, const KCanon<T>* Kd, const T* X, int64_t n, int d, const T* FU,
                          const T* FV, T* GU, T* GV, int64_t nf, const T* alpha, const T* C, int64_t ldc, double* part,
-                         double* acc, hipStream_t s, int og = 1, int orank = 0, int ogb = 1);  // og > 1: rank orank's rows
+                         double* acc, hipStream_t s,
+                         const uint64_t* ctab = nullptr);  // ctab: C tile (i, j) pointers of a sharded fit (gprx_dist.cpp)
 // Rectangular form for the sparse likelihood (k_pairs.hip): acc[3 l + q] = sum over the
 // na x nb pairs (xa_i, xb_j) of (a_i b_j - C_ij) d leaf_l / d p_q.
 template <typename T>
@@ -586,5 +618,9 @@ void launch_residual_rows(const double* Y, const double* Kx, const double* a, do
                           int64_t ld, int64_t row0, int64_t ncols, int mp, hipStream_t s);
 void launch_refine_accumulate(const float* delta, double* a, float* alpha, int64_t e, unsigned long long* nrm,
                               hipStream_t s);
+// the sharded refinement: the rows this process's ranks own (idx, q of them)
+void launch_gather_rows(const double* X, const int64_t* idx, int64_t q, int d, double* out, hipStream_t s);
+void launch_residual_scatter(const double* Y, const double* Kx, const double* a, double s2, const int64_t* idx,
+                             int64_t q, int m, float* rhs, hipStream_t s);
 
 }  // namespace gprx

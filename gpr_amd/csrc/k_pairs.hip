@@ -345,9 +345,9 @@ __global__ __launch_bounds__(NT) void grad_mma_kernel(const KCanon<T>* __restric
                                                       const T* __restrict__ FV, const T* __restrict__ GU,
                                                       const T* __restrict__ GV, int64_t nf, int Kr, int Kp, int Kf,
                                                       T hd, const T* __restrict__ alpha, const T* __restrict__ C,
-                                                      int64_t ldc, int64_t n, double* __restrict__ part, int og,
-                                                      int orank, int ogb, int64_t nfv = 0, int64_t ncol = 0,
-                                                      const T* __restrict__ beta = nullptr) {
+                                                      int64_t ldc, int64_t n, double* __restrict__ part,
+                                                      const uint64_t* __restrict__ ctab, int64_t nfv = 0,
+                                                      int64_t ncol = 0, const T* __restrict__ beta = nullptr) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     T* smem = reinterpret_cast<T*>(smem_raw);
     double* sacc = reinterpret_cast<double*>(smem_raw + gemm_lds<T>());  // [8 waves][MAX_LEAF * 3]
@@ -366,11 +366,17 @@ __global__ __launch_bounds__(NT) void grad_mma_kernel(const KCanon<T>* __restric
     }
     const int64_t nv_ = CROSS ? nfv : nf, ncol_ = CROSS ? ncol : n;
     const T* __restrict__ bvec = CROSS ? beta : alpha;
-    // a distributed context's share: only the tiles of row blocks rank `orank` owns (row block
-    // i on rank (i / ogb) mod og, gprx_dist.cpp); the others contribute zero
-    if (!CROSS && og > 1 && (ti / ogb) % og != orank) {
-        if (threadIdx.x < MAX_LEAF * 3) part[(int64_t)blockIdx.x * MAX_LEAF * 3 + threadIdx.x] = 0.0;
-        return;
+    // a distributed context's share (gprx_dist.cpp): C tile (ti, tj) from the rank's packed
+    // storage, stored negated (the C = U U^T chunks accumulate C -= U U^T), or 0 when row block
+    // ti is another rank's -- that tile contributes zero here
+    const T* __restrict__ ct = nullptr;
+    if (!CROSS && ctab) {
+        const uint64_t pv = ctab[ti * (nf / GT) + tj];
+        if (!pv) {
+            if (threadIdx.x < MAX_LEAF * 3) part[(int64_t)blockIdx.x * MAX_LEAF * 3 + threadIdx.x] = 0.0;
+            return;
+        }
+        ct = reinterpret_cast<const T*>(pv);
     }
     const int64_t i0 = ti * GT, j0 = tj * GT;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -402,7 +408,8 @@ __global__ __launch_bounds__(NT) void grad_mma_kernel(const KCanon<T>* __restric
                 const int64_t gi = gi_of(y);
                 const bool in = gi < n && gj < ncol_ && (CROSS || gi >= gj);
                 const int64_t ci = in ? gi : 0, cj = in ? gj : 0;
-                const T v = alpha[ci] * bvec[cj] - C[ci + cj * ldc];
+                const T cv = ct ? -ct[in ? (gi - i0) + (gj - j0) * DB : 0] : C[ci + cj * ldc];
+                const T v = alpha[ci] * bvec[cj] - cv;
                 wt[x][y][reg] = in ? (CROSS ? v : v * (gi == gj ? T(1) : T(2))) : T(0);
             }
         });
@@ -661,7 +668,7 @@ int64_t pairs_grad_feature_cols(const KCanon<T>& K, int d) {
 template <typename T>
 void launch_lml_grad_mma(const KCanon<T>& K, const KCanon<T>* Kd, const T* X, int64_t n, int d, const T* FU,
                          const T* FV, T* GU, T* GV, int64_t nf, const T* alpha, const T* C, int64_t ldc, double* part,
-                         double* acc, hipStream_t s, int og, int orank, int ogb) {
+                         double* acc, hipStream_t s, const uint64_t* ctab) {
     const int Kr = pr::kr_of(K, d), Kp = pr::kp_of(K, d), Kf = (int)pairs_grad_feature_cols(K, d);
     if (K.nper) {
         const dim3 g((unsigned)((nf + 255) / 256));
@@ -676,7 +683,7 @@ void launch_lml_grad_mma(const KCanon<T>& K, const KCanon<T>* Kd, const T* X, in
     auto go = [&](auto kfn) {
         GPRX_HIP(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         hipLaunchKernelGGL(kfn, grid, dim3(mm::NT), lds, s, Kd, FU, FV, (const T*)GU, (const T*)GV, nf, Kr, Kp, Kf,
-                           T(0.5) * T(d), alpha, C, ldc, n, part, og, orank, ogb > 1 ? ogb : 1, nf, n, alpha);
+                           T(0.5) * T(d), alpha, C, ldc, n, part, ctab, nf, n, alpha);
     };
     if (K.nper && K.need_r2) go(pr::grad_mma_kernel<T, 1, true>);
     else if (K.nper) go(pr::grad_mma_kernel<T, 1, false>);
@@ -713,7 +720,7 @@ void launch_lml_grad_mma_cross(const KCanon<T>& K, const KCanon<T>* Kd, const T*
     auto go = [&](auto kfn) {
         GPRX_HIP(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         hipLaunchKernelGGL(kfn, dim3((unsigned)ntiles), dim3(mm::NT), lds, s, Kd, FU, FV, (const T*)GU, (const T*)GV,
-                           nfu, Kr, Kp, Kf, T(0.5) * T(d), a, C, ldc, na, part, 1, 0, 1, nfv, nb, b);
+                           nfu, Kr, Kp, Kf, T(0.5) * T(d), a, C, ldc, na, part, (const uint64_t*)nullptr, nfv, nb, b);
     };
     if (K.nper && K.need_r2) go(pr::grad_mma_kernel<T, 1, true, true>);
     else if (K.nper) go(pr::grad_mma_kernel<T, 1, false, true>);
@@ -756,7 +763,7 @@ TileBuild<T> pairs_tile_build(const KCanon<T>& K, const KCanon<T>* Kd, const T* 
                                                hipStream_t);                                                      \
     template void launch_lml_grad_mma<T>(const KCanon<T>&, const KCanon<T>*, const T*, int64_t, int, const T*, \
                                          const T*, T*, T*, int64_t, const T*, const T*, int64_t, double*,     \
-                                         double*, hipStream_t, int, int, int);                                \
+                                         double*, hipStream_t, const uint64_t*);                                \
     template TileBuild<T> pairs_tile_build<T>(const KCanon<T>&, const KCanon<T>*, const T*, const T*, int64_t, int, \
                                               int64_t, T, int*);                                              \
     template bool pairs_mma_supported<T>(const KCanon<T>&, int);                                              \

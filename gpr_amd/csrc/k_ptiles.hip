@@ -65,14 +65,12 @@ static_assert(C_NCTL == C_NCTL_DIST, "counter block layout shared with gprx_dist
 // lower triangular (K = 128, a diagonal-block inverse): output columns 32 wc .. 32 wc + 31
 // need only k < 32 wc + 32, the waves skip the MFMAs of the zero part.
 // ------------------------------------------------------------------------------------------
-// Bpan: B by 128-column panels (tile_mma); C2 (optional, TRSM only): a second copy of the
-// result, packed 128 x 128 (ld DB) -- the distributed factorisation's send slot.
+// Bpan: B by 128-column panels (tile_mma): the distributed factorisation's window tiles.
 // MAP: the wave -> output-block map (k_mma.h wave_block): 1 for triangular B, 2 for lower.
 template <typename T, bool UPDATE, int MAP = 0>
 __device__ __forceinline__ void tile_gemm(T* __restrict__ C, int64_t ldc, const T* __restrict__ A, int64_t lda,
                                           const T* __restrict__ B, int64_t ldb, int K, bool lower, T* smem,
-                                          const int t, bool tri = false, const uint64_t* Bpan = nullptr,
-                                          T* __restrict__ C2 = nullptr) {
+                                          const int t, bool tri = false, const uint64_t* Bpan = nullptr) {
     typedef Mfma<T> Tr;
     typedef typename Tr::acc_t acc_t;
     const int lane = t & 63, w = t >> 6;
@@ -114,7 +112,6 @@ __device__ __forceinline__ void tile_gemm(T* __restrict__ C, int64_t ldc, const 
                     st_sc1(ccol + il, (lower && il < jl) ? cv[x][y][reg] : cv[x][y][reg] - acc[x][y][reg]);
                 else if (!lower || il >= jl)
                     st_sc1(ccol + il, acc[x][y][reg]);
-                if (!UPDATE && C2) st_sc1(C2 + il + (int64_t)jl * DB, acc[x][y][reg]);
             }
         }
     }
@@ -1181,6 +1178,7 @@ struct Args {
     const int4* tasks;
     int ntasks;
     int nc;        // column blocks (= diagonal blocks)
+    int nv;        // columns of the ver counter array (nc; 2 nc with the C tiles of DIST LML mode)
     int* ctl;      // [C_NCTL] control words, then lcnt[nr], then ver[nr * nc]
     int* lcnt;
     int* ver;
@@ -1200,9 +1198,125 @@ struct Args {
 // are made wave-uniform, so the loop is a scalar loop with no divergence).  Returns false on
 // timeout or when another workgroup raised the error flag.
 __device__ __forceinline__ int ld_uni(const int* p) { return __builtin_amdgcn_readfirstlane(ld_agent(p)); }
-// counters written by the transport (stream memory ops into uncached memory): system scope
-__device__ __forceinline__ int ld_sys_uni(const unsigned* p) {
-    return __builtin_amdgcn_readfirstlane((int)__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+// flag words another rank stores into this rank's mailbox: system scope
+__device__ __forceinline__ unsigned ld_sys(const unsigned* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void st_sys(unsigned* p, unsigned v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// ---- distributed factorisation (DIST): packed storage, mailbox pushes -----------------------
+// tile (i, j) of this rank's own row block i in the packed storage (ld DB): matrix / label rows
+// keep columns 0..i, identity row E_a = nc + 1 + a columns a..nc-1, then C columns E_0..E_a
+template <typename T>
+__device__ __forceinline__ T* dist_tile(T* A, const PtDist<T>& D, int i, int j) {
+    const int li = __builtin_amdgcn_readfirstlane(D.loc[i]);
+    int col = j;
+    if (i > D.nc) {
+        const int aa = i - D.nc - 1;
+        col = (j < D.nc) ? j - aa : D.nc - aa + (j - D.nc - 1);
+    }
+    const int64_t ro = D.roff[li];
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)ro), hi = __builtin_amdgcn_readfirstlane((uint32_t)(ro >> 32));
+    return A + (int64_t)(((uint64_t)hi << 32) | lo) + (int64_t)col * DB * DB;
+}
+// counter column of tile (i, j): the C tiles (j = E_c) after the nc matrix columns
+__device__ __forceinline__ int dist_col(int nc, int j) { return j > nc ? j - 1 : j; }
+
+template <typename T>
+__device__ __forceinline__ unsigned* dist_flags(const PtDist<T>& D, int q) {
+    const uint64_t b = D.mb[q] + (uint64_t)D.o_flags;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b), hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+    return reinterpret_cast<unsigned*>(((uint64_t)hi << 32) | lo);
+}
+template <typename T>
+__device__ __forceinline__ char* dist_mb(const PtDist<T>& D, int q, int64_t off) {
+    const uint64_t b = D.mb[q] + (uint64_t)off;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b), hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+    return reinterpret_cast<char*>(((uint64_t)hi << 32) | lo);
+}
+
+// ranks other than r that consume row block j (bit q)
+template <typename T>
+__device__ __forceinline__ unsigned dist_consumers(const PtDist<T>& D, int j) {
+    unsigned m = 0;
+    for (int q = 0; q < D.g; q++)
+        if (q != D.r && D.cons[(int64_t)q * D.nr + j]) m |= 1u << q;
+    return __builtin_amdgcn_readfirstlane(m);
+}
+
+// Wave 0: wait until every rank in `mask` released panel p (its window slot may be refilled);
+// ranks with no window-reading chunk on p never store the flag and are not waited for.
+template <typename T>
+__device__ bool dist_wait_release(const Args<T>& a, const PtDist<T>& D, unsigned mask, int p) {
+    if (p < 0) return true;
+    const unsigned* fl = dist_flags(D, D.r) + dist_f_rel(D.nr, D.nc);
+    const long long t0 = wall_clock64();
+    for (int q = 0; q < D.g; q++) {
+        if (!((mask >> q) & 1) || __builtin_amdgcn_readfirstlane(D.need[(int64_t)q * D.nc + p]) == 0) continue;
+        while (__builtin_amdgcn_readfirstlane(ld_sys(fl + (int64_t)q * D.nc + p)) != D.ep) {
+            if (ld_uni(a.ctl + C_ERR)) return false;
+            if (wall_clock64() - t0 > a.tlimit) {
+                st_agent(a.ctl + C_ERR, 1);
+                return false;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+    }
+    return true;
+}
+
+// The whole workgroup: copy one DB x DB tile (contiguous, written by this workgroup and
+// drained: its stores are visible to this CU) to byte offset `off` of the mailbox of every
+// rank in `mask`, then release (system scope) and set each one's flag word `fidx` to the epoch.
+template <typename T>
+__device__ void dist_push(const T* src, const PtDist<T>& D, unsigned mask, int64_t off, int64_t fidx, const int t) {
+    if (!mask) return;
+    typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+    constexpr int NV = DB * DB * (int)sizeof(T) / 16 / NT;  // 16-byte vectors per thread
+    constexpr int CH = 4;
+    if (wave_id() == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // this CU's L1: no stale lines of src
+    __syncthreads();
+    const u4* s4 = reinterpret_cast<const u4*>(src);
+#pragma unroll
+    for (int c = 0; c < NV; c += CH) {
+        u4 v[CH];
+#pragma unroll
+        for (int u = 0; u < CH; u++) v[u] = s4[t + (c + u) * NT];
+        for (int q = 0; q < D.g; q++) {
+            if (!((mask >> q) & 1)) continue;
+            u4* d4 = reinterpret_cast<u4*>(dist_mb(D, q, off));
+#pragma unroll
+            for (int u = 0; u < CH; u++) d4[t + (c + u) * NT] = v[u];
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (wave_id() == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        for (int q = 0; q < D.g; q++)
+            if ((mask >> q) & 1) st_sys(dist_flags(D, q) + fidx, D.ep);
+    }
+}
+
+// Wave 0 of an update that read row j from the window: count the chunk on its panels; the
+// chunk completing a panel's count stores the release flag into every other rank's mailbox.
+template <typename T>
+__device__ void dist_release(const PtDist<T>& D, int b0, int nb) {
+    const int lane = threadIdx.x & 63;
+    const int p = b0 + (lane < nb ? lane : 0);
+    const int old = __hip_atomic_fetch_add(D.ucnt + p, lane < nb ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool done = lane < nb && old + 1 == D.need[(int64_t)D.r * D.nc + p];
+    uint64_t m = __builtin_amdgcn_read_exec() & __ballot(done);
+    m = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(m >> 32)) << 32) | __builtin_amdgcn_readfirstlane((uint32_t)m);
+    while (m) {
+        const int l = __builtin_ctzll(m);
+        m &= m - 1;
+        for (int q = 0; q < D.g; q++)
+            if (q != D.r) st_sys(dist_flags(D, q) + dist_f_rel(D.nr, D.nc) + (int64_t)D.r * D.nc + b0 + l, D.ep);
+    }
 }
 
 template <typename T, bool DIST>
@@ -1215,9 +1329,11 @@ __device__ bool wait_inputs(const Args<T>& a, int type, int i, int j, int b0, in
     int lwant1;
     const int* lp2;
     int lwant2;
-    // DIST: one dependency may be data of another rank, a transport counter instead
+    // DIST: one dependency may be data of another rank: its flag words in this rank's mailbox
+    // (Linv_k: one word; the tiles of a remote row: one word per panel of the chunk)
     const unsigned* rp = nullptr;
-    int rwant = 0;
+    int rn = 0;
+    unsigned ep = 0;
     if (type == T_DIAGX && i == 0) {  // the first diagonal tile is built
         vp = a.ver;
         vwant = 0;
@@ -1230,24 +1346,26 @@ __device__ bool wait_inputs(const Args<T>& a, int type, int i, int j, int b0, in
     } else if (type == T_BUILD) {
         return true;
     } else if (type == T_DIAGX) {
-        vp = a.ver + (int64_t)i * a.nc + (i - 1);
+        vp = a.ver + (int64_t)i * a.nv + (i - 1);
         vwant = i - 1;
-        vp2 = a.ver + (int64_t)i * a.nc + i;
+        vp2 = a.ver + (int64_t)i * a.nv + i;
         vwant2 = i - 1;
         lp1 = a.lcnt + (i - 1);
         lwant1 = i;
         lp2 = lp1;
         lwant2 = lwant1;
         if constexpr (DIST) {
-            if (__builtin_amdgcn_readfirstlane(a.dist->loc[i - 1]) < 0) {  // Linv_{i-1} is broadcast
+            const PtDist<T>& D = *a.dist;
+            if (__builtin_amdgcn_readfirstlane(D.loc[i - 1]) < 0) {  // Linv_{i-1} pushed by its rank
                 lp1 = lp2 = a.lcnt + i;
                 lwant1 = lwant2 = 0;
-                rp = a.dist->drecv;
-                rwant = i;
+                rp = dist_flags(D, D.r) + dist_f_linv(D.nr, D.nc) + (i - 1);
+                rn = 1;
+                ep = D.ep;
             }
         }
     } else if (type == T_TRSM) {
-        vp = a.ver + (int64_t)i * a.nc + j;
+        vp = a.ver + (int64_t)i * a.nv + j;
         vwant = j;
         vp2 = vp;
         vwant2 = vwant;
@@ -1256,15 +1374,18 @@ __device__ bool wait_inputs(const Args<T>& a, int type, int i, int j, int b0, in
         lp2 = lp1;
         lwant2 = lwant1;
         if constexpr (DIST) {
-            if (__builtin_amdgcn_readfirstlane(a.dist->loc[j]) < 0) {  // Linv_j is broadcast
+            const PtDist<T>& D = *a.dist;
+            if (__builtin_amdgcn_readfirstlane(D.loc[j]) < 0) {  // Linv_j pushed by its rank
                 lp1 = lp2 = a.lcnt + i;
                 lwant1 = lwant2 = 0;
-                rp = a.dist->drecv;
-                rwant = j + 1;
+                rp = dist_flags(D, D.r) + dist_f_linv(D.nr, D.nc) + j;
+                rn = 1;
+                ep = D.ep;
             }
         }
     } else {
-        vp = a.ver + (int64_t)i * a.nc + j;
+        const int jc = DIST ? dist_col(a.dist->nc, j) : j;
+        vp = a.ver + (int64_t)i * a.nv + jc;
         vwant = b0;
         vp2 = vp;
         vwant2 = vwant;
@@ -1273,20 +1394,26 @@ __device__ bool wait_inputs(const Args<T>& a, int type, int i, int j, int b0, in
         lp2 = a.lcnt + j;
         lwant2 = b0 + nb;
         if constexpr (DIST) {
-            if (__builtin_amdgcn_readfirstlane(a.dist->loc[j]) < 0) {  // row j's tiles arrive with the panels
+            const PtDist<T>& D = *a.dist;
+            if (__builtin_amdgcn_readfirstlane(D.loc[j]) < 0) {  // row j's tiles: pushed, one flag per panel
                 lp2 = lp1;
-                rp = a.dist->precv;
-                rwant = b0 + nb;
+                rp = dist_flags(D, D.r) + dist_f_tile() + (int64_t)j * D.nc + b0;
+                rn = nb;
+                ep = D.ep;
             }
         }
     }
+    const int lane = threadIdx.x & 63;
     const long long t0 = wall_clock64();
     for (;;) {
         // bitwise: all four loads are issued before any compare resolves
         int ok = int(ld_uni(vp) == vwant) & int(ld_uni(vp2) == vwant2) & int(ld_uni(lp1) >= lwant1) &
                  int(ld_uni(lp2) >= lwant2);
         if constexpr (DIST) {
-            if (rp) ok &= int(ld_sys_uni(rp) >= rwant);
+            if (rp) {  // lane l checks flag l (l < rn): one vector load, one ballot
+                const bool good = lane >= rn || ld_sys(rp + (lane < rn ? lane : 0)) == ep;
+                ok &= int(__builtin_amdgcn_readfirstlane((uint32_t)(__ballot(!good) == 0)));
+            }
         }
         if (ok) return true;
         if (ld_uni(a.ctl + C_ERR)) return false;
@@ -1298,30 +1425,19 @@ __device__ bool wait_inputs(const Args<T>& a, int type, int i, int j, int b0, in
     }
 }
 
-// DIST: a host-visible flag = 1 after every wave's stores (sc1 or plain) reached memory
-// (system-scope release: the transport reads them from another agent)
-__device__ __forceinline__ void publish_host(unsigned* p) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (wave_id() == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-}
-
 // DIAGX(k > 0)'s two products before the diagonal factor, with the result left in the
 // factor's LDS image (f64, diag_factor_la):
 //   T = A_{k,k-1} Linv_{k-1}^T  on the staging ring (triangular B, MAP 1), stored to HBM as
-//       L_{k,k-1} (+ the distributed send slot) AND into the LDS image as an operand;
+//       L_{k,k-1} AND into the LDS image as an operand;
 //   A_kk - T T^T  with both fragments read from that image (no second HBM round trip, no
 //       ring fill), the diagonal tile's lower 16 x 16 tiles only (MAP 2), accumulated onto
 //       A_kk itself (loaded while T is stored); the result overwrites the image (lower part).
 // Publishes L_{k,k-1} (lcnt[k] = k) after S (the two-call form published between the two).
-template <typename T, bool DIST>
+// (The distributed form pushes L_{k,k-1} to the other ranks after the diagonal factor.)
+template <typename T>
 __device__ __forceinline__ long long diagx_ts(T* __restrict__ Akm, T* __restrict__ Akk, int64_t ld,
-                                              const T* __restrict__ Lp, T* __restrict__ send, int* lflag, int k,
-                                              unsigned* hslot, T* smem, const int t, bool mark) {
+                                              const T* __restrict__ Lp, int* lflag, int k, T* smem, const int t,
+                                              bool mark) {
     typedef Mfma<T> Tr;
     typedef typename Tr::acc_t acc_t;
     const int lane = t & 63, w = t >> 6, lr = lane & 15, lk = lane >> 4;
@@ -1354,7 +1470,6 @@ __device__ __forceinline__ long long diagx_ts(T* __restrict__ Akm, T* __restrict
                 for (int y = 0; y < 4; y++) {
                     const int il = tr_ * 64 + y * 16 + lr;
                     st_sc1(Akm + il + (int64_t)jl * ld, acc[x][y][reg]);
-                    if (send) st_sc1(send + il + (int64_t)jl * DB, acc[x][y][reg]);
                     smem[il + jl * SIL] = acc[x][y][reg];
                 }
             }
@@ -1385,9 +1500,6 @@ __device__ __forceinline__ long long diagx_ts(T* __restrict__ Akm, T* __restrict
     // L_{k,k-1} final: unblocks the updates of column k.  Published after S so the HBM stores'
     // latency hides under S; its barrier is also "every read of T done" for the image below.
     publish(lflag, k, false);
-    if constexpr (DIST) {
-        if (send) publish_host(hslot);
-    }
 #pragma unroll
     for (int x = 0; x < 2; x++)
 #pragma unroll
@@ -1439,7 +1551,14 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
         if (wv == 0) {
             const bool ok0 = wait_inputs<T, DIST>(a, type, i, j, b0, nb);
             if (ok0 && !(a.variant & 32)) {
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                bool remote = false;  // DIST: an input pushed by another rank (system-scope acquire)
+                if constexpr (DIST) {
+                    const PtDist<T>& D = *a.dist;
+                    const int dep = (type == T_DIAGX) ? i - 1 : (type == T_BUILD ? -1 : j);
+                    remote = dep >= 0 && __builtin_amdgcn_readfirstlane(D.loc[dep]) < 0;
+                }
+                if (remote) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+                else __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
             s_ok = ok0 ? 1 : 0;
@@ -1453,56 +1572,115 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
         // task instead of hoisted (and held in registers) across the whole task loop
         int tid = t;
         asm volatile("" : "+v"(tid));
-        // row block i of this rank's storage (DIST: only the rank's own row blocks are stored)
-        int li = i;
-        if constexpr (DIST) li = __builtin_amdgcn_readfirstlane(a.dist->loc[i]);
-        T* Ci = a.A + (int64_t)li * GT;  // row block i, column 0
+        if constexpr (DIST) {
+            // ---- one rank of the distributed factorisation: packed own rows (ld DB), remote
+            // rows from the window, final tiles pushed to their consumers' mailboxes ----------
+            const PtDist<T>& D = *a.dist;
+            bool ok = true;
+            if (type == T_BUILD) {
+                const TileBuild<T>& b = *a.tb;
+                T* tij = dist_tile(a.A, D, i, j);
+                // build_tile_sum addresses element (gi, gj) at base + gi + gj ld (global indices)
+                const bool bad = pr::build_tile_sum<T, 1, true>(
+                    b.Kd, b.FU, b.FV, b.nf, b.Kr, b.Kp, b.hd, tij - (int64_t)i * GT - (int64_t)j * GT * DB, DB, b.n,
+                    b.sigma2, (int64_t)i * GT, (int64_t)j * GT, smem, tid);
+                if (__builtin_amdgcn_readfirstlane(__any(bad))) atomicOr(b.flag, 1);
+                publish(a.ver + (int64_t)i * a.nv + j, 0, false);
+            } else if (type == T_UPD) {
+                // row j of this rank: its stored tiles; of another rank: the window, one tile per
+                // panel (one call site: two inlined mainloops crashed hipcc 7.2)
+                const int lj = __builtin_amdgcn_readfirstlane(D.loc[j]);
+                const bool loc = lj >= 0;
+                const T* Bop = loc ? dist_tile(a.A, D, j, b0) : nullptr;
+                const uint64_t* bp = loc ? nullptr : D.tptr + (int64_t)j * D.nc + b0;
+                tile_gemm<T, true>(dist_tile(a.A, D, i, j), DB, dist_tile(a.A, D, i, b0), DB, Bop, DB, nb * GT, i == j,
+                                   smem, tid, false, bp);
+                publish(a.ver + (int64_t)i * a.nv + dist_col(D.nc, j), b0 + nb, false);
+                if (!loc && wv == 0) dist_release(D, b0, nb);  // this chunk's window reads are done
+            } else if (type == T_TRSM) {
+                T* Cik = dist_tile(a.A, D, i, j);
+                tile_gemm<T, false, 1>(Cik, DB, Cik, DB, a.Linv + (int64_t)j * DB * DB, DB, GT, false, smem, tid, true);
+                publish(a.lcnt + i, j + 1, false);
+                if (i == D.nc) {  // the label rows z^T: every other rank's z area (the solves read it)
+                    const unsigned all = ((1u << D.g) - 1u) & ~(1u << D.r);
+                    dist_push(Cik, D, all, D.o_z + (int64_t)j * DB * DB * (int64_t)sizeof(T),
+                              dist_f_tile() + (int64_t)i * D.nc + j, tid);
+                } else {
+                    const unsigned cm = dist_consumers(D, i);
+                    if (wv == 0) ok = dist_wait_release(a, D, cm, j - D.ww);
+                    if (wv == 0) s_ok = ok ? 1 : 0;
+                    __syncthreads();
+                    ok = __builtin_amdgcn_readfirstlane(s_ok) != 0;
+                    if (ok)
+                        dist_push(Cik, D, cm, D.o_win + ((int64_t)(j % D.ww) * D.nr + i) * DB * DB * (int64_t)sizeof(T),
+                                  dist_f_tile() + (int64_t)i * D.nc + j, tid);
+                }
+            } else {  // DIAGX(k = i)
+                const int k = i;
+                T* Akk = dist_tile(a.A, D, k, k);
+                T* Akm = k > 0 ? dist_tile(a.A, D, k, k - 1) : nullptr;
+                constexpr bool fused_ts = std::is_same<T, double>::value && DIAG_LA;
+                if (fused_ts && k > 0) {
+                    diagx_ts<T>(Akm, Akk, DB, a.Linv + (int64_t)(k - 1) * DB * DB, a.lcnt + k, k, smem, tid, false);
+                } else if (k > 0) {
+                    tile_gemm<T, false, 1>(Akm, DB, Akm, DB, a.Linv + (int64_t)(k - 1) * DB * DB, DB, GT, false, smem,
+                                           tid, true);
+                    publish(a.lcnt + k, k, false);
+                    tile_gemm<T, true, 2>(Akk, DB, Akm, DB, Akm, DB, GT, true, smem, tid);
+                    local_sync();
+                }
+                diag_factor<T>(Akk, DB, a.Linv + (int64_t)k * DB * DB, a.info, (int64_t)k * DB, smem_raw, tid, a.dbg,
+                               nullptr, fused_ts && k > 0);
+                publish(a.lcnt + k, k + 1, !(std::is_same<T, double>::value && DIAG_LA));
+                // pushes after the local publication (this rank's chain goes on meanwhile): the
+                // next diagonal step's rank first, L_{k,k-1} before Linv_k
+                const unsigned cm = k > 0 ? dist_consumers(D, k) : 0u;
+                const unsigned all = ((1u << D.g) - 1u) & ~(1u << D.r);
+                const int nx = (k + 1 < D.nc) ? __builtin_amdgcn_readfirstlane(D.own[k + 1]) : D.r;
+                const unsigned first = (nx != D.r) ? (1u << nx) : 0u;
+                if (k > 0) {
+                    if (wv == 0) ok = dist_wait_release(a, D, cm, k - 1 - D.ww);
+                    if (wv == 0) s_ok = ok ? 1 : 0;
+                    __syncthreads();
+                    ok = __builtin_amdgcn_readfirstlane(s_ok) != 0;
+                }
+                const int64_t owin = D.o_win + ((int64_t)((k - 1 + D.ww) % D.ww) * D.nr + k) * DB * DB * (int64_t)sizeof(T);
+                const int64_t olinv = D.o_linv + (int64_t)k * DB * DB * (int64_t)sizeof(T);
+                if (ok && k > 0) dist_push(Akm, D, cm & first, owin, dist_f_tile() + (int64_t)k * D.nc + (k - 1), tid);
+                if (ok) dist_push(a.Linv + (int64_t)k * DB * DB, D, all & first, olinv, dist_f_linv(D.nr, D.nc) + k, tid);
+                if (ok && k > 0) dist_push(Akm, D, cm & ~first, owin, dist_f_tile() + (int64_t)k * D.nc + (k - 1), tid);
+                if (ok) dist_push(a.Linv + (int64_t)k * DB * DB, D, all & ~first, olinv, dist_f_linv(D.nr, D.nc) + k, tid);
+            }
+            if (!ok) break;
+        } else {
+        T* Ci = a.A + (int64_t)i * GT;  // row block i, column 0
         if (type == T_BUILD) {
             // ver[i][j] goes from -1 (not built) to 0; the tile's values go out write-through
             const TileBuild<T>& b = *a.tb;
             bool bad;
             // one instantiation for every mode: an absent statistic has a zero-depth product
-            // (its accumulators stay 0) and no leaves of its class.  The features are indexed by
-            // the global row, the storage by the local one.
-            bad = pr::build_tile_sum<T, 1, true>(b.Kd, b.FU, b.FV, b.nf, b.Kr, b.Kp, b.hd,
-                                                 a.A + (int64_t)(li - i) * GT, ld, b.n, b.sigma2, (int64_t)i * GT,
-                                                 (int64_t)j * GT, smem, tid);
+            // (its accumulators stay 0) and no leaves of its class
+            bad = pr::build_tile_sum<T, 1, true>(b.Kd, b.FU, b.FV, b.nf, b.Kr, b.Kp, b.hd, a.A, ld, b.n, b.sigma2,
+                                                 (int64_t)i * GT, (int64_t)j * GT, smem, tid);
             if (__builtin_amdgcn_readfirstlane(__any(bad))) atomicOr(b.flag, 1);  // wave-uniform branch
-            publish(a.ver + (int64_t)i * a.nc + j, 0, false);
+            publish(a.ver + (int64_t)i * a.nv + j, 0, false);
         } else if (type == T_UPD) {
             // variant 64 (timing experiment, wrong results): every update streams the same
             // L2-resident operands, to separate memory-feed from MFMA limits
-            const int64_t oa = (a.variant & 64) ? 0 : (int64_t)li * GT + (int64_t)b0 * GT * ld;
-            if constexpr (DIST) {
-                // row j of this rank: its stored tiles; of another rank: its received tiles, one
-                // per panel (one call site: two inlined mainloops crashed hipcc 7.2)
-                const int lj = __builtin_amdgcn_readfirstlane(a.dist->loc[j]);
-                const bool loc = lj >= 0;
-                const T* Bop = loc ? a.A + (int64_t)lj * GT + (int64_t)b0 * GT * ld : nullptr;
-                const uint64_t* bp = loc ? nullptr : reinterpret_cast<const uint64_t*>(a.dist->tptr) + (int64_t)j * a.nc + b0;
-                tile_gemm<T, true>(Ci + (int64_t)j * GT * ld, ld, a.A + oa, ld, Bop, loc ? ld : (int64_t)DB, nb * GT,
-                                   i == j, smem, tid, false, bp);
-            } else {
-                const int64_t ob = (a.variant & 64) ? GT : (int64_t)j * GT + (int64_t)b0 * GT * ld;
-                // variant 128 (timing experiment, wrong results): operand stride 0 along k, every
-                // k-slice of the update re-reads the same 1 KB column -- a truly cache-resident feed
-                const int64_t lop = (a.variant & 128) ? 0 : ld;
-                if (!(a.variant & 2))
-                    tile_gemm<T, true>(Ci + (int64_t)j * GT * ld, ld, a.A + oa, lop, a.A + ob, lop, nb * GT, i == j,
-                                       smem, tid);
-            }
-            publish(a.ver + (int64_t)i * a.nc + j, b0 + nb, false);
+            const int64_t oa = (a.variant & 64) ? 0 : (int64_t)i * GT + (int64_t)b0 * GT * ld;
+            const int64_t ob = (a.variant & 64) ? GT : (int64_t)j * GT + (int64_t)b0 * GT * ld;
+            // variant 128 (timing experiment, wrong results): operand stride 0 along k, every
+            // k-slice of the update re-reads the same 1 KB column -- a truly cache-resident feed
+            const int64_t lop = (a.variant & 128) ? 0 : ld;
+            if (!(a.variant & 2))
+                tile_gemm<T, true>(Ci + (int64_t)j * GT * ld, ld, a.A + oa, lop, a.A + ob, lop, nb * GT, i == j, smem,
+                                   tid);
+            publish(a.ver + (int64_t)i * a.nv + j, b0 + nb, false);
         } else if (type == T_TRSM) {
             T* Cik = Ci + (int64_t)j * GT * ld;
-            T* send = nullptr;
-            if constexpr (DIST) send = a.dist->sptr[(int64_t)i * a.nc + j];
             if (!(a.variant & 1))
-                tile_gemm<T, false, 1>(Cik, ld, Cik, ld, a.Linv + (int64_t)j * DB * DB, DB, GT, false, smem, tid, true,
-                                       nullptr, send);
+                tile_gemm<T, false, 1>(Cik, ld, Cik, ld, a.Linv + (int64_t)j * DB * DB, DB, GT, false, smem, tid, true);
             publish(a.lcnt + i, j + 1, false);
-            if constexpr (DIST) {
-                if (send) publish_host(a.dist->hslot + (int64_t)i * a.nc + j);
-            }
         } else {  // DIAGX(k = i)
             const int k = i;
             T* Akk = Ci + (int64_t)k * GT * ld;
@@ -1510,26 +1688,15 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
             constexpr bool fused_ts = std::is_same<T, double>::value && DIAG_LA;
             if (fused_ts && k > 0) {
                 T* Akm = Ci + (int64_t)(k - 1) * GT * ld;
-                T* send = nullptr;
-                unsigned* hs = nullptr;
-                if constexpr (DIST) {
-                    send = a.dist->sptr[(int64_t)k * a.nc + (k - 1)];
-                    hs = a.dist->hslot + (int64_t)k * a.nc + (k - 1);
-                }
-                dt[0] = diagx_ts<T, DIST>(Akm, Akk, ld, a.Linv + (int64_t)(k - 1) * DB * DB, send, a.lcnt + k, k,
-                                          hs, smem, tid, a.trace != nullptr);
+                dt[0] = diagx_ts<T>(Akm, Akk, ld, a.Linv + (int64_t)(k - 1) * DB * DB, a.lcnt + k, k, smem, tid,
+                                    a.trace != nullptr);
                 dt[1] = dt[0];
             } else if (k > 0) {
                 T* Akm = Ci + (int64_t)(k - 1) * GT * ld;
-                T* send = nullptr;
-                if constexpr (DIST) send = a.dist->sptr[(int64_t)k * a.nc + (k - 1)];
                 tile_gemm<T, false, 1>(Akm, ld, Akm, ld, a.Linv + (int64_t)(k - 1) * DB * DB, DB, GT, false, smem,
-                                       tid, true, nullptr, send);
+                                       tid, true);
                 if (a.trace) dt[0] = wall_clock64();
                 publish(a.lcnt + k, k, false);  // L_{k,k-1} final: unblocks the updates of column k
-                if constexpr (DIST) {
-                    if (send) publish_host(a.dist->hslot + (int64_t)k * a.nc + (k - 1));
-                }
                 if (a.trace) dt[1] = wall_clock64();
                 tile_gemm<T, true, 2>(Akk, ld, Akm, ld, Akm, ld, GT, true, smem, tid);
                 local_sync();
@@ -1542,11 +1709,11 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
             // the look-ahead factor (f64) stores write-through (sc1) like the tile tasks; the
             // rank-8 image (f32) stores plain and needs the release fence
             publish(a.lcnt + k, k + 1, !(std::is_same<T, double>::value && DIAG_LA));
-            if constexpr (DIST) publish_host(a.dist->hdiag + k);
             if (a.trace && wv == 0) {
                 long long* dp = a.trace + 4 * (int64_t)a.ntasks + 4 * (int64_t)k;
                 for (int u = 0; u < 4; u++) dp[u] = dt[u];
             }
+        }
         }
         if (a.trace && wv == 0) {
             long long* tp = a.trace + 4 * (int64_t)q;
@@ -1772,28 +1939,42 @@ static Schedule make_schedule(int nc, int nr, int W, int near, int P, const Cost
 }
 
 // ------------------------------------------------------------------------------------------
-// Distributed schedule: the same task DAG with row block i on rank (i / gb) mod g, plus the two
-// transport steps of every panel as timed nodes that occupy no worker:
-//   bcast(k)  Linv_k from DIAGX(k)'s rank to all ranks (its consumers elsewhere: TRSM(., k),
-//             DIAGX(k + 1)); after bcast(k - 1) (one broadcast stream)
-//   panel(b)  every final tile L_ib (i > b) to every other rank (consumers: updates of tiles
-//             (i', i) on other ranks); after all its producers on all ranks and panel(b - 1)
-// A task whose input lives on another rank depends on the transport node instead of the
-// producer.  Simulated on g x P workers (each task on its rank's P); each rank's ticket list
-// is its tasks in start order.  The simulation order is one topological order of the whole
-// DAG, transport included, so on every rank the smallest unfinished ticket can proceed once
-// the transport has delivered what precedes it: the single-GPU deadlock argument, extended.
+// Distributed schedule (gprx_dist.cpp): the single-GPU task DAG with row block i on rank
+// own(i) = (i / gb) mod g (identity row E_a with row a), plus, as timed nodes that occupy no
+// worker:
+//   push(i, b)   tile L_ib from its rank into the window of every rank that reads row i
+//   pushL(k)     Linv_k from DIAGX(k)'s rank into every other rank's Linv array
+//   rel(q, p)    rank q's last window-reading update chunk covering panel p is done: the window
+//                slot p mod ww may be refilled on q
+// A task whose input lives on another rank depends on its push node; a task that pushes a tile
+// of panel b into a window depends on rel(q, b - ww) of every consumer q (flow control: chunks
+// are at most ww / 2 panels wide, so a release never waits on the panel being pushed).
+// Simulated on g x P workers; each rank's ticket list is its tasks in start order.  The
+// simulation order is one topological order of the whole DAG, flow control included, so the
+// unfinished task that started first in the simulation always has its inputs and a worker:
+// the single-GPU deadlock argument, extended to the ranks and their windows.
+//
+// inv (LML mode): nc identity row blocks E_a = nc + 1 + a ride along (U = L^{-T}, tiles
+// (E_a, b), b >= a) and the lower C = U U^T accumulates in tiles (E_a, E_c), c <= a, as
+// update chunks over the panels b >= a (C_ac = -sum_b U_ab U_cb^T, stored negated).
 // ------------------------------------------------------------------------------------------
-struct DistSchedule {
-    std::vector<std::vector<int4>> lists;  // per rank
-    double est_us = 0;
-};
+static void c_chunks(int a, int W, int nc, std::vector<std::pair<int, int>>& out) {
+    out.clear();
+    for (int b = a; b < nc;) {
+        const int e = std::min(nc, (b / W + 1) * W);
+        out.push_back({b, e - b});
+        b = e;
+    }
+}
 
-static DistSchedule make_schedule_dist(int nc, int nr, int W, int near, int P, int g, int gb, const Cost& cm,
-                                       bool build, double bcast_us, double tile_us) {
+static DistSched make_schedule_dist(int nc, bool inv, int W, int near, int P, int g, int gb, int ww, const Cost& cm,
+                                    bool build, double push_us, double rel_us) {
+    const int nr = nc + 1 + (inv ? nc : 0), nci = inv ? 2 * nc : nc;
+    auto own = [&](int i) { return i <= nc ? (i / gb) % g : ((i - nc - 1) / gb) % g; };
+    auto colx = [&](int j) { return j > nc ? j - 1 : j; };  // counter column of tile (., j)
+    auto start_of = [&](int i) { return i > nc ? i - nc - 1 : 0; };
     std::vector<Task> tasks;
     std::vector<int> rank_of;  // -1: transport node
-    tasks.reserve((size_t)nr * nc * 2);
     auto add = [&](int type, int i, int j, int b0, int nb, double dur, int rk) {
         Task tk;
         tk.type = type;
@@ -1806,9 +1987,8 @@ static DistSchedule make_schedule_dist(int nc, int nr, int W, int near, int P, i
         rank_of.push_back(rk);
         return (int)tasks.size() - 1;
     };
-    auto own = [&](int i) { return (i / gb) % g; };  // gprx_dist.cpp DistLayout
-    std::vector<int> diagx(nc, -1), bcast(nc, -1), panel(nc, -1);
-    std::vector<int> trsm((size_t)nr * nc, -1), last_upd((size_t)nr * nc, -1);
+    std::vector<int> diagx(nc, -1), pushl(nc, -1);
+    std::vector<int> trsm((size_t)nr * nc, -1), push((size_t)nr * nc, -1), last_upd((size_t)nr * nci, -1);
     std::vector<std::vector<int>> deps, edeps;
     auto dep = [&](int tsk, int on, bool early = false) {
         if (on < 0) return;
@@ -1821,8 +2001,8 @@ static DistSchedule make_schedule_dist(int nc, int nr, int W, int near, int P, i
         if (i < nc && (b == i || b == i - 1)) return diagx[i];
         return trsm[(size_t)i * nc + b];
     };
-    // Linv_k as seen from rank rk
-    auto linv = [&](int k, int rk) { return own(k) == rk ? diagx[k] : bcast[k]; };
+    auto linv = [&](int k, int rk) { return own(k) == rk ? diagx[k] : pushl[k]; };
+    // the update chunks: (i, j, b0, nb), bucketed by their last panel
     struct Chunk {
         int i, j, b0, nb;
     };
@@ -1831,68 +2011,110 @@ static DistSchedule make_schedule_dist(int nc, int nr, int W, int near, int P, i
         std::vector<std::pair<int, int>> ch;
         for (int j = 1; j < nc; j++)
             for (int i = j; i < nr; i++) {
-                tile_chunks(i, j, W, near, ch, 0);
+                if (i > nc && start_of(i) >= j) continue;  // identity row E_a: tiles (E_a, j > a) only
+                tile_chunks(i, j, W, near, ch, start_of(i));
                 for (auto& c : ch) by_last[c.first + c.second - 1].push_back(Chunk{i, j, c.first, c.second});
             }
+        if (inv)
+            for (int aa = 0; aa < nc; aa++) {
+                c_chunks(aa, W, nc, ch);
+                for (int c = 0; c <= aa; c++)
+                    for (auto& x : ch) by_last[x.first + x.second - 1].push_back(Chunk{nc + 1 + aa, nc + 1 + c, x.first, x.second});
+            }
     }
+    // who reads which row through the window, and the window-reading chunks per (rank, panel)
+    DistSched S;
+    S.cons.assign((size_t)g * nr, 0);
+    S.need.assign((size_t)g * nc, 0);
+    for (int k = 0; k < nc; k++)
+        for (const Chunk& c : by_last[k]) {
+            const int q = own(c.i);
+            if (own(c.j) == q) continue;
+            S.cons[(size_t)q * nr + c.j] = 1;
+            for (int p = c.b0; p < c.b0 + c.nb; p++) S.need[(size_t)q * nc + p]++;
+        }
+    std::vector<int> rel((size_t)g * nc, -1);
+    // producers of panel p's window tiles wait for every consumer's release of panel p - ww
+    auto flow = [&](int id, int i, int p) {
+        if (i == nc || p - ww < 0) return;  // the label rows go to the z area, not the window
+        for (int q = 0; q < g; q++)
+            if (q != own(i) && S.cons[(size_t)q * nr + i]) dep(id, rel[(size_t)q * nc + (p - ww)]);
+    };
+    auto make_push = [&](int i, int b, int prod) {
+        bool any = false;
+        for (int q = 0; q < g && !any; q++) any = q != own(i) && S.cons[(size_t)q * nr + i];
+        if (!any) return;
+        const int id = add(-2, i, b, 0, 0, push_us, -1);
+        push[(size_t)i * nc + b] = id;
+        dep(id, prod);
+    };
     auto make_diagx = [&](int k) {
         const int id = add(T_DIAGX, k, k, 0, 0, (k == 0) ? cm.diag0 : cm.diagx, own(k));
         diagx[k] = id;
         if (k >= 1) {
             dep(id, linv(k - 1, own(k)));
-            dep(id, last_upd[(size_t)k * nc + (k - 1)]);
-            dep(id, last_upd[(size_t)k * nc + k]);
+            dep(id, last_upd[(size_t)k * nci + (k - 1)]);
+            dep(id, last_upd[(size_t)k * nci + k]);
+            flow(id, k, k - 1);  // it pushes L_{k,k-1} into window slot k - 1
+            make_push(k, k - 1, id);
         }
-        const int b = add(-1, k, k, 0, 0, bcast_us, -1);  // bcast(k)
-        bcast[k] = b;
-        dep(b, id);
-        if (k >= 1) dep(b, bcast[k - 1]);
+        pushl[k] = add(-3, k, k, 0, 0, push_us, -1);
+        dep(pushl[k], id);
     };
     if (build)
         for (int i = 0; i < nc; i++)
-            for (int j = 0; j <= i; j++) last_upd[(size_t)i * nc + j] = add(T_BUILD, i, j, 0, 0, cm.build, own(i));
+            for (int j = 0; j <= i; j++) last_upd[(size_t)i * nci + j] = add(T_BUILD, i, j, 0, 0, cm.build, own(i));
     make_diagx(0);
     dep(diagx[0], last_upd[0]);
     for (int k = 0; k < nc; k++) {
+        if (k - ww >= 0)  // releases of panel k - ww: every chunk covering it was created already
+            for (int q = 0; q < g; q++) {
+                const int p = k - ww;
+                if (!S.need[(size_t)q * nc + p]) continue;
+                rel[(size_t)q * nc + p] = add(-4, q, p, 0, 0, rel_us, -1);  // its chunks: wired below
+            }
         for (int i = k + 1; i < nr; i++) {
             if (i == k + 1 && i < nc) continue;  // inside DIAGX(k+1)
+            if (k < start_of(i)) continue;        // zero block of an identity row
             const int id = add(T_TRSM, i, k, 0, 0, cm.trsm, own(i));
             trsm[(size_t)i * nc + k] = id;
             dep(id, linv(k, own(i)));
-            dep(id, last_upd[(size_t)i * nc + k]);
+            dep(id, last_upd[(size_t)i * nci + k]);
+            flow(id, i, k);
+            make_push(i, k, id);
         }
         if (k + 1 < nc) make_diagx(k + 1);
-        {  // panel(k): every tile L_ik, i > k, delivered everywhere
-            const int ntile = nr - k - 1;
-            const int pn = add(-2, k, k, 0, 0, ntile > 0 ? tile_us * ntile : 0.0, -1);
-            panel[k] = pn;
-            for (int i = k + 1; i < nr; i++) {
-                bool e;
-                const int p = prodL(i, k, e);
-                dep(pn, p, e);
-            }
-            if (k >= 1) dep(pn, panel[k - 1]);
-        }
         for (const Chunk& c : by_last[k]) {
             const int rk = own(c.i);
             const double dur = cm.ovh + c.nb * cm.k128 * (c.i == c.j ? cm.diagf : 1.0);
             const int id = add(T_UPD, c.i, c.j, c.b0, c.nb, dur, rk);
-            dep(id, last_upd[(size_t)c.i * nc + c.j]);
+            dep(id, last_upd[(size_t)c.i * nci + colx(c.j)]);
             bool e1, e2;
-            const int p1 = prodL(c.i, k, e1);
-            dep(id, p1, e1);
+            dep(id, prodL(c.i, k, e1), e1);
             if (own(c.j) == rk) {
-                const int p2 = prodL(c.j, k, e2);
-                dep(id, p2, e2);
+                dep(id, prodL(c.j, k, e2), e2);
             } else {
-                dep(id, panel[k]);
+                for (int b = c.b0; b <= k; b++) dep(id, push[(size_t)c.j * nc + b]);
             }
-            last_upd[(size_t)c.i * nc + c.j] = id;
+            last_upd[(size_t)c.i * nci + colx(c.j)] = id;
         }
     }
+    // the release nodes depend on the chunks that read the window (chunks are at most W <= ww
+    // panels wide, so every chunk covering panel p was created before rel(., p))
     const int nt = (int)tasks.size();
     deps.resize(nt);
     edeps.resize(nt);
+    for (int id = 0; id < nt; id++) {
+        if (rank_of[id] >= 0 && tasks[id].type == T_UPD) {
+            const Task& c = tasks[id];
+            const int q = rank_of[id];
+            if (own(c.j) != q)
+                for (int p = c.b0; p < c.b0 + c.nb; p++) {
+                    const int r = rel[(size_t)q * nc + p];
+                    if (r >= 0) deps[r].push_back(id);
+                }
+        }
+    }
     for (int id = 0; id < nt; id++) {
         auto& d = deps[id];
         auto& ed = edeps[id];
@@ -1913,22 +2135,45 @@ static DistSchedule make_schedule_dist(int nc, int nr, int W, int near, int P, i
         }
         tasks[id].ndep = (int)d.size() + ne;
     }
-    for (int id = nt - 1; id >= 0; id--) {
-        double m = 0;
-        for (int s2 : tasks[id].succ) m = std::max(m, tasks[s2].bl);
-        for (int s2 : tasks[id].esucc) m = std::max(m, tasks[s2].bl - (tasks[id].dur - cm.early));
-        tasks[id].bl = tasks[id].dur + m;
+    // bottom levels: a release node's producers may come after it in id order, so iterate the
+    // longest-path recurrence to a fixed point over a topological order (Kahn)
+    {
+        std::vector<int> indeg(nt, 0), order;
+        order.reserve(nt);
+        for (int id = 0; id < nt; id++)
+            for (int s2 : tasks[id].succ) indeg[s2]++;
+        for (int id = 0; id < nt; id++)
+            for (int s2 : tasks[id].esucc) indeg[s2]++;
+        std::vector<int> st;
+        for (int id = 0; id < nt; id++)
+            if (!indeg[id]) st.push_back(id);
+        while (!st.empty()) {
+            const int id = st.back();
+            st.pop_back();
+            order.push_back(id);
+            for (int s2 : tasks[id].succ)
+                if (--indeg[s2] == 0) st.push_back(s2);
+            for (int s2 : tasks[id].esucc)
+                if (--indeg[s2] == 0) st.push_back(s2);
+        }
+        if ((int)order.size() != nt) throw Error{GPRX_ERR_ARG, "potrf dist schedule: dependency cycle"};
+        for (int x = nt - 1; x >= 0; x--) {
+            const int id = order[x];
+            double m = 0;
+            for (int s2 : tasks[id].succ) m = std::max(m, tasks[s2].bl);
+            for (int s2 : tasks[id].esucc) m = std::max(m, tasks[s2].bl - (tasks[id].dur - cm.early));
+            tasks[id].bl = tasks[id].dur + m;
+        }
     }
     typedef std::pair<double, int> PQ;
     std::vector<std::priority_queue<PQ>> ready(g);
     std::priority_queue<PQ, std::vector<PQ>, std::greater<PQ>> running;
     std::vector<int> indeg(nt), freew(g, P);
-    DistSchedule S;
-    S.lists.resize(g);
+    S.lists.assign(g, {});
     double now = 0;
     int started = 0;
     auto make_ready = [&](int id) {
-        if (rank_of[id] < 0) {  // transport: starts at once, no worker
+        if (rank_of[id] < 0) {  // transport / release: starts at once, no worker
             running.push({now + tasks[id].dur, id});
             started++;
         } else {
@@ -1965,6 +2210,7 @@ static DistSchedule make_schedule_dist(int nc, int nr, int W, int near, int P, i
             if (--indeg[s2] == 0) make_ready(s2);
     }
     S.est_us = now;
+    S.W = W;
     return S;
 }
 
@@ -2123,6 +2369,7 @@ void potrf_tiles(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info
     a.tasks = sd.list;
     a.ntasks = (int)sd.n;
     a.nc = nc;
+    a.nv = nc;
     a.ctl = st.ctr;
     a.lcnt = st.ctr + C_NCTL;
     a.ver = st.ctr + C_NCTL + nr;
@@ -2181,15 +2428,18 @@ void potrf_tiles(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info
 }
 
 // ---- distributed factorisation: per-rank ticket lists and one rank's launch ------------------
-std::vector<std::vector<int4>> potrf_dist_schedule(int nc, int nr, int P, int g, int gb, bool build, double* est_us) {
+DistSched potrf_dist_schedule(int nc, int g, int gb, int ww, int P, bool build, bool inv) {
     const pt::Params& pr = pt::params();
-    double bcast_us = 30.0, tile_us = 0.5;  // transport estimates: a broadcast's latency, one tile
-    if (const char* e = std::getenv("GPRX_DIST_BCAST_US")) bcast_us = std::atof(e);
-    if (const char* e = std::getenv("GPRX_DIST_TILE_US")) tile_us = std::atof(e);
-    pt::DistSchedule S =
-        pt::make_schedule_dist(nc, nr, pr.W, pr.near_for(nc), P, g, std::max(1, gb), pr.cm, build, bcast_us, tile_us);
-    if (est_us) *est_us = S.est_us;
-    return S.lists;
+    // a push: one tile's stores over xGMI plus the flag (measured on one GPU as a same-device
+    // copy; GPRX_DIST_PUSH_US / GPRX_DIST_REL_US override)
+    double push_us = 4.0, rel_us = 2.0;
+    if (const char* e = std::getenv("GPRX_DIST_PUSH_US")) push_us = std::atof(e);
+    if (const char* e = std::getenv("GPRX_DIST_REL_US")) rel_us = std::atof(e);
+    ww = std::max(2, std::min(ww, nc));
+    // update chunks at most half a window wide (flow control, make_schedule_dist), powers of two
+    int W = 1;
+    while (2 * W <= std::min(pr.W, std::max(1, ww / 2))) W *= 2;
+    return pt::make_schedule_dist(nc, inv, W, pr.near_for(nc), P, g, std::max(1, gb), ww, pr.cm, build, push_us, rel_us);
 }
 
 template <typename T>
@@ -2198,11 +2448,12 @@ void potrf_tiles_dist_launch(const DistLaunch<T>& L) {
     Args<T> a;
     std::memset(&a, 0, sizeof(a));
     a.A = L.A;
-    a.ld = L.ld;
+    a.ld = DB;
     a.Linv = L.Linv;
     a.tasks = L.list;
     a.ntasks = L.ntasks;
     a.nc = L.nc;
+    a.nv = L.nci;
     a.ctl = L.ctr;
     a.lcnt = L.ctr + C_NCTL;
     a.ver = L.ctr + C_NCTL + L.nr;

@@ -66,7 +66,40 @@ __global__ void accumulate_kernel(const float* __restrict__ delta, double* __res
     }
 }
 
+// the sharded refinement (gprx_dist.cpp owns the rows): out[t][k] = X[idx[t]][k]
+__global__ void gather_rows_kernel(const double* __restrict__ X, const int64_t* __restrict__ idx, int64_t q, int d,
+                                   double* __restrict__ out) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= q * d) return;
+    const int64_t t = e / d;
+    out[e] = X[idx[t] * d + (e % d)];
+}
+
+// rhs[idx[t]][c] = Y - Kx - s2 a at the rows this process's ranks own (Kx: q x m, row t)
+__global__ void residual_scatter_kernel(const double* __restrict__ Y, const double* __restrict__ Kx,
+                                        const double* __restrict__ a, double s2, const int64_t* __restrict__ idx,
+                                        int64_t q, int m, float* __restrict__ rhs) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= q * m) return;
+    const int64_t t = e / m;
+    const int c = (int)(e % m);
+    const int64_t k = idx[t] * m + c;
+    rhs[k] = (float)(Y[k] - Kx[e] - s2 * a[k]);
+}
+
 }  // namespace rf
+
+void launch_gather_rows(const double* X, const int64_t* idx, int64_t q, int d, double* out, hipStream_t s) {
+    if (q * d <= 0) return;
+    hipLaunchKernelGGL(rf::gather_rows_kernel, dim3((unsigned)((q * d + 255) / 256)), dim3(256), 0, s, X, idx, q, d, out);
+}
+
+void launch_residual_scatter(const double* Y, const double* Kx, const double* a, double s2, const int64_t* idx,
+                             int64_t q, int m, float* rhs, hipStream_t s) {
+    if (q * m <= 0) return;
+    hipLaunchKernelGGL(rf::residual_scatter_kernel, dim3((unsigned)((q * m + 255) / 256)), dim3(256), 0, s, Y, Kx, a,
+                       s2, idx, q, m, rhs);
+}
 
 template <typename S, typename D>
 void launch_convert(const S* in, D* out, int64_t n, hipStream_t s) {

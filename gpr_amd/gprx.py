@@ -36,6 +36,7 @@ STATUS = {0: "OK", 1: "NONFINITE", 2: "NOT_SPD", 3: "SINGULAR", 4: "DIM", 5: "HI
 # Every symbol include/gprx.h declares (checked by tests/test_abi.py).
 EXPORTED = [
     "gprx_abi_version", "gprx_device_count", "gprx_ctx_create", "gprx_dist_unique_id", "gprx_ctx_create_dist",
+    "gprx_ctx_create_peer",
     "gprx_ctx_destroy", "gprx_last_error", "gprx_model_create", "gprx_model_destroy", "gprx_model_set_data",
     "gprx_model_set_kernel", "gprx_model_set_noise", "gprx_model_fit", "gprx_model_get_alpha",
     "gprx_model_set_alpha",
@@ -76,6 +77,30 @@ class FitInfo(ctypes.Structure):
 
 _lib = None
 
+# gprx_allgather_fn (include/gprx.h): int fn(void* user, const void* send, size_t bytes, void* recv)
+ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p)
+
+
+def torch_allgather(group=None):
+    """A gprx_allgather_fn over torch.distributed (any backend: gloo on the host here): the
+    caller-side collective gprx_ctx_create_peer bootstraps with."""
+    import torch
+    import torch.distributed as dist
+
+    def fn(user, send, nbytes, recv):
+        try:
+            world = dist.get_world_size(group)
+            mine = torch.frombuffer(bytearray(ctypes.string_at(send, nbytes)), dtype=torch.uint8) if nbytes else \
+                torch.empty(0, dtype=torch.uint8)
+            out = [torch.empty(nbytes, dtype=torch.uint8) for _ in range(world)]
+            dist.all_gather(out, mine, group=group)
+            if nbytes:
+                ctypes.memmove(recv, b"".join(o.numpy().tobytes() for o in out), nbytes * world)
+            return 0
+        except Exception:  # reported to the library as a failed collective
+            return 1
+    return fn
+
 
 def lib():
     """Load libgprx.so (built in-tree by `make` / __graft_entry__.build())."""
@@ -89,6 +114,9 @@ def lib():
         L.gprx_ctx_create.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
         L.gprx_ctx_create_dist.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                            ctypes.POINTER(ctypes.c_void_p)]
+        L.gprx_ctx_create_peer.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ALLGATHER_FN, ctypes.c_void_p,
+                                           ctypes.POINTER(ctypes.c_void_p)]
+        L.gprx_dev_dist_info.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64)]
         L.gprx_ctx_destroy.argtypes = [ctypes.c_void_p]
         L.gprx_model_create.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
         L.gprx_model_destroy.argtypes = [ctypes.c_void_p]
@@ -206,12 +234,20 @@ def query_shard(q, rank, world):
 class Context:
     """One per process per GPU (gprx_ctx)."""
 
-    def __init__(self, device=0, dist=None, virtual=0):
+    def __init__(self, device=0, dist=None, virtual=0, peer=None):
         """dist = (rank, world, unique_id): one RCCL rank per process; virtual = g: g virtual
-        ranks of the distributed fit in this process on one GPU (gprx_ctx_create_virtual)."""
+        ranks of the distributed fit in this process on one GPU (gprx_ctx_create_virtual);
+        peer = (rank, world, fn): one rank per process bootstrapped by the caller's all-gather
+        fn(send_bytes) -> list of every rank's bytes (gprx_ctx_create_peer), e.g.
+        torch_allgather() over a gloo process group."""
         h = ctypes.c_void_p()
+        self._cb = None
         if virtual:
             _check(lib().gprx_ctx_create_virtual(device, int(virtual), ctypes.byref(h)))
+        elif peer is not None:
+            rank, world, fn = peer
+            self._cb = ALLGATHER_FN(fn)  # kept alive as long as the context
+            _check(lib().gprx_ctx_create_peer(device, rank, world, self._cb, None, ctypes.byref(h)))
         elif dist is None:
             _check(lib().gprx_ctx_create(device, ctypes.byref(h)))
         else:
@@ -408,6 +444,15 @@ class Model:
         info = FitInfo()
         self._c(lib().gprx_model_fit(self.h, flags, ctypes.byref(info)))
         return info
+
+    def dist_info(self):
+        """Layout and memory of the last distributed fit (gprx_dev_dist_info): per-rank device
+        bytes of the engine and of the packed storage, row-block group, window panels, update
+        chunk width, workgroups per rank, simulated makespan (us)."""
+        v = (ctypes.c_int64 * 8)()
+        self._c(lib().gprx_dev_dist_info(self.h, v))
+        keys = ["bytes_rank", "bytes_storage", "gb", "ww", "chunk_w", "P", "est_us", "world"]
+        return dict(zip(keys, list(v)))
 
     def alpha(self):
         a = np.empty((self.n, self.m), self.dtype)

@@ -27,6 +27,7 @@
 #define GPRX_H
 
 #include <stdint.h>
+#include <stddef.h>
 
 #ifdef __cplusplus
 extern "C" {
@@ -116,6 +117,15 @@ gprx_status gprx_ctx_create(int device, gprx_ctx** out);
 #define GPRX_UNIQUE_ID_BYTES 128
 gprx_status gprx_dist_unique_id(void* out);
 gprx_status gprx_ctx_create_dist(int device, int rank, int world, const void* unique_id, gprx_ctx** out);
+/* Multi-process context bootstrapped by the CALLER's collective instead of RCCL (e.g. over
+ * torch.distributed gloo or MPI): `fn` must all-gather `bytes` bytes from every rank into recv
+ * (world * bytes, rank order) and return 0.  The library calls it only for its own host-side
+ * exchanges (the mailboxes' IPC handles once per problem shape, a few bytes of reductions per
+ * fit); the factorisation's panel traffic goes device to device.  Ranks may share one GPU
+ * (GPRX_DIST_SHARED_GPU=1: each takes 1/world of the CUs), which is how the multi-process path
+ * is tested on a one-GPU box. */
+typedef int (*gprx_allgather_fn)(void* user, const void* send, size_t bytes, void* recv);
+gprx_status gprx_ctx_create_peer(int device, int rank, int world, gprx_allgather_fn fn, void* user, gprx_ctx** out);
 void gprx_ctx_destroy(gprx_ctx* ctx);
 /* Message of the last failing call on this context (ctx may be NULL: last failure of
  * any call on this thread). */

@@ -31,10 +31,13 @@ gprx_status gprx_dev_bench(gprx_ctx* ctx, gprx_dtype dtype, int32_t what, int64_
  * device: GPRX_ERR_ARG if the ticket order would violate a dependency. */
 gprx_status gprx_dev_schedule(int32_t nc, int32_t nr, int32_t P, int32_t build, double* est_us, int64_t* ntasks);
 /* Host-only: the distributed factorisation's schedule (g ranks of P workers each, row blocks
- * grouped by gb, build as above), simulated over all ranks with the transports as timed nodes;
- * returns the simulated makespan (us) -- the figure gprx_dist.cpp picks gb by. */
-gprx_status gprx_dev_dist_schedule(int32_t nc, int32_t nr, int32_t P, int32_t g, int32_t gb, int32_t build,
-                                   double* est_us);
+ * grouped by gb, a window of ww panels; flags bit 0: with the fused covariance-build tasks,
+ * bit 1: LML mode, the inverse's identity rows and the C = U U^T tiles riding along), simulated
+ * over all ranks with the pushes and window releases as timed nodes; returns the simulated
+ * makespan (us), the update chunk width and the task count -- the figures gprx_dist.cpp picks
+ * gb and ww by.  GPRX_ERR_ARG if the ticket order would violate a dependency. */
+gprx_status gprx_dev_dist_schedule(int32_t nc, int32_t P, int32_t g, int32_t gb, int32_t ww, int32_t flags,
+                                   double* est_us, int32_t* chunk_w, int64_t* ntasks);
 /* GPRX_PT_DEBUG=1: copy the per-workgroup status {ticket, phase, i, j} of the running (or last)
  * potrf_tiles launch out of pinned host memory, without synchronising; returns workgroups. */
 int32_t gprx_dev_pt_debug(int32_t* out, int32_t max_wg);
@@ -63,6 +66,11 @@ gprx_status gprx_dev_build_time(gprx_ctx* ctx, gprx_dtype dtype, const gprx_kern
  * with device copies in place of the RCCL broadcast / panel exchange (gprx_dist.cpp).  Models
  * of this context fit with the multi-GPU algorithm end to end on a single device. */
 gprx_status gprx_ctx_create_virtual(int device, int world, gprx_ctx** out);
+/* Layout and memory of a model's last distributed fit (gprx_dist.cpp): out[0] device bytes the
+ * engine holds per rank (max over this process's ranks), out[1] of which the packed own row
+ * blocks, out[2] row-block group gb, out[3] window panels ww, out[4] update chunk width, out[5]
+ * workgroups per rank, out[6] simulated makespan (us), out[7] ranks. */
+gprx_status gprx_dev_dist_info(gprx_model* model, int64_t* out);
 /* Parity hook for the tile engine's diagonal-block factor: the 128 x 128 SPD block A (column-
  * major, host) factored by variant 0 (rank-8 register image), 1 (blocked) or 2 (blocked with
  * look-ahead): L (lower triangle meaningful, the upper keeps A), Linv = L^{-1} (column-major)

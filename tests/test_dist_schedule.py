@@ -1,8 +1,9 @@
-"""World-size-2 gloo test of the storage-sharded multi-GPU fit and of the distributed LML
-gradient reduction (tests/dist_schedule.py restates gprx_dist.cpp / potrf_tiles_kernel<T,
-true> and model_lml on a distributed context): each rank stores only its row blocks, the
-diagonal inverses are broadcast and the panels exchanged, and every rank ends with alpha,
-log det and data fit equal to a single-process solve; the per-rank gradient partials
+"""World-size-2/3 gloo test of the storage-sharded multi-GPU fit (tests/dist_schedule.py restates
+gprx_dist.cpp / potrf_tiles_kernel<T, true> / k_dsolve.hip): each rank stores only the lower
+tiles of its row blocks, the diagonal inverses are pushed to every rank and the factored tiles
+into bounded, flow-controlled windows; the back substitution sums the ranks' partials at each
+block's owner.  Every rank ends with alpha, log det and data fit equal to a single-process solve;
+in LML mode the C tiles each rank accumulated give its gradient partial, and the partials
 all-reduce to the full gradient."""
 import os
 import socket
@@ -29,12 +30,12 @@ def _gauss(X, sig, sc):
     return K, [sc * sc * r2 / sig ** 3 * e, 2.0 * sc * e]
 
 
-def _worker(rank, world, port, n, B, gb, out):
+def _worker(rank, world, port, n, B, gb, ww, out):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import torch
-    from tests.dist_schedule import assemble_L, grad_partial, sharded_fit
+    from tests.dist_schedule import forward_substitution, back_substitution, grad_partial_tiles, sharded_fit
     from gpr_amd.synth import make_data
     X, Y = make_data(n, 3, 2)
     K, dK = _gauss(X, 0.9, 1.1)
@@ -54,23 +55,27 @@ def _worker(rank, world, port, n, B, gb, out):
         dist.all_reduce(t)
         return t.numpy()
 
-    alpha, logdet, datafit, tiles, Linv, np_ = sharded_fit(K, Y, 0.5, n, B, rank, world, gb, bcast,
-                                                           allgather_obj, allreduce_sum)
-    L = assemble_L(tiles, Linv, np_ // B, B)
-    Wi = np.linalg.inv(L)
-    C = Wi.T @ Wi
-    part = grad_partial(alpha[:, :1], C, dK, n, B, rank, world, gb)
+    r = sharded_fit(K, Y, 0.5, n, B, rank, world, gb, ww, bcast, allgather_obj, allreduce_sum, inv=True)
+    part = grad_partial_tiles(r["alpha"][:, :1], r["C"], dK, n, B)
     grad = 0.5 * allreduce_sum(part)
-    np.savez(out + f"_{rank}.npz", alpha=alpha, logdet=logdet, datafit=datafit, grad=grad, part=part)
+    # the refinement's correction solve through the sharded factor: (L L^T)^{-1} rhs
+    nc = -(-n // B)
+    rhs = np.zeros((nc * B, 2))
+    rhs[:n] = Y
+    z = forward_substitution(r["T"], r["Linv"], rhs, nc, B, rank, world, gb, allgather_obj)
+    sol = back_substitution(r["T"], r["Linv"], {k: z[k * B:(k + 1) * B] for k in range(nc)}, nc, B, 2, rank, world,
+                            gb, allgather_obj)
+    np.savez(out + f"_{rank}.npz", alpha=r["alpha"], logdet=r["logdet"], datafit=r["datafit"], grad=grad, part=part,
+             stored=r["stored"], window_max=r["window_max"], sol=sol[:n])
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n,B,gb", [(300, 64, 1), (513, 64, 2), (400, 32, 3)])
-def test_sharded_fit_world2(tmp_path, n, B, gb):
-    world = 2
+@pytest.mark.parametrize("world,n,B,gb,ww", [(2, 300, 64, 1, 2), (2, 513, 64, 2, 3), (3, 400, 32, 3, 4),
+                                              (3, 700, 64, 1, 16)])
+def test_sharded_fit_gloo(tmp_path, world, n, B, gb, ww):
     out = str(tmp_path / "res")
-    mp.spawn(_worker, args=(world, _free_port(), n, B, gb, out), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), n, B, gb, ww, out), nprocs=world, join=True)
     from gpr_amd.synth import make_data
     X, Y = make_data(n, 3, 2)
     K, dK = _gauss(X, 0.9, 1.1)
@@ -81,14 +86,21 @@ def test_sharded_fit_world2(tmp_path, n, B, gb):
     C = np.linalg.inv(Kn)
     a1 = aref[:, 0]
     gref = np.array([0.5 * np.trace((np.outer(a1, a1) - C) @ D) for D in dK])
-    parts = []
+    parts, stored = [], 0
+    nc = -(-n // B)
     for r in range(world):
         z = np.load(out + f"_{r}.npz")
         assert np.max(np.abs(z["alpha"] - aref)) <= 1e-10 * np.max(np.abs(aref))
+        assert np.max(np.abs(z["sol"] - aref)) <= 1e-10 * np.max(np.abs(aref))
         assert abs(float(z["logdet"]) - ldref) <= 1e-10 * abs(ldref)
         assert abs(float(z["datafit"]) - dfref) <= 1e-10 * abs(dfref)
         assert np.max(np.abs(z["grad"] - gref)) <= 1e-9 * np.max(np.abs(gref))
+        assert int(z["window_max"]) <= ww
         parts.append(z["part"])
-    # each rank's partial covers only its row blocks: the two differ and sum to the gradient
+        stored += int(z["stored"])
+    # each rank's partial covers only its row blocks; together they are the gradient
     assert np.max(np.abs(parts[0] - parts[1])) > 0
-    assert np.max(np.abs(0.5 * (parts[0] + parts[1]) - gref)) <= 1e-9 * np.max(np.abs(gref))
+    assert np.max(np.abs(0.5 * sum(parts) - gref)) <= 1e-9 * np.max(np.abs(gref))
+    # the ranks together store the lower factor once (+ label, U and C tiles), never N^2 each
+    lower = nc * (nc + 1) // 2 + nc + nc * (nc + 1) // 2 + nc * (nc + 1) // 2
+    assert stored == lower * B * B

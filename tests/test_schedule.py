@@ -3,6 +3,8 @@ exported as gprx_dev_schedule): every task's producers hold earlier tickets (the
 argument of the persistent kernel), task counts match the tile decomposition, and the simulated
 makespan behaves.  No device needed."""
 import ctypes
+
+import numpy as np
 import os
 
 import pytest
@@ -113,33 +115,58 @@ def test_schedule_more_workers_never_slower():
     assert e256 <= e64
 
 
-def _dist_sched(nc, nr, P, g, gb, build=True):
+def _dist_sched(nc, P, g, gb, ww, build=True, inv=False):
     L = lib()
-    L.gprx_dev_dist_schedule.argtypes = [ctypes.c_int32] * 6 + [ctypes.POINTER(ctypes.c_double)]
-    est = ctypes.c_double()
-    st = L.gprx_dev_dist_schedule(nc, nr, P, g, gb, 1 if build else 0, ctypes.byref(est))
-    return st, est.value
+    L.gprx_dev_dist_schedule.argtypes = [ctypes.c_int32] * 6 + [ctypes.POINTER(ctypes.c_double),
+                                                                 ctypes.POINTER(ctypes.c_int32),
+                                                                 ctypes.POINTER(ctypes.c_int64)]
+    est, w, nt = ctypes.c_double(), ctypes.c_int32(), ctypes.c_int64()
+    st = L.gprx_dev_dist_schedule(nc, P, g, gb, ww, (1 if build else 0) | (2 if inv else 0), ctypes.byref(est),
+                                  ctypes.byref(w), ctypes.byref(nt))
+    return st, est.value, w.value, nt.value
 
 
 def test_dist_schedule_makespan_scales_and_is_chain_bound():
-    # C3 (nc = 128, one label row block) on g ranks of 240 workers (gprx_dist.cpp: two CU
-    # slots per XCC reserved for RCCL): more ranks never simulate slower at the best grouping,
-    # and the makespan stays above the DIAGX chain (nc diagonal steps of the cost model's
-    # 70 us) -- the sharded fit is chain-bound at 8 ranks
+    # C3 (nc = 128, one label row block) on g ranks of 256 workers, the best of the row-block
+    # groupings and windows gprx_dist.cpp picks from: more ranks never simulate slower, and the
+    # makespan stays above the DIAGX chain (nc diagonal steps of the cost model's 70 us) -- the
+    # sharded fit is chain-bound at 8 ranks
     best = {}
     for g in (1, 2, 4, 8):
         ests = []
         for gb in (1, 2, 4, 8):
             if g > 1 and 128 < 2 * gb * g:
                 continue
-            st, est = _dist_sched(128, 129, 240, g, gb)
-            assert st == 0 and est > 0
-            ests.append(est)
+            for ww in ((128,) if g == 1 else (8, 16, 32, 64)):
+                st, est, w, _ = _dist_sched(128, 256, g, gb, ww)
+                assert st == 0 and est > 0 and 2 * w <= ww
+                ests.append(est)
         best[g] = min(ests)
     assert best[2] < best[1] and best[4] < best[2] and best[8] <= best[4]
     assert best[8] > 128 * 70.0
 
 
+def test_dist_schedule_window_flow_control():
+    # windows down to 2 panels (single-panel chunks) still give a valid ticket order on every
+    # rank (the simulation would raise on a cycle: the flow-control edges rel(q, p) -> pushes of
+    # panel p + ww never close one), including the LML mode with identity rows and C tiles
+    for ww in (2, 3, 4, 8):
+        for g in (2, 3, 5):
+            st, est, w, nt = _dist_sched(24, 30, g, 2, ww)
+            assert st == 0 and est > 0 and w == max(1, 2 ** int(np.log2(max(1, ww // 2))))
+            st, est, w, nt = _dist_sched(16, 30, g, 1, ww, inv=True)
+            assert st == 0 and est > 0
+
+
+def test_dist_schedule_lml_mode_costs_about_three_factorisations():
+    # the inverse riding along: n^3/3 (factor) + n^3/3 (U = L^{-T}) + n^3/3 (C = U U^T) flops
+    st, e1, _, _ = _dist_sched(48, 64, 2, 2, 16)
+    st2, e3, _, _ = _dist_sched(48, 64, 2, 2, 16, inv=True)
+    assert st == 0 and st2 == 0
+    assert 1.8 * e1 < e3 < 4.0 * e1
+
+
 def test_dist_schedule_rejects_bad_arguments():
-    assert _dist_sched(0, 1, 240, 1, 1)[0] != 0
-    assert _dist_sched(4, 3, 240, 1, 1)[0] != 0
+    assert _dist_sched(0, 240, 1, 1, 8)[0] != 0
+    assert _dist_sched(4, 240, 0, 1, 8)[0] != 0
+    assert _dist_sched(4, 240, 33, 1, 8)[0] != 0
