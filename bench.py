@@ -11,13 +11,20 @@ HBM before the timed region.
 
 Multi-GPU: launched by torch.distributed.run, one process per GPU.  The headline (--mode
 dist, the default for N > 1) is ONE fit per step whose matrix is sharded over the ranks:
-row blocks dealt cyclically (each GPU stores ~N^2/(2g) of the lower triangle and builds only
-its own tiles), each rank runs the persistent tile-dataflow factorisation on its rows, the
-diagonal-block inverses go out by RCCL broadcast and the factored panels by a full-mesh
-grouped send/recv (gpr_amd/csrc/gprx_dist.cpp; strong scaling: value = fits/s of the
-job).  The same run also measures --mode replicas (every rank fits its own GP, weak
-scaling) and reports it under "replicas"; `--mode replicas` makes that the headline.
-Predict is query-sharded over the ranks (X and alpha replicated).
+row blocks dealt in cyclic groups (each GPU stores only the lower tiles of its own row blocks,
+~N^2/(2g), and builds only those), each rank runs the persistent tile-dataflow factorisation on
+its rows, and the exchange is device-initiated: a finished tile is stored by the task that
+produced it straight into the windows of the ranks that read it (IPC-mapped over xGMI), the
+diagonal-block inverses likewise into every rank (gpr_amd/csrc/gprx_dist.cpp; strong scaling:
+value = fits/s of the job).  The same run also measures --mode replicas (every rank fits its
+own GP, weak scaling) and reports it under "replicas"; `--mode replicas` makes that the
+headline.  Predict is query-sharded over the ranks (X and alpha replicated).
+
+The other BASELINE.json configurations are measured in the same run ("configs" in the JSON
+line, --configs 0 skips them), each with its own dominant-kernel roofline and a labelled CPU
+baseline: C2 (N=4096 d=16 Gaussian fp64, replicas), C4 (N=32768 d=32 RationalQuadratic fp32 with
+the fp64 refinement; sharded over the ranks for N > 1, its BASELINE form), C5 (sparse GP M=2048
+inducing, N=1e6 d=64 fp64, dense rows sharded over the ranks).
 
 Prints ONE JSON line on rank 0 (plus human-readable detail on stderr).
 """
@@ -33,6 +40,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 PEAK_FP64_TFLOPS = 78.6   # MI355X dense fp64 (vector = matrix), MI355X_MICROARCH.md / SURVEY.md §8(d)
+PEAK_FP32_TFLOPS = 157.3  # MI355X dense fp32 matrix
 PEAK_HBM_GBS = 8000.0     # HBM3E spec
 
 
@@ -87,6 +95,163 @@ def traffic_from_profile(kernels=("potrf_tiles_kernel<double, false>", "potrf_ti
     return None
 
 
+def run_configs(args, world, rank, local_rank, dctx, max_over_ranks, barrier_sync):
+    """BASELINE.json configs[1], [3], [4] (C2, C4, C5), each timed like the headline (warmup,
+    then K steps between barriers, max over ranks) with the dominant kernel's roofline from its
+    HIP-event device time, and (rank 0, N = 1) a labelled CPU baseline on a bounded sample."""
+    import gpr_amd
+    from gpr_amd.synth import C2, C4, make_data
+    from gpr_amd.gprx import FIT_DISTRIBUTED
+    out = {}
+
+    def fit_leg(cfg, ctx, flags, dtype, steps):
+        X, Y = make_data(cfg["n"], cfg["d"], cfg["m"])
+        M = gpr_amd.Model(ctx, dtype)
+        M.set_data(X.astype(dtype), Y.astype(dtype))
+        M.set_kernel(cfg["kernel"])
+        M.set_noise(cfg["sigma"])
+        for _ in range(max(1, args.warmup)):
+            M.fit(flags)
+        ctx.set_stats(True)
+        barrier_sync()
+        t0 = time.perf_counter()
+        infos = [M.fit(flags) for _ in range(steps)]
+        barrier_sync()
+        el = max_over_ranks(time.perf_counter() - t0)
+        st = ctx.stats()
+        ctx.set_stats(False)
+        dinfo = M.dist_info() if flags & FIT_DISTRIBUTED else None
+        M.close()
+        return el, infos, st, dinfo
+
+    # ---- C2: N=4096 d=16 GaussianKernel fp64 (replicas: every rank fits its own) -----------------
+    try:
+        n, m = C2["n"], C2["m"]
+        ctx = gpr_amd.Context(local_rank)
+        el, infos, st, _ = fit_leg(C2, ctx, 0, np.float64, max(args.steps, 10))
+        ctx.close()
+        steps = max(args.steps, 10)
+        fac = st.get("potrf_tiles", {"ms": 0, "launches": 0})
+        t_k = max_over_ranks(fac["ms"] / fac["launches"]) if fac["launches"] else None
+        alg = n ** 3 / 3.0 + m * float(n) ** 2
+        c2 = {"workload": "C2: GP fit N=4096 d=16 m=1 GaussianKernel(1,1) sigma=0.1 fp64 (BASELINE.json configs[1])",
+              "metric": "GP fits/sec", "value": world * steps / el, "unit": "fits/s", "ms_per_step": 1e3 * el / steps,
+              "scaling": "weak" if world > 1 else None, "dtype": "f64",
+              "roofline": {"bound": "mfma", "kernel": "potrf_tiles_kernel<double, false> (fused build + Cholesky)",
+                           "achieved": alg / (t_k * 1e-3) / 1e12 if t_k else None, "peak": PEAK_FP64_TFLOPS,
+                           "unit": "TFLOP/s", "frac": alg / (t_k * 1e-3) / 1e12 / PEAK_FP64_TFLOPS if t_k else None,
+                           "avg_launch_us": 1e3 * t_k if t_k else None, "algorithmic_flops_per_launch": alg,
+                           "note": "latency-bound: N/128 = 32 serial diagonal steps"}}
+        if rank == 0 and world == 1 and args.cpu_n > 0:
+            from oracle import oracle as O
+            X, Y = make_data(n, C2["d"], m)
+            t0 = time.perf_counter()
+            O.fit(C2["kernel"], X, Y, C2["sigma"], np.float64, want_core=False)
+            dt = time.perf_counter() - t0
+            c2["cpu_baseline"] = {"value": 1.0 / dt, "unit": "fits/s", "cores": O.num_threads(), "kind": "port",
+                                  "sample": f"1 full fit at N={n} (oracle: kernel loop + LAPACK {O.lapack_name()} "
+                                            f"getrf+getri in fp64 + C Y) in {dt:.2f} s"}
+        out["C2"] = c2
+    except Exception as e:
+        out["C2"] = {"error": repr(e)}
+    # ---- C4: N=32768 d=32 RationalQuadratic fp32 (sharded for N > 1, its BASELINE form) ----------
+    try:
+        n, m = C4["n"], C4["m"]
+        steps = max(3, min(args.steps, 5))
+        if world > 1 and dctx is not None:
+            el, infos, st, dinfo = fit_leg(C4, dctx, FIT_DISTRIBUTED, np.float32, steps)
+            t_k = max_over_ranks(float(np.mean([i.ms_factor for i in infos])))
+            kname = "potrf_tiles_kernel<float, true> (one per rank, sharded)"
+            peak = PEAK_FP32_TFLOPS * world
+        else:
+            ctx = gpr_amd.Context(local_rank)
+            el, infos, st, dinfo = fit_leg(C4, ctx, 0, np.float32, steps)
+            ctx.close()
+            fac = st.get("potrf_tiles", {"ms": 0, "launches": 0})
+            t_k = fac["ms"] / fac["launches"] if fac["launches"] else None
+            kname = "potrf_tiles_kernel<float, false> (Cholesky + forward solve)"
+            peak = PEAK_FP32_TFLOPS
+        alg = n ** 3 / 3.0 + m * float(n) ** 2
+        c4 = {"workload": "C4: GP fit N=32768 d=32 m=1 RationalQuadraticKernel(1,0.3,1) sigma=1.0 fp32, alpha refined "
+                          "in fp64 (BASELINE.json configs[3])",
+              "metric": "GP fits/sec", "value": steps / el, "unit": "fits/s", "ms_per_step": 1e3 * el / steps,
+              "n_gpus": world, "scaling": "strong" if world > 1 else None, "dtype": "f32 (factor) + f64 (refinement)",
+              "refine_steps": int(infos[-1].refine_steps), "refine_delta": float(infos[-1].refine_delta),
+              "ms_refine": float(np.mean([i.ms_refine for i in infos])),
+              "roofline": {"bound": "mfma", "kernel": kname,
+                           "achieved": alg / (t_k * 1e-3) / 1e12 if t_k else None, "peak": peak, "unit": "TFLOP/s",
+                           "frac": alg / (t_k * 1e-3) / 1e12 / peak if t_k else None,
+                           "avg_launch_us": 1e3 * t_k if t_k else None, "algorithmic_flops_per_launch": alg},
+              "dist": dinfo}
+        if rank == 0 and world == 1 and args.cpu_n > 0:
+            from oracle import oracle as O
+            ns = 8192
+            X, Y = make_data(ns, C4["d"], m)
+            t0 = time.perf_counter()
+            O.fit(C4["kernel"], X.astype(np.float32), Y.astype(np.float32), C4["sigma"], np.float32, want_core=False)
+            dt = time.perf_counter() - t0
+            c4["cpu_baseline"] = {"value": 1.0 / (dt * (n / ns) ** 3), "unit": "fits/s", "cores": O.num_threads(),
+                                  "kind": "port", "extrapolated": True,
+                                  "sample": f"1 fit at N={ns} (oracle fp32 path: K in fp32 cast to double, LAPACK "
+                                            f"{O.lapack_name()} getrf+getri) in {dt:.2f} s, EXTRAPOLATED cubically "
+                                            f"to N={n}"}
+        out["C4"] = c4
+    except Exception as e:
+        out["C4"] = {"error": repr(e)}
+    # ---- C5: sparse GP M=2048, N=1e6, d=64 fp64 (dense rows sharded over the ranks) ------------
+    try:
+        n, M_, d = 1_000_000, 2048, 64
+        ks, sig, jit = "GaussianKernel(3,1,)", 0.1, 1e-4
+        X, Y = make_data(n, d, 1)
+        Xm = X[:: n // M_][:M_].copy()
+        rows = np.array_split(np.arange(n), world)[rank]
+        Xl, Yl = X[rows].copy(), Y[rows].copy()
+        del X, Y
+        ctx = dctx if (world > 1 and dctx is not None) else gpr_amd.Context(local_rank)
+        ctx.sparse_fit(ks, Xl, Yl, Xm, sig, jit)
+        steps = max(3, min(args.steps, 5))
+        ctx.set_stats(True)
+        barrier_sync()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            ctx.sparse_fit(ks, Xl, Yl, Xm, sig, jit)
+        barrier_sync()
+        el = max_over_ranks(time.perf_counter() - t0)
+        st = ctx.stats()
+        ctx.set_stats(False)
+        if ctx is not dctx:
+            ctx.close()
+        syrk = st.get("other_gemm", {"ms": 0, "launches": 0, "flops": 0})
+        t_s = max_over_ranks(syrk["ms"] / steps) if syrk["launches"] else None
+        f_syrk = float(len(rows)) * M_ * (M_ + 1)  # the rank's sigma^-2 Knm^T Knm (+ label row), lower
+        flops = 2.0 * n * M_ * d + n * M_ * (M_ + 1) + 2.0 * M_ ** 3
+        c5 = {"workload": "C5: sparse GP fit M=2048 inducing, N=1e6 dense rows, d=64 fp64 GaussianKernel(3,1) "
+                          "sigma=0.1 jitter=1e-4 (BASELINE.json configs[4])",
+              "metric": "sparse GP fits/sec", "value": steps / el, "unit": "fits/s", "ms_per_step": 1e3 * el / steps,
+              "n_gpus": world, "scaling": "strong" if world > 1 else None, "dtype": "f64",
+              "note": "wall time per fit incl. the upload of the rank's rows (0.5 GB / world) and host outputs",
+              "fit_tflops_effective": flops / (el / steps) / 1e12,
+              "roofline": {"bound": "mfma", "kernel": "syrk_splitk_kernel<double> (sigma^-2 Knm^T Knm, k_syrk.hip)",
+                           "achieved": f_syrk / (t_s * 1e-3) / 1e12 if t_s else None, "peak": PEAK_FP64_TFLOPS,
+                           "unit": "TFLOP/s", "frac": f_syrk / (t_s * 1e-3) / 1e12 / PEAK_FP64_TFLOPS if t_s else None,
+                           "avg_launch_us": 1e3 * t_s if t_s else None, "algorithmic_flops_per_launch": f_syrk}}
+        if rank == 0 and world == 1 and args.cpu_n > 0:
+            from oracle import oracle as O
+            ns = 62500
+            t0 = time.perf_counter()
+            O.sparse_fit(ks, Xl[:ns], Yl[:ns], Xm, sig, jit)
+            dt = time.perf_counter() - t0
+            c5["cpu_baseline"] = {"value": 1.0 / (dt * n / ns), "unit": "fits/s", "cores": O.num_threads(),
+                                  "kind": "port", "extrapolated": True,
+                                  "sample": f"1 sparse fit on the first {ns} rows (oracle: Knm build + Knm^T Knm + "
+                                            f"M x M LAPACK inverses) in {dt:.2f} s, scaled LINEARLY in N to {n} rows "
+                                            "(the M x M part counted 16x: an overestimate of the CPU rate's cost)"}
+        out["C5"] = c5
+    except Exception as e:
+        out["C5"] = {"error": repr(e)}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -103,6 +268,7 @@ def main():
     ap.add_argument("--mode", choices=["replicas", "dist"], default="dist",
                     help="N>1 headline: one fit whose matrix is sharded over the GPUs (dist, strong "
                          "scaling) or independent fits per GPU (replicas, weak scaling); both are measured")
+    ap.add_argument("--configs", type=int, default=1, help="also measure BASELINE configs C2, C4, C5 (0 = skip)")
     ap.add_argument("--force-dist", action="store_true",
                     help="testing: run the sharded-fit leg (and make it the headline) even at N = 1")
     args = ap.parse_args()
@@ -166,7 +332,7 @@ def main():
         return max_over_ranks(el), infos, st
 
     # ---- the sharded fit over all ranks (the N > 1 headline) -------------------------------
-    dres, dist_error = None, None
+    dres, dist_error, dctx = None, None, None
     if world > 1 or args.force_dist:
         try:
             uid = [gpr_amd.unique_id() if rank == 0 else None]
@@ -183,7 +349,6 @@ def main():
                 dmodel.lml(grad=True, distributed=True)
                 dres["lml_ms_wall"] = 1e3 * max_over_ranks(time.perf_counter() - tl0)
             dmodel.close()
-            dctx.close()
         except Exception as e:  # reported; the replicas line stands in
             dist_error = repr(e)
             log("distributed fit failed:", dist_error)
@@ -320,6 +485,13 @@ def main():
     traffic = traffic_from_profile() if not headline_dist else None
     fit_ms = float(np.median([i.ms_build + i.ms_factor + i.ms_solve for i in infos]))
 
+    configs = None
+    if args.configs:
+        configs = run_configs(args, world, rank, local_rank, dctx if dist_error is None else None, max_over_ranks,
+                              barrier_sync)
+    if dctx is not None:
+        dctx.close()
+
     if rank == 0:
         cpu = None
         if world == 1 and args.cpu_n > 0:
@@ -343,8 +515,8 @@ def main():
             "config": {"workload": "C3: GP fit N=16384 d=32 m=1 Sum(Gaussian(2,0.15)+Periodic(0.1,pi,1)) "
                                    "sigma=1.0 fp64 (BASELINE.json configs[2])",
                        "n": n, "d": d, "m": m, "kernel": cfg["kernel"],
-                       "parallelism": (f"sharded: row blocks cyclic over {world} GPUs, tile-dataflow per rank, "
-                                       "RCCL broadcast + full-mesh panel exchange" if headline_dist
+                       "parallelism": (f"sharded: row blocks in cyclic groups over {world} GPUs, tile-dataflow per "
+                                       "rank, device-initiated tile pushes over xGMI" if headline_dist
                                        else ("replicas" if world > 1 else "single-gpu"))},
             "roofline": {"bound": "mfma", "kernel": kname,
                          "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
@@ -365,6 +537,7 @@ def main():
             "build": build,
             "lml_grad_sharded_ms_wall": (dres or {}).get("lml_ms_wall"),
             "cpu_baseline": cpu,
+            "configs": configs,
         }
         print(json.dumps(line), flush=True)
     if dist is not None:

@@ -193,7 +193,8 @@ struct DistLayout {
 
 // mailbox byte layout (identical on every rank): see PtDist / DSArgs
 struct MailboxLayout {
-    int64_t o_linv = 0, o_win = 0, o_z = 0, o_alpha = 0, o_zf = 0, o_part = 0, o_flags = 0, o_sflags = 0, bytes = 0;
+    int64_t o_linv = 0, o_win = 0, o_z = 0, o_alpha = 0, o_zf = 0, o_part = 0, o_flags = 0, o_sflags = 0, o_tags = 0,
+            bytes = 0;
     void init(int g, int nc, int nr, int ww, int m, size_t s, bool window) {
         const int64_t DB2 = (int64_t)DB * DB, np = (int64_t)nc * DB;
         int64_t o = 0;
@@ -213,6 +214,8 @@ struct MailboxLayout {
         o = align256(o + 4 * (dist_f_rel(nr, nc) + (int64_t)g * nc));
         o_sflags = o;
         o = align256(o + 4 * ((int64_t)(2 + g) * nc));
+        o_tags = o;
+        o = align256(o + 4 * (window ? (int64_t)ww * nr : 1));
         bytes = o;
     }
 };
@@ -450,7 +453,8 @@ static void setup(DistEngine<T>& E, const DistContext& C, int64_t n, int m, bool
         R->mbox.alloc((size_t)E.MB.bytes, true);
         GPRX_HIP(hipMemset(R->mbox.p, 0, E.MB.bytes));  // flags 0: below every epoch
         R->ctr.alloc(sizeof(int) * ((size_t)C_NCTL_DIST + nr + (size_t)nr * nci + nc), false);
-        R->info.alloc(sizeof(int), false);
+        R->info.alloc(160 * sizeof(int), false);  // info, then the GPRX_DIST_CHECK counters and log
+        GPRX_HIP(hipMemset(R->info.p, 0, 160 * sizeof(int)));
         R->flag.alloc(sizeof(int), false);
         R->red.alloc(sizeof(double) * 4 + sizeof(TileBuild<T>) + 64, false);
         R->sctl.alloc(sizeof(int) * 8, false);
@@ -564,6 +568,9 @@ static PtDist<T> make_ptdist(const DistEngine<T>& E, const DistRank<T>& R) {
     pd.o_win = E.MB.o_win;
     pd.o_z = E.MB.o_z;
     pd.o_flags = E.MB.o_flags;
+    pd.o_tags = E.MB.o_tags;
+    pd.check = std::getenv("GPRX_DIST_CHECK") != nullptr ? 1 : 0;
+    pd.check_err = R.info.template as<int>() + 1;
     return pd;
 }
 
@@ -705,6 +712,20 @@ void dist_fit(DistEngineBase*& eng, const DistContext& C, const DistFitIn<T>& in
         int info, flag;
     };
     Part tot{0, 0, INT_MAX, 0};
+    if (std::getenv("GPRX_DIST_CHECK"))  // the window-slot verification's findings (PtDist::check)
+        for (auto& Rp : E.ranks) {
+            int ce[3 + 1 + 128];
+            GPRX_HIP(hipMemcpy(ce, Rp->info.template as<int>() + 1, sizeof(ce), hipMemcpyDeviceToHost));
+            if (ce[0] || ce[1]) {
+                std::fprintf(stderr, "gprx dist check rank %d fit %u: %d stale window reads, %d slots overwritten during a read:",
+                             Rp->r, E.ep, ce[0], ce[1]);
+                for (int e = 0; e < std::min(ce[2], 32); e++)
+                    std::fprintf(stderr, " [%s: row %d panel %d]", ce[4 + 4 * e] ? "during" : "stale", ce[5 + 4 * e],
+                                 ce[6 + 4 * e]);
+                std::fprintf(stderr, "\n");
+            }
+            GPRX_HIP(hipMemset(Rp->info.template as<int>() + 1, 0, sizeof(ce)));
+        }
     for (auto& Rp : E.ranks) {
         DistRank<T>& R = *Rp;
         DSArgs<T> a = make_dsargs(E, R);

@@ -441,6 +441,9 @@ struct PtDist {
     const uint64_t* mb;        // [g] mailbox base of every rank (as mapped in this process)
     // mailbox byte offsets (the same on every rank)
     int64_t o_linv, o_win, o_z, o_flags;
+    int64_t o_tags;            // GPRX_DIST_CHECK: per window slot (panel, row) the tag of its occupant
+    int check;                 // GPRX_DIST_CHECK: verify every window read against the slot's tag
+    int* check_err;            // [2] window reads of a stale slot / of a slot overwritten during the read
     // flag words in the mailbox (unsigned, from o_flags): tile (j, b) received at
     // [F_TILE + j * nc + b], Linv_k at [F_LINV(nr, nc) + k], panel p released by rank q at
     // [F_REL(nr, nc) + q * nc + p]
@@ -541,13 +544,6 @@ template <typename T>
 void potrf_auto(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info, Exec& ex);
 bool potrf_uses_tiles();
 int64_t potrf_tiles_schedule_stats(int nc, int nr, int P, bool build, double* est_us, int ni = 0);
-// Multi-GPU form: column panels of outer_block() columns dealt cyclically over `world`
-// ranks (np must be a multiple of outer_block()); the factored panels are RCCL-broadcast so
-// every rank ends with the full factor.  pack: device scratch of nrows * outer_block().
-template <typename T>
-void potrf_dist(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info, Exec& ex, ncclComm_t comm, int rank,
-                int world, T* pack);
-
 // Generic C = beta C + alpha A B^T on GT-multiples (column-major).  lower: only tiles
 // with col-tile <= row-tile are computed, and inside diagonal tiles only row >= col.
 template <typename T>

@@ -698,80 +698,6 @@ void potrf_blocked(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* in
 }
 
 // ======================================================================================
-// Multi-GPU factorisation (one process per GPU, RCCL over xGMI).
-//
-// Column panels of NBO columns are dealt cyclically: panel K belongs to rank K mod W, which
-// builds it, applies every update to it, factors it (potrf_panel) and RCCL-broadcasts the
-// factored panel (rows c0.., packed) with its diagonal-block inverses.  Every rank unpacks
-// it into its full-size copy of the matrix and updates the later panels it owns, the next
-// panel first so its owner can factor it while the rest of the updates run (look-ahead:
-// main stream = factor + broadcast, aux stream = updates).  The trailing-update flops
-// (n^3/3) are split W ways; the factor ends up replicated, so the solve, logdet and predict
-// run locally on every rank.  The step's exchange is one broadcast of (n - c0) x NBO + NBO x
-// 128 values.
-// ======================================================================================
-template <typename T>
-static ncclDataType_t rccl_type();
-template <>
-ncclDataType_t rccl_type<double>() {
-    return ncclFloat64;
-}
-template <>
-ncclDataType_t rccl_type<float>() {
-    return ncclFloat32;
-}
-
-static void rccl_check(ncclResult_t r, const char* what) {
-    if (r != ncclSuccess) throw Error{GPRX_ERR_RCCL, std::string(what) + ": " + ncclGetErrorString(r)};
-}
-
-template <typename T>
-void potrf_dist(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info, Exec& ex, ncclComm_t comm, int rank,
-                int world, T* pack) {
-    const int64_t NBO = outer_block();
-    hipStream_t S0 = ex.s0, S1 = ex.s1 ? ex.s1 : ex.s0;
-    const int64_t nK = np / NBO;
-    auto owner = [&](int64_t K) { return (int)(K % world); };
-    for (int64_t K = 0; K < nK; K++) {
-        const int64_t c0 = K * NBO, rows = nrows - c0;
-        const int root = owner(K);
-        if (root == rank) {
-            if (K > 0 && S1 != S0) GPRX_HIP(hipStreamWaitEvent(S0, ex.event(2 * K), 0));  // panel K updated
-            potrf_panel<T>(A, ld, nrows, c0, NBO, Linv, info, S0, 0);
-            GPRX_HIP(hipMemcpy2DAsync(pack, sizeof(T) * rows, A + c0 + c0 * ld, sizeof(T) * ld, sizeof(T) * rows, NBO,
-                                      hipMemcpyDeviceToDevice, S0));
-        }
-        if (world > 1) {
-            T* Lk = Linv + (c0 / DB) * (int64_t)DB * DB;
-            rccl_check(ncclGroupStart(), "ncclGroupStart");
-            rccl_check(ncclBroadcast(pack, pack, (size_t)(rows * NBO), rccl_type<T>(), root, comm, S0), "ncclBroadcast");
-            rccl_check(ncclBroadcast(Lk, Lk, (size_t)(NBO * DB), rccl_type<T>(), root, comm, S0), "ncclBroadcast");
-            rccl_check(ncclGroupEnd(), "ncclGroupEnd");
-            if (root != rank)
-                GPRX_HIP(hipMemcpy2DAsync(A + c0 + c0 * ld, sizeof(T) * ld, pack, sizeof(T) * rows, sizeof(T) * rows, NBO,
-                                          hipMemcpyDeviceToDevice, S0));
-        }
-        if (K == nK - 1) break;
-        // updates of this rank's later panels with panel K (aux stream), next panel first
-        GPRX_HIP(hipEventRecord(ex.event(2 * K + 1), S0));
-        if (S1 != S0) GPRX_HIP(hipStreamWaitEvent(S1, ex.event(2 * K + 1), 0));
-        const T* Pan = A + c0 * ld;
-        for (int64_t J = K + 1; J < nK; J++) {
-            if (owner(J) != rank) continue;
-            const int64_t cj = J * NBO;
-            launch_gemm_nt<T>(A + cj + cj * ld, ld, Pan + cj, ld, Pan + cj, ld, nrows - cj, NBO, NBO, T(-1), T(1), true,
-                              S1);
-            if (J == K + 1) GPRX_HIP(hipEventRecord(ex.event(2 * (K + 1)), S1));
-        }
-    }
-    if (S1 != S0) {
-        GPRX_HIP(hipEventRecord(ex.event(2 * nK + 1), S1));
-        GPRX_HIP(hipStreamWaitEvent(S0, ex.event(2 * nK + 1), 0));
-    }
-    if (world > 1) rccl_check(ncclAllReduce(info, info, 1, ncclInt32, ncclMin, comm, S0), "ncclAllReduce");
-}
-
-// ======================================================================================
 // Back substitution  L^T alpha = z   (z: m rows of length np, alpha: np x m row-major)
 // ======================================================================================
 template <typename T>
@@ -930,7 +856,6 @@ void launch_fit_reductions(const T* A, int64_t ld, int64_t n, int64_t np, int m,
 #define GPRX_INST(T)                                                                                      \
     template void potrf_blocked<T>(T*, int64_t, int64_t, int64_t, T*, int*, Exec&);                      \
     template void potrf_auto<T>(T*, int64_t, int64_t, int64_t, T*, int*, Exec&);                         \
-    template void potrf_dist<T>(T*, int64_t, int64_t, int64_t, T*, int*, Exec&, ncclComm_t, int, int, T*);   \
     template void launch_gemm_nt_splitk<T>(T*, int64_t, int64_t, const T*, int64_t, const T*, int64_t,   \
                                            int64_t, int64_t, int64_t, int, T, bool, hipStream_t);         \
     template void launch_gemm_nt<T>(T*, int64_t, const T*, int64_t, const T*, int64_t, int64_t, int64_t, \

@@ -1271,7 +1271,8 @@ __device__ bool dist_wait_release(const Args<T>& a, const PtDist<T>& D, unsigned
 // drained: its stores are visible to this CU) to byte offset `off` of the mailbox of every
 // rank in `mask`, then release (system scope) and set each one's flag word `fidx` to the epoch.
 template <typename T>
-__device__ void dist_push(const T* src, const PtDist<T>& D, unsigned mask, int64_t off, int64_t fidx, const int t) {
+__device__ void dist_push(const T* src, const PtDist<T>& D, unsigned mask, int64_t off, int64_t fidx, const int t,
+                          int64_t tag_idx = -1, unsigned tag = 0) {
     if (!mask) return;
     typedef unsigned int u4 __attribute__((ext_vector_type(4)));
     constexpr int NV = DB * DB * (int)sizeof(T) / 16 / NT;  // 16-byte vectors per thread
@@ -1296,8 +1297,35 @@ __device__ void dist_push(const T* src, const PtDist<T>& D, unsigned mask, int64
     if (wave_id() == 0) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (D.check && tag_idx >= 0)
+            for (int q = 0; q < D.g; q++)
+                if ((mask >> q) & 1) st_sys(reinterpret_cast<unsigned*>(dist_mb(D, q, D.o_tags)) + tag_idx, tag);
         for (int q = 0; q < D.g; q++)
             if ((mask >> q) & 1) st_sys(dist_flags(D, q) + fidx, D.ep);
+    }
+}
+
+// GPRX_DIST_CHECK: the window slots of row j, panels b0.. b0 + nb - 1, hold exactly those tiles
+// of this fit (tag = epoch << 16 | panel + 1); counts mismatches into check_err[which]
+template <typename T>
+__device__ void dist_check_tags(const PtDist<T>& D, int j, int b0, int nb, int which) {
+    const int lane = threadIdx.x & 63;
+    if (lane < nb) {
+        const int b = b0 + lane;
+        const unsigned* tg = reinterpret_cast<const unsigned*>(dist_mb(D, D.r, D.o_tags)) + (int64_t)(b % D.ww) * D.nr + j;
+        const unsigned want = (D.ep << 16) | (unsigned)(b + 1);
+        const unsigned got = ld_sys(tg);
+        if (got != want) {
+            atomicAdd(D.check_err + which, 1);
+            const int e = atomicAdd(D.check_err + 2, 1);
+            if (e < 32) {  // log: which, row, panel, time
+                int* lg = D.check_err + 4 + 4 * e;
+                lg[0] = which;
+                lg[1] = j;
+                lg[2] = b;
+                lg[3] = (int)(wall_clock64() & 0x7fffffff);
+            }
+        }
     }
 }
 
@@ -1305,15 +1333,17 @@ __device__ void dist_push(const T* src, const PtDist<T>& D, unsigned mask, int64
 // chunk completing a panel's count stores the release flag into every other rank's mailbox.
 template <typename T>
 __device__ void dist_release(const PtDist<T>& D, int b0, int nb) {
+    // lane l < nb counts the chunk on panel b0 + l (its own counter word); the others add 0.
+    // Integer masks throughout: the 64-bit ballot / count-trailing-zeros form of this loop was
+    // seen to release panel b0 + 32 together with panel b0 (lane 32 of a 32-wide chunk).
     const int lane = threadIdx.x & 63;
-    const int p = b0 + (lane < nb ? lane : 0);
-    const int old = __hip_atomic_fetch_add(D.ucnt + p, lane < nb ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const bool done = lane < nb && old + 1 == D.need[(int64_t)D.r * D.nc + p];
-    uint64_t m = __builtin_amdgcn_read_exec() & __ballot(done);
-    m = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(m >> 32)) << 32) | __builtin_amdgcn_readfirstlane((uint32_t)m);
-    while (m) {
-        const int l = __builtin_ctzll(m);
-        m &= m - 1;
+    const int valid = lane < nb ? 1 : 0;
+    const int p = b0 + (valid ? lane : 0);
+    const int old = __hip_atomic_fetch_add(D.ucnt + p, valid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int needv = D.need[(int64_t)D.r * D.nc + p];
+    const int dn = valid & (old + 1 == needv ? 1 : 0);
+    for (int l = 0; l < nb; l++) {
+        if (!__builtin_amdgcn_readfirstlane(__shfl(dn, l))) continue;
         for (int q = 0; q < D.g; q++)
             if (q != D.r) st_sys(dist_flags(D, q) + dist_f_rel(D.nr, D.nc) + (int64_t)D.r * D.nc + b0 + l, D.ep);
     }
@@ -1593,9 +1623,11 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
                 const bool loc = lj >= 0;
                 const T* Bop = loc ? dist_tile(a.A, D, j, b0) : nullptr;
                 const uint64_t* bp = loc ? nullptr : D.tptr + (int64_t)j * D.nc + b0;
+                if (D.check && !loc && wv == 0) dist_check_tags(D, j, b0, nb, 0);
                 tile_gemm<T, true>(dist_tile(a.A, D, i, j), DB, dist_tile(a.A, D, i, b0), DB, Bop, DB, nb * GT, i == j,
                                    smem, tid, false, bp);
                 publish(a.ver + (int64_t)i * a.nv + dist_col(D.nc, j), b0 + nb, false);
+                if (D.check && !loc && wv == 0) dist_check_tags(D, j, b0, nb, 1);
                 if (!loc && wv == 0) dist_release(D, b0, nb);  // this chunk's window reads are done
             } else if (type == T_TRSM) {
                 T* Cik = dist_tile(a.A, D, i, j);
@@ -1613,7 +1645,8 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
                     ok = __builtin_amdgcn_readfirstlane(s_ok) != 0;
                     if (ok)
                         dist_push(Cik, D, cm, D.o_win + ((int64_t)(j % D.ww) * D.nr + i) * DB * DB * (int64_t)sizeof(T),
-                                  dist_f_tile() + (int64_t)i * D.nc + j, tid);
+                                  dist_f_tile() + (int64_t)i * D.nc + j, tid, (int64_t)(j % D.ww) * D.nr + i,
+                                  (D.ep << 16) | (unsigned)(j + 1));
                 }
             } else {  // DIAGX(k = i)
                 const int k = i;
@@ -1646,9 +1679,13 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
                 }
                 const int64_t owin = D.o_win + ((int64_t)((k - 1 + D.ww) % D.ww) * D.nr + k) * DB * DB * (int64_t)sizeof(T);
                 const int64_t olinv = D.o_linv + (int64_t)k * DB * DB * (int64_t)sizeof(T);
-                if (ok && k > 0) dist_push(Akm, D, cm & first, owin, dist_f_tile() + (int64_t)k * D.nc + (k - 1), tid);
+                const int64_t tix = (int64_t)((k - 1 + D.ww) % D.ww) * D.nr + k;
+                const unsigned tgv = (D.ep << 16) | (unsigned)k;
+                if (ok && k > 0)
+                    dist_push(Akm, D, cm & first, owin, dist_f_tile() + (int64_t)k * D.nc + (k - 1), tid, tix, tgv);
                 if (ok) dist_push(a.Linv + (int64_t)k * DB * DB, D, all & first, olinv, dist_f_linv(D.nr, D.nc) + k, tid);
-                if (ok && k > 0) dist_push(Akm, D, cm & ~first, owin, dist_f_tile() + (int64_t)k * D.nc + (k - 1), tid);
+                if (ok && k > 0)
+                    dist_push(Akm, D, cm & ~first, owin, dist_f_tile() + (int64_t)k * D.nc + (k - 1), tid, tix, tgv);
                 if (ok) dist_push(a.Linv + (int64_t)k * DB * DB, D, all & ~first, olinv, dist_f_linv(D.nr, D.nc) + k, tid);
             }
             if (!ok) break;

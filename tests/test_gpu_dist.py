@@ -311,6 +311,35 @@ def test_virtual_ranks_small_window(monkeypatch):
         vctx.close()
 
 
+@pytest.mark.parametrize("g,ww", [(6, 64), (8, 16), (5, 4)])
+def test_virtual_ranks_window_slots_verified(g, ww, monkeypatch, capfd):
+    """GPRX_DIST_CHECK: every window read is verified against a tag the producer wrote with the
+    tile (this fit's epoch and the panel) before and after the read -- a slot refilled before
+    its consumers released it shows up as a stale or overwritten read.  Repeated fits at C3
+    size with windows smaller than the matrix (every slot reused), 5-8 ranks."""
+    import gpr_amd
+    monkeypatch.setenv("GPRX_DIST_CHECK", "1")
+    monkeypatch.setenv("GPRX_DIST_WINDOW", str(ww))
+    n, d, sigma = 16384 if g > 5 else 8192, 32, 1.0
+    X, Y = make_data(n, d, 1)
+    a_ref = _single_alpha(X, Y, sigma)
+    vctx = gpr_amd.Context(0, virtual=g)
+    try:
+        M = gpr_amd.Model(vctx, np.float64)
+        M.set_data(X, Y)
+        M.set_kernel(C3K)
+        M.set_noise(sigma)
+        for _ in range(3):
+            M.fit()
+            assert relerr(M.alpha(), a_ref) <= 1e-10
+        assert M.dist_info()["ww"] == ww
+        err = capfd.readouterr().err
+        assert "stale window reads" not in err, err
+        M.close()
+    finally:
+        vctx.close()
+
+
 @pytest.mark.parametrize("g", [2, 4])
 def test_virtual_ranks_storage_is_sharded(g):
     """Per-rank device memory of the sharded fit: the packed lower tiles of the rank's own row
