@@ -79,8 +79,10 @@ def cpu_baseline(cfg, n_cpu):
 
 def traffic_from_profile(kernels=("potrf_tiles_kernel<double, false>", "potrf_tiles_kernel<double>")):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC passes
-    (profiles/*_pmc_traffic.json, written by scripts/pmc_traffic.py: FETCH_SIZE x 2 (gfx950
-    wide-read correction, MI355X_MICROARCH.md §HBM) + WRITE_SIZE, averaged over launches)."""
+    (profiles/*_pmc_traffic.json, written by scripts/pmc_traffic.py).  L2-fabric bytes:
+    FETCH_SIZE x 2 -- the gfx950 correction for 16-B-per-lane streaming reads, which is how the
+    tile kernel reads all of its operands (MI355X_MICROARCH.md §HBM) -- + WRITE_SIZE, averaged
+    over launches; Infinity-Cache hits are included, so this bounds HBM bytes from above."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
     for path in reversed(files):
@@ -523,9 +525,11 @@ def main():
                          "frac": achieved / peak,
                          "avg_launch_us": 1e3 * avg_ms if avg_ms else None,
                          "algorithmic_flops_per_launch": alg_flops,
-                         # HBM bytes per launch from the committed PMC passes (FETCH_SIZE x 2 +
-                         # WRITE_SIZE, MI355X_MICROARCH.md), null if none is committed
+                         # L2-fabric bytes per launch from the committed PMC passes (FETCH_SIZE x 2
+                         # for the 16 B/lane operand feed + WRITE_SIZE; MALL hits included, so an
+                         # upper bound on HBM bytes), null if none is committed
                          "traffic": (traffic["bytes_per_launch"] if traffic else None),
+                         "traffic_kind": "l2_fabric_bytes",
                          "traffic_source": (traffic["source"] if traffic else None)},
             "fit_roofline": {"t_roof_ms": t_roof, "gpus": g_roof, "t_fit_device_ms": fit_ms, "frac": t_roof / fit_ms},
             "replicas": replicas if world > 1 else None,

@@ -177,6 +177,10 @@ struct DevBuf {
         if (b == 0) return;
         GPRX_HIP(hipMalloc(&p, b));
         bytes = b;
+        // GPRX_POISON (debugging): fresh buffers hold finite garbage (bytes 0x41: 12.1f, 2.3e6),
+        // as reused memory does, so a read of unwritten memory shows in the results
+        static const bool poison = std::getenv("GPRX_POISON") != nullptr;
+        if (poison) GPRX_HIP(hipMemset(p, 0x41, b));
     }
     void release() {
         if (p) (void)hipFree(p);

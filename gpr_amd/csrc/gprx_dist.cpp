@@ -68,6 +68,8 @@ struct DMem {
         if (fine) GPRX_HIP(hipExtMallocWithFlags(&p, b, hipDeviceMallocFinegrained));
         else GPRX_HIP(hipMalloc(&p, b));
         bytes = b;
+        static const bool poison = std::getenv("GPRX_POISON") != nullptr;  // (debugging, as DevBuf)
+        if (poison) GPRX_HIP(hipMemset(p, 0x41, b));
     }
     void release() {
         if (p) (void)hipFree(p);
@@ -329,6 +331,23 @@ __global__ __launch_bounds__(256) void dist_gather_kernel(const uint64_t* __rest
         const int r = e & (DB - 1), c = e >> 7;
         d[r + (int64_t)c * ld] = s[e];
     }
+}
+
+// out of a mailbox (alpha, Linv) into ordinary memory: system-scope loads.  A plain copy
+// (hipMemcpy D2D) of a mailbox that the ranks' kernels wrote from other XCDs was seen to return
+// the previous solve's values (alpha + 2 delta_1 in place of alpha + delta_1 + delta_2 in the
+// fp32 refinement, one run in six; stale columns in an m = 2 fit).
+template <typename T>
+__global__ __launch_bounds__(256) void dist_copy_sys(const T* __restrict__ src, T* __restrict__ dst, int64_t count) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < count) dst[e] = __hip_atomic_load(src + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+template <typename T>
+void copy_from_mailbox(const void* src, T* dst, int64_t count, hipStream_t s) {
+    if (count <= 0) return;
+    hipLaunchKernelGGL(dist_copy_sys<T>, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, s,
+                       reinterpret_cast<const T*>(src), dst, count);
+    GPRX_HIP(hipGetLastError());
 }
 
 }  // namespace
@@ -741,6 +760,18 @@ void dist_fit(DistEngineBase*& eng, const DistContext& C, const DistFitIn<T>& in
         tot.info = std::min(tot.info, hi);
         tot.flag = std::max(tot.flag, hf);
     }
+    if (tot.info != INT_MAX && tot.info < 0)  // a timed-out wait: where each rank stood
+        for (auto& Rp : E.ranks) {
+            int rec[8], tk = 0;
+            GPRX_HIP(hipMemcpy(rec, Rp->info.template as<int>() + 1 + 132, sizeof(rec), hipMemcpyDeviceToHost));
+            GPRX_HIP(hipMemcpy(&tk, Rp->ctr.p, sizeof(int), hipMemcpyDeviceToHost));
+            std::fprintf(stderr,
+                         "gprx dist timeout rank %d/%d fit %u: tickets %d of %d; first timed-out wait: kind %d type %d "
+                         "i %d j %d b0 %d nb %d detail 0x%x seen %d (ww %d gb %d P %d)\n",
+                         Rp->r, E.g, E.ep, tk, Rp->ntasks, rec[0], rec[1], rec[2], rec[3], rec[4] & 0xffff, rec[4] >> 16,
+                         rec[5], rec[6], E.ww, E.gb, E.P);
+            GPRX_HIP(hipMemset(Rp->info.template as<int>() + 1 + 132, 0, sizeof(rec)));
+        }
     if (!E.virt && E.g > 1) {  // across the processes (rank order: identical sums everywhere)
         std::vector<Part> all(E.g);
         E.hc->allgather(&tot, sizeof(Part), all.data());
@@ -799,8 +830,8 @@ void dist_fit(DistEngineBase*& eng, const DistContext& C, const DistFitIn<T>& in
         return;
     }
     const DistRank<T>& R0 = *E.ranks[0];
-    GPRX_HIP(hipMemcpy(alpha_dev, R0.mbox.template as<char>() + E.MB.o_alpha, sizeof(T) * np * E.m,
-                       hipMemcpyDeviceToDevice));
+    copy_from_mailbox<T>(R0.mbox.template as<char>() + E.MB.o_alpha, alpha_dev, np * E.m, R0.s);
+    GPRX_HIP(hipStreamSynchronize(R0.s));
 }
 
 // ---------------------------------------------------------------------------------------
@@ -837,7 +868,7 @@ void dist_solve(DistEngineBase* eng, const T* rhs, T* out, hipStream_t s) {
     }
     if (hinfo != INT_MAX) throw Error{GPRX_ERR_HIP, "gprx: distributed solve timed out (flag wait)"};
     const DistRank<T>& R0 = *E.ranks[0];
-    GPRX_HIP(hipMemcpy(out, R0.mbox.template as<char>() + E.MB.o_alpha, sizeof(T) * E.np * E.m, hipMemcpyDeviceToDevice));
+    copy_from_mailbox<T>(R0.mbox.template as<char>() + E.MB.o_alpha, out, E.np * E.m, s);
 }
 template void dist_solve<double>(DistEngineBase*, const double*, double*, hipStream_t);
 template void dist_solve<float>(DistEngineBase*, const float*, float*, hipStream_t);
@@ -865,8 +896,7 @@ void dist_gather_factor(DistEngineBase* eng, T* A, int64_t ld, T* Linv, hipStrea
     if (nc > 1)
         hipLaunchKernelGGL(dist_gather_kernel<T>, dim3((unsigned)nc, (unsigned)nc), dim3(256), 0, s,
                            tab.as<uint64_t>(), nc, A, ld);
-    GPRX_HIP(hipMemcpyAsync(Linv, R0.mbox.template as<char>() + E.MB.o_linv, sizeof(T) * (size_t)nc * DB2,
-                            hipMemcpyDeviceToDevice, s));
+    copy_from_mailbox<T>(R0.mbox.template as<char>() + E.MB.o_linv, Linv, (int64_t)nc * DB2, s);
     GPRX_HIP(hipStreamSynchronize(s));
     GPRX_HIP(hipGetLastError());
 }

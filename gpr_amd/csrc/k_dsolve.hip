@@ -108,6 +108,9 @@ __global__ __launch_bounds__(NT) void dist_back_kernel(DSArgs<T> a) {
     if ((t >> 6) == 0) {
         const int v = __hip_atomic_fetch_add(a.ctl + C_TICKET, (t == 0) ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         s_int[0] = __builtin_amdgcn_readfirstlane(v);
+        // no line of an earlier solve's mailbox traffic (or right-hand side) left in this CU's
+        // or this XCD's caches: the plain loads below (Linv, rhs, own tiles) see this solve's data
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     }
     __syncthreads();
     const int tk = __builtin_amdgcn_readfirstlane(s_int[0]);
@@ -122,6 +125,7 @@ __global__ __launch_bounds__(NT) void dist_back_kernel(DSArgs<T> a) {
     const bool has = a.last_own > k;
     bool ok = true;
     auto agree = [&](bool good) {
+        __syncthreads();  // every thread has read the previous verdict
         if (t == 0) s_int[1] = 0;
         __syncthreads();
         if (!good && lane == 0) s_int[1] = 1;
@@ -162,6 +166,7 @@ __global__ __launch_bounds__(NT) void dist_back_kernel(DSArgs<T> a) {
 #pragma unroll
                 for (int u = 0; u < QR; u++) s = fma(L[u], ld_nc(ai + (int64_t)(QR * qq + u) * a.m + r), s);
             }
+            __syncthreads();  // every thread done reading the previous right-hand side's s_part
             s_part[qq][c] = s;
             if (!agree(ok)) break;
             const T w = (t < DB) ? s_part[0][t] + s_part[1][t] + s_part[2][t] + s_part[3][t] : T(0);
@@ -225,6 +230,9 @@ __global__ __launch_bounds__(NT) void dist_forward_kernel(DSArgs<T> a) {
     if ((t >> 6) == 0) {
         const int v = __hip_atomic_fetch_add(a.ctl + C_TICKET, (t == 0) ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         s_int[0] = __builtin_amdgcn_readfirstlane(v);
+        // no line of an earlier solve's mailbox traffic (or right-hand side) left in this CU's
+        // or this XCD's caches: the plain loads below (Linv, rhs, own tiles) see this solve's data
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     }
     __syncthreads();
     const int i = __builtin_amdgcn_readfirstlane(s_int[0]);
@@ -234,6 +242,7 @@ __global__ __launch_bounds__(NT) void dist_forward_kernel(DSArgs<T> a) {
     T* my_z = mb_ptr<T>(a, a.r, a.o_zf);
     bool ok = true;
     auto agree = [&](bool good) {
+        __syncthreads();  // every thread has read the previous verdict
         if (t == 0) s_int[1] = 0;
         __syncthreads();
         if (!good && lane == 0) s_int[1] = 1;
@@ -254,6 +263,7 @@ __global__ __launch_bounds__(NT) void dist_forward_kernel(DSArgs<T> a) {
 #pragma unroll
                 for (int u = 0; u < QR; u++) s = fma(L[u], ld_nc(zk + (int64_t)(QR * cq + u) * a.m), s);
             }
+            __syncthreads();
             s_part[cq][row] = s;
             if (!agree(ok)) break;
             if (t < DB) s_v[t] = a.rhs[((int64_t)i * DB + t) * a.m + r] - (s_part[0][t] + s_part[1][t] + s_part[2][t] + s_part[3][t]);

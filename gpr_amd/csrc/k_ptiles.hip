@@ -1206,6 +1206,24 @@ __device__ __forceinline__ void st_sys(unsigned* p, unsigned v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// A timed-out wait of the distributed factorisation leaves one record (the first) at
+// check_err[DIST_TO_REC..+7]: kind (1 inputs, 2 window release), task type, i, j, b0 | nb << 16,
+// detail (inputs: bit mask of the unmet conditions; release: the consumer rank), the value seen,
+// the ticket.  gprx_dist.cpp prints it with the fit's timeout error.
+constexpr int DIST_TO_REC = 132;
+__device__ __forceinline__ void dist_note_timeout(int* rec, int kind, int type, int i, int j, int b0nb, int detail,
+                                                  int seen) {
+    if (!rec) return;
+    if (__hip_atomic_fetch_add(rec, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
+    if (atomicCAS(rec, 0, kind) != 0) return;
+    rec[1] = type;
+    rec[2] = i;
+    rec[3] = j;
+    rec[4] = b0nb;
+    rec[5] = detail;
+    rec[6] = seen;
+}
+
 // ---- distributed factorisation (DIST): packed storage, mailbox pushes -----------------------
 // tile (i, j) of this rank's own row block i in the packed storage (ld DB): matrix / label rows
 // keep columns 0..i, identity row E_a = nc + 1 + a columns a..nc-1, then C columns E_0..E_a
@@ -1255,9 +1273,11 @@ __device__ bool dist_wait_release(const Args<T>& a, const PtDist<T>& D, unsigned
     const long long t0 = wall_clock64();
     for (int q = 0; q < D.g; q++) {
         if (!((mask >> q) & 1) || __builtin_amdgcn_readfirstlane(D.need[(int64_t)q * D.nc + p]) == 0) continue;
-        while (__builtin_amdgcn_readfirstlane(ld_sys(fl + (int64_t)q * D.nc + p)) != D.ep) {
+        unsigned seen;
+        while ((seen = __builtin_amdgcn_readfirstlane(ld_sys(fl + (int64_t)q * D.nc + p))) != D.ep) {
             if (ld_uni(a.ctl + C_ERR)) return false;
             if (wall_clock64() - t0 > a.tlimit) {
+                if ((threadIdx.x & 63) == 0) dist_note_timeout(D.check_err + DIST_TO_REC, 2, -1, D.r, p, 0, q, (int)seen);
                 st_agent(a.ctl + C_ERR, 1);
                 return false;
             }
@@ -1448,6 +1468,20 @@ __device__ bool wait_inputs(const Args<T>& a, int type, int i, int j, int b0, in
         if (ok) return true;
         if (ld_uni(a.ctl + C_ERR)) return false;
         if (wall_clock64() - t0 > a.tlimit) {
+            if constexpr (DIST) {
+                int miss = int(ld_uni(vp) != vwant) | (int(ld_uni(vp2) != vwant2) << 1) | (int(ld_uni(lp1) < lwant1) << 2) |
+                           (int(ld_uni(lp2) < lwant2) << 3);
+                int seen = ld_uni(vp);
+                if (rp) {
+                    const bool good = lane >= rn || ld_sys(rp + (lane < rn ? lane : 0)) == ep;
+                    const unsigned long long bad = __ballot(!good);
+                    if (bad) {
+                        miss |= 16 | ((int)__builtin_ctzll(bad) << 8);
+                        seen = (int)__builtin_amdgcn_readfirstlane(ld_sys(rp + (int)__builtin_ctzll(bad)));
+                    }
+                }
+                if (lane == 0) dist_note_timeout(a.dist->check_err + DIST_TO_REC, 1, type, i, j, b0 | (nb << 16), miss, seen);
+            }
             st_agent(a.ctl + C_ERR, 1);
             return false;
         }
