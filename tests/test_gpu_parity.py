@@ -176,6 +176,22 @@ def test_lml_gradient_f32(ctx, ks):
     assert relerr(g, gr) <= 1e-3
 
 
+def test_lml_gradient_f32_c3_tree_4096(ctx):
+    """The fp32 LML gradient at a C3-shaped size (the C3 tree, d = 32, N = 4096) against the
+    oracle's fp32 path (K in float, inverted in double: include/LAPACKUtils.h:85-97) at the
+    BASELINE fp32 tolerance.  Measured 5.6e-7 here and 7.4e-6 against the fp64 model at
+    N = 16384 (profiles/r03c_lml_f32_error.jsonl)."""
+    ks = "SumKernel(GaussianKernel(2,0.15,),PeriodicKernel(0.1,3.141592653589793,1,))"
+    n, d, sigma = 4096, 32, 1.0
+    X, Y = make_data(n, d)
+    X32, Y32 = X.astype(np.float32), Y.astype(np.float32)
+    M, _ = _fit(ctx, ks, X32, Y32, sigma, np.float32)
+    v, g, _ = M.lml(grad=True)
+    vr, gr, _, _ = O.lml(ks, X32, Y32, sigma, np.float32)
+    assert abs(v - vr) <= 1e-3 * abs(vr)
+    assert relerr(g, gr) <= 1e-3
+
+
 def test_nonfinite_kernel_matrix(ctx):
     import gpr_amd
     X = np.array([[0.0], [np.inf]])
