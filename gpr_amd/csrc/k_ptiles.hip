@@ -1835,10 +1835,31 @@ struct Schedule {
 // the diagonal chain waits for, still go one at a time.
 // s > 0 (an identity row block of the inverse, whose panels before s are zero): the same
 // rule on the panels [s, e), shifted.
-static void tile_chunks(int i, int j, int W, int near, std::vector<std::pair<int, int>>& out, int s = 0) {
+// ratio > 0 (chosen per shape by the simulated makespan, potrf_tiles): greedy from the first
+// panel, the widest power-of-two piece p <= W (W-aligned when p == W) that ends at least `near`
+// panels before e and is at most ratio x the panels left after it.  A piece can start only
+// when its last panel is final, so a wide piece close to the tile's last panel holds up the
+// tile's consumer: at N = 4096 the [0, 16) piece of tiles (18, 17) and (18, 18) became ready
+// with panel 15 and ran 280 us, and DIAGX(18) waited 184 us for it (r03 trace).
+static void tile_chunks(int i, int j, int W, int near, std::vector<std::pair<int, int>>& out, int s = 0,
+                        int ratio = 0) {
     out.clear();
     const int e = ((i == j) ? j - 1 : j) - s;
     if (e <= 0) return;
+    if (ratio > 0) {
+        for (int b = 0; b < e;) {
+            int p = W;
+            for (; p > 1; p /= 2) {
+                if (p == W && b % W) continue;
+                const int end = b + p;
+                if (end > e - near || p > ratio * (e - end)) continue;
+                break;
+            }
+            out.push_back({s + b, p});
+            b += p;
+        }
+        return;
+    }
     int hb = std::max(0, std::min(W * ((j - s) / W), e));
     hb -= hb % W;
     int b = 0;
@@ -1853,7 +1874,8 @@ static void tile_chunks(int i, int j, int W, int near, std::vector<std::pair<int
 
 // ni > 0: the last ni row blocks are the identity (the inverse L^{-1} riding along as
 // L^{-T} rows): identity block a = i - (nr - ni) has zero L blocks before column block a.
-static Schedule make_schedule(int nc, int nr, int W, int near, int P, const Cost& cm, bool build, int ni = 0) {
+static Schedule make_schedule(int nc, int nr, int W, int near, int P, const Cost& cm, bool build, int ni = 0,
+                              int ratio = 0) {
     const int nr0 = nr - ni;
     auto start_of = [&](int i) { return i >= nr0 ? i - nr0 : 0; };
     std::vector<Task> tasks;
@@ -1894,7 +1916,7 @@ static Schedule make_schedule(int nc, int nr, int W, int near, int P, const Cost
         std::vector<std::pair<int, int>> ch;
         for (int j = 1; j < nc; j++)
             for (int i = j; i < nr; i++) {
-                tile_chunks(i, j, W, near, ch, start_of(i));
+                tile_chunks(i, j, W, near, ch, start_of(i), ratio);
                 for (auto& c : ch) by_last[c.first + c.second - 1].push_back(Chunk{i, j, c.first, c.second});
             }
     }
@@ -2039,7 +2061,7 @@ static void c_chunks(int a, int W, int nc, std::vector<std::pair<int, int>>& out
 }
 
 static DistSched make_schedule_dist(int nc, bool inv, int W, int near, int P, int g, int gb, int ww, const Cost& cm,
-                                    bool build, double push_us, double rel_us) {
+                                    bool build, double push_us, double rel_us, int ratio = 0) {
     const int nr = nc + 1 + (inv ? nc : 0), nci = inv ? 2 * nc : nc;
     auto own = [&](int i) { return i <= nc ? (i / gb) % g : ((i - nc - 1) / gb) % g; };
     auto colx = [&](int j) { return j > nc ? j - 1 : j; };  // counter column of tile (., j)
@@ -2083,7 +2105,7 @@ static DistSched make_schedule_dist(int nc, bool inv, int W, int near, int P, in
         for (int j = 1; j < nc; j++)
             for (int i = j; i < nr; i++) {
                 if (i > nc && start_of(i) >= j) continue;  // identity row E_a: tiles (E_a, j > a) only
-                tile_chunks(i, j, W, near, ch, start_of(i));
+                tile_chunks(i, j, W, near, ch, start_of(i), ratio);
                 for (auto& c : ch) by_last[c.first + c.second - 1].push_back(Chunk{i, j, c.first, c.second});
             }
         if (inv)
@@ -2289,11 +2311,13 @@ struct Params {
     // r01i sweep (scripts/sched_sweep.sh): at N = 16384 W = 64 with no single-panel tail is
     // 1.6-2.0% faster than W = 32, near = 1; at N = 4096 (chain-bound) near = 1 stays 6% faster
     int W = 64, near = -1;  // near < 0: by size (near_for)
+    int ratio = -1;         // chunk-width rule of tile_chunks: < 0 picked per shape by the simulation
     Cost cm;
     int near_for(int nc) const { return near >= 0 ? near : (nc <= 64 ? 1 : 0); }
     Params() {
         if (const char* e = std::getenv("GPRX_PT_W")) W = std::max(1, std::atoi(e));
         if (const char* e = std::getenv("GPRX_PT_NEAR")) near = std::max(0, std::atoi(e));
+        if (const char* e = std::getenv("GPRX_PT_RATIO")) ratio = std::max(0, std::atoi(e));
         if (const char* e = std::getenv("GPRX_PT_DIAGX_US")) cm.diagx = std::atof(e);
         if (const char* e = std::getenv("GPRX_PT_TRSM_US")) cm.trsm = std::atof(e);
         if (const char* e = std::getenv("GPRX_PT_K128_US")) cm.k128 = std::atof(e);
@@ -2304,6 +2328,23 @@ struct Params {
 static const Params& params() {
     static Params p;
     return p;
+}
+
+// the chunk rule with the shortest simulated makespan (ratio 0: the fixed rule; 8, 4, 2: width
+// capped by the distance to the tile's last panel), unless GPRX_PT_RATIO fixes it
+static const int kRatios[] = {0, 8, 4, 2};
+static Schedule best_schedule(int nc, int nr, const Params& pr, int P, bool build, int ni) {
+    if (pr.ratio >= 0) return make_schedule(nc, nr, pr.W, pr.near_for(nc), P, pr.cm, build, ni, pr.ratio);
+    Schedule best;
+    bool have = false;
+    for (int r : kRatios) {
+        Schedule S = make_schedule(nc, nr, pr.W, pr.near_for(nc), P, pr.cm, build, ni, r);
+        if (!have || S.est_us < best.est_us * 0.995) {  // a wider rule must win by > 0.5%
+            best = std::move(S);
+            have = true;
+        }
+    }
+    return best;
 }
 
 }  // namespace pt
@@ -2405,7 +2446,7 @@ void potrf_tiles(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info
             for (int i = 0; i < nc; i++)
                 for (int j = 0; j <= i; j++) S.list.push_back(make_int4(T_BUILD, i, j, 0));
         } else {
-            S = make_schedule(nc, nr, pr.W, pr.near_for(nc), st.ncu, pr.cm, fused, ni);
+            S = best_schedule(nc, nr, pr, st.ncu, fused, ni);
         }
         PtState::Dev d;
         d.n = (int64_t)S.list.size();
@@ -2556,7 +2597,7 @@ int64_t potrf_tiles_schedule_stats(int nc, int nr, int P, bool build, double* es
     if (nc < 1 || nr < nc || P < 1 || ni < 0 || ni > nr - nc)
         throw Error{GPRX_ERR_ARG, "potrf tile schedule: need nc >= 1, nr >= nc + ni, P >= 1"};
     const pt::Params& pr = pt::params();
-    pt::Schedule S = pt::make_schedule(nc, nr, pr.W, pr.near_for(nc), P, pr.cm, build, ni);
+    pt::Schedule S = pt::best_schedule(nc, nr, pr, P, build, ni);
     if (est_us) *est_us = S.est_us;
     return S.ntasks;
 }

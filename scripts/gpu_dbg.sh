@@ -1,13 +1,12 @@
 #!/bin/bash
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
-timeout -k 10 300 python -u scripts/dist_f32_determinism.py > gpurun_out/f32det.jsonl 2>&1; R=$?
-python -c "
-import json
-for l in open('gpurun_out/f32det.jsonl'):
-    if l.startswith('{'):
-        d = json.loads(l); print(d['g'], d['steps'], d['distinct'], sorted(set(tuple(r[1:]) for r in d['runs'])))
-"
-[ $R -eq 0 ] || exit $R
-timeout -k 10 400 python -u -m pytest tests/test_gpu_dist.py -q --timeout 200 --timeout-method thread > gpurun_out/dbg_dist.log 2>&1; R=$?
-grep -n "^E  \|passed\|failed\|gprx dist timeout" gpurun_out/dbg_dist.log | cut -c1-300 | tail -20; exit $R
+for N in 4096 8192 16384; do
+  PT_TRACE_OUT=gpurun_out/pt$N.npz timeout -k 10 120 python -u scripts/pt_trace.py $N > gpurun_out/pt$N.json 2>&1 || exit 1
+  python3 -c "
+import json,sys
+d=json.loads(open('gpurun_out/pt$N.json').read()[open('gpurun_out/pt$N.json').read().index('{'):])
+print($N, 'span', d['span_us'], 'devbench_ms', d['ms_devbench'], 'diagx', d['diagx_exec_mean_us'], 'gap', d['diagx_gap_mean_us'], 'tasks', d['tasks'])"
+done
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_configs.py -q -x --timeout 120 --timeout-method thread > gpurun_out/par.log 2>&1; R=$?
+tail -2 gpurun_out/par.log; exit $R
