@@ -233,8 +233,10 @@ extern "C" int32_t gprx_dev_pt_debug(int32_t* out, int32_t max_wg) { return gprx
 extern "C" gprx_status gprx_dev_schedule(int32_t nc, int32_t nr, int32_t P, int32_t build, double* est_us,
                                          int64_t* ntasks) {
     try {
-        // build: bit 0 = fused covariance build, bit 1 = the last nc row blocks are identity
-        const int64_t n = potrf_tiles_schedule_stats(nc, nr, P, (build & 1) != 0, est_us, (build & 2) ? nc : 0);
+        // build: bit 0 = fused covariance build, bit 1 = the last nc row blocks are identity,
+        // bits 8..15 = chunk rule ratio + 1 (0: the one the simulation picks)
+        const int64_t n = potrf_tiles_schedule_stats(nc, nr, P, (build & 1) != 0, est_us, (build & 2) ? nc : 0,
+                                                     ((build >> 8) & 0xff) - 1);
         if (ntasks) *ntasks = n;
         return GPRX_OK;
     } catch (const Error& e) {

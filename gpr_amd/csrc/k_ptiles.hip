@@ -2593,11 +2593,12 @@ template void potrf_tiles_dist_launch<float>(const DistLaunch<float>&);
 
 // Host-only schedule statistics (no device work): tasks, predicted makespan, and a check
 // that every task's producers come earlier in the ticket order.
-int64_t potrf_tiles_schedule_stats(int nc, int nr, int P, bool build, double* est_us, int ni) {
+int64_t potrf_tiles_schedule_stats(int nc, int nr, int P, bool build, double* est_us, int ni, int ratio) {
     if (nc < 1 || nr < nc || P < 1 || ni < 0 || ni > nr - nc)
         throw Error{GPRX_ERR_ARG, "potrf tile schedule: need nc >= 1, nr >= nc + ni, P >= 1"};
     const pt::Params& pr = pt::params();
-    pt::Schedule S = pt::best_schedule(nc, nr, pr, P, build, ni);
+    pt::Schedule S = ratio >= 0 ? pt::make_schedule(nc, nr, pr.W, pr.near_for(nc), P, pr.cm, build, ni, ratio)
+                                : pt::best_schedule(nc, nr, pr, P, build, ni);
     if (est_us) *est_us = S.est_us;
     return S.ntasks;
 }

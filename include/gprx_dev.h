@@ -26,7 +26,8 @@ gprx_status gprx_dev_bench(gprx_ctx* ctx, gprx_dtype dtype, int32_t what, int64_
                            int32_t iters, double* ms);
 /* Host-only: build the tile-dataflow potrf schedule for nc diagonal blocks, nr row blocks
  * and P workers (build bit 0: with the fused covariance-build tasks; bit 1: the last nc of
- * the nr row blocks are identity rows, the inverse riding along); returns its task count
+ * the nr row blocks are identity rows, the inverse riding along; bits 8..15: the update
+ * chunk rule's ratio + 1, 0 = the rule the simulated makespan picks); returns its task count
  * and simulated makespan (us).  Throws nothing, needs no
  * device: GPRX_ERR_ARG if the ticket order would violate a dependency. */
 gprx_status gprx_dev_schedule(int32_t nc, int32_t nr, int32_t P, int32_t build, double* est_us, int64_t* ntasks);

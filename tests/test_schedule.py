@@ -12,13 +12,17 @@ import pytest
 from gpr_amd.gprx import lib
 
 
-def _sched(nc, nr, P=256, build=False, ident=False):
+def _sched(nc, nr, P=256, build=False, ident=False, ratio=0):
+    """ratio: the chunk rule (0 = the fixed rule, r > 0 = width capped at r x the panels left,
+    None = the rule the simulated makespan picks)."""
     L = lib()
     L.gprx_dev_schedule.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                     ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]
     est = ctypes.c_double()
     n = ctypes.c_int64()
-    st = L.gprx_dev_schedule(nc, nr, P, (1 if build else 0) | (2 if ident else 0), ctypes.byref(est), ctypes.byref(n))
+    sel = 0 if ratio is None else (ratio + 1) << 8
+    st = L.gprx_dev_schedule(nc, nr, P, (1 if build else 0) | (2 if ident else 0) | sel, ctypes.byref(est),
+                             ctypes.byref(n))
     return st, n.value, est.value
 
 
@@ -55,12 +59,66 @@ def _expected_tasks(nc, nr, W=W_DEF, near=None):
     return diag + trsm + upd
 
 
+def _ratio_chunks(e, W, near, ratio):
+    """k_ptiles.hip tile_chunks with ratio > 0: greedy widest power-of-two piece p <= W
+    (W-aligned when p == W) ending >= near panels before e with p <= ratio x the panels left."""
+    out, b = [], 0
+    while b < e:
+        p = W
+        while p > 1:
+            end = b + p
+            if not (p == W and b % W) and end <= e - near and p <= ratio * (e - end):
+                break
+            p //= 2
+        out.append((b, p))
+        b += p
+    return out
+
+
+def _expected_tasks_ratio(nc, nr, ratio, W=W_DEF):
+    near = near_def(nc)
+    trsm = sum(1 for k in range(nc) for i in range(k + 1, nr) if not (i == k + 1 and i < nc))
+    upd = 0
+    for j in range(1, nc):
+        for i in range(j, nr):
+            e = j - 1 if i == j else j
+            if e > 0:
+                upd += len(_ratio_chunks(e, W, near, ratio))
+    return nc + trsm + upd
+
+
 @pytest.mark.parametrize("nc,extra", [(1, 0), (1, 1), (2, 1), (7, 1), (8, 1), (9, 1), (33, 1), (128, 1), (64, 0)])
 def test_schedule_valid_and_counted(nc, extra):
     st, n, est = _sched(nc, nc + extra)
     assert st == 0, "ticket order violates a dependency"
     assert n == _expected_tasks(nc, nc + extra)
     assert est > 0
+
+
+@pytest.mark.parametrize("ratio", [2, 4, 8])
+@pytest.mark.parametrize("nc", [1, 9, 33, 70])
+def test_schedule_ratio_rule_valid_and_counted(nc, ratio):
+    """The capped chunk rule: pieces cover each tile's panels exactly once, the ticket order
+    stays valid, and the count matches the restatement."""
+    for e in range(1, 3 * W_DEF):
+        ch = _ratio_chunks(e, W_DEF, 1, ratio)
+        assert [b for b, _ in ch] == list(np.cumsum([0] + [p for _, p in ch])[:-1])
+        assert sum(p for _, p in ch) == e
+    st, n, est = _sched(nc, nc + 1, ratio=ratio)
+    assert st == 0, "ticket order violates a dependency"
+    assert n == _expected_tasks_ratio(nc, nc + 1, ratio)
+
+
+def test_schedule_picks_the_shortest_rule():
+    """The rule potrf_tiles uses is the candidate with the shortest simulated makespan: the
+    capped rule at N = 4096 (chain-bound: DIAGX(18) waited 184 us for a 16-panel piece under the
+    fixed rule), the fixed rule at N = 16384 (throughput-bound: fewer tasks)."""
+    for nc, want in [(32, 2), (128, 0)]:
+        ests = {r: _sched(nc, nc + 1, build=True, ratio=r)[2] for r in (0, 8, 4, 2)}
+        _, n_auto, est_auto = _sched(nc, nc + 1, build=True, ratio=None)
+        assert est_auto == min(ests.values())
+        assert est_auto == ests[want]
+    assert _sched(32, 33, ratio=2)[2] < 0.92 * _sched(32, 33, ratio=0)[2]
 
 
 @pytest.mark.parametrize("nc", [1, 2, 9, 64])
