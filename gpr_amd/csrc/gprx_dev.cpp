@@ -300,7 +300,9 @@ extern "C" gprx_status gprx_dev_dist_schedule(int32_t nc, int32_t P, int32_t g, 
                                               double* est_us, int32_t* chunk_w, int64_t* ntasks) {
     if (nc < 1 || P < 1 || g < 1 || g > 32 || gb < 1 || ww < 1 || !est_us) return GPRX_ERR_ARG;
     try {
-        const DistSched S = potrf_dist_schedule(nc, g, gb, ww, P, (flags & 1) != 0, (flags & 2) != 0);
+        // flags bits 8..15: the update-chunk rule's ratio + 1 (0: the fixed rule)
+        const DistSched S = potrf_dist_schedule(nc, g, gb, ww, P, (flags & 1) != 0, (flags & 2) != 0,
+                                                std::max(0, ((flags >> 8) & 0xff) - 1));
         *est_us = S.est_us;
         if (chunk_w) *chunk_w = S.W;
         if (ntasks) {

@@ -482,7 +482,7 @@ struct DistSched {
     double est_us = 0;
     int W = 0;              // update chunk width used
 };
-DistSched potrf_dist_schedule(int nc, int g, int gb, int ww, int P, bool build, bool inv);
+DistSched potrf_dist_schedule(int nc, int g, int gb, int ww, int P, bool build, bool inv, int ratio = 0);
 template <typename T>
 void potrf_tiles_dist_launch(const DistLaunch<T>& L);
 

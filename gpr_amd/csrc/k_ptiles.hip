@@ -2540,7 +2540,7 @@ void potrf_tiles(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info
 }
 
 // ---- distributed factorisation: per-rank ticket lists and one rank's launch ------------------
-DistSched potrf_dist_schedule(int nc, int g, int gb, int ww, int P, bool build, bool inv) {
+DistSched potrf_dist_schedule(int nc, int g, int gb, int ww, int P, bool build, bool inv, int ratio) {
     const pt::Params& pr = pt::params();
     // a push: one tile's stores over xGMI plus the flag (measured on one GPU as a same-device
     // copy; GPRX_DIST_PUSH_US / GPRX_DIST_REL_US override)
@@ -2551,7 +2551,8 @@ DistSched potrf_dist_schedule(int nc, int g, int gb, int ww, int P, bool build, 
     // update chunks at most half a window wide (flow control, make_schedule_dist), powers of two
     int W = 1;
     while (2 * W <= std::min(pr.W, std::max(1, ww / 2))) W *= 2;
-    return pt::make_schedule_dist(nc, inv, W, pr.near_for(nc), P, g, std::max(1, gb), ww, pr.cm, build, push_us, rel_us);
+    return pt::make_schedule_dist(nc, inv, W, pr.near_for(nc), P, g, std::max(1, gb), ww, pr.cm, build, push_us, rel_us,
+                                  pr.ratio >= 0 ? pr.ratio : ratio);
 }
 
 template <typename T>

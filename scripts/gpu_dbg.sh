@@ -1,12 +1,15 @@
 #!/bin/bash
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
-for N in 4096 8192 16384; do
-  PT_TRACE_OUT=gpurun_out/pt$N.npz timeout -k 10 120 python -u scripts/pt_trace.py $N > gpurun_out/pt$N.json 2>&1 || exit 1
-  python3 -c "
-import json,sys
-d=json.loads(open('gpurun_out/pt$N.json').read()[open('gpurun_out/pt$N.json').read().index('{'):])
-print($N, 'span', d['span_us'], 'devbench_ms', d['ms_devbench'], 'diagx', d['diagx_exec_mean_us'], 'gap', d['diagx_gap_mean_us'], 'tasks', d['tasks'])"
-done
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_configs.py -q -x --timeout 120 --timeout-method thread > gpurun_out/par.log 2>&1; R=$?
-tail -2 gpurun_out/par.log; exit $R
+timeout -k 10 400 python -u -m pytest tests/test_gpu_dist.py -q -x --timeout 200 --timeout-method thread > gpurun_out/dbg_dist.log 2>&1; R=$?
+grep -n "^E  \|passed\|failed\|gprx dist timeout" gpurun_out/dbg_dist.log | cut -c1-300 | tail -8
+[ $R -eq 0 ] || exit $R
+timeout -k 10 200 python -u scripts/dist_time.py 4096 10 single v1 v2 v4 > gpurun_out/dt4096.jsonl 2>&1 || exit 1
+timeout -k 10 300 python -u scripts/dist_time.py 16384 5 single v1 v2 v4 v8 > gpurun_out/dt16384.jsonl 2>&1 || exit 1
+python3 -c "
+import json
+for f in ('gpurun_out/dt4096.jsonl','gpurun_out/dt16384.jsonl'):
+    for l in open(f):
+        if l.startswith('{'):
+            d=json.loads(l); print(d['n'], d['mode'], round(d['ms_per_fit'],2), round(d['ms_factor_kernel'],2), d.get('dist',{}).get('gb'), d.get('dist',{}).get('ww'), d['alpha_vs_first'])
+"

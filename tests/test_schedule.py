@@ -173,14 +173,14 @@ def test_schedule_more_workers_never_slower():
     assert e256 <= e64
 
 
-def _dist_sched(nc, P, g, gb, ww, build=True, inv=False):
+def _dist_sched(nc, P, g, gb, ww, build=True, inv=False, ratio=0):
     L = lib()
     L.gprx_dev_dist_schedule.argtypes = [ctypes.c_int32] * 6 + [ctypes.POINTER(ctypes.c_double),
                                                                  ctypes.POINTER(ctypes.c_int32),
                                                                  ctypes.POINTER(ctypes.c_int64)]
     est, w, nt = ctypes.c_double(), ctypes.c_int32(), ctypes.c_int64()
-    st = L.gprx_dev_dist_schedule(nc, P, g, gb, ww, (1 if build else 0) | (2 if inv else 0), ctypes.byref(est),
-                                  ctypes.byref(w), ctypes.byref(nt))
+    st = L.gprx_dev_dist_schedule(nc, P, g, gb, ww, (1 if build else 0) | (2 if inv else 0) | ((ratio + 1) << 8),
+                                  ctypes.byref(est), ctypes.byref(w), ctypes.byref(nt))
     return st, est.value, w.value, nt.value
 
 
@@ -214,6 +214,22 @@ def test_dist_schedule_window_flow_control():
             assert st == 0 and est > 0 and w == max(1, 2 ** int(np.log2(max(1, ww // 2))))
             st, est, w, nt = _dist_sched(16, 30, g, 1, ww, inv=True)
             assert st == 0 and est > 0
+
+
+def test_dist_schedule_capped_chunk_rule():
+    # the capped update-chunk rule (gprx_dist.cpp tries ratios 4 and 2 for the chosen grouping
+    # and window) keeps every rank's ticket order valid, flow control and LML mode included, and
+    # shortens the chain-bound N = 4096 shape
+    for ratio in (2, 4):
+        for ww in (2, 4, 8):
+            for g in (2, 3):
+                st, est, w, nt = _dist_sched(24, 30, g, 2, ww, ratio=ratio)
+                assert st == 0 and est > 0
+                st, est, w, nt = _dist_sched(16, 30, g, 1, ww, inv=True, ratio=ratio)
+                assert st == 0 and est > 0
+    e0 = _dist_sched(32, 120, 2, 2, 16)[1]
+    e2 = _dist_sched(32, 120, 2, 2, 16, ratio=2)[1]
+    assert e2 < e0
 
 
 def test_dist_schedule_lml_mode_costs_about_three_factorisations():
