@@ -279,11 +279,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # GPRX_DIST_SHARED_GPU=1: a rehearsal of the N > 1 path on ONE GPU (every rank on device 0,
+    # each on its share of the CUs, gloo for the host collectives, the peer context's all-gather
+    # for the bootstrap: RCCL refuses two ranks on one device).  Timings are not N-GPU numbers.
+    shared = os.environ.get("GPRX_DIST_SHARED_GPU") == "1" and world > 1
+    if shared:
+        local_rank = 0
     if world > 1:
         import torch
         import torch.distributed as tdist
         torch.cuda.set_device(local_rank)
-        tdist.init_process_group("nccl")
+        tdist.init_process_group("gloo" if shared else "nccl")
         dist = tdist
 
     import gpr_amd
@@ -315,7 +321,7 @@ def main():
         if dist is None:
             return x
         import torch
-        t = torch.tensor([x], dtype=torch.float64, device="cuda")
+        t = torch.tensor([x], dtype=torch.float64, device="cpu" if shared else "cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
@@ -337,10 +343,14 @@ def main():
     dres, dist_error, dctx = None, None, None
     if world > 1 or args.force_dist:
         try:
-            uid = [gpr_amd.unique_id() if rank == 0 else None]
-            if dist is not None:
-                dist.broadcast_object_list(uid, src=0)
-            dctx = gpr_amd.Context(local_rank, dist=(rank, world, uid[0]))
+            if shared:
+                from gpr_amd.gprx import torch_allgather
+                dctx = gpr_amd.Context(0, peer=(rank, world, torch_allgather()))
+            else:
+                uid = [gpr_amd.unique_id() if rank == 0 else None]
+                if dist is not None:
+                    dist.broadcast_object_list(uid, src=0)
+                dctx = gpr_amd.Context(local_rank, dist=(rank, world, uid[0]))
             dmodel = make_model(dctx)
             el, infos, st = timed_fits(dmodel, dctx, gpr_amd.gprx.FIT_DISTRIBUTED)
             dres = {"elapsed": el, "infos": infos}

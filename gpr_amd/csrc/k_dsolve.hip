@@ -22,8 +22,13 @@
 // substitution, first block first for the forward one, so a workgroup waits only on blocks
 // claimed before it, on every rank).  A block no rank of this launch works on is still
 // waited for (its alpha / z arrives by push), so the launch ends with the whole vector here.
-// Hand-off: data stores to the destination mailbox, s_waitcnt vmcnt(0), system-scope release,
-// then the flag word (the solve's epoch); waits are bounded in wall-clock time.
+// Hand-off: every data store to a mailbox is a system-scope relaxed store (`sc0 sc1`: written
+// through, the line dropped from this XCD's L2) and every read of pushed data a system-scope load,
+// so a flag needs only each storing wave's s_waitcnt vmcnt(0) and a barrier before it -- no L2
+// write-back fence per block (MI355X_MICROARCH.md, inter-workgroup visibility, the {sc0 sc1
+// stores and loads both sides} form; a buffer_wbl2 costs 1.7-6.5 us, on the chain once per
+// block).  The diagonal inverse of the block sits in LDS (loaded before any wait); waits are
+// bounded in wall-clock time.
 #include "gprx_dist.h"
 
 #include <algorithm>
@@ -46,6 +51,20 @@ __device__ __forceinline__ void st_sys(unsigned* p, unsigned v) {
 template <typename T>
 __device__ __forceinline__ T ld_nc(const T* p) {  // data another rank pushed (bypass stale lines)
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+template <typename T>
+__device__ __forceinline__ void st_nc(T* p, T v) {  // data for another workgroup or rank (written through)
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+constexpr int LSL = DB + 1;  // LDS column stride of the diagonal inverse (conflict-free row and column reads)
+// Linv block (column-major, DB x DB) into LDS with stride LSL: coalesced global reads
+template <typename T>
+__device__ __forceinline__ void load_linv_lds(const T* __restrict__ Lb, T* __restrict__ sL, int t) {
+#pragma unroll 8
+    for (int v = 0; v < DB * DB / NT; v++) {
+        const int e = t + v * NT, row = e & (DB - 1), col = e >> 7;
+        sL[row + col * LSL] = Lb[e];
+    }
 }
 __device__ __forceinline__ uint64_t uni64(uint64_t v) {
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
@@ -78,15 +97,13 @@ __device__ __forceinline__ unsigned* mb_flag(const uint64_t* mb, int q, int64_t 
     return reinterpret_cast<unsigned*>(uni64(mb[q] + (uint64_t)off));
 }
 
-// every wave's stores drained, system-scope release, then (wave 0) flag word `fo` (byte
-// offset in the mailboxes) = ep at every rank in mask
+// every wave's (written-through) stores drained, then (wave 0) flag word `fo` (byte offset in
+// the mailboxes) = ep at every rank in mask
 template <typename T>
 __device__ void signal(const DSArgs<T>& a, unsigned mask, int64_t fo, unsigned ep) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if ((threadIdx.x >> 6) == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         for (int q = 0; q < a.g; q++)
             if ((mask >> q) & 1) st_sys(mb_flag(a.mb, q, fo), ep);
     }
@@ -103,6 +120,8 @@ __global__ __launch_bounds__(NT) void dist_back_kernel(DSArgs<T> a) {
     __shared__ T s_part[4][DB];
     __shared__ T s_v[DB];
     __shared__ int s_int[2];
+    extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
+    T* sL = reinterpret_cast<T*>(s_dyn);  // Linv_k, stride LSL
     const int t = threadIdx.x, lane = t & 63;
     const int c = t & (DB - 1), qq = t >> 7;
     if ((t >> 6) == 0) {
@@ -117,6 +136,10 @@ __global__ __launch_bounds__(NT) void dist_back_kernel(DSArgs<T> a) {
     if (tk >= a.nc) return;
     const int k = a.nc - 1 - tk;
     const int ok_ = a.own[k];
+    if (ok_ == a.r) {
+        load_linv_lds(a.Linv + (int64_t)k * DB * DB, sL, t);
+        __syncthreads();
+    }
     const long long t0 = wall_clock64();
     const unsigned all = ((1u << a.g) - 1u);
     T* my_alpha = mb_ptr<T>(a, a.r, a.o_alpha);
@@ -172,7 +195,7 @@ __global__ __launch_bounds__(NT) void dist_back_kernel(DSArgs<T> a) {
             const T w = (t < DB) ? s_part[0][t] + s_part[1][t] + s_part[2][t] + s_part[3][t] : T(0);
             if (!mine) {  // push this rank's partial for block k to its owner
                 if (t < DB)
-                    mb_ptr<T>(a, ok_, a.o_part)[((int64_t)a.r * a.nc + k) * DB * a.m + (int64_t)t * a.m + r] = w;
+                    st_nc(mb_ptr<T>(a, ok_, a.o_part) + ((int64_t)a.r * a.nc + k) * DB * a.m + (int64_t)t * a.m + r, w);
                 continue;
             }
             // the owner: the other ranks' partials (ranks owning a row block above k)
@@ -192,7 +215,7 @@ __global__ __launch_bounds__(NT) void dist_back_kernel(DSArgs<T> a) {
             }
             __syncthreads();
             {  // alpha_k = Linv_k^T v: column c, rows of quarter qq
-                const T* Lk = a.Linv + (int64_t)k * DB * DB + (int64_t)c * DB + QR * qq;
+                const T* Lk = sL + c * LSL + QR * qq;
                 T acc = 0;
 #pragma unroll
                 for (int u = 0; u < QR; u++) acc = fma(Lk[u], s_v[QR * qq + u], acc);
@@ -201,7 +224,7 @@ __global__ __launch_bounds__(NT) void dist_back_kernel(DSArgs<T> a) {
             __syncthreads();
             if (t < DB) {
                 const T al = s_part[0][t] + s_part[1][t] + s_part[2][t] + s_part[3][t];
-                for (int q = 0; q < a.g; q++) mb_ptr<T>(a, q, a.o_alpha)[((int64_t)k * DB + t) * a.m + r] = al;
+                for (int q = 0; q < a.g; q++) st_nc(mb_ptr<T>(a, q, a.o_alpha) + ((int64_t)k * DB + t) * a.m + r, al);
             }
             __syncthreads();
         }
@@ -223,8 +246,9 @@ template <typename T>
 __global__ __launch_bounds__(NT) void dist_forward_kernel(DSArgs<T> a) {
     __shared__ T s_part[4][DB];
     __shared__ T s_v[DB];
-    __shared__ T s_z[DB];
     __shared__ int s_int[2];
+    extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
+    T* sL = reinterpret_cast<T*>(s_dyn);  // Linv_i, stride LSL
     const int t = threadIdx.x, lane = t & 63;
     const int row = t & (DB - 1), cq = t >> 7;
     if ((t >> 6) == 0) {
@@ -250,6 +274,8 @@ __global__ __launch_bounds__(NT) void dist_forward_kernel(DSArgs<T> a) {
         return s_int[1] == 0;
     };
     if (a.own[i] == a.r) {
+        load_linv_lds(a.Linv + (int64_t)i * DB * DB, sL, t);
+        __syncthreads();
         for (int r = 0; r < a.m && ok; r++) {
             T s = 0;
             for (int k = 0; k < i && ok; k++) {
@@ -269,17 +295,16 @@ __global__ __launch_bounds__(NT) void dist_forward_kernel(DSArgs<T> a) {
             if (t < DB) s_v[t] = a.rhs[((int64_t)i * DB + t) * a.m + r] - (s_part[0][t] + s_part[1][t] + s_part[2][t] + s_part[3][t]);
             __syncthreads();
             {
-                const T* Li = a.Linv + (int64_t)i * DB * DB + row + (int64_t)(QR * cq) * DB;
+                const T* Li = sL + row + QR * cq * LSL;
                 T acc = 0;
 #pragma unroll
-                for (int u = 0; u < QR; u++) acc = fma(Li[(int64_t)u * DB], s_v[QR * cq + u], acc);
+                for (int u = 0; u < QR; u++) acc = fma(Li[u * LSL], s_v[QR * cq + u], acc);
                 s_part[cq][row] = acc;
             }
             __syncthreads();
             if (t < DB) {
                 const T zi = s_part[0][t] + s_part[1][t] + s_part[2][t] + s_part[3][t];
-                s_z[t] = zi;
-                for (int q = 0; q < a.g; q++) mb_ptr<T>(a, q, a.o_zf)[((int64_t)i * DB + t) * a.m + r] = zi;
+                for (int q = 0; q < a.g; q++) st_nc(mb_ptr<T>(a, q, a.o_zf) + ((int64_t)i * DB + t) * a.m + r, zi);
             }
             __syncthreads();
         }
@@ -332,16 +357,33 @@ __global__ __launch_bounds__(256) void dist_reduce_kernel(DSArgs<T> a, int64_t n
 
 }  // namespace ds
 
+// dynamic LDS of the two solve kernels (the diagonal inverse, padded), set once per type
+template <typename T>
+static size_t dsolve_lds() {
+    const size_t lds = sizeof(T) * (size_t)DB * ds::LSL;
+    static bool attr = false;
+    if (!attr) {
+        GPRX_HIP(hipFuncSetAttribute((const void*)ds::dist_back_kernel<T>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)lds));
+        GPRX_HIP(hipFuncSetAttribute((const void*)ds::dist_forward_kernel<T>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)lds));
+        attr = true;
+    }
+    return lds;
+}
+
 template <typename T>
 void launch_dist_back(const DSArgs<T>& a, hipStream_t s) {
     GPRX_REQUIRE(a.g <= 32 && a.m >= 1 && a.nc >= 1, GPRX_ERR_ARG, "dist back substitution: bad sizes");
-    hipLaunchKernelGGL(ds::dist_back_kernel<T>, dim3((unsigned)a.nc), dim3(ds::NT), 0, s, a);
+    const size_t lds = dsolve_lds<T>();
+    hipLaunchKernelGGL(ds::dist_back_kernel<T>, dim3((unsigned)a.nc), dim3(ds::NT), lds, s, a);
     GPRX_HIP(hipGetLastError());
 }
 template <typename T>
 void launch_dist_forward(const DSArgs<T>& a, hipStream_t s) {
     GPRX_REQUIRE(a.g <= 32 && a.m >= 1 && a.nc >= 1 && a.rhs, GPRX_ERR_ARG, "dist forward substitution: bad sizes");
-    hipLaunchKernelGGL(ds::dist_forward_kernel<T>, dim3((unsigned)a.nc), dim3(ds::NT), 0, s, a);
+    const size_t lds = dsolve_lds<T>();
+    hipLaunchKernelGGL(ds::dist_forward_kernel<T>, dim3((unsigned)a.nc), dim3(ds::NT), lds, s, a);
     GPRX_HIP(hipGetLastError());
 }
 template <typename T>

@@ -1289,7 +1289,12 @@ __device__ bool dist_wait_release(const Args<T>& a, const PtDist<T>& D, unsigned
 
 // The whole workgroup: copy one DB x DB tile (contiguous, written by this workgroup and
 // drained: its stores are visible to this CU) to byte offset `off` of the mailbox of every
-// rank in `mask`, then release (system scope) and set each one's flag word `fidx` to the epoch.
+// rank in `mask`, then set each one's flag word `fidx` to the epoch.  Across devices (D.wt) the
+// copies are 16-byte `sc0 sc1` stores (written through to the destination, not left dirty in
+// this XCD's L2), so the flag needs only every wave's s_waitcnt vmcnt(0) and a barrier -- no
+// buffer_wbl2, which would write back every dirty line of the XCD's L2 (the update tasks'
+// tiles) on each push (MI355X_MICROARCH.md, the {sc0 sc1 stores} form; the consumer acquires
+// before its loads).  Ranks of one device: plain stores and one system-scope release.
 template <typename T>
 __device__ void dist_push(const T* src, const PtDist<T>& D, unsigned mask, int64_t off, int64_t fidx, const int t,
                           int64_t tag_idx = -1, unsigned tag = 0) {
@@ -1297,6 +1302,7 @@ __device__ void dist_push(const T* src, const PtDist<T>& D, unsigned mask, int64
     typedef unsigned int u4 __attribute__((ext_vector_type(4)));
     constexpr int NV = DB * DB * (int)sizeof(T) / 16 / NT;  // 16-byte vectors per thread
     constexpr int CH = 4;
+    const bool wt = __builtin_amdgcn_readfirstlane(D.wt) != 0;
     if (wave_id() == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // this CU's L1: no stale lines of src
     __syncthreads();
     const u4* s4 = reinterpret_cast<const u4*>(src);
@@ -1308,15 +1314,24 @@ __device__ void dist_push(const T* src, const PtDist<T>& D, unsigned mask, int64
         for (int q = 0; q < D.g; q++) {
             if (!((mask >> q) & 1)) continue;
             u4* d4 = reinterpret_cast<u4*>(dist_mb(D, q, off));
+            if (wt) {
 #pragma unroll
-            for (int u = 0; u < CH; u++) d4[t + (c + u) * NT] = v[u];
+                for (int u = 0; u < CH; u++)
+                    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(d4 + t + (c + u) * NT), "v"(v[u])
+                                 : "memory");
+            } else {
+#pragma unroll
+                for (int u = 0; u < CH; u++) d4[t + (c + u) * NT] = v[u];
+            }
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (wave_id() == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (!wt) {  // ranks of one device: plain stores, one release
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         if (D.check && tag_idx >= 0)
             for (int q = 0; q < D.g; q++)
                 if ((mask >> q) & 1) st_sys(reinterpret_cast<unsigned*>(dist_mb(D, q, D.o_tags)) + tag_idx, tag);

@@ -340,6 +340,32 @@ def test_virtual_ranks_window_slots_verified(g, ww, monkeypatch, capfd):
         vctx.close()
 
 
+@pytest.mark.parametrize("g", [2, 5])
+def test_virtual_ranks_written_through_pushes(g, monkeypatch, capfd):
+    """The cross-device push flavour (GPRX_DIST_WT=1: 16-byte sc0 sc1 stores, no L2 write-back
+    fence before the flag; the default for ranks on different GPUs) forced on virtual ranks, with
+    every window read verified (GPRX_DIST_CHECK) and repeated fits bit-identical."""
+    import gpr_amd
+    monkeypatch.setenv("GPRX_DIST_WT", "1")
+    monkeypatch.setenv("GPRX_DIST_CHECK", "1")
+    monkeypatch.setenv("GPRX_DIST_WINDOW", "8")
+    n, d, m, sigma = 4000, 8, 2, 0.5
+    X, Y = make_data(n, d, m)
+    a_ref, _ = O.fit(C3K, X, Y, sigma, want_core=False)
+    vctx = gpr_amd.Context(0, virtual=g)
+    try:
+        M, info = _fit(vctx, C3K, X, Y, sigma, np.float64)
+        a0 = M.alpha()
+        assert relerr(a0, a_ref) <= 1e-6
+        for _ in range(2):
+            M.fit()
+            assert np.array_equal(M.alpha(), a0)
+        assert "stale window reads" not in capfd.readouterr().err
+        M.close()
+    finally:
+        vctx.close()
+
+
 @pytest.mark.parametrize("g", [2, 4])
 def test_virtual_ranks_storage_is_sharded(g):
     """Per-rank device memory of the sharded fit: the packed lower tiles of the rank's own row
