@@ -229,6 +229,7 @@ struct DistRank {
     hipStream_t s = nullptr;
     DMem store, mbox, ctr, info, flag, red, sctl, part;
     DMem t_loc, t_roff, t_own, t_tptr, t_cons, t_need, t_mb, t_orows, t_lastof, t_ctab, pd, list;
+    DMem trace;                        // GPRX_DIST_TRACE_FILE: per-ticket timeline of the last launch
     std::vector<uint64_t> mb;          // every rank's mailbox as mapped here
     std::vector<uint64_t> st;          // every rank's storage as mapped here
     std::vector<void*> opened;         // IPC mappings to close
@@ -477,7 +478,8 @@ static void setup(DistEngine<T>& E, const DistContext& C, int64_t n, int m, bool
         GPRX_HIP(hipEventCreate(&R->t0));
         GPRX_HIP(hipEventCreate(&R->t1));
         R->store.alloc(sizeof(T) * (size_t)E.L.elems[r], false);
-        R->mbox.alloc((size_t)E.MB.bytes, true);
+        static const bool coarse = std::getenv("GPRX_DIST_COARSE") && std::atoi(std::getenv("GPRX_DIST_COARSE")) != 0;
+        R->mbox.alloc((size_t)E.MB.bytes, !coarse);
         GPRX_HIP(hipMemset(R->mbox.p, 0, E.MB.bytes));  // flags 0: below every epoch
         R->ctr.alloc(sizeof(int) * ((size_t)C_NCTL_DIST + nr + (size_t)nr * nci + nc), false);
         R->info.alloc(160 * sizeof(int), false);  // info, then the GPRX_DIST_CHECK counters and log
@@ -603,6 +605,8 @@ static PtDist<T> make_ptdist(const DistEngine<T>& E, const DistRank<T>& R) {
     // every dirty line of the producer's L2 for a tile that lives on another GPU
     pd.wt = (E.virt || E.shared_dev) ? 0 : 1;
     if (const char* e = std::getenv("GPRX_DIST_WT")) pd.wt = std::atoi(e) != 0;
+    pd.acq_agent = 0;
+    if (const char* e = std::getenv("GPRX_DIST_ACQ_AGENT")) pd.acq_agent = std::atoi(e) != 0;
     pd.check_err = R.info.template as<int>() + 1;
     return pd;
 }
@@ -730,6 +734,11 @@ void dist_fit(DistEngineBase*& eng, const DistContext& C, const DistFitIn<T>& in
         Lc.s = s;
         Lc.dbg = nullptr;
         Lc.trace = nullptr;
+        if (std::getenv("GPRX_DIST_TRACE_FILE")) {  // {taken, ready, published, workgroup} per ticket
+            const size_t tb = sizeof(long long) * 4 * ((size_t)R.ntasks + 2 * (size_t)nc);
+            if (R.trace.bytes < tb) R.trace.alloc(tb, false);
+            Lc.trace = R.trace.template as<long long>();
+        }
     }
     // every rank's persistent launch back to back, nothing that could block in between
     for (size_t v = 0; v < E.ranks.size(); v++) {
@@ -739,6 +748,23 @@ void dist_fit(DistEngineBase*& eng, const DistContext& C, const DistFitIn<T>& in
     }
     for (auto& R : E.ranks) GPRX_HIP(hipStreamSynchronize(R->s));
     GPRX_HIP(hipGetLastError());
+    if (const char* tf = std::getenv("GPRX_DIST_TRACE_FILE")) {
+        // one file per rank (overwritten each fit): int32 ntasks, int32 rank, int32 g, int32 nc,
+        // then the ticket list (int4 per ticket) and the timeline (4 int64 per ticket, 100 MHz)
+        for (auto& Rp : E.ranks) {
+            DistRank<T>& R = *Rp;
+            std::vector<long long> tm((size_t)4 * R.ntasks);
+            GPRX_HIP(hipMemcpy(tm.data(), R.trace.p, sizeof(long long) * tm.size(), hipMemcpyDeviceToHost));
+            const std::string path = std::string(tf) + ".r" + std::to_string(R.r);
+            if (FILE* f = std::fopen(path.c_str(), "wb")) {
+                const int hdr[4] = {R.ntasks, R.r, E.g, nc};
+                std::fwrite(hdr, sizeof(hdr), 1, f);
+                std::fwrite(E.S.lists[R.r].data(), sizeof(int4), E.S.lists[R.r].size(), f);
+                std::fwrite(tm.data(), sizeof(long long), tm.size(), f);
+                std::fclose(f);
+            }
+        }
+    }
     // ---- reductions: log det, data fit, status (one small all-gather over the processes) --------
     struct Part {
         double logdet, datafit;

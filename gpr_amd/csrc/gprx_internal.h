@@ -444,6 +444,7 @@ struct PtDist {
     int64_t o_tags;            // GPRX_DIST_CHECK: per window slot (panel, row) the tag of its occupant
     int check;                 // GPRX_DIST_CHECK: verify every window read against the slot's tag
     int wt;                    // pushes cross devices: written-through (sc0 sc1) stores, no L2 write-back fence
+    int acq_agent;             // ranks of one device: agent-scope acquire before reading pushed data
     int* check_err;            // [2] window reads of a stale slot / of a slot overwritten during the read
     // flag words in the mailbox (unsigned, from o_flags): tile (j, b) received at
     // [F_TILE + j * nc + b], Linv_k at [F_LINV(nr, nc) + k], panel p released by rank q at

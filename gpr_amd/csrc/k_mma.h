@@ -133,6 +133,17 @@ __device__ __forceinline__ void tile_mma(typename Mfma<T>::acc_t (&acc)[2][4], c
     wave_block<MAP>(w, wr, wc);
     const int lr = lane & 15, lk = lane >> 4;
     const int lcol = lane / S::LPC, lrow = (lane % S::LPC) * S::E;
+    // Bpan: the K / 128 <= 64 panel addresses, lane l holding panel l's, loaded ONCE here.  (A
+    // load of the address inside issue() made every stage's issue wait -- readfirstlane needs
+    // the value, and vmcnt counts in order -- for all the staging loads still in flight: the
+    // window-fed updates of the sharded fit ran 68% slower per panel than the local ones.)
+    uint32_t bp_lo = 0, bp_hi = 0;
+    if (Bpan) {
+        const int npan = (K + GT - 1) / GT;
+        const uint64_t v = (lane < npan) ? Bpan[lane] : 0ull;
+        bp_lo = (uint32_t)v;
+        bp_hi = (uint32_t)(v >> 32);
+    }
 
     auto issue = [&](int st) {
         T* buf = smem + (st % NBUF) * S::STG;
@@ -145,10 +156,9 @@ __device__ __forceinline__ void tile_mma(typename Mfma<T>::acc_t (&acc)[2][4], c
             const T* src;
             if (isB && Bpan) {  // the stage's 16 columns lie in one 128-column panel
                 // (addresses as integers: a pointer-to-pointer operand crashed hipcc 7.2)
-                // (__builtin_amdgcn_readfirstlane is 32-bit: the halves separately)
-                const uint64_t pv = Bpan[(st * BKS) >> 7];
-                const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)pv);
-                const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(pv >> 32));
+                const int pn = (st * BKS) >> 7;
+                const uint32_t lo = __builtin_amdgcn_readlane(bp_lo, pn);
+                const uint32_t hi = __builtin_amdgcn_readlane(bp_hi, pn);
                 const T* pb = reinterpret_cast<const T*>(((uint64_t)hi << 32) | lo);
                 src = pb + lrow + (col & (GT - 1)) * ldb;
             } else {

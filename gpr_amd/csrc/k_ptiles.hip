@@ -1634,7 +1634,8 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
                 if constexpr (DIST) {
                     const PtDist<T>& D = *a.dist;
                     const int dep = (type == T_DIAGX) ? i - 1 : (type == T_BUILD ? -1 : j);
-                    remote = dep >= 0 && __builtin_amdgcn_readfirstlane(D.loc[dep]) < 0;
+                    remote = dep >= 0 && __builtin_amdgcn_readfirstlane(D.loc[dep]) < 0 &&
+                             !__builtin_amdgcn_readfirstlane(D.acq_agent);
                 }
                 if (remote) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
                 else __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
