@@ -427,33 +427,32 @@ static void setup(DistEngine<T>& E, const DistContext& C, int64_t n, int m, bool
             }
         }
     }
-    if (!ew && E.g > 1) {  // the smallest window within 2% of the best simulated makespan
-        std::vector<std::pair<int, DistSched>> cands;
-        for (int w : {8, 16, 64})
-            if (w < nc && w != ww) cands.push_back({w, sim(gb, w)});
-        double bw = E.S.est_us;
-        for (auto& c : cands) bw = std::min(bw, c.second.est_us);
-        int pick = ww;
-        double pe = E.S.est_us;
-        for (auto& c : cands)
-            if (c.first < pick && c.second.est_us <= 1.02 * bw) {
-                pick = c.first;
-                pe = c.second.est_us;
+    if (!ew && E.g > 1) {
+        // the window with the shortest simulated makespan among those within the memory budget
+        // (GPRX_DIST_WINDOW_MB; default an eighth of the device's memory per rank -- a wider
+        // window means wider update chunks: C3 on 8 virtual ranks 35.0 ms at 64 panels, 34.0 at
+        // 128), near-ties (0.5%) to the smaller window
+        size_t fr = 0, tot = 0;
+        GPRX_HIP(hipMemGetInfo(&fr, &tot));
+        double budget = (double)tot / 8.0 / (double)(E.virt ? E.g : std::max(1, C.cu_slots));
+        if (const char* e = std::getenv("GPRX_DIST_WINDOW_MB")) budget = std::atof(e) * 1048576.0;
+        const int nrw = nc + 1 + (inv ? nc : 0);
+        auto wbytes = [&](int w) { return (double)w * nrw * DB * DB * (double)sizeof(T); };
+        std::vector<int> cws;
+        for (int w = 8; w < nc; w *= 2) cws.push_back(w);
+        cws.push_back(std::max(2, nc));
+        int pick = -1;
+        DistSched ps;
+        for (int w : cws) {
+            if (pick >= 0 && wbytes(w) > budget) break;
+            DistSched c = sim(gb, w);
+            if (pick < 0 || c.est_us < 0.995 * ps.est_us) {
+                pick = w;
+                ps = std::move(c);
             }
-        if (E.S.est_us > 1.02 * bw && pick == ww)  // a wider window is clearly faster
-            for (auto& c : cands)
-                if (c.second.est_us <= 1.02 * bw && (pick == ww || c.first < pick)) {
-                    pick = c.first;
-                    pe = c.second.est_us;
-                }
-        if (pick != ww)
-            for (auto& c : cands)
-                if (c.first == pick) {
-                    E.S = std::move(c.second);
-                    ww = pick;
-                    break;
-                }
-        (void)pe;
+        }
+        ww = pick;
+        E.S = std::move(ps);
     }
     // the update-chunk rule (k_ptiles.hip tile_chunks): the capped rules, tried for the chosen
     // grouping and window, replace the fixed one when they simulate > 0.5% shorter

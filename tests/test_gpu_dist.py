@@ -367,19 +367,22 @@ def test_virtual_ranks_written_through_pushes(g, monkeypatch, capfd):
 
 
 @pytest.mark.parametrize("g", [2, 4])
-def test_virtual_ranks_storage_is_sharded(g):
+def test_virtual_ranks_storage_is_sharded(g, monkeypatch):
     """Per-rank device memory of the sharded fit: the packed lower tiles of the rank's own row
     blocks (~N^2/(2g)), the window (ww panels of N x 128) and O(N x 128) of diagonal inverses,
     label tiles, flags and tables -- never the N^2 factor (the verdict's round-2 finding: 0.56
     N^2 per rank at g = 8).  C3-shaped, N = 8192."""
     import gpr_amd
     n, d, sigma = 8192, 32, 1.0
+    # a window budget of 150 MiB: 16 panels of (nc + 1) tiles fit, 32 do not
+    monkeypatch.setenv("GPRX_DIST_WINDOW_MB", "150")
     X, Y = make_data(n, d, 1)
     vctx = gpr_amd.Context(0, virtual=g)
     try:
         M, info = _fit(vctx, C3K, X, Y, sigma, np.float64)
         di = M.dist_info()
         s, nb = 8, 128
+        assert di["ww"] <= 16 and di["ww"] * (n // nb + 1) * nb * nb * s <= 150 * 2**20
         nc = n // nb
         # own row blocks (cyclic groups): at most ceil(nc / (g gb)) gb blocks, the worst-placed
         # rank's rows are the latest ones: bound its lower tiles by the last blocks of the matrix
