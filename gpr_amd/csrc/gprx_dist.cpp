@@ -227,7 +227,7 @@ template <typename T>
 struct DistRank {
     int r = 0;
     hipStream_t s = nullptr;
-    DMem store, mbox, ctr, info, flag, red, sctl, part;
+    DMem store, mbox, ctr, info, flag, red, sctl, part, pbuf;
     DMem t_loc, t_roff, t_own, t_tptr, t_cons, t_need, t_mb, t_orows, t_lastof, t_ctab, pd, list;
     DMem trace;                        // GPRX_DIST_TRACE_FILE: per-ticket timeline of the last launch
     std::vector<uint64_t> mb;          // every rank's mailbox as mapped here
@@ -407,7 +407,8 @@ static void setup(DistEngine<T>& E, const DistContext& C, int64_t n, int m, bool
     // GPRX_DIST_WINDOW force them).  Every rank runs the same deterministic simulation.
     int gb = 1, ww = std::min(32, nc);
     double best = 0;
-    auto sim = [&](int gbc, int wwc) { return potrf_dist_schedule(nc, E.g, gbc, wwc, E.P, fused, inv); };
+    constexpr bool f64 = std::is_same<T, double>::value;
+    auto sim = [&](int gbc, int wwc) { return potrf_dist_schedule(nc, E.g, gbc, wwc, E.P, fused, inv, 0, f64); };
     const char* eg = std::getenv("GPRX_DIST_GROUP");
     const char* ew = std::getenv("GPRX_DIST_WINDOW");
     if (ew) ww = std::max(2, std::min(nc, std::atoi(ew)));
@@ -457,7 +458,7 @@ static void setup(DistEngine<T>& E, const DistContext& C, int64_t n, int m, bool
     // the update-chunk rule (k_ptiles.hip tile_chunks): the capped rules, tried for the chosen
     // grouping and window, replace the fixed one when they simulate > 0.5% shorter
     for (int ratio : {4, 2}) {
-        DistSched c = potrf_dist_schedule(nc, E.g, gb, ww, E.P, fused, inv, ratio);
+        DistSched c = potrf_dist_schedule(nc, E.g, gb, ww, E.P, fused, inv, ratio, f64);
         if (c.est_us < 0.995 * E.S.est_us) E.S = std::move(c);
     }
     E.gb = gb;
@@ -480,7 +481,8 @@ static void setup(DistEngine<T>& E, const DistContext& C, int64_t n, int m, bool
         static const bool coarse = std::getenv("GPRX_DIST_COARSE") && std::atoi(std::getenv("GPRX_DIST_COARSE")) != 0;
         R->mbox.alloc((size_t)E.MB.bytes, !coarse);
         GPRX_HIP(hipMemset(R->mbox.p, 0, E.MB.bytes));  // flags 0: below every epoch
-        R->ctr.alloc(sizeof(int) * ((size_t)C_NCTL_DIST + nr + (size_t)nr * nci + nc), false);
+        R->ctr.alloc(sizeof(int) * ((size_t)C_NCTL_DIST + nr + (size_t)nr * nci + nc + 4 * (size_t)nc), false);
+        if (potrf_split_for(std::is_same<T, double>::value, E.P)) R->pbuf.alloc(sizeof(T) * 4 * DB * DB, false);
         R->info.alloc(160 * sizeof(int), false);  // info, then the GPRX_DIST_CHECK counters and log
         GPRX_HIP(hipMemset(R->info.p, 0, 160 * sizeof(int)));
         R->flag.alloc(sizeof(int), false);
@@ -666,7 +668,7 @@ void dist_fit(DistEngineBase*& eng, const DistContext& C, const DistFitIn<T>& in
         DistRank<T>& R = *E.ranks[v];
         const int r = R.r;
         hipStream_t s = R.s;
-        const size_t nctr = (size_t)C_NCTL_DIST + nr + (size_t)nr * nci + nc;
+        const size_t nctr = (size_t)C_NCTL_DIST + nr + (size_t)nr * nci + nc + 4 * (size_t)nc;  // + TPART states
         GPRX_HIP(hipMemsetAsync(R.ctr.p, 0, sizeof(int) * nctr, s));
         int* lcnt = R.ctr.template as<int>() + C_NCTL_DIST;
         hipLaunchKernelGGL(dist_init_counters, dim3((unsigned)nr), dim3(256), 0, s, lcnt, lcnt + nr, nc, nr, nci,
@@ -733,6 +735,9 @@ void dist_fit(DistEngineBase*& eng, const DistContext& C, const DistFitIn<T>& in
         Lc.s = s;
         Lc.dbg = nullptr;
         Lc.trace = nullptr;
+        Lc.split = potrf_split_for(std::is_same<T, double>::value, E.P) ? 1 : 0;
+        Lc.pbuf = R.pbuf.template as<T>();
+        Lc.tflag = R.ctr.template as<int>() + C_NCTL_DIST + nr + (size_t)nr * nci + nc;
         if (std::getenv("GPRX_DIST_TRACE_FILE")) {  // {taken, ready, published, workgroup} per ticket
             const size_t tb = sizeof(long long) * 4 * ((size_t)R.ntasks + 2 * (size_t)nc);
             if (R.trace.bytes < tb) R.trace.alloc(tb, false);
@@ -837,7 +842,7 @@ void dist_fit(DistEngineBase*& eng, const DistContext& C, const DistFitIn<T>& in
     for (auto& Rp : E.ranks) {
         float ms = 0;
         if (hipEventElapsedTime(&ms, Rp->t0, Rp->t1) == hipSuccess) out.ms_kernel = std::max(out.ms_kernel, (double)ms);
-        const int64_t b = (int64_t)(Rp->store.bytes + Rp->mbox.bytes + Rp->ctr.bytes + Rp->part.bytes + Rp->t_tptr.bytes +
+        const int64_t b = (int64_t)(Rp->store.bytes + Rp->mbox.bytes + Rp->ctr.bytes + Rp->part.bytes + Rp->pbuf.bytes + Rp->t_tptr.bytes +
                                     Rp->t_cons.bytes + Rp->t_need.bytes + Rp->list.bytes + Rp->t_ctab.bytes);
         out.bytes_rank = std::max(out.bytes_rank, b);
         out.bytes_storage = std::max(out.bytes_storage, (int64_t)Rp->store.bytes);

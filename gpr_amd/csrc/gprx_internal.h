@@ -472,6 +472,9 @@ struct DistLaunch {
     hipStream_t s;
     int* dbg;          // optional: per-workgroup {ticket, phase, i, j} in coherent host memory
     long long* trace;  // optional: 4 * (ntasks + 2 nc) words, as GPRX_PT_TRACE (k_ptiles.hip)
+    int split;         // the split diagonal step (f64): TPART tasks in the list
+    T* pbuf;           // [4][DB x DB] the TPART products
+    int* tflag;        // [nc][4] TPART states (zeroed per fit with the counters)
 };
 // The simulated schedule of a distributed factorisation: per-rank ticket lists (in start
 // order of one list-schedule simulation of all ranks, window flow control included), the
@@ -484,7 +487,8 @@ struct DistSched {
     double est_us = 0;
     int W = 0;              // update chunk width used
 };
-DistSched potrf_dist_schedule(int nc, int g, int gb, int ww, int P, bool build, bool inv, int ratio = 0);
+DistSched potrf_dist_schedule(int nc, int g, int gb, int ww, int P, bool build, bool inv, int ratio = 0, bool f64 = true);
+bool potrf_split_for(bool f64, int P);  // the split diagonal step is on (this precision, P workgroups)
 template <typename T>
 void potrf_tiles_dist_launch(const DistLaunch<T>& L);
 

@@ -20,7 +20,7 @@ namespace mm {
 constexpr int NT = 512;     // threads per workgroup
 constexpr int PAD = 16;     // LDS row pad (elements)
 
-enum { T_DIAGX = 0, T_TRSM = 1, T_UPD = 2, T_BUILD = 3 };
+enum { T_DIAGX = 0, T_TRSM = 1, T_UPD = 2, T_BUILD = 3, T_TPART = 4 };
 enum { C_TICKET = 0, C_ERR = 1, C_NCTL = 16 };  // control words at the head of the counter block
 
 typedef double d4_t __attribute__((ext_vector_type(4)));

@@ -1068,14 +1068,22 @@ __device__ __forceinline__ void diag_factor_la(T* __restrict__ A, int64_t ld, T*
     }
 }
 
+#ifdef GPRX_NO_SPLIT  // (A/B builds: the split diagonal step compiled out)
+constexpr bool SPLIT_CODE = false;
+#else
+constexpr bool SPLIT_CODE = true;
+#endif
 #ifndef GPRX_DIAG_RANK8
 constexpr bool DIAG_LA = true;
 #else
 constexpr bool DIAG_LA = false;
 #endif
 // from_lds (f64 look-ahead form only): the block is in the LDS image already (diagx_ts)
+// (out of line: its registers (fact32's accumulators, the pivot block) no longer count against
+// the task loop, which sits at 256 VGPRs -- inlined, any growth of the loop spilled, and a
+// spill reload inside the update mainloop broke its counted vmcnt pipelining)
 template <typename T>
-__device__ __forceinline__ void diag_factor(T* __restrict__ A, int64_t ld, T* __restrict__ Linv, int* __restrict__ info,
+__device__ __noinline__ void diag_factor(T* __restrict__ A, int64_t ld, T* __restrict__ Linv, int* __restrict__ info,
                                             int64_t col0, unsigned char* smem_raw, const int t, int* dbg = nullptr,
                                             long long* prof = nullptr, bool from_lds = false) {
     // f64: the blocked factor with look-ahead (diag_factor_la: 43 us per block in isolation
@@ -1187,10 +1195,16 @@ struct Args {
     int* dbg;          // GPRX_PT_DEBUG: per-workgroup {ticket, phase, i, j} in pinned host memory
     int variant;       // GPRX_PT_VARIANT debug bits: 1 no TRSM math, 2 no UPD math, 4 no diag factor
     long long* trace;  // GPRX_PT_TRACE: per ticket {ticket taken, inputs ready, published, workgroup}
+    long long* xt;     // GPRX_PT_TRACE, one GPU: the split step's phase stamps (TpCtx::xt)
     const TileBuild<T>* tb;  // BUILD tasks: covariance tiles from pair statistics (device copy,
                              // read per task: as kernel arguments they stayed live in SGPRs and
                              // pushed the whole kernel into spills)
     const PtDist<T>* dist;   // distributed factorisation (potrf_tiles_kernel<T, true> only)
+    // split diagonal step (f64): TPART(k, c) tasks form the column blocks of L_{k,k-1} and
+    // their rank-32 products; DIAGX(k) only sums them (diagx_split)
+    int split;
+    T* pbuf;     // [4][DB x DB] the TPART products P_c = T_c T_c^T (lower tiles)
+    int* tflag;  // [nc][4] TPART(k, c) state: 1 its A operand is read, 2 T_c and P_c stored
 };
 
 
@@ -1399,7 +1413,26 @@ __device__ bool wait_inputs(const Args<T>& a, int type, int i, int j, int b0, in
     const unsigned* rp = nullptr;
     int rn = 0;
     unsigned ep = 0;
-    if (type == T_DIAGX && i == 0) {  // the first diagonal tile is built
+    if (type == T_TPART) {  // its A operand final (Linv_{i-1} is waited for inside the task)
+        vp = a.ver + (int64_t)i * a.nv + (i - 1);
+        vwant = i - 1;
+        vp2 = vp;
+        vwant2 = vwant;
+        lp1 = a.lcnt + i;
+        lwant1 = 0;
+        lp2 = lp1;
+        lwant2 = 0;
+    } else if (type == T_DIAGX && i > 0 && a.split) {  // A_ii through panel i-2
+        vp = a.ver + (int64_t)i * a.nv + i;
+        vwant = i - 1;
+        vp2 = vp;
+        vwant2 = vwant;
+        lp1 = a.lcnt + i;
+        lwant1 = 0;
+        lp2 = lp1;
+        lwant2 = 0;
+        // (A_kk only: the TPART products are waited for inside the task, A_kk loads meanwhile)
+    } else if (type == T_DIAGX && i == 0) {  // the first diagonal tile is built
         vp = a.ver;
         vwant = 0;
         vp2 = vp;
@@ -1594,6 +1627,268 @@ __device__ __forceinline__ long long diagx_ts(T* __restrict__ Akm, T* __restrict
     return tm;
 }
 
+// ---- the split diagonal step (f64) ---------------------------------------------------------
+// DIAGX(k)'s two products before the factor (T = A_{k,k-1} Linv_{k-1}^T, A_kk - T T^T: 2432
+// MFMAs, 31 us on the one CU of the chain) spread over four more workgroups:
+//   TPART(k, p), p = 0..3: the 16-column groups p and 7 - p of T = L_{k,k-1} (tpart_run),
+//       stored in place, and P_p = T_p T_p^T over those 32 columns into pbuf[p];
+//   DIAGX(k):  S = A_kk - P_0 - P_1 - P_2 - P_3 (A_kk - T T^T = sum over the column groups),
+//       in this fixed order as the parts finish, straight into the factor's LDS image.
+// A part's in-place stores overwrite A columns the other parts read: each part raises "A
+// read" (tflag 1) once its operand is in registers and stores only after all four have.
+// Tickets: the parts are consecutive (TPART(k, 3), (k, 2), (k, 1), (k, 0), order_tparts) and
+// DIAGX(k) comes after them; a part waits only on its three siblings, whose tickets are
+// claimed as soon as any CU frees (nothing before them depends on the parts), so with P >= 4
+// workgroups every wait ends.
+// (the out-of-line functions take these by value: a reference to the kernel's Args put the
+// whole struct in scratch memory, and every a.x of every task became a scratch load)
+template <typename T>
+struct TpCtx {
+    int* ctl;
+    int* lcnt;
+    int* tflag;
+    T* pbuf;
+    const PtDist<T>* dist;
+    long long tlimit;
+    long long* xt;  // GPRX_PT_TRACE (one GPU): phase stamps, TPART(k, c) at 4 (4 k + c), DIAGX(k) at 4 (4 nc + k)
+    int nc;
+};
+// LDS of a TPART: T's 32 columns (the operand of P), then the part's 32 Linv rows
+constexpr int TP_TSS = DB + 16;      // T column stride
+constexpr int TP_LOFF = 32 * TP_TSS;
+constexpr int TP_LSB = 34;           // Linv rows: column stride (16-B aligned pairs)
+static_assert((TP_LOFF + DB * TP_LSB) * sizeof(double) <= gemm_lds<double>(), "TPART staging exceeds the LDS of the launch");
+
+// wave 0: Linv_kk available to this rank (local publication, or the owner's push)
+template <typename T, bool DIST>
+__device__ bool tpart_wait_linv(const TpCtx<T>& a, int kk, bool& remote) {
+    const unsigned* rp = nullptr;
+    unsigned ep = 0;
+    remote = false;
+    if constexpr (DIST) {
+        const PtDist<T>& D = *a.dist;
+        if (__builtin_amdgcn_readfirstlane(D.loc[kk]) < 0) {
+            rp = dist_flags(D, D.r) + dist_f_linv(D.nr, D.nc) + kk;
+            ep = D.ep;
+            remote = !__builtin_amdgcn_readfirstlane(D.acq_agent);
+        }
+    }
+    const long long t0 = wall_clock64();
+    for (;;) {
+        const bool ok = rp ? (__builtin_amdgcn_readfirstlane(ld_sys(rp)) == ep) : (ld_uni(a.lcnt + kk) >= kk + 1);
+        if (ok) return true;
+        if (ld_uni(a.ctl + C_ERR)) return false;
+        if (wall_clock64() - t0 > a.tlimit) {
+            st_agent(a.ctl + C_ERR, 1);
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
+// wave 0: lane l < n checks f[l] >= want (one vector load, one ballot per poll)
+template <typename T>
+__device__ bool tpart_wait_flags(const TpCtx<T>& a, const int* f, int n, int want) {
+    const int lane = threadIdx.x & 63;
+    const long long t0 = wall_clock64();
+    for (;;) {
+        const bool good = lane >= n || ld_agent(f + (lane < n ? lane : 0)) >= want;
+        if (__builtin_amdgcn_readfirstlane((uint32_t)(__ballot(!good) == 0))) return true;
+        if (ld_uni(a.ctl + C_ERR)) return false;
+        if (wall_clock64() - t0 > a.tlimit) {
+            st_agent(a.ctl + C_ERR, 1);
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
+// TPART(k, p): the 16-column groups p and 7 - p of L_{k,k-1} = A_{k,k-1} Linv_{k-1}^T (group g
+// needs K = 16 (g + 1): each part 36 MFMAs per wave, balanced) and their rank-32 product P_p.
+// Wave w forms rows 16 w .. 16 w + 15: its A fragments (every A element read by one lane of
+// one part) go straight to registers at task start, before Linv_{k-1} is even waited for;
+// the 32 Linv rows, shared by all waves, through LDS.  Out of line, one body for every p:
+// inlined into the task loop the parts' code made every other task type 2-3x slower (TRSM
+// 16 -> 44 us, even with no TPART in the list) -- the loop's registers (it sits at 256 VGPRs)
+// and its hot code in the instruction cache.
+template <typename T, bool DIST>
+__device__ __noinline__ bool tpart_run(const TpCtx<T> a, T* __restrict__ Akm, int64_t ld, const T* __restrict__ Lp,
+                                       T* __restrict__ pc, int* tf, int k, const int C, T* smem, int& s_ok, const int t) {
+    typedef Mfma<T> Tr;
+    typedef typename Tr::acc_t acc_t;
+    typedef typename Tr::vec_t vec_t;
+    const int lane = t & 63, w = t >> 6, lr = lane & 15, lk = lane >> 4;
+    const int g0 = C, g1 = 7 - C;              // the part's column groups
+    const int nk0 = 4 * (g0 + 1), nk1 = 4 * (g1 + 1);  // k-steps of 4 of each group (nk1 > nk0)
+    T* Ls = smem + TP_LOFF;
+    // A fragments: row 16 w + lr, k = 4 kq + lk, kq < nk1 (<= 32)
+    T af[32];
+    {
+        const T* ar = Akm + 16 * w + lr + (int64_t)lk * ld;
+#pragma unroll
+        for (int kq = 0; kq < 32; kq++)
+            if (kq < nk1) af[kq] = ar[(int64_t)(4 * kq) * ld];
+    }
+    if (w == 0) {
+        bool remote = false;
+        const bool ok = tpart_wait_linv<T, DIST>(a, k - 1, remote);
+        if (ok) {
+            if (remote) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+            else __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        }
+        s_ok = ok ? 1 : 0;
+    }
+    __syncthreads();
+    if (!__builtin_amdgcn_readfirstlane(s_ok)) return false;
+    long long* xs = a.xt ? a.xt + 4 * (4 * (int64_t)k + C) : nullptr;
+    if (xs && w == 0) xs[0] = wall_clock64();  // Linv_{k-1} seen
+    // Linv_{k-1} rows 16 g0 + r (r < 16) and 16 g1 + r - 16 (r >= 16), all 128 columns (zero
+    // above the diagonal), as Ls[r + col TP_LSB]: four 16-B loads per thread, all in flight
+    {
+        vec_t lv[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int e = u * NT + t, r = 2 * (e & 15), col = e >> 4;
+            const int row = (r < 16) ? 16 * g0 + r : 16 * g1 + r - 16;
+            lv[u] = *reinterpret_cast<const vec_t*>(Lp + row + (int64_t)col * DB);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int e = u * NT + t;
+            *reinterpret_cast<vec_t*>(Ls + 2 * (e & 15) + (e >> 4) * TP_LSB) = lv[u];
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (w == 0) st_agent(tf + C, 1);  // "A read": this part's A fragments have landed
+    // acc[x][reg] = T(16 w + lr, 16 g_x + orow(lk, reg))
+    acc_t acc[2] = {acc_t{0}, acc_t{0}};
+#pragma unroll
+    for (int kq = 0; kq < 32; kq++) {
+        if (kq < nk1) {
+            const int kc = 4 * kq + lk;
+            acc[1] = Tr::mma(Ls[(16 + lr) + kc * TP_LSB], af[kq], acc[1]);
+            if (kq < nk0) acc[0] = Tr::mma(Ls[lr + kc * TP_LSB], af[kq], acc[0]);
+        }
+    }
+    if (xs && w == 0) xs[1] = wall_clock64();  // T computed
+    // T's 32 columns -> LDS (operand of P): column x 16 + c of Ts = group g_x's column c
+#pragma unroll
+    for (int x = 0; x < 2; x++)
+#pragma unroll
+        for (int reg = 0; reg < 4; reg++) smem[(16 * w + lr) + (16 * x + Tr::orow(lk, reg)) * TP_TSS] = acc[x][reg];
+    // the in-place stores overwrite A columns the other parts read: wait for their "A read"
+    // (the four parts hold consecutive tickets and need only a CU each: P >= 4, potrf_tiles)
+    if (w == 0) s_ok = tpart_wait_flags<T>(a, tf, 4, 1) ? 1 : 0;
+    __syncthreads();
+    if (!__builtin_amdgcn_readfirstlane(s_ok)) return false;
+    if (xs && w == 0) xs[2] = wall_clock64();
+#pragma unroll
+    for (int x = 0; x < 2; x++)
+#pragma unroll
+        for (int reg = 0; reg < 4; reg++)
+            st_sc1(Akm + 16 * w + lr + (int64_t)(16 * (x ? g1 : g0) + Tr::orow(lk, reg)) * ld, acc[x][reg]);
+    // P = T_p T_p^T (rank 32): the lower 16 x 16 tiles, wave blocks as the diagonal tile's (MAP 2)
+    int sr, sc;
+    wave_block<2>(w, sr, sc);
+    acc_t pacc[2][4];
+#pragma unroll
+    for (int x = 0; x < 2; x++)
+#pragma unroll
+        for (int y = 0; y < 4; y++) pacc[x][y] = acc_t{0};
+#pragma unroll
+    for (int kq = 0; kq < 8; kq++) {
+        const int kc = 4 * kq + lk;
+        T fb[2], fa[4];
+#pragma unroll
+        for (int x = 0; x < 2; x++) fb[x] = smem[(sc * 32 + x * 16 + lr) + kc * TP_TSS];
+#pragma unroll
+        for (int y = 0; y < 4; y++) fa[y] = smem[(sr * 64 + y * 16 + lr) + kc * TP_TSS];
+#pragma unroll
+        for (int x = 0; x < 2; x++)
+#pragma unroll
+            for (int y = 0; y < 4; y++)
+                if (4 * sr + y >= 2 * sc + x) pacc[x][y] = Tr::mma(fb[x], fa[y], pacc[x][y]);
+    }
+#pragma unroll
+    for (int x = 0; x < 2; x++)
+#pragma unroll
+        for (int reg = 0; reg < 4; reg++) {
+            const int jl = sc * 32 + x * 16 + Tr::orow(lk, reg);
+#pragma unroll
+            for (int y = 0; y < 4; y++)
+                if (4 * sr + y >= 2 * sc + x) st_sc1(pc + (sr * 64 + y * 16 + lr) + (int64_t)jl * DB, pacc[x][y][reg]);
+        }
+    if (xs && w == 0) xs[3] = wall_clock64();  // P computed (its stores in flight)
+    publish(tf + C, 2, false);
+    return true;
+}
+
+template <typename T, bool DIST>
+__device__ __forceinline__ bool tpart_task(const TpCtx<T>& a, T* Akm, int64_t ld, const T* Lp, int k, int c, T* smem,
+                                           int& s_ok, const int t) {
+    return tpart_run<T, DIST>(a, Akm, ld, Lp, a.pbuf + (int64_t)c * DB * DB, a.tflag + 4 * k, k, c, smem, s_ok, t);
+}
+
+// DIAGX(k > 0) of the split step: S = A_kk - P_0 - P_1 - P_2 - P_3 into the factor's LDS image
+// (the 36 lower 16 x 16 tiles), then L_{k,k-1} is final (lcnt[k] = k).  A_kk loads at once
+// (the task waited only for it); the four parts finish within ~0.3 us of each other, so each
+// wave waits for all four flags and issues the 36 loads of its products together -- one
+// memory latency on the chain instead of four (summing each product as its flag came cost
+// ~1.9 us per product).  Each wave owns 576 element pairs, 9 per lane (lower tile
+// tau = q / 128, pair q % 8 of its column (q % 128) / 8): no barrier until the image is full.
+template <typename T>
+__device__ __noinline__ bool diagx_split(const TpCtx<T> a, const T* __restrict__ Akk, int64_t ld, int k, T* smem,
+                                         int& s_ok, const int t) {
+    typedef typename Mfma<T>::vec_t vec_t;
+    const int lane = t & 63, w = t >> 6;
+    const int* tf = a.tflag + 4 * k;
+    long long* xs = a.xt ? a.xt + 4 * (4 * (int64_t)a.nc + k) : nullptr;
+    int rr[9], cc[9];
+#pragma unroll
+    for (int u = 0; u < 9; u++) {
+        const int q = 576 * w + 64 * u + lane, tau = q >> 7, e = q & 127;
+        int R = 0;  // lower tile tau = R (R + 1) / 2 + C
+        while ((R + 1) * (R + 2) / 2 <= tau) R++;
+        const int C = tau - R * (R + 1) / 2;
+        rr[u] = 16 * R + 2 * (e & 7);
+        cc[u] = 16 * C + (e >> 3);
+    }
+    vec_t s[9];
+#pragma unroll
+    for (int u = 0; u < 9; u++) s[u] = *reinterpret_cast<const vec_t*>(Akk + rr[u] + (int64_t)cc[u] * ld);
+    const bool ok = tpart_wait_flags<T>(a, tf, 4, 2);  // this wave polls the four parts itself
+    if (ok) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        if (xs && w == 0) xs[2] = wall_clock64();  // every P_c seen
+        vec_t p[4][9];
+#pragma unroll
+        for (int c = 0; c < 4; c++)
+#pragma unroll
+            for (int u = 0; u < 9; u++)
+                p[c][u] = *reinterpret_cast<const vec_t*>(a.pbuf + (int64_t)c * DB * DB + rr[u] + cc[u] * DB);
+#pragma unroll
+        for (int u = 0; u < 9; u++) {
+#pragma unroll
+            for (int c = 0; c < 4; c++) s[u] -= p[c][u];  // fixed order: P_0, P_1, P_2, P_3
+            smem[rr[u] + cc[u] * SIL] = s[u][0];
+            smem[rr[u] + 1 + cc[u] * SIL] = s[u][1];
+        }
+    }
+    if (w == 0) s_ok = ok ? 1 : 0;
+    __syncthreads();
+    if (!__builtin_amdgcn_readfirstlane(s_ok)) return false;
+    // every column block of L_{k,k-1} is stored (each TPART's flag came after its stores)
+    if (w == 0) st_agent(a.lcnt + k, k);
+    if (xs && w == 0) xs[3] = wall_clock64();  // S in the image
+    return true;
+}
+
+template <typename T>
+__device__ __forceinline__ TpCtx<T> tp_ctx(const Args<T>& a) {
+    return TpCtx<T>{a.ctl, a.lcnt, a.tflag, a.pbuf, a.dist, a.tlimit, a.xt, a.nc};
+}
+
 template <typename T, bool DIST>
 __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
@@ -1633,7 +1928,7 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
                 bool remote = false;  // DIST: an input pushed by another rank (system-scope acquire)
                 if constexpr (DIST) {
                     const PtDist<T>& D = *a.dist;
-                    const int dep = (type == T_DIAGX) ? i - 1 : (type == T_BUILD ? -1 : j);
+                    const int dep = (type == T_DIAGX) ? i - 1 : ((type == T_BUILD || type == T_TPART) ? -1 : j);
                     remote = dep >= 0 && __builtin_amdgcn_readfirstlane(D.loc[dep]) < 0 &&
                              !__builtin_amdgcn_readfirstlane(D.acq_agent);
                 }
@@ -1657,7 +1952,11 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
             // rows from the window, final tiles pushed to their consumers' mailboxes ----------
             const PtDist<T>& D = *a.dist;
             bool ok = true;
-            if (type == T_BUILD) {
+            if (type == T_TPART) {
+                if constexpr (std::is_same<T, double>::value && DIAG_LA && SPLIT_CODE)
+                    ok = tpart_task<T, true>(tp_ctx(a), dist_tile(a.A, D, i, i - 1), DB,
+                                             a.Linv + (int64_t)(i - 1) * DB * DB, i, j, smem, s_ok, tid);
+            } else if (type == T_BUILD) {
                 const TileBuild<T>& b = *a.tb;
                 T* tij = dist_tile(a.A, D, i, j);
                 // build_tile_sum addresses element (gi, gj) at base + gi + gj ld (global indices)
@@ -1703,7 +2002,10 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
                 T* Akk = dist_tile(a.A, D, k, k);
                 T* Akm = k > 0 ? dist_tile(a.A, D, k, k - 1) : nullptr;
                 constexpr bool fused_ts = std::is_same<T, double>::value && DIAG_LA;
-                if (fused_ts && k > 0) {
+                if (SPLIT_CODE && fused_ts && k > 0 && a.split) {
+                    ok = diagx_split<T>(tp_ctx(a), Akk, DB, k, smem, s_ok, tid);
+                    if (!ok) break;
+                } else if (fused_ts && k > 0) {
                     diagx_ts<T>(Akm, Akk, DB, a.Linv + (int64_t)(k - 1) * DB * DB, a.lcnt + k, k, smem, tid, false);
                 } else if (k > 0) {
                     tile_gemm<T, false, 1>(Akm, DB, Akm, DB, a.Linv + (int64_t)(k - 1) * DB * DB, DB, GT, false, smem,
@@ -1741,7 +2043,14 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
             if (!ok) break;
         } else {
         T* Ci = a.A + (int64_t)i * GT;  // row block i, column 0
-        if (type == T_BUILD) {
+        constexpr bool fused_ts = std::is_same<T, double>::value && DIAG_LA;
+        // (a failed wait inside a task has raised C_ERR: the task ends on garbage, which the
+        // launch reports as info = -1, and the next wait_inputs drains the workgroup)
+        if (type == T_TPART) {
+            if constexpr (fused_ts && SPLIT_CODE)
+                (void)tpart_task<T, false>(tp_ctx(a), Ci + (int64_t)(i - 1) * GT * ld, ld,
+                                           a.Linv + (int64_t)(i - 1) * DB * DB, i, j, smem, s_ok, tid);
+        } else if (type == T_BUILD) {
             // ver[i][j] goes from -1 (not built) to 0; the tile's values go out write-through
             const TileBuild<T>& b = *a.tb;
             bool bad;
@@ -1772,8 +2081,10 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
             const int k = i;
             T* Akk = Ci + (int64_t)k * GT * ld;
             long long dt[4] = {0, 0, 0, 0};
-            constexpr bool fused_ts = std::is_same<T, double>::value && DIAG_LA;
-            if (fused_ts && k > 0) {
+            if (SPLIT_CODE && fused_ts && k > 0 && a.split) {
+                (void)diagx_split<T>(tp_ctx(a), Akk, ld, k, smem, s_ok, tid);
+                if (a.trace) dt[0] = dt[1] = wall_clock64();
+            } else if (fused_ts && k > 0) {
                 T* Akm = Ci + (int64_t)(k - 1) * GT * ld;
                 dt[0] = diagx_ts<T>(Akm, Akk, ld, a.Linv + (int64_t)(k - 1) * DB * DB, a.lcnt + k, k, smem, tid,
                                     a.trace != nullptr);
@@ -1827,7 +2138,26 @@ struct Cost {  // per-task durations (us, one CU), calibrated from GPRX_PT_TRACE
     double early = 31.0;   // DIAGX(k) publishes L_{k,k-1} after its trsm and syrk phases
     double diagf = 0.97;   // diagonal-tile update relative to a full one (2 of 8 waves idle)
     double build = 28.0;   // BUILD tile (pair statistics + kernel values + stores)
+    // the split diagonal step (f64): TPART(k, c) takes tpart + tpart_c (c + 1); DIAGX(k) then
+    // sums the products and factors (diagx_s), publishing L_{k,k-1} early_s into it
+    double tpart = 9.0, tpart_c = 0.0;
+    double diagx_s = 44.0, early_s = 2.0;
 };
+
+// TPART tickets of one k in the order TPART(k, 3), (k, 2), (k, 1), (k, 0): each part waits for
+// the reads of the parts with a larger c, so those must hold the earlier tickets (the parts
+// have the same inputs and one consumer, DIAGX(k): permuting them over their slots keeps
+// every other order of the list)
+static void order_tparts(std::vector<int4>& list) {
+    std::map<int, std::vector<int>> pos;
+    for (size_t q = 0; q < list.size(); q++)
+        if ((list[q].x & 0xff) == T_TPART) pos[list[q].y].push_back((int)q);
+    for (auto& kv : pos) {
+        std::vector<int>& v = kv.second;
+        std::sort(v.begin(), v.end());
+        for (size_t u = 0; u < v.size(); u++) list[v[u]].z = 3 - (int)u;
+    }
+}
 
 struct Task {
     int type, i, j, b0, nb;
@@ -1890,8 +2220,10 @@ static void tile_chunks(int i, int j, int W, int near, std::vector<std::pair<int
 
 // ni > 0: the last ni row blocks are the identity (the inverse L^{-1} riding along as
 // L^{-T} rows): identity block a = i - (nr - ni) has zero L blocks before column block a.
-static Schedule make_schedule(int nc, int nr, int W, int near, int P, const Cost& cm, bool build, int ni = 0,
-                              int ratio = 0) {
+static Schedule make_schedule(int nc, int nr, int W, int near, int P, const Cost& cm0, bool build, int ni = 0,
+                              int ratio = 0, bool split = false) {
+    Cost cm = cm0;
+    if (split) cm.early = cm.early_s;
     const int nr0 = nr - ni;
     auto start_of = [&](int i) { return i >= nr0 ? i - nr0 : 0; };
     std::vector<Task> tasks;
@@ -1937,6 +2269,19 @@ static Schedule make_schedule(int nc, int nr, int W, int near, int P, const Cost
             }
     }
     auto make_diagx = [&](int k) {
+        if (split && k >= 1) {  // TPART(k, 3..0), then DIAGX(k) on their products
+            int tp[4];
+            for (int c = 3; c >= 0; c--) {
+                tp[c] = add(T_TPART, k, c, 0, 0, cm.tpart + cm.tpart_c * (c + 1));
+                dep(tp[c], diagx[k - 1]);
+                dep(tp[c], last_upd[(size_t)k * nc + (k - 1)]);
+            }
+            const int id = add(T_DIAGX, k, k, 0, 0, cm.diagx_s);
+            diagx[k] = id;
+            for (int c = 0; c < 4; c++) dep(id, tp[c]);
+            dep(id, last_upd[(size_t)k * nc + k]);
+            return;
+        }
         const double dur = (k == 0) ? cm.diag0 : cm.diagx;
         const int id = add(T_DIAGX, k, k, 0, 0, dur);
         diagx[k] = id;
@@ -2044,6 +2389,7 @@ static Schedule make_schedule(int nc, int nr, int W, int near, int P, const Cost
     }
     S.est_us = now;
     S.ntasks = nt;
+    if (split) order_tparts(S.list);
     return S;
 }
 
@@ -2076,8 +2422,10 @@ static void c_chunks(int a, int W, int nc, std::vector<std::pair<int, int>>& out
     }
 }
 
-static DistSched make_schedule_dist(int nc, bool inv, int W, int near, int P, int g, int gb, int ww, const Cost& cm,
-                                    bool build, double push_us, double rel_us, int ratio = 0) {
+static DistSched make_schedule_dist(int nc, bool inv, int W, int near, int P, int g, int gb, int ww, const Cost& cm0,
+                                    bool build, double push_us, double rel_us, int ratio = 0, bool split = false) {
+    Cost cm = cm0;
+    if (split) cm.early = cm.early_s;
     const int nr = nc + 1 + (inv ? nc : 0), nci = inv ? 2 * nc : nc;
     auto own = [&](int i) { return i <= nc ? (i / gb) % g : ((i - nc - 1) / gb) % g; };
     auto colx = [&](int j) { return j > nc ? j - 1 : j; };  // counter column of tile (., j)
@@ -2158,9 +2506,17 @@ static DistSched make_schedule_dist(int nc, bool inv, int W, int near, int P, in
         dep(id, prod);
     };
     auto make_diagx = [&](int k) {
-        const int id = add(T_DIAGX, k, k, 0, 0, (k == 0) ? cm.diag0 : cm.diagx, own(k));
+        int tp[4] = {-1, -1, -1, -1};
+        if (split && k >= 1)  // TPART(k, 3..0) on the owner of row block k
+            for (int c = 3; c >= 0; c--) {
+                tp[c] = add(T_TPART, k, c, 0, 0, cm.tpart + cm.tpart_c * (c + 1), own(k));
+                dep(tp[c], linv(k - 1, own(k)));
+                dep(tp[c], last_upd[(size_t)k * nci + (k - 1)]);
+            }
+        const int id = add(T_DIAGX, k, k, 0, 0, (k == 0) ? cm.diag0 : (split ? cm.diagx_s : cm.diagx), own(k));
         diagx[k] = id;
         if (k >= 1) {
+            for (int c = 0; c < 4; c++) dep(id, tp[c]);
             dep(id, linv(k - 1, own(k)));
             dep(id, last_upd[(size_t)k * nci + (k - 1)]);
             dep(id, last_upd[(size_t)k * nci + k]);
@@ -2320,6 +2676,8 @@ static DistSched make_schedule_dist(int nc, bool inv, int W, int near, int P, in
     }
     S.est_us = now;
     S.W = W;
+    if (split)
+        for (auto& l : S.lists) order_tparts(l);
     return S;
 }
 
@@ -2328,6 +2686,7 @@ struct Params {
     // 1.6-2.0% faster than W = 32, near = 1; at N = 4096 (chain-bound) near = 1 stays 6% faster
     int W = 64, near = -1;  // near < 0: by size (near_for)
     int ratio = -1;         // chunk-width rule of tile_chunks: < 0 picked per shape by the simulation
+    int split = 1;          // f64: the split diagonal step (TPART tasks); GPRX_PT_SPLIT=0 turns it off
     Cost cm;
     int near_for(int nc) const { return near >= 0 ? near : (nc <= 64 ? 1 : 0); }
     Params() {
@@ -2339,6 +2698,9 @@ struct Params {
         if (const char* e = std::getenv("GPRX_PT_K128_US")) cm.k128 = std::atof(e);
         if (const char* e = std::getenv("GPRX_PT_OVH_US")) cm.ovh = std::atof(e);
         if (const char* e = std::getenv("GPRX_PT_BUILD_US")) cm.build = std::atof(e);
+        if (const char* e = std::getenv("GPRX_PT_SPLIT")) split = std::atoi(e);
+        if (const char* e = std::getenv("GPRX_PT_TPART_US")) cm.tpart = std::atof(e);
+        if (const char* e = std::getenv("GPRX_PT_DIAGXS_US")) cm.diagx_s = std::atof(e);
     }
 };
 static const Params& params() {
@@ -2349,12 +2711,12 @@ static const Params& params() {
 // the chunk rule with the shortest simulated makespan (ratio 0: the fixed rule; 8, 4, 2: width
 // capped by the distance to the tile's last panel), unless GPRX_PT_RATIO fixes it
 static const int kRatios[] = {0, 8, 4, 2};
-static Schedule best_schedule(int nc, int nr, const Params& pr, int P, bool build, int ni) {
-    if (pr.ratio >= 0) return make_schedule(nc, nr, pr.W, pr.near_for(nc), P, pr.cm, build, ni, pr.ratio);
+static Schedule best_schedule(int nc, int nr, const Params& pr, int P, bool build, int ni, bool split) {
+    if (pr.ratio >= 0) return make_schedule(nc, nr, pr.W, pr.near_for(nc), P, pr.cm, build, ni, pr.ratio, split);
     Schedule best;
     bool have = false;
     for (int r : kRatios) {
-        Schedule S = make_schedule(nc, nr, pr.W, pr.near_for(nc), P, pr.cm, build, ni, r);
+        Schedule S = make_schedule(nc, nr, pr.W, pr.near_for(nc), P, pr.cm, build, ni, r, split);
         if (!have || S.est_us < best.est_us * 0.995) {  // a wider rule must win by > 0.5%
             best = std::move(S);
             have = true;
@@ -2362,6 +2724,11 @@ static Schedule best_schedule(int nc, int nr, const Params& pr, int P, bool buil
     }
     return best;
 }
+
+// the split diagonal step runs for f64 (the look-ahead factor's LDS image), unless disabled
+static bool split_for(bool f64) { return f64 && DIAG_LA && SPLIT_CODE && params().split != 0; }
+// (the four parts of a step wait for each other: at least four workgroups)
+static bool split_for(bool f64, int P) { return P >= 4 && split_for(f64); }
 
 }  // namespace pt
 
@@ -2373,8 +2740,9 @@ struct PtState {
         double est_us = 0;
         std::vector<int4> host;
     };
-    std::map<std::tuple<int, int, bool, int>, Dev> sched;
+    std::map<std::tuple<int, int, bool, int, bool>, Dev> sched;
     int* ctr = nullptr;
+    void* pbuf = nullptr;  // the split diagonal step's four TPART products (DB x DB each)
     size_t ctr_ints = 0;
     int ncu = 0;
     int* dbg = nullptr;  // pinned host status words (GPRX_PT_DEBUG)
@@ -2384,6 +2752,7 @@ struct PtState {
     void* tb = nullptr;  // device copy of the launch's TileBuild
     ~PtState() {
         if (tb) (void)hipFree(tb);
+        if (pbuf) (void)hipFree(pbuf);
         if (trace) (void)hipFree(trace);
         if (dbg) (void)hipHostFree(dbg);
         for (auto& kv : sched) (void)hipFree(kv.second.list);
@@ -2398,10 +2767,13 @@ void pt_state_free(PtState* p) { delete p; }
 static PtState* g_pt_state = nullptr;
 int64_t pt_trace_copy(int32_t* tasks, long long* times, int64_t max) {
     if (!g_pt_state || !g_pt_state->trace || !g_pt_state->last_list) return 0;
-    const int64_t n = std::min<int64_t>(max, g_pt_state->trace_n + 2 * g_pt_state->trace_nc);
+    // rows: one per ticket, then nc DIAGX phase rows, nc diagonal-factor rows, 4 nc TPART stamp rows,
+    // nc split-DIAGX stamp rows
+    const int64_t n = std::min<int64_t>(max, g_pt_state->trace_n + 7 * g_pt_state->trace_nc);
     GPRX_HIP(hipDeviceSynchronize());
     GPRX_HIP(hipMemcpy(times, g_pt_state->trace, sizeof(long long) * 4 * n, hipMemcpyDeviceToHost));
-    std::memcpy(tasks, g_pt_state->last_list->data(), sizeof(int4) * n);
+    const int64_t nl = std::min<int64_t>(n, (int64_t)g_pt_state->last_list->size());
+    std::memcpy(tasks, g_pt_state->last_list->data(), sizeof(int4) * nl);
     return n;
 }
 
@@ -2453,7 +2825,8 @@ void potrf_tiles(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info
     GPRX_REQUIRE(!build_only || fused, GPRX_ERR_ARG, "potrf_tiles: build_only needs a fused build");
     // build_only (a parity hook, gprx_dev_build_matrix): the ticket list holds the BUILD tasks
     // alone, so the launch writes exactly the covariance tiles the fused factorisation starts from
-    auto key = std::make_tuple(nc, nr, fused, build_only ? -1 : ni);
+    const bool split = split_for(std::is_same<T, double>::value, st.ncu);
+    auto key = std::make_tuple(nc, nr, fused, build_only ? -1 : ni, split);
     auto it = st.sched.find(key);
     if (it == st.sched.end()) {
         const Params& pr = params();
@@ -2462,7 +2835,7 @@ void potrf_tiles(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info
             for (int i = 0; i < nc; i++)
                 for (int j = 0; j <= i; j++) S.list.push_back(make_int4(T_BUILD, i, j, 0));
         } else {
-            S = best_schedule(nc, nr, pr, st.ncu, fused, ni);
+            S = best_schedule(nc, nr, pr, st.ncu, fused, ni, split);
         }
         PtState::Dev d;
         d.n = (int64_t)S.list.size();
@@ -2473,7 +2846,7 @@ void potrf_tiles(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info
         it = st.sched.emplace(key, d).first;
     }
     const PtState::Dev& sd = it->second;
-    const size_t need = (size_t)C_NCTL + nr + (size_t)nr * nc;
+    const size_t need = (size_t)C_NCTL + nr + (size_t)nr * nc + 4 * (size_t)nc;  // + the TPART states
     if (st.ctr_ints < need) {
         if (st.ctr) GPRX_HIP(hipFree(st.ctr));
         st.ctr = nullptr;
@@ -2504,6 +2877,10 @@ void potrf_tiles(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info
     a.info = info;
     a.tb = nullptr;
     a.dist = nullptr;
+    a.split = split ? 1 : 0;
+    a.tflag = st.ctr + C_NCTL + nr + (size_t)nr * nc;
+    if (split && !st.pbuf) GPRX_HIP(hipMalloc(&st.pbuf, sizeof(T) * 4 * DB * DB));
+    a.pbuf = static_cast<T*>(st.pbuf);
     if (fused) {
         GPRX_REQUIRE(build->nf == np, GPRX_ERR_ARG, "potrf_tiles: build features must have np rows");
         if (!st.tb) GPRX_HIP(hipMalloc(&st.tb, sizeof(TileBuild<double>)));
@@ -2512,15 +2889,18 @@ void potrf_tiles(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info
     }
     a.dbg = nullptr;
     a.trace = nullptr;
+    a.xt = nullptr;
     static const bool tracing = std::getenv("GPRX_PT_TRACE") != nullptr;
     if (tracing) {
-        if (st.trace_n + 2 * st.trace_nc < sd.n + 2 * nc) {
+        if (st.trace_n + 7 * st.trace_nc < sd.n + 7 * nc) {  // + the split step's 5 nc stamp rows
             if (st.trace) GPRX_HIP(hipFree(st.trace));
-            GPRX_HIP(hipMalloc(&st.trace, sizeof(long long) * 4 * (sd.n + 2 * nc)));
+            GPRX_HIP(hipMalloc(&st.trace, sizeof(long long) * 4 * (sd.n + 7 * nc)));
         }
         st.trace_n = sd.n;
         st.trace_nc = nc;
         a.trace = st.trace;
+        a.xt = st.trace + 4 * (sd.n + 2 * nc);
+        GPRX_HIP(hipMemsetAsync(a.xt, 0, sizeof(long long) * 4 * 5 * nc, s));
         g_pt_state = &st;
         st.last_list = &sd.host;
     }
@@ -2556,7 +2936,7 @@ void potrf_tiles(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info
 }
 
 // ---- distributed factorisation: per-rank ticket lists and one rank's launch ------------------
-DistSched potrf_dist_schedule(int nc, int g, int gb, int ww, int P, bool build, bool inv, int ratio) {
+DistSched potrf_dist_schedule(int nc, int g, int gb, int ww, int P, bool build, bool inv, int ratio, bool f64) {
     const pt::Params& pr = pt::params();
     // a push: one tile's stores over xGMI plus the flag (measured on one GPU as a same-device
     // copy; GPRX_DIST_PUSH_US / GPRX_DIST_REL_US override)
@@ -2568,7 +2948,7 @@ DistSched potrf_dist_schedule(int nc, int g, int gb, int ww, int P, bool build, 
     int W = 1;
     while (2 * W <= std::min(pr.W, std::max(1, ww / 2))) W *= 2;
     return pt::make_schedule_dist(nc, inv, W, pr.near_for(nc), P, g, std::max(1, gb), ww, pr.cm, build, push_us, rel_us,
-                                  pr.ratio >= 0 ? pr.ratio : ratio);
+                                  pr.ratio >= 0 ? pr.ratio : ratio, pt::split_for(f64, P));
 }
 
 template <typename T>
@@ -2592,6 +2972,10 @@ void potrf_tiles_dist_launch(const DistLaunch<T>& L) {
     a.dist = L.dist_dev;
     a.dbg = L.dbg;
     a.trace = L.trace;
+    a.xt = nullptr;
+    a.split = L.split;
+    a.pbuf = L.pbuf;
+    a.tflag = L.tflag;
     auto lds_of = [](size_t b) { return std::max<size_t>(b + 16, 96 * 1024); };
     const size_t lds = lds_of(pt_lds_bytes<T>());
     static bool attr = false;
@@ -2614,11 +2998,14 @@ int64_t potrf_tiles_schedule_stats(int nc, int nr, int P, bool build, double* es
     if (nc < 1 || nr < nc || P < 1 || ni < 0 || ni > nr - nc)
         throw Error{GPRX_ERR_ARG, "potrf tile schedule: need nc >= 1, nr >= nc + ni, P >= 1"};
     const pt::Params& pr = pt::params();
-    pt::Schedule S = ratio >= 0 ? pt::make_schedule(nc, nr, pr.W, pr.near_for(nc), P, pr.cm, build, ni, ratio)
-                                : pt::best_schedule(nc, nr, pr, P, build, ni);
+    const bool split = pt::split_for(true);  // the f64 schedule
+    pt::Schedule S = ratio >= 0 ? pt::make_schedule(nc, nr, pr.W, pr.near_for(nc), P, pr.cm, build, ni, ratio, split)
+                                : pt::best_schedule(nc, nr, pr, P, build, ni, split);
     if (est_us) *est_us = S.est_us;
     return S.ntasks;
 }
+
+bool potrf_split_for(bool f64, int P) { return pt::split_for(f64, P); }
 
 template void potrf_tiles<double>(double*, int64_t, int64_t, int64_t, double*, int*, Exec&, const TileBuild<double>*,
                                   int, bool);

@@ -36,9 +36,12 @@ k = L.gprx_dev_pt_trace(tasks.ctypes.data, times.ctypes.data, MAX)
 ntask = int(((k - 1) // 1))
 # the last nc rows of `times` are DIAGX phase stamps {trsm done, published, syrk done, diag done}
 nc = n // 128
-dprof = times[k - nc:k].copy()          # diag_factor {load, pivot phases, update phases} ticks
-dph = times[k - 2 * nc:k - nc].copy()
-tasks, times = tasks[:k - 2 * nc], times[:k - 2 * nc]
+nt = k - 7 * nc                         # rows: tickets, DIAGX phases, diag_factor, TPART / split stamps
+dph = times[nt:nt + nc].copy()
+dprof = times[nt + nc:nt + 2 * nc].copy()  # diag_factor {load, pivot phases, update phases} ticks
+xtp = times[nt + 2 * nc:nt + 6 * nc].reshape(nc, 4, 4).copy()  # TPART(k, c) stamps
+xdg = times[nt + 6 * nc:nt + 7 * nc].copy()                   # split DIAGX(k) stamps
+tasks, times = tasks[:nt], times[:nt]
 out = os.environ.get("PT_TRACE_OUT")
 if out:
     np.savez_compressed(out, tasks=tasks, times=times)
@@ -56,12 +59,19 @@ okc = dur_ticks > 500
 clock_ghz = float(np.median(cyc[okc] / dur_ticks[okc]) * 0.1)
 res = {"clock_ghz_median": clock_ghz, "n": n, "ms_devbench": ms.value, "span_us": span, "tasks": int(k), "workers": P,
        "busy_frac": float(ex.sum() / (span * P)), "wait_frac": float(wt.sum() / (span * P))}
-names = {0: "DIAGX", 1: "TRSM", 2: "UPD", 3: "BUILD"}
-for t in (0, 1, 2, 3):
+names = {0: "DIAGX", 1: "TRSM", 2: "UPD", 3: "BUILD", 4: "TPART"}
+for t in (0, 1, 2, 3, 4):
     for b in sorted(set(nb[typ == t])):
         m = (typ == t) & (nb == b)
         diag = (tasks[:, 1] == tasks[:, 2])
         key = f"{names[t]}{'' if t != 2 else '_nb' + str(b)}"
+        if t == 4:  # the split diagonal step's parts, by column block c
+            for c in range(4):
+                mc = m & (tasks[:, 2] == c)
+                if mc.any():
+                    res[f"TPART_c{c}"] = {"count": int(mc.sum()), "exec_us_mean": float(ex[mc].mean()),
+                                          "wait_us_mean": float(wt[mc].mean())}
+            continue
         res[key] = {"count": int(m.sum()), "exec_us_mean": float(ex[m].mean()), "exec_us_p90": float(np.percentile(ex[m], 90)),
                     "wait_us_mean": float(wt[m].mean())}
         if t == 2:
@@ -69,7 +79,7 @@ for t in (0, 1, 2, 3):
             if md.any():
                 res[key]["diagtile_exec_us_mean"] = float(ex[md].mean())
 # worker time per task type, in ms of the whole chip (sum of exec / workers)
-res["chip_ms_by_type"] = {names[t]: round(float(ex[typ == t].sum() / P / 1e3), 3) for t in (0, 1, 2, 3)}
+res["chip_ms_by_type"] = {names[t]: round(float(ex[typ == t].sum() / P / 1e3), 3) for t in (0, 1, 2, 3, 4)}
 res["chip_ms_wait"] = round(float(wt.sum() / P / 1e3), 3)
 res["chip_ms_idle"] = round(float(span / 1e3 - (ex.sum() + wt.sum()) / P / 1e3), 3)
 res["upd_panels"] = int(nb[typ == 2].sum())
@@ -83,6 +93,10 @@ res["diagx_exec_mean_us"] = float((en - st).mean())
 gaps = st[1:] - en[:-1]
 res["diagx_gap_mean_us"] = float(gaps.mean())
 res["diagx_chain_first_last"] = [float(st[0]), float(en[-1])]
+# the chain's period: DIAGX(k) end - DIAGX(k-1) end (the split step's parts included)
+per = en[1:] - en[:-1]
+res["chain_period_us"] = {"mean": float(per.mean()), "median": float(np.median(per)),
+                          "last16_mean": float(per[-16:].mean())}
 # time profile: busy workers per 1 ms window
 bins = np.arange(0, span + 1000, 1000)
 busy = []
@@ -100,5 +114,22 @@ res["diagx_phase_us"] = {"trsm_tile": float(np.mean((dv[:, 0] - (times[d[1:], 1]
                          "final_publish": float(np.mean((times[d[1:], 2] - dv[:, 3]) / 100.0))}
 res["diag_factor_us"] = {"load": float(dprof[:, 0].mean() / 100), "pivot_solve": float(dprof[:, 1].mean() / 100),
                          "update": float(dprof[:, 2].mean() / 100)}
+# the split step: per k >= 1, microseconds after Linv_{k-1} was published (DIAGX(k-1) done)
+if (xtp[1:, :, 0] > 0).all():
+    t_lin = tk[d[:-1], 2] * 100.0 + t0  # DIAGX(k-1) published, ticks
+    rel = lambda a: (a - t_lin[:, None]) / 100.0
+    ph = {}
+    for c in range(4):
+        s_ = xtp[1:, c, :]
+        ph[f"c{c}"] = {"linv_seen": float(np.median(rel(s_[:, :1]))), "t_done": float(np.median(rel(s_[:, 1:2]))),
+                       "stored": float(np.median(rel(s_[:, 2:3]))), "p_done": float(np.median(rel(s_[:, 3:4])))}
+        tpi = np.where((typ == 4) & (tasks[:, 2] == c))[0]
+        tpi = tpi[np.argsort(tasks[tpi, 1])]
+        ph[f"c{c}"]["published"] = float(np.median((tk[tpi, 2] * 100.0 + t0 - t_lin) / 100.0))
+    dgs = xdg[1:]
+    ph["diagx"] = {"start": float(np.median((tk[d[1:], 1] * 100.0 + t0 - t_lin) / 100.0)),
+                   "parts_seen": float(np.median(rel(dgs[:, 2:3]))), "s_done": float(np.median(rel(dgs[:, 3:4]))),
+                   "end": float(np.median((tk[d[1:], 2] * 100.0 + t0 - t_lin) / 100.0))}
+    res["split_step_us"] = ph
 res["diagx_last16"] = [[round(float(e - s_), 1), round(float(g), 1)] for s_, e, g in zip(st[-16:], en[-16:], np.r_[gaps, 0][-16:])]
 print(json.dumps(res, indent=1))

@@ -29,6 +29,11 @@ def _sched(nc, nr, P=256, build=False, ident=False, ratio=0):
 W_DEF = 64  # k_ptiles.hip Params defaults: update chunk width, single-panel tail by size
 
 
+def tparts(nc):
+    """The split diagonal step (f64 schedule): TPART(k, 0..3) for every k >= 1."""
+    return 4 * max(0, nc - 1)
+
+
 def near_def(nc):
     return 1 if nc <= 64 else 0
 
@@ -56,7 +61,7 @@ def _expected_tasks(nc, nr, W=W_DEF, near=None):
                     b += p
                 p //= 2
             upd += e - b
-    return diag + trsm + upd
+    return diag + trsm + upd + tparts(nc)
 
 
 def _ratio_chunks(e, W, near, ratio):
@@ -84,7 +89,7 @@ def _expected_tasks_ratio(nc, nr, ratio, W=W_DEF):
             e = j - 1 if i == j else j
             if e > 0:
                 upd += len(_ratio_chunks(e, W, near, ratio))
-    return nc + trsm + upd
+    return nc + trsm + upd + tparts(nc)
 
 
 @pytest.mark.parametrize("nc,extra", [(1, 0), (1, 1), (2, 1), (7, 1), (8, 1), (9, 1), (33, 1), (128, 1), (64, 0)])
