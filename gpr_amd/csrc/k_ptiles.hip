@@ -1082,18 +1082,22 @@ constexpr bool DIAG_LA = false;
 // (out of line: its registers (fact32's accumulators, the pivot block) no longer count against
 // the task loop, which sits at 256 VGPRs -- inlined, any growth of the loop spilled, and a
 // spill reload inside the update mainloop broke its counted vmcnt pipelining)
+// pub (optional): publish *pub = pub_v when the block is stored, inside the call -- the
+// callee-saved registers are restored after it (scratch loads), not before the chain goes on
+__device__ __forceinline__ void publish(int* flag, int v, bool release);
 template <typename T>
 __device__ __noinline__ void diag_factor(T* __restrict__ A, int64_t ld, T* __restrict__ Linv, int* __restrict__ info,
-                                            int64_t col0, unsigned char* smem_raw, const int t, int* dbg = nullptr,
-                                            long long* prof = nullptr, bool from_lds = false) {
+                                         int64_t col0, unsigned char* smem_raw, const int t, int* dbg = nullptr,
+                                         long long* prof = nullptr, bool from_lds = false, int* pub = nullptr,
+                                         int pub_v = 0) {
     // f64: the blocked factor with look-ahead (diag_factor_la: 43 us per block in isolation
-    // against 50.6 for the rank-8 image, scripts/diag_bench.py)
-    if constexpr (std::is_same<T, double>::value && DIAG_LA) {
-        diag_factor_la<T>(A, ld, Linv, info, col0, smem_raw, t, prof, from_lds);
-        return;
-    }
-    // f32 (and GPRX_DIAG_RANK8): the rank-8 register image
-    diag_factor_rank8<T>(A, ld, Linv, info, col0, smem_raw, t, dbg, prof);
+    // against 50.6 for the rank-8 image, scripts/diag_bench.py); its stores are write-through
+    // (sc1), so the publication needs no release fence.  f32 (and GPRX_DIAG_RANK8): the
+    // rank-8 register image, plain stores and the release fence.
+    constexpr bool la = std::is_same<T, double>::value && DIAG_LA;
+    if constexpr (la) diag_factor_la<T>(A, ld, Linv, info, col0, smem_raw, t, prof, from_lds);
+    else diag_factor_rank8<T>(A, ld, Linv, info, col0, smem_raw, t, dbg, prof);
+    if (pub) publish(pub, pub_v, !la);
 }
 
 // Developer microbenchmark (gprx_dev_bench what 11 / 12): one workgroup factors `reps` fresh
@@ -2015,8 +2019,7 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
                     local_sync();
                 }
                 diag_factor<T>(Akk, DB, a.Linv + (int64_t)k * DB * DB, a.info, (int64_t)k * DB, smem_raw, tid, a.dbg,
-                               nullptr, fused_ts && k > 0);
-                publish(a.lcnt + k, k + 1, !(std::is_same<T, double>::value && DIAG_LA));
+                               nullptr, fused_ts && k > 0, a.lcnt + k, k + 1);  // (publishes Linv_k locally)
                 // pushes after the local publication (this rank's chain goes on meanwhile): the
                 // next diagonal step's rank first, L_{k,k-1} before Linv_k
                 const unsigned cm = k > 0 ? dist_consumers(D, k) : 0u;
@@ -2102,11 +2105,8 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
             if (a.trace) dt[2] = wall_clock64();
             diag_factor<T>(Akk, ld, a.Linv + (int64_t)k * DB * DB, a.info, (int64_t)k * DB, smem_raw, tid, a.dbg,
                            a.trace ? a.trace + 4 * (int64_t)(a.ntasks + a.nc) + 4 * (int64_t)k : nullptr,
-                           fused_ts && k > 0);
+                           fused_ts && k > 0, a.lcnt + k, k + 1);  // (publishes Linv_k: lcnt[k] = k + 1)
             if (a.trace) dt[3] = wall_clock64();
-            // the look-ahead factor (f64) stores write-through (sc1) like the tile tasks; the
-            // rank-8 image (f32) stores plain and needs the release fence
-            publish(a.lcnt + k, k + 1, !(std::is_same<T, double>::value && DIAG_LA));
             if (a.trace && wv == 0) {
                 long long* dp = a.trace + 4 * (int64_t)a.ntasks + 4 * (int64_t)k;
                 for (int u = 0; u < 4; u++) dp[u] = dt[u];
@@ -2140,8 +2140,9 @@ struct Cost {  // per-task durations (us, one CU), calibrated from GPRX_PT_TRACE
     double build = 28.0;   // BUILD tile (pair statistics + kernel values + stores)
     // the split diagonal step (f64): TPART(k, c) takes tpart + tpart_c (c + 1); DIAGX(k) then
     // sums the products and factors (diagx_s), publishing L_{k,k-1} early_s into it
-    double tpart = 9.0, tpart_c = 0.0;
-    double diagx_s = 44.0, early_s = 2.0;
+    // (r03o trace, N = 4096: parts done 9.8 us after Linv_{k-1}, S summed 6 us later, step 56.4 us)
+    double tpart = 9.5, tpart_c = 0.0;
+    double diagx_s = 47.0, early_s = 6.0;
 };
 
 // TPART tickets of one k in the order TPART(k, 3), (k, 2), (k, 1), (k, 0): each part waits for
