@@ -2221,8 +2221,10 @@ static void tile_chunks(int i, int j, int W, int near, std::vector<std::pair<int
 
 // ni > 0: the last ni row blocks are the identity (the inverse L^{-1} riding along as
 // L^{-T} rows): identity block a = i - (nr - ni) has zero L blocks before column block a.
+// tail > 0: the capped rule (ratio) only for the tiles of the last `tail` column blocks, the
+// fixed rule before them
 static Schedule make_schedule(int nc, int nr, int W, int near, int P, const Cost& cm0, bool build, int ni = 0,
-                              int ratio = 0, bool split = false) {
+                              int ratio = 0, bool split = false, int tail = 0) {
     Cost cm = cm0;
     if (split) cm.early = cm.early_s;
     const int nr0 = nr - ni;
@@ -2265,7 +2267,7 @@ static Schedule make_schedule(int nc, int nr, int W, int near, int P, const Cost
         std::vector<std::pair<int, int>> ch;
         for (int j = 1; j < nc; j++)
             for (int i = j; i < nr; i++) {
-                tile_chunks(i, j, W, near, ch, start_of(i), ratio);
+                tile_chunks(i, j, W, near, ch, start_of(i), (tail <= 0 || j >= nc - tail) ? ratio : 0);
                 for (auto& c : ch) by_last[c.first + c.second - 1].push_back(Chunk{i, j, c.first, c.second});
             }
     }
@@ -2688,6 +2690,7 @@ struct Params {
     int W = 64, near = -1;  // near < 0: by size (near_for)
     int ratio = -1;         // chunk-width rule of tile_chunks: < 0 picked per shape by the simulation
     int split = 1;          // f64: the split diagonal step (TPART tasks); GPRX_PT_SPLIT=0 turns it off
+    int tail = 0;           // > 0: the capped chunk rule only in the last `tail` column blocks
     Cost cm;
     int near_for(int nc) const { return near >= 0 ? near : (nc <= 64 ? 1 : 0); }
     Params() {
@@ -2700,6 +2703,7 @@ struct Params {
         if (const char* e = std::getenv("GPRX_PT_OVH_US")) cm.ovh = std::atof(e);
         if (const char* e = std::getenv("GPRX_PT_BUILD_US")) cm.build = std::atof(e);
         if (const char* e = std::getenv("GPRX_PT_SPLIT")) split = std::atoi(e);
+        if (const char* e = std::getenv("GPRX_PT_TAIL")) tail = std::atoi(e);
         if (const char* e = std::getenv("GPRX_PT_TPART_US")) cm.tpart = std::atof(e);
         if (const char* e = std::getenv("GPRX_PT_DIAGXS_US")) cm.diagx_s = std::atof(e);
     }
@@ -2709,20 +2713,26 @@ static const Params& params() {
     return p;
 }
 
-// the chunk rule with the shortest simulated makespan (ratio 0: the fixed rule; 8, 4, 2: width
-// capped by the distance to the tile's last panel), unless GPRX_PT_RATIO fixes it
+// the chunk rule with the shortest simulated makespan: the fixed rule (ratio 0), or a capped
+// rule (ratio 8, 4, 2: width capped by the distance to the tile's last panel) on every tile or
+// only on the last 16 / 32 column blocks -- where the chain-bound tail waits for the diagonal
+// tiles' last wide chunks (N = 16384: ratio 2 on the last 16 blocks 25.46 -> 25.15 ms, the
+// simulation ranks it first too) -- unless GPRX_PT_RATIO fixes it (GPRX_PT_TAIL its reach)
 static const int kRatios[] = {0, 8, 4, 2};
+static const int kTails[] = {0, 16, 32};
 static Schedule best_schedule(int nc, int nr, const Params& pr, int P, bool build, int ni, bool split) {
-    if (pr.ratio >= 0) return make_schedule(nc, nr, pr.W, pr.near_for(nc), P, pr.cm, build, ni, pr.ratio, split);
+    if (pr.ratio >= 0) return make_schedule(nc, nr, pr.W, pr.near_for(nc), P, pr.cm, build, ni, pr.ratio, split, pr.tail);
     Schedule best;
     bool have = false;
-    for (int r : kRatios) {
-        Schedule S = make_schedule(nc, nr, pr.W, pr.near_for(nc), P, pr.cm, build, ni, r, split);
-        if (!have || S.est_us < best.est_us * 0.995) {  // a wider rule must win by > 0.5%
-            best = std::move(S);
-            have = true;
+    for (int r : kRatios)
+        for (int tl : kTails) {
+            if ((r == 0 && tl) || (tl && tl >= nc)) continue;
+            Schedule S = make_schedule(nc, nr, pr.W, pr.near_for(nc), P, pr.cm, build, ni, r, split, tl);
+            if (!have || S.est_us < best.est_us * 0.995) {  // a rule with more tasks must win by > 0.5%
+                best = std::move(S);
+                have = true;
+            }
         }
-    }
     return best;
 }
 
@@ -3000,7 +3010,7 @@ int64_t potrf_tiles_schedule_stats(int nc, int nr, int P, bool build, double* es
         throw Error{GPRX_ERR_ARG, "potrf tile schedule: need nc >= 1, nr >= nc + ni, P >= 1"};
     const pt::Params& pr = pt::params();
     const bool split = pt::split_for(true);  // the f64 schedule
-    pt::Schedule S = ratio >= 0 ? pt::make_schedule(nc, nr, pr.W, pr.near_for(nc), P, pr.cm, build, ni, ratio, split)
+    pt::Schedule S = ratio >= 0 ? pt::make_schedule(nc, nr, pr.W, pr.near_for(nc), P, pr.cm, build, ni, ratio, split, pr.tail)
                                 : pt::best_schedule(nc, nr, pr, P, build, ni, split);
     if (est_us) *est_us = S.est_us;
     return S.ntasks;

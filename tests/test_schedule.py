@@ -117,12 +117,16 @@ def test_schedule_ratio_rule_valid_and_counted(nc, ratio):
 def test_schedule_picks_the_shortest_rule():
     """The rule potrf_tiles uses is the candidate with the shortest simulated makespan: the
     capped rule at N = 4096 (chain-bound: DIAGX(18) waited 184 us for a 16-panel piece under the
-    fixed rule), the fixed rule at N = 16384 (throughput-bound: fewer tasks)."""
-    for nc, want in [(32, 2), (128, 0)]:
+    fixed rule); at N = 16384 the capped rule on the last column blocks only (the chain-bound
+    tail), the fixed rule elsewhere (throughput-bound: fewer tasks)."""
+    for nc, want in [(32, 2), (128, None)]:
         ests = {r: _sched(nc, nc + 1, build=True, ratio=r)[2] for r in (0, 8, 4, 2)}
         _, n_auto, est_auto = _sched(nc, nc + 1, build=True, ratio=None)
-        assert est_auto == min(ests.values())
-        assert est_auto == ests[want]
+        assert est_auto <= min(ests.values())
+        if want is not None:
+            assert est_auto == ests[want]
+        else:  # N = 16384: a capped rule on the last column blocks only (kTails) beats every plain rule
+            assert est_auto < 0.995 * min(ests.values())
     assert _sched(32, 33, ratio=2)[2] < 0.92 * _sched(32, 33, ratio=0)[2]
 
 
