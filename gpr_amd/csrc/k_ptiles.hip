@@ -1204,11 +1204,11 @@ struct Args {
                              // read per task: as kernel arguments they stayed live in SGPRs and
                              // pushed the whole kernel into spills)
     const PtDist<T>* dist;   // distributed factorisation (potrf_tiles_kernel<T, true> only)
-    // split diagonal step (f64): TPART(k, c) tasks form the column blocks of L_{k,k-1} and
-    // their rank-32 products; DIAGX(k) only sums them (diagx_split)
+    // split diagonal step (f64): TPART(k, p) tasks form L_{k,k-1} and S = A_kk - L L^T in
+    // quarters; DIAGX(k) copies S and factors it (diagx_split)
     int split;
-    T* pbuf;     // [4][DB x DB] the TPART products P_c = T_c T_c^T (lower tiles)
-    int* tflag;  // [nc][4] TPART(k, c) state: 1 its A operand is read, 2 T_c and P_c stored
+    T* pbuf;     // DB x DB: S, its lower tiles written by the four parts
+    int* tflag;  // [nc][4] TPART(k, p) state: 1 its A operand is read, 2 its T stored, 3 its S quarter stored
 };
 
 
@@ -1656,12 +1656,16 @@ struct TpCtx {
     long long tlimit;
     long long* xt;  // GPRX_PT_TRACE (one GPU): phase stamps, TPART(k, c) at 4 (4 k + c), DIAGX(k) at 4 (4 nc + k)
     int nc;
+    const int* ver;  // tile versions (A_kk final: ver[k][k] = k - 1)
+    int nv;
 };
-// LDS of a TPART: T's 32 columns (the operand of P), then the part's 32 Linv rows
-constexpr int TP_TSS = DB + 16;      // T column stride
-constexpr int TP_LOFF = 32 * TP_TSS;
-constexpr int TP_LSB = 34;           // Linv rows: column stride (16-B aligned pairs)
-static_assert((TP_LOFF + DB * TP_LSB) * sizeof(double) <= gemm_lds<double>(), "TPART staging exceeds the LDS of the launch");
+// LDS of a TPART: phase 1 the part's 32 Linv rows (column stride TP_LSB, 16-B aligned pairs);
+// phase 2 all of T (the 128 columns of L_{k,k-1}, column stride TP_TQ), then the 9th tile's
+// eight k-slices in the same area
+constexpr int TP_LSB = 34;
+constexpr int TP_TQ = DB + 4;
+static_assert(DB * TP_LSB * sizeof(double) <= gemm_lds<double>(), "TPART staging exceeds the LDS of the launch");
+static_assert(DB * TP_TQ * sizeof(double) <= gemm_lds<double>(), "TPART staging exceeds the LDS of the launch");
 
 // wave 0: Linv_kk available to this rank (local publication, or the owner's push)
 template <typename T, bool DIST>
@@ -1690,6 +1694,21 @@ __device__ bool tpart_wait_linv(const TpCtx<T>& a, int kk, bool& remote) {
     }
 }
 
+// wave 0: *v == want (A_kk final)
+template <typename T>
+__device__ bool tpart_wait_ver(const TpCtx<T>& a, const int* v, int want) {
+    const long long t0 = wall_clock64();
+    for (;;) {
+        if (ld_uni(v) == want) return true;
+        if (ld_uni(a.ctl + C_ERR)) return false;
+        if (wall_clock64() - t0 > a.tlimit) {
+            st_agent(a.ctl + C_ERR, 1);
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
 // wave 0: lane l < n checks f[l] >= want (one vector load, one ballot per poll)
 template <typename T>
 __device__ bool tpart_wait_flags(const TpCtx<T>& a, const int* f, int n, int want) {
@@ -1707,26 +1726,35 @@ __device__ bool tpart_wait_flags(const TpCtx<T>& a, const int* f, int n, int wan
     }
 }
 
-// TPART(k, p): the 16-column groups p and 7 - p of L_{k,k-1} = A_{k,k-1} Linv_{k-1}^T (group g
-// needs K = 16 (g + 1): each part 36 MFMAs per wave, balanced) and their rank-32 product P_p.
-// Wave w forms rows 16 w .. 16 w + 15: its A fragments (every A element read by one lane of
-// one part) go straight to registers at task start, before Linv_{k-1} is even waited for;
-// the 32 Linv rows, shared by all waves, through LDS.  Out of line, one body for every p:
-// inlined into the task loop the parts' code made every other task type 2-3x slower (TRSM
-// 16 -> 44 us, even with no TPART in the list) -- the loop's registers (it sits at 256 VGPRs)
-// and its hot code in the instruction cache.
+// TPART(k, p), two phases.
+// 1. The 16-column groups p and 7 - p of T = L_{k,k-1} = A_{k,k-1} Linv_{k-1}^T (group g needs
+//    K = 16 (g + 1): 36 MFMAs per wave in every part).  Wave w forms rows 16 w .. 16 w + 15: its
+//    A fragments (every A element read by one lane of one part) go to registers at task start,
+//    before Linv_{k-1} is even waited for; the 32 Linv rows, shared by all waves, through LDS.
+//    Stored in place once every part has read its A (tflag 1); then tflag 2.
+// 2. Once all of T is stored and A_kk is final: the part's quarter of S = A_kk - T T^T, the 9
+//    lower 16 x 16 tiles of tile-rows p and 7 - p (p + 1 and 8 - p of them), from all of T in
+//    LDS.  Wave w forms tile w over K = 128 and the 16-deep k-slice w of the 9th tile (36
+//    MFMAs each, the slices summed in a fixed order); the tiles go to the shared S buffer;
+//    tflag 3.  DIAGX(k) then copies 72 KB, not four 72 KB products (the products' sum had
+//    cost it 6 us of loads per step).
+// Out of line, one body for every p: inlined into the task loop the parts' code made every
+// other task type 2-3x slower (TRSM 16 -> 44 us, even with no TPART in the list) -- the loop's
+// registers (it sits at 256 VGPRs) and its hot code in the instruction cache.
 template <typename T, bool DIST>
-__device__ __noinline__ bool tpart_run(const TpCtx<T> a, T* __restrict__ Akm, int64_t ld, const T* __restrict__ Lp,
-                                       T* __restrict__ pc, int* tf, int k, const int C, T* smem, int& s_ok, const int t) {
+__device__ __noinline__ bool tpart_run(const TpCtx<T>* ap, T* __restrict__ Akm, const T* __restrict__ Akk, int64_t ld,
+                                       const T* __restrict__ Lp, T* __restrict__ sb, int* tf, int k, const int C,
+                                       T* smem, int& s_ok, const int t) {
     typedef Mfma<T> Tr;
     typedef typename Tr::acc_t acc_t;
     typedef typename Tr::vec_t vec_t;
+    const TpCtx<T> a = *ap;
     const int lane = t & 63, w = t >> 6, lr = lane & 15, lk = lane >> 4;
-    const int g0 = C, g1 = 7 - C;              // the part's column groups
+    const int g0 = C, g1 = 7 - C;                      // the part's column groups (and tile-rows)
     const int nk0 = 4 * (g0 + 1), nk1 = 4 * (g1 + 1);  // k-steps of 4 of each group (nk1 > nk0)
-    T* Ls = smem + TP_LOFF;
-    // A fragments: row 16 w + lr, k = 4 kq + lk, kq < nk1 (<= 32)
-    T af[32];
+    T* Ls = smem;
+    // ---- phase 1 ---------------------------------------------------------------------------
+    T af[32];  // A fragments: row 16 w + lr, k = 4 kq + lk, kq < nk1 (<= 32)
     {
         const T* ar = Akm + 16 * w + lr + (int64_t)lk * ld;
 #pragma unroll
@@ -1776,75 +1804,90 @@ __device__ __noinline__ bool tpart_run(const TpCtx<T> a, T* __restrict__ Akm, in
         }
     }
     if (xs && w == 0) xs[1] = wall_clock64();  // T computed
-    // T's 32 columns -> LDS (operand of P): column x 16 + c of Ts = group g_x's column c
-#pragma unroll
-    for (int x = 0; x < 2; x++)
-#pragma unroll
-        for (int reg = 0; reg < 4; reg++) smem[(16 * w + lr) + (16 * x + Tr::orow(lk, reg)) * TP_TSS] = acc[x][reg];
     // the in-place stores overwrite A columns the other parts read: wait for their "A read"
     // (the four parts hold consecutive tickets and need only a CU each: P >= 4, potrf_tiles)
     if (w == 0) s_ok = tpart_wait_flags<T>(a, tf, 4, 1) ? 1 : 0;
     __syncthreads();
     if (!__builtin_amdgcn_readfirstlane(s_ok)) return false;
-    if (xs && w == 0) xs[2] = wall_clock64();
 #pragma unroll
     for (int x = 0; x < 2; x++)
 #pragma unroll
         for (int reg = 0; reg < 4; reg++)
             st_sc1(Akm + 16 * w + lr + (int64_t)(16 * (x ? g1 : g0) + Tr::orow(lk, reg)) * ld, acc[x][reg]);
-    // P = T_p T_p^T (rank 32): the lower 16 x 16 tiles, wave blocks as the diagonal tile's (MAP 2)
-    int sr, sc;
-    wave_block<2>(w, sr, sc);
-    acc_t pacc[2][4];
+    publish(tf + C, 2, false);  // this part's columns of L_{k,k-1} stored
+    if (xs && w == 0) xs[2] = wall_clock64();
+    // ---- phase 2 ---------------------------------------------------------------------------
+    if (w == 0) {
+        bool ok = tpart_wait_flags<T>(a, tf, 4, 2);                           // all of T
+        if (ok) ok = tpart_wait_ver<T>(a, a.ver + (int64_t)k * a.nv + k, k - 1);  // A_kk final
+        if (ok) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        s_ok = ok ? 1 : 0;
+    }
+    __syncthreads();
+    if (!__builtin_amdgcn_readfirstlane(s_ok)) return false;
+    // T (column j at smem + j TP_TQ) by LDS-DMA, one 128-row column per wave instruction
+    for (int q = w; q < DB; q += NT / 64)
+        __builtin_amdgcn_global_load_lds((const void*)(Akm + 2 * lane + (int64_t)q * ld),
+                                         (__attribute__((address_space(3))) void*)(smem + q * TP_TQ), 16, 0, 0);
+    // the quarter's tiles: tau <= p -> (p, tau), else (7 - p, tau - p - 1); wave w: tile w, and
+    // the k-slice w of tile 8
+    auto tile_of = [&](int tau, int& R, int& Cc) {
+        R = (tau <= g0) ? g0 : g1;
+        Cc = (tau <= g0) ? tau : tau - g0 - 1;
+    };
+    int R0, C0, R8, C8;
+    tile_of(w, R0, C0);
+    tile_of(8, R8, C8);
+    acc_t s0;  // A_kk's tile w, loaded while T lands
 #pragma unroll
-    for (int x = 0; x < 2; x++)
-#pragma unroll
-        for (int y = 0; y < 4; y++) pacc[x][y] = acc_t{0};
-#pragma unroll
-    for (int kq = 0; kq < 8; kq++) {
+    for (int reg = 0; reg < 4; reg++) s0[reg] = Akk[(16 * R0 + lr) + (int64_t)(16 * C0 + Tr::orow(lk, reg)) * ld];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+#pragma unroll 8
+    for (int kq = 0; kq < 32; kq++) {
         const int kc = 4 * kq + lk;
-        T fb[2], fa[4];
+        s0 = Tr::mma(-smem[(16 * C0 + lr) + kc * TP_TQ], smem[(16 * R0 + lr) + kc * TP_TQ], s0);
+    }
+    acc_t s8 = acc_t{0};
 #pragma unroll
-        for (int x = 0; x < 2; x++) fb[x] = smem[(sc * 32 + x * 16 + lr) + kc * TP_TSS];
-#pragma unroll
-        for (int y = 0; y < 4; y++) fa[y] = smem[(sr * 64 + y * 16 + lr) + kc * TP_TSS];
-#pragma unroll
-        for (int x = 0; x < 2; x++)
-#pragma unroll
-            for (int y = 0; y < 4; y++)
-                if (4 * sr + y >= 2 * sc + x) pacc[x][y] = Tr::mma(fb[x], fa[y], pacc[x][y]);
+    for (int kq = 4 * w; kq < 4 * w + 4; kq++) {
+        const int kc = 4 * kq + lk;
+        s8 = Tr::mma(-smem[(16 * C8 + lr) + kc * TP_TQ], smem[(16 * R8 + lr) + kc * TP_TQ], s8);
     }
 #pragma unroll
-    for (int x = 0; x < 2; x++)
+    for (int reg = 0; reg < 4; reg++)
+        st_sc1(sb + (16 * R0 + lr) + (int64_t)(16 * C0 + Tr::orow(lk, reg)) * DB, s0[reg]);
+    __syncthreads();  // every wave done reading T: its area takes the 9th tile's k-slices
 #pragma unroll
-        for (int reg = 0; reg < 4; reg++) {
-            const int jl = sc * 32 + x * 16 + Tr::orow(lk, reg);
+    for (int reg = 0; reg < 4; reg++) smem[w * 256 + lane * 4 + reg] = s8[reg];
+    __syncthreads();
+    if (t < 256) {  // the 9th tile: A_kk + the eight k-slices, in order
+        const int ln = t >> 2, reg = t & 3;
+        const int r = 16 * R8 + (ln & 15), c = 16 * C8 + Tr::orow(ln >> 4, reg);
+        T v = Akk[r + (int64_t)c * ld];
 #pragma unroll
-            for (int y = 0; y < 4; y++)
-                if (4 * sr + y >= 2 * sc + x) st_sc1(pc + (sr * 64 + y * 16 + lr) + (int64_t)jl * DB, pacc[x][y][reg]);
-        }
-    if (xs && w == 0) xs[3] = wall_clock64();  // P computed (its stores in flight)
-    publish(tf + C, 2, false);
+        for (int w8 = 0; w8 < 8; w8++) v += smem[w8 * 256 + t];
+        st_sc1(sb + r + (int64_t)c * DB, v);
+    }
+    if (xs && w == 0) xs[3] = wall_clock64();  // S quarter computed (its stores in flight)
+    publish(tf + C, 3, false);
     return true;
 }
 
 template <typename T, bool DIST>
-__device__ __forceinline__ bool tpart_task(const TpCtx<T>& a, T* Akm, int64_t ld, const T* Lp, int k, int c, T* smem,
-                                           int& s_ok, const int t) {
-    return tpart_run<T, DIST>(a, Akm, ld, Lp, a.pbuf + (int64_t)c * DB * DB, a.tflag + 4 * k, k, c, smem, s_ok, t);
+__device__ __forceinline__ bool tpart_task(const TpCtx<T>* ap, T* Akm, const T* Akk, int64_t ld, const T* Lp, int k, int c,
+                                           T* smem, int& s_ok, const int t) {
+    return tpart_run<T, DIST>(ap, Akm, Akk, ld, Lp, ap->pbuf, ap->tflag + 4 * k, k, c, smem, s_ok, t);
 }
 
-// DIAGX(k > 0) of the split step: S = A_kk - P_0 - P_1 - P_2 - P_3 into the factor's LDS image
-// (the 36 lower 16 x 16 tiles), then L_{k,k-1} is final (lcnt[k] = k).  A_kk loads at once
-// (the task waited only for it); the four parts finish within ~0.3 us of each other, so each
-// wave waits for all four flags and issues the 36 loads of its products together -- one
-// memory latency on the chain instead of four (summing each product as its flag came cost
-// ~1.9 us per product).  Each wave owns 576 element pairs, 9 per lane (lower tile
-// tau = q / 128, pair q % 8 of its column (q % 128) / 8): no barrier until the image is full.
+// DIAGX(k > 0) of the split step: S (the 36 lower 16 x 16 tiles, assembled in the shared S
+// buffer by the four parts) into the factor's LDS image, then L_{k,k-1} is final (lcnt[k] =
+// k).  Each wave waits for the four parts itself and copies 576 element pairs, 9 per lane
+// (lower tile tau = q / 128, pair q % 8 of its column (q % 128) / 8), one batch of loads.
 template <typename T>
-__device__ __noinline__ bool diagx_split(const TpCtx<T> a, const T* __restrict__ Akk, int64_t ld, int k, T* smem,
-                                         int& s_ok, const int t) {
+__device__ __noinline__ bool diagx_split(const TpCtx<T>* ap, int k, T* smem, int& s_ok, const int t) {
     typedef typename Mfma<T>::vec_t vec_t;
+    const TpCtx<T> a = *ap;
     const int lane = t & 63, w = t >> 6;
     const int* tf = a.tflag + 4 * k;
     long long* xs = a.xt ? a.xt + 4 * (4 * (int64_t)a.nc + k) : nullptr;
@@ -1858,39 +1901,50 @@ __device__ __noinline__ bool diagx_split(const TpCtx<T> a, const T* __restrict__
         rr[u] = 16 * R + 2 * (e & 7);
         cc[u] = 16 * C + (e >> 3);
     }
-    vec_t s[9];
-#pragma unroll
-    for (int u = 0; u < 9; u++) s[u] = *reinterpret_cast<const vec_t*>(Akk + rr[u] + (int64_t)cc[u] * ld);
-    const bool ok = tpart_wait_flags<T>(a, tf, 4, 2);  // this wave polls the four parts itself
+    const bool ok = tpart_wait_flags<T>(a, tf, 4, 3);  // this wave polls the four parts itself
     if (ok) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        if (xs && w == 0) xs[2] = wall_clock64();  // every P_c seen
-        vec_t p[4][9];
+        if (xs && w == 0) xs[2] = wall_clock64();  // every quarter seen
+        vec_t v[9];
 #pragma unroll
-        for (int c = 0; c < 4; c++)
-#pragma unroll
-            for (int u = 0; u < 9; u++)
-                p[c][u] = *reinterpret_cast<const vec_t*>(a.pbuf + (int64_t)c * DB * DB + rr[u] + cc[u] * DB);
+        for (int u = 0; u < 9; u++) v[u] = *reinterpret_cast<const vec_t*>(a.pbuf + rr[u] + cc[u] * DB);
 #pragma unroll
         for (int u = 0; u < 9; u++) {
-#pragma unroll
-            for (int c = 0; c < 4; c++) s[u] -= p[c][u];  // fixed order: P_0, P_1, P_2, P_3
-            smem[rr[u] + cc[u] * SIL] = s[u][0];
-            smem[rr[u] + 1 + cc[u] * SIL] = s[u][1];
+            smem[rr[u] + cc[u] * SIL] = v[u][0];
+            smem[rr[u] + 1 + cc[u] * SIL] = v[u][1];
         }
     }
     if (w == 0) s_ok = ok ? 1 : 0;
     __syncthreads();
     if (!__builtin_amdgcn_readfirstlane(s_ok)) return false;
-    // every column block of L_{k,k-1} is stored (each TPART's flag came after its stores)
+    // every column block of L_{k,k-1} is stored (each part's flag came after its stores)
     if (w == 0) st_agent(a.lcnt + k, k);
     if (xs && w == 0) xs[3] = wall_clock64();  // S in the image
     return true;
 }
 
+// BUILD task body, out of line (the distributed kernel): its two accumulator sets (pair
+// statistics of both classes) are the task loop's largest register demand
+template <typename T>
+__device__ __noinline__ bool build_task(const TileBuild<T>* bp, T* A, int64_t ld, int64_t i0, int64_t j0, T* smem,
+                                        const int t) {
+    const TileBuild<T>& b = *bp;
+    return pr::build_tile_sum<T, 1, true>(b.Kd, b.FU, b.FV, b.nf, b.Kr, b.Kp, b.hd, A, ld, b.n, b.sigma2, i0, j0, smem, t);
+}
+
 template <typename T>
 __device__ __forceinline__ TpCtx<T> tp_ctx(const Args<T>& a) {
-    return TpCtx<T>{a.ctl, a.lcnt, a.tflag, a.pbuf, a.dist, a.tlimit, a.xt, a.nc};
+    return TpCtx<T>{a.ctl, a.lcnt, a.tflag, a.pbuf, a.dist, a.tlimit, a.xt, a.nc, a.ver, a.nv};
+}
+// the split step's context lives in LDS after the ticket words (written once per launch):
+// the out-of-line calls take one pointer (by value, its ten fields cost the task loop spills)
+template <typename T>
+constexpr size_t pt_lds_ctx_off() {
+    return pt_lds_bytes<T>() + 16;
+}
+template <typename T>
+constexpr size_t pt_lds_total() {
+    return pt_lds_ctx_off<T>() + sizeof(TpCtx<T>);
 }
 
 template <typename T, bool DIST>
@@ -1900,6 +1954,8 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
     // pipeline with vmcnt(0)); the ticket word sits after the largest per-task image
     int& s_q = *reinterpret_cast<int*>(smem_raw + pt_lds_bytes<T>());
     int& s_ok = *reinterpret_cast<int*>(smem_raw + pt_lds_bytes<T>() + sizeof(int));
+    TpCtx<T>* tpc = reinterpret_cast<TpCtx<T>*>(smem_raw + pt_lds_ctx_off<T>());
+    if (threadIdx.x == 0) *tpc = tp_ctx(a);  // (visible after the task loop's first barrier)
     T* smem = reinterpret_cast<T*>(smem_raw);
     const int t = threadIdx.x;
     const int wv = wave_id();
@@ -1958,16 +2014,14 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
             bool ok = true;
             if (type == T_TPART) {
                 if constexpr (std::is_same<T, double>::value && DIAG_LA && SPLIT_CODE)
-                    ok = tpart_task<T, true>(tp_ctx(a), dist_tile(a.A, D, i, i - 1), DB,
+                    ok = tpart_task<T, true>(tpc, dist_tile(a.A, D, i, i - 1), dist_tile(a.A, D, i, i), DB,
                                              a.Linv + (int64_t)(i - 1) * DB * DB, i, j, smem, s_ok, tid);
             } else if (type == T_BUILD) {
-                const TileBuild<T>& b = *a.tb;
                 T* tij = dist_tile(a.A, D, i, j);
                 // build_tile_sum addresses element (gi, gj) at base + gi + gj ld (global indices)
-                const bool bad = pr::build_tile_sum<T, 1, true>(
-                    b.Kd, b.FU, b.FV, b.nf, b.Kr, b.Kp, b.hd, tij - (int64_t)i * GT - (int64_t)j * GT * DB, DB, b.n,
-                    b.sigma2, (int64_t)i * GT, (int64_t)j * GT, smem, tid);
-                if (__builtin_amdgcn_readfirstlane(__any(bad))) atomicOr(b.flag, 1);
+                const bool bad = build_task<T>(a.tb, tij - (int64_t)i * GT - (int64_t)j * GT * DB, DB, (int64_t)i * GT,
+                                               (int64_t)j * GT, smem, tid);
+                if (__builtin_amdgcn_readfirstlane(__any(bad))) atomicOr(a.tb->flag, 1);
                 publish(a.ver + (int64_t)i * a.nv + j, 0, false);
             } else if (type == T_UPD) {
                 // row j of this rank: its stored tiles; of another rank: the window, one tile per
@@ -2007,7 +2061,7 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
                 T* Akm = k > 0 ? dist_tile(a.A, D, k, k - 1) : nullptr;
                 constexpr bool fused_ts = std::is_same<T, double>::value && DIAG_LA;
                 if (SPLIT_CODE && fused_ts && k > 0 && a.split) {
-                    ok = diagx_split<T>(tp_ctx(a), Akk, DB, k, smem, s_ok, tid);
+                    ok = diagx_split<T>(tpc, k, smem, s_ok, tid);
                     if (!ok) break;
                 } else if (fused_ts && k > 0) {
                     diagx_ts<T>(Akm, Akk, DB, a.Linv + (int64_t)(k - 1) * DB * DB, a.lcnt + k, k, smem, tid, false);
@@ -2051,17 +2105,18 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
         // launch reports as info = -1, and the next wait_inputs drains the workgroup)
         if (type == T_TPART) {
             if constexpr (fused_ts && SPLIT_CODE)
-                (void)tpart_task<T, false>(tp_ctx(a), Ci + (int64_t)(i - 1) * GT * ld, ld,
+                (void)tpart_task<T, false>(tpc, Ci + (int64_t)(i - 1) * GT * ld, Ci + (int64_t)i * GT * ld, ld,
                                            a.Linv + (int64_t)(i - 1) * DB * DB, i, j, smem, s_ok, tid);
         } else if (type == T_BUILD) {
             // ver[i][j] goes from -1 (not built) to 0; the tile's values go out write-through
-            const TileBuild<T>& b = *a.tb;
-            bool bad;
             // one instantiation for every mode: an absent statistic has a zero-depth product
             // (its accumulators stay 0) and no leaves of its class
-            bad = pr::build_tile_sum<T, 1, true>(b.Kd, b.FU, b.FV, b.nf, b.Kr, b.Kp, b.hd, a.A, ld, b.n, b.sigma2,
-                                                 (int64_t)i * GT, (int64_t)j * GT, smem, tid);
-            if (__builtin_amdgcn_readfirstlane(__any(bad))) atomicOr(b.flag, 1);  // wave-uniform branch
+            // (inline here: out of line its register saves cost the C3 fit 0.35 ms; the
+            // distributed kernel, with more live state, calls build_task)
+            const TileBuild<T>& b = *a.tb;
+            const bool bad = pr::build_tile_sum<T, 1, true>(b.Kd, b.FU, b.FV, b.nf, b.Kr, b.Kp, b.hd, a.A, ld, b.n,
+                                                            b.sigma2, (int64_t)i * GT, (int64_t)j * GT, smem, tid);
+            if (__builtin_amdgcn_readfirstlane(__any(bad))) atomicOr(a.tb->flag, 1);  // wave-uniform branch
             publish(a.ver + (int64_t)i * a.nv + j, 0, false);
         } else if (type == T_UPD) {
             // variant 64 (timing experiment, wrong results): every update streams the same
@@ -2085,7 +2140,7 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
             T* Akk = Ci + (int64_t)k * GT * ld;
             long long dt[4] = {0, 0, 0, 0};
             if (SPLIT_CODE && fused_ts && k > 0 && a.split) {
-                (void)diagx_split<T>(tp_ctx(a), Akk, ld, k, smem, s_ok, tid);
+                (void)diagx_split<T>(tpc, k, smem, s_ok, tid);
                 if (a.trace) dt[0] = dt[1] = wall_clock64();
             } else if (fused_ts && k > 0) {
                 T* Akm = Ci + (int64_t)(k - 1) * GT * ld;
@@ -2140,9 +2195,10 @@ struct Cost {  // per-task durations (us, one CU), calibrated from GPRX_PT_TRACE
     double build = 28.0;   // BUILD tile (pair statistics + kernel values + stores)
     // the split diagonal step (f64): TPART(k, c) takes tpart + tpart_c (c + 1); DIAGX(k) then
     // sums the products and factors (diagx_s), publishing L_{k,k-1} early_s into it
-    // (r03o trace, N = 4096: parts done 9.8 us after Linv_{k-1}, S summed 6 us later, step 56.4 us)
-    double tpart = 9.5, tpart_c = 0.0;
-    double diagx_s = 47.0, early_s = 6.0;
+    // (r03w trace, N = 4096: the parts publish S ~12 us after Linv_{k-1}, DIAGX copies it in
+    // 2 us and factors; step 54.4 us)
+    double tpart = 11.5, tpart_c = 0.0;
+    double diagx_s = 44.0, early_s = 2.0;
 };
 
 // TPART tickets of one k in the order TPART(k, 3), (k, 2), (k, 1), (k, 0): each part waits for
@@ -2278,6 +2334,7 @@ static Schedule make_schedule(int nc, int nr, int W, int near, int P, const Cost
                 tp[c] = add(T_TPART, k, c, 0, 0, cm.tpart + cm.tpart_c * (c + 1));
                 dep(tp[c], diagx[k - 1]);
                 dep(tp[c], last_upd[(size_t)k * nc + (k - 1)]);
+                dep(tp[c], last_upd[(size_t)k * nc + k]);  // phase 2 starts from A_kk
             }
             const int id = add(T_DIAGX, k, k, 0, 0, cm.diagx_s);
             diagx[k] = id;
@@ -2515,6 +2572,7 @@ static DistSched make_schedule_dist(int nc, bool inv, int W, int near, int P, in
                 tp[c] = add(T_TPART, k, c, 0, 0, cm.tpart + cm.tpart_c * (c + 1), own(k));
                 dep(tp[c], linv(k - 1, own(k)));
                 dep(tp[c], last_upd[(size_t)k * nci + (k - 1)]);
+                dep(tp[c], last_upd[(size_t)k * nci + k]);  // phase 2 starts from A_kk
             }
         const int id = add(T_DIAGX, k, k, 0, 0, (k == 0) ? cm.diag0 : (split ? cm.diagx_s : cm.diagx), own(k));
         diagx[k] = id;
@@ -2928,14 +2986,14 @@ void potrf_tiles(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info
     // one wait may take at most 2 s + 20x the whole predicted factorisation
     a.tlimit = (long long)(1e8 * (2.0 + 20.0 * sd.est_us * 1e-6));
     // + the ticket word; at least 96 KB so the launch stays at one workgroup per CU
-    auto lds_of = [](size_t b) { return std::max<size_t>(b + 16, 96 * 1024); };
-    const size_t lds = lds_of(pt_lds_bytes<T>());
+    auto lds_of = [](size_t b) { return std::max<size_t>(b, 96 * 1024); };
+    const size_t lds = lds_of(pt_lds_total<T>());
     static bool attr = false;
     if (!attr) {
         GPRX_HIP(hipFuncSetAttribute((const void*)potrf_tiles_kernel<double, false>,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_of(pt_lds_bytes<double>())));
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_of(pt_lds_total<double>())));
         GPRX_HIP(hipFuncSetAttribute((const void*)potrf_tiles_kernel<float, false>,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_of(pt_lds_bytes<float>())));
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_of(pt_lds_total<float>())));
         attr = true;
     }
     const double nn = (double)np;
@@ -2987,14 +3045,14 @@ void potrf_tiles_dist_launch(const DistLaunch<T>& L) {
     a.split = L.split;
     a.pbuf = L.pbuf;
     a.tflag = L.tflag;
-    auto lds_of = [](size_t b) { return std::max<size_t>(b + 16, 96 * 1024); };
-    const size_t lds = lds_of(pt_lds_bytes<T>());
+    auto lds_of = [](size_t b) { return std::max<size_t>(b, 96 * 1024); };
+    const size_t lds = lds_of(pt_lds_total<T>());
     static bool attr = false;
     if (!attr) {
         GPRX_HIP(hipFuncSetAttribute((const void*)potrf_tiles_kernel<double, true>,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_of(pt_lds_bytes<double>())));
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_of(pt_lds_total<double>())));
         GPRX_HIP(hipFuncSetAttribute((const void*)potrf_tiles_kernel<float, true>,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_of(pt_lds_bytes<float>())));
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_of(pt_lds_total<float>())));
         attr = true;
     }
     hipLaunchKernelGGL((potrf_tiles_kernel<T, true>), dim3((unsigned)L.P), dim3(NT), lds, L.s, a);

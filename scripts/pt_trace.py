@@ -122,13 +122,13 @@ if (xtp[1:, :, 0] > 0).all():
     for c in range(4):
         s_ = xtp[1:, c, :]
         ph[f"c{c}"] = {"linv_seen": float(np.median(rel(s_[:, :1]))), "t_done": float(np.median(rel(s_[:, 1:2]))),
-                       "stored": float(np.median(rel(s_[:, 2:3]))), "p_done": float(np.median(rel(s_[:, 3:4])))}
+                       "t_stored": float(np.median(rel(s_[:, 2:3]))), "s_quarter_done": float(np.median(rel(s_[:, 3:4])))}
         tpi = np.where((typ == 4) & (tasks[:, 2] == c))[0]
         tpi = tpi[np.argsort(tasks[tpi, 1])]
         ph[f"c{c}"]["published"] = float(np.median((tk[tpi, 2] * 100.0 + t0 - t_lin) / 100.0))
     dgs = xdg[1:]
     ph["diagx"] = {"start": float(np.median((tk[d[1:], 1] * 100.0 + t0 - t_lin) / 100.0)),
-                   "parts_seen": float(np.median(rel(dgs[:, 2:3]))), "s_done": float(np.median(rel(dgs[:, 3:4]))),
+                   "quarters_seen": float(np.median(rel(dgs[:, 2:3]))), "s_done": float(np.median(rel(dgs[:, 3:4]))),
                    "end": float(np.median((tk[d[1:], 2] * 100.0 + t0 - t_lin) / 100.0))}
     res["split_step_us"] = ph
 res["diagx_last16"] = [[round(float(e - s_), 1), round(float(g), 1)] for s_, e, g in zip(st[-16:], en[-16:], np.r_[gaps, 0][-16:])]
