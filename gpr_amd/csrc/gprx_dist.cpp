@@ -457,10 +457,13 @@ static void setup(DistEngine<T>& E, const DistContext& C, int64_t n, int m, bool
     }
     // the update-chunk rule (k_ptiles.hip tile_chunks): the capped rules, tried for the chosen
     // grouping and window, replace the fixed one when they simulate > 0.5% shorter
-    for (int ratio : {4, 2}) {
-        DistSched c = potrf_dist_schedule(nc, E.g, gb, ww, E.P, fused, inv, ratio, f64);
-        if (c.est_us < 0.995 * E.S.est_us) E.S = std::move(c);
-    }
+    // (on every tile, or on the last 16 column blocks only: the chain-bound tail)
+    for (int ratio : {4, 2})
+        for (int tail : {0, 16}) {
+            if (tail >= nc) continue;
+            DistSched c = potrf_dist_schedule(nc, E.g, gb, ww, E.P, fused, inv, ratio, f64, tail);
+            if (c.est_us < 0.995 * E.S.est_us) E.S = std::move(c);
+        }
     E.gb = gb;
     E.ww = ww;
     E.W = E.S.W;

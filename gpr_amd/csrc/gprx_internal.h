@@ -487,7 +487,8 @@ struct DistSched {
     double est_us = 0;
     int W = 0;              // update chunk width used
 };
-DistSched potrf_dist_schedule(int nc, int g, int gb, int ww, int P, bool build, bool inv, int ratio = 0, bool f64 = true);
+DistSched potrf_dist_schedule(int nc, int g, int gb, int ww, int P, bool build, bool inv, int ratio = 0, bool f64 = true,
+                              int tail = 0);
 bool potrf_split_for(bool f64, int P);  // the split diagonal step is on (this precision, P workgroups)
 template <typename T>
 void potrf_tiles_dist_launch(const DistLaunch<T>& L);

@@ -1923,15 +1923,6 @@ __device__ __noinline__ bool diagx_split(const TpCtx<T>* ap, int k, T* smem, int
     return true;
 }
 
-// BUILD task body, out of line (the distributed kernel): its two accumulator sets (pair
-// statistics of both classes) are the task loop's largest register demand
-template <typename T>
-__device__ __noinline__ bool build_task(const TileBuild<T>* bp, T* A, int64_t ld, int64_t i0, int64_t j0, T* smem,
-                                        const int t) {
-    const TileBuild<T>& b = *bp;
-    return pr::build_tile_sum<T, 1, true>(b.Kd, b.FU, b.FV, b.nf, b.Kr, b.Kp, b.hd, A, ld, b.n, b.sigma2, i0, j0, smem, t);
-}
-
 template <typename T>
 __device__ __forceinline__ TpCtx<T> tp_ctx(const Args<T>& a) {
     return TpCtx<T>{a.ctl, a.lcnt, a.tflag, a.pbuf, a.dist, a.tlimit, a.xt, a.nc, a.ver, a.nv};
@@ -2019,8 +2010,10 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
             } else if (type == T_BUILD) {
                 T* tij = dist_tile(a.A, D, i, j);
                 // build_tile_sum addresses element (gi, gj) at base + gi + gj ld (global indices)
-                const bool bad = build_task<T>(a.tb, tij - (int64_t)i * GT - (int64_t)j * GT * DB, DB, (int64_t)i * GT,
-                                               (int64_t)j * GT, smem, tid);
+                const TileBuild<T>& b = *a.tb;
+                const bool bad = pr::build_tile_sum<T, 1, true>(
+                    b.Kd, b.FU, b.FV, b.nf, b.Kr, b.Kp, b.hd, tij - (int64_t)i * GT - (int64_t)j * GT * DB, DB, b.n,
+                    b.sigma2, (int64_t)i * GT, (int64_t)j * GT, smem, tid);
                 if (__builtin_amdgcn_readfirstlane(__any(bad))) atomicOr(a.tb->flag, 1);
                 publish(a.ver + (int64_t)i * a.nv + j, 0, false);
             } else if (type == T_UPD) {
@@ -2111,8 +2104,8 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
             // ver[i][j] goes from -1 (not built) to 0; the tile's values go out write-through
             // one instantiation for every mode: an absent statistic has a zero-depth product
             // (its accumulators stay 0) and no leaves of its class
-            // (inline here: out of line its register saves cost the C3 fit 0.35 ms; the
-            // distributed kernel, with more live state, calls build_task)
+            // (inline: out of line, its register saves cost the C3 fit 0.35 ms and the sharded
+            // fit 1%, more than the task loop's few spills at task level, none in a mainloop)
             const TileBuild<T>& b = *a.tb;
             const bool bad = pr::build_tile_sum<T, 1, true>(b.Kd, b.FU, b.FV, b.nf, b.Kr, b.Kp, b.hd, a.A, ld, b.n,
                                                             b.sigma2, (int64_t)i * GT, (int64_t)j * GT, smem, tid);
@@ -2483,7 +2476,8 @@ static void c_chunks(int a, int W, int nc, std::vector<std::pair<int, int>>& out
 }
 
 static DistSched make_schedule_dist(int nc, bool inv, int W, int near, int P, int g, int gb, int ww, const Cost& cm0,
-                                    bool build, double push_us, double rel_us, int ratio = 0, bool split = false) {
+                                    bool build, double push_us, double rel_us, int ratio = 0, bool split = false,
+                                    int tail = 0) {
     Cost cm = cm0;
     if (split) cm.early = cm.early_s;
     const int nr = nc + 1 + (inv ? nc : 0), nci = inv ? 2 * nc : nc;
@@ -2529,7 +2523,7 @@ static DistSched make_schedule_dist(int nc, bool inv, int W, int near, int P, in
         for (int j = 1; j < nc; j++)
             for (int i = j; i < nr; i++) {
                 if (i > nc && start_of(i) >= j) continue;  // identity row E_a: tiles (E_a, j > a) only
-                tile_chunks(i, j, W, near, ch, start_of(i), ratio);
+                tile_chunks(i, j, W, near, ch, start_of(i), (tail <= 0 || j >= nc - tail) ? ratio : 0);
                 for (auto& c : ch) by_last[c.first + c.second - 1].push_back(Chunk{i, j, c.first, c.second});
             }
         if (inv)
@@ -3005,7 +2999,7 @@ void potrf_tiles(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info
 }
 
 // ---- distributed factorisation: per-rank ticket lists and one rank's launch ------------------
-DistSched potrf_dist_schedule(int nc, int g, int gb, int ww, int P, bool build, bool inv, int ratio, bool f64) {
+DistSched potrf_dist_schedule(int nc, int g, int gb, int ww, int P, bool build, bool inv, int ratio, bool f64, int tail) {
     const pt::Params& pr = pt::params();
     // a push: one tile's stores over xGMI plus the flag (measured on one GPU as a same-device
     // copy; GPRX_DIST_PUSH_US / GPRX_DIST_REL_US override)
@@ -3017,7 +3011,7 @@ DistSched potrf_dist_schedule(int nc, int g, int gb, int ww, int P, bool build, 
     int W = 1;
     while (2 * W <= std::min(pr.W, std::max(1, ww / 2))) W *= 2;
     return pt::make_schedule_dist(nc, inv, W, pr.near_for(nc), P, g, std::max(1, gb), ww, pr.cm, build, push_us, rel_us,
-                                  pr.ratio >= 0 ? pr.ratio : ratio, pt::split_for(f64, P));
+                                  pr.ratio >= 0 ? pr.ratio : ratio, pt::split_for(f64, P), pr.ratio >= 0 ? pr.tail : tail);
 }
 
 template <typename T>
