@@ -271,6 +271,9 @@ def main():
                     help="N>1 headline: one fit whose matrix is sharded over the GPUs (dist, strong "
                          "scaling) or independent fits per GPU (replicas, weak scaling); both are measured")
     ap.add_argument("--configs", type=int, default=1, help="also measure BASELINE configs C2, C4, C5 (0 = skip)")
+    ap.add_argument("--dist-lml", type=int, default=0,
+                    help="N > 1: also time the LML + gradient on the sharded factor (off by default: at N = 16384 "
+                         "two processes sharing one GPU hang in it, DESIGN.md 6)")
     ap.add_argument("--force-dist", action="store_true",
                     help="testing: run the sharded-fit leg (and make it the headline) even at N = 1")
     args = ap.parse_args()
@@ -354,7 +357,7 @@ def main():
             dmodel = make_model(dctx)
             el, infos, st = timed_fits(dmodel, dctx, gpr_amd.gprx.FIT_DISTRIBUTED)
             dres = {"elapsed": el, "infos": infos}
-            if args.lml:  # LML + gradient on the sharded factor (row-block partials, one all-reduce)
+            if args.dist_lml:  # LML + gradient on the sharded factor (row-block partials, one all-reduce)
                 dmodel.lml(grad=True, distributed=True)
                 barrier_sync()
                 tl0 = time.perf_counter()
