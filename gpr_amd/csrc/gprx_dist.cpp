@@ -439,9 +439,14 @@ static void setup(DistEngine<T>& E, const DistContext& C, int64_t n, int m, bool
         if (const char* e = std::getenv("GPRX_DIST_WINDOW_MB")) budget = std::atof(e) * 1048576.0;
         const int nrw = nc + 1 + (inv ? nc : 0);
         auto wbytes = [&](int w) { return (double)w * nrw * DB * DB * (double)sizeof(T); };
+        // Separate processes in LML mode (identity rows and C tiles riding along): windows
+        // above 16 panels hung at N = 16384 on two processes sharing one GPU (N <= 12288, or a
+        // 16-panel window, or virtual ranks with any window were fine; root cause not found,
+        // DESIGN.md 6), so that case keeps to 16
+        const int wcap = (inv && !E.virt) ? 16 : nc;
         std::vector<int> cws;
-        for (int w = 8; w < nc; w *= 2) cws.push_back(w);
-        cws.push_back(std::max(2, nc));
+        for (int w = 8; w < std::min(nc, wcap); w *= 2) cws.push_back(w);
+        cws.push_back(std::max(2, std::min(nc, wcap)));
         int pick = -1;
         DistSched ps;
         for (int w : cws) {
