@@ -568,3 +568,44 @@ def test_peer_two_processes(tmp_path):
     vr, gr, _, ldr = O.lml(C3K, X, Y[:, :1].copy(), 0.5)
     assert abs(res["lml"]["logdet"] - ldr) <= 1e-9 * abs(ldr)
     assert relerr(np.array(res["lml"]["grad"]), gr) <= 1e-6
+
+
+def test_peer_two_processes_lml_c3():
+    """The sharded LML at C3's size across two PROCESSES (peer context, one GPU shared): windows
+    above 16 panels hung here (known issue), so separate processes keep the LML
+    window at 16.  Both ranks must finish and agree with the single-GPU likelihood."""
+    import os
+    import socket
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = str(so.getsockname()[1])
+    probe = os.path.join(root, "scripts", "peer_lml_probe.py")
+    procs = [subprocess.Popen([sys.executable, "-u", probe, str(r), "2", port, "16384"], stdout=subprocess.PIPE,
+                              stderr=subprocess.STDOUT, text=True) for r in range(2)]
+    logs = []
+    for p in procs:
+        try:
+            logs.append(p.communicate(timeout=120)[0])
+        except subprocess.TimeoutExpired:
+            p.kill()
+            logs.append(p.communicate()[0])
+    assert all(p.returncode == 0 for p in procs), "\n".join(logs)
+    vals = [float(l.split("lml done")[1].split()[0]) for log in logs for l in log.splitlines() if "lml done" in l]
+    assert len(vals) == 2 and vals[0] == vals[1]
+    import gpr_amd
+    from gpr_amd.synth import C3, make_data
+    ctx = gpr_amd.Context(0)
+    try:
+        X, Y = make_data(16384, C3["d"], C3["m"])
+        M = gpr_amd.Model(ctx, np.float64)
+        M.set_data(X, Y)
+        M.set_kernel(C3["kernel"])
+        M.set_noise(C3["sigma"])
+        v, _, _ = M.lml(grad=True)
+        M.close()
+    finally:
+        ctx.close()
+    assert abs(vals[0] - v) <= 1e-9 * abs(v)
