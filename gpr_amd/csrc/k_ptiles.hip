@@ -1659,13 +1659,21 @@ struct TpCtx {
     const int* ver;  // tile versions (A_kk final: ver[k][k] = k - 1)
     int nv;
 };
-// LDS of a TPART: phase 1 the part's 32 Linv rows (column stride TP_LSB, 16-B aligned pairs);
-// phase 2 all of T (the 128 columns of L_{k,k-1}, column stride TP_TQ), then the 9th tile's
-// eight k-slices in the same area
-constexpr int TP_LSB = 34;
-constexpr int TP_TQ = DB + 4;
-static_assert(DB * TP_LSB * sizeof(double) <= gemm_lds<double>(), "TPART staging exceeds the LDS of the launch");
-static_assert(DB * TP_TQ * sizeof(double) <= gemm_lds<double>(), "TPART staging exceeds the LDS of the launch");
+// LDS of a TPART: phase 1 the part's 32 Linv rows (column stride LSB: 16-B aligned vectors);
+// phase 2 all of T (the 128 columns of L_{k,k-1}, CPI columns per LDS-DMA instruction, groups
+// TQ apart), then the 9th tile's eight k-slices in the same area
+template <typename T>
+struct TpL {
+    static constexpr int E = 16 / (int)sizeof(T);                    // elements per 16-B vector
+    static constexpr int LSB = sizeof(T) == 8 ? 34 : 36;
+    static constexpr int CPI = 64 * 16 / (DB * (int)sizeof(T));      // 1 (f64), 2 (f32)
+    static constexpr int TQ = CPI * DB + (sizeof(T) == 8 ? 4 : 8);
+    __device__ static int tcol(int c) { return (c / CPI) * TQ + (c % CPI) * DB; }
+};
+static_assert(DB * TpL<double>::LSB * sizeof(double) <= gemm_lds<double>(), "TPART staging exceeds the LDS of the launch");
+static_assert(DB / TpL<double>::CPI * TpL<double>::TQ * sizeof(double) <= gemm_lds<double>(), "TPART staging exceeds the LDS");
+static_assert(DB * TpL<float>::LSB * sizeof(float) <= gemm_lds<float>(), "TPART staging exceeds the LDS of the launch");
+static_assert(DB / TpL<float>::CPI * TpL<float>::TQ * sizeof(float) <= gemm_lds<float>(), "TPART staging exceeds the LDS");
 
 // wave 0: Linv_kk available to this rank (local publication, or the owner's push)
 template <typename T, bool DIST>
@@ -1743,8 +1751,9 @@ __device__ bool tpart_wait_flags(const TpCtx<T>& a, const int* f, int n, int wan
 // registers (it sits at 256 VGPRs) and its hot code in the instruction cache.
 template <typename T, bool DIST>
 __device__ __noinline__ bool tpart_run(const TpCtx<T>* ap, T* __restrict__ Akm, const T* __restrict__ Akk, int64_t ld,
-                                       const T* __restrict__ Lp, T* __restrict__ sb, int* tf, int k, const int C,
-                                       T* smem, int& s_ok, const int t) {
+                                       const T* __restrict__ Lp, T* __restrict__ sb, int64_t sld, int* tf, int k,
+                                       const int C, T* smem, int& s_ok, const int t) {
+    typedef TpL<T> Q;
     typedef Mfma<T> Tr;
     typedef typename Tr::acc_t acc_t;
     typedef typename Tr::vec_t vec_t;
@@ -1775,19 +1784,20 @@ __device__ __noinline__ bool tpart_run(const TpCtx<T>* ap, T* __restrict__ Akm, 
     long long* xs = a.xt ? a.xt + 4 * (4 * (int64_t)k + C) : nullptr;
     if (xs && w == 0) xs[0] = wall_clock64();  // Linv_{k-1} seen
     // Linv_{k-1} rows 16 g0 + r (r < 16) and 16 g1 + r - 16 (r >= 16), all 128 columns (zero
-    // above the diagonal), as Ls[r + col TP_LSB]: four 16-B loads per thread, all in flight
+    // above the diagonal), as Ls[r + col LSB]: 16-B loads (4 per thread f64, 2 f32), all in flight
     {
-        vec_t lv[4];
+        constexpr int VPC = 32 / Q::E, NV = 32 * DB / Q::E / NT;
+        vec_t lv[NV];
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int e = u * NT + t, r = 2 * (e & 15), col = e >> 4;
+        for (int u = 0; u < NV; u++) {
+            const int e = u * NT + t, r = Q::E * (e % VPC), col = e / VPC;
             const int row = (r < 16) ? 16 * g0 + r : 16 * g1 + r - 16;
             lv[u] = *reinterpret_cast<const vec_t*>(Lp + row + (int64_t)col * DB);
         }
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < NV; u++) {
             const int e = u * NT + t;
-            *reinterpret_cast<vec_t*>(Ls + 2 * (e & 15) + (e >> 4) * TP_LSB) = lv[u];
+            *reinterpret_cast<vec_t*>(Ls + Q::E * (e % VPC) + (e / VPC) * Q::LSB) = lv[u];
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1799,8 +1809,8 @@ __device__ __noinline__ bool tpart_run(const TpCtx<T>* ap, T* __restrict__ Akm, 
     for (int kq = 0; kq < 32; kq++) {
         if (kq < nk1) {
             const int kc = 4 * kq + lk;
-            acc[1] = Tr::mma(Ls[(16 + lr) + kc * TP_LSB], af[kq], acc[1]);
-            if (kq < nk0) acc[0] = Tr::mma(Ls[lr + kc * TP_LSB], af[kq], acc[0]);
+            acc[1] = Tr::mma(Ls[(16 + lr) + kc * Q::LSB], af[kq], acc[1]);
+            if (kq < nk0) acc[0] = Tr::mma(Ls[lr + kc * Q::LSB], af[kq], acc[0]);
         }
     }
     if (xs && w == 0) xs[1] = wall_clock64();  // T computed
@@ -1825,10 +1835,14 @@ __device__ __noinline__ bool tpart_run(const TpCtx<T>* ap, T* __restrict__ Akm, 
     }
     __syncthreads();
     if (!__builtin_amdgcn_readfirstlane(s_ok)) return false;
-    // T (column j at smem + j TP_TQ) by LDS-DMA, one 128-row column per wave instruction
-    for (int q = w; q < DB; q += NT / 64)
-        __builtin_amdgcn_global_load_lds((const void*)(Akm + 2 * lane + (int64_t)q * ld),
-                                         (__attribute__((address_space(3))) void*)(smem + q * TP_TQ), 16, 0, 0);
+    // T (column c at smem + tcol(c)) by LDS-DMA, CPI 128-row columns per wave instruction
+    {
+        constexpr int LPC = 64 / Q::CPI;  // lanes per column
+        for (int q = w; q < DB / Q::CPI; q += NT / 64)
+            __builtin_amdgcn_global_load_lds(
+                (const void*)(Akm + Q::E * (lane % LPC) + (int64_t)(Q::CPI * q + lane / LPC) * ld),
+                (__attribute__((address_space(3))) void*)(smem + q * Q::TQ), 16, 0, 0);
+    }
     // the quarter's tiles: tau <= p -> (p, tau), else (7 - p, tau - p - 1); wave w: tile w, and
     // the k-slice w of tile 8
     auto tile_of = [&](int tau, int& R, int& Cc) {
@@ -1846,17 +1860,17 @@ __device__ __noinline__ bool tpart_run(const TpCtx<T>* ap, T* __restrict__ Akm, 
 #pragma unroll 8
     for (int kq = 0; kq < 32; kq++) {
         const int kc = 4 * kq + lk;
-        s0 = Tr::mma(-smem[(16 * C0 + lr) + kc * TP_TQ], smem[(16 * R0 + lr) + kc * TP_TQ], s0);
+        s0 = Tr::mma(-smem[Q::tcol(kc) + 16 * C0 + lr], smem[Q::tcol(kc) + 16 * R0 + lr], s0);
     }
     acc_t s8 = acc_t{0};
 #pragma unroll
     for (int kq = 4 * w; kq < 4 * w + 4; kq++) {
         const int kc = 4 * kq + lk;
-        s8 = Tr::mma(-smem[(16 * C8 + lr) + kc * TP_TQ], smem[(16 * R8 + lr) + kc * TP_TQ], s8);
+        s8 = Tr::mma(-smem[Q::tcol(kc) + 16 * C8 + lr], smem[Q::tcol(kc) + 16 * R8 + lr], s8);
     }
 #pragma unroll
     for (int reg = 0; reg < 4; reg++)
-        st_sc1(sb + (16 * R0 + lr) + (int64_t)(16 * C0 + Tr::orow(lk, reg)) * DB, s0[reg]);
+        st_sc1(sb + (16 * R0 + lr) + (int64_t)(16 * C0 + Tr::orow(lk, reg)) * sld, s0[reg]);
     __syncthreads();  // every wave done reading T: its area takes the 9th tile's k-slices
 #pragma unroll
     for (int reg = 0; reg < 4; reg++) smem[w * 256 + lane * 4 + reg] = s8[reg];
@@ -1867,7 +1881,7 @@ __device__ __noinline__ bool tpart_run(const TpCtx<T>* ap, T* __restrict__ Akm, 
         T v = Akk[r + (int64_t)c * ld];
 #pragma unroll
         for (int w8 = 0; w8 < 8; w8++) v += smem[w8 * 256 + t];
-        st_sc1(sb + r + (int64_t)c * DB, v);
+        st_sc1(sb + r + (int64_t)c * sld, v);
     }
     if (xs && w == 0) xs[3] = wall_clock64();  // S quarter computed (its stores in flight)
     publish(tf + C, 3, false);
@@ -1875,9 +1889,30 @@ __device__ __noinline__ bool tpart_run(const TpCtx<T>* ap, T* __restrict__ Akm, 
 }
 
 template <typename T, bool DIST>
-__device__ __forceinline__ bool tpart_task(const TpCtx<T>* ap, T* Akm, const T* Akk, int64_t ld, const T* Lp, int k, int c,
+__device__ __forceinline__ bool tpart_task(const TpCtx<T>* ap, T* Akm, T* Akk, int64_t ld, const T* Lp, int k, int c,
                                            T* smem, int& s_ok, const int t) {
-    return tpart_run<T, DIST>(ap, Akm, Akk, ld, Lp, ap->pbuf, ap->tflag + 4 * k, k, c, smem, s_ok, t);
+    // S's quarters: f64 into the S buffer (DIAGX copies it into the look-ahead factor's LDS
+    // image); f32 in place into A_kk (the rank-8 factor reads its block from memory)
+    constexpr bool img = std::is_same<T, double>::value && DIAG_LA;
+    return tpart_run<T, DIST>(ap, Akm, Akk, ld, Lp, img ? ap->pbuf : Akk, img ? (int64_t)DB : ld, ap->tflag + 4 * k, k,
+                              c, smem, s_ok, t);
+}
+
+// DIAGX(k > 0) of the split step, f32 (the parts wrote S into A_kk): wait for the four
+// quarters, then L_{k,k-1} is final (lcnt[k] = k)
+template <typename T>
+__device__ __forceinline__ bool diagx_split_wait(const TpCtx<T>* ap, int k, int& s_ok) {
+    const int w = threadIdx.x >> 6;
+    if (w == 0) {
+        const bool ok = tpart_wait_flags<T>(*ap, ap->tflag + 4 * k, 4, 3);
+        if (ok) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            st_agent(ap->lcnt + k, k);
+        }
+        s_ok = ok ? 1 : 0;
+    }
+    __syncthreads();
+    return __builtin_amdgcn_readfirstlane(s_ok) != 0;
 }
 
 // DIAGX(k > 0) of the split step: S (the 36 lower 16 x 16 tiles, assembled in the shared S
@@ -2004,7 +2039,7 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
             const PtDist<T>& D = *a.dist;
             bool ok = true;
             if (type == T_TPART) {
-                if constexpr (std::is_same<T, double>::value && DIAG_LA && SPLIT_CODE)
+                if constexpr (SPLIT_CODE)
                     ok = tpart_task<T, true>(tpc, dist_tile(a.A, D, i, i - 1), dist_tile(a.A, D, i, i), DB,
                                              a.Linv + (int64_t)(i - 1) * DB * DB, i, j, smem, s_ok, tid);
             } else if (type == T_BUILD) {
@@ -2053,8 +2088,9 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
                 T* Akk = dist_tile(a.A, D, k, k);
                 T* Akm = k > 0 ? dist_tile(a.A, D, k, k - 1) : nullptr;
                 constexpr bool fused_ts = std::is_same<T, double>::value && DIAG_LA;
-                if (SPLIT_CODE && fused_ts && k > 0 && a.split) {
-                    ok = diagx_split<T>(tpc, k, smem, s_ok, tid);
+                if (SPLIT_CODE && k > 0 && a.split) {
+                    if constexpr (fused_ts) ok = diagx_split<T>(tpc, k, smem, s_ok, tid);
+                    else ok = diagx_split_wait<T>(tpc, k, s_ok);
                     if (!ok) break;
                 } else if (fused_ts && k > 0) {
                     diagx_ts<T>(Akm, Akk, DB, a.Linv + (int64_t)(k - 1) * DB * DB, a.lcnt + k, k, smem, tid, false);
@@ -2097,7 +2133,7 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
         // (a failed wait inside a task has raised C_ERR: the task ends on garbage, which the
         // launch reports as info = -1, and the next wait_inputs drains the workgroup)
         if (type == T_TPART) {
-            if constexpr (fused_ts && SPLIT_CODE)
+            if constexpr (SPLIT_CODE)
                 (void)tpart_task<T, false>(tpc, Ci + (int64_t)(i - 1) * GT * ld, Ci + (int64_t)i * GT * ld, ld,
                                            a.Linv + (int64_t)(i - 1) * DB * DB, i, j, smem, s_ok, tid);
         } else if (type == T_BUILD) {
@@ -2132,8 +2168,9 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
             const int k = i;
             T* Akk = Ci + (int64_t)k * GT * ld;
             long long dt[4] = {0, 0, 0, 0};
-            if (SPLIT_CODE && fused_ts && k > 0 && a.split) {
-                (void)diagx_split<T>(tpc, k, smem, s_ok, tid);
+            if (SPLIT_CODE && k > 0 && a.split) {
+                if constexpr (fused_ts) (void)diagx_split<T>(tpc, k, smem, s_ok, tid);
+                else (void)diagx_split_wait<T>(tpc, k, s_ok);
                 if (a.trace) dt[0] = dt[1] = wall_clock64();
             } else if (fused_ts && k > 0) {
                 T* Akm = Ci + (int64_t)(k - 1) * GT * ld;
@@ -2788,8 +2825,9 @@ static Schedule best_schedule(int nc, int nr, const Params& pr, int P, bool buil
     return best;
 }
 
-// the split diagonal step runs for f64 (the look-ahead factor's LDS image), unless disabled
-static bool split_for(bool f64) { return f64 && DIAG_LA && SPLIT_CODE && params().split != 0; }
+// the split diagonal step runs for both precisions (f64: S through the look-ahead factor's LDS
+// image; f32: S in place for the rank-8 factor), unless GPRX_PT_SPLIT=0
+static bool split_for(bool f64) { (void)f64; return SPLIT_CODE && params().split != 0; }
 // (the four parts of a step wait for each other: at least four workgroups)
 static bool split_for(bool f64, int P) { return P >= 4 && split_for(f64); }
 
