@@ -84,7 +84,13 @@ def traffic_from_profile(kernels=("potrf_tiles_kernel<double, false>", "potrf_ti
     tile kernel reads all of its operands (MI355X_MICROARCH.md §HBM) -- + WRITE_SIZE, averaged
     over launches; Infinity-Cache hits are included, so this bounds HBM bytes from above."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
+    import re
+
+    def order(path):  # tags r<round><a..z, aa..az ...>: by round, then by the tag's length and letters
+        m = re.match(r"r(\d+)([a-z]*)_", os.path.basename(path))
+        return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, "")
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")), key=order)
     for path in reversed(files):
         try:
             with open(path) as f:
