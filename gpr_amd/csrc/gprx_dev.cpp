@@ -245,6 +245,17 @@ extern "C" gprx_status gprx_dev_schedule(int32_t nc, int32_t nr, int32_t P, int3
     }
 }
 
+extern "C" int64_t gprx_dev_schedule_list(int32_t nc, int32_t nr, int32_t P, int32_t build, int32_t* out,
+                                          int64_t max) {
+    try {
+        return potrf_tiles_schedule_stats(nc, nr, P, (build & 1) != 0, nullptr, (build & 2) ? nc : 0,
+                                          ((build >> 8) & 0xff) - 1, out, max);
+    } catch (const Error& e) {
+        std::fprintf(stderr, "gprx_dev_schedule_list: %s\n", e.msg.c_str());
+        return -1;
+    }
+}
+
 namespace gprx {
 gprx_status gprx_dev_bench_impl(gprx_dtype dtype, int32_t what, int64_t M, int64_t N, int64_t K, int32_t iters,
                                 double* ms, Exec* ex) {

@@ -1633,19 +1633,24 @@ __device__ __forceinline__ long long diagx_ts(T* __restrict__ Akm, T* __restrict
 
 // ---- the split diagonal step (f64) ---------------------------------------------------------
 // DIAGX(k)'s two products before the factor (T = A_{k,k-1} Linv_{k-1}^T, A_kk - T T^T: 2432
-// MFMAs, 31 us on the one CU of the chain) spread over four more workgroups:
-//   TPART(k, p), p = 0..3: the 16-column groups p and 7 - p of T = L_{k,k-1} (tpart_run),
-//       stored in place, and P_p = T_p T_p^T over those 32 columns into pbuf[p];
-//   DIAGX(k):  S = A_kk - P_0 - P_1 - P_2 - P_3 (A_kk - T T^T = sum over the column groups),
-//       in this fixed order as the parts finish, straight into the factor's LDS image.
-// A part's in-place stores overwrite A columns the other parts read: each part raises "A
-// read" (tflag 1) once its operand is in registers and stores only after all four have.
-// Tickets: the parts are consecutive (TPART(k, 3), (k, 2), (k, 1), (k, 0), order_tparts) and
-// DIAGX(k) comes after them; a part waits only on its three siblings, whose tickets are
-// claimed as soon as any CU frees (nothing before them depends on the parts), so with P >= 4
-// workgroups every wait ends.
-// (the out-of-line functions take these by value: a reference to the kernel's Args put the
-// whole struct in scratch memory, and every a.x of every task became a scratch load)
+// MFMAs, 31 us on the one CU of the chain) spread over four more workgroups, in two phases
+// (tpart_run):
+//   1. TPART(k, p), p = 0..3: the 16-column groups p and 7 - p of T = L_{k,k-1}, stored in
+//      place.  A part's stores overwrite A columns the other parts read: each part raises
+//      "A read" (tflag 1) once its operand is in registers, stores only after all four have,
+//      then raises "T stored" (tflag 2);
+//   2. once all of T is stored and A_kk is final, part p forms the S = A_kk - T T^T quarter of
+//      tile-rows p and 7 - p (T staged in LDS) into pbuf (f64: DIAGX copies the quarters
+//      into its LDS image, diagx_split) or in place into A_kk (f32), and raises tflag 3.
+// Tickets: TPART(k, 3), (k, 2), (k, 1), (k, 0) in that order (order_tparts), after DIAGX(k-1)
+// and before DIAGX(k), and no other k's parts between them (test_schedule.py checks this).
+// Nothing but DIAGX(k) depends on the parts, so every ticket between them completes; a part
+// waits only on its siblings, so at most three workgroups wait at once and with P >= 4 one
+// is always free to claim the next sibling (split_for: fewer workers keep the whole step
+// inside DIAGX).
+// (the out-of-line functions read these through a pointer to the copy the kernel keeps in LDS,
+// pt_lds_ctx_off: a reference to the kernel's Args put the whole struct in scratch memory, and
+// every a.x of every task became a scratch load)
 template <typename T>
 struct TpCtx {
     int* ctl;
@@ -3095,14 +3100,20 @@ template void potrf_tiles_dist_launch<float>(const DistLaunch<float>&);
 
 // Host-only schedule statistics (no device work): tasks, predicted makespan, and a check
 // that every task's producers come earlier in the ticket order.
-int64_t potrf_tiles_schedule_stats(int nc, int nr, int P, bool build, double* est_us, int ni, int ratio) {
+int64_t potrf_tiles_schedule_stats(int nc, int nr, int P, bool build, double* est_us, int ni, int ratio,
+                                   int32_t* list_out, int64_t list_max) {
     if (nc < 1 || nr < nc || P < 1 || ni < 0 || ni > nr - nc)
         throw Error{GPRX_ERR_ARG, "potrf tile schedule: need nc >= 1, nr >= nc + ni, P >= 1"};
     const pt::Params& pr = pt::params();
-    const bool split = pt::split_for(true);  // the f64 schedule
+    const bool split = pt::split_for(true, P);  // the f64 schedule
     pt::Schedule S = ratio >= 0 ? pt::make_schedule(nc, nr, pr.W, pr.near_for(nc), P, pr.cm, build, ni, ratio, split, pr.tail)
                                 : pt::best_schedule(nc, nr, pr, P, build, ni, split);
     if (est_us) *est_us = S.est_us;
+    if (list_out)  // the ticket list: {type | nb << 8, i, j, b0} per ticket
+        for (int64_t q = 0; q < (int64_t)S.list.size() && q < list_max; q++) {
+            const int4 t = S.list[q];
+            list_out[4 * q] = t.x, list_out[4 * q + 1] = t.y, list_out[4 * q + 2] = t.z, list_out[4 * q + 3] = t.w;
+        }
     return S.ntasks;
 }
 

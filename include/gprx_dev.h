@@ -31,6 +31,10 @@ gprx_status gprx_dev_bench(gprx_ctx* ctx, gprx_dtype dtype, int32_t what, int64_
  * and simulated makespan (us).  Throws nothing, needs no
  * device: GPRX_ERR_ARG if the ticket order would violate a dependency. */
 gprx_status gprx_dev_schedule(int32_t nc, int32_t nr, int32_t P, int32_t build, double* est_us, int64_t* ntasks);
+/* Host-only: the same schedule's ticket list, 4 ints per ticket {type | chunk panels << 8, i, j,
+ * first panel} (types 0 DIAGX, 1 TRSM, 2 UPD, 3 BUILD, 4 TPART with j = the part), at most max
+ * tickets into out; returns the task count, -1 on bad arguments. */
+int64_t gprx_dev_schedule_list(int32_t nc, int32_t nr, int32_t P, int32_t build, int32_t* out, int64_t max);
 /* Host-only: the distributed factorisation's schedule (g ranks of P workers each, row blocks
  * grouped by gb, a window of ww panels; flags bit 0: with the fused covariance-build tasks,
  * bit 1: LML mode, the inverse's identity rows and the C = U U^T tiles riding along), simulated

@@ -253,3 +253,43 @@ def test_dist_schedule_rejects_bad_arguments():
     assert _dist_sched(0, 240, 1, 1, 8)[0] != 0
     assert _dist_sched(4, 240, 0, 1, 8)[0] != 0
     assert _dist_sched(4, 240, 33, 1, 8)[0] != 0
+
+
+def _sched_list(nc, nr, P=256, ratio=None, ident=False):
+    L = lib()
+    L.gprx_dev_schedule_list.restype = ctypes.c_int64
+    L.gprx_dev_schedule_list.argtypes = [ctypes.c_int32] * 4 + [ctypes.POINTER(ctypes.c_int32), ctypes.c_int64]
+    flags = (2 if ident else 0) | (0 if ratio is None else (ratio + 1) << 8)
+    n = L.gprx_dev_schedule_list(nc, nr, P, flags, None, 0)
+    assert n > 0
+    out = np.zeros((n, 4), np.int32)
+    assert L.gprx_dev_schedule_list(nc, nr, P, flags, out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), n) == n
+    return out
+
+
+@pytest.mark.parametrize("nc,ratio,ident", [(2, None, False), (9, 0, False), (33, 2, False), (40, 0, True),
+                                            (128, None, False)])
+def test_schedule_split_step_ticket_order(nc, ratio, ident):
+    """The split diagonal step's deadlock-freedom argument (k_ptiles.hip order_tparts): the four
+    TPART(k, c) tickets come in the order c = 3, 2, 1, 0, after DIAGX(k - 1) and before DIAGX(k),
+    and no other k's parts lie between them -- so at most three workgroups ever wait on a
+    sibling part and P >= 4 workers always leave one to claim the next ticket."""
+    lst = _sched_list(nc, 2 * nc + 1 if ident else nc + 1, ratio=ratio, ident=ident)
+    typ = lst[:, 0] & 0xFF
+    diag = {int(lst[q, 1]): q for q in np.nonzero(typ == 0)[0]}
+    assert sorted(diag) == list(range(nc))
+    tp = np.nonzero(typ == 4)[0]
+    assert len(tp) == tparts(nc)
+    for k in range(1, nc):
+        q = tp[lst[tp, 1] == k]
+        assert list(lst[q, 2]) == [3, 2, 1, 0]
+        assert diag[k - 1] < q[0] and q[-1] < diag[k]
+        assert np.all(lst[tp[(tp > q[0]) & (tp < q[-1])], 1] == k)
+
+
+def test_schedule_split_step_needs_four_workers():
+    """With fewer than four workers the parts could all wait on a sibling that no worker is
+    left to claim: the schedule falls back to the whole diagonal step inside DIAGX."""
+    lst = _sched_list(9, 10, P=3, ratio=0)
+    assert not np.any((lst[:, 0] & 0xFF) == 4)
+    assert len(lst) == _expected_tasks(9, 10) - tparts(9)
