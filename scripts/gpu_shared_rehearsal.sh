@@ -11,7 +11,8 @@ echo rc=$r
 grep -v 'amdgpu.ids\|socket.cpp' $O/bench.err | tail -5
 python - "$O" <<'PY'
 import json, sys
-d = json.load(open(sys.argv[1] + "/bench.json"))
+# gloo's connection message can share stdout with the JSON line
+d = json.loads([l for l in open(sys.argv[1] + "/bench.json") if l.startswith('{"metric"')][-1])
 print(round(d["value"], 2), d["ms_per_step"], d["dist_error"], d["config"]["parallelism"][:40], (d.get("replicas") or {}).get("value"))
 for k, v in (d.get("configs") or {}).items():
     print(k, (v or {}).get("value"), (v or {}).get("error"), (v or {}).get("scaling"))
