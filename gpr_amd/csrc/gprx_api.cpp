@@ -194,6 +194,50 @@ struct DevBuf {
     ~DevBuf() { release(); }
 };
 
+// Pinned host memory, mapped: the fit's status words come back by one kernel's stores into it
+// and one stream synchronisation (three synchronous hipMemcpy calls were three copy launches
+// and a host round trip each)
+struct PinnedBuf {
+    void* p = nullptr;
+    double* dev = nullptr;  // the device's address of it (mapped, coherent)
+    size_t bytes = 0;
+    void ensure(size_t b) {
+        if (b <= bytes && p) return;
+        release();
+        GPRX_HIP(hipHostMalloc(&p, b, hipHostMallocMapped | hipHostMallocCoherent));
+        void* d = nullptr;
+        GPRX_HIP(hipHostGetDevicePointer(&d, p, 0));
+        dev = static_cast<double*>(d);
+        bytes = b;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        dev = nullptr;
+        bytes = 0;
+    }
+    ~PinnedBuf() { release(); }
+};
+
+// Device copy of a small parameter struct, uploaded only when its bytes change (a pageable
+// hipMemcpyAsync blocks the host until the stream reaches it: every fit paid that wait between
+// its feature kernels and the factorisation launch)
+struct DevParam {
+    DevBuf buf;
+    std::vector<unsigned char> last;
+    template <typename S>
+    const S* put(const S& v, hipStream_t s) {
+        const bool fresh = buf.bytes < sizeof(S) || !buf.p;
+        buf.ensure(sizeof(S));
+        const unsigned char* b = reinterpret_cast<const unsigned char*>(&v);
+        if (fresh || last.size() != sizeof(S) || std::memcmp(last.data(), b, sizeof(S)) != 0) {
+            GPRX_HIP(hipMemcpyAsync(buf.p, &v, sizeof(S), hipMemcpyHostToDevice, s));
+            last.assign(b, b + sizeof(S));
+        }
+        return buf.as<S>();
+    }
+};
+
 static int64_t round_up(int64_t x, int64_t g) { return (x + g - 1) / g * g; }
 
 }  // namespace gprx
@@ -254,6 +298,8 @@ struct gprx_model {
     KCanon<double> kd{};
     KCanon<float> kf{};
     DevBuf X, Y, tab, A, Linv, z, alpha, info, flag, red, V, C, scratch1, scratch2, grad, pack, featU, featV, kdev;
+    DevParam kfit;     // the fit's kernel tree (uploaded when it changes)
+    PinnedBuf hstat;   // the fit's status words: flag, info, log det, data fit
     // fp32 models: fp64 iterative refinement state (k_refine.hip).  kd then holds the tree in
     // double with the parameters rounded to float first (the reference stores them in T).
     DevBuf Xd, Yd, ad, kxd, fud, fvd, kdev64, tabd, zd, outd, delta, nrm;
@@ -800,8 +846,7 @@ static gprx_status model_fit(gprx_model* M, uint32_t flags, gprx_fit_info* out) 
         M->tab.ensure(sizeof(T) * 2 * K.nper * n * M->d);
         launch_sincos_tables<T>(K, M->X.as<T>(), n, M->d, M->tab.as<T>(), s);
     }
-    GPRX_HIP(hipMemsetD32Async((hipDeviceptr_t)M->info.p, INT_MAX, 1, s));
-    GPRX_HIP(hipMemsetAsync(M->flag.p, 0, sizeof(int), s));
+    launch_fit_status_init(M->info.as<int>(), M->flag.as<int>(), s);
     const T sig = (T)M->sigma;
     const T sigma2 = sig * sig;  // m_Sigma*m_Sigma in T (lib/GaussianProcess.cpp:379)
     GPRX_HIP(hipEventRecord(ctx->ev[0], s));
@@ -823,13 +868,12 @@ static gprx_status model_fit(gprx_model* M, uint32_t flags, gprx_fit_info* out) 
         launch_pair_features<T>(K, M->X.as<T>(), n, M->d, M->X.as<T>(), false, M->featU.as<T>(), np, s,
                                 M->flag.as<int>());
         launch_pair_features<T>(K, M->X.as<T>(), n, M->d, M->X.as<T>(), true, M->featV.as<T>(), np, s);
-        M->kdev.ensure(sizeof(KCanon<T>));
-        GPRX_HIP(hipMemcpyAsync(M->kdev.p, &K, sizeof(KCanon<T>), hipMemcpyHostToDevice, s));
+        const KCanon<T>* kdev = M->kfit.put(K, s);
         if (!separate_build && potrf_uses_tiles())
-            tb = pairs_tile_build<T>(K, M->kdev.as<KCanon<T>>(), M->featU.as<T>(), M->featV.as<T>(), np, M->d, n, sigma2,
+            tb = pairs_tile_build<T>(K, kdev, M->featU.as<T>(), M->featV.as<T>(), np, M->d, n, sigma2,
                                      M->flag.as<int>());
         if (!tb.mode)
-            launch_kbuild_mma<T>(K, M->kdev.as<KCanon<T>>(), M->featU.as<T>(), M->featV.as<T>(), np, M->d, M->A.as<T>(),
+            launch_kbuild_mma<T>(K, kdev, M->featU.as<T>(), M->featV.as<T>(), np, M->d, M->A.as<T>(),
                                  ld, n, sigma2, M->flag.as<int>(), s);
         launch_aug_rows<T>(M->Y.as<T>(), n, M->m, M->A.as<T>(), ld, np, mp, s);
     } else {
@@ -854,13 +898,16 @@ static gprx_status model_fit(gprx_model* M, uint32_t flags, gprx_fit_info* out) 
         launch_gemm_nt_kskip<T>(M->C.as<T>(), np, U, ld, U, ld, np, np, np, s);
     }
     GPRX_HIP(hipEventRecord(ctx->ev[3], s));
+    // status words: one kernel stores them into mapped pinned memory, then one synchronisation
+    M->hstat.ensure(4 * sizeof(double));
+    volatile double* hs = static_cast<double*>(M->hstat.p);  // [0] flag, [1] info (ints), [2..3] log det, data fit
+    launch_fit_status_gather(M->flag.as<int>(), M->info.as<int>(), M->red.as<double>(), M->hstat.dev, s);
     GPRX_HIP(hipStreamSynchronize(s));
     GPRX_HIP(hipGetLastError());
     int hflag = 0, hinfo = 0;
-    double hred[2];
-    GPRX_HIP(hipMemcpy(&hflag, M->flag.p, sizeof(int), hipMemcpyDeviceToHost));
-    GPRX_HIP(hipMemcpy(&hinfo, M->info.p, sizeof(int), hipMemcpyDeviceToHost));
-    GPRX_HIP(hipMemcpy(hred, M->red.p, sizeof(hred), hipMemcpyDeviceToHost));
+    double hred[2] = {hs[2], hs[3]};
+    hflag = reinterpret_cast<volatile int*>(hs)[0];
+    hinfo = reinterpret_cast<volatile int*>(hs + 1)[0];
     M->fitted = false;
     M->has_alpha = false;
     M->inv_ready = false;

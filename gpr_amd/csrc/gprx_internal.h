@@ -367,6 +367,10 @@ void launch_aug_rows(const T* Y, int64_t n, int m, T* A, int64_t ld, int64_t np,
 // and for n <= j < ncols.
 template <typename T>
 void launch_diag_fix(T* A, int64_t ld, int64_t c0, int64_t w, int64_t n, T sigma2, hipStream_t s);
+// a fit's status words (k_build.hip): info = INT_MAX, flag = 0; and back into mapped pinned
+// host memory (out[0] flag, out[1] info as ints, out[2..3] = red[0..1])
+void launch_fit_status_init(int* info, int* flag, hipStream_t s);
+void launch_fit_status_gather(const int* flag, const int* info, const double* red, double* out_mapped, hipStream_t s);
 template <typename T>
 void launch_label_rows(const T* Y, int64_t n, int m, T* A, int64_t ld, int64_t row0, int64_t ncols, int64_t mp,
                        hipStream_t s);

@@ -16,6 +16,7 @@
 #include "gprx_internal.h"
 #include "k_tile.h"
 
+#include <climits>
 #include <cmath>
 #include <cstdint>
 
@@ -222,6 +223,36 @@ void launch_label_rows(const T* Y, int64_t n, int m, T* A, int64_t ld, int64_t r
 template <typename T>
 void launch_aug_rows(const T* Y, int64_t n, int m, T* A, int64_t ld, int64_t np, int64_t mp, hipStream_t s) {
     launch_label_rows<T>(Y, n, m, A, ld, np, np, mp, s);
+}
+
+// A fit's status words: info = INT_MAX (no failed pivot), flag = 0 (no non-finite entry), in
+// one launch (two memsets were two fill kernels, each with its dispatch gap, on every fit)
+__global__ void fit_status_init_kernel(int* __restrict__ info, int* __restrict__ flag) {
+    if (threadIdx.x == 0) {
+        *info = INT_MAX;
+        *flag = 0;
+    }
+}
+void launch_fit_status_init(int* info, int* flag, hipStream_t s) {
+    hipLaunchKernelGGL(fit_status_init_kernel, dim3(1), dim3(64), 0, s, info, flag);
+    GPRX_HIP(hipGetLastError());
+}
+
+// ... and back to the host: flag, info and the two reduced scalars into mapped pinned memory
+// (out[0], out[1] as ints, out[2..3]) by one kernel instead of three copy launches
+__global__ void fit_status_gather_kernel(const int* __restrict__ flag, const int* __restrict__ info,
+                                         const double* __restrict__ red, double* __restrict__ out) {
+    const int t = threadIdx.x;
+    if (t < 2) {
+        const int v = t == 0 ? *flag : *info;
+        __hip_atomic_store(reinterpret_cast<int*>(out + t), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    } else if (t < 4) {
+        __hip_atomic_store(out + t, red[t - 2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+void launch_fit_status_gather(const int* flag, const int* info, const double* red, double* out_mapped, hipStream_t s) {
+    hipLaunchKernelGGL(fit_status_gather_kernel, dim3(1), dim3(64), 0, s, flag, info, red, out_mapped);
+    GPRX_HIP(hipGetLastError());
 }
 
 template <typename T>

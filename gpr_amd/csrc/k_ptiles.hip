@@ -2856,6 +2856,7 @@ struct PtState {
     int64_t trace_n = 0, trace_nc = 0;
     const std::vector<int4>* last_list = nullptr;
     void* tb = nullptr;  // device copy of the launch's TileBuild
+    std::vector<unsigned char> tb_last;  // its bytes (re-uploaded only when they change)
     ~PtState() {
         if (tb) (void)hipFree(tb);
         if (pbuf) (void)hipFree(pbuf);
@@ -2891,6 +2892,12 @@ int pt_debug_snapshot(int* out, int max_wg) {
     const int n = std::min(max_wg, g_pt_dbg_n);
     for (int k = 0; k < 4 * n; k++) out[k] = __atomic_load_n(g_pt_dbg + k, __ATOMIC_RELAXED);
     return n;
+}
+
+// ctr[i] = -1 for i in [v0, v1), 0 elsewhere (i < n)
+__global__ void pt_init_counters(int* __restrict__ ctr, int64_t n, int64_t v0, int64_t v1) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) ctr[i] = (i >= v0 && i < v1) ? -1 : 0;
 }
 
 // counters of the identity row blocks (the inverse riding along): block a = i - nr0 has its
@@ -2960,9 +2967,15 @@ void potrf_tiles(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info
         st.ctr_ints = need;
     }
     hipStream_t s = ex.s0;
-    GPRX_HIP(hipMemsetAsync(st.ctr, 0, sizeof(int) * need, s));
-    if (fused)  // ver = -1 (not built) for the tiles of the leading block; the label rows are built
-        GPRX_HIP(hipMemsetAsync(st.ctr + C_NCTL + nr, 0xff, sizeof(int) * (size_t)nc * nc, s));
+    // counters zeroed, and (fused build) ver = -1 (not built) for the tiles of the leading
+    // block (the label rows are built): one launch (the two memsets of odd sizes were five
+    // fill kernels, each with its dispatch gap, on every fit)
+    {
+        const int64_t v0 = fused ? (int64_t)C_NCTL + nr : 0, v1 = fused ? v0 + (int64_t)nc * nc : 0;
+        hipLaunchKernelGGL(pt_init_counters, dim3((unsigned)((need + 255) / 256)), dim3(256), 0, s, st.ctr,
+                           (int64_t)need, v0, v1);
+        GPRX_HIP(hipGetLastError());
+    }
     if (ni > 0) {
         hipLaunchKernelGGL(pt_init_identity_counters, dim3((unsigned)ni), dim3(128), 0, s, st.ctr + C_NCTL,
                            st.ctr + C_NCTL + nr, nc, nr - ni, ni);
@@ -2990,7 +3003,12 @@ void potrf_tiles(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info
     if (fused) {
         GPRX_REQUIRE(build->nf == np, GPRX_ERR_ARG, "potrf_tiles: build features must have np rows");
         if (!st.tb) GPRX_HIP(hipMalloc(&st.tb, sizeof(TileBuild<double>)));
-        GPRX_HIP(hipMemcpyAsync(st.tb, build, sizeof(TileBuild<T>), hipMemcpyHostToDevice, s));
+        // (a pageable copy blocks the host until the stream reaches it: skipped when unchanged)
+        const unsigned char* tbb = reinterpret_cast<const unsigned char*>(build);
+        if (st.tb_last.size() != sizeof(TileBuild<T>) || std::memcmp(st.tb_last.data(), tbb, sizeof(TileBuild<T>)) != 0) {
+            GPRX_HIP(hipMemcpyAsync(st.tb, build, sizeof(TileBuild<T>), hipMemcpyHostToDevice, s));
+            st.tb_last.assign(tbb, tbb + sizeof(TileBuild<T>));
+        }
         a.tb = reinterpret_cast<const TileBuild<T>*>(st.tb);
     }
     a.dbg = nullptr;
