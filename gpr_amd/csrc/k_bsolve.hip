@@ -132,6 +132,31 @@ __device__ __forceinline__ bool wait_flag(const int* f, int* ctl, long long t0, 
     return true;
 }
 
+// alpha is pre-filled with a NaN of a fixed payload (bs_init_kernel): a consumer polls the
+// values of alpha_{k+1} themselves on the critical path -- one global round trip per block
+// instead of two (poll the flag, then load the values).  No computed value has this payload.
+__device__ __forceinline__ bool unset(double v) {
+    return __builtin_bit_cast(unsigned long long, v) == 0x7ff4deadbeef1234ull;
+}
+__device__ __forceinline__ bool unset(float v) { return __builtin_bit_cast(unsigned, v) == 0x7fa5deadu; }
+template <typename T>
+__device__ __forceinline__ T unset_value();
+template <>
+__device__ __forceinline__ double unset_value<double>() {
+    return __builtin_bit_cast(double, 0x7ff4deadbeef1234ull);
+}
+template <>
+__device__ __forceinline__ float unset_value<float>() {
+    return __builtin_bit_cast(float, 0x7fa5deadu);
+}
+// the chain's counters zeroed and alpha set to the "not yet solved" value, in one launch
+template <typename T>
+__global__ void bs_init_kernel(int* __restrict__ ctl, int64_t nctl, T* __restrict__ alpha, int64_t nalpha) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < nctl) ctl[i] = 0;
+    if (alpha && i < nalpha) alpha[i] = unset_value<T>();
+}
+
 // Load QR consecutive values starting at p (16-byte aligned) into registers.
 template <typename T>
 __device__ __forceinline__ void load_run(const T* __restrict__ p, T (&x)[QR]) {
@@ -149,8 +174,8 @@ __device__ __forceinline__ void load_run(const T* __restrict__ p, T (&x)[QR]) {
 // registers in the column layout (thread: column c, rows QR q ..), and it streams the tiles
 // L_{j,k}, j >= k + 2 (coalesced, lanes over rows; each tile's loads issued before its
 // alpha_j is waited for), reducing them in-wave.  The critical path once alpha_{k+1} is
-// published: 32 FMAs per thread, a 4-way combine through LDS, 32 FMAs against Linv_k, a
-// combine, the alpha_k stores.
+// published (its values polled directly, bs_init_kernel): 32 FMAs per thread, a 4-way
+// combine through LDS, 32 FMAs against Linv_k, a combine, the alpha_k stores.
 template <typename T>
 __global__ __launch_bounds__(NT) void backsolve_chain_kernel(Args<T> a) {
     __shared__ T s_alpha[DB];     // alpha_j being applied
@@ -187,21 +212,11 @@ __global__ __launch_bounds__(NT) void backsolve_chain_kernel(Args<T> a) {
         const T* p1 = bs_tile<T>(a, k + 1, k, nb, l1);
         load_run<T>(p1 + (int64_t)c * l1 + QR * q, t1);
     }
-    // one alpha block into s_alpha, then every thread's partial of (L^T alpha)_c over its rows
-    auto apply = [&](const T(&x)[QR], const T* alpha_j, int r) {
-        if (t < DB) s_alpha[t] = ld_sc1(alpha_j + (int64_t)t * a.m + r);
-        __syncthreads();
-        T s = 0;
-#pragma unroll
-        for (int i = 0; i < QR; i++) s = fma(x[i], s_alpha[QR * q + i], s);
-        s_part[q][c] = s;
-        __syncthreads();
-    };
     // agree on a failed wait (waves poll on their own) before using the barriers' results
     auto agree = [&](bool ok) {
         if (t == 0) s_int[1] = 0;
         __syncthreads();
-        if (!ok && lane == 0) s_int[1] = 1;
+        if (!ok) s_int[1] = 1;  // (any lane: the alpha poll fails per lane)
         __syncthreads();
         return s_int[1] == 0;
     };
@@ -239,10 +254,34 @@ __global__ __launch_bounds__(NT) void backsolve_chain_kernel(Args<T> a) {
         // ---- critical path ----
         T crit = 0;
         if (has1) {
-            ok = wait_flag(fl + k + 1, a.ctl, t0, a.tlimit);
+            // alpha_{k+1} polled value by value (lanes of waves 0-1), straight into s_alpha
+            if (t < DB) {
+                const T* ap = a.alpha + ((int64_t)(k + 1) * DB + t) * a.m + r;
+                T v = ld_sc1(ap);
+                while (unset(v)) {
+                    if (__hip_atomic_load(a.ctl + C_ERR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                        ok = false;
+                        break;
+                    }
+                    if (wall_clock64() - t0 > a.tlimit) {
+                        __hip_atomic_store(a.ctl + C_ERR, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        ok = false;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                    v = ld_sc1(ap);
+                }
+                s_alpha[t] = v;
+            }
             if (a.trace && r == 0 && t == 0) a.trace[4 * k + 2] = wall_clock64();
-            if (!agree(ok)) break;
-            apply(t1, a.alpha + (int64_t)(k + 1) * DB * a.m, r);
+            if (!agree(ok)) break;  // (its barriers also publish s_alpha)
+            {
+                T sp = 0;
+#pragma unroll
+                for (int i = 0; i < QR; i++) sp = fma(t1[i], s_alpha[QR * q + i], sp);
+                s_part[q][c] = sp;
+            }
+            __syncthreads();
             if (t < DB) crit = s_part[0][t] + s_part[1][t] + s_part[2][t] + s_part[3][t];
         } else {
             __syncthreads();  // s_other complete
@@ -315,7 +354,7 @@ __global__ __launch_bounds__(NT) void forward_chain_kernel(Args<T> a) {
         // agree on a failed wait (each wave polled on its own)
         if (t == 0) s_int[1] = 0;
         __syncthreads();
-        if (!ok && lane == 0) s_int[1] = 1;
+        if (!ok) s_int[1] = 1;  // (any lane: the alpha poll fails per lane)
         s_part[w][2 * lane] = p0;
         s_part[w][2 * lane + 1] = p1;
         __syncthreads();
@@ -380,7 +419,12 @@ void launch_backsolve_chain(const T* A, int64_t ld, int64_t np, int m, const T* 
     GPRX_REQUIRE(np % DB == 0, GPRX_ERR_ARG, "launch_backsolve_chain: bad sizes");
     int* scratch = ex.scratch_ints(need);
     ProfScope ps(KC_BACKSOLVE, s, 2.0 * (double)np * np * m / 2.0, (double)sizeof(T) * np * (np + 1) / 2.0);
-    GPRX_HIP(hipMemsetAsync(scratch, 0, sizeof(int) * need, s));
+    {
+        const int64_t na = np * (int64_t)m, nmax = std::max<int64_t>((int64_t)need, na);
+        hipLaunchKernelGGL(bs_init_kernel<T>, dim3((unsigned)((nmax + 255) / 256)), dim3(256), 0, s, scratch,
+                           (int64_t)need, alpha, na);
+        GPRX_HIP(hipGetLastError());
+    }
     Args<T> a;
     a.A = A;
     a.ld = ld;
