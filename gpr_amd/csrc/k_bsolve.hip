@@ -232,10 +232,31 @@ __global__ __launch_bounds__(NT) void backsolve_chain_kernel(Args<T> a) {
             int64_t lj;
             const T* pj = bs_tile<T>(a, j, k, nb, lj);
             tr.load(pj, lj, w, lane);
-            ok = wait_flag(fl + j, a.ctl, t0, a.tlimit);
-            if (!ok) break;
+            // alpha_j's two values of this lane, polled directly (no flag round trip first: the
+            // loop follows the chain front, and its last tile j = k + 2 was late for alpha_{k+1})
             const int64_t rj = (int64_t)j * DB + 2 * lane;
-            const T v0 = ld_sc1(a.alpha + rj * a.m + r), v1 = ld_sc1(a.alpha + (rj + 1) * a.m + r);
+            const T* p0 = a.alpha + rj * a.m + r;
+            const T* p1 = a.alpha + (rj + 1) * a.m + r;
+            T v0 = ld_sc1(p0), v1 = ld_sc1(p1);
+            while (unset(v0) || unset(v1)) {
+                if (__hip_atomic_load(a.ctl + C_ERR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                    ok = false;
+                    break;
+                }
+                if (wall_clock64() - t0 > a.tlimit) {
+                    __hip_atomic_store(a.ctl + C_ERR, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    ok = false;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+                v0 = ld_sc1(p0);
+                v1 = ld_sc1(p1);
+            }
+            // (a lane that failed leaves the loop at once; the others find the error word set)
+            if (!__builtin_amdgcn_readfirstlane(__ballot(ok) == __ballot(1))) {
+                ok = false;
+                break;
+            }
             tr.apply(v0, v1, p);
         }
         if (!agree(ok)) break;
