@@ -224,6 +224,12 @@ __global__ __launch_bounds__(NT) void backsolve_chain_kernel(Args<T> a) {
     for (int r = 0; r < a.m && ok; r++) {
         int* fl = flags + (int64_t)r * nb;
         const long long t0 = wall_clock64();
+        T zc;  // label row r of block k (z^T; final before the launch: loaded first, off the chain)
+        {
+            int64_t lz;
+            const T* pz = bs_tile<T>(a, nb, k, nb, lz);
+            zc = pz[r + (int64_t)c * lz];
+        }
         T p[CPW];
 #pragma unroll
         for (int cc = 0; cc < CPW; cc++) p[cc] = 0;
@@ -264,12 +270,6 @@ __global__ __launch_bounds__(NT) void backsolve_chain_kernel(Args<T> a) {
             int col;
             const T sum = wave_reduce_cols<T>(p, lane, col);
             if ((lane & 3) == 0) s_other[CPW * w + col] = sum;
-        }
-        T zc;  // label row r of block k (z^T)
-        {
-            int64_t lz;
-            const T* pz = bs_tile<T>(a, nb, k, nb, lz);
-            zc = pz[r + (int64_t)c * lz];
         }
         if (a.trace && r == 0 && t == 0) a.trace[4 * k + 1] = wall_clock64();
         // ---- critical path ----
