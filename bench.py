@@ -278,8 +278,8 @@ def main():
                          "scaling) or independent fits per GPU (replicas, weak scaling); both are measured")
     ap.add_argument("--configs", type=int, default=1, help="also measure BASELINE configs C2, C4, C5 (0 = skip)")
     ap.add_argument("--dist-lml", type=int, default=0,
-                    help="N > 1: also time the LML + gradient on the sharded factor (off by default: at N = 16384 "
-                         "two processes sharing one GPU hang in it, DESIGN.md 6)")
+                    help="N > 1: also time the LML + gradient on the sharded factor (off by default: not part "
+                         "of the headline; rehearsed with two processes on one GPU, DESIGN.md 6)")
     ap.add_argument("--force-dist", action="store_true",
                     help="testing: run the sharded-fit leg (and make it the headline) even at N = 1")
     args = ap.parse_args()

@@ -354,6 +354,15 @@ void copy_from_mailbox(const void* src, T* dst, int64_t count, hipStream_t s) {
 
 }  // namespace
 
+// GPRX_DIST_VERBOSE=1: host-side progress of the setup and the fit, with timestamps (stderr)
+static void dist_say(int rank, const char* what, long long a = -1) {
+    static const bool on = std::getenv("GPRX_DIST_VERBOSE") != nullptr;
+    if (!on) return;
+    static const auto t0 = std::chrono::steady_clock::now();
+    const double t = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    std::fprintf(stderr, "[gprx dist r%d %8.3f] %s %lld\n", rank, t, what, a);
+}
+
 // ---------------------------------------------------------------------------------------
 // engine setup (per shape): layout, schedule, buffers, mailbox mappings, tables
 // ---------------------------------------------------------------------------------------
@@ -362,7 +371,9 @@ static void setup(DistEngine<T>& E, const DistContext& C, int64_t n, int m, bool
     if (E.key_n == n && E.key_m == m && E.key_fused == fused && E.key_inv == inv && !E.ranks.empty()) return;
     GPRX_REQUIRE(m <= GT, GPRX_ERR_DIM, "distributed fit: at most 128 label columns");
     GPRX_REQUIRE(C.world >= 1 && C.world <= 32, GPRX_ERR_ARG, "distributed fit: 1..32 ranks");
+    dist_say(C.rank, "setup: teardown", n);
     E.teardown();
+    dist_say(C.rank, "setup: teardown done", inv ? 1 : 0);
     const int64_t np = (n + DB - 1) / DB * DB;
     const int nc = (int)(np / DB);
     E.g = C.world;
@@ -439,18 +450,24 @@ static void setup(DistEngine<T>& E, const DistContext& C, int64_t n, int m, bool
         if (const char* e = std::getenv("GPRX_DIST_WINDOW_MB")) budget = std::atof(e) * 1048576.0;
         const int nrw = nc + 1 + (inv ? nc : 0);
         auto wbytes = [&](int w) { return (double)w * nrw * DB * DB * (double)sizeof(T); };
-        // Separate processes in LML mode (identity rows and C tiles riding along): windows
-        // above 16 panels hung at N = 16384 on two processes sharing one GPU (N <= 12288, or a
-        // 16-panel window, or virtual ranks with any window were fine; root cause not found,
-        // DESIGN.md 6), so that case keeps to 16
-        const int wcap = (inv && !E.virt) ? 16 : nc;
+        // Separate processes map each other's mailbox through IPC, and hipIpcOpenMemHandle of
+        // a mailbox above 2 GiB never returned (the sharded LML at N = 16384 with a 64-panel
+        // window: 2.19 GB; GPRX_DIST_VERBOSE located it): the window keeps the
+        // mailbox below that
+        const bool ipc = !E.virt;
+        auto mb_bytes = [&](int w) {
+            MailboxLayout ml;
+            ml.init(E.g, nc, nrw, w, m, sizeof(T), true);
+            return ml.bytes;
+        };
+        constexpr int64_t kIpcMax = (int64_t(1) << 31) - (int64_t(1) << 20);
         std::vector<int> cws;
-        for (int w = 8; w < std::min(nc, wcap); w *= 2) cws.push_back(w);
-        cws.push_back(std::max(2, std::min(nc, wcap)));
+        for (int w = 8; w < nc; w *= 2) cws.push_back(w);
+        cws.push_back(std::max(2, nc));
         int pick = -1;
         DistSched ps;
         for (int w : cws) {
-            if (pick >= 0 && wbytes(w) > budget) break;
+            if (pick >= 0 && (wbytes(w) > budget || (ipc && mb_bytes(w) > kIpcMax))) break;
             DistSched c = sim(gb, w);
             if (pick < 0 || c.est_us < 0.995 * ps.est_us) {
                 pick = w;
@@ -477,6 +494,7 @@ static void setup(DistEngine<T>& E, const DistContext& C, int64_t n, int m, bool
     E.MB.init(E.g, nc, nr, ww, m, sizeof(T), E.g > 1);
     const int64_t DB2 = (int64_t)DB * DB;
     // ---- per local rank: buffers -------------------------------------------------------------
+    dist_say(C.rank, "setup: schedule done, window", ww);
     for (int v = 0; v < nlocal; v++) {
         auto R = std::make_unique<DistRank<T>>();
         R->r = E.virt ? v : C.rank;
@@ -487,8 +505,11 @@ static void setup(DistEngine<T>& E, const DistContext& C, int64_t n, int m, bool
         GPRX_HIP(hipEventCreate(&R->t1));
         R->store.alloc(sizeof(T) * (size_t)E.L.elems[r], false);
         static const bool coarse = std::getenv("GPRX_DIST_COARSE") && std::atoi(std::getenv("GPRX_DIST_COARSE")) != 0;
+        dist_say(C.rank, "setup: store allocated, mailbox bytes", (long long)E.MB.bytes);
         R->mbox.alloc((size_t)E.MB.bytes, !coarse);
+        dist_say(C.rank, "setup: mailbox allocated");
         GPRX_HIP(hipMemset(R->mbox.p, 0, E.MB.bytes));  // flags 0: below every epoch
+        dist_say(C.rank, "setup: mailbox cleared");
         R->ctr.alloc(sizeof(int) * ((size_t)C_NCTL_DIST + nr + (size_t)nr * nci + nc + 4 * (size_t)nc), false);
         if (potrf_split_for(std::is_same<T, double>::value, E.P)) R->pbuf.alloc(sizeof(T) * 4 * DB * DB, false);
         R->info.alloc(160 * sizeof(int), false);  // info, then the GPRX_DIST_CHECK counters and log
@@ -520,7 +541,9 @@ static void setup(DistEngine<T>& E, const DistContext& C, int64_t n, int m, bool
             GPRX_HIP(hipIpcGetMemHandle(&mine[0], R.mbox.p));
             GPRX_HIP(hipIpcGetMemHandle(&mine[1], R.store.p));
             std::vector<hipIpcMemHandle_t> all(2 * (size_t)E.g);
+            dist_say(C.rank, "setup: ipc handles taken");
             E.hc->allgather(mine, sizeof(mine), all.data());
+            dist_say(C.rank, "setup: ipc handles exchanged");
             for (int q = 0; q < E.g; q++) {
                 if (q == R.r) continue;
                 for (int h = 0; h < 2; h++) {
@@ -528,6 +551,7 @@ static void setup(DistEngine<T>& E, const DistContext& C, int64_t n, int m, bool
                     GPRX_HIP(hipIpcOpenMemHandle(&p, all[2 * (size_t)q + h], hipIpcMemLazyEnablePeerAccess));
                     R.opened.push_back(p);
                     (h == 0 ? R.mb : R.st)[q] = (uint64_t)p;
+                    dist_say(C.rank, "setup: ipc handle opened", 2 * q + h);
                 }
             }
         }
@@ -666,6 +690,7 @@ void dist_fit(DistEngineBase*& eng, const DistContext& C, const DistFitIn<T>& in
     DistEngine<T>& E = *Ep;
     const bool fused = in.tb.mode != 0;
     setup<T>(E, C, in.n, in.m, fused, in.inv);
+    dist_say(C.rank, "fit: setup done", in.inv ? 1 : 0);
     const int nc = E.L.nc, nr = E.L.nr, nci = E.L.nci;
     const int64_t np = E.np, n = in.n;
     const int64_t DB2 = (int64_t)DB * DB;
@@ -742,6 +767,19 @@ void dist_fit(DistEngineBase*& eng, const DistContext& C, const DistFitIn<T>& in
         Lc.P = E.P;
         Lc.s = s;
         Lc.dbg = nullptr;
+        static const bool dbg_on = std::getenv("GPRX_PT_DEBUG") != nullptr;
+        if (dbg_on && E.ranks.size() == 1) {  // {ticket, phase, i, j} per workgroup, read by gprx_dev_pt_debug
+            static int* hd = nullptr;
+            static int hn = 0;
+            if (hn < E.P) {
+                if (hd) (void)hipHostFree(hd);
+                GPRX_HIP(hipHostMalloc((void**)&hd, sizeof(int) * 4 * E.P, hipHostMallocCoherent));
+                hn = E.P;
+            }
+            std::memset(hd, 0xff, sizeof(int) * 4 * E.P);
+            pt_debug_register(hd, E.P);
+            Lc.dbg = hd;
+        }
         Lc.trace = nullptr;
         Lc.split = potrf_split_for(std::is_same<T, double>::value, E.P) ? 1 : 0;
         Lc.pbuf = R.pbuf.template as<T>();
@@ -753,6 +791,7 @@ void dist_fit(DistEngineBase*& eng, const DistContext& C, const DistFitIn<T>& in
         }
     }
     // every rank's persistent launch back to back, nothing that could block in between
+    dist_say(C.rank, "fit: launching");
     for (size_t v = 0; v < E.ranks.size(); v++) {
         GPRX_HIP(hipEventRecord(E.ranks[v]->t0, E.ranks[v]->s));
         potrf_tiles_dist_launch<T>(launches[v]);

@@ -493,7 +493,9 @@ struct DistSched {
 };
 DistSched potrf_dist_schedule(int nc, int g, int gb, int ww, int P, bool build, bool inv, int ratio = 0, bool f64 = true,
                               int tail = 0);
-bool potrf_split_for(bool f64, int P);  // the split diagonal step is on (this precision, P workgroups)
+bool potrf_split_for(bool f64, int P);
+// GPRX_PT_DEBUG: the per-workgroup status words gprx_dev_pt_debug reads (k_ptiles.hip)
+void pt_debug_register(int* dbg, int n);  // the split diagonal step is on (this precision, P workgroups)
 template <typename T>
 void potrf_tiles_dist_launch(const DistLaunch<T>& L);
 

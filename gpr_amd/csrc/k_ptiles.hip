@@ -2893,6 +2893,11 @@ int pt_debug_snapshot(int* out, int max_wg) {
     for (int k = 0; k < 4 * n; k++) out[k] = __atomic_load_n(g_pt_dbg + k, __ATOMIC_RELAXED);
     return n;
 }
+// a distributed rank's launch (GPRX_PT_DEBUG, one rank per process): its status words
+void pt_debug_register(int* dbg, int n) {
+    g_pt_dbg = dbg;
+    g_pt_dbg_n = n;
+}
 
 // ctr[i] = -1 for i in [v0, v1), 0 elsewhere (i < n)
 __global__ void pt_init_counters(int* __restrict__ ctr, int64_t n, int64_t v0, int64_t v1) {

@@ -571,9 +571,10 @@ def test_peer_two_processes(tmp_path):
 
 
 def test_peer_two_processes_lml_c3():
-    """The sharded LML at C3's size across two PROCESSES (peer context, one GPU shared): windows
-    above 16 panels hung here (known issue), so separate processes keep the LML
-    window at 16.  Both ranks must finish and agree with the single-GPU likelihood."""
+    """The sharded LML at C3's size across two PROCESSES (peer context, one GPU shared): with a
+    64-panel window the peer's mailbox was 2.19 GB and hipIpcOpenMemHandle of it never returned
+    (DESIGN.md 6); the window selection keeps every mailbox below 2 GiB.  Both ranks must finish
+    and agree with the single-GPU likelihood."""
     import os
     import socket
     import subprocess
