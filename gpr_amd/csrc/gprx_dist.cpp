@@ -193,6 +193,10 @@ struct DistLayout {
     }
 };
 
+// the largest allocation mapped into another process (hipIpcOpenMemHandle of a larger one never
+// returned on this stack: the sharded LML's 2.19 GB mailbox, a 2.1 GB rank storage at N = 32768)
+constexpr int64_t kIpcMaxBytes = (int64_t(1) << 31) - (int64_t(1) << 20);
+
 // mailbox byte layout (identical on every rank): see PtDist / DSArgs
 struct MailboxLayout {
     int64_t o_linv = 0, o_win = 0, o_z = 0, o_alpha = 0, o_zf = 0, o_part = 0, o_flags = 0, o_sflags = 0, o_tags = 0,
@@ -460,14 +464,13 @@ static void setup(DistEngine<T>& E, const DistContext& C, int64_t n, int m, bool
             ml.init(E.g, nc, nrw, w, m, sizeof(T), true);
             return ml.bytes;
         };
-        constexpr int64_t kIpcMax = (int64_t(1) << 31) - (int64_t(1) << 20);
         std::vector<int> cws;
         for (int w = 8; w < nc; w *= 2) cws.push_back(w);
         cws.push_back(std::max(2, nc));
         int pick = -1;
         DistSched ps;
         for (int w : cws) {
-            if (pick >= 0 && (wbytes(w) > budget || (ipc && mb_bytes(w) > kIpcMax))) break;
+            if (pick >= 0 && (wbytes(w) > budget || (ipc && mb_bytes(w) > kIpcMaxBytes))) break;
             DistSched c = sim(gb, w);
             if (pick < 0 || c.est_us < 0.995 * ps.est_us) {
                 pick = w;
@@ -492,6 +495,9 @@ static void setup(DistEngine<T>& E, const DistContext& C, int64_t n, int m, bool
     E.L.init(E.g, gb, nc, inv);
     const int nr = E.L.nr, nci = E.L.nci;
     E.MB.init(E.g, nc, nr, ww, m, sizeof(T), E.g > 1);
+    GPRX_REQUIRE(E.virt || E.g == 1 || E.MB.bytes < kIpcMaxBytes, GPRX_ERR_ARG,
+                 "distributed fit: the mailbox would exceed 2 GiB, the largest allocation another process can map "
+                 "(set GPRX_DIST_WINDOW lower)");
     const int64_t DB2 = (int64_t)DB * DB;
     // ---- per local rank: buffers -------------------------------------------------------------
     dist_say(C.rank, "setup: schedule done, window", ww);
@@ -547,6 +553,9 @@ static void setup(DistEngine<T>& E, const DistContext& C, int64_t n, int m, bool
             for (int q = 0; q < E.g; q++) {
                 if (q == R.r) continue;
                 for (int h = 0; h < 2; h++) {
+                    // hipIpcOpenMemHandle of an allocation above 2 GiB never returns:
+                    // a peer's storage that large is not mapped (only the dense gather reads it)
+                    if (h == 1 && (int64_t)sizeof(T) * E.L.elems[q] >= kIpcMaxBytes) continue;
                     void* p = nullptr;
                     GPRX_HIP(hipIpcOpenMemHandle(&p, all[2 * (size_t)q + h], hipIpcMemLazyEnablePeerAccess));
                     R.opened.push_back(p);
@@ -978,6 +987,9 @@ void dist_gather_factor(DistEngineBase* eng, T* A, int64_t ld, T* Linv, hipStrea
     std::vector<uint64_t> src((size_t)nc * nc, 0);
     for (int i = 0; i < nc; i++) {
         const int q = E.L.own[i];
+        GPRX_REQUIRE(R0.st[q] != 0, GPRX_ERR_STATE,
+                     "distributed fit: the dense factor gather needs every rank's storage mapped, and a rank's "
+                     "storage above 2 GiB cannot be mapped across processes");
         for (int j = 0; j < i; j++)
             src[(size_t)i * nc + j] = R0.st[q] + sizeof(T) * (uint64_t)(E.L.roff[q][E.L.loc[i]] + (int64_t)j * DB2);
     }
