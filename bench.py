@@ -29,8 +29,11 @@ inducing, N=1e6 d=64 fp64, dense rows sharded over the ranks).
 Prints ONE JSON line on rank 0 (plus human-readable detail on stderr).
 """
 import argparse
+import csv
+import glob
 import json
 import os
+import re
 import sys
 import time
 
@@ -42,6 +45,8 @@ sys.path.insert(0, ROOT)
 PEAK_FP64_TFLOPS = 78.6   # MI355X dense fp64 (vector = matrix), MI355X_MICROARCH.md / SURVEY.md §8(d)
 PEAK_FP32_TFLOPS = 157.3  # MI355X dense fp32 matrix
 PEAK_HBM_GBS = 8000.0     # HBM3E spec
+# the measured parts of one bench run; `--legs` selects a subset (one leg per profiled process)
+LEGS = ("c3", "predict", "variance", "lml", "build", "c2", "c4", "c5")
 
 
 def log(*a):
@@ -77,20 +82,31 @@ def cpu_baseline(cfg, n_cpu):
     }
 
 
-def traffic_from_profile(kernels=("potrf_tiles_kernel<double, false>", "potrf_tiles_kernel<double>")):
-    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC passes
-    (profiles/*_pmc_traffic.json, written by scripts/pmc_traffic.py).  L2-fabric bytes:
+def _short(name):
+    """Kernel name without `void`, namespaces and the argument list (as scripts/pmc_traffic.py)."""
+    m = re.match(r"(?:void )?(?:[A-Za-z_0-9]+::)*([A-Za-z_0-9]+<[^()]*>|[A-Za-z_0-9]+)", name)
+    return m.group(1) if m else name
+
+
+def _tagged(pattern):
+    """Committed profile summaries matching profiles/<pattern>, oldest first: tags r<round><a..z,
+    aa..az ...> order by round, then by the tag's length and letters (r03ak after r03t)."""
+    def order(path):
+        m = re.match(r"r(\d+)([a-z]*)_", os.path.basename(path))
+        return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, "")
+    return sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)), key=order)
+
+
+def traffic_from_profile(leg="c3", kernels=("potrf_tiles_kernel<double, false>",)):
+    """HBM bytes per launch of a leg's dominant kernel from the newest committed rocprofv3 PMC
+    passes of that leg (profiles/<tag>_<leg>_pmc_traffic.json, scripts/pmc_traffic.py; for the
+    C3 fit also the older leg-less profiles/<tag>_pmc_traffic.json).  L2-fabric bytes:
     FETCH_SIZE x 2 -- the gfx950 correction for 16-B-per-lane streaming reads, which is how the
     tile kernel reads all of its operands (MI355X_MICROARCH.md §HBM) -- + WRITE_SIZE, averaged
     over launches; Infinity-Cache hits are included, so this bounds HBM bytes from above."""
-    import glob
-    import re
-
-    def order(path):  # tags r<round><a..z, aa..az ...>: by round, then by the tag's length and letters
-        m = re.match(r"r(\d+)([a-z]*)_", os.path.basename(path))
-        return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, "")
-
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")), key=order)
+    files = _tagged(f"*_{leg}_pmc_traffic.json")
+    if leg == "c3" and not files:
+        files = [p for p in _tagged("*_pmc_traffic.json") if re.match(r"r\d+[a-z]*_pmc_traffic", os.path.basename(p))]
     for path in reversed(files):
         try:
             with open(path) as f:
@@ -103,7 +119,61 @@ def traffic_from_profile(kernels=("potrf_tiles_kernel<double, false>", "potrf_ti
     return None
 
 
-def run_configs(args, world, rank, local_rank, dctx, max_over_ranks, barrier_sync):
+def rocprof_from_profile(leg, kernels, inrun_us=None):
+    """The average launch duration of a leg's dominant kernel in the newest committed
+    `rocprofv3 --kernel-trace --stats` summary of that leg (profiles/<tag>_<leg>_kernel_stats.csv,
+    one profiled bench.py process per leg: scripts/gpu.sh profile), beside this run's in-run
+    HIP-event average, so every roofline in the line can be checked against a profile."""
+    for path in reversed(_tagged(f"*_{leg}_kernel_stats.csv")):
+        try:
+            with open(path) as f:
+                rows = [r for r in csv.DictReader(f) if _short(r["Name"]) in kernels]
+        except Exception:
+            continue
+        if rows:
+            r = max(rows, key=lambda r: float(r["TotalDurationNs"]))
+            avg = float(r["AverageNs"]) / 1e3
+            return {"avg_us": avg, "calls": int(r["Calls"]), "kernel": _short(r["Name"]),
+                    "source": os.path.basename(path),
+                    "inrun_over_rocprof": (inrun_us / avg) if inrun_us else None}
+    return None
+
+
+def rocprof_table(leg, min_percent=1.0):
+    """Every kernel above `min_percent` of the device time in the newest committed kernel-stats
+    summary of a leg (the LML's several launches)."""
+    files = _tagged(f"*_{leg}_kernel_stats.csv")
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        rows = [r for r in csv.DictReader(f) if float(r["Percentage"]) >= min_percent]
+    return {"source": os.path.basename(files[-1]),
+            "kernels": {_short(r["Name"]): {"avg_us": float(r["AverageNs"]) / 1e3, "calls": int(r["Calls"])}
+                        for r in rows}}
+
+
+def mfma_from_profile(leg, kernels):
+    """MFMA-busy fraction of a leg's dominant kernel from the newest committed PMC pass
+    (profiles/<tag>_<leg>_pmc_mfma.json, scripts/pmc_mfma.py), averaged over its launches."""
+    for path in reversed(_tagged(f"*_{leg}_pmc_mfma.json")):
+        try:
+            with open(path) as f:
+                ks = json.load(f)["kernels"]
+            v = next((ks[n] for n in kernels if n in ks), None)
+        except Exception:
+            continue
+        if v:
+            return {"mfma_busy_frac": float(np.mean([x["mfma_busy_frac"] for x in v])),
+                    "clock_ghz": float(np.mean([x["clock_ghz"] for x in v])), "launches": len(v),
+                    "source": os.path.basename(path)}
+    return None
+
+
+class _Skip(Exception):
+    """A leg left out by --legs."""
+
+
+def run_configs(args, world, rank, local_rank, dctx, max_over_ranks, barrier_sync, want):
     """BASELINE.json configs[1], [3], [4] (C2, C4, C5), each timed like the headline (warmup,
     then K steps between barriers, max over ranks) with the dominant kernel's roofline from its
     HIP-event device time, and (rank 0, N = 1) a labelled CPU baseline on a bounded sample."""
@@ -134,6 +204,8 @@ def run_configs(args, world, rank, local_rank, dctx, max_over_ranks, barrier_syn
 
     # ---- C2: N=4096 d=16 GaussianKernel fp64 (replicas: every rank fits its own) -----------------
     try:
+        if not want("c2"):
+            raise _Skip
         n, m = C2["n"], C2["m"]
         ctx = gpr_amd.Context(local_rank)
         el, infos, st, _ = fit_leg(C2, ctx, 0, np.float64, max(args.steps, 10))
@@ -150,6 +222,8 @@ def run_configs(args, world, rank, local_rank, dctx, max_over_ranks, barrier_syn
                            "unit": "TFLOP/s", "frac": alg / (t_k * 1e-3) / 1e12 / PEAK_FP64_TFLOPS if t_k else None,
                            "avg_launch_us": 1e3 * t_k if t_k else None, "algorithmic_flops_per_launch": alg,
                            "note": "latency-bound: N/128 = 32 serial diagonal steps"}}
+        c2["roofline"]["rocprof"] = rocprof_from_profile("c2", ("potrf_tiles_kernel<double, false>",),
+                                                         c2["roofline"]["avg_launch_us"])
         if rank == 0 and world == 1 and args.cpu_n > 0:
             from oracle import oracle as O
             X, Y = make_data(n, C2["d"], m)
@@ -160,10 +234,14 @@ def run_configs(args, world, rank, local_rank, dctx, max_over_ranks, barrier_syn
                                   "sample": f"1 full fit at N={n} (oracle: kernel loop + LAPACK {O.lapack_name()} "
                                             f"getrf+getri in fp64 + C Y) in {dt:.2f} s"}
         out["C2"] = c2
+    except _Skip:
+        pass
     except Exception as e:
         out["C2"] = {"error": repr(e)}
     # ---- C4: N=32768 d=32 RationalQuadratic fp32 (sharded for N > 1, its BASELINE form) ----------
     try:
+        if not want("c4"):
+            raise _Skip
         n, m = C4["n"], C4["m"]
         steps = max(3, min(args.steps, 5))
         if world > 1 and dctx is not None:
@@ -191,6 +269,10 @@ def run_configs(args, world, rank, local_rank, dctx, max_over_ranks, barrier_syn
                            "frac": alg / (t_k * 1e-3) / 1e12 / peak if t_k else None,
                            "avg_launch_us": 1e3 * t_k if t_k else None, "algorithmic_flops_per_launch": alg},
               "dist": dinfo}
+        if world == 1:
+            c4["roofline"]["rocprof"] = rocprof_from_profile("c4", ("potrf_tiles_kernel<float, false>",),
+                                                             c4["roofline"]["avg_launch_us"])
+            c4["roofline"]["mfma_busy"] = mfma_from_profile("c4", ("potrf_tiles_kernel<float, false>",))
         if rank == 0 and world == 1 and args.cpu_n > 0:
             from oracle import oracle as O
             ns = 8192
@@ -204,10 +286,14 @@ def run_configs(args, world, rank, local_rank, dctx, max_over_ranks, barrier_syn
                                             f"{O.lapack_name()} getrf+getri) in {dt:.2f} s, EXTRAPOLATED cubically "
                                             f"to N={n}"}
         out["C4"] = c4
+    except _Skip:
+        pass
     except Exception as e:
         out["C4"] = {"error": repr(e)}
     # ---- C5: sparse GP M=2048, N=1e6, d=64 fp64 (dense rows sharded over the ranks) ------------
     try:
+        if not want("c5"):
+            raise _Skip
         n, M_, d = 1_000_000, 2048, 64
         ks, sig, jit = "GaussianKernel(3,1,)", 0.1, 1e-4
         X, Y = make_data(n, d, 1)
@@ -243,6 +329,9 @@ def run_configs(args, world, rank, local_rank, dctx, max_over_ranks, barrier_syn
                            "achieved": f_syrk / (t_s * 1e-3) / 1e12 if t_s else None, "peak": PEAK_FP64_TFLOPS,
                            "unit": "TFLOP/s", "frac": f_syrk / (t_s * 1e-3) / 1e12 / PEAK_FP64_TFLOPS if t_s else None,
                            "avg_launch_us": 1e3 * t_s if t_s else None, "algorithmic_flops_per_launch": f_syrk}}
+        if world == 1:
+            c5["roofline"]["rocprof"] = rocprof_from_profile("c5", ("syrk_splitk_kernel<double>",),
+                                                             c5["roofline"]["avg_launch_us"])
         if rank == 0 and world == 1 and args.cpu_n > 0:
             from oracle import oracle as O
             ns = 62500
@@ -255,6 +344,8 @@ def run_configs(args, world, rank, local_rank, dctx, max_over_ranks, barrier_syn
                                             f"M x M LAPACK inverses) in {dt:.2f} s, scaled LINEARLY in N to {n} rows "
                                             "(the M x M part counted 16x: an overestimate of the CPU rate's cost)"}
         out["C5"] = c5
+    except _Skip:
+        pass
     except Exception as e:
         out["C5"] = {"error": repr(e)}
     return out
@@ -282,7 +373,16 @@ def main():
                          "of the headline; rehearsed with two processes on one GPU, DESIGN.md 6)")
     ap.add_argument("--force-dist", action="store_true",
                     help="testing: run the sharded-fit leg (and make it the headline) even at N = 1")
+    ap.add_argument("--legs", default="all",
+                    help="comma list of the legs to run: " + ",".join(LEGS) + " (profiling passes run one leg per "
+                         "process so each rocprof summary holds one configuration: scripts/gpu.sh profile)")
     args = ap.parse_args()
+    legs = None if args.legs == "all" else set(args.legs.split(","))
+    if legs is not None and not legs <= set(LEGS):
+        ap.error(f"unknown legs {sorted(legs - set(LEGS))}")
+
+    def want(leg):
+        return legs is None or leg in legs
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -350,7 +450,7 @@ def main():
 
     # ---- the sharded fit over all ranks (the N > 1 headline) -------------------------------
     dres, dist_error, dctx = None, None, None
-    if world > 1 or args.force_dist:
+    if (world > 1 or args.force_dist) and want("c3"):
         try:
             if shared:
                 from gpr_amd.gprx import torch_allgather
@@ -377,9 +477,14 @@ def main():
     # ---- one independent fit per GPU (the N = 1 headline; the replicas extra for N > 1) -----
     ctx = gpr_amd.Context(local_rank)
     model = make_model(ctx)
-    el_r, infos_r, stats = timed_fits(model, ctx)
-    replicas = {"value": world * args.steps / el_r, "ms_per_step": 1e3 * el_r / args.steps,
-                "scaling": "weak", "fits_per_step": world}
+    if want("c3"):
+        el_r, infos_r, stats = timed_fits(model, ctx)
+        replicas = {"value": world * args.steps / el_r, "ms_per_step": 1e3 * el_r / args.steps,
+                    "scaling": "weak", "fits_per_step": world}
+    else:  # a profiling pass of another leg: one untimed fit for predict / variance
+        if want("predict") or want("variance"):
+            model.fit()
+        el_r, infos_r, stats, replicas = None, [], {}, {"value": None, "ms_per_step": None}
 
     headline_dist = dres is not None and args.mode == "dist" and (world > 1 or args.force_dist)
     if headline_dist:
@@ -392,7 +497,7 @@ def main():
     # predicts its contiguous slice of the Q queries; device time of the fused predict
     # kernels, max over ranks
     pred = None
-    if args.predict_q > 0:
+    if args.predict_q > 0 and want("predict"):
         Xq = make_queries(args.predict_q, d)
         lo, hi = gpr_amd.query_shard(args.predict_q, rank, world)
         model.predict(Xq[lo:hi])
@@ -423,12 +528,14 @@ def main():
             pred["roofline_tree"] = {"bound": "mfma+valu (serial)", "t_roof_ms": 1e3 * t_roof,
                                      "t_device_ms": pms, "frac": 1e3 * t_roof / pms,
                                      "mfma_flop_per_pair": 6.0 * d, "valu_ops_per_pair": 28.0}
+            if world == 1:
+                pred["rocprof"] = rocprof_from_profile("predict", ("predict_mma_kernel<double, 1, true>",), 1e3 * pms)
 
     # posterior variance (GetCredibleInterval, lib/GaussianProcess.cpp:102-114): k(x,x) - |L^{-1} k_x|^2
     # for Qv queries, query-sharded; the forward solve with Qv right-hand sides on the tile GEMM
     # (Qv N^2 flop) dominates.  Wall time of the call (queries up, variances down: small)
     var = None
-    if args.variance_q > 0:
+    if args.variance_q > 0 and want("variance"):
         Xv = make_queries(args.variance_q, d)
         lo, hi = gpr_amd.query_shard(args.variance_q, rank, world)
         model.posterior_cov(Xv[lo:hi], Xv[lo:hi])
@@ -444,7 +551,7 @@ def main():
 
     # log-marginal likelihood + gradient (refit, explicit inverse, fused gradient pass)
     lml = None
-    if args.lml:
+    if args.lml and want("lml"):
         model.lml(grad=True)
         ctx.set_stats(True)
         tl0 = time.perf_counter()
@@ -452,14 +559,15 @@ def main():
         tl = time.perf_counter() - tl0
         ls = ctx.stats()
         ctx.set_stats(False)
-        lml = {"ms_wall": 1e3 * tl, "phases_ms": {k: v["ms"] for k, v in ls.items()}}
+        lml = {"ms_wall": 1e3 * tl, "phases_ms": {k: v["ms"] for k, v in ls.items()},
+               "rocprof": rocprof_table("lml") if world == 1 else None}
 
     # the covariance build alone (north_star asks for its HBM GB/s; in the fit it is fused into
     # the factorisation launch as BUILD tasks): the same BUILD tasks with no other task in the
     # ticket list, features resident, device time by HIP events.  Algorithmic bytes per build
     # (SURVEY.md 8(d)): 8 (n d + n (n + 1) / 2) -- X read once, the lower triangle written once.
     build = None
-    if args.build_iters > 0:
+    if args.build_iters > 0 and want("build"):
         try:
             bms = max_over_ranks(ctx.build_time(cfg["kernel"], X, cfg["sigma"], path=0, iters=args.build_iters))
             bbytes = 8.0 * (n * d + n * (n + 1) / 2)
@@ -476,6 +584,14 @@ def main():
                    + ntile * 128 * 128 * 40.0 / (PEAK_FP64_TFLOPS / 2 * 1e12) + bbytes / (PEAK_HBM_GBS * 1e9))
             build["roofline_tree"] = {"bound": "mfma+valu (serial) + hbm stores", "t_roof_ms": 1e3 * t_b,
                                       "frac": 1e3 * t_b / bms}
+            if world == 1:
+                # the same launch (BUILD tasks only) under rocprof, and its PMC bytes: the twin of
+                # `gbs` measured by counters (L2-fabric bytes, FETCH_SIZE x 2 + WRITE_SIZE)
+                bk = ("potrf_tiles_kernel<double, false>",)
+                build["rocprof"] = rocprof_from_profile("build", bk, 1e3 * bms)
+                tr = traffic_from_profile("build", bk)
+                build["pmc"] = ({"bytes_per_launch": tr["bytes_per_launch"], "source": tr["source"],
+                                 "gbs_pmc": tr["bytes_per_launch"] / (bms * 1e-3) / 1e9} if tr else None)
         except Exception as e:
             log("build timing failed:", e)
 
@@ -496,7 +612,7 @@ def main():
         infos = infos_r
         kname = "potrf_tiles_kernel<double> (persistent tile-dataflow covariance build + Cholesky + forward solve, k_ptiles.hip)"
     peak = PEAK_FP64_TFLOPS * (world if headline_dist else 1)
-    achieved = (alg_flops / (avg_ms * 1e-3) / 1e12) if avg_ms > 0 else 0.0
+    achieved = (alg_flops / (avg_ms * 1e-3) / 1e12) if avg_ms > 0 else None
     phases = {k: {"ms_per_fit": v["ms"] / args.steps, "launches_per_fit": v["launches"] / args.steps,
                   "tflops": (v["flops"] / (v["ms"] * 1e-3) / 1e12) if v["ms"] and v["flops"] else None,
                   "gbs": (v["bytes"] / (v["ms"] * 1e-3) / 1e9) if v["ms"] and v["bytes"] else None}
@@ -504,18 +620,18 @@ def main():
     g_roof = world if headline_dist else 1
     t_roof = fit_roofline_ms(n, d, m, g_roof)
     traffic = traffic_from_profile() if not headline_dist else None
-    fit_ms = float(np.median([i.ms_build + i.ms_factor + i.ms_solve for i in infos]))
+    fit_ms = float(np.median([i.ms_build + i.ms_factor + i.ms_solve for i in infos])) if infos else None
 
     configs = None
     if args.configs:
         configs = run_configs(args, world, rank, local_rank, dctx if dist_error is None else None, max_over_ranks,
-                              barrier_sync)
+                              barrier_sync, want)
     if dctx is not None:
         dctx.close()
 
     if rank == 0:
         cpu = None
-        if world == 1 and args.cpu_n > 0:
+        if world == 1 and args.cpu_n > 0 and want("c3"):
             try:
                 cpu = cpu_baseline(cfg, args.cpu_n)
             except Exception as e:  # the baseline is reported, never required
@@ -541,7 +657,7 @@ def main():
                                        else ("replicas" if world > 1 else "single-gpu"))},
             "roofline": {"bound": "mfma", "kernel": kname,
                          "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
-                         "frac": achieved / peak,
+                         "frac": achieved / peak if achieved else None,
                          "avg_launch_us": 1e3 * avg_ms if avg_ms else None,
                          "algorithmic_flops_per_launch": alg_flops,
                          # L2-fabric bytes per launch from the committed PMC passes (FETCH_SIZE x 2
@@ -549,8 +665,16 @@ def main():
                          # upper bound on HBM bytes), null if none is committed
                          "traffic": (traffic["bytes_per_launch"] if traffic else None),
                          "traffic_kind": "l2_fabric_bytes",
-                         "traffic_source": (traffic["source"] if traffic else None)},
-            "fit_roofline": {"t_roof_ms": t_roof, "gpus": g_roof, "t_fit_device_ms": fit_ms, "frac": t_roof / fit_ms},
+                         "traffic_source": (traffic["source"] if traffic else None),
+                         # the same launch in the committed rocprofv3 summary of the C3 leg, and
+                         # its matrix-pipe busy fraction from the committed PMC pass
+                         "rocprof": (rocprof_from_profile("c3", ("potrf_tiles_kernel<double, false>",),
+                                                          1e3 * avg_ms if avg_ms else None)
+                                     if not headline_dist else None),
+                         "mfma_busy": (mfma_from_profile("c3", ("potrf_tiles_kernel<double, false>",))
+                                       if not headline_dist else None)},
+            "fit_roofline": {"t_roof_ms": t_roof, "gpus": g_roof, "t_fit_device_ms": fit_ms,
+                             "frac": t_roof / fit_ms if fit_ms else None},
             "replicas": replicas if world > 1 else None,
             "dist_error": dist_error,
             "phases": phases,

@@ -156,15 +156,19 @@ template void hostcoll_allreduce_dev<float>(HostColl*, float*, int, hipStream_t)
 // ---------------------------------------------------------------------------------------
 // layout: which rank holds which row block, and where in its packed storage
 // ---------------------------------------------------------------------------------------
+// A rank's storage is one or more PIECES (separate allocations of whole row blocks, each at most
+// piece_elems): only allocations below 2 GiB can be mapped into another process (kIpcMaxBytes).
 struct DistLayout {
     int g = 1, gb = 1, nc = 0, nr = 0, nci = 0;
     bool inv = false;
     std::vector<int> own, loc;            // per row block: owner rank, index among its rows
     std::vector<std::vector<int>> rows;   // per rank: owned row blocks, ascending
-    std::vector<std::vector<int64_t>> roff;  // per rank: element offset of each own row block
-    std::vector<int64_t> elems;           // per rank: storage elements
+    std::vector<std::vector<int64_t>> roff;  // per rank: element offset of each own row block in its piece
+    std::vector<std::vector<int>> piece;     // per rank: the piece of each own row block
+    std::vector<std::vector<int64_t>> pelems;  // per rank: elements of each piece
+    std::vector<int64_t> elems;           // per rank: storage elements (all pieces)
     int ncols(int i) const { return i < nc ? i + 1 : (i == nc ? nc : nc + 1); }
-    void init(int g_, int gb_, int nc_, bool inv_) {
+    void init(int g_, int gb_, int nc_, bool inv_, int64_t piece_elems) {
         g = g_;
         gb = std::max(1, gb_);
         nc = nc_;
@@ -180,15 +184,26 @@ struct DistLayout {
             rows[own[i]].push_back(i);
         }
         roff.assign(g, {});
+        piece.assign(g, {});
+        pelems.assign(g, {});
         elems.assign(g, 0);
         const int64_t DB2 = (int64_t)DB * DB;
         for (int q = 0; q < g; q++) {
             int64_t o = 0;
+            int p = 0;
             for (int i : rows[q]) {
+                const int64_t sz = (int64_t)ncols(i) * DB2;
+                if (o > 0 && o + sz > piece_elems) {  // the next piece
+                    pelems[q].push_back(o);
+                    p++;
+                    o = 0;
+                }
                 roff[q].push_back(o);
-                o += (int64_t)ncols(i) * DB2;
+                piece[q].push_back(p);
+                o += sz;
+                elems[q] += sz;
             }
-            elems[q] = o;
+            pelems[q].push_back(o);
         }
     }
 };
@@ -197,17 +212,15 @@ struct DistLayout {
 // returned on this stack: the sharded LML's 2.19 GB mailbox, a 2.1 GB rank storage at N = 32768)
 constexpr int64_t kIpcMaxBytes = (int64_t(1) << 31) - (int64_t(1) << 20);
 
-// mailbox byte layout (identical on every rank): see PtDist / DSArgs
+// mailbox byte layout (identical on every rank): see PtDist / DSArgs.  The receive window is
+// not in it: its ww x nr tile slots are separate pieces below 2 GiB (WindowLayout)
 struct MailboxLayout {
-    int64_t o_linv = 0, o_win = 0, o_z = 0, o_alpha = 0, o_zf = 0, o_part = 0, o_flags = 0, o_sflags = 0, o_tags = 0,
-            bytes = 0;
+    int64_t o_linv = 0, o_z = 0, o_alpha = 0, o_zf = 0, o_part = 0, o_flags = 0, o_sflags = 0, o_tags = 0, bytes = 0;
     void init(int g, int nc, int nr, int ww, int m, size_t s, bool window) {
         const int64_t DB2 = (int64_t)DB * DB, np = (int64_t)nc * DB;
         int64_t o = 0;
         o_linv = o;
         o = align256(o + (int64_t)nc * DB2 * (int64_t)s);
-        o_win = o;
-        o = align256(o + (window ? (int64_t)ww * nr * DB2 * (int64_t)s : 0));
         o_z = o;
         o = align256(o + (int64_t)nc * DB2 * (int64_t)s);
         o_alpha = o;
@@ -226,17 +239,44 @@ struct MailboxLayout {
     }
 };
 
+// the receive window: slot (b mod ww, row j) = tile s = (b mod ww) nr + j, in piece s / tpp
+struct WindowLayout {
+    int64_t tiles = 0, tpp = 1;
+    int npc = 0;
+    void init(int ww, int nr, size_t s, int64_t piece_bytes, bool window) {
+        tiles = window ? (int64_t)ww * nr : 0;
+        tpp = std::max<int64_t>(1, piece_bytes / ((int64_t)DB * DB * (int64_t)s));
+        npc = (int)((tiles + tpp - 1) / tpp);
+    }
+    int64_t piece_tiles(int p) const { return std::min(tpp, tiles - (int64_t)p * tpp); }
+};
+
 // one rank's buffers and launch state
 template <typename T>
 struct DistRank {
     int r = 0;
     hipStream_t s = nullptr;
-    DMem store, mbox, ctr, info, flag, red, sctl, part, pbuf;
-    DMem t_loc, t_roff, t_own, t_tptr, t_cons, t_need, t_mb, t_orows, t_lastof, t_ctab, pd, list;
+    std::vector<std::unique_ptr<DMem>> store;  // the packed own row blocks, in pieces (DistLayout)
+    std::vector<std::unique_ptr<DMem>> win;    // the receive window, in pieces (WindowLayout)
+    DMem mbox, ctr, info, flag, red, sctl, part, pbuf;
+    DMem t_loc, t_roff, t_own, t_tptr, t_cons, t_need, t_mb, t_wpc, t_orows, t_lastof, t_ctab, pd, list;
     DMem trace;                        // GPRX_DIST_TRACE_FILE: per-ticket timeline of the last launch
     std::vector<uint64_t> mb;          // every rank's mailbox as mapped here
-    std::vector<uint64_t> st;          // every rank's storage as mapped here
+    std::vector<std::vector<uint64_t>> st;  // every rank's storage pieces as mapped here
+    std::vector<std::vector<uint64_t>> wp;  // every rank's window pieces as mapped here
+    std::vector<int64_t> roff;         // own row blocks: element offset from the first piece's base
     std::vector<void*> opened;         // IPC mappings to close
+    T* sbase() const { return store.empty() ? nullptr : store[0]->template as<T>(); }
+    int64_t store_bytes() const {
+        int64_t b = 0;
+        for (auto& p : store) b += (int64_t)p->bytes;
+        return b;
+    }
+    int64_t win_bytes() const {
+        int64_t b = 0;
+        for (auto& p : win) b += (int64_t)p->bytes;
+        return b;
+    }
     std::vector<int> orows;            // own matrix row blocks
     int ntasks = 0;
     hipEvent_t t0 = nullptr, t1 = nullptr;
@@ -260,6 +300,7 @@ struct DistEngine : DistEngineBase {
     HostColl* hc = nullptr;
     DistLayout L;
     MailboxLayout MB;
+    WindowLayout WL;
     DistSched S;
     int64_t key_n = -1;
     int key_m = -1;
@@ -268,7 +309,22 @@ struct DistEngine : DistEngineBase {
     int m = 0;
     unsigned ep = 0, sep = 0;  // epochs of the fits and of the solves (flag values)
     std::vector<std::unique_ptr<DistRank<T>>> ranks;  // virtual: all g; otherwise this process's rank
-    ~DistEngine() override { teardown(); }
+    int* dbg = nullptr;  // GPRX_PT_DEBUG: the launch's per-workgroup status words (pinned host memory)
+    int dbg_n = 0;
+    void free_dbg() {
+        if (!dbg) return;
+        pt_debug_register(dbg, 0);
+        (void)hipHostFree(dbg);
+        dbg = nullptr;
+        dbg_n = 0;
+    }
+    // On a multi-process context the destruction is COLLECTIVE: teardown() ends with a host
+    // all-gather (every process unmaps its peers' allocations before any frees its own), so
+    // every process must destroy its model (or re-key its engine) in the same order
+    ~DistEngine() override {
+        teardown();
+        free_dbg();
+    }
     void teardown() {
         if (!virt && hc && !ranks.empty()) {  // every rank unmaps before any rank frees
             for (auto& R : ranks) {
@@ -285,6 +341,27 @@ struct DistEngine : DistEngineBase {
         ranks.clear();
     }
 };
+
+// Every process of a multi-process context reaches this point before any goes on (a one-int
+// all-gather; a no-op for virtual ranks and one rank).  Used before each sharded launch, so ranks
+// that enter a fit seconds apart (I/O, GC on one of them) do not run into the launch's per-wait
+// time limit, and after a gather that read the peers' storage, before any of them rewrites it.
+template <typename T>
+static void host_barrier(DistEngine<T>& E) {
+    if (E.virt || E.g <= 1) return;
+    int x = 0;
+    std::vector<int> all(E.g);
+    E.hc->allgather(&x, sizeof(int), all.data());
+}
+
+// A status agreed by every process: the minimum over the ranks (INT_MAX = ok).
+template <typename T>
+static int agree_min(DistEngine<T>& E, int v) {
+    if (E.virt || E.g <= 1) return v;
+    std::vector<int> all(E.g);
+    E.hc->allgather(&v, sizeof(int), all.data());
+    return *std::min_element(all.begin(), all.end());
+}
 
 // ---------------------------------------------------------------------------------------
 // small kernels: counters, packed-storage initialisation, the factor gather
@@ -454,23 +531,14 @@ static void setup(DistEngine<T>& E, const DistContext& C, int64_t n, int m, bool
         if (const char* e = std::getenv("GPRX_DIST_WINDOW_MB")) budget = std::atof(e) * 1048576.0;
         const int nrw = nc + 1 + (inv ? nc : 0);
         auto wbytes = [&](int w) { return (double)w * nrw * DB * DB * (double)sizeof(T); };
-        // Separate processes map each other's mailbox through IPC, and hipIpcOpenMemHandle of
-        // a mailbox above 2 GiB never returned (the sharded LML at N = 16384 with a 64-panel
-        // window: 2.19 GB; GPRX_DIST_VERBOSE located it): the window keeps the
-        // mailbox below that
-        const bool ipc = !E.virt;
-        auto mb_bytes = [&](int w) {
-            MailboxLayout ml;
-            ml.init(E.g, nc, nrw, w, m, sizeof(T), true);
-            return ml.bytes;
-        };
+        // (the window is allocated in pieces below 2 GiB, so IPC puts no limit on its width)
         std::vector<int> cws;
         for (int w = 8; w < nc; w *= 2) cws.push_back(w);
         cws.push_back(std::max(2, nc));
         int pick = -1;
         DistSched ps;
         for (int w : cws) {
-            if (pick >= 0 && (wbytes(w) > budget || (ipc && mb_bytes(w) > kIpcMaxBytes))) break;
+            if (pick >= 0 && wbytes(w) > budget) break;
             DistSched c = sim(gb, w);
             if (pick < 0 || c.est_us < 0.995 * ps.est_us) {
                 pick = w;
@@ -492,12 +560,17 @@ static void setup(DistEngine<T>& E, const DistContext& C, int64_t n, int m, bool
     E.gb = gb;
     E.ww = ww;
     E.W = E.S.W;
-    E.L.init(E.g, gb, nc, inv);
+    // allocation pieces: below kIpcMaxBytes when other processes map them (GPRX_DIST_PIECE_MB
+    // forces smaller pieces in every mode, so the split layout runs at test sizes)
+    int64_t piece_bytes = (!E.virt && E.g > 1) ? kIpcMaxBytes : INT64_MAX / 2;
+    if (const char* e = std::getenv("GPRX_DIST_PIECE_MB"))
+        piece_bytes = std::min(piece_bytes, std::max<int64_t>(1, std::atoll(e)) << 20);
+    E.L.init(E.g, gb, nc, inv, piece_bytes / (int64_t)sizeof(T));
     const int nr = E.L.nr, nci = E.L.nci;
     E.MB.init(E.g, nc, nr, ww, m, sizeof(T), E.g > 1);
-    GPRX_REQUIRE(E.virt || E.g == 1 || E.MB.bytes < kIpcMaxBytes, GPRX_ERR_ARG,
-                 "distributed fit: the mailbox would exceed 2 GiB, the largest allocation another process can map "
-                 "(set GPRX_DIST_WINDOW lower)");
+    E.WL.init(ww, nr, sizeof(T), piece_bytes, E.g > 1);
+    GPRX_REQUIRE(E.virt || E.g == 1 || E.MB.bytes <= kIpcMaxBytes, GPRX_ERR_ARG,
+                 "distributed fit: the mailbox would exceed 2 GiB, the largest allocation another process can map");
     const int64_t DB2 = (int64_t)DB * DB;
     // ---- per local rank: buffers -------------------------------------------------------------
     dist_say(C.rank, "setup: schedule done, window", ww);
@@ -509,14 +582,25 @@ static void setup(DistEngine<T>& E, const DistContext& C, int64_t n, int m, bool
         R->s = masked_stream(slot * per, per);
         GPRX_HIP(hipEventCreate(&R->t0));
         GPRX_HIP(hipEventCreate(&R->t1));
-        R->store.alloc(sizeof(T) * (size_t)E.L.elems[r], false);
+        for (int64_t pe : E.L.pelems[r]) {
+            R->store.push_back(std::make_unique<DMem>());
+            R->store.back()->alloc(sizeof(T) * (size_t)pe, false);
+        }
+        R->roff.clear();
+        for (size_t x = 0; x < E.L.rows[r].size(); x++)  // (pieces are 256-byte aligned allocations)
+            R->roff.push_back(((int64_t)R->store[E.L.piece[r][x]]->p - (int64_t)R->store[0]->p) / (int64_t)sizeof(T) +
+                              E.L.roff[r][x]);
         static const bool coarse = std::getenv("GPRX_DIST_COARSE") && std::atoi(std::getenv("GPRX_DIST_COARSE")) != 0;
-        dist_say(C.rank, "setup: store allocated, mailbox bytes", (long long)E.MB.bytes);
+        for (int p = 0; p < E.WL.npc; p++) {
+            R->win.push_back(std::make_unique<DMem>());
+            R->win.back()->alloc(sizeof(T) * (size_t)E.WL.piece_tiles(p) * DB2, !coarse);
+        }
+        dist_say(C.rank, "setup: store and window allocated, mailbox bytes", (long long)E.MB.bytes);
         R->mbox.alloc((size_t)E.MB.bytes, !coarse);
         dist_say(C.rank, "setup: mailbox allocated");
         GPRX_HIP(hipMemset(R->mbox.p, 0, E.MB.bytes));  // flags 0: below every epoch
         dist_say(C.rank, "setup: mailbox cleared");
-        R->ctr.alloc(sizeof(int) * ((size_t)C_NCTL_DIST + nr + (size_t)nr * nci + nc + 4 * (size_t)nc), false);
+        R->ctr.alloc(sizeof(int) * ((size_t)C_NCTL_DIST + nr + (size_t)nr * nci + nc + TP_STRIDE * (size_t)nc), false);
         if (potrf_split_for(std::is_same<T, double>::value, E.P)) R->pbuf.alloc(sizeof(T) * 4 * DB * DB, false);
         R->info.alloc(160 * sizeof(int), false);  // info, then the GPRX_DIST_CHECK counters and log
         GPRX_HIP(hipMemset(R->info.p, 0, 160 * sizeof(int)));
@@ -527,41 +611,59 @@ static void setup(DistEngine<T>& E, const DistContext& C, int64_t n, int m, bool
         E.ranks.push_back(std::move(R));
     }
     // ---- every rank's mailbox and storage as mapped in this process ------------------------------
+    auto own_view = [](const DistRank<T>& Q, std::vector<uint64_t>& st, std::vector<uint64_t>& wp) {
+        st.clear();
+        wp.clear();
+        for (auto& p : Q.store) st.push_back((uint64_t)p->p);
+        for (auto& p : Q.win) wp.push_back((uint64_t)p->p);
+    };
     for (auto& R : E.ranks) {
         R->mb.assign(E.g, 0);
-        R->st.assign(E.g, 0);
+        R->st.assign(E.g, {});
+        R->wp.assign(E.g, {});
     }
     if (E.virt) {
         for (auto& R : E.ranks)
             for (auto& Q : E.ranks) {
                 R->mb[Q->r] = (uint64_t)Q->mbox.p;
-                R->st[Q->r] = (uint64_t)Q->store.p;
+                own_view(*Q, R->st[Q->r], R->wp[Q->r]);
             }
     } else {
         DistRank<T>& R = *E.ranks[0];
         R.mb[R.r] = (uint64_t)R.mbox.p;
-        R.st[R.r] = (uint64_t)R.store.p;
+        own_view(R, R.st[R.r], R.wp[R.r]);
         if (E.g > 1) {
+            // every allocation a peer reads or writes, one IPC handle each, every one below 2 GiB
+            // (hipIpcOpenMemHandle of a larger allocation never returned on this stack: DESIGN.md 6):
+            // [mailbox, window pieces, storage pieces]; the layout (identical on every rank) tells
+            // how many of each a rank has
+            size_t maxsp = 0;
+            for (int q = 0; q < E.g; q++) maxsp = std::max(maxsp, E.L.pelems[q].size());
+            const size_t nh = 1 + (size_t)E.WL.npc + maxsp;
             GPRX_REQUIRE(E.hc, GPRX_ERR_STATE, "distributed fit: no host collective");
-            hipIpcMemHandle_t mine[2];
+            std::vector<hipIpcMemHandle_t> mine(nh);
+            std::memset(mine.data(), 0, sizeof(hipIpcMemHandle_t) * nh);
             GPRX_HIP(hipIpcGetMemHandle(&mine[0], R.mbox.p));
-            GPRX_HIP(hipIpcGetMemHandle(&mine[1], R.store.p));
-            std::vector<hipIpcMemHandle_t> all(2 * (size_t)E.g);
-            dist_say(C.rank, "setup: ipc handles taken");
-            E.hc->allgather(mine, sizeof(mine), all.data());
+            for (int p = 0; p < E.WL.npc; p++) GPRX_HIP(hipIpcGetMemHandle(&mine[1 + p], R.win[p]->p));
+            for (size_t p = 0; p < R.store.size(); p++)
+                GPRX_HIP(hipIpcGetMemHandle(&mine[1 + E.WL.npc + p], R.store[p]->p));
+            std::vector<hipIpcMemHandle_t> all(nh * (size_t)E.g);
+            dist_say(C.rank, "setup: ipc handles taken", (long long)nh);
+            E.hc->allgather(mine.data(), sizeof(hipIpcMemHandle_t) * nh, all.data());
             dist_say(C.rank, "setup: ipc handles exchanged");
+            auto open = [&](const hipIpcMemHandle_t& h) {
+                void* p = nullptr;
+                GPRX_HIP(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
+                R.opened.push_back(p);
+                return (uint64_t)p;
+            };
             for (int q = 0; q < E.g; q++) {
                 if (q == R.r) continue;
-                for (int h = 0; h < 2; h++) {
-                    // hipIpcOpenMemHandle of an allocation above 2 GiB never returns:
-                    // a peer's storage that large is not mapped (only the dense gather reads it)
-                    if (h == 1 && (int64_t)sizeof(T) * E.L.elems[q] >= kIpcMaxBytes) continue;
-                    void* p = nullptr;
-                    GPRX_HIP(hipIpcOpenMemHandle(&p, all[2 * (size_t)q + h], hipIpcMemLazyEnablePeerAccess));
-                    R.opened.push_back(p);
-                    (h == 0 ? R.mb : R.st)[q] = (uint64_t)p;
-                    dist_say(C.rank, "setup: ipc handle opened", 2 * q + h);
-                }
+                const hipIpcMemHandle_t* hq = all.data() + nh * (size_t)q;
+                R.mb[q] = open(hq[0]);
+                for (int p = 0; p < E.WL.npc; p++) R.wp[q].push_back(open(hq[1 + p]));
+                for (size_t p = 0; p < E.L.pelems[q].size(); p++) R.st[q].push_back(open(hq[1 + E.WL.npc + p]));
+                dist_say(C.rank, "setup: ipc handles opened, rank", q);
             }
         }
     }
@@ -579,14 +681,19 @@ static void setup(DistEngine<T>& E, const DistContext& C, int64_t n, int m, bool
         std::vector<uint64_t> tptr((size_t)nr * nc, 0);
         if (E.g > 1)
             for (int j = 0; j < nr; j++)
-                for (int b = 0; b < nc; b++)
-                    tptr[(size_t)j * nc + b] =
-                        R.mb[r] + (uint64_t)(E.MB.o_win + ((int64_t)(b % ww) * nr + j) * DB2 * (int64_t)sizeof(T));
+                for (int b = 0; b < nc; b++) {
+                    const int64_t t = (int64_t)(b % ww) * nr + j;
+                    tptr[(size_t)j * nc + b] = R.wp[r][t / E.WL.tpp] + (uint64_t)((t % E.WL.tpp) * DB2 * (int64_t)sizeof(T));
+                }
+        std::vector<uint64_t> wpc((size_t)E.g * std::max(1, E.WL.npc), 0);  // every rank's window pieces
+        for (int q = 0; q < E.g; q++)
+            for (int p = 0; p < E.WL.npc; p++) wpc[(size_t)q * E.WL.npc + p] = R.wp[q][p];
         R.orows.clear();
         for (int i : E.L.rows[r])
             if (i < nc) R.orows.push_back(i);
         upload_vec(R.t_loc, loc);
-        upload_vec(R.t_roff, E.L.roff[r]);
+        upload_vec(R.t_roff, R.roff);
+        upload_vec(R.t_wpc, wpc);
         upload_vec(R.t_own, E.L.own);
         upload_vec(R.t_tptr, tptr);
         upload_vec(R.t_cons, E.S.cons);
@@ -604,8 +711,7 @@ static void setup(DistEngine<T>& E, const DistContext& C, int64_t n, int m, bool
                 const int i = nc + 1 + a;
                 if (E.L.own[i] != r) continue;
                 for (int c = 0; c <= a; c++)
-                    ctab[(size_t)a * nc + c] = (uint64_t)(R.store.template as<T>() + E.L.roff[r][E.L.loc[i]] +
-                                                          (int64_t)(nc - a + c) * DB2);
+                    ctab[(size_t)a * nc + c] = (uint64_t)(R.sbase() + R.roff[E.L.loc[i]] + (int64_t)(nc - a + c) * DB2);
             }
             upload_vec(R.t_ctab, ctab);
         }
@@ -636,7 +742,9 @@ static PtDist<T> make_ptdist(const DistEngine<T>& E, const DistRank<T>& R) {
     pd.ucnt = R.ctr.template as<int>() + C_NCTL_DIST + E.L.nr + (size_t)E.L.nr * E.L.nci;
     pd.mb = R.t_mb.template as<uint64_t>();
     pd.o_linv = E.MB.o_linv;
-    pd.o_win = E.MB.o_win;
+    pd.wpc = R.t_wpc.template as<uint64_t>();
+    pd.tpp = E.WL.tpp;
+    pd.npc = E.WL.npc;
     pd.o_z = E.MB.o_z;
     pd.o_flags = E.MB.o_flags;
     pd.o_tags = E.MB.o_tags;
@@ -664,7 +772,7 @@ static DSArgs<T> make_dsargs(const DistEngine<T>& E, const DistRank<T>& R) {
     a.own = R.t_own.template as<int>();
     a.loc = R.t_loc.template as<int>();
     a.roff = R.t_roff.template as<int64_t>();
-    a.store = R.store.template as<T>();
+    a.store = R.sbase();
     a.orows = R.t_orows.template as<int>();
     a.nown = (int)R.orows.size();
     a.last_of = R.t_lastof.template as<int>();
@@ -710,17 +818,17 @@ void dist_fit(DistEngineBase*& eng, const DistContext& C, const DistFitIn<T>& in
         DistRank<T>& R = *E.ranks[v];
         const int r = R.r;
         hipStream_t s = R.s;
-        const size_t nctr = (size_t)C_NCTL_DIST + nr + (size_t)nr * nci + nc + 4 * (size_t)nc;  // + TPART states
+        const size_t nctr = (size_t)C_NCTL_DIST + nr + (size_t)nr * nci + nc + TP_STRIDE * (size_t)nc;  // + split-step states
         GPRX_HIP(hipMemsetAsync(R.ctr.p, 0, sizeof(int) * nctr, s));
         int* lcnt = R.ctr.template as<int>() + C_NCTL_DIST;
         hipLaunchKernelGGL(dist_init_counters, dim3((unsigned)nr), dim3(256), 0, s, lcnt, lcnt + nr, nc, nr, nci,
                            fused ? 1 : 0);
         GPRX_HIP(hipMemsetD32Async((hipDeviceptr_t)R.info.p, INT_MAX, 1, s));
         GPRX_HIP(hipMemsetAsync(R.flag.p, 0, sizeof(int), s));
-        T* A = R.store.template as<T>();
+        T* A = R.sbase();
         for (int x = 0; x < (int)E.L.rows[r].size(); x++) {
             const int i = E.L.rows[r][x];
-            T* base = A + E.L.roff[r][x];
+            T* base = A + R.roff[x];
             if (i == nc) {  // the label rows: Y^T as row block nc (DB x np, ld DB)
                 launch_label_rows<T>(in.Y, n, in.m, base, DB, 0, np, GT, s);
             } else if (i > nc) {  // identity row block of the inverse (LML mode)
@@ -778,16 +886,14 @@ void dist_fit(DistEngineBase*& eng, const DistContext& C, const DistFitIn<T>& in
         Lc.dbg = nullptr;
         static const bool dbg_on = std::getenv("GPRX_PT_DEBUG") != nullptr;
         if (dbg_on && E.ranks.size() == 1) {  // {ticket, phase, i, j} per workgroup, read by gprx_dev_pt_debug
-            static int* hd = nullptr;
-            static int hn = 0;
-            if (hn < E.P) {
-                if (hd) (void)hipHostFree(hd);
-                GPRX_HIP(hipHostMalloc((void**)&hd, sizeof(int) * 4 * E.P, hipHostMallocCoherent));
-                hn = E.P;
+            if (E.dbg_n < E.P) {
+                E.free_dbg();
+                GPRX_HIP(hipHostMalloc((void**)&E.dbg, sizeof(int) * 4 * E.P, hipHostMallocCoherent));
+                E.dbg_n = E.P;
             }
-            std::memset(hd, 0xff, sizeof(int) * 4 * E.P);
-            pt_debug_register(hd, E.P);
-            Lc.dbg = hd;
+            std::memset(E.dbg, 0xff, sizeof(int) * 4 * E.P);
+            pt_debug_register(E.dbg, E.P);
+            Lc.dbg = E.dbg;
         }
         Lc.trace = nullptr;
         Lc.split = potrf_split_for(std::is_same<T, double>::value, E.P) ? 1 : 0;
@@ -799,6 +905,9 @@ void dist_fit(DistEngineBase*& eng, const DistContext& C, const DistFitIn<T>& in
             Lc.trace = R.trace.template as<long long>();
         }
     }
+    // every process has prepared its storage: the persistent launches start together (a rank's
+    // waits on its peers' pushes are time-limited per wait, the processes' arrival is not)
+    host_barrier(E);
     // every rank's persistent launch back to back, nothing that could block in between
     dist_say(C.rank, "fit: launching");
     for (size_t v = 0; v < E.ranks.size(); v++) {
@@ -898,10 +1007,11 @@ void dist_fit(DistEngineBase*& eng, const DistContext& C, const DistFitIn<T>& in
     for (auto& Rp : E.ranks) {
         float ms = 0;
         if (hipEventElapsedTime(&ms, Rp->t0, Rp->t1) == hipSuccess) out.ms_kernel = std::max(out.ms_kernel, (double)ms);
-        const int64_t b = (int64_t)(Rp->store.bytes + Rp->mbox.bytes + Rp->ctr.bytes + Rp->part.bytes + Rp->pbuf.bytes + Rp->t_tptr.bytes +
+        const int64_t b = Rp->store_bytes() + Rp->win_bytes() +
+                          (int64_t)(Rp->mbox.bytes + Rp->ctr.bytes + Rp->part.bytes + Rp->pbuf.bytes + Rp->t_tptr.bytes +
                                     Rp->t_cons.bytes + Rp->t_need.bytes + Rp->list.bytes + Rp->t_ctab.bytes);
         out.bytes_rank = std::max(out.bytes_rank, b);
-        out.bytes_storage = std::max(out.bytes_storage, (int64_t)Rp->store.bytes);
+        out.bytes_storage = std::max(out.bytes_storage, Rp->store_bytes());
     }
     if (tot.info != INT_MAX || tot.flag) return;  // the caller reports it
     // ---- alpha = L^{-T} z: the distributed back substitution ---------------------------------
@@ -924,6 +1034,7 @@ void dist_fit(DistEngineBase*& eng, const DistContext& C, const DistFitIn<T>& in
         GPRX_HIP(hipStreamSynchronize(Rp->s));
         hinfo = std::min(hinfo, hi);
     }
+    hinfo = agree_min(E, hinfo);  // every process reports the same outcome
     out.ms_solve = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts0).count();
     if (hinfo != INT_MAX) {
         out.info = -1;
@@ -943,6 +1054,7 @@ void dist_solve(DistEngineBase* eng, const T* rhs, T* out, hipStream_t s) {
     GPRX_REQUIRE(Ep && !Ep->ranks.empty(), GPRX_ERR_STATE, "distributed solve: no factor");
     DistEngine<T>& E = *Ep;
     GPRX_HIP(hipStreamSynchronize(s));  // rhs written on the caller's stream
+    host_barrier(E);                    // as before a fit: the ranks' solve launches start together
     E.sep++;
     for (auto& Rp : E.ranks) {
         GPRX_HIP(hipMemsetAsync(Rp->sctl.p, 0, sizeof(int) * 8, Rp->s));
@@ -966,7 +1078,7 @@ void dist_solve(DistEngineBase* eng, const T* rhs, T* out, hipStream_t s) {
         GPRX_HIP(hipStreamSynchronize(Rp->s));
         hinfo = std::min(hinfo, hi);
     }
-    if (hinfo != INT_MAX) throw Error{GPRX_ERR_HIP, "gprx: distributed solve timed out (flag wait)"};
+    if (agree_min(E, hinfo) != INT_MAX) throw Error{GPRX_ERR_HIP, "gprx: distributed solve timed out (flag wait)"};
     const DistRank<T>& R0 = *E.ranks[0];
     copy_from_mailbox<T>(R0.mbox.template as<char>() + E.MB.o_alpha, out, E.np * E.m, s);
 }
@@ -986,12 +1098,9 @@ void dist_gather_factor(DistEngineBase* eng, T* A, int64_t ld, T* Linv, hipStrea
     const int64_t DB2 = (int64_t)DB * DB;
     std::vector<uint64_t> src((size_t)nc * nc, 0);
     for (int i = 0; i < nc; i++) {
-        const int q = E.L.own[i];
-        GPRX_REQUIRE(R0.st[q] != 0, GPRX_ERR_STATE,
-                     "distributed fit: the dense factor gather needs every rank's storage mapped, and a rank's "
-                     "storage above 2 GiB cannot be mapped across processes");
-        for (int j = 0; j < i; j++)
-            src[(size_t)i * nc + j] = R0.st[q] + sizeof(T) * (uint64_t)(E.L.roff[q][E.L.loc[i]] + (int64_t)j * DB2);
+        const int q = E.L.own[i], x = E.L.loc[i];
+        const uint64_t base = R0.st[q][E.L.piece[q][x]];  // the piece of row block i, as mapped here
+        for (int j = 0; j < i; j++) src[(size_t)i * nc + j] = base + sizeof(T) * (uint64_t)(E.L.roff[q][x] + (int64_t)j * DB2);
     }
     DMem tab;
     upload_vec(tab, src);
@@ -1002,6 +1111,7 @@ void dist_gather_factor(DistEngineBase* eng, T* A, int64_t ld, T* Linv, hipStrea
     copy_from_mailbox<T>(R0.mbox.template as<char>() + E.MB.o_linv, Linv, (int64_t)nc * DB2, s);
     GPRX_HIP(hipStreamSynchronize(s));
     GPRX_HIP(hipGetLastError());
+    host_barrier(E);  // no peer rewrites its storage (the next fit) while this process still reads it
 }
 template void dist_gather_factor<double>(DistEngineBase*, double*, int64_t, double*, hipStream_t);
 template void dist_gather_factor<float>(DistEngineBase*, float*, int64_t, float*, hipStream_t);

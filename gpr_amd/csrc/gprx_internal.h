@@ -413,6 +413,11 @@ struct TileBuild {
     int* flag;
     int mode;
 };
+// Per diagonal block k, TP_STRIDE state words of the split diagonal step (k_ptiles.hip): [0..3]
+// TPART(k, p)'s phase, [TP_DPAN] DIAGX(k)'s published panels (the progressive TPART(k + 1, .)
+// follow it)
+constexpr int TP_STRIDE = 8, TP_DPAN = 4;
+
 // Distributed tile factorisation (k_ptiles.hip, potrf_tiles_kernel<T, true>; gprx_dist.cpp):
 // this rank's view of a factorisation whose row blocks are dealt over g ranks in groups of gb
 // (row block i on rank (i / gb) mod g).  Device copy, read per task.
@@ -424,9 +429,9 @@ struct TileBuild {
 //
 // Exchange: no host in the loop.  Every rank has a MAILBOX (one device allocation, the same
 // byte offsets on every rank, mapped into every peer: the same process for virtual ranks,
-// hipIpcOpenMemHandle across processes).  A producing task pushes its final tile straight into
-// the window slot of each rank that consumes the row -- slot (b mod ww, row j) -- and raises that
-// rank's per-tile flag; a diagonal task pushes Linv_k into every rank's Linv array.  Flags hold
+// hipIpcOpenMemHandle across processes) and a receive WINDOW (pieces below 2 GiB, mapped the
+// same way).  A producing task pushes its final tile straight into the window slot of each rank
+// that consumes the row -- slot (b mod ww, row j) -- and raises that rank's per-tile flag; a diagonal task pushes Linv_k into every rank's Linv array.  Flags hold
 // the fit's epoch (no reset between fits).  A window slot is reused for panel b + ww only after
 // every consumer released panel b: a rank counts its completed window-reading updates per panel
 // (ucnt) and, at the last one, stores its release flag into every peer's mailbox.
@@ -443,8 +448,13 @@ struct PtDist {
     const int* need;           // [g * nc] window-reading update chunks of rank q covering panel p
     int* ucnt;                 // [nc] this rank's completed window-reading chunks per panel (local)
     const uint64_t* mb;        // [g] mailbox base of every rank (as mapped in this process)
+    // the receive windows: slot (b mod ww, row j) is tile t = (b mod ww) nr + j of rank q's window,
+    // in its piece t / tpp (allocations below 2 GiB: IPC-mappable) at tile t mod tpp
+    const uint64_t* wpc;       // [g * npc] window piece bases of every rank (as mapped here)
+    int64_t tpp;               // tiles per window piece
+    int npc;                   // window pieces per rank
     // mailbox byte offsets (the same on every rank)
-    int64_t o_linv, o_win, o_z, o_flags;
+    int64_t o_linv, o_z, o_flags;
     int64_t o_tags;            // GPRX_DIST_CHECK: per window slot (panel, row) the tag of its occupant
     int check;                 // GPRX_DIST_CHECK: verify every window read against the slot's tag
     int wt;                    // pushes cross devices: written-through (sc0 sc1) stores, no L2 write-back fence
@@ -478,7 +488,7 @@ struct DistLaunch {
     long long* trace;  // optional: 4 * (ntasks + 2 nc) words, as GPRX_PT_TRACE (k_ptiles.hip)
     int split;         // the split diagonal step (f64): TPART tasks in the list
     T* pbuf;           // [4][DB x DB] the TPART products
-    int* tflag;        // [nc][4] TPART states (zeroed per fit with the counters)
+    int* tflag;        // [nc][TP_STRIDE] split-step states (zeroed per fit with the counters)
 };
 // The simulated schedule of a distributed factorisation: per-rank ticket lists (in start
 // order of one list-schedule simulation of all ranks, window flow control included), the
@@ -493,9 +503,10 @@ struct DistSched {
 };
 DistSched potrf_dist_schedule(int nc, int g, int gb, int ww, int P, bool build, bool inv, int ratio = 0, bool f64 = true,
                               int tail = 0);
-bool potrf_split_for(bool f64, int P);
-// GPRX_PT_DEBUG: the per-workgroup status words gprx_dev_pt_debug reads (k_ptiles.hip)
-void pt_debug_register(int* dbg, int n);  // the split diagonal step is on (this precision, P workgroups)
+bool potrf_split_for(bool f64, int P);  // the split diagonal step is on (this precision, P workgroups)
+// GPRX_PT_DEBUG: the per-workgroup status words gprx_dev_pt_debug reads (k_ptiles.hip);
+// n = 0 unregisters dbg (if registered)
+void pt_debug_register(int* dbg, int n);
 template <typename T>
 void potrf_tiles_dist_launch(const DistLaunch<T>& L);
 

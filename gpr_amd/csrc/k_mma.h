@@ -72,6 +72,22 @@ struct Stage {
     static constexpr int GRP = BKS / CPI;        // instructions per operand per stage
     static constexpr int IPW = 2 * GRP / 8;      // instructions per wave per stage
     static constexpr int STG = 2 * GRP * SRP;    // elements per stage buffer (A slots, then B)
+    // f32 (two columns per instruction): the second column of a pair is stored rotated by ROT
+    // rows.  The fragment reads are ds_read_b32 (banks (a/4) mod 32, lanes 0-31 one group):
+    // lanes with lk = 0 and lk = 1 read k-columns kr and kr + 1 of one pair, 128 words apart --
+    // the same banks, a 2-way conflict on every f32 fragment read; rotated, the two halves of the
+    // group land 16 banks apart
+    static constexpr int ROT = CPI == 2 ? 16 : 0;
+    // row of the operand column that lane `lane`'s 16-B load brings (its LDS position is fixed)
+    __device__ static inline int src_row(int lane) {
+        const int lcol = lane / LPC, lrow = (lane % LPC) * E;
+        return ROT ? (lrow + GT - ROT * lcol) & (GT - 1) : lrow;
+    }
+    // LDS element of row r of k-column kr of a stage's operand
+    __device__ static inline int at(int kr, int r) {
+        const int c = kr % CPI;
+        return (kr / CPI) * SRP + c * GT + (ROT ? ((r + ROT * c) & (GT - 1)) : r);
+    }
 };
 
 template <typename T>
@@ -132,7 +148,7 @@ __device__ __forceinline__ void tile_mma(typename Mfma<T>::acc_t (&acc)[2][4], c
     int wr, wc;
     wave_block<MAP>(w, wr, wc);
     const int lr = lane & 15, lk = lane >> 4;
-    const int lcol = lane / S::LPC, lrow = (lane % S::LPC) * S::E;
+    const int lcol = lane / S::LPC, lrow = S::src_row(lane);
     // Bpan: the K / 128 <= 64 panel addresses, lane l holding panel l's, loaded ONCE here.  (A
     // load of the address inside issue() made every stage's issue wait -- readfirstlane needs
     // the value, and vmcnt counts in order -- for all the staging loads still in flight: the
@@ -210,11 +226,10 @@ __device__ __forceinline__ void tile_mma(typename Mfma<T>::acc_t (&acc)[2][4], c
             T fa[2][4], fb[2][2];
             auto frag = [&](int kq, int r) {
                 const int kr = kq * 4 + lk;
-                const int ko = (kr / S::CPI) * S::SRP + (kr % S::CPI) * GT;
 #pragma unroll
-                for (int x = 0; x < 2; x++) fb[r][x] = b[ko + wc * 32 + x * 16 + lr];
+                for (int x = 0; x < 2; x++) fb[r][x] = b[S::at(kr, wc * 32 + x * 16 + lr)];
 #pragma unroll
-                for (int y = 0; y < 4; y++) fa[r][y] = a[ko + wr * 64 + y * 16 + lr];
+                for (int y = 0; y < 4; y++) fa[r][y] = a[S::at(kr, wr * 64 + y * 16 + lr)];
             };
             frag(0, 0);
 #pragma unroll
@@ -245,7 +260,7 @@ __device__ __forceinline__ void ring_issue(const T* __restrict__ A, int64_t lda,
                                            int st, T* smem, const int t) {
     typedef Stage<T> S;
     const int lane = t & 63, w = t >> 6;
-    const int lcol = lane / S::LPC, lrow = (lane % S::LPC) * S::E;
+    const int lcol = lane / S::LPC, lrow = S::src_row(lane);
     T* buf = smem + (st % NBUF) * S::STG;
 #pragma unroll
     for (int u = 0; u < S::IPW; u++) {
@@ -303,11 +318,10 @@ __device__ __forceinline__ void tile_mma2(typename Mfma<T>::acc_t (&acc1)[2][4],
             T fa[2][4], fb[2][2];
             auto frag = [&](int kq, int r) {
                 const int kr = kq * 4 + lk;
-                const int ko = (kr / S::CPI) * S::SRP + (kr % S::CPI) * GT;
 #pragma unroll
-                for (int x = 0; x < 2; x++) fb[r][x] = b[ko + wc * 32 + x * 16 + lr];
+                for (int x = 0; x < 2; x++) fb[r][x] = b[S::at(kr, wc * 32 + x * 16 + lr)];
 #pragma unroll
-                for (int y = 0; y < 4; y++) fa[r][y] = a[ko + wr * 64 + y * 16 + lr];
+                for (int y = 0; y < 4; y++) fa[r][y] = a[S::at(kr, wr * 64 + y * 16 + lr)];
             };
             frag(0, 0);
 #pragma unroll

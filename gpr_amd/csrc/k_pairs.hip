@@ -167,7 +167,7 @@ __global__ __launch_bounds__(NT) void predict_mma_kernel(const KCanon<T>* __rest
     const int nblk = (int)((n + GT - 1) / GT);
     const int NS1 = __builtin_amdgcn_readfirstlane(Kr) / BKS, NS = NS1 + __builtin_amdgcn_readfirstlane(Kp) / BKS;
     const int64_t total = (int64_t)nblk * NS;
-    const int lcol = lane / S::LPC, lrow = (lane % S::LPC) * S::E;
+    const int lcol = lane / S::LPC, lrow = S::src_row(lane);
     auto issue = [&](int64_t gs) {  // global stage gs: block gs / NS, k-columns (gs % NS) BKS ..
         const int jb = (int)(gs / NS), sx = (int)(gs % NS);
         T* buf = smem + (gs % NBUF) * S::STG;
@@ -214,11 +214,10 @@ __global__ __launch_bounds__(NT) void predict_mma_kernel(const KCanon<T>* __rest
             T fa[2][4], fb[2][2];
             auto frag = [&](int kq, int r) {
                 const int kr = kq * 4 + lk;
-                const int ko = (kr / S::CPI) * S::SRP + (kr % S::CPI) * GT;
 #pragma unroll
-                for (int x = 0; x < 2; x++) fb[r][x] = b[ko + wc * 32 + x * 16 + lr];
+                for (int x = 0; x < 2; x++) fb[r][x] = b[S::at(kr, wc * 32 + x * 16 + lr)];
 #pragma unroll
-                for (int y = 0; y < 4; y++) fa[r][y] = a[ko + wr * 64 + y * 16 + lr];
+                for (int y = 0; y < 4; y++) fa[r][y] = a[S::at(kr, wr * 64 + y * 16 + lr)];
             };
             frag(0, 0);
 #pragma unroll

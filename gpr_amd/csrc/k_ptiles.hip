@@ -135,6 +135,8 @@ __device__ __forceinline__ void tile_gemm(T* __restrict__ C, int64_t ldc, const 
 constexpr int SPL = DB + 4;
 constexpr int SIL = DB + 2;
 
+__device__ __forceinline__ void st_agent(int* p, int v);  // (hand-off helpers, below)
+
 // v_rsq_f64 (relative error ~2^-23) refined by ONE Halley step, y (1 + e/2 + 3e^2/8) with
 // e = 1 - x y^2 (cubic convergence: error ~2^-69 before rounding): 4 dependent f64 operations
 // after the rsq against the 6 of two Newton steps -- the pivot chain is latency-bound
@@ -884,15 +886,29 @@ __device__ __forceinline__ void la_store_linv_rows(T* __restrict__ Linv, const T
     }
 }
 
-// F(p)'s side phase, waves wlo..7: the stores of what panel p-1 finished (L panel p-1, Linv
-// row block p-2), then the jobs -- Linv row block p-1 (2 (p-1) units), at p = 3 also the
+// Dinv_q = L_qq^{-1} (the 32 x 32 diagonal block q of Linv, lower, zeros above) into Linv: the
+// progressive TPART(k + 1, .) read it as soon as DIAGX(k)'s panel counter says so (the full row
+// block q of Linv follows later with the same values)
+template <typename T>
+__device__ __forceinline__ void la_store_dinv(T* __restrict__ Linv, const T* __restrict__ sS, const T* __restrict__ sDi,
+                                              int q, int tid, int nth) {
+    for (int e = tid; e < 32 * 32; e += nth) {
+        const int r = 32 * q + (e & 31), c = 32 * q + (e >> 5);
+        st_sc1(Linv + r + c * DB, linv_at(sS, sDi, r, c));
+    }
+}
+
+// F(p)'s side phase, waves wlo..7: the stores of what panel p-1 finished (L panel p-1, with pan
+// also Dinv_{p-1}, Linv row block p-2), then the jobs -- Linv row block p-1 (2 (p-1) units), at p = 3 also the
 // partial sums of Linv row block 3 over kb < 2 (4 units), then the far trailing tiles of panel
 // p-1 (C >= 2p + 2, R >= C)
 template <typename T>
 __device__ __forceinline__ void la_side(T* __restrict__ A, int64_t ld, T* __restrict__ Linv, T* __restrict__ sS,
-                                        const T* __restrict__ sDi, int p, int t, int w, int wlo, int lr, int lk) {
+                                        const T* __restrict__ sDi, int p, int t, int w, int wlo, int lr, int lk,
+                                        bool dinv) {
     const int nth = NT - 64 * wlo, tid = t - 64 * wlo;
     la_store_lpanel<T>(A, ld, sS, p - 1, tid, nth);
+    if (dinv) la_store_dinv<T>(Linv, sS, sDi, p - 1, tid, nth);
     if (p >= 2) la_store_linv_rows<T>(Linv, sS, sDi, p - 2, tid, nth);
     const int pl = p - 1, nl = 2 * pl, np3 = (p == 3) ? 4 : 0;
     const int cmin = 2 * p + 2, nc = 8 - cmin, nt = nc > 0 ? nc * (nc + 1) / 2 : 0;
@@ -915,10 +931,13 @@ __device__ __forceinline__ void la_side(T* __restrict__ A, int64_t ld, T* __rest
 }
 
 // from_lds: the block is already in the LDS image (diagx_ts left the syrk result there)
+// pan (optional): the panel counter -- after F(p), p = 1..3, *pan = p: L panels 0..p-1 and
+// Dinv_0..Dinv_{p-1} are stored (write-through); Dinv_3 right after F(3): *pan = 4
 template <typename T>
 __device__ __forceinline__ void diag_factor_la(T* __restrict__ A, int64_t ld, T* __restrict__ Linv,
                                                int* __restrict__ info, int64_t col0, unsigned char* smem_raw,
-                                               const int t, long long* prof = nullptr, bool from_lds = false) {
+                                               const int t, long long* prof = nullptr, bool from_lds = false,
+                                               int* pan = nullptr) {
     typedef Mfma<T> Tr;
     typedef typename Tr::acc_t acc_t;
     constexpr int SL = SIL;
@@ -950,9 +969,11 @@ __device__ __forceinline__ void diag_factor_la(T* __restrict__ A, int64_t ld, T*
             fact32<T>(sS, sDi, c0, fail, prof ? prof + 4 : nullptr);
             if (prof) pfw += wall_clock64() - tf0;
         } else if (p > 0) {
-            la_side<T>(A, ld, Linv, sS, sDi, p, t, w, 1, lr, lk);
+            la_side<T>(A, ld, Linv, sS, sDi, p, t, w, 1, lr, lk, pan != nullptr);
+            if (pan) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the panel's stores drained
         }
         __syncthreads();
+        if (pan && p > 0 && w == 0) st_agent(pan, p);
         if (prof) {
             const long long tn = wall_clock64();
             pf += tn - tf0;
@@ -1055,6 +1076,11 @@ __device__ __forceinline__ void diag_factor_la(T* __restrict__ A, int64_t ld, T*
         const int j = w >> 1;
         la_linv_unit<T>(sS, sDi, 3, j, w & 1, 2, 3, (j < 2 ? LA_LOAD : 0) | LA_FINISH, lr, lk);
     } else {
+        if (pan && w == 6) {  // Dinv_3 first: the progressive parts' last input
+            la_store_dinv<T>(Linv, sS, sDi, 3, lane, 64);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            st_agent(pan, 4);
+        }
         la_store_lpanel<T>(A, ld, sS, 3, t - 384, 128);
         la_store_linv_rows<T>(Linv, sS, sDi, 2, t - 384, 128);
     }
@@ -1068,6 +1094,12 @@ __device__ __forceinline__ void diag_factor_la(T* __restrict__ A, int64_t ld, T*
     }
 }
 
+// GPRX_TP_LINV (A/B builds): the parts wait for the whole Linv_{k-1} (the round-3 form)
+#ifdef GPRX_TP_LINV
+__host__ __device__ constexpr bool tp_linv_form() { return true; }
+#else
+__host__ __device__ constexpr bool tp_linv_form() { return false; }
+#endif
 #ifdef GPRX_NO_SPLIT  // (A/B builds: the split diagonal step compiled out)
 constexpr bool SPLIT_CODE = false;
 #else
@@ -1089,13 +1121,13 @@ template <typename T>
 __device__ __noinline__ void diag_factor(T* __restrict__ A, int64_t ld, T* __restrict__ Linv, int* __restrict__ info,
                                          int64_t col0, unsigned char* smem_raw, const int t, int* dbg = nullptr,
                                          long long* prof = nullptr, bool from_lds = false, int* pub = nullptr,
-                                         int pub_v = 0) {
+                                         int pub_v = 0, int* pan = nullptr) {
     // f64: the blocked factor with look-ahead (diag_factor_la: 43 us per block in isolation
     // against 50.6 for the rank-8 image, scripts/diag_bench.py); its stores are write-through
     // (sc1), so the publication needs no release fence.  f32 (and GPRX_DIAG_RANK8): the
     // rank-8 register image, plain stores and the release fence.
     constexpr bool la = std::is_same<T, double>::value && DIAG_LA;
-    if constexpr (la) diag_factor_la<T>(A, ld, Linv, info, col0, smem_raw, t, prof, from_lds);
+    if constexpr (la) diag_factor_la<T>(A, ld, Linv, info, col0, smem_raw, t, prof, from_lds, pan);
     else diag_factor_rank8<T>(A, ld, Linv, info, col0, smem_raw, t, dbg, prof);
     if (pub) publish(pub, pub_v, !la);
 }
@@ -1208,7 +1240,8 @@ struct Args {
     // quarters; DIAGX(k) copies S and factors it (diagx_split)
     int split;
     T* pbuf;     // DB x DB: S, its lower tiles written by the four parts
-    int* tflag;  // [nc][4] TPART(k, p) state: 1 its A operand is read, 2 its T stored, 3 its S quarter stored
+    int* tflag;  // [nc][TP_STRIDE] TPART(k, p) state: 1 its A operand is read, 2 its T stored, 3 its S quarter
+                 // stored; [TP_DPAN] DIAGX(k)'s published panels
 };
 
 
@@ -1266,6 +1299,15 @@ __device__ __forceinline__ unsigned* dist_flags(const PtDist<T>& D, int q) {
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b), hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
     return reinterpret_cast<unsigned*>(((uint64_t)hi << 32) | lo);
 }
+// window slot t (= (b mod ww) nr + j) of rank q
+template <typename T>
+__device__ __forceinline__ char* dist_win(const PtDist<T>& D, int q, int64_t t) {
+    const int64_t tpp = D.tpp;
+    const int64_t pc = t / tpp;
+    const uint64_t b = D.wpc[(int64_t)q * D.npc + pc] + (uint64_t)((t - pc * tpp) * DB * DB * (int64_t)sizeof(T));
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b), hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+    return reinterpret_cast<char*>(((uint64_t)hi << 32) | lo);
+}
 template <typename T>
 __device__ __forceinline__ char* dist_mb(const PtDist<T>& D, int q, int64_t off) {
     const uint64_t b = D.mb[q] + (uint64_t)off;
@@ -1307,7 +1349,8 @@ __device__ bool dist_wait_release(const Args<T>& a, const PtDist<T>& D, unsigned
 
 // The whole workgroup: copy one DB x DB tile (contiguous, written by this workgroup and
 // drained: its stores are visible to this CU) to byte offset `off` of the mailbox of every
-// rank in `mask`, then set each one's flag word `fidx` to the epoch.  Across devices (D.wt) the
+// rank in `mask` (off < 0: to window slot tag_idx), then set each one's flag word `fidx` to the
+// epoch.  Across devices (D.wt) the
 // copies are 16-byte `sc0 sc1` stores (written through to the destination, not left dirty in
 // this XCD's L2), so the flag needs only every wave's s_waitcnt vmcnt(0) and a barrier -- no
 // buffer_wbl2, which would write back every dirty line of the XCD's L2 (the update tasks'
@@ -1331,7 +1374,7 @@ __device__ void dist_push(const T* src, const PtDist<T>& D, unsigned mask, int64
         for (int u = 0; u < CH; u++) v[u] = s4[t + (c + u) * NT];
         for (int q = 0; q < D.g; q++) {
             if (!((mask >> q) & 1)) continue;
-            u4* d4 = reinterpret_cast<u4*>(dist_mb(D, q, off));
+            u4* d4 = reinterpret_cast<u4*>(off < 0 ? dist_win(D, q, tag_idx) : dist_mb(D, q, off));
             if (wt) {
 #pragma unroll
                 for (int u = 0; u < CH; u++)
@@ -1754,10 +1797,105 @@ __device__ bool tpart_wait_flags(const TpCtx<T>& a, const int* f, int n, int wan
 // Out of line, one body for every p: inlined into the task loop the parts' code made every
 // other task type 2-3x slower (TRSM 16 -> 44 us, even with no TPART in the list) -- the loop's
 // registers (it sits at 256 VGPRs) and its hot code in the instruction cache.
+
+// TPART(k, p) phase 1, PROGRESSIVE form (f64 look-ahead factor; on a sharded fit when DIAGX(k-1)
+// is this rank's): the part's 32 rows R = 32 p .. 32 p + 31 of T = L_{k,k-1} by blocked forward
+// substitution against the factor of block k - 1 AS DIAGX(k-1) PRODUCES IT, following its panel
+// counter (TP_DPAN >= c + 1: L panels 0..c and Dinv_0..Dinv_c stored):
+//     X_c = V_c Dinv_c^T,   then V_c' -= X_c L_{c'c}^T for c' > c,   V = A_{k,k-1}[R, :] at start
+// (T L_{k-1,k-1}^T = A_{k,k-1}, column panel by column panel).  Rows are independent, so the
+// parts need nothing from each other in this phase (no "A read" round).  After DIAGX(k-1)'s last
+// fact32 only Dinv_3's store, X_3 (8 MFMAs per tile) and the T store remain on the chain: the
+// Linv_{k-1} form waited for the whole inverse (its last row block, stores and publication, ~8 us
+// of DIAGX(k-1) after F(3)) and then formed all of T.
+template <typename T>
+__device__ __noinline__ bool tpart_prog(const TpCtx<T>* ap, T* __restrict__ Akm, int64_t ld, const T* __restrict__ Lkk,
+                                        const T* __restrict__ Lv, const int* pan, int* tf, int k, const int C, T* smem,
+                                        int& s_ok, const int t) {
+    typedef Mfma<T> Tr;
+    typedef typename Tr::acc_t acc_t;
+    const TpCtx<T> a = *ap;
+    const int lane = t & 63, w = t >> 6, lr = lane & 15, lk = lane >> 4;
+    // LDS (column-major; strides = 16 mod 32 elements: the ds_read_b64 fragment reads of lanes
+    // k and k + 1 land in opposite halves of the 64 banks)
+    constexpr int WS = 48, LS = 112, DS = 48;
+    T* W = smem;             // [128][WS]: V (32 rows), column panel c becoming X_c
+    T* Ls = W + DB * WS;     // [32][LS]: rows 32 (c + 1) .. 127 of L panel c
+    T* Ds = Ls + 32 * LS;    // [32][DS]: Dinv_c
+    const int r0 = 32 * C;
+    long long* xs = a.xt ? a.xt + 4 * (4 * (int64_t)k + C) : nullptr;
+    for (int e = t; e < 32 * DB; e += NT) {  // V = A_{k,k-1}[R, :] (final: wait_inputs)
+        const int r = e & 31, c = e >> 5;
+        W[r + c * WS] = Akm[r0 + r + (int64_t)c * ld];
+    }
+#pragma unroll 1
+    for (int c = 0; c < 4; c++) {
+        const int c0 = 32 * c, nl = 96 - c0;
+        if (w == 0) {
+            const bool ok = tpart_wait_flags<T>(a, pan, 1, c + 1);
+            if (ok) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            s_ok = ok ? 1 : 0;
+        }
+        __syncthreads();
+        if (!__builtin_amdgcn_readfirstlane(s_ok)) return false;
+        if (c == 3 && xs && w == 0) xs[0] = wall_clock64();  // DIAGX(k-1)'s last panel seen
+        for (int e = t; e < 32 * 32; e += NT) {
+            const int r = e & 31, q = e >> 5;
+            Ds[r + q * DS] = Lv[(c0 + r) + (int64_t)(c0 + q) * DB];
+        }
+        for (int e = t; e < nl * 32; e += NT) {
+            const int r = e % nl, q = e / nl;
+            Ls[r + q * LS] = Lkk[(c0 + 32 + r) + (int64_t)(c0 + q) * ld];
+        }
+        __syncthreads();
+        // X_c = V_c Dinv_c^T: waves 0-3, one 16 x 16 tile (ty, tx) each
+        acc_t x = acc_t{0};
+        const int ty = (w >> 1) & 1, tx = w & 1;
+        if (w < 4) {
+#pragma unroll
+            for (int kq = 0; kq < 8; kq++) {
+                const int m = 4 * kq + lk;
+                x = Tr::mma(Ds[(16 * tx + lr) + m * DS], W[(16 * ty + lr) + (c0 + m) * WS], x);
+            }
+        }
+        __syncthreads();  // every read of V_c done
+        if (w < 4) {
+#pragma unroll
+            for (int reg = 0; reg < 4; reg++) W[(16 * ty + lr) + (c0 + 16 * tx + Tr::orow(lk, reg)) * WS] = x[reg];
+        }
+        __syncthreads();
+        // V_c' -= X_c L_{c'c}^T, c' > c: 2 x (nl / 16) tiles over the eight waves
+#pragma unroll 1
+        for (int tt = w; tt < 2 * (nl / 16); tt += NT / 64) {
+            const int uy = tt & 1, ux = tt >> 1;  // rows 16 uy, columns c0 + 32 + 16 ux
+            acc_t v;
+#pragma unroll
+            for (int reg = 0; reg < 4; reg++) v[reg] = W[(16 * uy + lr) + (c0 + 32 + 16 * ux + Tr::orow(lk, reg)) * WS];
+#pragma unroll
+            for (int kq = 0; kq < 8; kq++) {
+                const int m = 4 * kq + lk;
+                v = Tr::mma(-Ls[(16 * ux + lr) + m * LS], W[(16 * uy + lr) + (c0 + m) * WS], v);
+            }
+#pragma unroll
+            for (int reg = 0; reg < 4; reg++) W[(16 * uy + lr) + (c0 + 32 + 16 * ux + Tr::orow(lk, reg)) * WS] = v[reg];
+        }
+        // (the next round's first barrier orders these writes before any read)
+    }
+    __syncthreads();
+    if (xs && w == 0) xs[1] = wall_clock64();  // X_3 computed
+    for (int e = t; e < 32 * DB; e += NT) {  // T rows R in place: L_{k,k-1}
+        const int r = e & 31, c = e >> 5;
+        st_sc1(Akm + r0 + r + (int64_t)c * ld, W[r + c * WS]);
+    }
+    publish(tf + C, 2, false);
+    if (xs && w == 0) xs[2] = wall_clock64();
+    return true;
+}
+
 template <typename T, bool DIST>
 __device__ __noinline__ bool tpart_run(const TpCtx<T>* ap, T* __restrict__ Akm, const T* __restrict__ Akk, int64_t ld,
                                        const T* __restrict__ Lp, T* __restrict__ sb, int64_t sld, int* tf, int k,
-                                       const int C, T* smem, int& s_ok, const int t) {
+                                       const int C, T* smem, int& s_ok, const int t, const T* Lkk) {
     typedef TpL<T> Q;
     typedef Mfma<T> Tr;
     typedef typename Tr::acc_t acc_t;
@@ -1765,6 +1903,11 @@ __device__ __noinline__ bool tpart_run(const TpCtx<T>* ap, T* __restrict__ Akm, 
     const TpCtx<T> a = *ap;
     const int lane = t & 63, w = t >> 6, lr = lane & 15, lk = lane >> 4;
     const int g0 = C, g1 = 7 - C;                      // the part's column groups (and tile-rows)
+    long long* xs = a.xt ? a.xt + 4 * (4 * (int64_t)k + C) : nullptr;
+    if (Lkk) {  // ---- phase 1, progressive --------------------------------------------------------
+        if (!tpart_prog<T>(ap, Akm, ld, Lkk, Lp, a.tflag + TP_STRIDE * (k - 1) + TP_DPAN, tf, k, C, smem, s_ok, t))
+            return false;
+    } else {
     const int nk0 = 4 * (g0 + 1), nk1 = 4 * (g1 + 1);  // k-steps of 4 of each group (nk1 > nk0)
     T* Ls = smem;
     // ---- phase 1 ---------------------------------------------------------------------------
@@ -1786,7 +1929,6 @@ __device__ __noinline__ bool tpart_run(const TpCtx<T>* ap, T* __restrict__ Akm, 
     }
     __syncthreads();
     if (!__builtin_amdgcn_readfirstlane(s_ok)) return false;
-    long long* xs = a.xt ? a.xt + 4 * (4 * (int64_t)k + C) : nullptr;
     if (xs && w == 0) xs[0] = wall_clock64();  // Linv_{k-1} seen
     // Linv_{k-1} rows 16 g0 + r (r < 16) and 16 g1 + r - 16 (r >= 16), all 128 columns (zero
     // above the diagonal), as Ls[r + col LSB]: 16-B loads (4 per thread f64, 2 f32), all in flight
@@ -1831,6 +1973,7 @@ __device__ __noinline__ bool tpart_run(const TpCtx<T>* ap, T* __restrict__ Akm, 
             st_sc1(Akm + 16 * w + lr + (int64_t)(16 * (x ? g1 : g0) + Tr::orow(lk, reg)) * ld, acc[x][reg]);
     publish(tf + C, 2, false);  // this part's columns of L_{k,k-1} stored
     if (xs && w == 0) xs[2] = wall_clock64();
+    }
     // ---- phase 2 ---------------------------------------------------------------------------
     if (w == 0) {
         bool ok = tpart_wait_flags<T>(a, tf, 4, 2);                           // all of T
@@ -1893,14 +2036,16 @@ __device__ __noinline__ bool tpart_run(const TpCtx<T>* ap, T* __restrict__ Akm, 
     return true;
 }
 
+// Lkk: L_{k-1,k-1} (ld) when DIAGX(k-1) publishes its panels where these parts can read them
+// (one GPU, or DIAGX(k-1) on this rank): the progressive phase 1; null: the Linv_{k-1} form
 template <typename T, bool DIST>
 __device__ __forceinline__ bool tpart_task(const TpCtx<T>* ap, T* Akm, T* Akk, int64_t ld, const T* Lp, int k, int c,
-                                           T* smem, int& s_ok, const int t) {
+                                           T* smem, int& s_ok, const int t, const T* Lkk) {
     // S's quarters: f64 into the S buffer (DIAGX copies it into the look-ahead factor's LDS
     // image); f32 in place into A_kk (the rank-8 factor reads its block from memory)
     constexpr bool img = std::is_same<T, double>::value && DIAG_LA;
-    return tpart_run<T, DIST>(ap, Akm, Akk, ld, Lp, img ? ap->pbuf : Akk, img ? (int64_t)DB : ld, ap->tflag + 4 * k, k,
-                              c, smem, s_ok, t);
+    return tpart_run<T, DIST>(ap, Akm, Akk, ld, Lp, img ? ap->pbuf : Akk, img ? (int64_t)DB : ld, ap->tflag + TP_STRIDE * k, k,
+                              c, smem, s_ok, t, img ? Lkk : nullptr);
 }
 
 // DIAGX(k > 0) of the split step, f32 (the parts wrote S into A_kk): wait for the four
@@ -1909,7 +2054,7 @@ template <typename T>
 __device__ __forceinline__ bool diagx_split_wait(const TpCtx<T>* ap, int k, int& s_ok) {
     const int w = threadIdx.x >> 6;
     if (w == 0) {
-        const bool ok = tpart_wait_flags<T>(*ap, ap->tflag + 4 * k, 4, 3);
+        const bool ok = tpart_wait_flags<T>(*ap, ap->tflag + TP_STRIDE * k, 4, 3);
         if (ok) {
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             st_agent(ap->lcnt + k, k);
@@ -1929,7 +2074,7 @@ __device__ __noinline__ bool diagx_split(const TpCtx<T>* ap, int k, T* smem, int
     typedef typename Mfma<T>::vec_t vec_t;
     const TpCtx<T> a = *ap;
     const int lane = t & 63, w = t >> 6;
-    const int* tf = a.tflag + 4 * k;
+    const int* tf = a.tflag + TP_STRIDE * k;
     long long* xs = a.xt ? a.xt + 4 * (4 * (int64_t)a.nc + k) : nullptr;
     int rr[9], cc[9];
 #pragma unroll
@@ -2046,7 +2191,9 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
             if (type == T_TPART) {
                 if constexpr (SPLIT_CODE)
                     ok = tpart_task<T, true>(tpc, dist_tile(a.A, D, i, i - 1), dist_tile(a.A, D, i, i), DB,
-                                             a.Linv + (int64_t)(i - 1) * DB * DB, i, j, smem, s_ok, tid);
+                                             a.Linv + (int64_t)(i - 1) * DB * DB, i, j, smem, s_ok, tid,
+                                             __builtin_amdgcn_readfirstlane(D.loc[i - 1]) >= 0 && !tp_linv_form()
+                                                 ? dist_tile(a.A, D, i - 1, i - 1) : nullptr);
             } else if (type == T_BUILD) {
                 T* tij = dist_tile(a.A, D, i, j);
                 // build_tile_sum addresses element (gi, gj) at base + gi + gj ld (global indices)
@@ -2084,9 +2231,8 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
                     __syncthreads();
                     ok = __builtin_amdgcn_readfirstlane(s_ok) != 0;
                     if (ok)
-                        dist_push(Cik, D, cm, D.o_win + ((int64_t)(j % D.ww) * D.nr + i) * DB * DB * (int64_t)sizeof(T),
-                                  dist_f_tile() + (int64_t)i * D.nc + j, tid, (int64_t)(j % D.ww) * D.nr + i,
-                                  (D.ep << 16) | (unsigned)(j + 1));
+                        dist_push(Cik, D, cm, -1, dist_f_tile() + (int64_t)i * D.nc + j, tid,
+                                  (int64_t)(j % D.ww) * D.nr + i, (D.ep << 16) | (unsigned)(j + 1));
                 }
             } else {  // DIAGX(k = i)
                 const int k = i;
@@ -2107,7 +2253,8 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
                     local_sync();
                 }
                 diag_factor<T>(Akk, DB, a.Linv + (int64_t)k * DB * DB, a.info, (int64_t)k * DB, smem_raw, tid, a.dbg,
-                               nullptr, fused_ts && k > 0, a.lcnt + k, k + 1);  // (publishes Linv_k locally)
+                               nullptr, fused_ts && k > 0, a.lcnt + k, k + 1,  // (publishes Linv_k locally)
+                               a.split ? a.tflag + TP_STRIDE * k + TP_DPAN : nullptr);  // (and its panels)
                 // pushes after the local publication (this rank's chain goes on meanwhile): the
                 // next diagonal step's rank first, L_{k,k-1} before Linv_k
                 const unsigned cm = k > 0 ? dist_consumers(D, k) : 0u;
@@ -2120,7 +2267,7 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
                     __syncthreads();
                     ok = __builtin_amdgcn_readfirstlane(s_ok) != 0;
                 }
-                const int64_t owin = D.o_win + ((int64_t)((k - 1 + D.ww) % D.ww) * D.nr + k) * DB * DB * (int64_t)sizeof(T);
+                const int64_t owin = -1;  // the window slot tix
                 const int64_t olinv = D.o_linv + (int64_t)k * DB * DB * (int64_t)sizeof(T);
                 const int64_t tix = (int64_t)((k - 1 + D.ww) % D.ww) * D.nr + k;
                 const unsigned tgv = (D.ep << 16) | (unsigned)k;
@@ -2140,7 +2287,9 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
         if (type == T_TPART) {
             if constexpr (SPLIT_CODE)
                 (void)tpart_task<T, false>(tpc, Ci + (int64_t)(i - 1) * GT * ld, Ci + (int64_t)i * GT * ld, ld,
-                                           a.Linv + (int64_t)(i - 1) * DB * DB, i, j, smem, s_ok, tid);
+                                           a.Linv + (int64_t)(i - 1) * DB * DB, i, j, smem, s_ok, tid,
+                                           tp_linv_form() ? nullptr
+                                                          : a.A + (int64_t)(i - 1) * GT + (int64_t)(i - 1) * GT * ld);
         } else if (type == T_BUILD) {
             // ver[i][j] goes from -1 (not built) to 0; the tile's values go out write-through
             // one instantiation for every mode: an absent statistic has a zero-depth product
@@ -2195,7 +2344,8 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
             if (a.trace) dt[2] = wall_clock64();
             diag_factor<T>(Akk, ld, a.Linv + (int64_t)k * DB * DB, a.info, (int64_t)k * DB, smem_raw, tid, a.dbg,
                            a.trace ? a.trace + 4 * (int64_t)(a.ntasks + a.nc) + 4 * (int64_t)k : nullptr,
-                           fused_ts && k > 0, a.lcnt + k, k + 1);  // (publishes Linv_k: lcnt[k] = k + 1)
+                           fused_ts && k > 0, a.lcnt + k, k + 1,  // (publishes Linv_k: lcnt[k] = k + 1)
+                           a.split ? a.tflag + TP_STRIDE * k + TP_DPAN : nullptr);  // (and its panels)
             if (a.trace) dt[3] = wall_clock64();
             if (a.trace && wv == 0) {
                 long long* dp = a.trace + 4 * (int64_t)a.ntasks + 4 * (int64_t)k;
@@ -2234,6 +2384,11 @@ struct Cost {  // per-task durations (us, one CU), calibrated from GPRX_PT_TRACE
     // 2 us and factors; step 54.4 us)
     double tpart = 11.5, tpart_c = 0.0;
     double diagx_s = 44.0, early_s = 2.0;
+    // the progressive parts (f64, tpart_prog; DIAGX(k-1) on the same rank): they follow DIAGX(k-1)'s
+    // panels and publish S this long after its end (X_3, T and S remain after its last fact32,
+    // ~8 us before its end)
+    double tpart_prog = 2.5;
+    bool prog = false;  // this schedule is for the progressive form (set by the callers)
 };
 
 // TPART tickets of one k in the order TPART(k, 3), (k, 2), (k, 1), (k, 0): each part waits for
@@ -2366,7 +2521,7 @@ static Schedule make_schedule(int nc, int nr, int W, int near, int P, const Cost
         if (split && k >= 1) {  // TPART(k, 3..0), then DIAGX(k) on their products
             int tp[4];
             for (int c = 3; c >= 0; c--) {
-                tp[c] = add(T_TPART, k, c, 0, 0, cm.tpart + cm.tpart_c * (c + 1));
+                tp[c] = add(T_TPART, k, c, 0, 0, cm.prog ? cm.tpart_prog : cm.tpart + cm.tpart_c * (c + 1));
                 dep(tp[c], diagx[k - 1]);
                 dep(tp[c], last_upd[(size_t)k * nc + (k - 1)]);
                 dep(tp[c], last_upd[(size_t)k * nc + k]);  // phase 2 starts from A_kk
@@ -2605,7 +2760,8 @@ static DistSched make_schedule_dist(int nc, bool inv, int W, int near, int P, in
         int tp[4] = {-1, -1, -1, -1};
         if (split && k >= 1)  // TPART(k, 3..0) on the owner of row block k
             for (int c = 3; c >= 0; c--) {
-                tp[c] = add(T_TPART, k, c, 0, 0, cm.tpart + cm.tpart_c * (c + 1), own(k));
+                tp[c] = add(T_TPART, k, c, 0, 0,
+                            (cm.prog && own(k - 1) == own(k)) ? cm.tpart_prog : cm.tpart + cm.tpart_c * (c + 1), own(k));
                 dep(tp[c], linv(k - 1, own(k)));
                 dep(tp[c], last_upd[(size_t)k * nci + (k - 1)]);
                 dep(tp[c], last_upd[(size_t)k * nci + k]);  // phase 2 starts from A_kk
@@ -2800,6 +2956,13 @@ struct Params {
         if (const char* e = std::getenv("GPRX_PT_TAIL")) tail = std::atoi(e);
         if (const char* e = std::getenv("GPRX_PT_TPART_US")) cm.tpart = std::atof(e);
         if (const char* e = std::getenv("GPRX_PT_DIAGXS_US")) cm.diagx_s = std::atof(e);
+        if (const char* e = std::getenv("GPRX_PT_TPARTP_US")) cm.tpart_prog = std::atof(e);
+    }
+    // the cost model for a precision: the progressive parts are the f64 look-ahead factor's
+    Cost cost(bool f64) const {
+        Cost c = cm;
+        c.prog = f64 && DIAG_LA && !tp_linv_form();
+        return c;
     }
 };
 static const Params& params() {
@@ -2814,14 +2977,15 @@ static const Params& params() {
 // simulation ranks it first too) -- unless GPRX_PT_RATIO fixes it (GPRX_PT_TAIL its reach)
 static const int kRatios[] = {0, 8, 4, 2};
 static const int kTails[] = {0, 16, 32};
-static Schedule best_schedule(int nc, int nr, const Params& pr, int P, bool build, int ni, bool split) {
-    if (pr.ratio >= 0) return make_schedule(nc, nr, pr.W, pr.near_for(nc), P, pr.cm, build, ni, pr.ratio, split, pr.tail);
+static Schedule best_schedule(int nc, int nr, const Params& pr, int P, bool build, int ni, bool split, bool f64) {
+    const Cost cm = pr.cost(f64);
+    if (pr.ratio >= 0) return make_schedule(nc, nr, pr.W, pr.near_for(nc), P, cm, build, ni, pr.ratio, split, pr.tail);
     Schedule best;
     bool have = false;
     for (int r : kRatios)
         for (int tl : kTails) {
             if ((r == 0 && tl) || (tl && tl >= nc)) continue;
-            Schedule S = make_schedule(nc, nr, pr.W, pr.near_for(nc), P, pr.cm, build, ni, r, split, tl);
+            Schedule S = make_schedule(nc, nr, pr.W, pr.near_for(nc), P, cm, build, ni, r, split, tl);
             if (!have || S.est_us < best.est_us * 0.995) {  // a rule with more tasks must win by > 0.5%
                 best = std::move(S);
                 have = true;
@@ -2846,7 +3010,7 @@ struct PtState {
         double est_us = 0;
         std::vector<int4> host;
     };
-    std::map<std::tuple<int, int, bool, int, bool>, Dev> sched;
+    std::map<std::tuple<int, int, bool, int, bool, int>, Dev> sched;  // (nc, nr, fused, ni, split, sizeof(T))
     int* ctr = nullptr;
     void* pbuf = nullptr;  // the split diagonal step's four TPART products (DB x DB each)
     size_t ctr_ints = 0;
@@ -2887,16 +3051,25 @@ int64_t pt_trace_copy(int32_t* tasks, long long* times, int64_t max) {
 // debug snapshot of the last launch's per-workgroup status (GPRX_PT_DEBUG)
 static int* g_pt_dbg = nullptr;
 static int g_pt_dbg_n = 0;
+static std::mutex g_pt_dbg_mu;
 int pt_debug_snapshot(int* out, int max_wg) {
+    std::lock_guard<std::mutex> lk(g_pt_dbg_mu);
     if (!g_pt_dbg) return 0;
     const int n = std::min(max_wg, g_pt_dbg_n);
     for (int k = 0; k < 4 * n; k++) out[k] = __atomic_load_n(g_pt_dbg + k, __ATOMIC_RELAXED);
     return n;
 }
-// a distributed rank's launch (GPRX_PT_DEBUG, one rank per process): its status words
+// a distributed rank's launch (GPRX_PT_DEBUG, one rank per process): its status words, owned by
+// the engine; n = 0 unregisters `dbg` if it is the registered buffer (the engine's teardown)
 void pt_debug_register(int* dbg, int n) {
-    g_pt_dbg = dbg;
-    g_pt_dbg_n = n;
+    std::lock_guard<std::mutex> lk(g_pt_dbg_mu);
+    if (n > 0) {
+        g_pt_dbg = dbg;
+        g_pt_dbg_n = n;
+    } else if (g_pt_dbg == dbg) {
+        g_pt_dbg = nullptr;
+        g_pt_dbg_n = 0;
+    }
 }
 
 // ctr[i] = -1 for i in [v0, v1), 0 elsewhere (i < n)
@@ -2944,7 +3117,7 @@ void potrf_tiles(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info
     // build_only (a parity hook, gprx_dev_build_matrix): the ticket list holds the BUILD tasks
     // alone, so the launch writes exactly the covariance tiles the fused factorisation starts from
     const bool split = split_for(std::is_same<T, double>::value, st.ncu);
-    auto key = std::make_tuple(nc, nr, fused, build_only ? -1 : ni, split);
+    auto key = std::make_tuple(nc, nr, fused, build_only ? -1 : ni, split, (int)sizeof(T));
     auto it = st.sched.find(key);
     if (it == st.sched.end()) {
         const Params& pr = params();
@@ -2953,7 +3126,7 @@ void potrf_tiles(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info
             for (int i = 0; i < nc; i++)
                 for (int j = 0; j <= i; j++) S.list.push_back(make_int4(T_BUILD, i, j, 0));
         } else {
-            S = best_schedule(nc, nr, pr, st.ncu, fused, ni, split);
+            S = best_schedule(nc, nr, pr, st.ncu, fused, ni, split, std::is_same<T, double>::value);
         }
         PtState::Dev d;
         d.n = (int64_t)S.list.size();
@@ -2964,7 +3137,7 @@ void potrf_tiles(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info
         it = st.sched.emplace(key, d).first;
     }
     const PtState::Dev& sd = it->second;
-    const size_t need = (size_t)C_NCTL + nr + (size_t)nr * nc + 4 * (size_t)nc;  // + the TPART states
+    const size_t need = (size_t)C_NCTL + nr + (size_t)nr * nc + TP_STRIDE * (size_t)nc;  // + the split step's states
     if (st.ctr_ints < need) {
         if (st.ctr) GPRX_HIP(hipFree(st.ctr));
         st.ctr = nullptr;
@@ -3076,7 +3249,7 @@ DistSched potrf_dist_schedule(int nc, int g, int gb, int ww, int P, bool build, 
     // update chunks at most half a window wide (flow control, make_schedule_dist), powers of two
     int W = 1;
     while (2 * W <= std::min(pr.W, std::max(1, ww / 2))) W *= 2;
-    return pt::make_schedule_dist(nc, inv, W, pr.near_for(nc), P, g, std::max(1, gb), ww, pr.cm, build, push_us, rel_us,
+    return pt::make_schedule_dist(nc, inv, W, pr.near_for(nc), P, g, std::max(1, gb), ww, pr.cost(f64), build, push_us, rel_us,
                                   pr.ratio >= 0 ? pr.ratio : ratio, pt::split_for(f64, P), pr.ratio >= 0 ? pr.tail : tail);
 }
 
@@ -3129,8 +3302,9 @@ int64_t potrf_tiles_schedule_stats(int nc, int nr, int P, bool build, double* es
         throw Error{GPRX_ERR_ARG, "potrf tile schedule: need nc >= 1, nr >= nc + ni, P >= 1"};
     const pt::Params& pr = pt::params();
     const bool split = pt::split_for(true, P);  // the f64 schedule
-    pt::Schedule S = ratio >= 0 ? pt::make_schedule(nc, nr, pr.W, pr.near_for(nc), P, pr.cm, build, ni, ratio, split, pr.tail)
-                                : pt::best_schedule(nc, nr, pr, P, build, ni, split);
+    pt::Schedule S = ratio >= 0 ? pt::make_schedule(nc, nr, pr.W, pr.near_for(nc), P, pr.cost(true), build, ni, ratio, split,
+                                                    pr.tail)
+                                : pt::best_schedule(nc, nr, pr, P, build, ni, split, true);
     if (est_us) *est_us = S.est_us;
     if (list_out)  // the ticket list: {type | nb << 8, i, j, b0} per ticket
         for (int64_t q = 0; q < (int64_t)S.list.size() && q < list_max; q++) {

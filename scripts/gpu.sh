@@ -1,0 +1,127 @@
+#!/bin/bash
+# One parametrised wrapper for the GPU box (run through gpurun from the repo root):
+#
+#   gpurun --timeout 1200 -- bash scripts/gpu.sh TAG STEP [STEP ...]
+#
+# Output under gpurun_out/TAG/.  Every GPU step runs under its own `timeout -k`; the steps are
+# chained and the script stops at the first failure (no GPU step after a fault, abort or time
+# limit).  Steps:
+#   tests      the whole `pytest -m gpu` suite (GPU_TESTS="tests/test_x.py ..." selects files,
+#              GPU_K="expr" a -k filter)
+#   smoke      __graft_entry__.smoke()
+#   bench      the default bench line (-> bench.json; extra args in BENCH_ARGS)
+#   profile    one `rocprofv3 --kernel-trace --stats` pass per bench leg (bench.py --legs L), then
+#              the PMC passes: FETCH_SIZE and WRITE_SIZE of the C3 fit and of the path-0 build,
+#              the MFMA-busy counters of the C3 and C4 factorisations.  scripts/profile_collect.py
+#              TAG turns the output into the profiles/TAG_<leg>_* summaries bench.py attaches.
+#   shared     the N = 2 bench path rehearsed on one GPU (two processes, gloo + peer context)
+#   peer       two-process sharded-fit tests (tests/test_gpu_dist.py -k peer)
+#   trace      the tile-engine timelines at N = 4096 and 16384 (scripts/pt_trace.py)
+#   diag       the isolated diagonal-factor microbenchmark (scripts/diag_bench.py)
+#   dist       the sharded fit on 1/2/4/8 virtual ranks (scripts/dist_time.py)
+#   ab         same-box A/B of the C3 bench leg: every tools/ab/*.so (GPRX_LIB_OVERRIDE) and this
+#              tree's library, alternated twice (AB_ARGS: extra bench args)
+#   distab     the same for the sharded fit on 1 and 8 virtual ranks
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(pwd)}" || exit 1
+R=$PWD
+TAG=${1:?tag}
+shift
+O=$R/gpurun_out/$TAG
+mkdir -p "$O"
+export TMPDIR=/tmp
+
+fail() { echo "step $1 failed (rc $2)"; tail -n 30 "$3" 2>/dev/null; exit "$2"; }
+
+prof_leg() {  # $1 = leg: kernel trace + stats of one bench leg in its own process
+    local leg=$1
+    (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_$leg" -o "$leg" \
+        -- python3 "$R/bench.py" --legs "$leg" --cpu-n 0 > "$O/prof_$leg.json" 2> "$O/prof_$leg.err") \
+        || fail "profile:$leg" $? "$O/prof_$leg.err"
+    echo "profile $leg ok"
+}
+
+pmc_leg() {  # $1 = leg, $2 = output name, $3.. = counters (one block-limited pass)
+    local leg=$1 name=$2
+    shift 2
+    (cd /tmp && timeout -s KILL 240 rocprofv3 --pmc "$@" --output-format csv -d "$O/$name" -o "$name" \
+        -- python3 "$R/bench.py" --legs "$leg" --cpu-n 0 --steps 2 --warmup 1 --build-iters 2 \
+        > "$O/$name.json" 2> "$O/$name.err") || fail "pmc:$name" $? "$O/$name.err"
+    echo "pmc $name ok"
+}
+
+for step in "$@"; do
+    case $step in
+    tests)
+        timeout -k 10 1000 python -u -m pytest ${GPU_TESTS:-tests} -m gpu -x -q ${GPU_K:+-k "$GPU_K"} \
+            --timeout 300 --timeout-method thread > "$O/gputest.log" 2>&1 || fail tests $? "$O/gputest.log"
+        tail -n 2 "$O/gputest.log"
+        ;;
+    smoke)
+        timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('__SMOKE_OK__')" \
+            > "$O/smoke.log" 2>&1 || fail smoke $? "$O/smoke.log"
+        tail -n 2 "$O/smoke.log"
+        ;;
+    bench)
+        timeout -k 10 600 python -u bench.py $BENCH_ARGS > "$O/bench.json" 2> "$O/bench.err" \
+            || fail bench $? "$O/bench.err"
+        python scripts/bench_brief.py "$O/bench.json"
+        ;;
+    profile)
+        for leg in c3 predict lml build c2 c4 c5; do prof_leg $leg; done
+        pmc_leg c3 pmcf_c3 FETCH_SIZE
+        pmc_leg c3 pmcw_c3 WRITE_SIZE
+        pmc_leg build pmcf_build FETCH_SIZE
+        pmc_leg build pmcw_build WRITE_SIZE
+        pmc_leg c3 pmcm_c3 SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE
+        pmc_leg c4 pmcm_c4 SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE
+        ;;
+    shared)
+        GPRX_DIST_SHARED_GPU=1 timeout -k 10 500 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+            --master-addr 127.0.0.1 --master-port $((29600 + RANDOM % 100)) bench.py --gpus 2 \
+            > "$O/shared_bench.json" 2> "$O/shared_bench.err" || fail shared $? "$O/shared_bench.err"
+        python scripts/bench_brief.py "$O/shared_bench.json"
+        ;;
+    peer)
+        timeout -k 10 900 python -u -m pytest tests/test_gpu_dist.py -m gpu -x -q -k peer \
+            --timeout 600 --timeout-method thread > "$O/peer.log" 2>&1 || fail peer $? "$O/peer.log"
+        tail -n 2 "$O/peer.log"
+        ;;
+    trace)
+        timeout -k 10 120 python scripts/pt_trace.py 4096 > "$O/pt4096.json" 2> "$O/pt4096.err" || fail trace $? "$O/pt4096.err"
+        timeout -k 10 120 python scripts/pt_trace.py 16384 > "$O/pt16384.json" 2> "$O/pt16384.err" || fail trace $? "$O/pt16384.err"
+        ;;
+    diag)
+        timeout -k 10 120 python scripts/diag_bench.py > "$O/diag_bench.json" 2> "$O/diag_bench.err" || fail diag $? "$O/diag_bench.err"
+        ;;
+    dist)
+        timeout -k 10 300 python scripts/dist_time.py > "$O/dist_time.jsonl" 2> "$O/dist_time.err" || fail dist $? "$O/dist_time.err"
+        ;;
+    ab)
+        shopt -s nullglob
+        Q="--cpu-n 0 --legs c3 --steps 20 $AB_ARGS"
+        for rep in 1 2; do
+            for f in tools/ab/*.so; do
+                b=$(basename "$f" .so)
+                GPRX_LIB_OVERRIDE=$R/$f timeout -k 10 300 python bench.py $Q > "$O/ab_${b}_$rep.json" 2> "$O/ab.err" \
+                    || fail ab $? "$O/ab.err"
+            done
+            timeout -k 10 300 python bench.py $Q > "$O/ab_tree_$rep.json" 2> "$O/ab.err" || fail ab $? "$O/ab.err"
+        done
+        for f in "$O"/ab_*.json; do echo "$(basename "$f") $(python scripts/bench_brief.py "$f" | head -1)"; done
+        ;;
+    distab)
+        shopt -s nullglob
+        for f in tools/ab/*.so; do
+            b=$(basename "$f" .so)
+            GPRX_LIB_OVERRIDE=$R/$f timeout -k 10 300 python -u scripts/dist_time.py 16384 5 v1 v8 > "$O/distab_$b.jsonl" \
+                2> "$O/distab.err" || fail distab $? "$O/distab.err"
+        done
+        timeout -k 10 300 python -u scripts/dist_time.py 16384 5 v1 v8 > "$O/distab_tree.jsonl" 2> "$O/distab.err" \
+            || fail distab $? "$O/distab.err"
+        ;;
+    *)
+        echo "unknown step $step"; exit 2 ;;
+    esac
+done
+echo "all steps done"
