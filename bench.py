@@ -316,8 +316,11 @@ def run_configs(args, world, rank, local_rank, dctx, max_over_ranks, barrier_syn
         if ctx is not dctx:
             ctx.close()
         syrk = st.get("other_gemm", {"ms": 0, "launches": 0, "flops": 0})
-        t_s = max_over_ranks(syrk["ms"] / steps) if syrk["launches"] else None
-        f_syrk = float(len(rows)) * M_ * (M_ + 1)  # the rank's sigma^-2 Knm^T Knm (+ label row), lower
+        # the rank's sigma^-2 Knm^T Knm (+ label row), lower: one split-K launch per streamed row
+        # chunk; per launch, the fit's algorithmic flops over its launches and the average device time
+        lpf = syrk["launches"] / steps if syrk["launches"] else 0
+        t_s = max_over_ranks(syrk["ms"] / syrk["launches"]) if syrk["launches"] else None
+        f_syrk = float(len(rows)) * M_ * (M_ + 1) / lpf if lpf else 0.0
         flops = 2.0 * n * M_ * d + n * M_ * (M_ + 1) + 2.0 * M_ ** 3
         c5 = {"workload": "C5: sparse GP fit M=2048 inducing, N=1e6 dense rows, d=64 fp64 GaussianKernel(3,1) "
                           "sigma=0.1 jitter=1e-4 (BASELINE.json configs[4])",
@@ -328,7 +331,8 @@ def run_configs(args, world, rank, local_rank, dctx, max_over_ranks, barrier_syn
               "roofline": {"bound": "mfma", "kernel": "syrk_splitk_kernel<double> (sigma^-2 Knm^T Knm, k_syrk.hip)",
                            "achieved": f_syrk / (t_s * 1e-3) / 1e12 if t_s else None, "peak": PEAK_FP64_TFLOPS,
                            "unit": "TFLOP/s", "frac": f_syrk / (t_s * 1e-3) / 1e12 / PEAK_FP64_TFLOPS if t_s else None,
-                           "avg_launch_us": 1e3 * t_s if t_s else None, "algorithmic_flops_per_launch": f_syrk}}
+                           "avg_launch_us": 1e3 * t_s if t_s else None, "algorithmic_flops_per_launch": f_syrk,
+                           "launches_per_fit": lpf}}
         if world == 1:
             c5["roofline"]["rocprof"] = rocprof_from_profile("c5", ("syrk_splitk_kernel<double>",),
                                                              c5["roofline"]["avg_launch_us"])

@@ -1094,11 +1094,15 @@ __device__ __forceinline__ void diag_factor_la(T* __restrict__ A, int64_t ld, T*
     }
 }
 
-// GPRX_TP_LINV (A/B builds): the parts wait for the whole Linv_{k-1} (the round-3 form)
-#ifdef GPRX_TP_LINV
-__host__ __device__ constexpr bool tp_linv_form() { return true; }
-#else
+// GPRX_TP_PROG (A/B builds): the progressive parts (tpart_prog) and DIAGX's panel counter.  Off
+// by default: same-box A/Bs (profiles/r04c_*, r04d_*) measured the chain step unchanged (C2
+// 1829 us against 1815 for the Linv form without the panel counter; the counter's stores and
+// drains cost DIAGX ~1.3 us per step, the early X_3 saves ~2 us of the parts' T phase, and the
+// parts' S phase, not T, dominates after DIAGX(k-1) ends) and C3 0.1-0.4% slower.
+#ifdef GPRX_TP_PROG
 __host__ __device__ constexpr bool tp_linv_form() { return false; }
+#else
+__host__ __device__ constexpr bool tp_linv_form() { return true; }
 #endif
 #ifdef GPRX_NO_SPLIT  // (A/B builds: the split diagonal step compiled out)
 constexpr bool SPLIT_CODE = false;
@@ -2254,7 +2258,7 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
                 }
                 diag_factor<T>(Akk, DB, a.Linv + (int64_t)k * DB * DB, a.info, (int64_t)k * DB, smem_raw, tid, a.dbg,
                                nullptr, fused_ts && k > 0, a.lcnt + k, k + 1,  // (publishes Linv_k locally)
-                               a.split ? a.tflag + TP_STRIDE * k + TP_DPAN : nullptr);  // (and its panels)
+                               (a.split && !tp_linv_form()) ? a.tflag + TP_STRIDE * k + TP_DPAN : nullptr);  // (its panels)
                 // pushes after the local publication (this rank's chain goes on meanwhile): the
                 // next diagonal step's rank first, L_{k,k-1} before Linv_k
                 const unsigned cm = k > 0 ? dist_consumers(D, k) : 0u;
@@ -2345,7 +2349,7 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
             diag_factor<T>(Akk, ld, a.Linv + (int64_t)k * DB * DB, a.info, (int64_t)k * DB, smem_raw, tid, a.dbg,
                            a.trace ? a.trace + 4 * (int64_t)(a.ntasks + a.nc) + 4 * (int64_t)k : nullptr,
                            fused_ts && k > 0, a.lcnt + k, k + 1,  // (publishes Linv_k: lcnt[k] = k + 1)
-                           a.split ? a.tflag + TP_STRIDE * k + TP_DPAN : nullptr);  // (and its panels)
+                           (a.split && !tp_linv_form()) ? a.tflag + TP_STRIDE * k + TP_DPAN : nullptr);  // (its panels)
             if (a.trace) dt[3] = wall_clock64();
             if (a.trace && wv == 0) {
                 long long* dp = a.trace + 4 * (int64_t)a.ntasks + 4 * (int64_t)k;

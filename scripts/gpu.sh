@@ -22,6 +22,8 @@
 #   ab         same-box A/B of the C3 bench leg: every tools/ab/*.so (GPRX_LIB_OVERRIDE) and this
 #              tree's library, alternated twice (AB_ARGS: extra bench args)
 #   distab     the same for the sharded fit on 1 and 8 virtual ranks
+#   envab      same-box A/B of environment settings: AB_ENVS="- GPRX_X=1 GPRX_Y=2" (one assignment
+#              or "-" per variant), the bench legs in AB_ARGS, alternated twice
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(pwd)}" || exit 1
 R=$PWD
@@ -119,6 +121,21 @@ for step in "$@"; do
         done
         timeout -k 10 300 python -u scripts/dist_time.py 16384 5 v1 v8 > "$O/distab_tree.jsonl" 2> "$O/distab.err" \
             || fail distab $? "$O/distab.err"
+        ;;
+    envab)
+        Q="--cpu-n 0 --legs c3 --steps 20 $AB_ARGS"
+        for rep in 1 2; do
+            for v in $AB_ENVS; do
+                b=$(echo "$v" | tr '=/' '__')
+                if [ "$v" = "-" ]; then
+                    timeout -k 10 300 python bench.py $Q > "$O/envab_base_$rep.json" 2> "$O/envab.err" || fail envab $? "$O/envab.err"
+                else
+                    env "$v" timeout -k 10 300 python bench.py $Q > "$O/envab_${b}_$rep.json" 2> "$O/envab.err" \
+                        || fail envab $? "$O/envab.err"
+                fi
+            done
+        done
+        for f in "$O"/envab_*.json; do echo "$(basename "$f")"; python scripts/bench_brief.py "$f" | head -4; done
         ;;
     *)
         echo "unknown step $step"; exit 2 ;;
