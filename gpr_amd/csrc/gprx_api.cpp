@@ -1029,11 +1029,64 @@ static void solve_rows_for(gprx_model* M, const T* dXq, const T* dtabQ, int64_t 
     trsm_rows<T>(M->A.as<T>(), M->ld, M->np, M->Linv.as<T>(), R, qp, qp, s);
 }
 
+// operator()(x, y) / GetCredibleInterval (lib/GaussianProcess.cpp:84-114) on a SHARDED fit:
+// k(x, y) - (L^{-1} k_x) . (L^{-1} k_y) by the distributed forward substitution of the queries
+// (dist_posterior, k_dsolve.hip dist_pvar_kernel): the ranks keep their own rows of L, the
+// query columns V_k travel through the receive windows, the row sums are all-reduced.  Pairs
+// (x_p, y_p) with x != y ride in the same chunk (64 + 64 columns), variances 128 per chunk.
+template <typename T>
+static gprx_status model_posterior_cov_dist(gprx_model* M, const void* Xa, const void* Xb, int64_t q, void* out) {
+    hipStream_t s = M->ctx->stream;
+    const KCanon<T>& K = kcanon<T>(M);
+    const int d = M->d;
+    const bool same = (Xa == Xb) || std::memcmp(Xa, Xb, sizeof(T) * q * d) == 0;
+    const int nchmax = dist_pvar_chunks(M->dist_engine);
+    const int per = same ? DB : DB / 2;  // pairs per chunk
+    const T* xa = static_cast<const T*>(Xa);
+    const T* xb = static_cast<const T*>(Xb);
+    DevBuf da, db, kab, dz, tz;
+    upload<T>(da, Xa, sizeof(T) * q * d, s);
+    upload<T>(db, Xb, sizeof(T) * q * d, s);
+    kab.ensure(sizeof(T) * q);
+    launch_pair_kernel<T>(K, da.as<T>(), db.as<T>(), q, d, kab.as<T>(), s);
+    std::vector<T> hk((size_t)q), res((size_t)q);
+    download(hk.data(), kab.p, sizeof(T) * q, s);
+    std::vector<double> sum;
+    for (int64_t p0 = 0; p0 < q;) {
+        const int64_t cnt = std::min<int64_t>(q - p0, (int64_t)nchmax * per);
+        const int nch = (int)((cnt + per - 1) / per);
+        const int64_t nq = (int64_t)nch * DB;
+        std::vector<T> Z((size_t)nq * d, T(0));
+        for (int64_t j = 0; j < cnt; j++) {
+            const int64_t c = j / per, jj = j % per;
+            std::memcpy(&Z[(size_t)(c * DB + jj) * d], xa + (p0 + j) * d, sizeof(T) * d);
+            if (!same) std::memcpy(&Z[(size_t)(c * DB + DB / 2 + jj) * d], xb + (p0 + j) * d, sizeof(T) * d);
+        }
+        upload<T>(dz, Z.data(), sizeof(T) * nq * d, s);
+        if (K.nper > 0) {
+            tz.ensure(sizeof(T) * 2 * K.nper * nq * d);
+            launch_sincos_tables<T>(K, dz.as<T>(), nq, d, tz.as<T>(), s);
+        }
+        dist_posterior<T>(M->dist_engine, K, M->X.as<T>(), K.nper > 0 ? M->tab.as<T>() : nullptr, M->n, d, dz.as<T>(),
+                          K.nper > 0 ? tz.as<T>() : nullptr, nch, !same, sum, s);
+        for (int64_t j = 0; j < cnt; j++) res[p0 + j] = (T)((double)hk[p0 + j] - sum[(j / per) * DB + j % per]);
+        p0 += cnt;
+    }
+    std::memcpy(out, res.data(), sizeof(T) * q);
+    return GPRX_OK;
+}
+
 template <typename T>
 static gprx_status model_posterior_cov(gprx_model* M, const void* Xa, const void* Xb, int64_t q, void* out) {
     GPRX_REQUIRE(M->fitted || M->sparse_cov, GPRX_ERR_STATE,
                  "GaussianProcess::ComputeKernelVectorInternal: gaussian process is not initialized.");
     GPRX_REQUIRE(!M->host_k, GPRX_ERR_STATE, "gprx: a caller-evaluated kernel uses gprx_model_posterior_cov_kx");
+    // a sharded fit solves the queries across the ranks (GPRX_DIST_POSTERIOR=dense: the dense
+    // factor gathered onto this process instead, as for the core matrix)
+    static const bool dense_forced = std::getenv("GPRX_DIST_POSTERIOR") &&
+                                     std::string(std::getenv("GPRX_DIST_POSTERIOR")) == "dense";
+    if (M->dist_fitted && !M->dist_dense && M->method == 0 && !dense_forced && dist_pvar_chunks(M->dist_engine) > 0)
+        return model_posterior_cov_dist<T>(M, Xa, Xb, q, out);
     ensure_dense_factor<T>(M);
     hipStream_t s = M->ctx->stream;
     const KCanon<T>& K = kcanon<T>(M);
@@ -2496,6 +2549,8 @@ gprx_status gprx_dev_dist_info(gprx_model* M, int64_t* out) {
     out[5] = o.P;
     out[6] = (int64_t)o.est_us;
     out[7] = M->ctx->world;
+    out[8] = M->dist_dense ? 1 : 0;
+    out[9] = M->dist_engine ? dist_pvar_chunks(M->dist_engine) : 0;
     return GPRX_OK;
     API_END(M ? M->ctx : nullptr)
 }

@@ -212,10 +212,14 @@ struct DistLayout {
 // returned on this stack: the sharded LML's 2.19 GB mailbox, a 2.1 GB rank storage at N = 32768)
 constexpr int64_t kIpcMaxBytes = (int64_t(1) << 31) - (int64_t(1) << 20);
 
+// query chunks of 128 columns one sharded posterior solve takes at most (its flag words)
+constexpr int kPvChunks = 64;
+
 // mailbox byte layout (identical on every rank): see PtDist / DSArgs.  The receive window is
 // not in it: its ww x nr tile slots are separate pieces below 2 GiB (WindowLayout)
 struct MailboxLayout {
-    int64_t o_linv = 0, o_z = 0, o_alpha = 0, o_zf = 0, o_part = 0, o_flags = 0, o_sflags = 0, o_tags = 0, bytes = 0;
+    int64_t o_linv = 0, o_z = 0, o_alpha = 0, o_zf = 0, o_part = 0, o_flags = 0, o_sflags = 0, o_tags = 0, o_vflags = 0,
+            bytes = 0;
     void init(int g, int nc, int nr, int ww, int m, size_t s, bool window) {
         const int64_t DB2 = (int64_t)DB * DB, np = (int64_t)nc * DB;
         int64_t o = 0;
@@ -233,6 +237,8 @@ struct MailboxLayout {
         o = align256(o + 4 * (dist_f_rel(nr, nc) + (int64_t)g * nc));
         o_sflags = o;
         o = align256(o + 4 * ((int64_t)(2 + g) * nc));
+        o_vflags = o;  // the posterior solve's V_k(c) flags (dist_posterior): nc x kPvChunks words
+        o = align256(o + 4 * (int64_t)nc * kPvChunks);
         o_tags = o;
         o = align256(o + 4 * (window ? (int64_t)ww * nr : 1));
         bytes = o;
@@ -265,6 +271,7 @@ struct DistRank {
     std::vector<std::vector<uint64_t>> st;  // every rank's storage pieces as mapped here
     std::vector<std::vector<uint64_t>> wp;  // every rank's window pieces as mapped here
     std::vector<int64_t> roff;         // own row blocks: element offset from the first piece's base
+    DMem t_vslot, pvpart, pvsum;       // posterior solve: window slots of V_k(c) on every rank, partial sums
     std::vector<void*> opened;         // IPC mappings to close
     T* sbase() const { return store.empty() ? nullptr : store[0]->template as<T>(); }
     int64_t store_bytes() const {
@@ -308,6 +315,9 @@ struct DistEngine : DistEngineBase {
     int64_t n = 0, np = 0;
     int m = 0;
     unsigned ep = 0, sep = 0;  // epochs of the fits and of the solves (flag values)
+    unsigned vep = 0;          // epoch of the posterior solves
+    int pv_nch = 0;            // query chunks per posterior solve (0: none: one rank, or no window)
+    DMem pvR;                  // the posterior solve's K(Z, X) / W (every local rank's blocks)
     std::vector<std::unique_ptr<DistRank<T>>> ranks;  // virtual: all g; otherwise this process's rank
     int* dbg = nullptr;  // GPRX_PT_DEBUG: the launch's per-workgroup status words (pinned host memory)
     int dbg_n = 0;
@@ -569,6 +579,7 @@ static void setup(DistEngine<T>& E, const DistContext& C, int64_t n, int m, bool
     const int nr = E.L.nr, nci = E.L.nci;
     E.MB.init(E.g, nc, nr, ww, m, sizeof(T), E.g > 1);
     E.WL.init(ww, nr, sizeof(T), piece_bytes, E.g > 1);
+    E.pv_nch = E.g > 1 ? (int)std::min<int64_t>(kPvChunks, E.WL.tiles / nc) : 0;
     GPRX_REQUIRE(E.virt || E.g == 1 || E.MB.bytes <= kIpcMaxBytes, GPRX_ERR_ARG,
                  "distributed fit: the mailbox would exceed 2 GiB, the largest allocation another process can map");
     const int64_t DB2 = (int64_t)DB * DB;
@@ -694,6 +705,18 @@ static void setup(DistEngine<T>& E, const DistContext& C, int64_t n, int m, bool
         upload_vec(R.t_loc, loc);
         upload_vec(R.t_roff, R.roff);
         upload_vec(R.t_wpc, wpc);
+        // the posterior solve's V_k(c) slots: tile t = c nc + k of every rank's window
+        if (E.g > 1 && E.pv_nch > 0) {
+            std::vector<uint64_t> vs((size_t)E.g * E.pv_nch * nc);
+            for (int q = 0; q < E.g; q++)
+                for (int c = 0; c < E.pv_nch; c++)
+                    for (int k = 0; k < nc; k++) {
+                        const int64_t t = (int64_t)c * nc + k;
+                        vs[((size_t)q * E.pv_nch + c) * nc + k] =
+                            R.wp[q][t / E.WL.tpp] + (uint64_t)((t % E.WL.tpp) * DB2 * (int64_t)sizeof(T));
+                    }
+            upload_vec(R.t_vslot, vs);
+        }
         upload_vec(R.t_own, E.L.own);
         upload_vec(R.t_tptr, tptr);
         upload_vec(R.t_cons, E.S.cons);
@@ -1115,6 +1138,118 @@ void dist_gather_factor(DistEngineBase* eng, T* A, int64_t ld, T* Linv, hipStrea
 }
 template void dist_gather_factor<double>(DistEngineBase*, double*, int64_t, double*, hipStream_t);
 template void dist_gather_factor<float>(DistEngineBase*, float*, int64_t, float*, hipStream_t);
+
+// ---------------------------------------------------------------------------------------
+// posterior covariance with the sharded factor: k(x, y) - (L^{-1} k_x) . (L^{-1} k_y) with no
+// rank holding more than its own rows of L (GaussianProcess::operator() / GetCredibleInterval,
+// lib/GaussianProcess.cpp:84-114; the reference uses C = K^{-1}, the same quantity)
+// ---------------------------------------------------------------------------------------
+namespace {
+// out[j] = sum over the rows li < nown of part[li][j] (fixed order)
+__global__ void pv_rowsum(const double* __restrict__ part, int nown, int64_t nq, double* __restrict__ out) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= nq) return;
+    double v = 0;
+    for (int li = 0; li < nown; li++) v += part[(int64_t)li * nq + j];
+    out[j] = v;
+}
+}  // namespace
+
+template <typename T>
+static int pv_chunks_of(DistEngineBase* eng) {
+    auto* E = dynamic_cast<DistEngine<T>*>(eng);
+    return (E && !E->ranks.empty()) ? E->pv_nch : -1;
+}
+int dist_pvar_chunks(DistEngineBase* eng) {
+    int v = pv_chunks_of<double>(eng);
+    if (v < 0) v = pv_chunks_of<float>(eng);
+    return std::max(0, v);
+}
+
+template <typename T>
+void dist_posterior(DistEngineBase* eng, const KCanon<T>& K, const T* X, const T* tabX, int64_t n, int d, const T* Z,
+                    const T* tabZ, int nch, bool pairs, std::vector<double>& sum, hipStream_t s) {
+    auto* Ep = dynamic_cast<DistEngine<T>*>(eng);
+    GPRX_REQUIRE(Ep && !Ep->ranks.empty() && Ep->pv_nch > 0, GPRX_ERR_STATE, "distributed posterior: no sharded factor");
+    DistEngine<T>& E = *Ep;
+    GPRX_REQUIRE(nch >= 1 && nch <= E.pv_nch, GPRX_ERR_ARG, "distributed posterior: too many query chunks");
+    const int nc = E.L.nc;
+    const int64_t np = E.np, nq = (int64_t)nch * DB;
+    // K(Z, X): nq x np, ld nq (the padding columns >= n stay zero); each rank's task overwrites its
+    // own blocks' columns with W = K - sum L V
+    if (E.pvR.bytes < sizeof(T) * (size_t)nq * np) E.pvR.alloc(sizeof(T) * (size_t)nq * np, false);
+    T* R = E.pvR.template as<T>();
+    GPRX_HIP(hipMemsetAsync(R, 0, sizeof(T) * (size_t)nq * np, s));
+    launch_kbuild<T>(K, Z, tabZ, nq, X, tabX, n, d, R, nq, 0, false, T(0), E.ranks[0]->flag.template as<int>(), s);
+    GPRX_HIP(hipStreamSynchronize(s));
+    host_barrier(E);  // every rank's previous use of its window (a fit, an earlier batch) is over
+    E.vep++;
+    for (auto& Rp : E.ranks) {
+        DistRank<T>& Rk = *Rp;
+        const size_t pb = sizeof(double) * std::max<size_t>(1, Rk.orows.size()) * (size_t)nq;
+        if (Rk.pvpart.bytes < pb) Rk.pvpart.alloc(pb, false);
+        if (Rk.pvsum.bytes < sizeof(double) * (size_t)nq) Rk.pvsum.alloc(sizeof(double) * (size_t)nq, false);
+        GPRX_HIP(hipMemsetAsync(Rk.sctl.p, 0, sizeof(int) * 8, Rk.s));
+        GPRX_HIP(hipMemsetD32Async((hipDeviceptr_t)Rk.info.p, INT_MAX, 1, Rk.s));
+        PVArgs<T> a;
+        std::memset(&a, 0, sizeof(a));
+        a.g = E.g;
+        a.r = Rk.r;
+        a.nc = nc;
+        a.loc = Rk.t_loc.template as<int>();
+        a.roff = Rk.t_roff.template as<int64_t>();
+        a.store = Rk.sbase();
+        a.orows = Rk.t_orows.template as<int>();
+        a.nown = (int)Rk.orows.size();
+        a.Linv = reinterpret_cast<const T*>(Rk.mbox.template as<char>() + E.MB.o_linv);
+        a.mb = Rk.t_mb.template as<uint64_t>();
+        a.o_vflags = E.MB.o_vflags;
+        a.vslot = Rk.t_vslot.template as<uint64_t>();
+        a.vstride = E.pv_nch;
+        a.R = R;
+        a.nch = nch;
+        a.pairs = pairs ? 1 : 0;
+        a.ep = E.vep;
+        a.part = Rk.pvpart.template as<double>();
+        a.ctl = Rk.sctl.template as<int>();
+        a.info = Rk.info.template as<int>();
+        a.tlimit = (long long)(1e8 * 4.0);
+        if (a.nown > 0) launch_dist_pvar<T>(a, E.P, Rk.s);
+    }
+    int hinfo = INT_MAX;
+    for (auto& Rp : E.ranks) {
+        int hi = 0;
+        GPRX_HIP(hipMemcpyAsync(&hi, Rp->info.p, sizeof(int), hipMemcpyDeviceToHost, Rp->s));
+        GPRX_HIP(hipStreamSynchronize(Rp->s));
+        hinfo = std::min(hinfo, hi);
+    }
+    if (agree_min(E, hinfo) != INT_MAX) throw Error{GPRX_ERR_HIP, "gprx: distributed posterior solve timed out (flag wait)"};
+    // this process's ranks' sums (rank order), then over the processes (rank order)
+    sum.assign((size_t)nq, 0.0);
+    std::vector<double> mine((size_t)nq);
+    for (auto& Rp : E.ranks) {
+        DistRank<T>& Rk = *Rp;
+        if (Rk.orows.empty()) continue;
+        hipLaunchKernelGGL(pv_rowsum, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, Rk.s,
+                           Rk.pvpart.template as<double>(), (int)Rk.orows.size(), nq, Rk.pvsum.template as<double>());
+        GPRX_HIP(hipMemcpyAsync(mine.data(), Rk.pvsum.p, sizeof(double) * nq, hipMemcpyDeviceToHost, Rk.s));
+        GPRX_HIP(hipStreamSynchronize(Rk.s));
+        for (int64_t j = 0; j < nq; j++) sum[j] += mine[j];
+    }
+    if (!E.virt && E.g > 1) {
+        std::vector<double> all((size_t)nq * E.g);
+        E.hc->allgather(sum.data(), sizeof(double) * nq, all.data());
+        for (int64_t j = 0; j < nq; j++) {
+            double v = 0;
+            for (int q = 0; q < E.g; q++) v += all[(size_t)q * nq + j];
+            sum[j] = v;
+        }
+    }
+}
+template void dist_posterior<double>(DistEngineBase*, const KCanon<double>&, const double*, const double*, int64_t, int,
+                                     const double*, const double*, int, bool, std::vector<double>&, hipStream_t);
+template void dist_posterior<float>(DistEngineBase*, const KCanon<float>&, const float*, const float*, int64_t, int,
+                                    const float*, const float*, int, bool, std::vector<double>&, hipStream_t);
 
 // ---------------------------------------------------------------------------------------
 // LML gradient from the ranks' C tiles

@@ -79,6 +79,15 @@ template <typename T>
 void dist_lml_grad(DistEngineBase* eng, const KCanon<T>& K, const KCanon<T>* Kd, const T* X, int64_t n, int d,
                    const T* FU, const T* FV, T* GU, T* GV, int64_t nf, const T* alpha, double* part, double* acc,
                    hipStream_t s);
+// The sharded posterior covariance (dist_pvar_kernel): the query chunks of 128 columns one solve
+// takes (0: not available -- one rank, or no receive window to carry the V tiles).
+int dist_pvar_chunks(DistEngineBase* eng);
+// sum[j] = sum over the n training rows of V[., j] V[., j'] with V = L^{-1} K(X, Z), Z = nch x 128
+// queries (device, row-major nch 128 x d; tabZ their sin/cos tables when K has periodic leaves),
+// j' = j, or (pairs) j' = j + 64 within each chunk of 128; summed over every rank (host result).
+template <typename T>
+void dist_posterior(DistEngineBase* eng, const KCanon<T>& K, const T* X, const T* tabX, int64_t n, int d, const T* Z,
+                    const T* tabZ, int nch, bool pairs, std::vector<double>& sum, hipStream_t s);
 // The rows this process's ranks own (row blocks of 128, the label block excluded), ascending.
 std::vector<int> dist_own_blocks(DistEngineBase* eng);
 // Sum over the ranks of `count` doubles in device memory (no-op for virtual ranks).
@@ -106,6 +115,37 @@ struct DSArgs {
     int* info;             // atomicMin -1 on a timed-out wait
     long long tlimit;
 };
+// ---- the sharded posterior covariance (k_dsolve.hip dist_pvar_kernel), one launch per rank ----
+// V = L^{-1} K(X, Z) for nch chunks of 128 query columns, by a distributed forward substitution:
+// task (own row block i, chunk c) accumulates sum_{k<i} L_ik V_k(c) on the MFMA tiles as the
+// V_k(c) of every rank arrive in its window, forms V_i(c) = Linv_i (K(X_i, Z_c) - sum), pushes it
+// into every rank's window slot (c, i) and adds its rows' sum of V[., j] V[., j'] (the
+// ||L^{-1} k||^2 of the pairs) to part.  No rank holds more than its own rows of L.
+template <typename T>
+struct PVArgs {
+    int g, r, nc;
+    const int* loc;          // [nr] local index of an own row block
+    const int64_t* roff;     // [nloc] element offset of local row block li in the packed storage
+    const T* store;          // this rank's packed row blocks
+    const int* orows;        // this rank's matrix row blocks (< nc), ascending
+    int nown;
+    const T* Linv;           // all nc diagonal inverses (this rank's mailbox)
+    const uint64_t* mb;      // [g] mailbox bases as mapped here (flags)
+    int64_t o_vflags;        // byte offset of the V flags: rank q's word (c nc + k) = ep when V_k(c) landed
+    const uint64_t* vslot;   // [(q vstride + c) nc + k] window slot of V_k(c) in rank q (DB x DB, (query, row))
+    int vstride;
+    T* R;                    // nch DB x np, ld nch DB: K(Z, X); W = K - sum L V overwrites the own blocks
+    int nch;                 // chunks of 128 query columns
+    int pairs;               // 0: column j with itself; 1: columns j and 64 + j of a chunk (j < 64)
+    unsigned ep;             // this solve's epoch
+    double* part;            // [nown][nch DB]: sum over block i's rows of V[., j] V[., j']
+    int* ctl;                // [4] ticket, error (zeroed)
+    int* info;               // atomicMin -1 on a timed-out wait
+    long long tlimit;
+};
+template <typename T>
+void launch_dist_pvar(const PVArgs<T>& a, int P, hipStream_t s);
+
 template <typename T>
 void launch_dist_back(const DSArgs<T>& a, hipStream_t s);
 template <typename T>

@@ -30,6 +30,7 @@
 // block).  The diagonal inverse of the block sits in LDS (loaded before any wait); waits are
 // bounded in wall-clock time.
 #include "gprx_dist.h"
+#include "k_mma.h"
 
 #include <algorithm>
 #include <climits>
@@ -355,7 +356,152 @@ __global__ __launch_bounds__(256) void dist_reduce_kernel(DSArgs<T> a, int64_t n
     }
 }
 
+// ---- the sharded posterior covariance ---------------------------------------------------------
+// One workgroup per CU of the rank's slice, tasks (own row block i, chunk c) claimed in i-major
+// order: a task waits only on V_k(c), k < i, produced by tasks of smaller i on every rank, each
+// rank claims its tickets in i order, so the smallest unfinished i always runs (no deadlock).
+template <typename T>
+__global__ __launch_bounds__(NT) void dist_pvar_kernel(PVArgs<T> a) {
+    typedef mm::Mfma<T> Tr;
+    typedef typename Tr::acc_t acc_t;
+    typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+    extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
+    T* smem = reinterpret_cast<T*>(s_dyn);
+    __shared__ int s_int[4];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6, lr = lane & 15, lk = lane >> 4;
+    const int wr = w & 1, wc = w >> 1;
+    const int64_t ldr = (int64_t)a.nch * DB;
+    constexpr int VS = DB + 16 / (int)sizeof(T);  // LDS stride of the V tile (rows of 16-B vectors, fewer conflicts)
+    const unsigned* vf0 = nullptr;
+    bool ok = true;
+    for (;;) {
+        if (w == 0) {
+            const int v = __hip_atomic_fetch_add(a.ctl + C_TICKET, (t == 0) ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_int[0] = __builtin_amdgcn_readfirstlane(v);
+        }
+        __syncthreads();
+        const int tk = __builtin_amdgcn_readfirstlane(s_int[0]);
+        if (tk >= a.nown * a.nch || !ok) break;
+        const int li = tk / a.nch, c = tk - li * a.nch;
+        const int i = __builtin_amdgcn_readfirstlane(a.orows[li]);
+        const T* Li = a.store + a.roff[__builtin_amdgcn_readfirstlane(a.loc[i])];  // 128 x 128 i, ld DB
+        vf0 = mb_flag(a.mb, a.r, a.o_vflags + 4 * (int64_t)c * a.nc);
+        // acc(m, q) = sum_{k < i} L_ik V_k(c)(row, q): the ready V_k in runs of at most 64 panels
+        acc_t acc[2][4];
+#pragma unroll
+        for (int x = 0; x < 2; x++)
+#pragma unroll
+            for (int y = 0; y < 4; y++) acc[x][y] = acc_t{0};
+        for (int k0 = 0; k0 < i && ok;) {
+            if (w == 0) {
+                const int nmax = min(64, i - k0);
+                const long long t0 = wall_clock64();
+                int nk = 0;
+                for (;;) {
+                    const bool good = lane >= nmax || ld_sys(vf0 + k0 + (lane < nmax ? lane : 0)) == a.ep;
+                    const unsigned long long bad = __ballot(!good);
+                    nk = bad ? (int)__builtin_ctzll(bad) : nmax;  // the ready prefix
+                    nk = __builtin_amdgcn_readfirstlane(nk);
+                    if (nk > 0) break;
+                    if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(a.ctl + C_ERR, __ATOMIC_RELAXED,
+                                                                         __HIP_MEMORY_SCOPE_AGENT))) break;
+                    if (wall_clock64() - t0 > a.tlimit) {
+                        __hip_atomic_store(a.ctl + C_ERR, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                // pushed data: no stale line of an earlier use of the window in this CU's or XCD's caches
+                if (nk > 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+                s_int[1] = nk;
+            }
+            __syncthreads();
+            const int nk = __builtin_amdgcn_readfirstlane(s_int[1]);
+            if (nk <= 0) {
+                ok = false;
+                break;
+            }
+            // (B unused with Bpan; a null B crashed hipcc 7.2's optimizer)
+            mm::tile_mma<T, 0, true>(acc, Li + (int64_t)k0 * DB * DB, DB, Li, DB, DB * nk, DB * nk, smem, t,
+                                     a.vslot + ((int64_t)a.r * a.vstride + c) * a.nc + k0);
+            __syncthreads();  // the staging ring is reused
+            k0 += nk;
+        }
+        if (!ok) break;
+        // W(q, m) = K(z_q, x_m) - acc(m, q), in place in R (chunk c's rows, block i's columns)
+        T* Wt = a.R + (int64_t)c * DB + (int64_t)i * DB * ldr;
+#pragma unroll
+        for (int x = 0; x < 2; x++)
+#pragma unroll
+            for (int y = 0; y < 4; y++)
+#pragma unroll
+                for (int reg = 0; reg < 4; reg++) {
+                    const int m = 64 * wr + 16 * y + lr, q = 32 * wc + 16 * x + Tr::orow(lk, reg);
+                    T* p = Wt + q + (int64_t)m * ldr;
+                    *p = *p - acc[x][y][reg];
+                }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        // V_i(c)(r, q) = sum_m Linv_i(r, m) W(q, m)
+        mm::tile_mma<T>(acc, a.Linv + (int64_t)i * DB * DB, DB, Wt, ldr, DB, DB, smem, t);
+        __syncthreads();  // ring done: the LDS takes V (q + r VS)
+#pragma unroll
+        for (int x = 0; x < 2; x++)
+#pragma unroll
+            for (int y = 0; y < 4; y++)
+#pragma unroll
+                for (int reg = 0; reg < 4; reg++) {
+                    const int rr = 64 * wr + 16 * y + lr, q = 32 * wc + 16 * x + Tr::orow(lk, reg);
+                    smem[q + rr * VS] = acc[x][y][reg];
+                }
+        __syncthreads();
+        // this block's share of |L^{-1} k|^2 (or of (L^{-1} k_a) . (L^{-1} k_b)) per query column
+        if (t < (a.pairs ? 64 : DB)) {
+            const int j2 = a.pairs ? 64 + t : t;
+            double sum = 0;
+            for (int rr = 0; rr < DB; rr++) sum += (double)smem[t + rr * VS] * (double)smem[j2 + rr * VS];
+            a.part[(int64_t)li * ldr + (int64_t)c * DB + t] = sum;
+        }
+        // V_i(c) into every rank's window slot (c, i): 16-B written-through stores, then the flags
+        {
+            constexpr int E = 16 / (int)sizeof(T), VPR = DB / E;  // elements per vector, vectors per row
+            constexpr int NV = DB * VPR / NT;
+            u4 v[NV];
+#pragma unroll
+            for (int u = 0; u < NV; u++) {
+                const int e = t + u * NT, rr = e / VPR, q = (e % VPR) * E;
+                v[u] = *reinterpret_cast<const u4*>(smem + q + rr * VS);
+            }
+            for (int q = 0; q < a.g; q++) {
+                u4* d4 = reinterpret_cast<u4*>(uni64(a.vslot[((int64_t)q * a.vstride + c) * a.nc + i]));
+#pragma unroll
+                for (int u = 0; u < NV; u++)
+                    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(d4 + t + u * NT), "v"(v[u]) : "memory");
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (w == 0)
+            for (int q = 0; q < a.g; q++) st_sys(mb_flag(a.mb, q, a.o_vflags + 4 * ((int64_t)c * a.nc + i)), a.ep);
+    }
+    if (t == 0 && __hip_atomic_load(a.ctl + C_ERR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(a.info, -1);
+}
+
 }  // namespace ds
+
+template <typename T>
+void launch_dist_pvar(const PVArgs<T>& a, int P, hipStream_t s) {
+    GPRX_REQUIRE(a.g <= 32 && a.nch >= 1 && a.nc >= 1 && P >= 1, GPRX_ERR_ARG, "dist posterior covariance: bad sizes");
+    const size_t lds = std::max(mm::gemm_lds<T>(), sizeof(T) * (size_t)DB * (DB + 16 / sizeof(T)));
+    static bool attr = false;
+    if (!attr) {
+        GPRX_HIP(hipFuncSetAttribute((const void*)ds::dist_pvar_kernel<T>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)lds));
+        attr = true;
+    }
+    hipLaunchKernelGGL(ds::dist_pvar_kernel<T>, dim3((unsigned)P), dim3(ds::NT), lds, s, a);
+    GPRX_HIP(hipGetLastError());
+}
 
 // dynamic LDS of the two solve kernels (the diagonal inverse, padded), set once per type
 template <typename T>
@@ -395,7 +541,8 @@ void launch_dist_reduce(const DSArgs<T>& a, int64_t n, double* out, hipStream_t 
 #define GPRX_INST(T)                                                          \
     template void launch_dist_back<T>(const DSArgs<T>&, hipStream_t);         \
     template void launch_dist_forward<T>(const DSArgs<T>&, hipStream_t);      \
-    template void launch_dist_reduce<T>(const DSArgs<T>&, int64_t, double*, hipStream_t);
+    template void launch_dist_reduce<T>(const DSArgs<T>&, int64_t, double*, hipStream_t);  \
+    template void launch_dist_pvar<T>(const PVArgs<T>&, int, hipStream_t);
 GPRX_INST(double)
 GPRX_INST(float)
 #undef GPRX_INST

@@ -62,14 +62,28 @@ struct Mfma<float> {
 constexpr int BKS = GPRX_PT_BKS;
 constexpr int NBUF = GPRX_PT_NBUF;
 constexpr int AHEAD = NBUF - 1;  // stages in flight ahead of the one being computed
-
+// k-columns per stage of the factorisation's products by precision (the pair statistics keep
+// BKS: their feature widths are multiples of 16).  GPRX_F32_BKS (A/B builds): f32 stages twice
+// as deep -- half the barriers per flop, the f64 stage's LDS bytes
+#ifndef GPRX_F32_BKS
+#define GPRX_F32_BKS 16
+#endif
 template <typename T>
+struct BkOf {
+    static constexpr int v = BKS;
+};
+template <>
+struct BkOf<float> {
+    static constexpr int v = GPRX_F32_BKS;
+};
+
+template <typename T, int BK = BkOf<T>::v>
 struct Stage {
     static constexpr int E = 16 / sizeof(T);     // elements per lane per load
     static constexpr int LPC = GT / E;           // lanes per column
     static constexpr int CPI = 64 / LPC;         // columns per wave-instruction
     static constexpr int SRP = CPI * GT + PAD;   // LDS elements per instruction slot
-    static constexpr int GRP = BKS / CPI;        // instructions per operand per stage
+    static constexpr int GRP = BK / CPI;         // instructions per operand per stage
     static constexpr int IPW = 2 * GRP / 8;      // instructions per wave per stage
     static constexpr int STG = 2 * GRP * SRP;    // elements per stage buffer (A slots, then B)
     // f32 (two columns per instruction): the second column of a pair is stored rotated by ROT
@@ -91,8 +105,8 @@ struct Stage {
 };
 
 template <typename T>
-constexpr size_t gemm_lds() {
-    return sizeof(T) * NBUF * Stage<T>::STG;
+constexpr size_t gemm_lds() {  // (the larger of the two stage depths a launch may use)
+    return sizeof(T) * NBUF * (Stage<T>::STG > Stage<T, BKS>::STG ? Stage<T>::STG : Stage<T, BKS>::STG);
 }
 
 template <typename T>
@@ -137,13 +151,14 @@ __device__ __forceinline__ void wave_block(int w, int& wr, int& wc) {
 // Bpan (optional): B given per 128-column panel -- column c of B at Bpan[c / 128] + (c % 128)
 // ldb (the distributed factorisation's received tiles: one packed 128 x 128 tile per panel,
 // ldb = 128, each panel in its own receive buffer).
-template <typename T, int MAP = 0>
+// ACC: acc += A B^T (acc is not cleared: consecutive K ranges into one accumulator).
+template <typename T, int MAP = 0, bool ACC = false, int BK = BkOf<T>::v>
 __device__ __forceinline__ void tile_mma(typename Mfma<T>::acc_t (&acc)[2][4], const T* __restrict__ A, int64_t lda,
                                          const T* __restrict__ B, int64_t ldb, int K, int kact, T* smem,
                                          const int t, const uint64_t* Bpan = nullptr) {
     typedef Mfma<T> Tr;
     typedef typename Tr::acc_t acc_t;
-    typedef Stage<T> S;
+    typedef Stage<T, BK> S;
     const int lane = t & 63, w = t >> 6;
     int wr, wc;
     wave_block<MAP>(w, wr, wc);
@@ -168,11 +183,11 @@ __device__ __forceinline__ void tile_mma(typename Mfma<T>::acc_t (&acc)[2][4], c
             const int g = w * S::IPW + u;  // wave-uniform slot: A 0..GRP-1, B GRP..2GRP-1
             const bool isB = g >= S::GRP;
             const int gg = isB ? g - S::GRP : g;
-            const int64_t col = (int64_t)st * BKS + gg * S::CPI + lcol;
+            const int64_t col = (int64_t)st * BK + gg * S::CPI + lcol;
             const T* src;
             if (isB && Bpan) {  // the stage's 16 columns lie in one 128-column panel
                 // (addresses as integers: a pointer-to-pointer operand crashed hipcc 7.2)
-                const int pn = (st * BKS) >> 7;
+                const int pn = (st * BK) >> 7;
                 const uint32_t lo = __builtin_amdgcn_readlane(bp_lo, pn);
                 const uint32_t hi = __builtin_amdgcn_readlane(bp_hi, pn);
                 const T* pb = reinterpret_cast<const T*>(((uint64_t)hi << 32) | lo);
@@ -185,12 +200,14 @@ __device__ __forceinline__ void tile_mma(typename Mfma<T>::acc_t (&acc)[2][4], c
         }
     };
 
+    if (!ACC) {
 #pragma unroll
-    for (int x = 0; x < 2; x++)
+        for (int x = 0; x < 2; x++)
 #pragma unroll
-        for (int y = 0; y < 4; y++) acc[x][y] = acc_t{0};
+            for (int y = 0; y < 4; y++) acc[x][y] = acc_t{0};
+    }
 
-    const int nst = K / BKS;
+    const int nst = K / BK;
 #pragma unroll
     for (int p = 0; p < AHEAD; p++)
         if (p < nst) issue(p);
@@ -212,7 +229,7 @@ __device__ __forceinline__ void tile_mma(typename Mfma<T>::acc_t (&acc)[2][4], c
     // triangle of a triangular B) are loops of their own with the same barriers: with a
     // wave-uniform test inside one loop, the accumulators merged from two paths every stage
     // (64 register moves, and a wait for the last MFMAs, per stage).
-    const int nmf = __builtin_amdgcn_readfirstlane(kact < K ? kact : K) / BKS;
+    const int nmf = __builtin_amdgcn_readfirstlane(kact < K ? kact : K) / BK;
     int st0 = 0;
     {
         const T* a0 = smem;
@@ -233,8 +250,8 @@ __device__ __forceinline__ void tile_mma(typename Mfma<T>::acc_t (&acc)[2][4], c
             };
             frag(0, 0);
 #pragma unroll
-            for (int kq = 0; kq < BKS / 4; kq++) {
-                if (kq + 1 < BKS / 4) frag(kq + 1, (kq + 1) & 1);
+            for (int kq = 0; kq < BK / 4; kq++) {
+                if (kq + 1 < BK / 4) frag(kq + 1, (kq + 1) & 1);
                 __builtin_amdgcn_sched_barrier(0);  // keep those reads ahead of these MFMAs
 #pragma unroll
                 for (int x = 0; x < 2; x++)
@@ -258,7 +275,7 @@ __device__ __forceinline__ void tile_mma(typename Mfma<T>::acc_t (&acc)[2][4], c
 template <typename T>
 __device__ __forceinline__ void ring_issue(const T* __restrict__ A, int64_t lda, const T* __restrict__ B, int64_t ldb,
                                            int st, T* smem, const int t) {
-    typedef Stage<T> S;
+    typedef Stage<T, BKS> S;
     const int lane = t & 63, w = t >> 6;
     const int lcol = lane / S::LPC, lrow = S::src_row(lane);
     T* buf = smem + (st % NBUF) * S::STG;
@@ -280,7 +297,7 @@ __device__ __forceinline__ void tile_mma2(typename Mfma<T>::acc_t (&acc1)[2][4],
                                           int K1, int K2, T* smem, const int t) {
     typedef Mfma<T> Tr;
     typedef typename Tr::acc_t acc_t;
-    typedef Stage<T> S;
+    typedef Stage<T, BKS> S;
     const int lane = t & 63, w = t >> 6;
     const int wr = w & 1, wc = w >> 1;
     const int lr = lane & 15, lk = lane >> 4;

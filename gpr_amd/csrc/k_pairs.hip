@@ -160,7 +160,7 @@ __global__ __launch_bounds__(NT) void predict_mma_kernel(const KCanon<T>* __rest
     // ring per block exposed its fill latency 128 times per workgroup).  Column norms and alpha
     // of a block go through LDS after the ring, double-buffered by block parity: block jb + 1's
     // are loaded at the end of block jb's epilogue (alpha = 0 masks the padding columns).
-    typedef Stage<T> S;
+    typedef Stage<T, BKS> S;
     typedef typename Tr::acc_t acc_t;
     T* nvs = smem + gemm_lds<T>() / sizeof(T);  // [2][GT]
     T* als = nvs + 2 * GT;                      // [2][GT]
@@ -427,7 +427,7 @@ __global__ __launch_bounds__(NT) void grad_mma_kernel(const KCanon<T>* __restric
     __syncthreads();
     typename Tr::acc_t ar[2][4];
     if (R2) {
-        tile_mma<T>(ar, FU + i0, nf, FV + j0, nv_, Kr, Kr, smem, t);
+        tile_mma<T, 0, false, BKS>(ar, FU + i0, nf, FV + j0, nv_, Kr, Kr, smem, t);
         load_weights();
         T nu[4];
 #pragma unroll
@@ -498,7 +498,7 @@ __global__ __launch_bounds__(NT) void grad_mma_kernel(const KCanon<T>* __restric
         const KLeaf<T>& L = Kd->leaf[lp];
         const T sc = L.p[0], sig = L.p[2], c1 = L.c1;
         if (R2) __syncthreads();  // the staging ring is reused
-        tile_mma<T>(ar, FU + (int64_t)Kr * nf + i0, nf, FV + (int64_t)Kr * nv_ + j0, nv_, Kp, Kp, smem, t);
+        tile_mma<T, 0, false, BKS>(ar, FU + (int64_t)Kr * nf + i0, nf, FV + (int64_t)Kr * nv_ + j0, nv_, Kp, Kp, smem, t);
         load_weights();
         double a0 = 0, a2 = 0;
         each([&](auto cc) {
@@ -518,7 +518,7 @@ __global__ __launch_bounds__(NT) void grad_mma_kernel(const KCanon<T>* __restric
         });
         __syncthreads();
         typename Tr::acc_t af[2][4];
-        tile_mma<T>(af, GU + i0, nf, GV + j0, nv_, Kf, Kf, smem, t);
+        tile_mma<T, 0, false, BKS>(af, GU + i0, nf, GV + j0, nv_, Kf, Kf, smem, t);
         double a1 = 0;
         each([&](auto cc) {
             constexpr int x = decltype(cc)::value >> 2, reg = decltype(cc)::value & 3;

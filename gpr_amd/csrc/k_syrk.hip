@@ -65,7 +65,7 @@ template <typename T>
 void launch_syrk_splitk(T* C, int64_t ldc, int64_t cstride, const T* A, int64_t lda, int64_t M, int64_t N, int64_t K,
                         int P, T alpha, hipStream_t s) {
     if (M <= 0 || N <= 0 || K <= 0 || P <= 0) return;
-    GPRX_REQUIRE(M % GT == 0 && N % GT == 0 && K % mm::BKS == 0 && lda % 2 == 0 && K <= INT32_MAX, GPRX_ERR_ARG,
+    GPRX_REQUIRE(M % GT == 0 && N % GT == 0 && K % mm::BkOf<T>::v == 0 && lda % 2 == 0 && K <= INT32_MAX, GPRX_ERR_ARG,
                  "launch_syrk_splitk: tile-aligned operands required");
     const int64_t ntm = M / GT, ntn = N / GT;
     const int64_t ntiles = ntn * (ntn + 1) / 2 + (ntm - ntn) * ntn;

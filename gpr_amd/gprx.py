@@ -449,9 +449,10 @@ class Model:
         """Layout and memory of the last distributed fit (gprx_dev_dist_info): per-rank device
         bytes of the engine and of the packed storage, row-block group, window panels, update
         chunk width, workgroups per rank, simulated makespan (us)."""
-        v = (ctypes.c_int64 * 8)()
+        v = (ctypes.c_int64 * 10)()
         self._c(lib().gprx_dev_dist_info(self.h, v))
-        keys = ["bytes_rank", "bytes_storage", "gb", "ww", "chunk_w", "P", "est_us", "world"]
+        keys = ["bytes_rank", "bytes_storage", "gb", "ww", "chunk_w", "P", "est_us", "world", "dense_factor",
+                "posterior_chunks"]
         return dict(zip(keys, list(v)))
 
     def alpha(self):

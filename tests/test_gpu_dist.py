@@ -292,6 +292,42 @@ def test_virtual_ranks_posterior_and_core(g):
         vctx.close()
 
 
+@pytest.mark.parametrize("g", [2, 3])
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_virtual_ranks_posterior_sharded(g, dtype):
+    """The posterior covariance on a sharded fit without the dense factor: the queries' forward
+    substitution runs across the ranks (dist_pvar_kernel: each rank's own rows of L, the query
+    columns V_k pushed through the receive windows, the row sums all-reduced).  Variances and
+    pairs (x != y) against the oracle; more queries than one solve takes (several batches); the
+    model must not have gathered the N x N factor, and no rank may hold more than its rows."""
+    import gpr_amd
+    n, d, sigma = 1400, 4, 0.5
+    X, Y = make_data(n, d, 1)
+    vctx = gpr_amd.Context(0, virtual=g)
+    try:
+        M, _ = _fit(vctx, C3K, X.astype(dtype), Y.astype(dtype), sigma, dtype)
+        info = M.dist_info()
+        assert info["posterior_chunks"] >= 1
+        Xd = X.astype(dtype).astype(np.float64)
+        _, C_ref = O.fit(C3K, Xd, Y.astype(dtype).astype(np.float64), sigma)
+        qn = info["posterior_chunks"] * 128 + 77  # more than one batch of variances
+        Xa = make_queries(qn, d).astype(dtype).astype(np.float64)
+        Xb = Xa[::-1].copy()
+        tol = TOL[np.dtype(dtype)]
+        for xb in (Xa, Xb):
+            c = M.posterior_cov(Xa.astype(dtype), xb.astype(dtype))
+            ref = O.posterior_cov(C3K, Xd, C_ref, Xa, xb)
+            kab = np.array([O.kernel_eval(C3K, a, b, with_grad=False) for a, b in zip(Xa, xb)])
+            # a difference of O(1) terms: compared on the scale of k(x, y), as on one GPU
+            assert np.max(np.abs(c - ref)) <= tol * max(1.0, np.max(np.abs(kab)))
+        after = M.dist_info()
+        assert after["dense_factor"] == 0
+        assert after["bytes_storage"] <= n * n * np.dtype(dtype).itemsize / g * 1.3 + 40 * 128 * 128 * 8
+        M.close()
+    finally:
+        vctx.close()
+
+
 def test_virtual_ranks_small_window(monkeypatch):
     """A 2-panel window (GPRX_DIST_WINDOW) and single-panel update chunks over 3 ranks: every
     window slot is refilled many times, so the release protocol (a producer may overwrite slot
