@@ -594,8 +594,9 @@ static void lu_fit_replicated(gprx_model* M, gprx_fit_info* out) {
     lu_fit<T>(M, out);
 }
 
-// The dense factor of a distributed fit on this process, for the calls that solve with the
-// whole factor (posterior covariance, core matrix, the VALU gradient's C): gathered once per
+// The dense factor of a distributed fit on this process, for the calls that need the whole
+// factor (the core matrix -- the reference returns all of C -- and the VALU gradient's C; the
+// posterior covariance solves across the ranks instead, model_posterior_cov_dist): gathered once per
 // fit from every rank's packed rows (device reads through the mappings of the mailboxes'
 // storage) into A (ld np) and Linv.  The one place a sharded fit holds N^2 on a process.
 template <typename T>

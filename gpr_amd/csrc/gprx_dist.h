@@ -68,8 +68,8 @@ void dist_engine_free(DistEngineBase* e);
 template <typename T>
 void dist_solve(DistEngineBase* eng, const T* rhs, T* out, hipStream_t s);
 // After a successful dist_fit: the dense factor on this process, gathered from every rank's
-// storage (a documented N^2 copy for the calls that need the whole factor: posterior covariance,
-// core matrix): the strictly-lower blocks of L into A (np x np, column-major, ld) and Linv.
+// storage (a documented N^2 copy for the calls that need the whole factor: the core matrix, a
+// VALU-gradient LML): the strictly-lower blocks of L into A (np x np, column-major, ld) and Linv.
 template <typename T>
 void dist_gather_factor(DistEngineBase* eng, T* A, int64_t ld, T* Linv, hipStream_t s);
 // After an LML-mode fit: this process's ranks' gradient partials of
