@@ -63,10 +63,11 @@ constexpr int BKS = GPRX_PT_BKS;
 constexpr int NBUF = GPRX_PT_NBUF;
 constexpr int AHEAD = NBUF - 1;  // stages in flight ahead of the one being computed
 // k-columns per stage of the factorisation's products by precision (the pair statistics keep
-// BKS: their feature widths are multiples of 16).  GPRX_F32_BKS (A/B builds): f32 stages twice
-// as deep -- half the barriers per flop, the f64 stage's LDS bytes
+// BKS: their feature widths are multiples of 16).  f32 stages are twice as deep (the f64
+// stage's LDS bytes, half the barriers per flop): C4's f32 factor 101.9 -> 98.6 ms, same-box
+// A/B (profiles/r04f); GPRX_F32_BKS=16 builds the round-3 depth
 #ifndef GPRX_F32_BKS
-#define GPRX_F32_BKS 16
+#define GPRX_F32_BKS 32
 #endif
 template <typename T>
 struct BkOf {

@@ -454,6 +454,19 @@ __device__ __forceinline__ void fact32(T* __restrict__ sS, T* __restrict__ sDi, 
             // the 4 x 4 pivot block (lower) of tile (tc, tc): P[i][j] at lane (pl + i) + 16 j;
             // its factor, then Q = L_P^{-1}, reduced to this lane's row qr = Q[lk][.]
             double qr[4];
+            // the panel operands a[r][k0 + i] of every row, gathered to the lanes of column i: their
+            // shuffles go out right after the last deferred MFMA of step st - 1 (the last write to
+            // this tile column), so their LDS latency hides under the pivot chain of column 3 and the
+            // 4 x 4 inverse instead of following them (GPRX_F32_LATE_SHFL: the round-3 order)
+            double sv[4][4];
+            auto gather_panel = [&]() {
+#pragma unroll
+                for (int tr = 0; tr < 4; tr++) {
+                    if (TI[tr][tc] < 0) continue;
+#pragma unroll
+                    for (int i = 0; i < 4; i++) sv[tr][i] = __shfl(acc[TI[tr][tc]][rg], lr + 16 * i, 64);
+                }
+            };
             {
                 double Lp[4][4], rq[4];
 #pragma unroll
@@ -461,6 +474,9 @@ __device__ __forceinline__ void fact32(T* __restrict__ sS, T* __restrict__ sDi, 
                     __builtin_amdgcn_sched_barrier(0);
                     deferred(i == 0 ? 0 : i + 1);
                     if (i == 0) deferred(1);
+#ifndef GPRX_F32_LATE_SHFL
+                    if (i == 3) gather_panel();
+#endif
                     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                     for (int j = 0; j < i; j++) {
@@ -507,6 +523,9 @@ __device__ __forceinline__ void fact32(T* __restrict__ sS, T* __restrict__ sDi, 
                 }
             }
             F32_MARK(f32_piv, qr[0] + qr[1] + qr[2] + qr[3]);
+#ifdef GPRX_F32_LATE_SHFL
+            gather_panel();
+#endif
             // panel: L[r][k0 + lk] = sum_{i <= lk} a[r][k0 + i] Q[lk][i] (D rows above k0 kept)
             double pv[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -515,7 +534,7 @@ __device__ __forceinline__ void fact32(T* __restrict__ sS, T* __restrict__ sDi, 
                 const double v = acc[TI[tr][tc]][rg];
                 double nv = 0.0;
 #pragma unroll
-                for (int i = 0; i < 4; i++) nv = fma(__shfl(v, lr + 16 * i, 64), qr[i], nv);
+                for (int i = 0; i < 4; i++) nv = fma(sv[tr][i], qr[i], nv);
                 const bool keep = tr < 2 && 16 * tr + lr < k0;
                 pv[tr] = keep ? v : nv;  // (pivot rows: masked out of the trailing operands)
                 acc[TI[tr][tc]][rg] = pv[tr];
