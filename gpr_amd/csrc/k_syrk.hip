@@ -38,7 +38,7 @@ __global__ __launch_bounds__(mm::NT) void syrk_splitk_kernel(T* __restrict__ C, 
     typedef mm::Mfma<T> Tr;
     typename Tr::acc_t acc[2][4];
     const int t = threadIdx.x;
-    mm::tile_mma<T>(acc, A + i0, lda, A + j0, lda, K, K, smem, t);
+    mm::tile_mma<T, 0, false, mm::BKS>(acc, A + i0, lda, A + j0, lda, K, K, smem, t);  // (K: multiples of 16)
     const int lane = t & 63, w = t >> 6;
     const int wr = w & 1, wc = w >> 1, lr = lane & 15, lk = lane >> 4;
     const bool diag = ti == tj;
@@ -65,7 +65,7 @@ template <typename T>
 void launch_syrk_splitk(T* C, int64_t ldc, int64_t cstride, const T* A, int64_t lda, int64_t M, int64_t N, int64_t K,
                         int P, T alpha, hipStream_t s) {
     if (M <= 0 || N <= 0 || K <= 0 || P <= 0) return;
-    GPRX_REQUIRE(M % GT == 0 && N % GT == 0 && K % mm::BkOf<T>::v == 0 && lda % 2 == 0 && K <= INT32_MAX, GPRX_ERR_ARG,
+    GPRX_REQUIRE(M % GT == 0 && N % GT == 0 && K % mm::BKS == 0 && lda % 2 == 0 && K <= INT32_MAX, GPRX_ERR_ARG,
                  "launch_syrk_splitk: tile-aligned operands required");
     const int64_t ntm = M / GT, ntn = N / GT;
     const int64_t ntiles = ntn * (ntn + 1) / 2 + (ntm - ntn) * ntn;
