@@ -87,6 +87,8 @@ struct Stage {
     static constexpr int GRP = BK / CPI;         // instructions per operand per stage
     static constexpr int IPW = 2 * GRP / 8;      // instructions per wave per stage
     static constexpr int STG = 2 * GRP * SRP;    // elements per stage buffer (A slots, then B)
+    static constexpr int NB = BK > 32 ? 2 : NBUF;  // ring buffers (deeper stages: fewer of them)
+    static constexpr int AH = NB - 1;              // stages in flight ahead of the one computed
     // f32 (two columns per instruction): the second column of a pair is stored rotated by ROT
     // rows.  The fragment reads are ds_read_b32 (banks (a/4) mod 32, lanes 0-31 one group):
     // lanes with lk = 0 and lk = 1 read k-columns kr and kr + 1 of one pair, 128 words apart --
@@ -107,7 +109,8 @@ struct Stage {
 
 template <typename T>
 constexpr size_t gemm_lds() {  // (the larger of the two stage depths a launch may use)
-    return sizeof(T) * NBUF * (Stage<T>::STG > Stage<T, BKS>::STG ? Stage<T>::STG : Stage<T, BKS>::STG);
+    return sizeof(T) * (Stage<T>::NB * Stage<T>::STG > NBUF * Stage<T, BKS>::STG ? Stage<T>::NB * Stage<T>::STG
+                                                                                  : NBUF * Stage<T, BKS>::STG);
 }
 
 template <typename T>
@@ -178,7 +181,7 @@ __device__ __forceinline__ void tile_mma(typename Mfma<T>::acc_t (&acc)[2][4], c
     }
 
     auto issue = [&](int st) {
-        T* buf = smem + (st % NBUF) * S::STG;
+        T* buf = smem + (st % S::NB) * S::STG;
 #pragma unroll
         for (int u = 0; u < S::IPW; u++) {
             const int g = w * S::IPW + u;  // wave-uniform slot: A 0..GRP-1, B GRP..2GRP-1
@@ -210,21 +213,21 @@ __device__ __forceinline__ void tile_mma(typename Mfma<T>::acc_t (&acc)[2][4], c
 
     const int nst = K / BK;
 #pragma unroll
-    for (int p = 0; p < AHEAD; p++)
+    for (int p = 0; p < S::AH; p++)
         if (p < nst) issue(p);
     // this wave's loads of stage st have landed (later stages may stay in flight), and every
     // wave's, and every wave is done reading the buffer refilled next; then the refill
     auto stage_sync = [&](int st) {
         const int ahead = nst - 1 - st;
-        if (AHEAD >= 3 && ahead >= 2) wait_vm<(AHEAD >= 3 ? 2 : 0) * S::IPW>();
-        else if (AHEAD >= 2 && ahead >= 1) wait_vm<S::IPW>();
+        if (S::AH >= 3 && ahead >= 2) wait_vm<(S::AH >= 3 ? 2 : 0) * S::IPW>();
+        else if (S::AH >= 2 && ahead >= 1) wait_vm<S::IPW>();
         else wait_vm<0>();
         // (Reading the next stage's first fragments before this barrier, so the MFMAs start
         // right after it, measured +0.5% alone but cost 3% inside the factorisation: it
         // shortens the load lead to two stages.)
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
-        if (st + AHEAD < nst) issue(st + AHEAD);
+        if (st + S::AH < nst) issue(st + S::AH);
     };
     // The MFMA stages and the idle ones (above the diagonal of a diagonal tile, beyond the
     // triangle of a triangular B) are loops of their own with the same barriers: with a
@@ -239,8 +242,8 @@ __device__ __forceinline__ void tile_mma(typename Mfma<T>::acc_t (&acc)[2][4], c
         for (int st = 0; st < nmf; st++) {
             stage_sync(st);
             // fragments of step kq+1 are read while the MFMAs of step kq run
-            const T* a = a0 + (st % NBUF) * S::STG;
-            const T* b = b0 + (st % NBUF) * S::STG;
+            const T* a = a0 + (st % S::NB) * S::STG;
+            const T* b = b0 + (st % S::NB) * S::STG;
             T fa[2][4], fb[2][2];
             auto frag = [&](int kq, int r) {
                 const int kr = kq * 4 + lk;
