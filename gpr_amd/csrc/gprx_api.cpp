@@ -965,12 +965,14 @@ static void model_inverse(gprx_model* M) {
 }
 
 // Host <-> device transfers use pageable caller memory: always synchronous, after the
-// work stream has drained (no async copies from/to pageable memory).
+// work stream has drained (no async copies from/to pageable memory).  An input may also be
+// device memory (unified addressing decides the direction, hipMemcpyDefault): a caller whose
+// samples already live in HBM passes them without a PCIe round trip.
 template <typename T>
 static void upload(DevBuf& b, const void* host, size_t bytes, hipStream_t s) {
     b.ensure(bytes);
     GPRX_HIP(hipStreamSynchronize(s));
-    if (bytes) GPRX_HIP(hipMemcpy(b.p, host, bytes, hipMemcpyHostToDevice));
+    if (bytes) GPRX_HIP(hipMemcpy(b.p, host, bytes, hipMemcpyDefault));
 }
 
 static void download(void* host, const void* dev, size_t bytes, hipStream_t s) {

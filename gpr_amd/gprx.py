@@ -207,7 +207,23 @@ def _dt(dtype):
 
 
 def _ptr(a):
-    return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
+    """Address of an input: a numpy array (host), or any object with data_ptr() -- e.g. a
+    torch CUDA tensor, device memory the library reads without a PCIe copy (gprx.h)."""
+    if a is None:
+        return None
+    if hasattr(a, "data_ptr"):
+        return ctypes.c_void_p(a.data_ptr())
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _input(a, dtype):
+    """A contiguous input of `dtype`: numpy arrays are converted, device tensors are taken as they are
+    (they must already be contiguous and of the model's dtype)."""
+    if hasattr(a, "data_ptr"):
+        if not a.is_contiguous() or str(a.dtype).replace("torch.", "") != np.dtype(dtype).name:
+            raise TypeError("device inputs must be contiguous and of the model's dtype")
+        return a
+    return np.ascontiguousarray(a, dtype)
 
 
 def device_count():
@@ -341,10 +357,11 @@ class Context:
         return A
 
     def sparse_fit(self, kernel, X, Y, Xm, sigma, jitter, dtype=np.float64):
-        X = np.ascontiguousarray(X, dtype)
-        Y = np.ascontiguousarray(Y, dtype)
+        """SparseGaussianProcess::Initialize; X, Y may be device tensors (no PCIe copy)."""
+        X = _input(X, dtype)
+        Y = _input(Y, dtype)
         if Y.ndim == 1:
-            Y = Y[:, None]
+            Y = Y[:, None] if not hasattr(Y, "data_ptr") else Y.reshape(-1, 1)
         Xm = np.ascontiguousarray(Xm, dtype)
         n, d = X.shape
         m = Y.shape[1]

@@ -279,6 +279,8 @@ gprx_status gprx_spd_inverse(gprx_ctx* ctx, gprx_dtype dtype, void* A, int64_t n
  * without the N x N core matrix (:309-311, infeasible at N = 1e6): returns Kmm^{-1}
  * (M x M), the regression vectors RV (M x m) and the regression matrix RM (M x M), all
  * host, row-major.  Any pointer may be NULL. */
+/* (X, Y and Xm may be host or device memory: unified addressing decides the copy's direction, so
+ * samples already resident in HBM are read without a PCIe transfer.) */
 gprx_status gprx_sparse_fit(gprx_ctx* ctx, gprx_dtype dtype, const gprx_kernel_desc* kernel, const void* X,
                             const void* Y, int64_t n, int32_t d, int32_t m, const void* Xm, int64_t M,
                             double sigma, double jitter, void* Kinv, void* RV, void* RM);

@@ -151,3 +151,20 @@ def test_sparse_lml_rccl_one_rank():
     finally:
         dctx.close()
         lctx.close()
+
+
+def test_sparse_fit_device_resident_inputs(ctx):
+    """X and Y already in HBM (a torch CUDA tensor's memory): the library reads them without a
+    PCIe copy (unified addressing picks the copy's direction) and returns the same bits as from
+    host arrays."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no torch CUDA device")
+    ks = "GaussianKernel(0.7,1.3,)"
+    X, Y, Xm = _inputs(3000, 4, 64, 1, np.float64)
+    host = ctx.sparse_fit(ks, X, Y, Xm, 0.3, 1e-4)
+    Xd, Yd = torch.from_numpy(X).to("cuda:0"), torch.from_numpy(Y).to("cuda:0")
+    torch.cuda.synchronize()
+    dev = ctx.sparse_fit(ks, Xd, Yd, Xm, 0.3, 1e-4)
+    for a, b in zip(host, dev):
+        assert np.array_equal(a, b)
