@@ -96,6 +96,16 @@ for step in "$@"; do
     diag)
         timeout -k 10 120 python scripts/diag_bench.py > "$O/diag_bench.json" 2> "$O/diag_bench.err" || fail diag $? "$O/diag_bench.err"
         ;;
+    probe)  # the tile mainloop alone per operand-feed variant (tools/probe/mma_probe*, built from scripts/mma_probe.hip)
+        for f in tools/probe/mma_probe*; do
+            for dt in f32 f64; do
+                for mode in 0 1; do
+                    timeout -k 10 60 "$f" $dt 4096 10 $mode 2> "$O/probe.err" | sed "s/^{/{\"bin\": \"$(basename "$f")\", /" >> "$O/mma_probe.jsonl" || fail probe $? "$O/probe.err"
+                done
+            done
+        done
+        cat "$O/mma_probe.jsonl"
+        ;;
     dist)
         timeout -k 10 300 python scripts/dist_time.py > "$O/dist_time.jsonl" 2> "$O/dist_time.err" || fail dist $? "$O/dist_time.err"
         ;;
