@@ -384,7 +384,9 @@ def main():
     ap.add_argument("--n", type=int, default=None)
     ap.add_argument("--d", type=int, default=None)
     ap.add_argument("--predict-q", type=int, default=65536)
-    ap.add_argument("--variance-q", type=int, default=4096, help="posterior-variance queries (0 = skip)")
+    ap.add_argument("--variance-q", type=int, default=None,
+                    help="posterior-variance queries (0 = skip; default SURVEY.md 8(d)'s Q = 65536 on one GPU, "
+                         "4096 on a sharded fit, whose distributed solve goes chunk by chunk)")
     ap.add_argument("--lml", type=int, default=1, help="also time one log-marginal likelihood + gradient "
                                                         "(BASELINE.json configs[2]); 0 = skip")
     ap.add_argument("--build-iters", type=int, default=3, help="time the covariance build alone (0 = skip)")
@@ -560,6 +562,8 @@ def main():
     # for Qv queries, query-sharded; the forward solve with Qv right-hand sides on the tile GEMM
     # (Qv N^2 flop) dominates.  Wall time of the call (queries up, variances down: small)
     var = None
+    if args.variance_q is None:
+        args.variance_q = 65536 if world == 1 else 4096
     if args.variance_q > 0 and want("variance"):
         Xv = make_queries(args.variance_q, d)
         lo, hi = gpr_amd.query_shard(args.variance_q, rank, world)

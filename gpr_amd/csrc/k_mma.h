@@ -78,6 +78,47 @@ struct BkOf<float> {
     static constexpr int v = GPRX_F32_BKS;
 };
 
+// tile_mma's operand feed by precision (scripts/mma_probe.hip decomposes the f64 stage: 4880
+// cycles against the 4096-cycle MFMA bound, of which the per-stage barrier costs ~330 and the
+// LDS-DMA refill ~400; profiles/r04q):
+//   late: the stage barrier sits inside the stage's last k-step -- it publishes the NEXT stage,
+//         whose first fragments are then read under this stage's remaining MFMAs, so the waves
+//         do not drain at the stage boundary (the refill's lead is one stage shorter);
+//   mid:  step kq+1's fragment reads are pinned after the first `mid` MFMAs of step kq (-1: read
+//         ahead of all of them, where hipcc then issued them behind the MFMAs and waited on
+//         them -- lgkmcnt(0), with an LDS-DMA pending -- before the next step's first MFMA).
+// f64: late + mid 2 + spread refill (probe 0.839 -> 0.873 of the bound; C3 launch 26.45 ->
+// 25.71 ms and the C5 syrk 2.47 -> 2.39 ms per launch, same box, profiles/r04s); f32: all off
+// (late + mid 2 cost C4's factor 3%: 100.8 -> 103.6 ms, r04q).
+// GPRX_MMA_LATE / GPRX_MMA_MID / GPRX_MMA_SPREAD force a form for both (A/B builds).
+#ifndef GPRX_PAIR_FEED
+#define GPRX_PAIR_FEED 0
+#endif
+#ifndef GPRX_SHORT_FEED
+#define GPRX_SHORT_FEED -1
+#endif
+template <typename T>
+struct FeedOf {
+#ifdef GPRX_MMA_LATE
+    static constexpr bool late = GPRX_MMA_LATE != 0;
+#else
+    static constexpr bool late = sizeof(T) == 8;
+#endif
+#ifdef GPRX_MMA_MID
+    static constexpr int mid = GPRX_MMA_MID;
+#else
+    static constexpr int mid = sizeof(T) == 8 ? 2 : -1;
+#endif
+    // late form: the refill's LDS-DMA issues one after each of the MFMAs that follow the
+    // barrier, not in a burst after it (each issue holds its wave ~60 cycles; behind an MFMA
+    // the pipe stays busy meanwhile): probe 0.860 -> 0.873, C3 launch 25.76 -> 25.71 ms
+#ifdef GPRX_MMA_SPREAD
+    static constexpr bool spread = GPRX_MMA_SPREAD != 0;
+#else
+    static constexpr bool spread = sizeof(T) == 8;
+#endif
+};
+
 template <typename T, int BK = BkOf<T>::v>
 struct Stage {
     static constexpr int E = 16 / sizeof(T);     // elements per lane per load
@@ -156,7 +197,9 @@ __device__ __forceinline__ void wave_block(int w, int& wr, int& wc) {
 // ldb (the distributed factorisation's received tiles: one packed 128 x 128 tile per panel,
 // ldb = 128, each panel in its own receive buffer).
 // ACC: acc += A B^T (acc is not cleared: consecutive K ranges into one accumulator).
-template <typename T, int MAP = 0, bool ACC = false, int BK = BkOf<T>::v>
+// FEED: -1 the precision's form (FeedOf), 0 the early barrier with reads ahead of each step
+// (the pair statistics' K = 32..96 products: the late form made the stand-alone build 4% slower)
+template <typename T, int MAP = 0, bool ACC = false, int BK = BkOf<T>::v, int FEED = -1>
 __device__ __forceinline__ void tile_mma(typename Mfma<T>::acc_t (&acc)[2][4], const T* __restrict__ A, int64_t lda,
                                          const T* __restrict__ B, int64_t ldb, int K, int kact, T* smem,
                                          const int t, const uint64_t* Bpan = nullptr) {
@@ -180,10 +223,9 @@ __device__ __forceinline__ void tile_mma(typename Mfma<T>::acc_t (&acc)[2][4], c
         bp_hi = (uint32_t)(v >> 32);
     }
 
-    auto issue = [&](int st) {
+    auto issue_u = [&](int st, int u) {
         T* buf = smem + (st % S::NB) * S::STG;
-#pragma unroll
-        for (int u = 0; u < S::IPW; u++) {
+        {
             const int g = w * S::IPW + u;  // wave-uniform slot: A 0..GRP-1, B GRP..2GRP-1
             const bool isB = g >= S::GRP;
             const int gg = isB ? g - S::GRP : g;
@@ -202,6 +244,10 @@ __device__ __forceinline__ void tile_mma(typename Mfma<T>::acc_t (&acc)[2][4], c
             __builtin_amdgcn_global_load_lds((const void*)src,
                                              (__attribute__((address_space(3))) void*)(buf + g * S::SRP), 16, 0, 0);
         }
+    };
+    auto issue = [&](int st) {
+#pragma unroll
+        for (int u = 0; u < S::IPW; u++) issue_u(st, u);
     };
 
     if (!ACC) {
@@ -234,41 +280,134 @@ __device__ __forceinline__ void tile_mma(typename Mfma<T>::acc_t (&acc)[2][4], c
     // wave-uniform test inside one loop, the accumulators merged from two paths every stage
     // (64 register moves, and a wait for the last MFMAs, per stage).
     const int nmf = __builtin_amdgcn_readfirstlane(kact < K ? kact : K) / BK;
-    int st0 = 0;
-    {
-        const T* a0 = smem;
-        const T* b0 = smem + S::GRP * S::SRP;
-#pragma nounroll
-        for (int st = 0; st < nmf; st++) {
-            stage_sync(st);
-            // fragments of step kq+1 are read while the MFMAs of step kq run
-            const T* a = a0 + (st % S::NB) * S::STG;
-            const T* b = b0 + (st % S::NB) * S::STG;
+    constexpr bool LATE = FEED < 0 && FeedOf<T>::late;
+    constexpr int MID = FEED < 0 ? FeedOf<T>::mid : -1;
+    if constexpr (LATE) {
+        // late barrier B_st inside stage st's last k-step (after MID of its MFMAs): stage
+        // st + 1 has landed for every wave and every wave is past stage st - 1, whose buffer takes
+        // stage st + AH; stage st + 1's first fragments are read right after it, under the rest of
+        // stage st's MFMAs
+        static_assert(S::AH >= 2 && MID >= 0, "late barrier: two stages ahead, mid-step reads");
+        constexpr bool SPREAD = FeedOf<T>::spread;
+        auto late_sync = [&](int st, bool refill) {
+            if (S::AH >= 3 && nst - 2 - st >= 1) wait_vm<(S::AH >= 3 ? 1 : 0) * S::IPW>();
+            else wait_vm<0>();
+            __builtin_amdgcn_s_barrier();
+            if (refill && st + S::AH < nst) issue(st + S::AH);
+        };
+        if (nst > 0) {  // stage 0 visible
+            if (S::AH >= 3 && nst >= 3) wait_vm<(S::AH >= 3 ? 2 : 0) * S::IPW>();
+            else if (S::AH >= 2 && nst >= 2) wait_vm<S::IPW>();
+            else wait_vm<0>();
+            __builtin_amdgcn_s_barrier();
+        }
+        {
+            const T* a0 = smem;
+            const T* b0 = smem + S::GRP * S::SRP;
             T fa[2][4], fb[2][2];
-            auto frag = [&](int kq, int r) {
+            auto frag = [&](int st, int kq, int r) {
+                const T* a = a0 + (st % S::NB) * S::STG;
+                const T* b = b0 + (st % S::NB) * S::STG;
                 const int kr = kq * 4 + lk;
 #pragma unroll
                 for (int x = 0; x < 2; x++) fb[r][x] = b[S::at(kr, wc * 32 + x * 16 + lr)];
 #pragma unroll
                 for (int y = 0; y < 4; y++) fa[r][y] = a[S::at(kr, wr * 64 + y * 16 + lr)];
             };
-            frag(0, 0);
+            if (nmf > 0) frag(0, 0, 0);
+            constexpr int KQ = BK / 4;
+            static_assert(KQ % 2 == 0, "late barrier: an even number of k-steps per stage");
+#pragma nounroll
+            for (int st = 0; st < nmf; st++) {
 #pragma unroll
-            for (int kq = 0; kq < BK / 4; kq++) {
-                if (kq + 1 < BK / 4) frag(kq + 1, (kq + 1) & 1);
-                __builtin_amdgcn_sched_barrier(0);  // keep those reads ahead of these MFMAs
+                for (int kq = 0; kq < KQ; kq++) {
+                    int m = 0;
 #pragma unroll
-                for (int x = 0; x < 2; x++)
+                    for (int x = 0; x < 2; x++)
 #pragma unroll
-                    for (int y = 0; y < 4; y++)
-                        if (MAP != 2 || 4 * wr + y >= 2 * wc + x)  // (MAP 2: wave-uniform tile skip)
-                            acc[x][y] = Tr::mma(fb[kq & 1][x], fa[kq & 1][y], acc[x][y]);
+                        for (int y = 0; y < 4; y++) {
+                            if (m == MID) {
+                                __builtin_amdgcn_sched_barrier(0);
+                                if (kq + 1 < KQ) {
+                                    frag(st, kq + 1, (kq + 1) & 1);
+                                } else {
+                                    late_sync(st, !SPREAD);
+                                    if (st + 1 < nmf) frag(st + 1, 0, 0);
+                                }
+                                __builtin_amdgcn_sched_barrier(0);
+                            }
+                            if (MAP != 2 || 4 * wr + y >= 2 * wc + x)
+                                acc[x][y] = Tr::mma(fb[kq & 1][x], fa[kq & 1][y], acc[x][y]);
+                            if (SPREAD && kq == KQ - 1 && m > MID && m - MID - 1 < S::IPW) {
+                                __builtin_amdgcn_sched_barrier(0);
+                                if (st + S::AH < nst) issue_u(st + S::AH, m - MID - 1);
+                                __builtin_amdgcn_sched_barrier(0);
+                            }
+                            m++;
+                        }
+                }
             }
         }
-        st0 = nmf;
-    }
 #pragma nounroll
-    for (int st = st0; st < nst; st++) stage_sync(st);
+        for (int st = nmf; st < nst; st++) late_sync(st, true);
+    } else {
+        int st0 = 0;
+        {
+            const T* a0 = smem;
+            const T* b0 = smem + S::GRP * S::SRP;
+#pragma nounroll
+            for (int st = 0; st < nmf; st++) {
+                stage_sync(st);
+                // fragments of step kq+1 are read while the MFMAs of step kq run
+                const T* a = a0 + (st % S::NB) * S::STG;
+                const T* b = b0 + (st % S::NB) * S::STG;
+                T fa[2][4], fb[2][2];
+                auto frag = [&](int kq, int r) {
+                    const int kr = kq * 4 + lk;
+#pragma unroll
+                    for (int x = 0; x < 2; x++) fb[r][x] = b[S::at(kr, wc * 32 + x * 16 + lr)];
+#pragma unroll
+                    for (int y = 0; y < 4; y++) fa[r][y] = a[S::at(kr, wr * 64 + y * 16 + lr)];
+                };
+                frag(0, 0);
+                if constexpr (MID < 0) {
+#pragma unroll
+                    for (int kq = 0; kq < BK / 4; kq++) {
+                        if (kq + 1 < BK / 4) frag(kq + 1, (kq + 1) & 1);
+                        __builtin_amdgcn_sched_barrier(0);  // keep those reads ahead of these MFMAs
+#pragma unroll
+                        for (int x = 0; x < 2; x++)
+#pragma unroll
+                            for (int y = 0; y < 4; y++)
+                                if (MAP != 2 || 4 * wr + y >= 2 * wc + x)  // (MAP 2: wave-uniform tile skip)
+                                    acc[x][y] = Tr::mma(fb[kq & 1][x], fa[kq & 1][y], acc[x][y]);
+                    }
+                } else {
+                    // step kq+1's fragment reads pinned after the first MID MFMAs of step kq
+#pragma unroll
+                    for (int kq = 0; kq < BK / 4; kq++) {
+                        int m = 0;
+#pragma unroll
+                        for (int x = 0; x < 2; x++)
+#pragma unroll
+                            for (int y = 0; y < 4; y++) {
+                                if (m == MID) {
+                                    __builtin_amdgcn_sched_barrier(0);
+                                    if (kq + 1 < BK / 4) frag(kq + 1, (kq + 1) & 1);
+                                    __builtin_amdgcn_sched_barrier(0);
+                                }
+                                if (MAP != 2 || 4 * wr + y >= 2 * wc + x)  // (MAP 2: wave-uniform tile skip)
+                                    acc[x][y] = Tr::mma(fb[kq & 1][x], fa[kq & 1][y], acc[x][y]);
+                                m++;
+                            }
+                    }
+                }
+            }
+            st0 = nmf;
+        }
+#pragma nounroll
+        for (int st = st0; st < nst; st++) stage_sync(st);
+    }
 }
 
 // Two products over consecutive column ranges of the same operands in ONE pass of the

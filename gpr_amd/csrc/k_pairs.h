@@ -102,10 +102,10 @@ __device__ __forceinline__ void block_stats(const T* FU, int64_t nu, int64_t i0,
         tile_mma2<T>(ar, ap, FU + i0, nu, FV + j0, nv, Kr, Kp, smem, t);
         return;
     }
-    if (R2) tile_mma<T, 0, false, BKS>(ar, FU + i0, nu, FV + j0, nv, Kr, Kr, smem, t);
+    if (R2) tile_mma<T, 0, false, BKS, GPRX_PAIR_FEED>(ar, FU + i0, nu, FV + j0, nv, Kr, Kr, smem, t);
     if (NPER) {
         __syncthreads();  // the second product reuses the staging ring
-        tile_mma<T, 0, false, BKS>(ap, FU + (int64_t)Kr * nu + i0, nu, FV + (int64_t)Kr * nv + j0, nv, Kp, Kp, smem, t);
+        tile_mma<T, 0, false, BKS, GPRX_PAIR_FEED>(ap, FU + (int64_t)Kr * nu + i0, nu, FV + (int64_t)Kr * nv + j0, nv, Kp, Kp, smem, t);
     }
 }
 
@@ -332,7 +332,7 @@ __device__ __forceinline__ bool build_tile_sum(const KCanon<T>* __restrict__ Kd,
         fn(std::integral_constant<int, 7>{});
     };
     if (R2) {
-        tile_mma<T, 0, false, BKS>(ar, FU + i0, nf, FV + j0, nf, Kr, Kr, smem, t);
+        tile_mma<T, 0, false, BKS, GPRX_PAIR_FEED>(ar, FU + i0, nf, FV + j0, nf, Kr, Kr, smem, t);
         T nu[4];
 #pragma unroll
         for (int y = 0; y < 4; y++) nu[y] = FU[(int64_t)(Kr + Kp) * nf + i0 + wr * 64 + y * 16 + lr];
@@ -354,7 +354,7 @@ __device__ __forceinline__ bool build_tile_sum(const KCanon<T>* __restrict__ Kd,
     }
     if (NPER) {
         if (R2) __syncthreads();  // the second product reuses the staging ring
-        tile_mma<T, 0, false, BKS>(ap, FU + (int64_t)Kr * nf + i0, nf, FV + (int64_t)Kr * nf + j0, nf, Kp, Kp, smem, t);
+        tile_mma<T, 0, false, BKS, GPRX_PAIR_FEED>(ap, FU + (int64_t)Kr * nf + i0, nf, FV + (int64_t)Kr * nf + j0, nf, Kp, Kp, smem, t);
     }
     bool bad = false;
     each([&](auto cc) {

@@ -427,7 +427,7 @@ __global__ __launch_bounds__(NT) void grad_mma_kernel(const KCanon<T>* __restric
     __syncthreads();
     typename Tr::acc_t ar[2][4];
     if (R2) {
-        tile_mma<T, 0, false, BKS>(ar, FU + i0, nf, FV + j0, nv_, Kr, Kr, smem, t);
+        tile_mma<T, 0, false, BKS, GPRX_PAIR_FEED>(ar, FU + i0, nf, FV + j0, nv_, Kr, Kr, smem, t);
         load_weights();
         T nu[4];
 #pragma unroll
@@ -498,7 +498,7 @@ __global__ __launch_bounds__(NT) void grad_mma_kernel(const KCanon<T>* __restric
         const KLeaf<T>& L = Kd->leaf[lp];
         const T sc = L.p[0], sig = L.p[2], c1 = L.c1;
         if (R2) __syncthreads();  // the staging ring is reused
-        tile_mma<T, 0, false, BKS>(ar, FU + (int64_t)Kr * nf + i0, nf, FV + (int64_t)Kr * nv_ + j0, nv_, Kp, Kp, smem, t);
+        tile_mma<T, 0, false, BKS, GPRX_PAIR_FEED>(ar, FU + (int64_t)Kr * nf + i0, nf, FV + (int64_t)Kr * nv_ + j0, nv_, Kp, Kp, smem, t);
         load_weights();
         double a0 = 0, a2 = 0;
         each([&](auto cc) {
@@ -518,7 +518,7 @@ __global__ __launch_bounds__(NT) void grad_mma_kernel(const KCanon<T>* __restric
         });
         __syncthreads();
         typename Tr::acc_t af[2][4];
-        tile_mma<T, 0, false, BKS>(af, GU + i0, nf, GV + j0, nv_, Kf, Kf, smem, t);
+        tile_mma<T, 0, false, BKS, GPRX_PAIR_FEED>(af, GU + i0, nf, GV + j0, nv_, Kf, Kf, smem, t);
         double a1 = 0;
         each([&](auto cc) {
             constexpr int x = decltype(cc)::value >> 2, reg = decltype(cc)::value & 3;

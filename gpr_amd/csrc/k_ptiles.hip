@@ -67,7 +67,7 @@ static_assert(C_NCTL == C_NCTL_DIST, "counter block layout shared with gprx_dist
 // ------------------------------------------------------------------------------------------
 // Bpan: B by 128-column panels (tile_mma): the distributed factorisation's window tiles.
 // MAP: the wave -> output-block map (k_mma.h wave_block): 1 for triangular B, 2 for lower.
-template <typename T, bool UPDATE, int MAP = 0>
+template <typename T, bool UPDATE, int MAP = 0, int FEED = -1>
 __device__ __forceinline__ void tile_gemm(T* __restrict__ C, int64_t ldc, const T* __restrict__ A, int64_t lda,
                                           const T* __restrict__ B, int64_t ldb, int K, bool lower, T* smem,
                                           const int t, bool tri = false, const uint64_t* Bpan = nullptr) {
@@ -94,7 +94,8 @@ __device__ __forceinline__ void tile_gemm(T* __restrict__ C, int64_t ldc, const 
             }
     }
     acc_t acc[2][4];
-    tile_mma<T, MAP>(acc, A, lda, B, ldb, K, !active ? 0 : (tri ? 32 * (wc + 1) : K), smem, t, Bpan);
+    tile_mma<T, MAP, false, BkOf<T>::v, FEED>(acc, A, lda, B, ldb, K, !active ? 0 : (tri ? 32 * (wc + 1) : K), smem, t,
+                                           Bpan);
     if (!active) return;
 #pragma unroll
     for (int x = 0; x < 2; x++) {
@@ -2241,7 +2242,7 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
                 if (!loc && wv == 0) dist_release(D, b0, nb);  // this chunk's window reads are done
             } else if (type == T_TRSM) {
                 T* Cik = dist_tile(a.A, D, i, j);
-                tile_gemm<T, false, 1>(Cik, DB, Cik, DB, a.Linv + (int64_t)j * DB * DB, DB, GT, false, smem, tid, true);
+                tile_gemm<T, false, 1, GPRX_SHORT_FEED>(Cik, DB, Cik, DB, a.Linv + (int64_t)j * DB * DB, DB, GT, false, smem, tid, true);
                 publish(a.lcnt + i, j + 1, false);
                 if (i == D.nc) {  // the label rows z^T: every other rank's z area (the solves read it)
                     const unsigned all = ((1u << D.g) - 1u) & ~(1u << D.r);
@@ -2269,10 +2270,10 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
                 } else if (fused_ts && k > 0) {
                     diagx_ts<T>(Akm, Akk, DB, a.Linv + (int64_t)(k - 1) * DB * DB, a.lcnt + k, k, smem, tid, false);
                 } else if (k > 0) {
-                    tile_gemm<T, false, 1>(Akm, DB, Akm, DB, a.Linv + (int64_t)(k - 1) * DB * DB, DB, GT, false, smem,
+                    tile_gemm<T, false, 1, GPRX_SHORT_FEED>(Akm, DB, Akm, DB, a.Linv + (int64_t)(k - 1) * DB * DB, DB, GT, false, smem,
                                            tid, true);
                     publish(a.lcnt + k, k, false);
-                    tile_gemm<T, true, 2>(Akk, DB, Akm, DB, Akm, DB, GT, true, smem, tid);
+                    tile_gemm<T, true, 2, GPRX_SHORT_FEED>(Akk, DB, Akm, DB, Akm, DB, GT, true, smem, tid);
                     local_sync();
                 }
                 diag_factor<T>(Akk, DB, a.Linv + (int64_t)k * DB * DB, a.info, (int64_t)k * DB, smem_raw, tid, a.dbg,
@@ -2339,7 +2340,7 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
         } else if (type == T_TRSM) {
             T* Cik = Ci + (int64_t)j * GT * ld;
             if (!(a.variant & 1))
-                tile_gemm<T, false, 1>(Cik, ld, Cik, ld, a.Linv + (int64_t)j * DB * DB, DB, GT, false, smem, tid, true);
+                tile_gemm<T, false, 1, GPRX_SHORT_FEED>(Cik, ld, Cik, ld, a.Linv + (int64_t)j * DB * DB, DB, GT, false, smem, tid, true);
             publish(a.lcnt + i, j + 1, false);
         } else {  // DIAGX(k = i)
             const int k = i;
@@ -2356,12 +2357,12 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
                 dt[1] = dt[0];
             } else if (k > 0) {
                 T* Akm = Ci + (int64_t)(k - 1) * GT * ld;
-                tile_gemm<T, false, 1>(Akm, ld, Akm, ld, a.Linv + (int64_t)(k - 1) * DB * DB, DB, GT, false, smem,
+                tile_gemm<T, false, 1, GPRX_SHORT_FEED>(Akm, ld, Akm, ld, a.Linv + (int64_t)(k - 1) * DB * DB, DB, GT, false, smem,
                                        tid, true);
                 if (a.trace) dt[0] = wall_clock64();
                 publish(a.lcnt + k, k, false);  // L_{k,k-1} final: unblocks the updates of column k
                 if (a.trace) dt[1] = wall_clock64();
-                tile_gemm<T, true, 2>(Akk, ld, Akm, ld, Akm, ld, GT, true, smem, tid);
+                tile_gemm<T, true, 2, GPRX_SHORT_FEED>(Akk, ld, Akm, ld, Akm, ld, GT, true, smem, tid);
                 local_sync();
             }
             if (a.trace) dt[2] = wall_clock64();
