@@ -289,6 +289,7 @@ __device__ __forceinline__ void tile_mma(typename Mfma<T>::acc_t (&acc)[2][4], c
         // stage st's MFMAs
         static_assert(S::AH >= 2 && MID >= 0, "late barrier: two stages ahead, mid-step reads");
         constexpr bool SPREAD = FeedOf<T>::spread;
+        static_assert(!SPREAD || MID + S::IPW < 8, "spread refill: a DMA behind each MFMA after the barrier");
         auto late_sync = [&](int st, bool refill) {
             if (S::AH >= 3 && nst - 2 - st >= 1) wait_vm<(S::AH >= 3 ? 1 : 0) * S::IPW>();
             else wait_vm<0>();
