@@ -304,14 +304,12 @@ def run_configs(args, world, rank, local_rank, dctx, max_over_ranks, barrier_syn
         ctx = dctx if (world > 1 and dctx is not None) else gpr_amd.Context(local_rank)
         # the rank's rows resident in HBM before the timed region (the value's rule); the
         # PCIe-inclusive rate from host arrays is reported beside it
+        # (the library's own device buffers: torch's bundled HIP runtime cannot allocate once
+        # this library owns the device, so torch CUDA tensors are not an option here)
         resident = False
         try:
-            import torch
-            if torch.cuda.is_available():
-                Xr = torch.from_numpy(Xl).to(f"cuda:{local_rank}")
-                Yr = torch.from_numpy(Yl).to(f"cuda:{local_rank}")
-                torch.cuda.synchronize()
-                resident = True
+            Xr, Yr = ctx.device_array(Xl), ctx.device_array(Yl)
+            resident = True
         except Exception as e:  # (the host arrays then, labelled)
             log("C5: device-resident inputs unavailable:", e)
         Xin, Yin = (Xr, Yr) if resident else (Xl, Yl)

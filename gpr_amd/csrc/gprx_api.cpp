@@ -2478,6 +2478,54 @@ gprx_status gprx_ctx_set_stats(gprx_ctx* ctx, int32_t enable) {
     API_END(ctx)
 }
 
+gprx_status gprx_device_alloc(gprx_ctx* ctx, int64_t bytes, void** out) {
+    API_BEGIN
+    GPRX_REQUIRE(ctx && out && bytes >= 0, GPRX_ERR_ARG, "gprx_device_alloc: NULL argument or negative size");
+    *out = nullptr;
+    if (bytes == 0) return GPRX_OK;
+    void* p = nullptr;
+    GPRX_HIP(hipSetDevice(ctx->device));
+    const hipError_t e = hipMalloc(&p, (size_t)bytes);
+    if (e != hipSuccess)
+        throw Error{GPRX_ERR_OOM, std::string("gprx_device_alloc: hipMalloc: ") + hipGetErrorString(e)};
+    *out = p;
+    return GPRX_OK;
+    API_END(ctx)
+}
+
+gprx_status gprx_device_free(gprx_ctx* ctx, void* p) {
+    API_BEGIN
+    GPRX_REQUIRE(ctx, GPRX_ERR_ARG, "gprx_device_free: NULL ctx");
+    if (p) {
+        GPRX_HIP(hipStreamSynchronize(ctx->stream));  // (no launch may still read it)
+        GPRX_HIP(hipFree(p));
+    }
+    return GPRX_OK;
+    API_END(ctx)
+}
+
+gprx_status gprx_device_upload(gprx_ctx* ctx, void* dst, const void* src, int64_t bytes) {
+    API_BEGIN
+    GPRX_REQUIRE(ctx && (bytes == 0 || (dst && src)) && bytes >= 0, GPRX_ERR_ARG, "gprx_device_upload: bad argument");
+    if (bytes > 0) {
+        GPRX_HIP(hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyHostToDevice, ctx->stream));
+        GPRX_HIP(hipStreamSynchronize(ctx->stream));
+    }
+    return GPRX_OK;
+    API_END(ctx)
+}
+
+gprx_status gprx_device_download(gprx_ctx* ctx, void* dst, const void* src, int64_t bytes) {
+    API_BEGIN
+    GPRX_REQUIRE(ctx && (bytes == 0 || (dst && src)) && bytes >= 0, GPRX_ERR_ARG, "gprx_device_download: bad argument");
+    if (bytes > 0) {
+        GPRX_HIP(hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDeviceToHost, ctx->stream));
+        GPRX_HIP(hipStreamSynchronize(ctx->stream));
+    }
+    return GPRX_OK;
+    API_END(ctx)
+}
+
 gprx_status gprx_ctx_get_stats(gprx_ctx* ctx, gprx_kstat* out, int32_t max, int32_t* count) {
     API_BEGIN
     GPRX_REQUIRE(ctx, GPRX_ERR_ARG, "gprx_ctx_get_stats: NULL ctx");

@@ -45,6 +45,7 @@ EXPORTED = [
     "gprx_sparse_fit", "gprx_ctx_set_stats", "gprx_ctx_get_stats",
     "gprx_model_set_kernel_matrix", "gprx_model_predict_kx", "gprx_model_posterior_cov_kx", "gprx_model_lml_dk",
     "gprx_model_set_sparse_cov", "gprx_sparse_lml",
+    "gprx_device_alloc", "gprx_device_free", "gprx_device_upload", "gprx_device_download",
 ]
 
 
@@ -112,6 +113,10 @@ def lib():
         L.gprx_last_error.restype = ctypes.c_char_p
         L.gprx_last_error.argtypes = [ctypes.c_void_p]
         L.gprx_ctx_create.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
+        L.gprx_device_alloc.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_void_p)]
+        L.gprx_device_free.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        L.gprx_device_upload.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
+        L.gprx_device_download.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
         L.gprx_ctx_create_dist.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                            ctypes.POINTER(ctypes.c_void_p)]
         L.gprx_ctx_create_peer.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ALLGATHER_FN, ctypes.c_void_p,
@@ -247,6 +252,67 @@ def query_shard(q, rank, world):
     return (q * rank) // world, (q * (rank + 1)) // world
 
 
+class DeviceArray:
+    """A copy of a host array in the context's device memory (gprx_device_alloc): inputs that stay
+    resident in HBM across calls.  Passes wherever the API takes device inputs (data_ptr()).
+    (A framework's CUDA tensors cannot serve once this library owns the device when the framework
+    bundles its own HIP runtime, as the PyTorch wheel does.)"""
+
+    def __init__(self, ctx, a=None, *, _base=None, _shape=None):
+        if _base is not None:  # a reshaped view of _base's buffer
+            self.ctx, self.p, self.dtype, self._base = _base.ctx, _base.p, _base.dtype, _base
+            self.shape = tuple(_shape)
+            return
+        a = np.ascontiguousarray(a)
+        self.ctx, self.dtype, self.shape, self._base = ctx, a.dtype, a.shape, None
+        p = ctypes.c_void_p()
+        ctx._c(lib().gprx_device_alloc(ctx.h, a.nbytes, ctypes.byref(p)))
+        self.p = p.value
+        ctx._c(lib().gprx_device_upload(ctx.h, ctypes.c_void_p(self.p), a.ctypes.data_as(ctypes.c_void_p),
+                                        a.nbytes))
+
+    @property
+    def ndim(self):
+        return len(self.shape)
+
+    @property
+    def nbytes(self):
+        return int(np.prod(self.shape)) * self.dtype.itemsize
+
+    def data_ptr(self):
+        return self.p or 0
+
+    def is_contiguous(self):
+        return True
+
+    def reshape(self, *shape):
+        shape = shape[0] if len(shape) == 1 and isinstance(shape[0], tuple) else shape
+        shape = list(shape)
+        if -1 in shape:
+            k = shape.index(-1)
+            shape[k] = int(np.prod(self.shape)) // int(np.prod([s for s in shape if s != -1]))
+        if int(np.prod(shape)) != int(np.prod(self.shape)):
+            raise ValueError("cannot reshape")
+        return DeviceArray(None, _base=self._base or self, _shape=shape)
+
+    def numpy(self):
+        out = np.empty(self.shape, self.dtype)
+        self.ctx._c(lib().gprx_device_download(self.ctx.h, out.ctypes.data_as(ctypes.c_void_p),
+                                               ctypes.c_void_p(self.p), out.nbytes))
+        return out
+
+    def free(self):
+        if self._base is None and self.p and self.ctx.h:
+            lib().gprx_device_free(self.ctx.h, ctypes.c_void_p(self.p))
+        self.p = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
 class Context:
     """One per process per GPU (gprx_ctx)."""
 
@@ -285,6 +351,10 @@ class Context:
 
     def _c(self, st):
         _check(st, self.h)
+
+    def device_array(self, a):
+        """`a` copied into this context's device memory (DeviceArray)."""
+        return DeviceArray(self, a)
 
     def set_stats(self, enable=True):
         """Per-kernel HIP-event timing of the library's launches (gprx_ctx_set_stats)."""

@@ -146,6 +146,16 @@ typedef struct gprx_kstat {
 gprx_status gprx_ctx_set_stats(gprx_ctx* ctx, int32_t enable);
 gprx_status gprx_ctx_get_stats(gprx_ctx* ctx, gprx_kstat* out, int32_t max, int32_t* count);
 
+/* Device buffers on the context's GPU, for inputs that stay resident in HBM across calls (the
+ * calls documented as taking "host or device memory" read them without a PCIe transfer).  A
+ * process that loads this library next to another HIP runtime (a framework's bundled one) cannot
+ * hand over that runtime's allocations once this library has initialised the device, so the
+ * library allocates them itself.  Upload / download are synchronous on the context's stream. */
+gprx_status gprx_device_alloc(gprx_ctx* ctx, int64_t bytes, void** out);
+gprx_status gprx_device_free(gprx_ctx* ctx, void* p);
+gprx_status gprx_device_upload(gprx_ctx* ctx, void* dst, const void* src, int64_t bytes);
+gprx_status gprx_device_download(gprx_ctx* ctx, void* dst, const void* src, int64_t bytes);
+
 /* ---- dense GP model ------------------------------------------------------------- */
 /* Replaces the GaussianProcess<T> state (include/GaussianProcess.h:267-280). */
 gprx_status gprx_model_create(gprx_ctx* ctx, gprx_dtype dtype, gprx_model** out);

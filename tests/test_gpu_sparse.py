@@ -153,10 +153,32 @@ def test_sparse_lml_rccl_one_rank():
         lctx.close()
 
 
+def test_sparse_fit_device_array_inputs(ctx):
+    """X and Y already in HBM (the library's own device buffers, gprx_device_alloc): read without a
+    PCIe copy (unified addressing picks the copy's direction), the same bits as from host arrays;
+    the buffers round-trip, a reshaped view shares its base's memory, m = 1 labels as a vector."""
+    ks = "GaussianKernel(0.7,1.3,)"
+    X, Y, Xm = _inputs(3000, 4, 64, 1, np.float64)
+    host = ctx.sparse_fit(ks, X, Y, Xm, 0.3, 1e-4)
+    Xd, Yd = ctx.device_array(X), ctx.device_array(Y)
+    assert np.array_equal(Xd.numpy(), X) and Xd.shape == X.shape
+    dev = ctx.sparse_fit(ks, Xd, Yd, Xm, 0.3, 1e-4)
+    for a, b in zip(host, dev):
+        assert np.array_equal(a, b)
+    Yv = ctx.device_array(np.ascontiguousarray(Y[:, 0]))  # (n,) -> reshaped to (n, 1) inside
+    dev1 = ctx.sparse_fit(ks, Xd, Yv, Xm, 0.3, 1e-4)
+    for a, b in zip(host, dev1):
+        assert np.array_equal(a, b)
+    assert Yv.reshape(-1, 1).data_ptr() == Yv.data_ptr()
+    with pytest.raises(TypeError):
+        ctx.sparse_fit(ks, Xd, ctx.device_array(Y.astype(np.float32)), Xm, 0.3, 1e-4)
+
+
 def test_sparse_fit_device_resident_inputs(ctx):
     """X and Y already in HBM (a torch CUDA tensor's memory): the library reads them without a
     PCIe copy (unified addressing picks the copy's direction) and returns the same bits as from
-    host arrays."""
+    host arrays.  (Skipped in a process where this library initialised the device first: the
+    PyTorch wheel's bundled HIP runtime then sees no GPU -- the DeviceArray test above covers it.)"""
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
         pytest.skip("no torch CUDA device")
