@@ -423,7 +423,11 @@ def main():
         import torch
         import torch.distributed as tdist
         torch.cuda.set_device(local_rank)
-        tdist.init_process_group("gloo" if shared else "nccl")
+        # gloo: torch.distributed only bootstraps (the RCCL unique id), barriers and reduces the
+        # per-rank times; the device collectives are the library's own (its RCCL communicator,
+        # IPC peer stores).  A torch "nccl" group would bring up a second RCCL on torch's bundled
+        # HIP runtime next to the library's.
+        tdist.init_process_group("gloo")
         dist = tdist
 
     import gpr_amd
@@ -455,7 +459,7 @@ def main():
         if dist is None:
             return x
         import torch
-        t = torch.tensor([x], dtype=torch.float64, device="cpu" if shared else "cuda")
+        t = torch.tensor([x], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
