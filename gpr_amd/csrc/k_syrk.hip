@@ -38,10 +38,20 @@ __global__ __launch_bounds__(mm::NT) void syrk_splitk_kernel(T* __restrict__ C, 
     typedef mm::Mfma<T> Tr;
     typename Tr::acc_t acc[2][4];
     const int t = threadIdx.x;
-    mm::tile_mma<T, 0, false, mm::BKS>(acc, A + i0, lda, A + j0, lda, K, K, smem, t);  // (K: multiples of 16)
     const int lane = t & 63, w = t >> 6;
-    const int wr = w & 1, wc = w >> 1, lr = lane & 15, lk = lane >> 4;
+    const int lr = lane & 15, lk = lane >> 4;
     const bool diag = ti == tj;
+    int wr, wc;
+    // (K: multiples of 16) a diagonal tile skips its 16 x 16 tiles above the diagonal, waves
+    // mapped so each SIMD's pair carries the same number of live tiles (k_mma.h wave_block<2>):
+    // the 16 diagonal tiles of M = 2048 are 12% of the launch's tiles
+    if (diag) {
+        mm::tile_mma<T, 2, false, mm::BKS>(acc, A + i0, lda, A + j0, lda, K, K, smem, t);
+        mm::wave_block<2>(w, wr, wc);
+    } else {
+        mm::tile_mma<T, 0, false, mm::BKS>(acc, A + i0, lda, A + j0, lda, K, K, smem, t);
+        mm::wave_block<0>(w, wr, wc);
+    }
 #pragma unroll
     for (int x = 0; x < 2; x++)
 #pragma unroll
