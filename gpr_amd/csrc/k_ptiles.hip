@@ -834,9 +834,11 @@ __device__ __forceinline__ void la_trail_tile(T* __restrict__ sS, int c0, int R,
 // S = sum_{kb_lo <= kb < kb_hi} L_{p,kb} Linv_{kb,j} (LA_LOAD: plus the partial S staged by an
 // earlier call), staged transposed in the unit's own Linv slot; LA_FINISH: Linv_pj = -Dinv_p S.
 enum { LA_LOAD = 1, LA_FINISH = 2 };
+// gout (LA_FINISH): the finished Linv_pj half also goes straight to global memory (Linv,
+// column-major, ld DB; write-through) from the registers
 template <typename T>
 __device__ __forceinline__ void la_linv_unit(T* __restrict__ sS, const T* __restrict__ sDi, int p, int j, int ct,
-                                             int kb_lo, int kb_hi, int mode, int lr, int lk) {
+                                             int kb_lo, int kb_hi, int mode, int lr, int lk, T* gout = nullptr) {
     typedef Mfma<T> Tr;
     typedef typename Tr::acc_t acc_t;
     acc_t s0 = acc_t{0}, s1 = acc_t{0};
@@ -883,6 +885,10 @@ __device__ __forceinline__ void la_linv_unit(T* __restrict__ sS, const T* __rest
         const int c = 32 * j + 16 * ct + Tr::orow(lk, reg);
         sS[c + (32 * p + lr) * SIL] = -o0[reg];
         sS[c + (32 * p + 16 + lr) * SIL] = -o1[reg];
+        if (gout) {
+            st_sc1(gout + (32 * p + lr) + (int64_t)c * DB, -o0[reg]);
+            st_sc1(gout + (32 * p + 16 + lr) + (int64_t)c * DB, -o1[reg]);
+        }
     }
 }
 
@@ -1090,11 +1096,18 @@ __device__ __forceinline__ void diag_factor_la(T* __restrict__ A, int64_t ld, T*
         if (prof) pside += wall_clock64() - ts0;
     }
     if (fail >= 0) atomicMin(info, (int)(col0 + fail + 1));  // wave 0, every lane the same value
-    // Linv's last row block: the kb = 2 term and -Dinv_3 S (6 units, waves 0-5); the stores of
-    // L panel 3 and Linv row block 2 by waves 6-7 meanwhile
+    // Linv's last row block: the kb = 2 term and -Dinv_3 S (6 units, waves 0-5), each storing its
+    // half block to global memory from its registers; the stores of L panel 3, Linv row block 2
+    // and the rest of row block 3 (its diagonal block Dinv_3 and the zeros right of it) by waves
+    // 6-7 meanwhile (GPRX_LA_TAIL_LDS: row block 3 from LDS after a barrier, the round-3 order)
+#ifndef GPRX_LA_TAIL_LDS
+    constexpr bool direct = true;
+#else
+    constexpr bool direct = false;
+#endif
     if (w < 6) {
         const int j = w >> 1;
-        la_linv_unit<T>(sS, sDi, 3, j, w & 1, 2, 3, (j < 2 ? LA_LOAD : 0) | LA_FINISH, lr, lk);
+        la_linv_unit<T>(sS, sDi, 3, j, w & 1, 2, 3, (j < 2 ? LA_LOAD : 0) | LA_FINISH, lr, lk, direct ? Linv : nullptr);
     } else {
         if (pan && w == 6) {  // Dinv_3 first: the progressive parts' last input
             la_store_dinv<T>(Linv, sS, sDi, 3, lane, 64);
@@ -1103,9 +1116,14 @@ __device__ __forceinline__ void diag_factor_la(T* __restrict__ A, int64_t ld, T*
         }
         la_store_lpanel<T>(A, ld, sS, 3, t - 384, 128);
         la_store_linv_rows<T>(Linv, sS, sDi, 2, t - 384, 128);
+        if (direct)  // row block 3, columns 96..127 (Dinv_3, zeros above its diagonal)
+            for (int e = t - 384; e < 32 * 32; e += 128) {
+                const int r = 96 + (e & 31), c = 96 + (e >> 5);
+                st_sc1(Linv + r + c * DB, linv_at(sS, sDi, r, c));
+            }
     }
     __syncthreads();
-    la_store_linv_rows<T>(Linv, sS, sDi, 3, t, NT);
+    if (!direct) la_store_linv_rows<T>(Linv, sS, sDi, 3, t, NT);
     if (prof && t == 0) {  // load, F phases (barrier to barrier), P + Ua phases, fact32 alone
         prof[0] = pload - pt0;
         prof[1] = pf;
