@@ -87,8 +87,9 @@ struct BkOf<float> {
 //   mid:  step kq+1's fragment reads are pinned after the first `mid` MFMAs of step kq (-1: read
 //         ahead of all of them, where hipcc then issued them behind the MFMAs and waited on
 //         them -- lgkmcnt(0), with an LDS-DMA pending -- before the next step's first MFMA).
-// f64: late + mid 2 + spread refill (probe 0.839 -> 0.873 of the bound; C3 launch 26.45 ->
-// 25.71 ms and the C5 syrk 2.47 -> 2.39 ms per launch, same box, profiles/r04s); f32: all off
+// f64: late + mid 1 + spread refill (probe 0.839 -> 0.877 of the bound; C3 launch 26.45 ->
+// 25.71 ms and the C5 syrk 2.47 -> 2.39 ms per launch with mid 2, same box, profiles/r04s; mid 1
+// another 0.5% on both, r04ak); f32: all off
 // (late + mid 2 cost C4's factor 3%: 100.8 -> 103.6 ms, r04q).
 // GPRX_MMA_LATE / GPRX_MMA_MID / GPRX_MMA_SPREAD force a form for both (A/B builds).
 #ifndef GPRX_PAIR_FEED
@@ -107,7 +108,7 @@ struct FeedOf {
 #ifdef GPRX_MMA_MID
     static constexpr int mid = GPRX_MMA_MID;
 #else
-    static constexpr int mid = sizeof(T) == 8 ? 2 : -1;
+    static constexpr int mid = sizeof(T) == 8 ? 1 : -1;
 #endif
     // late form: the refill's LDS-DMA issues one after each of the MFMAs that follow the
     // barrier, not in a burst after it (each issue holds its wave ~60 cycles; behind an MFMA
