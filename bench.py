@@ -82,6 +82,68 @@ def cpu_baseline(cfg, n_cpu):
     }
 
 
+def cpu_lml_baseline(cfg, ns, t_gpu_ms=None):
+    """The CPU restatement of the reference's log-marginal likelihood + gradient
+    (GaussianLogLikelihood::GetValueAndParameterDerivatives, include/Likelihood.h:231-285:
+    K, the LU inverse C in fp64, the long-double determinant of lib/GaussianProcess.cpp:513-528,
+    the P derivative matrices and tr((alpha alpha^T - C) dK_p)) timed at the sizes `ns` on this
+    host's cores and EXTRAPOLATED to the bench N by the cubic t(n) = a n^3 + b n^2 + c through
+    the measured points (a full run at N = 16384 is dominated by the
+    long-double determinant, est. >= 30 min)."""
+    from oracle import oracle as O
+    from gpr_amd.synth import make_data
+    ts = []
+    for n_ in ns:
+        X, Y = make_data(n_, cfg["d"], cfg["m"])
+        t0 = time.perf_counter()
+        O.lml(cfg["kernel"], X, Y, cfg["sigma"], np.float64, with_grad=True)
+        ts.append(time.perf_counter() - t0)
+    n = cfg["n"]
+    nn = np.array(ns, dtype=np.float64)
+    if len(ns) >= 3:
+        A = np.stack([nn ** 3, nn ** 2, np.ones_like(nn)], axis=1)
+        coef = np.linalg.lstsq(A, np.array(ts), rcond=None)[0]
+        t_n = float(coef[0] * n ** 3 + coef[1] * n ** 2 + coef[2])
+        how = "least-squares cubic a n^3 + b n^2 + c through the points"
+    else:
+        t_n = ts[-1] * (n / ns[-1]) ** 3
+        coef = None
+        how = "pure cubic from the largest point"
+    # (a cubic fit whose n^3 term comes out non-positive is no extrapolation: use the pure cubic)
+    if coef is not None and (coef[0] <= 0 or t_n < ts[-1] * (n / ns[-1]) ** 2):
+        t_n = ts[-1] * (n / ns[-1]) ** 3
+        how = "pure cubic from the largest point (the 3-term fit was not increasing)"
+    return {
+        "value": 1.0 / t_n,
+        "unit": "LML+gradient evaluations/s",
+        "ms_extrapolated": 1e3 * t_n,
+        "cores": O.num_threads(),
+        "kind": "port",
+        "extrapolated": True,
+        "sample": (f"oracle LML + gradient (LU inverse via LAPACK {O.lapack_name()}, long-double determinant, "
+                   f"P={5} derivative traces) measured at N={list(ns)}: "
+                   + ", ".join(f"{t:.2f} s" for t in ts) + f"; EXTRAPOLATED to N={n} by {how}"),
+        "gpu_over_cpu": (t_n * 1e3 / t_gpu_ms) if t_gpu_ms else None,
+    }
+
+
+def cpu_predict_baseline(cfg, X, alpha, q_cpu):
+    """The reference's Predict (lib/GaussianProcess.cpp:54-61: one kernel vector k(x, X) and a
+    dot with alpha per point, apps/GaussianProcessPredict.cpp:185-193 loops over the points)
+    restated (oracle predict, OpenMP over the points) and timed on this host's cores for q_cpu
+    queries against the same N-sample model."""
+    from oracle import oracle as O
+    from gpr_amd.synth import make_queries
+    Xq = make_queries(q_cpu, cfg["d"])
+    O.predict(cfg["kernel"], X, alpha, Xq[:64])  # (thread pool, pages)
+    t0 = time.perf_counter()
+    O.predict(cfg["kernel"], X, alpha, Xq)
+    dt = time.perf_counter() - t0
+    return {"value": q_cpu / dt, "unit": "pts/s", "cores": O.num_threads(), "kind": "port",
+            "sample": f"{q_cpu} query points against the N={cfg['n']} d={cfg['d']} model (oracle per-point predict, "
+                      f"OpenMP over the points) in {dt:.2f} s"}
+
+
 def _short(name):
     """Kernel name without `void`, namespaces and the argument list (as scripts/pmc_traffic.py)."""
     m = re.match(r"(?:void )?(?:[A-Za-z_0-9]+::)*([A-Za-z_0-9]+<[^()]*>|[A-Za-z_0-9]+)", name)
@@ -167,6 +229,37 @@ def mfma_from_profile(leg, kernels):
                     "clock_ghz": float(np.mean([x["clock_ghz"] for x in v])), "launches": len(v),
                     "source": os.path.basename(path)}
     return None
+
+
+def make_dist_context(gpr_amd, group, rank, world, local_rank, shared):
+    """The multi-process context of the sharded fit: an RCCL communicator over the GPUs
+    (gprx_ctx_create_dist, nonblocking initialisation with a deadline), or, when any rank's
+    RCCL initialisation fails or times out, every rank falls back to the peer context over the
+    host group's all-gather (gprx_ctx_create_peer: the same device-initiated exchange, host
+    collectives over the sockets instead of RCCL).  The ranks agree on the choice.  Returns
+    (context, transport, error-or-None).  GPRX_DIST_SHARED_GPU (one GPU for every rank, which
+    RCCL refuses) goes to the peer context directly."""
+    if group is None:  # --force-dist at N = 1: a one-rank RCCL communicator
+        return gpr_amd.Context(local_rank, dist=(0, 1, gpr_amd.unique_id())), "rccl", None
+    # (a shared-GPU rehearsal tries RCCL only under GPRX_RCCL_FAIL, which fails it on purpose:
+    # the fallback below, rehearsed on one GPU)
+    if shared and os.environ.get("GPRX_RCCL_FAIL", "0") == "0":
+        return gpr_amd.Context(0, peer=(rank, world, group.allgather_fn())), "peer (shared GPU)", None
+    err = None
+    ctx = None
+    try:
+        uid = group.broadcast(gpr_amd.unique_id() if rank == 0 else None)
+        ctx = gpr_amd.Context(local_rank, dist=(rank, world, uid))
+    except Exception as e:
+        err = f"rank {rank}: RCCL context: {e!r}"
+        log(err)
+    errs = [e.decode() for e in group.allgather((err or "").encode()) if e]
+    if not errs:
+        return ctx, "rccl", None
+    if ctx is not None:
+        ctx.close()  # (ncclCommAbort: local, never waits on the ranks that failed)
+    ctx = gpr_amd.Context(local_rank, peer=(rank, world, group.allgather_fn()))
+    return ctx, "peer (fallback: RCCL initialisation failed)", "; ".join(errs)
 
 
 class _Skip(Exception):
@@ -389,6 +482,9 @@ def main():
                                                         "(BASELINE.json configs[2]); 0 = skip")
     ap.add_argument("--build-iters", type=int, default=3, help="time the covariance build alone (0 = skip)")
     ap.add_argument("--cpu-n", type=int, default=16384, help="N of the CPU-baseline sample (0 = skip)")
+    ap.add_argument("--cpu-lml-ns", default="1024,2048,4096",
+                    help="sizes of the CPU LML + gradient baseline, extrapolated cubically to N ('' = skip)")
+    ap.add_argument("--cpu-predict-q", type=int, default=4096, help="queries of the CPU predict baseline (0 = skip)")
     ap.add_argument("--mode", choices=["replicas", "dist"], default="dist",
                     help="N>1 headline: one fit whose matrix is sharded over the GPUs (dist, strong "
                          "scaling) or independent fits per GPU (replicas, weak scaling); both are measured")
@@ -419,19 +515,16 @@ def main():
     shared = os.environ.get("GPRX_DIST_SHARED_GPU") == "1" and world > 1
     if shared:
         local_rank = 0
-    if world > 1:
-        import torch
-        import torch.distributed as tdist
-        torch.cuda.set_device(local_rank)
-        # gloo: torch.distributed only bootstraps (the RCCL unique id), barriers and reduces the
-        # per-rank times; the device collectives are the library's own (its RCCL communicator,
-        # IPC peer stores).  A torch "nccl" group would bring up a second RCCL on torch's bundled
-        # HIP runtime next to the library's.
-        tdist.init_process_group("gloo")
-        dist = tdist
-
+    # the library first and no PyTorch at all: the process maps ONE HIP runtime and RCCL,
+    # /opt/rocm's (gpr_amd.runtime_info(), reported as "runtime"); the host collectives around
+    # the device work (the RCCL unique id, barriers, max over ranks, the peer context's
+    # all-gather) are gpr_amd.hostcoll's sockets on the loopback
     import gpr_amd
     from gpr_amd.synth import C3, make_data, make_queries
+    gpr_amd.lib()
+    if world > 1:
+        from gpr_amd.hostcoll import SocketGroup
+        dist = SocketGroup.from_env()
 
     cfg = dict(C3)
     if args.n:
@@ -450,18 +543,13 @@ def main():
         return mdl
 
     def barrier_sync():
+        # (every library call has drained its streams when it returns: the barrier is the
+        # host's alone)
         if dist is not None:
-            import torch
             dist.barrier()
-            torch.cuda.synchronize()
 
     def max_over_ranks(x):
-        if dist is None:
-            return x
-        import torch
-        t = torch.tensor([x], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t.item())
+        return x if dist is None else dist.max(x)
 
     def timed_fits(mdl, c, flags=0):
         """W untimed warmup fits, then exactly K fits between barrier + synchronize; max over ranks."""
@@ -478,17 +566,10 @@ def main():
         return max_over_ranks(el), infos, st
 
     # ---- the sharded fit over all ranks (the N > 1 headline) -------------------------------
-    dres, dist_error, dctx = None, None, None
+    dres, dist_error, dctx, transport = None, None, None, None
     if (world > 1 or args.force_dist) and want("c3"):
         try:
-            if shared:
-                from gpr_amd.gprx import torch_allgather
-                dctx = gpr_amd.Context(0, peer=(rank, world, torch_allgather()))
-            else:
-                uid = [gpr_amd.unique_id() if rank == 0 else None]
-                if dist is not None:
-                    dist.broadcast_object_list(uid, src=0)
-                dctx = gpr_amd.Context(local_rank, dist=(rank, world, uid[0]))
+            dctx, transport, dist_error = make_dist_context(gpr_amd, dist, rank, world, local_rank, shared)
             dmodel = make_model(dctx)
             el, infos, st = timed_fits(dmodel, dctx, gpr_amd.gprx.FIT_DISTRIBUTED)
             dres = {"elapsed": el, "infos": infos}
@@ -500,7 +581,7 @@ def main():
                 dres["lml_ms_wall"] = 1e3 * max_over_ranks(time.perf_counter() - tl0)
             dmodel.close()
         except Exception as e:  # reported; the replicas line stands in
-            dist_error = repr(e)
+            dist_error = ((dist_error + "; ") if dist_error else "") + repr(e)
             log("distributed fit failed:", dist_error)
 
     # ---- one independent fit per GPU (the N = 1 headline; the replicas extra for N > 1) -----
@@ -559,6 +640,11 @@ def main():
                                      "mfma_flop_per_pair": 6.0 * d, "valu_ops_per_pair": 28.0}
             if world == 1:
                 pred["rocprof"] = rocprof_from_profile("predict", ("predict_mma_kernel<double, 1, true>",), 1e3 * pms)
+        if rank == 0 and world == 1 and args.cpu_predict_q > 0:
+            try:
+                pred["cpu_baseline"] = cpu_predict_baseline(cfg, X, model.alpha(), args.cpu_predict_q)
+            except Exception as e:
+                log("cpu predict baseline failed:", e)
 
     # posterior variance (GetCredibleInterval, lib/GaussianProcess.cpp:102-114): k(x,x) - |L^{-1} k_x|^2
     # for Qv queries, query-sharded; the forward solve with Qv right-hand sides on the tile GEMM
@@ -570,15 +656,24 @@ def main():
         Xv = make_queries(args.variance_q, d)
         lo, hi = gpr_amd.query_shard(args.variance_q, rank, world)
         model.posterior_cov(Xv[lo:hi], Xv[lo:hi])
+        ctx.set_stats(True)
         barrier_sync()
         tv0 = time.perf_counter()
         model.posterior_cov(Xv[lo:hi], Xv[lo:hi])
         tv = max_over_ranks(time.perf_counter() - tv0)
+        vs = ctx.stats().get("posterior")
+        ctx.set_stats(False)
+        # device time of the solve (HIP events around K(x, X), the forward solve and the row
+        # dots, on the stream they run on), max over ranks; `ms` is the call's wall time
+        vms = max_over_ranks(vs["ms"]) if vs else None
         fl = float(args.variance_q) * n * n
         var = {"q": args.variance_q, "sharded_over": world, "pts_per_s_wall": args.variance_q / tv,
-               "ms": 1e3 * tv, "roofline": {"bound": "mfma", "achieved": fl / tv / 1e12 / world,
-                                            "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
-                                            "frac": fl / tv / 1e12 / world / PEAK_FP64_TFLOPS}}
+               "ms": 1e3 * tv, "device_ms": vms,
+               "pts_per_s_device": (args.variance_q / (vms * 1e-3)) if vms else None,
+               "roofline": {"bound": "mfma", "achieved": fl / tv / 1e12 / world,
+                            "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
+                            "frac": fl / tv / 1e12 / world / PEAK_FP64_TFLOPS,
+                            "algorithmic_flops": fl, "time": "wall"}}
 
     # log-marginal likelihood + gradient (refit, explicit inverse, fused gradient pass)
     lml = None
@@ -590,8 +685,33 @@ def main():
         tl = time.perf_counter() - tl0
         ls = ctx.stats()
         ctx.set_stats(False)
+        # T_roof = the fit's (B_build + B_solve at HBM rate, n^3/3 at the
+        # f64 peak) + potri's 2 n^3 / 3 at the f64 peak + one read of the N(N+1)/2 lower C
+        # for the gradient reduction = 56.5 ms; achieved = the LML's algorithmic flops
+        # (n^3/3 potrf + n^3/3 trtri + n^3/3 lauum) over the wall time of the call
+        t_roof_lml = (fit_roofline_ms(n, d, m) + 1e3 * (2.0 * n ** 3 / 3.0) / (PEAK_FP64_TFLOPS * 1e12)
+                      + 1e3 * 8.0 * n * (n + 1) / 2 / (PEAK_HBM_GBS * 1e9))
+        lml_flops = float(n) ** 3
+        dev_ms = sum(v["ms"] for k, v in ls.items() if k in ("potrf_tiles", "other_gemm", "lml_grad", "backsolve"))
         lml = {"ms_wall": 1e3 * tl, "phases_ms": {k: v["ms"] for k, v in ls.items()},
+               "device_ms": dev_ms or None,
+               "roofline": {"bound": "mfma", "t_roof_ms": t_roof_lml, "t_ms": 1e3 * tl, "time": "wall",
+                            "frac": t_roof_lml / (1e3 * tl),
+                            "achieved": lml_flops / tl / 1e12, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
+                            "algorithmic_flops": lml_flops,
+                            "note": "factor n^3/3 + triangular inverse n^3/3 (both in one tile launch) + C = U U^T "
+                                    "n^3/3, then the gradient pass over the lower C"},
                "rocprof": rocprof_table("lml") if world == 1 else None}
+        if lml["rocprof"]:
+            # (the committed profile's per-kernel averages summed: one call's device time over
+            # the kernels above 1% of the leg)
+            lml["roofline"]["rocprof_sum_ms"] = sum(v["avg_us"] for v in lml["rocprof"]["kernels"].values()) / 1e3
+        if rank == 0 and world == 1 and args.cpu_lml_ns:
+            try:
+                lml["cpu_baseline"] = cpu_lml_baseline(cfg, [int(v) for v in args.cpu_lml_ns.split(",")],
+                                                       1e3 * tl)
+            except Exception as e:
+                log("cpu LML baseline failed:", e)
 
     # the covariance build alone (north_star asks for its HBM GB/s; in the fit it is fused into
     # the factorisation launch as BUILD tasks): the same BUILD tasks with no other task in the
@@ -655,7 +775,9 @@ def main():
 
     configs = None
     if args.configs:
-        configs = run_configs(args, world, rank, local_rank, dctx if dist_error is None else None, max_over_ranks,
+        # (the ranks agree whether the sharded fit ran everywhere before the sharded configs use it)
+        dist_ok = dres is not None if dist is None else dist.min(1.0 if dres is not None else 0.0) > 0
+        configs = run_configs(args, world, rank, local_rank, dctx if dist_ok else None, max_over_ranks,
                               barrier_sync, want)
     if dctx is not None:
         dctx.close()
@@ -708,6 +830,9 @@ def main():
                              "frac": t_roof / fit_ms if fit_ms else None},
             "replicas": replicas if world > 1 else None,
             "dist_error": dist_error,
+            "dist_transport": transport,
+            # the HIP runtime, HSA runtime and RCCL this process mapped (one copy each)
+            "runtime": gpr_amd.runtime_info(),
             "phases": phases,
             "predict": pred,
             "variance": var,
@@ -720,7 +845,7 @@ def main():
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.barrier()
-        dist.destroy_process_group()
+        dist.close()
 
 
 if __name__ == "__main__":

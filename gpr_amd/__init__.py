@@ -7,7 +7,9 @@ tests and bench.py; the C++ host API mirroring the reference classes is in inclu
 from . import kernels
 from .kernels import (Gaussian, GaussianExp, White, RationalQuadratic, Periodic, Sum, Product, parse_kernel,
                       general_kernel)
-from .gprx import Context, DeviceArray, Model, GprxError, lib, device_count, unique_id, query_shard, LIB_PATH
+from .gprx import (Context, DeviceArray, Model, GprxError, lib, device_count, unique_id, query_shard, LIB_PATH,
+                   runtime_info)
 
 __all__ = ["DeviceArray", "kernels", "Gaussian", "GaussianExp", "White", "RationalQuadratic", "Periodic", "Sum", "Product",
-           "parse_kernel", "general_kernel", "Context", "Model", "GprxError", "lib", "device_count", "unique_id", "LIB_PATH"]
+           "parse_kernel", "general_kernel", "Context", "Model", "GprxError", "lib", "device_count", "unique_id", "LIB_PATH",
+           "runtime_info"]

@@ -298,6 +298,10 @@ struct gprx_model {
     KCanon<double> kd{};
     KCanon<float> kf{};
     DevBuf X, Y, tab, A, Linv, z, alpha, info, flag, red, V, C, scratch1, scratch2, grad, pack, featU, featV, kdev;
+    // posterior covariance workspace (L^{-1} K(X, x) for a query batch: qp x np each), kept
+    // across calls -- at Q = 65536, N = 16384 one buffer is 8.6 GB, whose hipMalloc + free per
+    // call cost more than the solve on some boxes
+    DevBuf pvRa, pvRb;
     DevParam kfit;     // the fit's kernel tree (uploaded when it changes)
     PinnedBuf hstat;   // the fit's status words: flag, info, log det, data fit
     // fp32 models: fp64 iterative refinement state (k_refine.hip).  kd then holds the tree in
@@ -1038,11 +1042,76 @@ static void solve_rows_for(gprx_model* M, const T* dXq, const T* dtabQ, int64_t 
 // query columns V_k travel through the receive windows, the row sums are all-reduced.  Pairs
 // (x_p, y_p) with x != y ride in the same chunk (64 + 64 columns), variances 128 per chunk.
 template <typename T>
+static gprx_status model_posterior_cov_dist_core(gprx_model* M, const void* Xa, const void* Xb, int64_t q, bool same,
+                                                 void* out);
+
+// FNV-1a over bytes (the processes' query agreement below)
+static uint64_t fnv1a(const void* p, size_t n, uint64_t h = 1469598103934665603ull) {
+    const unsigned char* b = static_cast<const unsigned char*>(p);
+    for (size_t i = 0; i < n; i++) h = (h ^ b[i]) * 1099511628211ull;
+    return h;
+}
+
+// On a multi-process context the sharded solve is a collective: every process runs the same
+// sequence of launches and exchanges.  The processes first agree on their arguments (q, whether
+// x == y, a hash of the queries).  Identical arguments (every process asks for the same pairs)
+// take the solve as they are; different ones -- e.g. each process its own query_shard slice,
+// q = 0 included -- are all-gathered, the solve runs once over every process's pairs, and each
+// process keeps its own.
+template <typename T>
 static gprx_status model_posterior_cov_dist(gprx_model* M, const void* Xa, const void* Xb, int64_t q, void* out) {
+    const int d = M->d;
+    const bool same = q == 0 || (Xa == Xb) || std::memcmp(Xa, Xb, sizeof(T) * q * d) == 0;
+    gprx_ctx* ctx = M->ctx;
+    if (!ctx->hc || ctx->world <= 1) return model_posterior_cov_dist_core<T>(M, Xa, Xb, q, same, out);
+    const int g = ctx->world;
+    struct Hdr {
+        int64_t q;
+        int64_t same;
+        uint64_t hash;
+    } h{q, same ? 1 : 0, fnv1a(Xa, sizeof(T) * q * d, fnv1a(same ? Xa : Xb, sizeof(T) * q * d))};
+    std::vector<Hdr> all(g);
+    ctx->hc->allgather(&h, sizeof(Hdr), all.data());
+    bool uniform = true;
+    int64_t qmax = 0, qtot = 0;
+    bool all_same = true;
+    for (const Hdr& x : all) {
+        uniform = uniform && x.q == h.q && x.same == h.same && x.hash == h.hash;
+        qmax = std::max(qmax, x.q);
+        qtot += x.q;
+        all_same = all_same && x.same;
+    }
+    if (uniform) return q ? model_posterior_cov_dist_core<T>(M, Xa, Xb, q, same, out) : GPRX_OK;
+    // every process's pairs, in rank order; this process's results from offset `off`
+    std::vector<T> mine((size_t)qmax * d * 2, T(0));
+    if (q) {
+        std::memcpy(mine.data(), Xa, sizeof(T) * q * d);
+        std::memcpy(mine.data() + (size_t)qmax * d, Xb, sizeof(T) * q * d);
+    }
+    std::vector<T> gath((size_t)qmax * d * 2 * g);
+    ctx->hc->allgather(mine.data(), sizeof(T) * mine.size(), gath.data());
+    std::vector<T> xa((size_t)std::max<int64_t>(qtot, 1) * d), xb((size_t)std::max<int64_t>(qtot, 1) * d);
+    int64_t off = 0, mine_off = 0;
+    for (int r = 0; r < g; r++) {
+        const T* src = gath.data() + (size_t)r * qmax * d * 2;
+        if (r == ctx->rank) mine_off = off;
+        std::memcpy(xa.data() + off * d, src, sizeof(T) * all[r].q * d);
+        std::memcpy(xb.data() + off * d, src + (size_t)qmax * d, sizeof(T) * all[r].q * d);
+        off += all[r].q;
+    }
+    if (qtot == 0) return GPRX_OK;
+    std::vector<T> res((size_t)qtot);
+    model_posterior_cov_dist_core<T>(M, xa.data(), all_same ? xa.data() : xb.data(), qtot, all_same, res.data());
+    if (q) std::memcpy(out, res.data() + mine_off, sizeof(T) * q);
+    return GPRX_OK;
+}
+
+template <typename T>
+static gprx_status model_posterior_cov_dist_core(gprx_model* M, const void* Xa, const void* Xb, int64_t q, bool same,
+                                                 void* out) {
     hipStream_t s = M->ctx->stream;
     const KCanon<T>& K = kcanon<T>(M);
     const int d = M->d;
-    const bool same = (Xa == Xb) || std::memcmp(Xa, Xb, sizeof(T) * q * d) == 0;
     const int nchmax = dist_pvar_chunks(M->dist_engine);
     const int per = same ? DB : DB / 2;  // pairs per chunk
     const T* xa = static_cast<const T*>(Xa);
@@ -1090,7 +1159,8 @@ static gprx_status model_posterior_cov(gprx_model* M, const void* Xa, const void
                                      std::string(std::getenv("GPRX_DIST_POSTERIOR")) == "dense";
     if (M->dist_fitted && !M->dist_dense && M->method == 0 && !dense_forced && dist_pvar_chunks(M->dist_engine) > 0)
         return model_posterior_cov_dist<T>(M, Xa, Xb, q, out);
-    ensure_dense_factor<T>(M);
+    ensure_dense_factor<T>(M);  // (collective on a sharded fit's first dense use)
+    if (q == 0) return GPRX_OK;
     hipStream_t s = M->ctx->stream;
     const KCanon<T>& K = kcanon<T>(M);
     const int d = M->d;
@@ -1154,16 +1224,20 @@ static gprx_status model_posterior_cov(gprx_model* M, const void* Xa, const void
     }
     // the variance (GetCredibleInterval, :102-114, pairs (x, x)): one solve, |L^{-1} k_x|^2
     const bool same = (Xa == Xb) || std::memcmp(Xa, Xb, sizeof(T) * q * d) == 0;
-    Ra.ensure(sizeof(T) * qp * M->np);
-    solve_rows_for<T>(M, da.as<T>(), ta.as<T>(), q, qp, Ra.as<T>());
-    if (!same) {
-        Rb.ensure(sizeof(T) * qp * M->np);
-        solve_rows_for<T>(M, db.as<T>(), tb.as<T>(), q, qp, Rb.as<T>());
-    }
     kab.ensure(sizeof(T) * q);
     res.ensure(sizeof(T) * q);
-    launch_pair_kernel<T>(K, da.as<T>(), db.as<T>(), q, d, kab.as<T>(), s);
-    launch_rowdot<T>(Ra.as<T>(), same ? Ra.as<T>() : Rb.as<T>(), qp, q, M->np, kab.as<T>(), res.as<T>(), s);
+    M->pvRa.ensure(sizeof(T) * qp * M->np);
+    if (!same) M->pvRb.ensure(sizeof(T) * qp * M->np);
+    {
+        // device time of the whole solve (stats class "posterior"): K(x, X), the forward
+        // solve (q np^2 flop) and the row dots
+        ProfScope ps_(KC_POSTERIOR, s, (same ? 1.0 : 2.0) * (double)q * (double)M->np * (double)M->np);
+        T* Ra_ = M->pvRa.as<T>();
+        solve_rows_for<T>(M, da.as<T>(), ta.as<T>(), q, qp, Ra_);
+        if (!same) solve_rows_for<T>(M, db.as<T>(), tb.as<T>(), q, qp, M->pvRb.as<T>());
+        launch_pair_kernel<T>(K, da.as<T>(), db.as<T>(), q, d, kab.as<T>(), s);
+        launch_rowdot<T>(Ra_, same ? Ra_ : M->pvRb.as<T>(), qp, q, M->np, kab.as<T>(), res.as<T>(), s);
+    }
     download(out, res.p, sizeof(T) * q, s);
     return GPRX_OK;
 }
@@ -1777,9 +1851,8 @@ static void sparse_normal_eq(gprx_ctx* ctx, SparseNE<T>& st, const gprx_kernel_d
     }
     launch_sum_partials<T>(dS.as<T>(), sstride, P, s);  // dS[0] += dS[1..P-1]
     if (ctx->comm) {  // rows sharded over the ranks: sum the partial normal equations
-        const ncclResult_t r =
-            ncclAllReduce(dS.p, dS.p, (size_t)(ld * Mp), nccl_type<T>(), ncclSum, ctx->comm, s);
-        if (r != ncclSuccess) throw Error{GPRX_ERR_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(r)};
+        rccl_settle(ctx->comm, ncclAllReduce(dS.p, dS.p, (size_t)(ld * Mp), nccl_type<T>(), ncclSum, ctx->comm, s),
+                    "ncclAllReduce");
     } else if (ctx->peer && ctx->world > 1) {  // the caller's collective (host round trip)
         hostcoll_allreduce_dev<T>(ctx->hc, dS.as<T>(), (int)(ld * Mp), s);
     }
@@ -2003,8 +2076,8 @@ static gprx_status sparse_lml_impl(gprx_ctx* ctx, const gprx_kernel_desc* desc, 
         DevBuf dl;
         upload<double>(dl, loc, sizeof(loc), s);
         if (ctx->comm) {
-            const ncclResult_t r = ncclAllReduce(dl.p, dl.p, MAX_LEAF * 3 + 2, ncclFloat64, ncclSum, ctx->comm, s);
-            if (r != ncclSuccess) throw Error{GPRX_ERR_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(r)};
+            rccl_settle(ctx->comm, ncclAllReduce(dl.p, dl.p, MAX_LEAF * 3 + 2, ncclFloat64, ncclSum, ctx->comm, s),
+                        "ncclAllReduce");
         } else {
             hostcoll_allreduce_dev<double>(ctx->hc, dl.as<double>(), MAX_LEAF * 3 + 2, s);
         }
@@ -2126,7 +2199,10 @@ void gprx_ctx_destroy(gprx_ctx* ctx) {
     if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
     if (ctx->aux2) (void)hipStreamDestroy(ctx->aux2);
     delete ctx->hc;
-    if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
+    // abort, not destroy: local, never waits on the peers (a communicator whose collective
+    // timed out, or whose peers already left, would block ncclCommDestroy); every stream of
+    // this context has drained by now
+    if (ctx->comm) (void)ncclCommAbort(ctx->comm);
     delete ctx;
 }
 
@@ -2275,8 +2351,12 @@ gprx_status gprx_model_predict(gprx_model* M, const void* Xq, int64_t q, void* m
 gprx_status gprx_model_posterior_cov(gprx_model* M, const void* Xa, const void* Xb, int64_t q, void* out) {
     gprx_ctx* ctx = M ? M->ctx : nullptr;
     API_BEGIN
-    GPRX_REQUIRE(M && Xa && Xb && out, GPRX_ERR_ARG, "gprx_model_posterior_cov: NULL argument");
-    if (q == 0) return GPRX_OK;
+    GPRX_REQUIRE(M && q >= 0, GPRX_ERR_ARG, "gprx_model_posterior_cov: NULL model or negative q");
+    // on a sharded fit of a multi-process context this is a collective call (gprx.h): a process
+    // with no pairs of its own still takes part
+    const bool collective = M->dist_fitted && ctx->hc && ctx->world > 1;
+    if (q == 0 && !collective) return GPRX_OK;
+    GPRX_REQUIRE(q == 0 || (Xa && Xb && out), GPRX_ERR_ARG, "gprx_model_posterior_cov: NULL argument");
     ModelLock lk(M);
     ProfBind pb_(ctx);  // after the lock: resolved (streams drained) before it is released
     GPRX_HIP(hipSetDevice(ctx->device));
@@ -2464,7 +2544,8 @@ gprx_status gprx_spd_inverse(gprx_ctx* ctx, gprx_dtype dt, void* A, int64_t n, i
 
 static const char* kclass_name(int c) {
     static const char* names[KC_COUNT] = {"kbuild", "potrf_diag", "potrf_trsm", "potrf_update", "backsolve",
-                                          "predict", "lml_grad", "spd_inverse", "other_gemm", "potrf_tiles"};
+                                          "predict", "lml_grad", "spd_inverse", "other_gemm", "potrf_tiles",
+                                          "posterior"};
     return names[c];
 }
 
@@ -2586,22 +2667,17 @@ gprx_status gprx_dev_build_time(gprx_ctx* ctx, gprx_dtype dt, const gprx_kernel_
     API_END(ctx)
 }
 
-gprx_status gprx_dev_dist_info(gprx_model* M, int64_t* out) {
+gprx_status gprx_dev_dist_info(gprx_model* M, int64_t* out, int32_t nout) {
     API_BEGIN
     GPRX_REQUIRE(M && out, GPRX_ERR_ARG, "gprx_dev_dist_info: NULL argument");
     GPRX_REQUIRE(M->dist_fitted || M->dist_stats.bytes_rank > 0, GPRX_ERR_STATE,
                  "gprx_dev_dist_info: no distributed fit on this model");
     const DistFitOut& o = M->dist_stats;
-    out[0] = o.bytes_rank;
-    out[1] = o.bytes_storage;
-    out[2] = o.gb;
-    out[3] = o.ww;
-    out[4] = o.chunk_w;
-    out[5] = o.P;
-    out[6] = (int64_t)o.est_us;
-    out[7] = M->ctx->world;
-    out[8] = M->dist_dense ? 1 : 0;
-    out[9] = M->dist_engine ? dist_pvar_chunks(M->dist_engine) : 0;
+    const int64_t v[11] = {o.bytes_rank, o.bytes_storage, o.gb, o.ww, o.chunk_w, o.P, (int64_t)o.est_us,
+                           M->ctx->world, M->dist_dense ? 1 : 0,
+                           M->dist_engine ? dist_pvar_chunks(M->dist_engine) : 0,
+                           M->dist_engine ? dist_pvar_bytes(M->dist_engine) : 0};
+    for (int i = 0; i < std::min<int32_t>(nout, 11); i++) out[i] = v[i];
     return GPRX_OK;
     API_END(M ? M->ctx : nullptr)
 }
@@ -2639,11 +2715,31 @@ gprx_status gprx_ctx_create_dist(int device, int rank, int world, const void* un
     ctx->world = world;
     ncclUniqueId id;
     std::memcpy(&id, unique_id, sizeof(id));
-    const ncclResult_t r = ncclCommInitRank(&ctx->comm, world, id, rank);
-    if (r != ncclSuccess) {
+    // GPRX_RCCL_FAIL=1 (testing): fail as an initialisation that never completes would, so the
+    // caller's fallback (a peer context over its own all-gather) can be exercised
+    if (const char* e = std::getenv("GPRX_RCCL_FAIL"); e && std::atoi(e) != 0) {
         gprx_ctx_destroy(ctx);
-        throw Error{GPRX_ERR_RCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(r)};
+        throw Error{GPRX_ERR_RCCL, "ncclCommInitRankConfig: forced failure (GPRX_RCCL_FAIL)"};
     }
+    // nonblocking initialisation, polled with a deadline (GPRX_RCCL_INIT_TIMEOUT_S, default
+    // 120 s): a rank that cannot reach its peers returns GPRX_ERR_RCCL instead of blocking
+    // the process for ever inside ncclCommInitRank
+    double tmo = 120.0;
+    if (const char* e = std::getenv("GPRX_RCCL_INIT_TIMEOUT_S"); e && std::atof(e) > 0) tmo = std::atof(e);
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    ncclComm_t comm = nullptr;
+    ncclResult_t r = ncclCommInitRankConfig(&comm, world, id, rank, &cfg);
+    try {
+        if (r != ncclSuccess && r != ncclInProgress)
+            throw Error{GPRX_ERR_RCCL, std::string("ncclCommInitRankConfig: ") + ncclGetErrorString(r)};
+        rccl_settle(comm, r, "ncclCommInitRankConfig", tmo);
+    } catch (...) {
+        if (comm) (void)ncclCommAbort(comm);
+        gprx_ctx_destroy(ctx);
+        throw;
+    }
+    ctx->comm = comm;
     ctx->hc = make_rccl_coll(ctx->comm, world, device);
     *out = ctx;
     return GPRX_OK;

@@ -46,6 +46,7 @@
 #include <cstring>
 #include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "gprx_dist.h"
@@ -115,12 +116,31 @@ struct RcclColl : HostColl {
         if (sb.bytes < bytes) sb.alloc(bytes, false);
         if (rb.bytes < bytes * world) rb.alloc(bytes * world, false);
         GPRX_HIP(hipMemcpy(sb.p, send, bytes, hipMemcpyHostToDevice));
-        rccl_ok(ncclAllGather(sb.p, rb.p, bytes, ncclUint8, comm, s), "ncclAllGather");
+        rccl_settle(comm, ncclAllGather(sb.p, rb.p, bytes, ncclUint8, comm, s), "ncclAllGather");
         GPRX_HIP(hipStreamSynchronize(s));
         GPRX_HIP(hipMemcpy(recv, rb.p, bytes * world, hipMemcpyDeviceToHost));
     }
 };
 HostColl* make_rccl_coll(ncclComm_t comm, int world, int device) { return new RcclColl(comm, world, device); }
+
+void rccl_settle(ncclComm_t comm, ncclResult_t r, const char* what, double timeout_s) {
+    const auto t0 = std::chrono::steady_clock::now();
+    while (r == ncclInProgress) {
+        ncclResult_t a = ncclInProgress;
+        const ncclResult_t q = ncclCommGetAsyncError(comm, &a);
+        if (q != ncclSuccess) {
+            r = q;
+            break;
+        }
+        r = a;
+        if (r != ncclInProgress) break;
+        if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s)
+            throw Error{GPRX_ERR_RCCL, std::string(what) + ": not complete after " + std::to_string((int)timeout_s) +
+                                           " s"};
+        std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+    rccl_ok(r, what);
+}
 
 struct CallbackColl : HostColl {
     gprx_allgather_fn fn;
@@ -272,6 +292,7 @@ struct DistRank {
     std::vector<std::vector<uint64_t>> wp;  // every rank's window pieces as mapped here
     std::vector<int64_t> roff;         // own row blocks: element offset from the first piece's base
     DMem t_vslot, pvpart, pvsum;       // posterior solve: window slots of V_k(c) on every rank, partial sums
+    DMem pvR, pvX, pvTab;              // posterior solve: K(Z, X_own) / W (nq x own rows), X_own, its tables
     std::vector<void*> opened;         // IPC mappings to close
     T* sbase() const { return store.empty() ? nullptr : store[0]->template as<T>(); }
     int64_t store_bytes() const {
@@ -317,7 +338,6 @@ struct DistEngine : DistEngineBase {
     unsigned ep = 0, sep = 0;  // epochs of the fits and of the solves (flag values)
     unsigned vep = 0;          // epoch of the posterior solves
     int pv_nch = 0;            // query chunks per posterior solve (0: none: one rank, or no window)
-    DMem pvR;                  // the posterior solve's K(Z, X) / W (every local rank's blocks)
     std::vector<std::unique_ptr<DistRank<T>>> ranks;  // virtual: all g; otherwise this process's rank
     int* dbg = nullptr;  // GPRX_PT_DEBUG: the launch's per-workgroup status words (pinned host memory)
     int dbg_n = 0;
@@ -1167,6 +1187,20 @@ int dist_pvar_chunks(DistEngineBase* eng) {
 }
 
 template <typename T>
+static int64_t pv_bytes_of(DistEngineBase* eng) {
+    auto* E = dynamic_cast<DistEngine<T>*>(eng);
+    if (!E) return -1;
+    int64_t b = 0;
+    for (auto& Rp : E->ranks) b = std::max<int64_t>(b, (int64_t)Rp->pvR.bytes);
+    return b;
+}
+int64_t dist_pvar_bytes(DistEngineBase* eng) {
+    int64_t v = pv_bytes_of<double>(eng);
+    if (v < 0) v = pv_bytes_of<float>(eng);
+    return std::max<int64_t>(0, v);
+}
+
+template <typename T>
 void dist_posterior(DistEngineBase* eng, const KCanon<T>& K, const T* X, const T* tabX, int64_t n, int d, const T* Z,
                     const T* tabZ, int nch, bool pairs, std::vector<double>& sum, hipStream_t s) {
     auto* Ep = dynamic_cast<DistEngine<T>*>(eng);
@@ -1174,13 +1208,43 @@ void dist_posterior(DistEngineBase* eng, const KCanon<T>& K, const T* X, const T
     DistEngine<T>& E = *Ep;
     GPRX_REQUIRE(nch >= 1 && nch <= E.pv_nch, GPRX_ERR_ARG, "distributed posterior: too many query chunks");
     const int nc = E.L.nc;
-    const int64_t np = E.np, nq = (int64_t)nch * DB;
-    // K(Z, X): nq x np, ld nq (the padding columns >= n stay zero); each rank's task overwrites its
-    // own blocks' columns with W = K - sum L V
-    if (E.pvR.bytes < sizeof(T) * (size_t)nq * np) E.pvR.alloc(sizeof(T) * (size_t)nq * np, false);
-    T* R = E.pvR.template as<T>();
-    GPRX_HIP(hipMemsetAsync(R, 0, sizeof(T) * (size_t)nq * np, s));
-    launch_kbuild<T>(K, Z, tabZ, nq, X, tabX, n, d, R, nq, 0, false, T(0), E.ranks[0]->flag.template as<int>(), s);
+    const int64_t nq = (int64_t)nch * DB;
+    (void)tabX;
+    // per rank: K(Z, X_own), nq x (own row blocks x 128), ld nq -- only the rank's own training rows
+    // (packed in orows order; the padding columns >= n stay zero); each task overwrites its block's
+    // columns with W = K - sum L V.  X_own is gathered from X and gets its own sin/cos tables.
+    int* nfl = E.ranks[0]->flag.template as<int>();
+    GPRX_HIP(hipMemsetAsync(nfl, 0, sizeof(int), s));
+    for (auto& Rp : E.ranks) {
+        DistRank<T>& Rk = *Rp;
+        const int64_t nown = (int64_t)Rk.orows.size();
+        if (nown == 0) continue;
+        const size_t rb = sizeof(T) * (size_t)nq * nown * DB;
+        if (Rk.pvR.bytes < rb) Rk.pvR.alloc(rb, false);
+        if (Rk.pvX.bytes < sizeof(T) * (size_t)nown * DB * d) Rk.pvX.alloc(sizeof(T) * (size_t)nown * DB * d, false);
+        T* Xo = Rk.pvX.template as<T>();
+        int64_t nvalid = 0;
+        for (int64_t li = 0; li < nown; li++) {
+            const int64_t r0 = (int64_t)Rk.orows[li] * DB, cnt = std::min<int64_t>(DB, n - r0);
+            if (cnt <= 0) continue;
+            // (own blocks are full but possibly the last one, nc - 1, which comes last in orows)
+            GPRX_HIP(hipMemcpyAsync(Xo + li * DB * d, X + r0 * d, sizeof(T) * cnt * d, hipMemcpyDeviceToDevice, s));
+            nvalid = li * DB + cnt;
+        }
+        const T* tabo = nullptr;
+        if (K.nper > 0) {
+            const size_t tb = sizeof(T) * 2 * K.nper * (size_t)std::max<int64_t>(nvalid, 1) * d;
+            if (Rk.pvTab.bytes < tb) Rk.pvTab.alloc(tb, false);
+            launch_sincos_tables<T>(K, Xo, nvalid, d, Rk.pvTab.template as<T>(), s);
+            tabo = Rk.pvTab.template as<T>();
+        }
+        GPRX_HIP(hipMemsetAsync(Rk.pvR.p, 0, rb, s));
+        launch_kbuild<T>(K, Z, tabZ, nq, Xo, tabo, nvalid, d, Rk.pvR.template as<T>(), nq, 0, false, T(0), nfl, s);
+    }
+    // (non-finite query kernel values are not an error: the reference's ComputeKernelVectorInternal
+    // has no check, lib/GaussianProcess.cpp:684-693, and its operator() returns the NaN, as the
+    // single-GPU path does; the flag the build raises is cleared here and by the next fit)
+    GPRX_HIP(hipMemsetAsync(nfl, 0, sizeof(int), s));
     GPRX_HIP(hipStreamSynchronize(s));
     host_barrier(E);  // every rank's previous use of its window (a fit, an earlier batch) is over
     E.vep++;
@@ -1206,7 +1270,7 @@ void dist_posterior(DistEngineBase* eng, const KCanon<T>& K, const T* X, const T
         a.o_vflags = E.MB.o_vflags;
         a.vslot = Rk.t_vslot.template as<uint64_t>();
         a.vstride = E.pv_nch;
-        a.R = R;
+        a.R = Rk.pvR.template as<T>();
         a.nch = nch;
         a.pairs = pairs ? 1 : 0;
         a.ep = E.vep;

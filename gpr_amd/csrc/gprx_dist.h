@@ -17,6 +17,12 @@ struct HostColl {
 };
 // RCCL (ncclAllGather through a device staging buffer)
 HostColl* make_rccl_coll(ncclComm_t comm, int world, int device);
+// An RCCL call on a nonblocking communicator (gprx_ctx_create_dist creates it with
+// config.blocking = 0 so that its initialisation can be time-limited): a result of
+// ncclInProgress is polled with ncclCommGetAsyncError until it settles; a failure, or no
+// result after `timeout_s`, throws GPRX_ERR_RCCL (the context's destruction then aborts the
+// communicator: gprx_ctx_destroy uses ncclCommAbort, which never waits on the peers).
+void rccl_settle(ncclComm_t comm, ncclResult_t r, const char* what, double timeout_s = 600.0);
 // the caller's function (gprx_ctx_create_peer)
 HostColl* make_callback_coll(gprx_allgather_fn fn, void* user, int world);
 
@@ -82,6 +88,8 @@ void dist_lml_grad(DistEngineBase* eng, const KCanon<T>& K, const KCanon<T>* Kd,
 // The sharded posterior covariance (dist_pvar_kernel): the query chunks of 128 columns one solve
 // takes (0: not available -- one rank, or no receive window to carry the V tiles).
 int dist_pvar_chunks(DistEngineBase* eng);
+// device bytes of the last posterior solve's K(Z, X_own) workspace (max over this process's ranks)
+int64_t dist_pvar_bytes(DistEngineBase* eng);
 // sum[j] = sum over the n training rows of V[., j] V[., j'] with V = L^{-1} K(X, Z), Z = nch x 128
 // queries (device, row-major nch 128 x d; tabZ their sin/cos tables when K has periodic leaves),
 // j' = j, or (pairs) j' = j + 64 within each chunk of 128; summed over every rank (host result).
@@ -134,7 +142,8 @@ struct PVArgs {
     int64_t o_vflags;        // byte offset of the V flags: rank q's word (c nc + k) = ep when V_k(c) landed
     const uint64_t* vslot;   // [(q vstride + c) nc + k] window slot of V_k(c) in rank q (DB x DB, (query, row))
     int vstride;
-    T* R;                    // nch DB x np, ld nch DB: K(Z, X); W = K - sum L V overwrites the own blocks
+    T* R;                    // nch DB x nown DB, ld nch DB: K(Z, X_own), own block orows[li] at column
+                             // block li; W = K - sum L V overwrites it
     int nch;                 // chunks of 128 query columns
     int pairs;               // 0: column j with itself; 1: columns j and 64 + j of a chunk (j < 64)
     unsigned ep;             // this solve's epoch

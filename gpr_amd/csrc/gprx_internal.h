@@ -228,7 +228,7 @@ struct Error {
 // of the classes below, on the stream the kernel is launched on.
 // ---------------------------------------------------------------------------------
 enum KClass { KC_BUILD = 0, KC_DIAG, KC_TRSM, KC_UPDATE, KC_BACKSOLVE, KC_PREDICT, KC_LML_GRAD, KC_INVERSE, KC_OTHER,
-              KC_TILES, KC_COUNT };
+              KC_TILES, KC_POSTERIOR, KC_COUNT };
 struct Prof {
     bool on = false;
     struct Rec {

@@ -429,7 +429,7 @@ __global__ __launch_bounds__(NT) void dist_pvar_kernel(PVArgs<T> a) {
         }
         if (!ok) break;
         // W(q, m) = K(z_q, x_m) - acc(m, q), in place in R (chunk c's rows, block i's columns)
-        T* Wt = a.R + (int64_t)c * DB + (int64_t)i * DB * ldr;
+        T* Wt = a.R + (int64_t)c * DB + (int64_t)li * DB * ldr;
 #pragma unroll
         for (int x = 0; x < 2; x++)
 #pragma unroll

@@ -121,7 +121,7 @@ def lib():
                                            ctypes.POINTER(ctypes.c_void_p)]
         L.gprx_ctx_create_peer.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ALLGATHER_FN, ctypes.c_void_p,
                                            ctypes.POINTER(ctypes.c_void_p)]
-        L.gprx_dev_dist_info.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64)]
+        L.gprx_dev_dist_info.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64), ctypes.c_int32]
         L.gprx_ctx_destroy.argtypes = [ctypes.c_void_p]
         L.gprx_model_create.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
         L.gprx_model_destroy.argtypes = [ctypes.c_void_p]
@@ -229,6 +229,36 @@ def _input(a, dtype):
             raise TypeError("device inputs must be contiguous and of the model's dtype")
         return a
     return np.ascontiguousarray(a, dtype)
+
+
+def runtime_info():
+    """The HIP runtime, HSA runtime and RCCL this process has mapped (from /proc/self/maps), and
+    whether more than one copy of any is mapped.
+
+    libgprx asks for them by soname (libamdhip64.so.7, librccl.so.1; RUNPATH /opt/rocm/lib).
+    The dynamic loader resolves a soname to an object already loaded under that soname first,
+    so the binding is set by whichever comes first in the process: loading libgprx first binds
+    /opt/rocm's (ROCm 7.2, what it is compiled with, and what bench.py and the tests use); importing
+    the PyTorch wheel first binds the copies it bundles (torch/lib), which libgprx then shares.
+    Either way there is ONE runtime per process."""
+    found = {"libamdhip64": set(), "librccl": set(), "libhsa-runtime64": set()}
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                parts = line.split()
+                if len(parts) < 6:
+                    continue
+                path = parts[5]
+                base = os.path.basename(path)
+                for k in found:
+                    if base.startswith(k + ".so"):
+                        found[k].add(os.path.realpath(path))
+    except OSError:
+        pass
+    out = {k: sorted(v) for k, v in found.items()}
+    out["single_copy"] = all(len(v) <= 1 for v in found.values())
+    out["torch_loaded_first"] = any("/torch/lib/" in p for v in found.values() for p in v)
+    return out
 
 
 def device_count():
@@ -536,10 +566,10 @@ class Model:
         """Layout and memory of the last distributed fit (gprx_dev_dist_info): per-rank device
         bytes of the engine and of the packed storage, row-block group, window panels, update
         chunk width, workgroups per rank, simulated makespan (us)."""
-        v = (ctypes.c_int64 * 10)()
-        self._c(lib().gprx_dev_dist_info(self.h, v))
         keys = ["bytes_rank", "bytes_storage", "gb", "ww", "chunk_w", "P", "est_us", "world", "dense_factor",
-                "posterior_chunks"]
+                "posterior_chunks", "posterior_bytes_rank"]
+        v = (ctypes.c_int64 * len(keys))()
+        self._c(lib().gprx_dev_dist_info(self.h, v, len(keys)))
         return dict(zip(keys, list(v)))
 
     def alpha(self):

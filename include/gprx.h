@@ -12,9 +12,11 @@
  * below instead of Eigen + LAPACK.  Each entry point names the reference code it replaces.
  *
  * Conventions
- *   - plain C types only; every matrix a caller passes is HOST memory, row-major, in the
- *     model's scalar type (float for GPRX_F32, double for GPRX_F64), exactly the layout of
- *     the reference's Eigen RowMajor MatrixType (include/GaussianProcess.h:42);
+ *   - plain C types only; every matrix a caller passes is row-major, in the model's scalar
+ *     type (float for GPRX_F32, double for GPRX_F64), exactly the layout of the reference's
+ *     Eigen RowMajor MatrixType (include/GaussianProcess.h:42); it is HOST memory except where
+ *     an entry point says "host or device memory" (gprx_model_set_data, gprx_sparse_fit: a
+ *     pointer from gprx_device_alloc is read in HBM, without a PCIe transfer);
  *   - no entry point throws; each returns a gprx_status and records a message retrievable
  *     with gprx_last_error();
  *   - a model owns its device buffers (training inputs, labels, Cholesky factor, regression
@@ -112,8 +114,12 @@ gprx_status gprx_device_count(int* count);
 gprx_status gprx_ctx_create(int device, gprx_ctx** out);
 /* Multi-GPU context: one process per GPU, RCCL communicator over xGMI.  `unique_id` is
  * GPRX_UNIQUE_ID_BYTES produced by gprx_dist_unique_id() on rank 0 and shared by the
- * caller (e.g. torch.distributed broadcast).  New capability: the reference is
- * single-host OpenMP only. */
+ * caller (any host channel: bench.py uses gpr_amd/hostcoll.py's sockets).  The communicator is
+ * initialised nonblocking and polled with a deadline (GPRX_RCCL_INIT_TIMEOUT_S, default 120 s):
+ * a rank that cannot reach its peers gets GPRX_ERR_RCCL instead of blocking for ever, and the
+ * caller can fall back to gprx_ctx_create_peer (every rank must then do so: bench.py agrees on
+ * it over its host channel).  GPRX_RCCL_FAIL=1 fails the call on purpose (tests).  New
+ * capability: the reference is single-host OpenMP only. */
 #define GPRX_UNIQUE_ID_BYTES 128
 gprx_status gprx_dist_unique_id(void* out);
 gprx_status gprx_ctx_create_dist(int device, int rank, int world, const void* unique_id, gprx_ctx** out);
@@ -147,10 +153,15 @@ gprx_status gprx_ctx_set_stats(gprx_ctx* ctx, int32_t enable);
 gprx_status gprx_ctx_get_stats(gprx_ctx* ctx, gprx_kstat* out, int32_t max, int32_t* count);
 
 /* Device buffers on the context's GPU, for inputs that stay resident in HBM across calls (the
- * calls documented as taking "host or device memory" read them without a PCIe transfer).  A
- * process that loads this library next to another HIP runtime (a framework's bundled one) cannot
- * hand over that runtime's allocations once this library has initialised the device, so the
- * library allocates them itself.  Upload / download are synchronous on the context's stream. */
+ * calls documented as taking "host or device memory" read them without a PCIe transfer).
+ * Upload / download are synchronous on the context's stream.
+ * Runtime binding: libgprx asks for libamdhip64.so.7 and librccl.so.1 by soname (RUNPATH
+ * /opt/rocm/lib), and the loader resolves a soname to an object already in the process first.
+ * Loaded before any other HIP user it binds /opt/rocm's runtime and RCCL (what it is compiled
+ * against; bench.py and the tests load it so).  Loaded after the PyTorch wheel it binds the
+ * copies that wheel bundles instead -- one runtime in the process either way, and a pointer
+ * from that runtime's allocator is then this library's too; loaded BEFORE the wheel, the wheel
+ * maps a second, separate runtime whose allocations this library cannot use. */
 gprx_status gprx_device_alloc(gprx_ctx* ctx, int64_t bytes, void** out);
 gprx_status gprx_device_free(gprx_ctx* ctx, void* p);
 gprx_status gprx_device_upload(gprx_ctx* ctx, void* dst, const void* src, int64_t bytes);
@@ -175,14 +186,21 @@ gprx_status gprx_model_set_noise(gprx_model* model, double sigma);
                                       gprx_fit_info.method = 1 then.  An exactly singular matrix
                                       gives GPRX_ERR_SINGULAR (the reference returns non-finite
                                       regression vectors there) */
-#define GPRX_FIT_DISTRIBUTED 2u    /* multi-GPU fit on a gprx_ctx_create_dist context (implied when
-                                      world > 1; forces the path at world = 1): row blocks dealt
-                                      cyclically over the ranks (N^2/world of the factor per GPU),
-                                      one persistent tile launch per rank, RCCL broadcast of each
-                                      diagonal-block inverse and exchange of each factored panel.
-                                      Afterwards alpha and predict are available, and the LML
-                                      (value and gradient, GPRX_LML_DISTRIBUTED) runs on it; the
-                                      posterior covariance and core matrix need a single-GPU fit */
+#define GPRX_FIT_DISTRIBUTED 2u    /* multi-GPU fit on a gprx_ctx_create_dist / _peer context
+                                      (implied when world > 1; forces the path at world = 1): row
+                                      blocks dealt in cyclic groups over the ranks (each GPU stores
+                                      and builds only the lower tiles of its own rows, ~N^2/(2 world)),
+                                      one persistent tile launch per rank; the exchange is device-
+                                      initiated: the task that factors a diagonal block stores its
+                                      inverse into every peer's IPC-mapped mailbox, the task that
+                                      finishes a panel tile stores it into the receive windows of
+                                      the ranks that read it (xGMI stores + flags; RCCL / the
+                                      caller's collective only for host-side agreement).  Afterwards
+                                      alpha, predict, the posterior covariance (the queries' forward
+                                      solve sharded the same way, no N^2 on any rank) and the LML
+                                      (value and gradient, GPRX_LML_DISTRIBUTED) run on it; the core
+                                      matrix gathers the dense factor onto each process (the
+                                      reference returns all of C) */
 #define GPRX_FIT_F32_NO_REFINE 4u  /* fp32 models: skip the fp64 iterative refinement of alpha.  By
                                       default an fp32 fit factorises in fp32 and refines alpha in
                                       fp64 until it agrees with the double solve: the reference
@@ -215,10 +233,16 @@ gprx_status gprx_model_set_alpha(gprx_model* model, const void* alpha);
 gprx_status gprx_model_predict(gprx_model* model, const void* Xq, int64_t q, void* mean, void* deriv);
 /* operator()(x,y) = k(x,y) - Kx^T C Ky for q pairs (lib/GaussianProcess.cpp:84-99), via
  * the Cholesky factor: k(x,y) - (L^{-1}Kx).(L^{-1}Ky).  GetCredibleInterval (:102-114) is
- * 2*sqrt(max(0, out)) of the pair (x,x). */
+ * 2*sqrt(max(0, out)) of the pair (x,x).  Non-finite kernel values give NaN, as the
+ * reference's (no check in ComputeKernelVectorInternal, :684-693).
+ * On a SHARDED fit of a multi-process context this is a COLLECTIVE call: every process calls
+ * it (q = 0 and NULL pointers allowed for a process with no pairs).  The processes agree on
+ * their arguments first: identical pairs are solved once; different ones (e.g. each process
+ * its own query slice) are gathered, solved together, and each process receives its own. */
 gprx_status gprx_model_posterior_cov(gprx_model* model, const void* Xa, const void* Xb, int64_t q, void* out);
 /* The core matrix C = (K + sigma^2 I)^{-1} (m_CoreMatrix, lib/GaussianProcess.cpp:652)
- * materialised from the factor (potri) into host memory, N x N. */
+ * materialised from the factor (potri) into host memory, N x N.  On a sharded fit of a
+ * multi-process context a COLLECTIVE call (the dense factor is gathered from every rank). */
 gprx_status gprx_model_core_matrix(gprx_model* model, void* C);
 
 #define GPRX_LML_GRAD 1u   /* also compute the hyper-parameter gradient */
@@ -227,9 +251,10 @@ gprx_status gprx_model_core_matrix(gprx_model* model, void* C);
 #define GPRX_LML_FORCE_LU 8u /* refit with GPRX_FIT_FORCE_LU (the SVD inversion methods) */
 #define GPRX_LML_DISTRIBUTED 4u /* refit with GPRX_FIT_DISTRIBUTED (implied on a multi-rank or
                               virtual context): log det = sum of the ranks' diagonal blocks,
-                              C from the factor every rank assembles from its tiles (replicated
-                              potri), each rank's gradient partial over its own row blocks
-                              combined by one all-reduce of the P partials */
+                              C = U U^T in tiles riding along in the sharded factorisation (no
+                              rank holds N^2), each rank's gradient partial over its own row
+                              blocks combined by one all-reduce of the P partials (SURVEY.md
+                              8(e)).  A collective call on a multi-process context */
 /* GaussianLogLikelihood::operator() / GetValueAndParameterDerivatives
  * (include/Likelihood.h:166-285) for m = 1: value = -1/2 y^T C y - 1/2 log det - N/2 log 2pi,
  * grad_p = 1/2 tr((alpha alpha^T - C) dK/dp).  Refits from scratch like the reference.

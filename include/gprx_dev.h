@@ -71,14 +71,16 @@ gprx_status gprx_dev_build_time(gprx_ctx* ctx, gprx_dtype dtype, const gprx_kern
  * with device copies in place of the RCCL broadcast / panel exchange (gprx_dist.cpp).  Models
  * of this context fit with the multi-GPU algorithm end to end on a single device. */
 gprx_status gprx_ctx_create_virtual(int device, int world, gprx_ctx** out);
-/* Layout and memory of a model's last distributed fit (gprx_dist.cpp): out[0] device bytes the
- * engine holds per rank (max over this process's ranks), out[1] of which the packed own row
- * blocks, out[2] row-block group gb, out[3] window panels ww, out[4] update chunk width, out[5]
- * workgroups per rank, out[6] simulated makespan (us), out[7] ranks, out[8] 1 when this process
- * holds the dense N x N factor (gathered for the core matrix or a VALU-gradient tree; the
- * posterior covariance solves across the ranks without it), out[9] query chunks of 128 one
- * sharded posterior solve takes (0: none on this layout). */
-gprx_status gprx_dev_dist_info(gprx_model* model, int64_t* out);
+/* Layout and memory of a model's last distributed fit (gprx_dist.cpp), written to the first
+ * min(nout, 11) slots of out: out[0] device bytes the engine holds per rank (max over this
+ * process's ranks; the fit's buffers), out[1] of which the packed own row blocks, out[2] row-block
+ * group gb, out[3] window panels ww, out[4] update chunk width, out[5] workgroups per rank, out[6]
+ * simulated makespan (us), out[7] ranks, out[8] 1 when this process holds the dense N x N factor
+ * (gathered for the core matrix or a VALU-gradient tree; the posterior covariance solves across
+ * the ranks without it), out[9] query chunks of 128 one sharded posterior solve takes (0: none
+ * on this layout), out[10] device bytes of the last sharded posterior solve's K(Z, X_own)
+ * workspace per rank (its queries x this rank's own rows only). */
+gprx_status gprx_dev_dist_info(gprx_model* model, int64_t* out, int32_t nout);
 /* Parity hook for the tile engine's diagonal-block factor: the 128 x 128 SPD block A (column-
  * major, host) factored by variant 0 (rank-8 register image), 1 (blocked) or 2 (blocked with
  * look-ahead): L (lower triangle meaningful, the upper keeps A), Linv = L^{-1} (column-major)

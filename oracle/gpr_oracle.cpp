@@ -635,48 +635,70 @@ static std::vector<T> core_matrix(const Node<T>& k, const T* X, int n, int d, T 
 // and complexity gradients (:255-273), EfficientDeterminant (:138-145) with the clamps
 // (:305-314) and the constant term (:325).  Y is n x 1.  det_out: the long-double
 // determinant; logdet_out: log of its three factors summed (exact).
+// The sparse likelihood's core quantities: SparseGaussianProcess::ComputeCoreMatrices
+// (include/SparseGaussianProcess.h:323-350: K = Kmm + jitter I, K_inv, Knm, I_sigma),
+// SparseGaussianLogLikelihood::EfficientInversion (include/SparseLikelihood.h:129-135, called
+// with B = K_inv, B_inv = K: C_inv = inv(sigma^2 I + Knm K_inv Knm^T) by Woodbury) and the
+// "inner" matrix B_inv + X^T A_inv X = K + Knm^T Knm / sigma^2 whose determinant enters
+// EfficientDeterminant (:138-145).
 template <class T>
-static void sparse_lml(const Node<T>& k, const T* X, const T* Y, int n, int d, const T* Xm, int M, T sigma, T jitter,
-                       T* value, T* grad, double* det_out, double* logdet_out) {
-    typedef long double HP;
+struct SparseCore {
+    std::vector<T> K, Kinv, Knm, inner, Cinv;
+    T s2, ainv;
+};
+template <class T>
+static SparseCore<T> sparse_core(const Node<T>& k, const T* X, int n, int d, const T* Xm, int M, T sigma, T jitter) {
     if (M == 0)
         throw std::string("SparseLikelihood::GetValueAndParameterDerivative: there are no inducing samples specified");
+    SparseCore<T> c;
     const bool stable = (jitter < std::numeric_limits<T>::min()) ? true : false;
     // ComputeKernelMatrixWithJitter (SparseGaussianProcess.h:174-180), InvertKernelMatrix
-    std::vector<T> K((size_t)M * M);
-    kernel_matrix(k, Xm, M, d, K.data());
-    for (int i = 0; i < M; i++) K[(size_t)i * M + i] += jitter;
-    std::vector<T> Kinv = invert<T>(K, M, FullPivotLU, stable);
+    c.K.resize((size_t)M * M);
+    kernel_matrix(k, Xm, M, d, c.K.data());
+    for (int i = 0; i < M; i++) c.K[(size_t)i * M + i] += jitter;
+    c.Kinv = invert<T>(c.K, M, FullPivotLU, stable);
     if (!(M <= n))
         throw std::string("SparseGaussianProcess::ComputeKernelVectorMatrix: number of dense samples must be higher than the number of sparse samples");
-    std::vector<T> Knm((size_t)n * M);
+    c.Knm.resize((size_t)n * M);
 #pragma omp parallel for schedule(static)
     for (int i = 0; i < n; i++)
-        for (int j = 0; j < M; j++) Knm[(size_t)i * M + j] = keval(k, X + (size_t)i * d, Xm + (size_t)j * d, d);
+        for (int j = 0; j < M; j++) c.Knm[(size_t)i * M + j] = keval(k, X + (size_t)i * d, Xm + (size_t)j * d, d);
     if (sigma <= 0) throw std::string("SparseGaussianProcess::ComputeCoreMatrices: sigma must be positive.");
     if (n == 0) throw std::string("SparseGaussianProcess::ComputeCoreMatrices: empty sample set.");
-    const T s2 = sigma * sigma;  // I_sigma diagonal (GetSigmaSquared)
-    const T ainv = T(1.0) / s2;  // A_inv = 1 / A.diagonal()
+    c.s2 = sigma * sigma;     // I_sigma diagonal (GetSigmaSquared)
+    c.ainv = T(1.0) / c.s2;  // A_inv = 1 / A.diagonal()
+    const T ainv = c.ainv;
+    const std::vector<T>& Knm = c.Knm;
     // EfficientInversion: inner = B_inv + X^T A_inv X = K + Knm^T A_inv Knm; C_inv = A_inv - A_inv X inner^-1 X^T A_inv
-    std::vector<T> inner((size_t)M * M, T(0));
+    c.inner.assign((size_t)M * M, T(0));
 #pragma omp parallel for schedule(static)
     for (int a = 0; a < M; a++)
         for (int b = 0; b < M; b++) {
             T acc = 0;
             for (int i = 0; i < n; i++) acc += Knm[(size_t)i * M + a] * ainv * Knm[(size_t)i * M + b];
-            inner[(size_t)a * M + b] = K[(size_t)a * M + b] + acc;
+            c.inner[(size_t)a * M + b] = c.K[(size_t)a * M + b] + acc;
         }
-    std::vector<T> inner_inv = invert<T>(inner, M, FullPivotLU, false);  // GetInverseMatrix (SparseLikelihood.h:100-102)
+    std::vector<T> inner_inv = invert<T>(c.inner, M, FullPivotLU, false);  // GetInverseMatrix (SparseLikelihood.h:100-102)
     std::vector<T> Z((size_t)n * M);  // X inner^-1
     gemm(Knm.data(), inner_inv.data(), Z.data(), n, M, M);
-    std::vector<T> Cinv((size_t)n * n);
+    c.Cinv.resize((size_t)n * n);
 #pragma omp parallel for schedule(static)
     for (int i = 0; i < n; i++)
         for (int j = 0; j < n; j++) {
             T acc = 0;
             for (int a = 0; a < M; a++) acc += Z[(size_t)i * M + a] * Knm[(size_t)j * M + a];
-            Cinv[(size_t)i * n + j] = (i == j ? ainv : T(0)) - ainv * acc * ainv;
+            c.Cinv[(size_t)i * n + j] = (i == j ? ainv : T(0)) - ainv * acc * ainv;
         }
+    return c;
+}
+
+template <class T>
+static void sparse_lml(const Node<T>& k, const T* X, const T* Y, int n, int d, const T* Xm, int M, T sigma, T jitter,
+                       T* value, T* grad, double* det_out, double* logdet_out) {
+    typedef long double HP;
+    SparseCore<T> core = sparse_core(k, X, n, d, Xm, M, sigma, jitter);
+    const std::vector<T>&Kinv = core.Kinv, &Knm = core.Knm, &inner = core.inner, &Cinv = core.Cinv;
+    const T s2 = core.s2;
     // data fit (:301-302): -0.5 Y^T C_inv Y
     std::vector<T> v(n);  // C_inv Y
     for (int i = 0; i < n; i++) {
@@ -1009,6 +1031,33 @@ int orc_num_threads() { return omp_get_max_threads(); }
     }
 ORC_DEFINE_SPARSE_LML(f64, double)
 ORC_DEFINE_SPARSE_LML(f32, float)
+
+/* SparseLikelihood::GetCoreMatrices + EfficientInversion + EfficientDeterminant (the quantities
+   tests/SparseInferenceTest.cpp:37-224 checks): K = Kmm + jitter I (M x M), Kinv (M x M), Knm
+   (n x M), Cinv = the Woodbury inverse of sigma^2 I + Knm Kinv Knm^T (n x n), det_eff = the
+   long-double |Kinv| |sigma^2 I| |K + Knm^T Knm / sigma^2| (include/SparseLikelihood.h:138-145;
+   |B| made finite as there), narrowed to double.  Any output pointer may be NULL. */
+#define ORC_DEFINE_SPARSE_CORE(SUF, T)                                                             \
+    int orc_sparse_core_##SUF(const char* ks, const T* X, int n, int d, const T* Xm, int M, T sigma, T jitter, \
+                              T* K, T* Kinv, T* Knm, T* Cinv, double* det_eff) {                   \
+        ORC_TRY auto k = kernel_from<T>(ks);                                                       \
+        SparseCore<T> c = sparse_core(*k, X, n, d, Xm, M, sigma, jitter);                           \
+        if (K) std::copy(c.K.begin(), c.K.end(), K);                                               \
+        if (Kinv) std::copy(c.Kinv.begin(), c.Kinv.end(), Kinv);                                   \
+        if (Knm) std::copy(c.Knm.begin(), c.Knm.end(), Knm);                                       \
+        if (Cinv) std::copy(c.Cinv.begin(), c.Cinv.end(), Cinv);                                   \
+        if (det_eff) {                                                                             \
+            typedef long double HP;                                                                \
+            HP det_B = det_long_double(c.Kinv, M);                                                 \
+            if (std::isinf(det_B)) det_B = std::numeric_limits<HP>::max();                         \
+            HP prodA = 1;                                                                          \
+            for (int i = 0; i < n; i++) prodA *= (HP)c.s2;                                         \
+            *det_eff = (double)(det_B * prodA * det_long_double(c.inner, M));                      \
+        }                                                                                          \
+        ORC_CATCH                                                                                  \
+    }
+ORC_DEFINE_SPARSE_CORE(f64, double)
+ORC_DEFINE_SPARSE_CORE(f32, float)
 
 ORC_DEFINE(f64, double)
 ORC_DEFINE(f32, float)

@@ -198,6 +198,23 @@ def sparse_fit(kstr, X, Y, Xm, sigma, jitter, dtype=np.float64):
     return Kinv, RV, RM
 
 
+def sparse_core(kstr, X, Xm, sigma, jitter, dtype=np.float64):
+    """The sparse likelihood's core quantities (SparseLikelihood::GetCoreMatrices,
+    EfficientInversion, EfficientDeterminant; include/SparseLikelihood.h:62-145):
+    returns (K = Kmm + jitter I, Kinv, Knm, Cinv = inv(sigma^2 I + Knm Kinv Knm^T) by Woodbury,
+    det_eff = the long-double efficient determinant narrowed to double)."""
+    suf, ct = _dt(dtype)
+    X, Xm = _c(X, dtype), _c(Xm, dtype)
+    n, d = X.shape
+    M = Xm.shape[0]
+    K, Kinv = np.empty((M, M), dtype), np.empty((M, M), dtype)
+    Knm, Cinv = np.empty((n, M), dtype), np.empty((n, n), dtype)
+    det = ctypes.c_double()
+    _call(f"orc_sparse_core_{suf}", kstr.encode(), _p(X), n, d, _p(Xm), M, ct(sigma), ct(jitter), _p(K), _p(Kinv),
+          _p(Knm), _p(Cinv), ctypes.byref(det))
+    return K, Kinv, Knm, Cinv, det.value
+
+
 def sparse_lml(kstr, X, Y, Xm, sigma, jitter, dtype=np.float64, with_grad=True):
     """SparseGaussianLogLikelihood value (+ gradient), N x N restatement (small n).
     Returns (value, grad, det, logdet)."""

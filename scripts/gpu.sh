@@ -38,7 +38,7 @@ fail() { echo "step $1 failed (rc $2)"; tail -n 30 "$3" 2>/dev/null; exit "$2"; 
 prof_leg() {  # $1 = leg: kernel trace + stats of one bench leg in its own process
     local leg=$1
     (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_$leg" -o "$leg" \
-        -- python3 "$R/bench.py" --legs "$leg" --cpu-n 0 > "$O/prof_$leg.json" 2> "$O/prof_$leg.err") \
+        -- python3 "$R/bench.py" --legs "$leg" --cpu-n 0 --cpu-lml-ns "" --cpu-predict-q 0 > "$O/prof_$leg.json" 2> "$O/prof_$leg.err") \
         || fail "profile:$leg" $? "$O/prof_$leg.err"
     echo "profile $leg ok"
 }
@@ -47,7 +47,7 @@ pmc_leg() {  # $1 = leg, $2 = output name, $3.. = counters (one block-limited pa
     local leg=$1 name=$2
     shift 2
     (cd /tmp && timeout -s KILL 240 rocprofv3 --pmc "$@" --output-format csv -d "$O/$name" -o "$name" \
-        -- python3 "$R/bench.py" --legs "$leg" --cpu-n 0 --steps 2 --warmup 1 --build-iters 2 \
+        -- python3 "$R/bench.py" --legs "$leg" --cpu-n 0 --cpu-lml-ns "" --cpu-predict-q 0 --steps 2 --warmup 1 --build-iters 2 \
         > "$O/$name.json" 2> "$O/$name.err") || fail "pmc:$name" $? "$O/$name.err"
     echo "pmc $name ok"
 }
@@ -111,7 +111,7 @@ for step in "$@"; do
         ;;
     ab)
         shopt -s nullglob
-        Q="--cpu-n 0 --legs c3 --steps 20 $AB_ARGS"
+        Q="--cpu-n 0 --cpu-predict-q 0 --legs c3 --steps 20 $AB_ARGS"
         for rep in 1 2; do
             for f in tools/ab/*.so; do
                 b=$(basename "$f" .so)
@@ -133,7 +133,7 @@ for step in "$@"; do
             || fail distab $? "$O/distab.err"
         ;;
     envab)
-        Q="--cpu-n 0 --legs c3 --steps 20 $AB_ARGS"
+        Q="--cpu-n 0 --cpu-predict-q 0 --legs c3 --steps 20 $AB_ARGS"
         for rep in 1 2; do
             for v in $AB_ENVS; do
                 b=$(echo "$v" | tr '=/' '__')

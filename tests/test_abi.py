@@ -50,3 +50,73 @@ def test_no_device_fails_loudly():
     with pytest.raises(gpr_amd.GprxError) as e:
         gpr_amd.Context(0)
     assert "no HIP device" in str(e.value)
+
+
+def _runtime_in_subprocess(torch_first):
+    import json
+    import subprocess
+    import sys
+    code = ("import json, sys\nsys.path.insert(0, %r)\n" % ROOT
+            + ("import torch\n" if torch_first else "")
+            + "import gpr_amd\ngpr_amd.lib()\nprint(json.dumps(gpr_amd.runtime_info()))\n")
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, check=True)
+    return json.loads(out.stdout.strip().splitlines()[-1])
+
+
+def test_runtime_binding_library_first():
+    """libgprx loaded with no PyTorch in the process (bench.py at every N, the two-process tests'
+    socket-bootstrapped ranks) binds /opt/rocm's HIP runtime, HSA runtime and RCCL, one copy each."""
+    info = _runtime_in_subprocess(False)
+    assert info["single_copy"] and not info["torch_loaded_first"], info
+    for k in ("libamdhip64", "librccl", "libhsa-runtime64"):
+        assert len(info[k]) == 1 and info[k][0].startswith("/opt/rocm"), info
+
+
+def test_runtime_binding_torch_first():
+    """With the PyTorch wheel imported first, libgprx shares the runtime and RCCL torch bundles
+    (the loader resolves libgprx's sonames to the objects torch loaded): still ONE copy each."""
+    pytest.importorskip("torch")
+    info = _runtime_in_subprocess(True)
+    assert info["single_copy"] and info["torch_loaded_first"], info
+    assert len(info["libamdhip64"]) == 1 and "/torch/lib/" in info["libamdhip64"][0], info
+
+
+_HC_SCRIPT = r"""
+import sys
+sys.path.insert(0, sys.argv[1])
+from gpr_amd.hostcoll import SocketGroup
+import ctypes
+rank, world, port = int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
+g = SocketGroup(rank, world, port=port, timeout=60)
+parts = g.allgather(bytes([rank]) * (rank + 3))
+assert parts == [bytes([r]) * (r + 3) for r in range(world)], parts
+assert g.max(rank * 1.5) == (world - 1) * 1.5 and g.min(rank) == 0
+assert g.broadcast(b"uid" if rank == 0 else None) == b"uid"
+fn = g.allgather_fn()
+send = (ctypes.c_double * 2)(rank, -rank)
+recv = (ctypes.c_double * (2 * world))()
+assert fn(None, ctypes.addressof(send), 16, ctypes.addressof(recv)) == 0
+assert list(recv) == [v for r in range(world) for v in (float(r), float(-r))]
+big = bytes(range(256)) * 40000 if rank == world - 1 else b"x"
+assert g.allgather(big)[world - 1] == bytes(range(256)) * 40000
+g.barrier()
+g.close()
+print("ok", rank)
+"""
+
+
+def test_hostcoll_socket_group(tmp_path):
+    """gpr_amd.hostcoll (bench.py's and the two-process tests' host collectives): all-gather of
+    ragged and 10 MB payloads, max/min, broadcast and the C all-gather callback over 3 processes."""
+    import socket
+    import subprocess
+    import sys
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = str(so.getsockname()[1])
+    script = tmp_path / "hc.py"
+    script.write_text(_HC_SCRIPT)
+    procs = [subprocess.Popen([sys.executable, str(script), ROOT, str(r), "3", port], stdout=subprocess.PIPE,
+                              stderr=subprocess.STDOUT, text=True) for r in range(3)]
+    outs = [p.communicate(timeout=120)[0] for p in procs]
+    assert all(p.returncode == 0 for p in procs), outs

@@ -528,12 +528,12 @@ import numpy as np
 rank, world, port, out = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4]
 sys.path.insert(0, os.environ["GPRX_ROOT"])
 os.environ["GPRX_DIST_SHARED_GPU"] = "1"
-import torch.distributed as dist
-dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
-import gpr_amd
-from gpr_amd.gprx import torch_allgather
+import gpr_amd   # (library first, no PyTorch: /opt/rocm's runtime, as bench.py)
+from gpr_amd.hostcoll import SocketGroup
 from gpr_amd.synth import make_data
-ctx = gpr_amd.Context(0, peer=(rank, world, torch_allgather()))
+dist = SocketGroup(rank, world, port=port)
+ctx = gpr_amd.Context(0, peer=(rank, world, dist.allgather_fn()))
+assert gpr_amd.runtime_info()["single_copy"] and not gpr_amd.runtime_info()["torch_loaded_first"]
 res = {}
 X, Y = make_data(1800, 5, 2)
 ks = "SumKernel(GaussianKernel(2,0.15,),PeriodicKernel(0.1,3.141592653589793,1,))"
@@ -558,7 +558,7 @@ if rank == 0:
     with open(out, "w") as f:
         json.dump(res, f)
 dist.barrier()
-dist.destroy_process_group()
+dist.close()
 """
 
 
@@ -681,12 +681,11 @@ import numpy as np
 rank, world, port, out, n, sleep_s = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4], int(sys.argv[5]), float(sys.argv[6])
 sys.path.insert(0, os.environ["GPRX_ROOT"])
 os.environ["GPRX_DIST_SHARED_GPU"] = "1"
-import torch.distributed as dist
-dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
-import gpr_amd
-from gpr_amd.gprx import torch_allgather
+import gpr_amd   # (library first, no PyTorch: /opt/rocm's runtime, as bench.py)
+from gpr_amd.hostcoll import SocketGroup
 from gpr_amd.synth import make_data, make_queries
-ctx = gpr_amd.Context(0, peer=(rank, world, torch_allgather()))
+dist = SocketGroup(rank, world, port=port)
+ctx = gpr_amd.Context(0, peer=(rank, world, dist.allgather_fn()))
 X, Y = make_data(n, 5, 1)
 Xq = make_queries(30, 5)
 ks = "SumKernel(GaussianKernel(2,0.15,),PeriodicKernel(0.1,3.141592653589793,1,))"
@@ -707,7 +706,7 @@ np.savez(f"{out}.r{rank}.npz", a1=a1, c1=c1, a2=a2, c2=c2, info=np.array(M.dist_
 M.close()
 ctx.close()
 dist.barrier()
-dist.destroy_process_group()
+dist.close()
 """
 
 
@@ -758,6 +757,8 @@ def test_virtual_ranks_pieces(g, monkeypatch):
         vctx.close()
 
 
+# (this one keeps torch.distributed, imported first: libgprx then runs on the runtime and RCCL
+# the PyTorch wheel bundles -- the other supported binding, gpr_amd.runtime_info())
 PEER_BIG_SCRIPT = r"""
 import os, sys
 import numpy as np
@@ -778,6 +779,8 @@ M.set_noise(C3["sigma"])
 info = M.fit()
 Xq = make_queries(64, C3["d"])
 cov = M.posterior_cov(Xq, Xq)
+rt = gpr_amd.runtime_info()
+assert rt["single_copy"] and rt["torch_loaded_first"], rt
 if rank == 0:
     np.savez(out, alpha=M.alpha(), cov=cov, storage=np.array(M.dist_info()["bytes_storage"]))
 M.close()
@@ -813,3 +816,94 @@ def test_peer_two_processes_n32768_fp64(tmp_path):
         M.close()
     finally:
         ctx.close()
+
+
+def test_bench_two_processes_rccl_fallback(tmp_path):
+    """bench.py's N > 1 path as the driver launches it (torch.distributed.run, one process per
+    rank), rehearsed on one GPU (GPRX_DIST_SHARED_GPU) with the RCCL initialisation failed on
+    purpose (GPRX_RCCL_FAIL): every rank falls back to the peer context over the socket group,
+    the sharded fit runs, the failure is reported in dist_error, and the processes map one HIP
+    runtime (/opt/rocm's; no PyTorch in a bench rank)."""
+    import json
+    import os
+    import socket
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = str(so.getsockname()[1])
+    env = dict(os.environ, GPRX_DIST_SHARED_GPU="1", GPRX_RCCL_FAIL="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", port, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "2",
+           "--warmup", "1", "--n", "2048", "--configs", "0", "--lml", "0", "--build-iters", "0", "--cpu-n", "0",
+           "--predict-q", "256", "--variance-q", "0", "--cpu-lml-ns", "", "--cpu-predict-q", "0"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=root)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["value"] > 0
+    assert line["dist_transport"].startswith("peer (fallback"), line["dist_transport"]
+    assert "GPRX_RCCL_FAIL" in line["dist_error"]
+    assert line["config"]["parallelism"].startswith("sharded")
+    rt = line["runtime"]
+    assert rt["single_copy"] and not rt["torch_loaded_first"], rt
+
+
+PEER_SLICE_SCRIPT = r"""
+import os, sys
+import numpy as np
+rank, world, port, out = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4]
+sys.path.insert(0, os.environ["GPRX_ROOT"])
+os.environ["GPRX_DIST_SHARED_GPU"] = "1"
+import gpr_amd
+from gpr_amd.hostcoll import SocketGroup
+from gpr_amd.synth import make_data, make_queries
+grp = SocketGroup(rank, world, port=port)
+ctx = gpr_amd.Context(0, peer=(rank, world, grp.allgather_fn()))
+X, Y = make_data(1500, 5, 1)
+Xq = make_queries(37, 5)
+ks = "SumKernel(GaussianKernel(2,0.15,),PeriodicKernel(0.1,3.141592653589793,1,))"
+M = gpr_amd.Model(ctx, np.float64)
+M.set_data(X, Y)
+M.set_kernel(ks)
+M.set_noise(0.5)
+M.fit()
+lo, hi = gpr_amd.query_shard(37, rank, world)
+v_own = M.posterior_cov(Xq[lo:hi], Xq[lo:hi])           # variances, each process its own slice
+c_own = M.posterior_cov(Xq[lo:hi], Xq[::-1][lo:hi].copy())  # pairs x != y, own slices
+e = Xq[:0]
+v_one = M.posterior_cov(Xq[:9], Xq[:9]) if rank == 0 else M.posterior_cov(e, e)  # rank 1: no pairs
+v_all = M.posterior_cov(Xq, Xq)                          # identical arguments everywhere
+np.savez(f"{out}.r{rank}.npz", v_own=v_own, c_own=c_own, v_one=v_one, v_all=v_all, lo=lo, hi=hi,
+         pv=np.array(M.dist_info()["posterior_bytes_rank"]))
+M.close()
+ctx.close()
+grp.barrier()
+grp.close()
+"""
+
+
+def test_peer_posterior_differing_slices(tmp_path):
+    """posterior_cov on a sharded fit is a collective: two processes passing their OWN query_shard
+    slices (different q, different queries; one process with none) get their own variances and
+    covariances -- the arguments are agreed first and differing ones solved together -- instead
+    of a hang or another process's values (round-4 advisor finding).  Against the oracle; the
+    posterior workspace per rank is K(Z, X_own): the queries x that rank's rows only."""
+    n = 1500
+    out = tmp_path / "res"
+    _run_peers(tmp_path, PEER_SLICE_SCRIPT, [out], timeout=240)
+    X, Y = make_data(n, 5, 1)
+    Xq = make_queries(37, 5)
+    _, C_ref = O.fit(C3K, X, Y, 0.5)
+    for r in range(2):
+        res = np.load(f"{out}.r{r}.npz")
+        lo, hi = int(res["lo"]), int(res["hi"])
+        assert relerr(res["v_own"], O.posterior_cov(C3K, X, C_ref, Xq[lo:hi], Xq[lo:hi])) <= 1e-6
+        assert relerr(res["c_own"], O.posterior_cov(C3K, X, C_ref, Xq[lo:hi], Xq[::-1][lo:hi].copy())) <= 1e-6
+        assert relerr(res["v_all"], O.posterior_cov(C3K, X, C_ref, Xq, Xq)) <= 1e-6
+        if r == 0:
+            assert relerr(res["v_one"], O.posterior_cov(C3K, X, C_ref, Xq[:9], Xq[:9])) <= 1e-6
+        else:
+            assert res["v_one"].size == 0
+        # (K(Z, X_own): at most the padded chunks x this rank's ~half of the 12 row blocks, not all N)
+        assert 0 < int(res["pv"]) <= 8 * 128 * 2 * 7 * 128

@@ -240,3 +240,81 @@ def test_parameter_order_roundtrip():
     v0, g0 = O.kernel_eval(ks, X0, Y0)
     v1, g1 = O.kernel_eval_params(ks, np.array([[1.5, 0.7, 0.3, 2.2, 0.9]]), X0, Y0)
     assert v0 == v1[0] and np.array_equal(g0, g1[0])
+
+
+# ---- tests/SparseInferenceTest.cpp (disabled in the reference's main, :486-489, fully written) ----
+# The reference draws its label noise from boost::minstd_rand seeded with time(0); here a
+# fixed-seed normal stream of the same standard deviation stands in (the checks do not depend
+# on the draw).
+
+
+def _sparse_f(x):
+    """the tests' ground truth, tests/SparseInferenceTest.cpp:40"""
+    return (0.5 * np.sin(x + 10 * x) + np.sin(4 * x)) * x * x
+
+
+def _sparse_grid(count, start=-2.0, stop=5.0):
+    return np.array([start + i * (stop - start) / count for i in range(count)])[:, None]
+
+
+def test_sparse_efficient_inversion_and_determinant():
+    """SparseInferenceTest Test1 (:37-133): n = 1000 dense and m = 25 inducing points on [-2, 5),
+    GaussianKernel(0.23, 10), noise 0.1, jitter 0.5.  The Woodbury inverse C_inv
+    (EfficientInversion, include/SparseLikelihood.h:129-135) against the direct inverse of
+    sigma^2 I + Knm Kmm^{-1} Knm^T: ||D - T||_F < 1e-7; the efficient determinant
+    (:138-145) against the direct one: |diff| < 1e-10."""
+    ks, noise, jitter = "GaussianKernel(0.23,10,)", 0.1, 0.5
+    Xn, Xm = _sparse_grid(1000), _sparse_grid(25)
+    K, Kinv, Knm, D, det = O.sparse_core(ks, Xn, Xm, noise, jitter)
+    A = noise ** 2 * np.eye(1000) + Knm @ Kinv @ Knm.T
+    T = np.linalg.inv(A)
+    assert np.linalg.norm(D - T) < 1e-7
+    sign, logdet = np.linalg.slogdet(A)
+    assert abs(det - sign * np.exp(logdet)) < 1e-10
+    # (the determinant underflows double at this size, as in the reference; its logarithm,
+    # which the device sparse likelihood reports, is pinned too)
+    _, _, _, ld = O.sparse_lml(ks, Xn, _sparse_f(Xn[:, 0]), Xm, noise, jitter, with_grad=False)
+    assert abs(ld - logdet) <= 1e-9 * abs(logdet)
+
+
+@pytest.mark.parametrize("jitter", [0.0, 0.001])
+def test_sparse_core_matrix_and_trace(jitter):
+    """SparseInferenceTest Test2 (:135-224), jitter 0 and 0.001 as its main (:487-488): with the
+    inducing points equal to the 10 dense points, the core matrix C = Knm Kmm^{-1} Kmn
+    (include/SparseGaussianProcess.h:375-377) reproduces the dense kernel matrix:
+    ||C - K||_F < 1e-2 (jitter > 0) or < 2000 (jitter 0); the kernel-matrix trace
+    (lib/GaussianProcess.cpp:419-428) equals the dense matrix's exactly."""
+    ks, noise = "GaussianKernel(0.23,10,)", 0.01
+    X = _sparse_grid(10)
+    K, Kinv, Knm, _, _ = O.sparse_core(ks, X, X, noise, jitter)
+    C = Knm @ Kinv @ Knm.T
+    Kd = O.kernel_matrix(ks, X)
+    err = np.linalg.norm(C - Kd)
+    assert err < (1e-2 if jitter > 0 else 2000)
+    trace = 0.0
+    for i in range(10):  # ComputeKernelMatrixTraceInternal: k(x_i, x_i) summed in order
+        trace += O.kernel_eval(ks, X[i], X[i], with_grad=False)
+    assert np.trace(Kd) == trace
+
+
+def test_sparse_likelihood_gradient_central_differences():
+    """SparseInferenceTest Test3 (:226-336): for iter = 0..9, n = 50 + iter dense and m = 5 + iter
+    inducing points, GaussianKernel(0.1 + 0.02 iter, 10), noise 0.2, jitter 0.01: the analytic
+    gradient of the sparse log likelihood against central differences with h = 1e-4, within 1
+    (sigma) and 0.1 (scale)."""
+    rng = np.random.default_rng(0x53504733)
+    noise, jitter, h = 0.2, 0.01, 1e-4
+    for it in range(10):
+        sigma, scale = 0.1 + it * 0.02, 10.0
+        n, m = 50 + it, 5 + it
+        Xn, Xm = _sparse_grid(n), _sparse_grid(m)
+        Y = _sparse_f(Xn[:, 0]) + rng.normal(0, noise, n)
+        _ = rng.normal(0, noise, m)  # (the inducing labels the reference draws and never uses)
+        _, g, _, _ = O.sparse_lml(f"GaussianKernel({sigma!r},{scale!r},)", Xn, Y, Xm, noise, jitter)
+
+        def val(sg, sc):
+            return O.sparse_lml(f"GaussianKernel({sg!r},{sc!r},)", Xn, Y, Xm, noise, jitter, with_grad=False)[0]
+        d_sigma = (val(sigma + h / 2, scale) - val(sigma - h / 2, scale)) / h
+        d_scale = (val(sigma, scale + h / 2) - val(sigma, scale - h / 2)) / h
+        assert abs(g[0] - d_sigma) <= 1, (it, g[0], d_sigma)
+        assert abs(g[1] - d_scale) <= 0.1, (it, g[1], d_scale)
