@@ -20,6 +20,12 @@ CPPTESTS  := $(LIBDIR)/gp_host_test $(LIBDIR)/host_cpu_test
 
 all: $(LIBDIR)/libgprx.so $(LIBDIR)/libgpr_amd.so cpptests oracle
 
+# The VALU fallback build and gradient (k_build.hip, k_lml.hip) ask for a full unroll of their
+# 4 x 4 store / reduce loops around the inlined kernel-tree evaluation; its size exceeds LLVM's
+# default pragma budget (the request was silently dropped: -Wpass-failed), so it is raised for
+# these two files (fewer VGPRs, no scratch: the loop indices stay compile-time register indices).
+$(BUILD)/k_build.o $(BUILD)/k_lml.o: HIPFLAGS += -mllvm -pragma-unroll-threshold=200000
+
 $(BUILD)/%.o: gpr_amd/csrc/%.hip $(HDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 

@@ -472,7 +472,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--n", type=int, default=None)
+    ap.add_argument("--n", "--ntrain", dest="n", type=int, default=None,
+                    help="training points (--ntrain under torch.distributed.run, whose parser takes --n)")
     ap.add_argument("--d", type=int, default=None)
     ap.add_argument("--predict-q", type=int, default=65536)
     ap.add_argument("--variance-q", type=int, default=None,
@@ -692,7 +693,7 @@ def main():
         t_roof_lml = (fit_roofline_ms(n, d, m) + 1e3 * (2.0 * n ** 3 / 3.0) / (PEAK_FP64_TFLOPS * 1e12)
                       + 1e3 * 8.0 * n * (n + 1) / 2 / (PEAK_HBM_GBS * 1e9))
         lml_flops = float(n) ** 3
-        dev_ms = sum(v["ms"] for k, v in ls.items() if k in ("potrf_tiles", "other_gemm", "lml_grad", "backsolve"))
+        dev_ms = sum(v["ms"] for k, v in ls.items() if k in ("potrf_tiles", "spd_inverse", "other_gemm", "lml_grad", "backsolve"))
         lml = {"ms_wall": 1e3 * tl, "phases_ms": {k: v["ms"] for k, v in ls.items()},
                "device_ms": dev_ms or None,
                "roofline": {"bound": "mfma", "t_roof_ms": t_roof_lml, "t_ms": 1e3 * tl, "time": "wall",

@@ -836,7 +836,7 @@ def test_bench_two_processes_rccl_fallback(tmp_path):
     env = dict(os.environ, GPRX_DIST_SHARED_GPU="1", GPRX_RCCL_FAIL="1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
            "127.0.0.1", "--master-port", port, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "2",
-           "--warmup", "1", "--n", "2048", "--configs", "0", "--lml", "0", "--build-iters", "0", "--cpu-n", "0",
+           "--warmup", "1", "--ntrain", "2048", "--configs", "0", "--lml", "0", "--build-iters", "0", "--cpu-n", "0",
            "--predict-q", "256", "--variance-q", "0", "--cpu-lml-ns", "", "--cpu-predict-q", "0"]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=root)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
