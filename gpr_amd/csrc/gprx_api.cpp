@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <limits>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <type_traits>
@@ -263,6 +264,7 @@ struct gprx_ctx {
     Exec ex;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     Prof prof;
+    std::shared_ptr<void> sparse_state[2];  // the sparse fit's device buffers per scalar type (sparse_state)
     std::string err;
     std::mutex mu;
 };
@@ -979,10 +981,25 @@ static void upload(DevBuf& b, const void* host, size_t bytes, hipStream_t s) {
     if (bytes) GPRX_HIP(hipMemcpy(b.p, host, bytes, hipMemcpyDefault));
 }
 
+// (the destination may be device memory too -- unified addressing decides the direction -- so
+// a caller that keeps results in HBM gets them without a PCIe round trip)
 static void download(void* host, const void* dev, size_t bytes, hipStream_t s) {
     GPRX_HIP(hipStreamSynchronize(s));
     GPRX_HIP(hipGetLastError());
-    if (bytes) GPRX_HIP(hipMemcpy(host, dev, bytes, hipMemcpyDeviceToHost));
+    if (bytes) GPRX_HIP(hipMemcpy(host, dev, bytes, hipMemcpyDefault));
+}
+
+// An input the caller may pass as host or as device memory: device memory of this context's GPU
+// is used where it is (no copy), anything else is copied into `b`.
+template <typename T>
+static const T* dev_input(DevBuf& b, const void* p, size_t bytes, int device, hipStream_t s) {
+    hipPointerAttribute_t at;
+    std::memset(&at, 0, sizeof(at));
+    if (p && hipPointerGetAttributes(&at, p) == hipSuccess && at.type == hipMemoryTypeDevice && at.device == device)
+        return static_cast<const T*>(p);
+    (void)hipGetLastError();  // (an unregistered host pointer reports an error: not sticky)
+    upload<T>(b, p, bytes, s);
+    return b.as<T>();
 }
 
 template <typename T>
@@ -1726,7 +1743,7 @@ static void download_sym(void* out, const DevBuf& C, int64_t ldc, int64_t n, hip
     // row- or column-major, so it lands in the caller's buffer as is
     launch_sym_fill<T>(C.as<T>(), ldc, n, s);
     GPRX_HIP(hipGetLastError());
-    GPRX_HIP(hipMemcpy2DAsync(out, sizeof(T) * n, C.p, sizeof(T) * ldc, sizeof(T) * n, n, hipMemcpyDeviceToHost, s));
+    GPRX_HIP(hipMemcpy2DAsync(out, sizeof(T) * n, C.p, sizeof(T) * ldc, sizeof(T) * n, n, hipMemcpyDefault, s));
     GPRX_HIP(hipStreamSynchronize(s));
 }
 
@@ -1738,7 +1755,20 @@ struct SparseNE {
     bool mma = false;
     T is2 = 0;
     DevBuf dXm, dtm, dX, dtx, dY, dS, dA, dK, dLinv, dLinvK, dinfo, dflag, dz, dalpha, dV, dC, dFU, dFV, dKd;
+    const T* pX = nullptr;  // the dense rows and labels in HBM: the caller's device memory, or dX / dY
+    const T* pY = nullptr;
 };
+
+// The sparse fit's device state lives in the context between calls (its buffers -- the
+// partial normal equations, the streamed Kmn blocks, the M x M factors: hundreds of MB at C5 --
+// are allocated once per shape, not per call).  One per scalar type; calls on a context are
+// serialised by its mutex.
+template <typename T>
+static SparseNE<T>& sparse_state(gprx_ctx* ctx) {
+    std::shared_ptr<void>& h = ctx->sparse_state[sizeof(T) == 8 ? 1 : 0];
+    if (!h) h = std::make_shared<SparseNE<T>>();
+    return *static_cast<SparseNE<T>*>(h.get());
+}
 
 // SparseGaussianProcess::PreComputeRegression (include/SparseGaussianProcess.h:274-313) up to
 // the factorisation: S = Kmm + jitter I + sigma^-2 Kmn Knm with b = sigma^-2 Kmn Y riding
@@ -1767,8 +1797,8 @@ static void sparse_normal_eq(gprx_ctx* ctx, SparseNE<T>& st, const gprx_kernel_d
            &dKd = st.dKd;
     st.chunk = chunk;
     upload<T>(dXm, Xmh, sizeof(T) * M * d, s);
-    upload<T>(dX, Xh, sizeof(T) * std::max<int64_t>(n, 1) * d, s);
-    upload<T>(dY, Yh, sizeof(T) * std::max<int64_t>(n, 1) * m, s);
+    st.pX = dev_input<T>(dX, Xh, sizeof(T) * std::max<int64_t>(n, 1) * d, ctx->device, s);
+    st.pY = dev_input<T>(dY, Yh, sizeof(T) * std::max<int64_t>(n, 1) * m, ctx->device, s);
     // Kmn blocks as MFMA pair statistics (k_pairs.hip) when the tree allows it: features of
     // the inducing points once, of each dense chunk per chunk, both centred on Xm's first row
     const bool mma = pairs_mma_supported<T>(K, 1);
@@ -1828,23 +1858,23 @@ static void sparse_normal_eq(gprx_ctx* ctx, SparseNE<T>& st, const gprx_kernel_d
         if (nc < chunk || off == 0) GPRX_HIP(hipMemsetAsync(dA.p, 0, sizeof(T) * ld * acols, s));
         if (mma) {
             const int64_t nc128 = round_up(nc, GT);
-            launch_pair_features<T>(K, dX.as<T>() + off * d, nc, d, dXm.as<T>(), true, dFV.as<T>(), nc128, s,
+            launch_pair_features<T>(K, st.pX + off * d, nc, d, dXm.as<T>(), true, dFV.as<T>(), nc128, s,
                                     dflag.as<int>());
             launch_kcross_mma<T>(K, dKd.as<KCanon<T>>(), dFU.as<T>(), Mp, M, dFV.as<T>(), nc128, nc, d, dA.as<T>(), ld,
-                                 dflag.as<int>(), s, fused ? dY.as<T>() + off : nullptr,
+                                 dflag.as<int>(), s, fused ? st.pY + off : nullptr,
                                  fused ? dKY.as<T>() : nullptr);
             if (fused)  // label row Mp of partial 0, in chunk order
                 launch_ky_reduce<T>(dKY.as<T>(), Mp, (int)(nc128 / GT), M, is2, dS.as<T>(), ld, Mp, s);
         } else {
             const T* tabc = nullptr;
             if (K.nper > 0) {
-                launch_sincos_tables<T>(K, dX.as<T>() + off * d, nc, d, dtx.as<T>(), s);
+                launch_sincos_tables<T>(K, st.pX + off * d, nc, d, dtx.as<T>(), s);
                 tabc = dtx.as<T>();
             }
-            launch_kbuild<T>(K, dXm.as<T>(), dtm.as<T>(), M, dX.as<T>() + off * d, tabc, nc, d, dA.as<T>(), ld, 0,
+            launch_kbuild<T>(K, dXm.as<T>(), dtm.as<T>(), M, st.pX + off * d, tabc, nc, d, dA.as<T>(), ld, 0,
                              false, T(0), dflag.as<int>(), s);
         }
-        if (!fused) launch_label_rows<T>(dY.as<T>() + off * m, nc, m, dA.as<T>(), ld, Mp, ncp, mp, s);
+        if (!fused) launch_label_rows<T>(st.pY + off * m, nc, m, dA.as<T>(), ld, Mp, ncp, mp, s);
         const int64_t kpart = round_up((ncp + P - 1) / P, 16);  // zero-padded columns make up the rest
         const int Pc = (int)((ncp + kpart - 1) / kpart);
         launch_syrk_splitk<T>(dS.as<T>(), ld, sstride, dA.as<T>(), ld, fused ? Mp : ld, Mp, kpart, Pc, is2, s);
@@ -1899,7 +1929,7 @@ template <typename T>
 static gprx_status sparse_fit_impl(gprx_ctx* ctx, const gprx_kernel_desc* desc, const void* Xh, const void* Yh,
                                    int64_t n, int d, int m, const void* Xmh, int64_t M, double sigma, double jitter,
                                    void* Kinv, void* RV, void* RM) {
-    SparseNE<T> st;
+    SparseNE<T>& st = sparse_state<T>(ctx);
     sparse_normal_eq<T>(ctx, st, desc, Xh, Yh, n, d, m, Xmh, M, sigma, jitter);
     hipStream_t s = ctx->stream;
     const int64_t Mp = st.Mp, ld = st.ld;
@@ -1950,7 +1980,7 @@ static gprx_status sparse_lml_impl(gprx_ctx* ctx, const gprx_kernel_desc* desc, 
                  "SparseGaussianLogLikelihood: only one output dimension is supported (the reference's data-fit term "
                  "is m x m, include/SparseLikelihood.h:303)");
     GPRX_REQUIRE(n > 0, GPRX_ERR_DIM, "SparseGaussianProcess::ComputeCoreMatrices: empty sample set.");
-    SparseNE<T> st;
+    SparseNE<T>& st = sparse_state<T>(ctx);
     sparse_normal_eq<T>(ctx, st, desc, Xh, Yh, n, d, m, Xmh, M, sigma, jitter);
     sparse_factor_kmm<T>(ctx, st);
     hipStream_t s = ctx->stream;
@@ -1965,7 +1995,7 @@ static gprx_status sparse_lml_impl(gprx_ctx* ctx, const gprx_kernel_desc* desc, 
     GPRX_HIP(hipMemcpyAsync(dred, dred + 8, 2 * sizeof(double), hipMemcpyDeviceToDevice, s));
     launch_fit_reductions<T>(st.dK.template as<T>(), Mp, M, Mp, 0, dred + 8, s);
     GPRX_HIP(hipMemcpyAsync(dred + 2, dred + 8, sizeof(double), hipMemcpyDeviceToDevice, s));
-    launch_sq_sum<T>(st.dY.template as<T>(), n, dred + 4, s);
+    launch_sq_sum<T>(st.pY, n, dred + 4, s);
     double h[5];
     download(h, dred, sizeof(h), s);
     double yty = h[4], nn = (double)n;
@@ -2009,7 +2039,7 @@ static gprx_status sparse_lml_impl(gprx_ctx* ctx, const gprx_kernel_desc* desc, 
         }
         for (int64_t off = 0; off < n; off += chunk) {
             const int64_t nc = std::min(chunk, n - off), nc128 = round_up(nc, GT);
-            const T* Xc = st.dX.template as<T>() + off * d;
+            const T* Xc = st.pX + off * d;
             if (nc < chunk || off == 0) GPRX_HIP(hipMemsetAsync(dAt.p, 0, sizeof(T) * c128 * Mp, s));
             const T* tabc = nullptr;
             if (st.mma) {
@@ -2025,7 +2055,7 @@ static gprx_status sparse_lml_impl(gprx_ctx* ctx, const gprx_kernel_desc* desc, 
                 launch_kbuild<T>(K, Xc, tabc, nc, st.dXm.template as<T>(), st.dtm.template as<T>(), M, d, dAt.as<T>(), c128, 0, false,
                                  T(0), st.dflag.template as<int>(), s);
             }
-            launch_sparse_resid<T>(dAt.as<T>(), c128, nc, M, u, st.dY.template as<T>() + off, is2, dr.as<T>(), s);
+            launch_sparse_resid<T>(dAt.as<T>(), c128, nc, M, u, st.pY + off, is2, dr.as<T>(), s);
             launch_gemm_nt<T>(dG.as<T>(), c128, dAt.as<T>(), c128, dSig.as<T>(), Mp, nc128, Mp, Mp, is2, T(0), false,
                               s);
             if (gmma) {

@@ -288,10 +288,16 @@ class DeviceArray:
     (A framework's CUDA tensors cannot serve once this library owns the device when the framework
     bundles its own HIP runtime, as the PyTorch wheel does.)"""
 
-    def __init__(self, ctx, a=None, *, _base=None, _shape=None):
+    def __init__(self, ctx, a=None, *, _base=None, _shape=None, _empty=None):
         if _base is not None:  # a reshaped view of _base's buffer
             self.ctx, self.p, self.dtype, self._base = _base.ctx, _base.p, _base.dtype, _base
             self.shape = tuple(_shape)
+            return
+        if _empty is not None:  # (shape, dtype): allocated, not initialised
+            self.ctx, self.shape, self.dtype, self._base = ctx, tuple(_empty[0]), np.dtype(_empty[1]), None
+            p = ctypes.c_void_p()
+            ctx._c(lib().gprx_device_alloc(ctx.h, self.nbytes, ctypes.byref(p)))
+            self.p = p.value
             return
         a = np.ascontiguousarray(a)
         self.ctx, self.dtype, self.shape, self._base = ctx, a.dtype, a.shape, None
@@ -300,6 +306,11 @@ class DeviceArray:
         self.p = p.value
         ctx._c(lib().gprx_device_upload(ctx.h, ctypes.c_void_p(self.p), a.ctypes.data_as(ctypes.c_void_p),
                                         a.nbytes))
+
+    @classmethod
+    def empty(cls, ctx, shape, dtype=np.float64):
+        """Uninitialised device memory of the given shape (a destination, e.g. sparse_fit's out)."""
+        return cls(ctx, _empty=(shape, dtype))
 
     @property
     def ndim(self):
@@ -456,8 +467,10 @@ class Context:
         self._c(lib().gprx_spd_inverse(self.h, _dt(A.dtype), _ptr(A), A.shape[0], ctypes.byref(info)))
         return A
 
-    def sparse_fit(self, kernel, X, Y, Xm, sigma, jitter, dtype=np.float64):
-        """SparseGaussianProcess::Initialize; X, Y may be device tensors (no PCIe copy)."""
+    def sparse_fit(self, kernel, X, Y, Xm, sigma, jitter, dtype=np.float64, out=None):
+        """SparseGaussianProcess::Initialize; X, Y may be device arrays (read in HBM, no copy).
+        out = (Kinv, RV, RM): caller-owned destinations, host arrays or DeviceArrays (results
+        kept in HBM, no PCIe copy); by default new host arrays."""
         X = _input(X, dtype)
         Y = _input(Y, dtype)
         if Y.ndim == 1:
@@ -466,9 +479,13 @@ class Context:
         n, d = X.shape
         m = Y.shape[1]
         M = Xm.shape[0]
-        Kinv = np.empty((M, M), dtype)
-        RV = np.empty((M, m), dtype)
-        RM = np.empty((M, M), dtype)
+        if out is None:
+            Kinv, RV, RM = np.empty((M, M), dtype), np.empty((M, m), dtype), np.empty((M, M), dtype)
+        else:
+            Kinv, RV, RM = out
+            for a, shp in ((Kinv, (M, M)), (RV, (M, m)), (RM, (M, M))):
+                if a is not None and (tuple(a.shape) != shp or np.dtype(a.dtype) != np.dtype(dtype)):
+                    raise ValueError(f"sparse_fit: output of shape {tuple(a.shape)} / {a.dtype}, need {shp} / {np.dtype(dtype)}")
         self._c(lib().gprx_sparse_fit(self.h, _dt(dtype), ctypes.byref(kernel_desc(kernel)), _ptr(X), _ptr(Y), n, d,
                                       m, _ptr(Xm), M, sigma, jitter, _ptr(Kinv), _ptr(RV), _ptr(RM)))
         return Kinv, RV, RM

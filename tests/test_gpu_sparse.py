@@ -173,6 +173,25 @@ def test_sparse_fit_device_array_inputs(ctx):
     assert Yv.reshape(-1, 1).data_ptr() == Yv.data_ptr()
     with pytest.raises(TypeError):
         ctx.sparse_fit(ks, Xd, ctx.device_array(Y.astype(np.float32)), Xm, 0.3, 1e-4)
+    # results kept in HBM (DeviceArray destinations: no PCIe copy), the same bits; repeated calls
+    # reuse the context's sparse state (and a different shape in between re-sizes it)
+    import gpr_amd
+    outs = tuple(gpr_amd.DeviceArray.empty(ctx, shp) for shp in ((64, 64), (64, 1), (64, 64)))
+    X2, Y2, Xm2 = _inputs(1500, 4, 200, 1, np.float64)
+    fctx = gpr_amd.Context(0)  # (a fresh context: the reference bits for the other shape)
+    try:
+        fresh = fctx.sparse_fit(ks, X2, Y2, Xm2, 0.3, 1e-2)
+    finally:
+        fctx.close()
+    for _ in range(2):
+        ctx.sparse_fit(ks, Xd, Yd, Xm, 0.3, 1e-4, out=outs)
+        for a, b in zip(host, outs):
+            assert np.array_equal(a, b.numpy())
+        other = ctx.sparse_fit(ks, X2, Y2, Xm2, 0.3, 1e-2)
+        for a, b in zip(fresh, other):
+            assert np.array_equal(a, b)
+    with pytest.raises(ValueError):
+        ctx.sparse_fit(ks, Xd, Yd, Xm, 0.3, 1e-4, out=(outs[1], outs[1], outs[2]))
 
 
 def test_sparse_fit_device_resident_inputs(ctx):
