@@ -681,7 +681,10 @@ def main():
                "roofline": {"bound": "mfma", "achieved": fl / tv / 1e12 / world,
                             "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
                             "frac": fl / tv / 1e12 / world / PEAK_FP64_TFLOPS,
-                            "algorithmic_flops": fl, "time": "wall"}}
+                            "algorithmic_flops": fl, "time": "wall"},
+               # the leg's kernels (K(x, X), the recursive forward solve's GEMMs, the row dots) in
+               # the committed rocprofv3 summary of this leg
+               "rocprof": rocprof_table("variance") if world == 1 else None}
 
     # log-marginal likelihood + gradient (refit, explicit inverse, fused gradient pass)
     lml = None

@@ -1043,13 +1043,31 @@ static gprx_status model_predict(gprx_model* M, const void* Xq, int64_t q, void*
     return GPRX_OK;
 }
 
+// R = K(Xq, X) (qp x np, ld qp, zero padding), then R L^{-T} in place.  K(Xq, X) as MFMA pair
+// statistics (kcross_mma_kernel: the predict path's features of the queries and of the training
+// set) when the tree allows it -- 23 ms -> ~4 ms of the 300 ms variance leg at Q = 65536 against
+// the VALU kernel (GPRX_PREDICT=direct keeps that one)
 template <typename T>
 static void solve_rows_for(gprx_model* M, const T* dXq, const T* dtabQ, int64_t q, int64_t qp, T* R) {
     hipStream_t s = M->ctx->stream;
     const KCanon<T>& K = kcanon<T>(M);
     GPRX_HIP(hipMemsetAsync(R, 0, sizeof(T) * qp * M->np, s));
-    launch_kbuild<T>(K, dXq, dtabQ, q, M->X.as<T>(), M->tab.as<T>(), M->n, M->d, R, qp, 0, false, T(0),
-                     M->flag.as<int>(), s);
+    static const bool direct = std::getenv("GPRX_PREDICT") && std::string(std::getenv("GPRX_PREDICT")) == "direct";
+    const int64_t npf = round_up(M->n, GT);
+    if (!direct && pairs_mma_supported<T>(K, 1) && npf <= M->np) {
+        const int d = M->d;
+        const int64_t kf = pairs_feature_cols<T>(K, d);
+        DevBuf fq;
+        fq.ensure(sizeof(T) * qp * kf);
+        M->featV.ensure(sizeof(T) * npf * kf);
+        launch_pair_features<T>(K, M->X.as<T>(), M->n, d, M->X.as<T>(), true, M->featV.as<T>(), npf, s);
+        launch_pair_features<T>(K, dXq, q, d, M->X.as<T>(), false, fq.as<T>(), qp, s);
+        const KCanon<T>* kdev = M->kfit.put(K, s);
+        launch_kcross_mma<T>(K, kdev, fq.as<T>(), qp, q, M->featV.as<T>(), npf, M->n, d, R, qp, M->flag.as<int>(), s);
+    } else {
+        launch_kbuild<T>(K, dXq, dtabQ, q, M->X.as<T>(), M->tab.as<T>(), M->n, M->d, R, qp, 0, false, T(0),
+                         M->flag.as<int>(), s);
+    }
     trsm_rows<T>(M->A.as<T>(), M->ld, M->np, M->Linv.as<T>(), R, qp, qp, s);
 }
 

@@ -70,7 +70,7 @@ for step in "$@"; do
         python scripts/bench_brief.py "$O/bench.json"
         ;;
     profile)
-        for leg in c3 predict lml build c2 c4 c5; do prof_leg $leg; done
+        for leg in c3 predict variance lml build c2 c4 c5; do prof_leg $leg; done
         pmc_leg c3 pmcf_c3 FETCH_SIZE
         pmc_leg c3 pmcw_c3 WRITE_SIZE
         pmc_leg build pmcf_build FETCH_SIZE
