@@ -136,7 +136,10 @@ struct Stage {
     // lanes with lk = 0 and lk = 1 read k-columns kr and kr + 1 of one pair, 128 words apart --
     // the same banks, a 2-way conflict on every f32 fragment read; rotated, the two halves of the
     // group land 16 banks apart
-    static constexpr int ROT = CPI == 2 ? 16 : 0;
+    // (the factorisation's 32-deep f32 stages keep the pair adjacent instead: tile_mma reads
+    // both columns with ONE ds_read2_b32 -- PAIRED below -- and the pair's two k-columns are
+    // then read by the same lane, in different MFMA steps)
+    static constexpr int ROT = (CPI == 2 && BK != 32) ? 16 : 0;
     // row of the operand column that lane `lane`'s 16-B load brings (its LDS position is fixed)
     __device__ static inline int src_row(int lane) {
         const int lcol = lane / LPC, lrow = (lane % LPC) * E;
@@ -371,6 +374,47 @@ __device__ __forceinline__ void tile_mma(typename Mfma<T>::acc_t (&acc)[2][4], c
 #pragma unroll
                     for (int y = 0; y < 4; y++) fa[r][y] = a[S::at(kr, wr * 64 + y * 16 + lr)];
                 };
+                constexpr bool PAIRED = sizeof(T) == 4 && BK == 32 && S::CPI == 2 && S::ROT == 0;
+                if constexpr (PAIRED) {
+                    // f32, 32-deep stages: k-step 2 j + h takes the k-columns 2 (4 j + lk) + h, so a
+                    // lane's two operands of steps 2j, 2j + 1 are the two columns of ONE DMA pair
+                    // (GT floats apart in LDS): one ds_read2_b32 per operand fragment for two MFMA
+                    // steps -- half the fragment-read instructions of the 4-consecutive-column
+                    // order (the stage's 32 columns are summed in another order)
+                    T pa[2][2][4], pb[2][2][2];  // [buffer][h][.]
+                    auto frag2 = [&](int j, int r) {
+                        const int slot = 4 * j + lk;
+                        const T* ac = a + slot * S::SRP;
+                        const T* bc = b + slot * S::SRP;
+#pragma unroll
+                        for (int x = 0; x < 2; x++) {
+                            const int row = wc * 32 + x * 16 + lr;
+                            pb[r][0][x] = bc[row];
+                            pb[r][1][x] = bc[GT + row];
+                        }
+#pragma unroll
+                        for (int y = 0; y < 4; y++) {
+                            const int row = wr * 64 + y * 16 + lr;
+                            pa[r][0][y] = ac[row];
+                            pa[r][1][y] = ac[GT + row];
+                        }
+                    };
+                    frag2(0, 0);
+#pragma unroll
+                    for (int j = 0; j < BK / 8; j++) {
+                        if (j + 1 < BK / 8) frag2(j + 1, (j + 1) & 1);
+                        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                        for (int h = 0; h < 2; h++)
+#pragma unroll
+                            for (int x = 0; x < 2; x++)
+#pragma unroll
+                                for (int y = 0; y < 4; y++)
+                                    if (MAP != 2 || 4 * wr + y >= 2 * wc + x)
+                                        acc[x][y] = Tr::mma(pb[j & 1][h][x], pa[j & 1][h][y], acc[x][y]);
+                    }
+                    continue;
+                }
                 frag(0, 0);
                 if constexpr (MID < 0) {
 #pragma unroll
