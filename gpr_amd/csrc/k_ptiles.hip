@@ -912,6 +912,19 @@ __device__ __forceinline__ void la_store_linv_rows(T* __restrict__ Linv, const T
     }
 }
 
+// row block q of Linv, columns 32 q .. 127 (Dinv_q and the zeros right of it); its columns < 32 q
+// go out from the registers of the units that finish them (la_linv_unit gout), so the whole
+// row block is stored during the next F phase, not in the factor's tail
+template <typename T>
+__device__ __forceinline__ void la_store_linv_diag(T* __restrict__ Linv, const T* __restrict__ sS,
+                                                   const T* __restrict__ sDi, int q, int tid, int nth) {
+    const int nc = DB - 32 * q;
+    for (int e = tid; e < 32 * nc; e += nth) {
+        const int r = 32 * q + (e & 31), c = 32 * q + (e >> 5);
+        st_sc1(Linv + r + c * DB, linv_at(sS, sDi, r, c));
+    }
+}
+
 // Dinv_q = L_qq^{-1} (the 32 x 32 diagonal block q of Linv, lower, zeros above) into Linv: the
 // progressive TPART(k + 1, .) read it as soon as DIAGX(k)'s panel counter says so (the full row
 // block q of Linv follows later with the same values)
@@ -924,25 +937,27 @@ __device__ __forceinline__ void la_store_dinv(T* __restrict__ Linv, const T* __r
     }
 }
 
-// F(p)'s side phase, waves wlo..7: the stores of what panel p-1 finished (L panel p-1, with pan
-// also Dinv_{p-1}, Linv row block p-2), then the jobs -- Linv row block p-1 (2 (p-1) units), at p = 3 also the
-// partial sums of Linv row block 3 over kb < 2 (4 units), then the far trailing tiles of panel
-// p-1 (C >= 2p + 2, R >= C)
+// F(p)'s side phase, waves wlo..7: the stores of what panel p-1 finished (L panel p-1; Linv row
+// block p-1 right of column 32 (p-1), Dinv_{p-1} included), then the jobs -- Linv row block p-1
+// (2 (p-1) units, each storing its finished half from its registers), at p = 3 also the partial
+// sums of Linv row block 3 over kb < 2 (4 units), then the far trailing tiles of panel p-1
+// (C >= 2p + 2, R >= C).  (Row block p-2 was stored here whole, and row block 2 in the factor's
+// tail: 4096 of the tail's 6144 stores; chain step 53.0 -> 51.6 us, C2 523 -> 529 fits/s,
+// profiles/r05r.  Also moving row block 3's kb = 2 term into F(3)'s side phase, by the waves
+// that finish Linv_{2,j}, lengthened the F and P phases: 53.1 us.)
 template <typename T>
 __device__ __forceinline__ void la_side(T* __restrict__ A, int64_t ld, T* __restrict__ Linv, T* __restrict__ sS,
-                                        const T* __restrict__ sDi, int p, int t, int w, int wlo, int lr, int lk,
-                                        bool dinv) {
+                                        const T* __restrict__ sDi, int p, int t, int w, int wlo, int lr, int lk) {
     const int nth = NT - 64 * wlo, tid = t - 64 * wlo;
     la_store_lpanel<T>(A, ld, sS, p - 1, tid, nth);
-    if (dinv) la_store_dinv<T>(Linv, sS, sDi, p - 1, tid, nth);
-    if (p >= 2) la_store_linv_rows<T>(Linv, sS, sDi, p - 2, tid, nth);
+    la_store_linv_diag<T>(Linv, sS, sDi, p - 1, tid, nth);
     const int pl = p - 1, nl = 2 * pl, np3 = (p == 3) ? 4 : 0;
     const int cmin = 2 * p + 2, nc = 8 - cmin, nt = nc > 0 ? nc * (nc + 1) / 2 : 0;
     const int nw = 8 - wlo;
 #pragma unroll 1
     for (int job = w - wlo; job < nl + np3 + nt; job += nw) {
         if (job < nl) {
-            la_linv_unit<T>(sS, sDi, pl, job >> 1, job & 1, job >> 1, pl, LA_FINISH, lr, lk);
+            la_linv_unit<T>(sS, sDi, pl, job >> 1, job & 1, job >> 1, pl, LA_FINISH, lr, lk, Linv);
         } else if (job < nl + np3) {
             const int u = job - nl;
             la_linv_unit<T>(sS, sDi, 3, u >> 1, u & 1, u >> 1, 2, 0, lr, lk);
@@ -995,7 +1010,7 @@ __device__ __forceinline__ void diag_factor_la(T* __restrict__ A, int64_t ld, T*
             fact32<T>(sS, sDi, c0, fail, prof ? prof + 4 : nullptr);
             if (prof) pfw += wall_clock64() - tf0;
         } else if (p > 0) {
-            la_side<T>(A, ld, Linv, sS, sDi, p, t, w, 1, lr, lk, pan != nullptr);
+            la_side<T>(A, ld, Linv, sS, sDi, p, t, w, 1, lr, lk);
             if (pan) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the panel's stores drained
         }
         __syncthreads();
@@ -1097,9 +1112,9 @@ __device__ __forceinline__ void diag_factor_la(T* __restrict__ A, int64_t ld, T*
     }
     if (fail >= 0) atomicMin(info, (int)(col0 + fail + 1));  // wave 0, every lane the same value
     // Linv's last row block: the kb = 2 term and -Dinv_3 S (6 units, waves 0-5), each storing its
-    // half block to global memory from its registers; the stores of L panel 3, Linv row block 2
-    // and the rest of row block 3 (its diagonal block Dinv_3 and the zeros right of it) by waves
-    // 6-7 meanwhile (GPRX_LA_TAIL_LDS: row block 3 from LDS after a barrier, the round-3 order)
+    // half block to global memory from its registers; the stores of L panel 3 and the rest of row
+    // block 3 (its diagonal block Dinv_3 and the zeros right of it) by waves 6-7 meanwhile
+    // (GPRX_LA_TAIL_LDS: row block 3 from LDS after a barrier, the round-3 order)
 #ifndef GPRX_LA_TAIL_LDS
     constexpr bool direct = true;
 #else
@@ -1115,7 +1130,6 @@ __device__ __forceinline__ void diag_factor_la(T* __restrict__ A, int64_t ld, T*
             st_agent(pan, 4);
         }
         la_store_lpanel<T>(A, ld, sS, 3, t - 384, 128);
-        la_store_linv_rows<T>(Linv, sS, sDi, 2, t - 384, 128);
         if (direct)  // row block 3, columns 96..127 (Dinv_3, zeros above its diagonal)
             for (int e = t - 384; e < 32 * 32; e += 128) {
                 const int r = 96 + (e & 31), c = 96 + (e >> 5);
