@@ -66,6 +66,9 @@ constexpr int AHEAD = NBUF - 1;  // stages in flight ahead of the one being comp
 // BKS: their feature widths are multiples of 16).  f32 stages are twice as deep (the f64
 // stage's LDS bytes, half the barriers per flop): C4's f32 factor 101.9 -> 98.6 ms, same-box
 // A/B (profiles/r04f); GPRX_F32_BKS=16 builds the round-3 depth
+// (GPRX_F32_BKS=64: two 139 KB ring buffers, one stage ahead -- probe 0.818 -> 0.836 of the f32
+// bound, C4's factor only 101.7 -> 100.9 ms same box, profiles/r05yz; not the default: one
+// stage of lead is thin for the sharded fit's window-fed operands)
 #ifndef GPRX_F32_BKS
 #define GPRX_F32_BKS 32
 #endif
@@ -139,7 +142,7 @@ struct Stage {
     // (the factorisation's 32-deep f32 stages keep the pair adjacent instead: tile_mma reads
     // both columns with ONE ds_read2_b32 -- PAIRED below -- and the pair's two k-columns are
     // then read by the same lane, in different MFMA steps)
-    static constexpr int ROT = (CPI == 2 && BK != 32) ? 16 : 0;
+    static constexpr int ROT = (CPI == 2 && BK < 32) ? 16 : 0;
     // row of the operand column that lane `lane`'s 16-B load brings (its LDS position is fixed)
     __device__ static inline int src_row(int lane) {
         const int lcol = lane / LPC, lrow = (lane % LPC) * E;
@@ -283,7 +286,8 @@ __device__ __forceinline__ void tile_mma(typename Mfma<T>::acc_t (&acc)[2][4], c
     // triangle of a triangular B) are loops of their own with the same barriers: with a
     // wave-uniform test inside one loop, the accumulators merged from two paths every stage
     // (64 register moves, and a wait for the last MFMAs, per stage).
-    const int nmf = __builtin_amdgcn_readfirstlane(kact < K ? kact : K) / BK;
+    // (rounded up: kact = 32 (wc + 1) for a triangular B, whose columns beyond it are stored zeros)
+    const int nmf = (__builtin_amdgcn_readfirstlane(kact < K ? kact : K) + BK - 1) / BK;
     constexpr bool LATE = FEED < 0 && FeedOf<T>::late;
     constexpr int MID = FEED < 0 ? FeedOf<T>::mid : -1;
     if constexpr (LATE) {
@@ -374,7 +378,7 @@ __device__ __forceinline__ void tile_mma(typename Mfma<T>::acc_t (&acc)[2][4], c
 #pragma unroll
                     for (int y = 0; y < 4; y++) fa[r][y] = a[S::at(kr, wr * 64 + y * 16 + lr)];
                 };
-                constexpr bool PAIRED = sizeof(T) == 4 && BK == 32 && S::CPI == 2 && S::ROT == 0;
+                constexpr bool PAIRED = sizeof(T) == 4 && BK >= 32 && S::CPI == 2 && S::ROT == 0;
                 if constexpr (PAIRED) {
                     // f32, 32-deep stages: k-step 2 j + h takes the k-columns 2 (4 j + lk) + h, so a
                     // lane's two operands of steps 2j, 2j + 1 are the two columns of ONE DMA pair
