@@ -413,10 +413,10 @@ struct TileBuild {
     int* flag;
     int mode;
 };
-// Per diagonal block k, TP_STRIDE state words of the split diagonal step (k_ptiles.hip): [0..3]
+// Per diagonal block k, TP_STRIDE state words of the split diagonal step (k_ptiles.hip): [0..7]
 // TPART(k, p)'s phase, [TP_DPAN] DIAGX(k)'s published panels (the progressive TPART(k + 1, .)
 // follow it)
-constexpr int TP_STRIDE = 8, TP_DPAN = 4;
+constexpr int TP_STRIDE = 16, TP_DPAN = 8;  // (up to eight parts: k_ptiles.hip tp_parts)
 
 // Distributed tile factorisation (k_ptiles.hip, potrf_tiles_kernel<T, true>; gprx_dist.cpp):
 // this rank's view of a factorisation whose row blocks are dealt over g ranks in groups of gb

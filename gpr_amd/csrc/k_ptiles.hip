@@ -1156,6 +1156,15 @@ __host__ __device__ constexpr bool tp_linv_form() { return false; }
 #else
 __host__ __device__ constexpr bool tp_linv_form() { return true; }
 #endif
+// TPART workgroups per split diagonal step: f64 (the Linv form) eight -- part p = C + 4 h takes
+// the column groups C, 7 - C of T's rows 64 h .. 64 h + 63 and the S quarter of tile-rows C, 7 - C
+// over T's columns 64 h .. 64 h + 63 (tpart_run8) -- f32 and the progressive form four
+// (GPRX_TP_PARTS4: four for f64 too)
+#ifdef GPRX_TP_PARTS4
+__host__ __device__ constexpr int tp_parts(bool f64) { return (void)f64, 4; }
+#else
+__host__ __device__ constexpr int tp_parts(bool f64) { return f64 && tp_linv_form() ? 8 : 4; }
+#endif
 #ifdef GPRX_NO_SPLIT  // (A/B builds: the split diagonal step compiled out)
 constexpr bool SPLIT_CODE = false;
 #else
@@ -2092,6 +2101,172 @@ __device__ __noinline__ bool tpart_run(const TpCtx<T>* ap, T* __restrict__ Akm, 
     return true;
 }
 
+// TPART(k, p), eight parts (f64, the Linv form): p = C + 4 h, column groups g0 = C, g1 = 7 - C.
+// 1. T's rows 64 h .. 64 h + 63 of groups g0, g1: wave w forms the 16 x 16 block of row tile
+//    w & 3 and group w >> 2 (per SIMD, waves w and w + 4: one block of each group, 4 (g0 + 1) +
+//    4 (g1 + 1) = 36 MFMAs, half the four-part form's), stored in place once the four parts of
+//    the same rows have read their A operand (the other half's parts read other rows); tflag 2.
+// 2. Once all of T is stored and A_kk is final: tiles 5 h .. of the quarter of tile-rows g0, g1
+//    (5 and 4 of its 9), each over all of T as eight 16-column slices, one per wave (20 or 16
+//    MFMAs per wave against 36), summed with A_kk through LDS into the S buffer; tflag 3.  (A
+//    split of the quarter by T's column halves halved the staging too, but DIAGX then summed two
+//    S buffers: its copy went 1.9 -> 3.5 us.)
+// Same tickets and waits as the four-part form (order_tparts: TPART(k, 7) .. (k, 0); P >= 8).
+template <typename T, bool DIST>
+__device__ __noinline__ bool tpart_run8(const TpCtx<T>* ap, T* __restrict__ Akm, const T* __restrict__ Akk, int64_t ld,
+                                        const T* __restrict__ Lp, T* __restrict__ sb, int* tf, int k, const int p,
+                                        T* smem, int& s_ok, const int t) {
+    typedef TpL<T> Q;
+    typedef Mfma<T> Tr;
+    typedef typename Tr::acc_t acc_t;
+    typedef typename Tr::vec_t vec_t;
+    const TpCtx<T> a = *ap;
+    const int lane = t & 63, w = t >> 6, lr = lane & 15, lk = lane >> 4;
+    const int C = p & 3, h = p >> 2;
+    const int g0 = C, g1 = 7 - C;
+    long long* xs = (a.xt && h == 0) ? a.xt + 4 * (4 * (int64_t)k + C) : nullptr;  // (trace: the h = 0 parts)
+    // ---- phase 1 ---------------------------------------------------------------------------
+    {
+        const int rt = w & 3, gi = w >> 2, g = gi ? g1 : g0, nk = 4 * (g + 1);  // k-steps of 4 (<= 32)
+        const int row0 = 64 * h + 16 * rt;
+        T* Ls = smem;
+        T af[32];  // A fragments: row row0 + lr, k = 4 kq + lk, kq < nk
+        {
+            const T* ar = Akm + row0 + lr + (int64_t)lk * ld;
+#pragma unroll
+            for (int kq = 0; kq < 32; kq++)
+                if (kq < nk) af[kq] = ar[(int64_t)(4 * kq) * ld];
+        }
+        if (w == 0) {
+            bool remote = false;
+            const bool ok = tpart_wait_linv<T, DIST>(a, k - 1, remote);
+            if (ok) {
+                if (remote) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+                else __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            }
+            s_ok = ok ? 1 : 0;
+        }
+        __syncthreads();
+        if (!__builtin_amdgcn_readfirstlane(s_ok)) return false;
+        if (xs && w == 0) xs[0] = wall_clock64();  // Linv_{k-1} seen
+        // Linv_{k-1} rows 16 g0 + r (r < 16) and 16 g1 + r - 16 (r >= 16), all columns, as
+        // Ls[r + col LSB] (the four-part form's staging)
+        {
+            constexpr int VPC = 32 / Q::E, NV = 32 * DB / Q::E / NT;
+            vec_t lv[NV];
+#pragma unroll
+            for (int u = 0; u < NV; u++) {
+                const int e = u * NT + t, r = Q::E * (e % VPC), col = e / VPC;
+                const int row = (r < 16) ? 16 * g0 + r : 16 * g1 + r - 16;
+                lv[u] = *reinterpret_cast<const vec_t*>(Lp + row + (int64_t)col * DB);
+            }
+#pragma unroll
+            for (int u = 0; u < NV; u++) {
+                const int e = u * NT + t;
+                *reinterpret_cast<vec_t*>(Ls + Q::E * (e % VPC) + (e / VPC) * Q::LSB) = lv[u];
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (w == 0) st_agent(tf + p, 1);  // "A read"
+        acc_t acc = acc_t{0};  // T(row0 + lr, 16 g + orow(lk, reg))
+#pragma unroll
+        for (int kq = 0; kq < 32; kq++) {
+            if (kq < nk) {
+                const int kc = 4 * kq + lk;
+                acc = Tr::mma(Ls[(16 * gi + lr) + kc * Q::LSB], af[kq], acc);
+            }
+        }
+        if (xs && w == 0) xs[1] = wall_clock64();  // T computed
+        if (w == 0) s_ok = tpart_wait_flags<T>(a, tf + 4 * h, 4, 1) ? 1 : 0;  // this half's readers
+        __syncthreads();
+        if (!__builtin_amdgcn_readfirstlane(s_ok)) return false;
+#pragma unroll
+        for (int reg = 0; reg < 4; reg++) st_sc1(Akm + row0 + lr + (int64_t)(16 * g + Tr::orow(lk, reg)) * ld, acc[reg]);
+        publish(tf + p, 2, false);
+        if (xs && w == 0) xs[2] = wall_clock64();
+    }
+    // ---- phase 2 ---------------------------------------------------------------------------
+    if (w == 0) {
+        bool ok = tpart_wait_flags<T>(a, tf, 8, 2);                           // all of T
+        if (ok) ok = tpart_wait_ver<T>(a, a.ver + (int64_t)k * a.nv + k, k - 1);  // A_kk final
+        if (ok) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        s_ok = ok ? 1 : 0;
+    }
+    __syncthreads();
+    if (!__builtin_amdgcn_readfirstlane(s_ok)) return false;
+    // all of T (column c at smem + tcol(c)) by LDS-DMA
+    {
+        constexpr int LPC = 64 / Q::CPI;
+        for (int q = w; q < DB / Q::CPI; q += NT / 64)
+            __builtin_amdgcn_global_load_lds(
+                (const void*)(Akm + Q::E * (lane % LPC) + (int64_t)(Q::CPI * q + lane / LPC) * ld),
+                (__attribute__((address_space(3))) void*)(smem + q * Q::TQ), 16, 0, 0);
+    }
+    // the quarter's tiles tau (tau <= g0: (g0, tau), else (g1, tau - g0 - 1)); this part takes
+    // tau = 5 h .. 5 h + nt - 1 (5 and 4 of them), each as eight 16-column slices, slice w on
+    // wave w; the slices are summed with A_kk in a fixed order through LDS
+    auto tile_of = [&](int tau, int& R, int& Cc) {
+        R = (tau <= g0) ? g0 : g1;
+        Cc = (tau <= g0) ? tau : tau - g0 - 1;
+    };
+    const int tau0 = 5 * h, nt = h ? 4 : 5;
+    // this thread's output elements (e = t, t + 512, t + 1024 < 256 nt) and their A_kk values,
+    // loaded while T lands
+    T av[3];
+#pragma unroll
+    for (int u = 0; u < 3; u++) {
+        const int e = t + u * NT;
+        av[u] = T(0);
+        if (e < 256 * nt) {
+            int R, Cc;
+            tile_of(tau0 + (e >> 8), R, Cc);
+            const int ln = (e & 255) >> 2, reg = e & 3;
+            av[u] = Akk[(16 * R + (ln & 15)) + (int64_t)(16 * Cc + Tr::orow(ln >> 4, reg)) * ld];
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    acc_t sl[5];
+#pragma unroll
+    for (int i = 0; i < 5; i++) {
+        sl[i] = acc_t{0};
+        if (i < nt) {
+            int R, Cc;
+            tile_of(tau0 + i, R, Cc);
+#pragma unroll
+            for (int kq = 4 * w; kq < 4 * w + 4; kq++) {
+                const int kc = 4 * kq + lk;
+                sl[i] = Tr::mma(-smem[Q::tcol(kc) + 16 * Cc + lr], smem[Q::tcol(kc) + 16 * R + lr], sl[i]);
+            }
+        }
+    }
+    __syncthreads();  // every wave done reading T: its area takes the slices
+#pragma unroll
+    for (int i = 0; i < 5; i++)
+        if (i < nt)
+#pragma unroll
+            for (int reg = 0; reg < 4; reg++) smem[(i * 8 + w) * 256 + lane * 4 + reg] = sl[i][reg];
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 3; u++) {
+        const int e = t + u * NT;
+        if (e < 256 * nt) {
+            const int i = e >> 8, el = e & 255;
+            int R, Cc;
+            tile_of(tau0 + i, R, Cc);
+            const int ln = el >> 2, reg = el & 3;
+            T v = av[u];
+#pragma unroll
+            for (int w8 = 0; w8 < 8; w8++) v += smem[(i * 8 + w8) * 256 + el];
+            st_sc1(sb + (16 * R + (ln & 15)) + (int64_t)(16 * Cc + Tr::orow(ln >> 4, reg)) * DB, v);
+        }
+    }
+    if (xs && w == 0) xs[3] = wall_clock64();  // the part's S tiles computed (their stores in flight)
+    publish(tf + p, 3, false);
+    return true;
+}
+
 // Lkk: L_{k-1,k-1} (ld) when DIAGX(k-1) publishes its panels where these parts can read them
 // (one GPU, or DIAGX(k-1) on this rank): the progressive phase 1; null: the Linv_{k-1} form
 template <typename T, bool DIST>
@@ -2100,8 +2275,11 @@ __device__ __forceinline__ bool tpart_task(const TpCtx<T>* ap, T* Akm, T* Akk, i
     // S's quarters: f64 into the S buffer (DIAGX copies it into the look-ahead factor's LDS
     // image); f32 in place into A_kk (the rank-8 factor reads its block from memory)
     constexpr bool img = std::is_same<T, double>::value && DIAG_LA;
-    return tpart_run<T, DIST>(ap, Akm, Akk, ld, Lp, img ? ap->pbuf : Akk, img ? (int64_t)DB : ld, ap->tflag + TP_STRIDE * k, k,
-                              c, smem, s_ok, t, img ? Lkk : nullptr);
+    if constexpr (img && tp_parts(true) == 8)
+        return tpart_run8<T, DIST>(ap, Akm, Akk, ld, Lp, ap->pbuf, ap->tflag + TP_STRIDE * k, k, c, smem, s_ok, t);
+    else
+        return tpart_run<T, DIST>(ap, Akm, Akk, ld, Lp, img ? ap->pbuf : Akk, img ? (int64_t)DB : ld,
+                                  ap->tflag + TP_STRIDE * k, k, c, smem, s_ok, t, img ? Lkk : nullptr);
 }
 
 // DIAGX(k > 0) of the split step, f32 (the parts wrote S into A_kk): wait for the four
@@ -2142,7 +2320,8 @@ __device__ __noinline__ bool diagx_split(const TpCtx<T>* ap, int k, T* smem, int
         rr[u] = 16 * R + 2 * (e & 7);
         cc[u] = 16 * C + (e >> 3);
     }
-    const bool ok = tpart_wait_flags<T>(a, tf, 4, 3);  // this wave polls the four parts itself
+    constexpr int NP = tp_parts(std::is_same<T, double>::value);
+    const bool ok = tpart_wait_flags<T>(a, tf, NP, 3);  // this wave polls the parts itself
     if (ok) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         if (xs && w == 0) xs[2] = wall_clock64();  // every quarter seen
@@ -2445,6 +2624,7 @@ struct Cost {  // per-task durations (us, one CU), calibrated from GPRX_PT_TRACE
     // ~8 us before its end)
     double tpart_prog = 2.5;
     bool prog = false;  // this schedule is for the progressive form (set by the callers)
+    int np = 4;         // TPART tasks per split step (tp_parts; set by the callers)
 };
 
 // TPART tickets of one k in the order TPART(k, 3), (k, 2), (k, 1), (k, 0): each part waits for
@@ -2458,7 +2638,7 @@ static void order_tparts(std::vector<int4>& list) {
     for (auto& kv : pos) {
         std::vector<int>& v = kv.second;
         std::sort(v.begin(), v.end());
-        for (size_t u = 0; u < v.size(); u++) list[v[u]].z = 3 - (int)u;
+        for (size_t u = 0; u < v.size(); u++) list[v[u]].z = (int)v.size() - 1 - (int)u;
     }
 }
 
@@ -2574,9 +2754,9 @@ static Schedule make_schedule(int nc, int nr, int W, int near, int P, const Cost
             }
     }
     auto make_diagx = [&](int k) {
-        if (split && k >= 1) {  // TPART(k, 3..0), then DIAGX(k) on their products
-            int tp[4];
-            for (int c = 3; c >= 0; c--) {
+        if (split && k >= 1) {  // TPART(k, np-1..0), then DIAGX(k) on their products
+            int tp[8];
+            for (int c = cm.np - 1; c >= 0; c--) {
                 tp[c] = add(T_TPART, k, c, 0, 0, cm.prog ? cm.tpart_prog : cm.tpart + cm.tpart_c * (c + 1));
                 dep(tp[c], diagx[k - 1]);
                 dep(tp[c], last_upd[(size_t)k * nc + (k - 1)]);
@@ -2584,7 +2764,7 @@ static Schedule make_schedule(int nc, int nr, int W, int near, int P, const Cost
             }
             const int id = add(T_DIAGX, k, k, 0, 0, cm.diagx_s);
             diagx[k] = id;
-            for (int c = 0; c < 4; c++) dep(id, tp[c]);
+            for (int c = 0; c < cm.np; c++) dep(id, tp[c]);
             dep(id, last_upd[(size_t)k * nc + k]);
             return;
         }
@@ -2813,9 +2993,9 @@ static DistSched make_schedule_dist(int nc, bool inv, int W, int near, int P, in
         dep(id, prod);
     };
     auto make_diagx = [&](int k) {
-        int tp[4] = {-1, -1, -1, -1};
-        if (split && k >= 1)  // TPART(k, 3..0) on the owner of row block k
-            for (int c = 3; c >= 0; c--) {
+        int tp[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
+        if (split && k >= 1)  // TPART(k, np-1..0) on the owner of row block k
+            for (int c = cm.np - 1; c >= 0; c--) {
                 tp[c] = add(T_TPART, k, c, 0, 0,
                             (cm.prog && own(k - 1) == own(k)) ? cm.tpart_prog : cm.tpart + cm.tpart_c * (c + 1), own(k));
                 dep(tp[c], linv(k - 1, own(k)));
@@ -2825,7 +3005,7 @@ static DistSched make_schedule_dist(int nc, bool inv, int W, int near, int P, in
         const int id = add(T_DIAGX, k, k, 0, 0, (k == 0) ? cm.diag0 : (split ? cm.diagx_s : cm.diagx), own(k));
         diagx[k] = id;
         if (k >= 1) {
-            for (int c = 0; c < 4; c++) dep(id, tp[c]);
+            for (int c = 0; c < cm.np; c++) dep(id, tp[c]);
             dep(id, linv(k - 1, own(k)));
             dep(id, last_upd[(size_t)k * nci + (k - 1)]);
             dep(id, last_upd[(size_t)k * nci + k]);
@@ -3018,6 +3198,7 @@ struct Params {
     Cost cost(bool f64) const {
         Cost c = cm;
         c.prog = f64 && DIAG_LA && !tp_linv_form();
+        c.np = tp_parts(f64 && DIAG_LA);
         return c;
     }
 };
@@ -3054,7 +3235,7 @@ static Schedule best_schedule(int nc, int nr, const Params& pr, int P, bool buil
 // image; f32: S in place for the rank-8 factor), unless GPRX_PT_SPLIT=0
 static bool split_for(bool f64) { (void)f64; return SPLIT_CODE && params().split != 0; }
 // (the four parts of a step wait for each other: at least four workgroups)
-static bool split_for(bool f64, int P) { return P >= 4 && split_for(f64); }
+static bool split_for(bool f64, int P) { return P >= tp_parts(f64 && DIAG_LA) && split_for(f64); }
 
 }  // namespace pt
 

@@ -29,9 +29,12 @@ def _sched(nc, nr, P=256, build=False, ident=False, ratio=0):
 W_DEF = 64  # k_ptiles.hip Params defaults: update chunk width, single-panel tail by size
 
 
+NPARTS = 8  # TPART tasks per split step of the f64 schedule (k_ptiles.hip tp_parts)
+
+
 def tparts(nc):
-    """The split diagonal step (f64 schedule): TPART(k, 0..3) for every k >= 1."""
-    return 4 * max(0, nc - 1)
+    """The split diagonal step (f64 schedule): TPART(k, 0..7) for every k >= 1."""
+    return NPARTS * max(0, nc - 1)
 
 
 def near_def(nc):
@@ -270,10 +273,10 @@ def _sched_list(nc, nr, P=256, ratio=None, ident=False):
 @pytest.mark.parametrize("nc,ratio,ident", [(2, None, False), (9, 0, False), (33, 2, False), (40, 0, True),
                                             (128, None, False)])
 def test_schedule_split_step_ticket_order(nc, ratio, ident):
-    """The split diagonal step's deadlock-freedom argument (k_ptiles.hip order_tparts): the four
-    TPART(k, c) tickets come in the order c = 3, 2, 1, 0, after DIAGX(k - 1) and before DIAGX(k),
-    and no other k's parts lie between them -- so at most three workgroups ever wait on a
-    sibling part and P >= 4 workers always leave one to claim the next ticket."""
+    """The split diagonal step's deadlock-freedom argument (k_ptiles.hip order_tparts): the eight
+    TPART(k, c) tickets come in the order c = 7, .., 0, after DIAGX(k - 1) and before DIAGX(k),
+    and no other k's parts lie between them -- so at most seven workgroups ever wait on a
+    sibling part and P >= 8 workers always leave one to claim the next ticket."""
     lst = _sched_list(nc, 2 * nc + 1 if ident else nc + 1, ratio=ratio, ident=ident)
     typ = lst[:, 0] & 0xFF
     diag = {int(lst[q, 1]): q for q in np.nonzero(typ == 0)[0]}
@@ -282,14 +285,14 @@ def test_schedule_split_step_ticket_order(nc, ratio, ident):
     assert len(tp) == tparts(nc)
     for k in range(1, nc):
         q = tp[lst[tp, 1] == k]
-        assert list(lst[q, 2]) == [3, 2, 1, 0]
+        assert list(lst[q, 2]) == list(range(NPARTS - 1, -1, -1))
         assert diag[k - 1] < q[0] and q[-1] < diag[k]
         assert np.all(lst[tp[(tp > q[0]) & (tp < q[-1])], 1] == k)
 
 
-def test_schedule_split_step_needs_four_workers():
-    """With fewer than four workers the parts could all wait on a sibling that no worker is
+def test_schedule_split_step_needs_eight_workers():
+    """With fewer workers than parts the parts could all wait on a sibling that no worker is
     left to claim: the schedule falls back to the whole diagonal step inside DIAGX."""
-    lst = _sched_list(9, 10, P=3, ratio=0)
+    lst = _sched_list(9, 10, P=NPARTS - 1, ratio=0)
     assert not np.any((lst[:, 0] & 0xFF) == 4)
     assert len(lst) == _expected_tasks(9, 10) - tparts(9)
