@@ -1304,7 +1304,7 @@ struct Args {
     // split diagonal step (f64): TPART(k, p) tasks form L_{k,k-1} and S = A_kk - L L^T in
     // quarters; DIAGX(k) copies S and factors it (diagx_split)
     int split;
-    T* pbuf;     // DB x DB: S, its lower tiles written by the four parts
+    T* pbuf;     // DB x DB: S, its lower tiles written by the parts
     int* tflag;  // [nc][TP_STRIDE] TPART(k, p) state: 1 its A operand is read, 2 its T stored, 3 its S quarter
                  // stored; [TP_DPAN] DIAGX(k)'s published panels
 };
@@ -1750,10 +1750,10 @@ __device__ __forceinline__ long long diagx_ts(T* __restrict__ Akm, T* __restrict
 //   2. once all of T is stored and A_kk is final, part p forms the S = A_kk - T T^T quarter of
 //      tile-rows p and 7 - p (T staged in LDS) into pbuf (f64: DIAGX copies the quarters
 //      into its LDS image, diagx_split) or in place into A_kk (f32), and raises tflag 3.
-// Tickets: TPART(k, 3), (k, 2), (k, 1), (k, 0) in that order (order_tparts), after DIAGX(k-1)
+// Tickets: TPART(k, np-1) .. (k, 0) in that order (order_tparts; np = tp_parts), after DIAGX(k-1)
 // and before DIAGX(k), and no other k's parts between them (test_schedule.py checks this).
 // Nothing but DIAGX(k) depends on the parts, so every ticket between them completes; a part
-// waits only on its siblings, so at most three workgroups wait at once and with P >= 4 one
+// waits only on its siblings, so at most np - 1 workgroups wait at once and with P >= np one
 // is always free to claim the next sibling (split_for: fewer workers keep the whole step
 // inside DIAGX).
 // (the out-of-line functions read these through a pointer to the copy the kernel keeps in LDS,
@@ -2300,8 +2300,8 @@ __device__ __forceinline__ bool diagx_split_wait(const TpCtx<T>* ap, int k, int&
 }
 
 // DIAGX(k > 0) of the split step: S (the 36 lower 16 x 16 tiles, assembled in the shared S
-// buffer by the four parts) into the factor's LDS image, then L_{k,k-1} is final (lcnt[k] =
-// k).  Each wave waits for the four parts itself and copies 576 element pairs, 9 per lane
+// buffer by the parts) into the factor's LDS image, then L_{k,k-1} is final (lcnt[k] =
+// k).  Each wave waits for the parts itself and copies 576 element pairs, 9 per lane
 // (lower tile tau = q / 128, pair q % 8 of its column (q % 128) / 8), one batch of loads.
 template <typename T>
 __device__ __noinline__ bool diagx_split(const TpCtx<T>* ap, int k, T* smem, int& s_ok, const int t) {
@@ -2627,7 +2627,7 @@ struct Cost {  // per-task durations (us, one CU), calibrated from GPRX_PT_TRACE
     int np = 4;         // TPART tasks per split step (tp_parts; set by the callers)
 };
 
-// TPART tickets of one k in the order TPART(k, 3), (k, 2), (k, 1), (k, 0): each part waits for
+// TPART tickets of one k in the order TPART(k, np-1), .., (k, 0): each part waits for
 // the reads of the parts with a larger c, so those must hold the earlier tickets (the parts
 // have the same inputs and one consumer, DIAGX(k): permuting them over their slots keeps
 // every other order of the list)
@@ -3234,7 +3234,7 @@ static Schedule best_schedule(int nc, int nr, const Params& pr, int P, bool buil
 // the split diagonal step runs for both precisions (f64: S through the look-ahead factor's LDS
 // image; f32: S in place for the rank-8 factor), unless GPRX_PT_SPLIT=0
 static bool split_for(bool f64) { (void)f64; return SPLIT_CODE && params().split != 0; }
-// (the four parts of a step wait for each other: at least four workgroups)
+// (the parts of a step wait for each other: at least tp_parts workgroups)
 static bool split_for(bool f64, int P) { return P >= tp_parts(f64 && DIAG_LA) && split_for(f64); }
 
 }  // namespace pt
