@@ -586,6 +586,11 @@ void launch_gemm_nt_splitk(T* C, int64_t ldc, int64_t cstride, const T* A, int64
 template <typename T>
 void launch_syrk_splitk(T* C, int64_t ldc, int64_t cstride, const T* A, int64_t lda, int64_t M, int64_t N, int64_t K,
                         int P, T alpha, hipStream_t s);
+// C = alpha A B^T + beta C (no triangle) on 256 x 128 tiles (k_syrk.hip) when the shape allows:
+// returns false otherwise (launch_gemm_nt then takes its own kernel)
+template <typename T>
+bool launch_gemm_tall(T* C, int64_t ldc, const T* A, int64_t lda, const T* B, int64_t ldb, int64_t M, int64_t N,
+                      int64_t K, T alpha, T beta, hipStream_t s);
 
 // Back substitution L^T alpha = z with z given as the m augmented rows (row-major output
 // alpha: np x m, ld m).  Uses the diagonal-block inverses.

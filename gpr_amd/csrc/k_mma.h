@@ -460,6 +460,88 @@ __device__ __forceinline__ void tile_mma(typename Mfma<T>::acc_t (&acc)[2][4], c
     }
 }
 
+// 256 x 128 output tile (A: 256 rows, B: 128 rows), for stand-alone kernels only: 128
+// accumulator registers, which the factorisation's task loop (at 256 VGPRs) cannot hold.  The 8
+// waves take 4 x 2 blocks of 64 x 64: 16 MFMAs per k-step from 8 fragment reads (the 128 x 128
+// tile: 8 MFMAs from 6), and a stage's DMAs bring 384 rows' columns for twice the flops (the 128
+// tile: 256).  Two ring buffers of three operand groups (A rows 0-127, A rows 128-255, B): a
+// stage is 2 x 64 MFMAs per SIMD (8192 cycles f64), time enough for the next stage's loads,
+// issued right after the stage barrier.  Step kq+1's fragments are read after MID MFMAs of step
+// kq.  Probe (scripts/mma_probe.hip ... tall): f64 0.901 of the MFMA bound against 0.877 for the
+// 128 x 128 tile (profiles/r05u).
+template <typename T>
+constexpr size_t tall_lds() {
+    return sizeof(T) * 2 * 3 * Stage<T>::GRP * Stage<T>::SRP;
+}
+template <typename T, int MID = 1>
+__device__ __forceinline__ void tile_mma_tall(typename Mfma<T>::acc_t (&acc)[4][4], const T* __restrict__ A,
+                                              int64_t lda, const T* __restrict__ B, int64_t ldb, int K, T* smem,
+                                              const int t) {
+    typedef Mfma<T> Tr;
+    typedef Stage<T> S;
+    constexpr int BK = BkOf<T>::v;
+    static_assert(S::ROT == 0, "tall tile: unrotated staging");
+    constexpr int GR3 = 3 * S::GRP, IPW3 = GR3 / 8, STG3 = GR3 * S::SRP;
+    static_assert(GR3 % 8 == 0, "tall tile: whole DMA instructions per wave");
+    const int lane = t & 63, w = t >> 6;
+    const int wr = w & 3, wc = w >> 2, lr = lane & 15, lk = lane >> 4;
+    const int lcol = lane / S::LPC, lrow = S::src_row(lane);
+    auto issue = [&](int st) {
+        T* buf = smem + (st & 1) * STG3;
+#pragma unroll
+        for (int u = 0; u < IPW3; u++) {
+            const int g = w * IPW3 + u, op = g / S::GRP, gg = g - op * S::GRP;  // op 0, 1: A halves, 2: B
+            const int64_t col = (int64_t)st * BK + gg * S::CPI + lcol;
+            const T* src = (op == 2) ? (B + lrow + col * ldb) : (A + (int64_t)op * GT + lrow + col * lda);
+            __builtin_amdgcn_global_load_lds((const void*)src,
+                                             (__attribute__((address_space(3))) void*)(buf + g * S::SRP), 16, 0, 0);
+        }
+    };
+#pragma unroll
+    for (int x = 0; x < 4; x++)
+#pragma unroll
+        for (int y = 0; y < 4; y++) acc[x][y] = typename Tr::acc_t{0};
+    const int nst = K / BK;
+    if (nst > 0) issue(0);
+    const T* ab = smem + (wr >> 1) * S::GRP * S::SRP;  // this wave's half of A
+    const T* bb = smem + 2 * S::GRP * S::SRP;
+    const int ar = 64 * (wr & 1);
+    T fa[2][4], fb[2][4];
+#pragma nounroll
+    for (int st = 0; st < nst; st++) {
+        wait_vm<0>();  // this wave's loads of stage st (issued a stage ago)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // every wave's; every wave done with the other buffer
+        if (st + 1 < nst) issue(st + 1);
+        const T* a = ab + (st & 1) * STG3;
+        const T* b = bb + (st & 1) * STG3;
+        auto frag = [&](int kq, int r) {
+            const int kr = kq * 4 + lk;
+#pragma unroll
+            for (int x = 0; x < 4; x++) fb[r][x] = b[S::at(kr, 64 * wc + 16 * x + lr)];
+#pragma unroll
+            for (int y = 0; y < 4; y++) fa[r][y] = a[S::at(kr, ar + 16 * y + lr)];
+        };
+        frag(0, 0);
+#pragma unroll
+        for (int kq = 0; kq < BK / 4; kq++) {
+            int m = 0;
+#pragma unroll
+            for (int x = 0; x < 4; x++)
+#pragma unroll
+                for (int y = 0; y < 4; y++) {
+                    if (m == MID) {
+                        __builtin_amdgcn_sched_barrier(0);
+                        if (kq + 1 < BK / 4) frag(kq + 1, (kq + 1) & 1);
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+                    acc[x][y] = Tr::mma(fb[kq & 1][x], fa[kq & 1][y], acc[x][y]);
+                    m++;
+                }
+        }
+    }
+}
+
 // Two products over consecutive column ranges of the same operands in ONE pass of the
 // staging ring: acc1 = A[:, 0:K1] B[:, 0:K1]^T, acc2 = A[:, K1:K1+K2] B[:, K1:K1+K2]^T (K1, K2
 // multiples of BKS).  Two back-to-back tile_mma calls pay the ring's fill and drain twice

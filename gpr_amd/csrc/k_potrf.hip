@@ -484,6 +484,10 @@ void launch_gemm_nt(T* C, int64_t ldc, const T* A, int64_t lda, const T* B, int6
     }();
     const int64_t ntm = M / GT, ntn = N / GT;
     const int64_t nt128 = lower ? ntn * (ntn + 1) / 2 + (ntm - ntn) * ntn : ntm * ntn;
+    // bulk rectangular products: the 256 x 128 tile (half the workgroups of the 128 tile, which
+    // must still fill the chip twice over)
+    if (!lower && nt128 >= 2 * small_tiles && launch_gemm_tall<T>(C, ldc, A, lda, B, ldb, M, N, K, alpha, beta, s))
+        return;
     if (nt128 < small_tiles)
         gemm_launch<T, 64>(C, ldc, A, lda, B, ldb, M, N, K, alpha, beta, lower, s);
     else

@@ -8,6 +8,10 @@
 // rows below it (the label rows).  One workgroup per CU (the ring takes 139 KB of LDS).
 #include "k_mma.h"
 
+#include <cstdint>
+#include <cstdlib>
+#include <type_traits>
+
 namespace gprx {
 namespace sy {
 
@@ -67,7 +71,68 @@ __global__ __launch_bounds__(mm::NT) void syrk_splitk_kernel(T* __restrict__ C, 
         }
 }
 
+// C (M x N, ldc) = alpha A B^T + beta C on 256 x 128 tiles (k_mma.h tile_mma_tall): the
+// stand-alone f64 GEMMs of the posterior variance's recursive solves (launch_gemm_nt); A: M x K,
+// B: N x K, column-major
+template <typename T, bool BETA>
+__global__ __launch_bounds__(mm::NT) void gemm_tall_kernel(T* __restrict__ C, int64_t ldc, const T* __restrict__ A,
+                                                           int64_t lda, const T* __restrict__ B, int64_t ldb, int K,
+                                                           T alpha, T beta, int64_t ntm) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    T* smem = reinterpret_cast<T*>(smem_raw);
+    const int64_t ti = blockIdx.x % ntm, tj = blockIdx.x / ntm;
+    const int64_t i0 = ti * 2 * GT, j0 = tj * GT;
+    typedef mm::Mfma<T> Tr;
+    typename Tr::acc_t acc[4][4];
+    const int t = threadIdx.x;
+    const int lane = t & 63, w = t >> 6;
+    const int lr = lane & 15, lk = lane >> 4, wr = w & 3, wc = w >> 2;
+    mm::tile_mma_tall<T>(acc, A + i0, lda, B + j0, ldb, K, smem, t);
+#pragma unroll
+    for (int x = 0; x < 4; x++)
+#pragma unroll
+        for (int reg = 0; reg < 4; reg++) {
+            T* col = C + (j0 + wc * 64 + x * 16 + Tr::orow(lk, reg)) * ldc + i0 + wr * 64 + lr;
+#pragma unroll
+            for (int y = 0; y < 4; y++) {
+                T v = alpha * acc[x][y][reg];
+                if (BETA) v = fma(beta, col[y * 16], v);
+                col[y * 16] = v;
+            }
+        }
+}
+
 }  // namespace sy
+
+// the tall-tile GEMM when its shape applies (f64, M a multiple of 256, N of 128, K of the stage
+// depth, 16-byte aligned columns); false: the caller takes its own path
+template <typename T>
+bool launch_gemm_tall(T* C, int64_t ldc, const T* A, int64_t lda, const T* B, int64_t ldb, int64_t M, int64_t N,
+                      int64_t K, T alpha, T beta, hipStream_t s) {
+    static const bool off = [] {
+        const char* e = std::getenv("GPRX_GEMM_TALL");
+        return e && e[0] == '0';
+    }();
+    if (off || !std::is_same<T, double>::value || M <= 0 || N <= 0 || K <= 0) return false;
+    if (M % (2 * GT) || N % GT || K % mm::BkOf<T>::v || lda % 2 || ldb % 2 || K > INT32_MAX) return false;
+    if (((uintptr_t)A | (uintptr_t)B) % 16) return false;
+    const int64_t ntm = M / (2 * GT), ntiles = ntm * (N / GT);
+    const size_t lds = mm::tall_lds<T>();
+    const bool use_beta = beta != T(0);
+    auto go = [&](auto kfn) {
+        GPRX_HIP(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        hipLaunchKernelGGL(kfn, dim3((unsigned)ntiles), dim3(mm::NT), lds, s, C, ldc, A, lda, B, ldb, (int)K, alpha,
+                           beta, ntm);
+    };
+    if (use_beta) go(sy::gemm_tall_kernel<T, true>);
+    else go(sy::gemm_tall_kernel<T, false>);
+    GPRX_HIP(hipGetLastError());
+    return true;
+}
+template bool launch_gemm_tall<double>(double*, int64_t, const double*, int64_t, const double*, int64_t, int64_t,
+                                       int64_t, int64_t, double, double, hipStream_t);
+template bool launch_gemm_tall<float>(float*, int64_t, const float*, int64_t, const float*, int64_t, int64_t, int64_t,
+                                      int64_t, float, float, hipStream_t);
 
 // C_p (lower, M x N: M = rows of A incl. the rows below the N x N block) += alpha A_p A_p^T,
 // p < P, K (multiple of 16) columns per partial.
