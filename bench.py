@@ -62,24 +62,52 @@ def fit_roofline_ms(n, d, m, gpus=1):
                   + b_solve / (PEAK_HBM_GBS * 1e9))
 
 
+def host_info():
+    """The CPU the baselines ran on (nproc, CPU model and RAM beside the
+    result): /proc/cpuinfo's model name, /proc/meminfo's MemTotal, the CPUs this process may use."""
+    model, ram = None, None
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), None)
+        with open("/proc/meminfo") as f:
+            kb = next((int(ln.split()[1]) for ln in f if ln.startswith("MemTotal")), None)
+        ram = round(kb / 2 ** 20, 1) if kb else None
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        usable = os.cpu_count()
+    return {"cpu_model": model, "ram_gib": ram, "cpus_usable": usable, "cpus_machine": os.cpu_count()}
+
+
+def _cpu_warmup(O, cfg):
+    """One untimed small call (thread pool start, MKL initialisation, page faults of the code)
+    before a timed CPU leg, so no leg's first sample carries the cold start."""
+    from gpr_amd.synth import make_data
+    X, Y = make_data(512, cfg["d"], cfg["m"])
+    O.fit(cfg["kernel"], X, Y, cfg["sigma"], np.float64, want_core=False)
+
+
 def cpu_baseline(cfg, n_cpu):
     """The CPU restatement of the reference's fit (oracle/: kernel pair loop + LAPACK
-    dgetrf+dgetri in fp64 + C*Y), timed on this host's cores: one fit at n_cpu."""
+    dgetrf+dgetri in fp64 + C*Y), timed on this host's cores: one fit at n_cpu after a warm-up."""
     from oracle import oracle as O
     from gpr_amd.synth import make_data
+    _cpu_warmup(O, cfg)
     X, Y = make_data(n_cpu, cfg["d"], cfg["m"])
     t0 = time.perf_counter()
     O.fit(cfg["kernel"], X, Y, cfg["sigma"], np.float64, want_core=False)
     dt = time.perf_counter() - t0
     scale = (n_cpu / cfg["n"]) ** 3  # fits/s at the bench N (LU inverse is 2N^3)
-    return {
+    return dict({
         "value": (1.0 / dt) * scale,
         "unit": "fits/s",
         "cores": O.num_threads(),
         "kind": "port",
-        "sample": (f"1 fit at N={n_cpu} (d={cfg['d']}, same kernel) in {dt:.2f} s, LAPACK={O.lapack_name()}"
+        "sample": (f"1 fit at N={n_cpu} (d={cfg['d']}, same kernel) in {dt:.2f} s after a warm-up, LAPACK={O.lapack_name()}"
                    + ("" if n_cpu == cfg["n"] else f", cubic-scaled to N={cfg['n']}")),
-    }
+    }, **host_info())
 
 
 def cpu_lml_baseline(cfg, ns, t_gpu_ms=None):
@@ -92,6 +120,8 @@ def cpu_lml_baseline(cfg, ns, t_gpu_ms=None):
     long-double determinant, est. >= 30 min)."""
     from oracle import oracle as O
     from gpr_amd.synth import make_data
+    X, Y = make_data(512, cfg["d"], cfg["m"])  # (untimed warm-up: thread pool, MKL, code pages)
+    O.lml(cfg["kernel"], X, Y, cfg["sigma"], np.float64, with_grad=True)
     ts = []
     for n_ in ns:
         X, Y = make_data(n_, cfg["d"], cfg["m"])
@@ -100,31 +130,38 @@ def cpu_lml_baseline(cfg, ns, t_gpu_ms=None):
         ts.append(time.perf_counter() - t0)
     n = cfg["n"]
     nn = np.array(ns, dtype=np.float64)
-    if len(ns) >= 3:
-        A = np.stack([nn ** 3, nn ** 2, np.ones_like(nn)], axis=1)
-        coef = np.linalg.lstsq(A, np.array(ts), rcond=None)[0]
-        t_n = float(coef[0] * n ** 3 + coef[1] * n ** 2 + coef[2])
-        how = "least-squares cubic a n^3 + b n^2 + c through the points"
+    tt = np.array(ts)
+    pure = ts[-1] * (n / ns[-1]) ** 3
+    fit = None
+    if len(ns) >= 2:
+        # t(n) = a n^3 + b n^2 by least squares RELATIVE to each point (two terms: with three
+        # points a third would fit them exactly and say nothing about the fit's quality); the
+        # residual is the largest relative miss at the measured points
+        A = np.stack([nn ** 3, nn ** 2], axis=1) / tt[:, None]
+        coef = np.linalg.lstsq(A, np.ones_like(tt), rcond=None)[0]
+        pred = coef[0] * nn ** 3 + coef[1] * nn ** 2
+        fit = {"a_n3": float(coef[0]), "b_n2": float(coef[1]),
+               "max_rel_residual": float(np.max(np.abs(pred - tt) / tt)),
+               "t_extrapolated_s": float(coef[0] * n ** 3 + coef[1] * n ** 2)}
+    if fit is not None and fit["a_n3"] > 0 and fit["t_extrapolated_s"] >= ts[-1] * (n / ns[-1]) ** 2:
+        t_n, how = fit["t_extrapolated_s"], "least-squares a n^3 + b n^2 through the points (relative)"
     else:
-        t_n = ts[-1] * (n / ns[-1]) ** 3
-        coef = None
-        how = "pure cubic from the largest point"
-    # (a cubic fit whose n^3 term comes out non-positive is no extrapolation: use the pure cubic)
-    if coef is not None and (coef[0] <= 0 or t_n < ts[-1] * (n / ns[-1]) ** 2):
-        t_n = ts[-1] * (n / ns[-1]) ** 3
-        how = "pure cubic from the largest point (the 3-term fit was not increasing)"
-    return {
+        t_n, how = pure, "pure cubic from the largest point"
+    return dict({
         "value": 1.0 / t_n,
         "unit": "LML+gradient evaluations/s",
         "ms_extrapolated": 1e3 * t_n,
         "cores": O.num_threads(),
         "kind": "port",
         "extrapolated": True,
+        "points": {str(a): b for a, b in zip(ns, ts)},
+        "fit": fit,
+        "ms_pure_cubic_from_largest": 1e3 * pure,
         "sample": (f"oracle LML + gradient (LU inverse via LAPACK {O.lapack_name()}, long-double determinant, "
-                   f"P={5} derivative traces) measured at N={list(ns)}: "
+                   f"P={5} derivative traces) after a warm-up, measured at N={list(ns)}: "
                    + ", ".join(f"{t:.2f} s" for t in ts) + f"; EXTRAPOLATED to N={n} by {how}"),
         "gpu_over_cpu": (t_n * 1e3 / t_gpu_ms) if t_gpu_ms else None,
-    }
+    }, **host_info())
 
 
 def cpu_predict_baseline(cfg, X, alpha, q_cpu):
@@ -139,9 +176,9 @@ def cpu_predict_baseline(cfg, X, alpha, q_cpu):
     t0 = time.perf_counter()
     O.predict(cfg["kernel"], X, alpha, Xq)
     dt = time.perf_counter() - t0
-    return {"value": q_cpu / dt, "unit": "pts/s", "cores": O.num_threads(), "kind": "port",
-            "sample": f"{q_cpu} query points against the N={cfg['n']} d={cfg['d']} model (oracle per-point predict, "
-                      f"OpenMP over the points) in {dt:.2f} s"}
+    return dict({"value": q_cpu / dt, "unit": "pts/s", "cores": O.num_threads(), "kind": "port",
+                 "sample": f"{q_cpu} query points against the N={cfg['n']} d={cfg['d']} model (oracle per-point "
+                           f"predict, OpenMP over the points) in {dt:.2f} s after a warm-up"}, **host_info())
 
 
 def _short(name):
@@ -262,6 +299,60 @@ def make_dist_context(gpr_amd, group, rank, world, local_rank, shared):
     return ctx, "peer (fallback: RCCL initialisation failed)", "; ".join(errs)
 
 
+def chain_from_trace(path):
+    """The diagonal chain as this rank saw it, from a GPRX_DIST_TRACE_FILE dump of one sharded
+    fit (gprx_dist.cpp: int32 ntasks, rank, g, nc; int4 per ticket; 4 int64 per ticket: taken,
+    inputs ready, published, workgroup, 100 MHz ticks).  DIAGX(k) is ticket type 0 with k in
+    field 1.  chain_step_us: median of publish(k) - publish(k-1) over the consecutive steps this
+    rank owns both of (one rank's clock); exec_us: DIAGX's mean duration."""
+    raw = open(path, "rb").read()
+    nt, r, g, nc = (int(v) for v in np.frombuffer(raw[:16], np.int32))
+    tasks = np.frombuffer(raw[16:16 + 16 * nt], np.int32).reshape(nt, 4)
+    times = np.frombuffer(raw[16 + 16 * nt:16 + 48 * nt], np.int64).reshape(nt, 4)
+    sel = (tasks[:, 0] & 0xff) == 0
+    ks, pub, ready = tasks[sel, 1], times[sel, 2], times[sel, 1]
+    o = np.argsort(ks)
+    ks, pub, ready = ks[o], pub[o], ready[o]
+    cons = np.where(np.diff(ks) == 1)[0]
+    steps = (pub[cons + 1] - pub[cons]) / 100.0
+    span = (times[:, 2].max() - times[:, 0].min()) / 100.0
+    return {"diag_steps_owned": int(len(ks)), "chain_step_us_median": float(np.median(steps)) if len(steps) else None,
+            "chain_step_us_mean": float(np.mean(steps)) if len(steps) else None, "consecutive_pairs": int(len(steps)),
+            "diagx_exec_us_mean": float(np.mean((pub - ready) / 100.0)) if len(ks) else None,
+            "launch_span_us": float(span), "tickets": int(nt)}
+
+
+def dist_rank_record(ctx, model, transport):
+    """This rank's identity and exchange figures for the N > 1 line: the device (ordinal and PCI
+    address), the transport, the RCCL communicator's own rank count, the Linv / tile pushes of
+    one fit and their bytes (from the schedule, gprx_dev_dist_info), and the chain step measured
+    on a traced fit."""
+    rec = dict(ctx.info())
+    rec["transport_bench"] = transport
+    di = model.dist_info()
+    rec.update({k: di[k] for k in ("push_linv", "push_tiles", "push_bytes", "gb", "ww", "P", "est_us",
+                                   "bytes_rank", "bytes_storage")})
+    base = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"gprx_chain_{os.getpid()}")
+    os.environ["GPRX_DIST_TRACE_FILE"] = base
+    try:
+        info = model.fit(gpr_amd_fit_flag())
+        rec["traced_fit_ms_factor"] = float(info.ms_factor)
+    finally:
+        del os.environ["GPRX_DIST_TRACE_FILE"]
+    path = f"{base}.r{rec['rank']}"
+    try:
+        rec.update(chain_from_trace(path))
+    finally:
+        for f in glob.glob(base + ".r*"):
+            os.remove(f)
+    return rec
+
+
+def gpr_amd_fit_flag():
+    from gpr_amd.gprx import FIT_DISTRIBUTED
+    return FIT_DISTRIBUTED
+
+
 class _Skip(Exception):
     """A leg left out by --legs."""
 
@@ -319,13 +410,19 @@ def run_configs(args, world, rank, local_rank, dctx, max_over_ranks, barrier_syn
                                                          c2["roofline"]["avg_launch_us"])
         if rank == 0 and world == 1 and args.cpu_n > 0:
             from oracle import oracle as O
+            _cpu_warmup(O, C2)
             X, Y = make_data(n, C2["d"], m)
-            t0 = time.perf_counter()
-            O.fit(C2["kernel"], X, Y, C2["sigma"], np.float64, want_core=False)
-            dt = time.perf_counter() - t0
-            c2["cpu_baseline"] = {"value": 1.0 / dt, "unit": "fits/s", "cores": O.num_threads(), "kind": "port",
-                                  "sample": f"1 full fit at N={n} (oracle: kernel loop + LAPACK {O.lapack_name()} "
-                                            f"getrf+getri in fp64 + C Y) in {dt:.2f} s"}
+            dts = []
+            for _ in range(3):  # the median of three full fits (one cold sample swung 7x between boxes)
+                t0 = time.perf_counter()
+                O.fit(C2["kernel"], X, Y, C2["sigma"], np.float64, want_core=False)
+                dts.append(time.perf_counter() - t0)
+            dt = float(np.median(dts))
+            c2["cpu_baseline"] = dict({"value": 1.0 / dt, "unit": "fits/s", "cores": O.num_threads(), "kind": "port",
+                                       "samples_s": dts,
+                                       "sample": f"median of 3 full fits at N={n} after a warm-up (oracle: kernel loop + "
+                                                 f"LAPACK {O.lapack_name()} getrf+getri in fp64 + C Y): {dt:.3f} s"},
+                                      **host_info())
         out["C2"] = c2
     except _Skip:
         pass
@@ -368,16 +465,17 @@ def run_configs(args, world, rank, local_rank, dctx, max_over_ranks, barrier_syn
             c4["roofline"]["mfma_busy"] = mfma_from_profile("c4", ("potrf_tiles_kernel<float, false>",))
         if rank == 0 and world == 1 and args.cpu_n > 0:
             from oracle import oracle as O
+            _cpu_warmup(O, C4)
             ns = 8192
             X, Y = make_data(ns, C4["d"], m)
             t0 = time.perf_counter()
             O.fit(C4["kernel"], X.astype(np.float32), Y.astype(np.float32), C4["sigma"], np.float32, want_core=False)
             dt = time.perf_counter() - t0
-            c4["cpu_baseline"] = {"value": 1.0 / (dt * (n / ns) ** 3), "unit": "fits/s", "cores": O.num_threads(),
-                                  "kind": "port", "extrapolated": True,
-                                  "sample": f"1 fit at N={ns} (oracle fp32 path: K in fp32 cast to double, LAPACK "
-                                            f"{O.lapack_name()} getrf+getri) in {dt:.2f} s, EXTRAPOLATED cubically "
-                                            f"to N={n}"}
+            c4["cpu_baseline"] = dict({"value": 1.0 / (dt * (n / ns) ** 3), "unit": "fits/s", "cores": O.num_threads(),
+                                       "kind": "port", "extrapolated": True,
+                                       "sample": f"1 fit at N={ns} after a warm-up (oracle fp32 path: K in fp32 cast to "
+                                                 f"double, LAPACK {O.lapack_name()} getrf+getri) in {dt:.2f} s, "
+                                                 f"EXTRAPOLATED cubically to N={n}"}, **host_info())
         out["C4"] = c4
     except _Skip:
         pass
@@ -458,20 +556,87 @@ def run_configs(args, world, rank, local_rank, dctx, max_over_ranks, barrier_syn
         if rank == 0 and world == 1 and args.cpu_n > 0:
             from oracle import oracle as O
             ns = 62500
+            O.sparse_fit(ks, Xl[:4096], Yl[:4096], Xm, sig, jit)  # (untimed warm-up)
             t0 = time.perf_counter()
             O.sparse_fit(ks, Xl[:ns], Yl[:ns], Xm, sig, jit)
             dt = time.perf_counter() - t0
-            c5["cpu_baseline"] = {"value": 1.0 / (dt * n / ns), "unit": "fits/s", "cores": O.num_threads(),
-                                  "kind": "port", "extrapolated": True,
-                                  "sample": f"1 sparse fit on the first {ns} rows (oracle: Knm build + Knm^T Knm + "
-                                            f"M x M LAPACK inverses) in {dt:.2f} s, scaled LINEARLY in N to {n} rows "
-                                            "(the M x M part counted 16x: an overestimate of the CPU rate's cost)"}
+            c5["cpu_baseline"] = dict({"value": 1.0 / (dt * n / ns), "unit": "fits/s", "cores": O.num_threads(),
+                                       "kind": "port", "extrapolated": True,
+                                       "sample": f"1 sparse fit on the first {ns} rows after a warm-up (oracle: Knm build + "
+                                                 f"Knm^T Knm + M x M LAPACK inverses) in {dt:.2f} s, scaled LINEARLY in N "
+                                                 f"to {n} rows (the M x M part counted 16x: an overestimate of the CPU "
+                                                 "rate's cost)"}, **host_info())
         out["C5"] = c5
     except _Skip:
         pass
     except Exception as e:
         out["C5"] = {"error": repr(e)}
     return out
+
+
+def spawn_ranks(n, argv):
+    """`bench.py --gpus N` with no launcher around it (WORLD_SIZE unset): start the N ranks here,
+    one child process per GPU, each with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT
+    set and the same arguments -- what torch.distributed.run would do -- before this process
+    touches the GPU (it never does: no library is loaded here, and nothing is re-executed in
+    place).  Rank 0's stdout (the JSON line) is relayed; the other ranks' stdout goes to stderr.
+    Returns the exit status: non-zero when any rank fails, when rank 0 printed no JSON line, or
+    after GPRX_BENCH_TIMEOUT_S (default 3000 s), the remaining ranks then being killed (their own
+    PIDs)."""
+    import signal
+    import socket
+    import subprocess
+    import threading
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = []
+    lines = []
+
+    def relay(stream):
+        for ln in stream:
+            sys.stdout.write(ln)
+            sys.stdout.flush()
+            if ln.startswith("{"):
+                lines.append(ln)
+
+    def kill_all(*_):
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+
+    signal.signal(signal.SIGTERM, lambda *a: (kill_all(), sys.exit(143)))
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), GPRX_BENCH_SPAWNED="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr.fileno(), text=True))
+    th = threading.Thread(target=relay, args=(procs[0].stdout,), daemon=True)
+    th.start()
+    deadline = time.monotonic() + float(os.environ.get("GPRX_BENCH_TIMEOUT_S", "3000"))
+    rc = 0
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+        if bad:
+            log(f"bench.py: rank {bad[0][0]} exited with {bad[0][1]}; stopping the other ranks")
+            rc = bad[0][1] if bad[0][1] > 0 else 1
+            break
+        if all(c == 0 for c in codes):
+            break
+        if time.monotonic() > deadline:
+            log("bench.py: ranks still running at GPRX_BENCH_TIMEOUT_S; stopping them")
+            rc = 124
+            break
+        time.sleep(0.2)
+    kill_all()
+    for p in procs:
+        p.wait()
+    th.join(timeout=10)
+    if rc == 0 and not lines:
+        log("bench.py: rank 0 printed no JSON line")
+        rc = 1
+    return rc
 
 
 def main():
@@ -490,7 +655,7 @@ def main():
                                                         "(BASELINE.json configs[2]); 0 = skip")
     ap.add_argument("--build-iters", type=int, default=3, help="time the covariance build alone (0 = skip)")
     ap.add_argument("--cpu-n", type=int, default=16384, help="N of the CPU-baseline sample (0 = skip)")
-    ap.add_argument("--cpu-lml-ns", default="1024,2048,4096",
+    ap.add_argument("--cpu-lml-ns", default="2048,4096,8192",
                     help="sizes of the CPU LML + gradient baseline, extrapolated cubically to N ('' = skip)")
     ap.add_argument("--cpu-predict-q", type=int, default=4096, help="queries of the CPU predict baseline (0 = skip)")
     ap.add_argument("--mode", choices=["replicas", "dist"], default="dist",
@@ -513,6 +678,14 @@ def main():
     def want(leg):
         return legs is None or leg in legs
 
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        # no launcher: start the N ranks ourselves
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+    if env_world is not None and int(env_world) != args.gpus:
+        sys.exit(f"bench.py: WORLD_SIZE={env_world} from the launcher but --gpus {args.gpus}: they must agree")
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -581,6 +754,12 @@ def main():
             dmodel = make_model(dctx)
             el, infos, st = timed_fits(dmodel, dctx, gpr_amd.gprx.FIT_DISTRIBUTED)
             dres = {"elapsed": el, "infos": infos}
+            # per-rank evidence for reading a scaling curve: after the timed
+            # fits, one more traced fit (untimed) for the measured chain step
+            try:
+                dres["rank_rec"] = dist_rank_record(dctx, dmodel, transport)
+            except Exception as e:
+                dres["rank_rec"] = {"rank": rank, "error": repr(e)}
             if args.dist_lml:  # LML + gradient on the sharded factor (row-block partials, one all-reduce)
                 dmodel.lml(grad=True, distributed=True)
                 barrier_sync()
@@ -784,6 +963,18 @@ def main():
     traffic = traffic_from_profile() if not headline_dist else None
     fit_ms = float(np.median([i.ms_build + i.ms_factor + i.ms_solve for i in infos])) if infos else None
 
+    # every rank's identity and exchange figures (rank 0 prints them): ranks_seen counts the
+    # ranks that answered this all-gather, distinct_devices their distinct PCI addresses
+    ranks_rec = None
+    if world > 1 and dist is not None:
+        mine = (dres or {}).get("rank_rec")
+        if mine is None:
+            try:
+                mine = dict(ctx.info())
+                mine["note"] = "replicas context (no sharded fit)"
+            except Exception as e:
+                mine = {"rank": rank, "error": repr(e)}
+        ranks_rec = [json.loads(b.decode()) for b in dist.allgather(json.dumps(mine).encode())]
     configs = None
     if args.configs:
         # (the ranks agree whether the sharded fit ran everywhere before the sharded configs use it)
@@ -842,6 +1033,14 @@ def main():
             "replicas": replicas if world > 1 else None,
             "dist_error": dist_error,
             "dist_transport": transport,
+            # N > 1: how many ranks took part, on how many GPUs, and per rank its device, transport,
+            # pushes per fit and the measured diagonal-chain step
+            "ranks_seen": (len({r_.get("rank") for r_ in ranks_rec}) if ranks_rec else world),
+            "rccl_ranks_seen": (max((r_.get("rccl_count", -1) for r_ in ranks_rec), default=-1) if ranks_rec else None),
+            "distinct_devices": (len({r_.get("pci") for r_ in ranks_rec if r_.get("pci")}) if ranks_rec else 1),
+            "launcher": ("bench.py spawn" if os.environ.get("GPRX_BENCH_SPAWNED") else
+                         ("external (WORLD_SIZE)" if os.environ.get("WORLD_SIZE") else "none (one process)")),
+            "ranks": ranks_rec,
             # the HIP runtime, HSA runtime and RCCL this process mapped (one copy each)
             "runtime": gpr_amd.runtime_info(),
             "phases": phases,

@@ -303,7 +303,16 @@ struct gprx_model {
     // posterior covariance workspace (L^{-1} K(X, x) for a query batch: qp x np each), kept
     // across calls -- at Q = 65536, N = 16384 one buffer is 8.6 GB, whose hipMalloc + free per
     // call cost more than the solve on some boxes
-    DevBuf pvRa, pvRb;
+    DevBuf pvRa, pvRb, pvFq;  // (+ the queries' pair features)
+    // a refit, an LML call or new data frees that workspace when it is large (one
+    // big variance call must not leave too little HBM for the next fit on the device)
+    void trim_posterior_workspace() {
+        if (pvRa.bytes + pvRb.bytes + pvFq.bytes > (size_t(1) << 30)) {
+            pvRa.release();
+            pvRb.release();
+            pvFq.release();
+        }
+    }
     DevParam kfit;     // the fit's kernel tree (uploaded when it changes)
     PinnedBuf hstat;   // the fit's status words: flag, info, log det, data fit
     // fp32 models: fp64 iterative refinement state (k_refine.hip).  kd then holds the tree in
@@ -819,6 +828,7 @@ static gprx_status model_fit(gprx_model* M, uint32_t flags, gprx_fit_info* out) 
     GPRX_REQUIRE(M->has_data, GPRX_ERR_STATE, "GaussianProcess::Initialize: no input samples defined during initialization");
     GPRX_REQUIRE(M->has_kernel, GPRX_ERR_STATE, "gprx: no kernel set");
     GPRX_HIP(hipSetDevice(ctx->device));
+    M->trim_posterior_workspace();
     hipStream_t s = ctx->stream;
     const KCanon<T>& K = kcanon<T>(M);
     // multi-GPU factorisation: an RCCL context with world > 1, a virtual-rank context, or
@@ -1046,24 +1056,31 @@ static gprx_status model_predict(gprx_model* M, const void* Xq, int64_t q, void*
 // R = K(Xq, X) (qp x np, ld qp, zero padding), then R L^{-T} in place.  K(Xq, X) as MFMA pair
 // statistics (kcross_mma_kernel: the predict path's features of the queries and of the training
 // set) when the tree allows it -- 23 ms -> ~4 ms of the 300 ms variance leg at Q = 65536 against
-// the VALU kernel (GPRX_PREDICT=direct keeps that one)
+// the VALU kernel (GPRX_PREDICT=direct keeps that one).  fp64 only: the variance k(x,x) -
+// |L^{-1} k_x|^2 is a cancelling difference, and in fp32 the expanded |u|^2 + |v|^2 - 2 u.v
+// statistic loses ~eps (|x - c|/l)^2 per entry, which L^{-1} amplifies; fp32 models
+// keep the exact-difference VALU build.  feat_ready: the training features are already in
+// featV (the second side of a pair call).
 template <typename T>
-static void solve_rows_for(gprx_model* M, const T* dXq, const T* dtabQ, int64_t q, int64_t qp, T* R) {
+static void solve_rows_for(gprx_model* M, const T* dXq, const T* dtabQ, int64_t q, int64_t qp, T* R,
+                           bool feat_ready = false) {
     hipStream_t s = M->ctx->stream;
     const KCanon<T>& K = kcanon<T>(M);
     GPRX_HIP(hipMemsetAsync(R, 0, sizeof(T) * qp * M->np, s));
     static const bool direct = std::getenv("GPRX_PREDICT") && std::string(std::getenv("GPRX_PREDICT")) == "direct";
     const int64_t npf = round_up(M->n, GT);
-    if (!direct && pairs_mma_supported<T>(K, 1) && npf <= M->np) {
+    if (std::is_same<T, double>::value && !direct && pairs_mma_supported<T>(K, 1) && npf <= M->np) {
         const int d = M->d;
         const int64_t kf = pairs_feature_cols<T>(K, d);
-        DevBuf fq;
-        fq.ensure(sizeof(T) * qp * kf);
-        M->featV.ensure(sizeof(T) * npf * kf);
-        launch_pair_features<T>(K, M->X.as<T>(), M->n, d, M->X.as<T>(), true, M->featV.as<T>(), npf, s);
-        launch_pair_features<T>(K, dXq, q, d, M->X.as<T>(), false, fq.as<T>(), qp, s);
+        M->pvFq.ensure(sizeof(T) * qp * kf);  // (model-owned: no hipMalloc + hipFree per call)
+        if (!feat_ready) {
+            M->featV.ensure(sizeof(T) * npf * kf);
+            launch_pair_features<T>(K, M->X.as<T>(), M->n, d, M->X.as<T>(), true, M->featV.as<T>(), npf, s);
+        }
+        launch_pair_features<T>(K, dXq, q, d, M->X.as<T>(), false, M->pvFq.as<T>(), qp, s);
         const KCanon<T>* kdev = M->kfit.put(K, s);
-        launch_kcross_mma<T>(K, kdev, fq.as<T>(), qp, q, M->featV.as<T>(), npf, M->n, d, R, qp, M->flag.as<int>(), s);
+        launch_kcross_mma<T>(K, kdev, M->pvFq.as<T>(), qp, q, M->featV.as<T>(), npf, M->n, d, R, qp,
+                             M->flag.as<int>(), s);
     } else {
         launch_kbuild<T>(K, dXq, dtabQ, q, M->X.as<T>(), M->tab.as<T>(), M->n, M->d, R, qp, 0, false, T(0),
                          M->flag.as<int>(), s);
@@ -1269,7 +1286,7 @@ static gprx_status model_posterior_cov(gprx_model* M, const void* Xa, const void
         ProfScope ps_(KC_POSTERIOR, s, (same ? 1.0 : 2.0) * (double)q * (double)M->np * (double)M->np);
         T* Ra_ = M->pvRa.as<T>();
         solve_rows_for<T>(M, da.as<T>(), ta.as<T>(), q, qp, Ra_);
-        if (!same) solve_rows_for<T>(M, db.as<T>(), tb.as<T>(), q, qp, M->pvRb.as<T>());
+        if (!same) solve_rows_for<T>(M, db.as<T>(), tb.as<T>(), q, qp, M->pvRb.as<T>(), true);
         launch_pair_kernel<T>(K, da.as<T>(), db.as<T>(), q, d, kab.as<T>(), s);
         launch_rowdot<T>(Ra_, same ? Ra_ : M->pvRb.as<T>(), qp, q, M->np, kab.as<T>(), res.as<T>(), s);
     }
@@ -2285,8 +2302,10 @@ gprx_status gprx_model_set_data(gprx_model* M, const void* X, const void* Y, int
     const size_t es = esize(M->dt);
     M->X.ensure(es * n * d);
     M->Y.ensure(es * n * m);
-    GPRX_HIP(hipMemcpy(M->X.p, X, es * n * d, hipMemcpyHostToDevice));
-    GPRX_HIP(hipMemcpy(M->Y.p, Y, es * n * m, hipMemcpyHostToDevice));
+    M->trim_posterior_workspace();
+    // host or device memory (include/gprx.h conventions: a gprx_device_alloc pointer too)
+    GPRX_HIP(hipMemcpy(M->X.p, X, es * n * d, hipMemcpyDefault));
+    GPRX_HIP(hipMemcpy(M->Y.p, Y, es * n * m, hipMemcpyDefault));
     M->n = n;
     M->d = d;
     M->m = m;
@@ -2721,13 +2740,33 @@ gprx_status gprx_dev_dist_info(gprx_model* M, int64_t* out, int32_t nout) {
     GPRX_REQUIRE(M->dist_fitted || M->dist_stats.bytes_rank > 0, GPRX_ERR_STATE,
                  "gprx_dev_dist_info: no distributed fit on this model");
     const DistFitOut& o = M->dist_stats;
-    const int64_t v[11] = {o.bytes_rank, o.bytes_storage, o.gb, o.ww, o.chunk_w, o.P, (int64_t)o.est_us,
+    const int64_t v[15] = {o.bytes_rank, o.bytes_storage, o.gb, o.ww, o.chunk_w, o.P, (int64_t)o.est_us,
                            M->ctx->world, M->dist_dense ? 1 : 0,
                            M->dist_engine ? dist_pvar_chunks(M->dist_engine) : 0,
-                           M->dist_engine ? dist_pvar_bytes(M->dist_engine) : 0};
-    for (int i = 0; i < std::min<int32_t>(nout, 11); i++) out[i] = v[i];
+                           M->dist_engine ? dist_pvar_bytes(M->dist_engine) : 0,
+                           o.push_linv, o.push_tiles, o.push_bytes, o.push_rank};
+    for (int i = 0; i < std::min<int32_t>(nout, 15); i++) out[i] = v[i];
     return GPRX_OK;
     API_END(M ? M->ctx : nullptr)
+}
+
+gprx_status gprx_dev_ctx_info(gprx_ctx* ctx, int64_t* out, int32_t nout) {
+    API_BEGIN
+    GPRX_REQUIRE(ctx && out, GPRX_ERR_ARG, "gprx_dev_ctx_info: NULL argument");
+    int count = -1, urank = -1;
+    if (ctx->comm) {
+        if (ncclCommCount(ctx->comm, &count) != ncclSuccess) count = -1;
+        if (ncclCommUserRank(ctx->comm, &urank) != ncclSuccess) urank = -1;
+    }
+    int dom = -1, bus = -1, dev = -1;
+    (void)hipDeviceGetAttribute(&dom, hipDeviceAttributePciDomainID, ctx->device);
+    (void)hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, ctx->device);
+    (void)hipDeviceGetAttribute(&dev, hipDeviceAttributePciDeviceId, ctx->device);
+    const int64_t transport = ctx->virt ? 3 : (ctx->comm ? 1 : (ctx->peer ? 2 : 0));
+    const int64_t v[10] = {ctx->rank, ctx->world, ctx->device, transport, count, urank, dom, bus, dev, ctx->cu_slot};
+    for (int i = 0; i < std::min<int32_t>(nout, 10); i++) out[i] = v[i];
+    return GPRX_OK;
+    API_END(ctx)
 }
 
 gprx_status gprx_dist_unique_id(void* out) {

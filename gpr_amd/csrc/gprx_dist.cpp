@@ -1047,6 +1047,21 @@ void dist_fit(DistEngineBase*& eng, const DistContext& C, const DistFitIn<T>& in
     out.ms_kernel = 0;
     out.bytes_rank = 0;
     out.bytes_storage = 0;
+    {  // the pushes of this process's first rank, from the layout and the schedule's consumers
+        const int r0 = E.ranks.front()->r;
+        int64_t nl = 0, nt = 0;
+        for (int i = 0; i < nc; i++) {
+            if (E.L.own[i] != r0) continue;
+            nl += E.g - 1;  // Linv_i to every peer
+            int peers = 0;
+            for (int q = 0; q < E.g; q++) peers += (q != r0 && E.S.cons[(size_t)q * nr + i]) ? 1 : 0;
+            nt += (int64_t)peers * i;  // the final tiles L_ib, b < i
+        }
+        out.push_rank = r0;
+        out.push_linv = nl;
+        out.push_tiles = nt;
+        out.push_bytes = (nl + nt) * (int64_t)DB * DB * (int64_t)sizeof(T);
+    }
     for (auto& Rp : E.ranks) {
         float ms = 0;
         if (hipEventElapsedTime(&ms, Rp->t0, Rp->t1) == hipSuccess) out.ms_kernel = std::max(out.ms_kernel, (double)ms);

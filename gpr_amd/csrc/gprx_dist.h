@@ -59,6 +59,10 @@ struct DistFitOut {
     int gb = 1, ww = 0, chunk_w = 0;     // the layout and window the schedule picked
     int64_t bytes_rank = 0;              // device bytes the engine holds per rank (max over this process's ranks)
     int64_t bytes_storage = 0;           // of which the packed own rows
+    // this process's (first) rank's pushes per fit, from the schedule: Linv_k to every peer, final
+    // tiles to the peers that read their row through the window (gprx_dev_dist_info out[11..14])
+    int64_t push_linv = 0, push_tiles = 0, push_bytes = 0;
+    int push_rank = 0;
 };
 
 struct DistEngineBase;

@@ -122,6 +122,7 @@ def lib():
         L.gprx_ctx_create_peer.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ALLGATHER_FN, ctypes.c_void_p,
                                            ctypes.POINTER(ctypes.c_void_p)]
         L.gprx_dev_dist_info.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64), ctypes.c_int32]
+        L.gprx_dev_ctx_info.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64), ctypes.c_int32]
         L.gprx_ctx_destroy.argtypes = [ctypes.c_void_p]
         L.gprx_model_create.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
         L.gprx_model_destroy.argtypes = [ctypes.c_void_p]
@@ -379,6 +380,18 @@ class Context:
             _check(lib().gprx_ctx_create_dist(device, rank, world, buf, ctypes.byref(h)))
         self.h = h
 
+    TRANSPORTS = {0: "single", 1: "rccl", 2: "peer", 3: "virtual"}
+
+    def info(self):
+        """Identity of this context (gprx_dev_ctx_info, local): rank, world, HIP device, transport,
+        the RCCL communicator's own rank count and rank (ncclCommCount / ncclCommUserRank, -1 with
+        no communicator), the device's PCI domain:bus:device and the shared-GPU CU share."""
+        v = (ctypes.c_int64 * 10)()
+        _check(lib().gprx_dev_ctx_info(self.h, v, 10))
+        v = list(v)
+        return {"rank": v[0], "world": v[1], "device": v[2], "transport": self.TRANSPORTS.get(v[3], str(v[3])),
+                "rccl_count": v[4], "rccl_rank": v[5], "pci": f"{v[6]:04x}:{v[7]:02x}:{v[8]:02x}", "cu_slot": v[9]}
+
     def close(self):
         if self.h:
             lib().gprx_ctx_destroy(self.h)
@@ -584,7 +597,7 @@ class Model:
         bytes of the engine and of the packed storage, row-block group, window panels, update
         chunk width, workgroups per rank, simulated makespan (us)."""
         keys = ["bytes_rank", "bytes_storage", "gb", "ww", "chunk_w", "P", "est_us", "world", "dense_factor",
-                "posterior_chunks", "posterior_bytes_rank"]
+                "posterior_chunks", "posterior_bytes_rank", "push_linv", "push_tiles", "push_bytes", "push_rank"]
         v = (ctypes.c_int64 * len(keys))()
         self._c(lib().gprx_dev_dist_info(self.h, v, len(keys)))
         return dict(zip(keys, list(v)))

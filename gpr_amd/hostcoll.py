@@ -15,11 +15,18 @@ Star topology through rank 0 over TCP on the loopback (one node, as the bench co
 the data path of the sharded fit never goes through it (device-initiated IPC stores over xGMI,
 DESIGN.md section 6).
 
-Rendezvous: under torch.distributed.run every rank has the launcher's agent as its parent and
-the same MASTER_PORT (which that agent's own store occupies).  Rank 0 listens on an ephemeral
-port and publishes it in /tmp/gprx_coll_<parent pid>_<MASTER_PORT>_<restart>.port; the other
-ranks wait for that file.  GPRX_COLL_PORT fixes the port instead (rank 0 binds it, the others
-connect to it).
+Rendezvous: under torch.distributed.run (or bench.py's own spawner) every rank has the
+launcher as its parent and the same MASTER_PORT (which a torch launcher's own store occupies).
+Rank 0 listens on an ephemeral port of the loopback and publishes "<port> <token>" in
+/tmp/gprx_coll_<parent pid>_<MASTER_PORT>_<restart>.port (mode 0600); the other ranks wait for
+that file.  GPRX_COLL_PORT fixes the port instead (rank 0 binds it, the others connect to it; the
+token is then GPRX_COLL_TOKEN, empty by default).  The group binds 127.0.0.1 (one node, the
+bench contract) unless GPRX_COLL_ADDR names another address.
+
+Admission: a connecting rank announces its rank and the launch's token; rank 0 drops (closes and
+keeps waiting past) a connection with a wrong token, a rank outside 1..world-1, a rank that has
+already joined, or no announcement within 10 s -- a stray connection cannot take a rank's slot or
+hang the group.  This socket carries the IPC handles the peer context bootstraps with.
 """
 import os
 import socket
@@ -54,7 +61,8 @@ def _recv(sock):
 class SocketGroup:
     """`world` processes on one host; rank 0 is the hub."""
 
-    def __init__(self, rank, world, addr="127.0.0.1", port=None, port_file=None, timeout=300.0, op_timeout=None):
+    def __init__(self, rank, world, addr="127.0.0.1", port=None, port_file=None, timeout=300.0, op_timeout=None,
+                 token=None):
         if world < 1 or not (0 <= rank < world):
             raise ValueError("SocketGroup: need 0 <= rank < world")
         self.rank, self.world = rank, world
@@ -67,15 +75,19 @@ class SocketGroup:
         if world == 1:
             return
         deadline = time.monotonic() + timeout
+        if token is None:  # (a fixed port: the caller's token; a port file: one per launch, below)
+            token = os.environ.get("GPRX_COLL_TOKEN", "") if (port is not None or not port_file) else None
         if rank == 0:
+            if token is None:
+                token = os.urandom(16).hex()
             srv = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
             srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
             srv.bind((addr, int(port) if port else 0))
             srv.listen(world)
             if port_file:
                 fd, tmp = tempfile.mkstemp(dir=os.path.dirname(port_file) or ".")
-                with os.fdopen(fd, "w") as f:
-                    f.write(str(srv.getsockname()[1]))
+                with os.fdopen(fd, "w") as f:  # (mkstemp: mode 0600)
+                    f.write(f"{srv.getsockname()[1]} {token}")
                 os.replace(tmp, port_file)
                 self._port_file = port_file
             try:
@@ -87,8 +99,11 @@ class SocketGroup:
                         raise TimeoutError(f"gpr_amd.hostcoll: {len(self._conns) + 1} of {world} ranks arrived "
                                            f"within {timeout:.0f} s")
                     c.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+                    r = self._admit(c, token)
+                    if r is None:
+                        c.close()
+                        continue
                     c.settimeout(op_timeout)
-                    (r,) = struct.unpack("<i", _recv_exact(c, 4))
                     self._conns[r] = c
             finally:
                 srv.close()
@@ -103,10 +118,10 @@ class SocketGroup:
                 try:
                     if port is None:
                         with open(port_file) as f:
-                            txt = f.read().strip()
-                        if not txt:
+                            txt = f.read().split()
+                        if len(txt) != 2:
                             raise FileNotFoundError(port_file)
-                        p = int(txt)
+                        p, token = int(txt[0]), txt[1]
                     else:
                         p = int(port)
                     s = socket.create_connection((addr, p), timeout=5.0)
@@ -118,8 +133,23 @@ class SocketGroup:
                     time.sleep(0.05)
             s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
             s.settimeout(op_timeout)
-            s.sendall(struct.pack("<i", rank))
+            tok = (token or "").encode()
+            s.sendall(struct.pack("<ii", rank, len(tok)) + tok)
             self._sock = s
+
+    def _admit(self, c, token):
+        """The announced rank of a new connection, or None to drop it (see the module notes)."""
+        try:
+            c.settimeout(10.0)
+            r, nt = struct.unpack("<ii", _recv_exact(c, 8))
+            if not (0 <= nt <= 256):
+                return None
+            tok = _recv_exact(c, nt).decode(errors="replace") if nt else ""
+        except (OSError, ConnectionError, struct.error):
+            return None
+        if tok != (token or "") or not (1 <= r < self.world) or r in self._conns:
+            return None
+        return r
 
     @classmethod
     def from_env(cls, timeout=300.0):
@@ -127,7 +157,7 @@ class SocketGroup:
         or of any launcher that sets them; GPRX_COLL_PORT overrides the rendezvous file."""
         rank = int(os.environ.get("RANK", "0"))
         world = int(os.environ.get("WORLD_SIZE", "1"))
-        addr = os.environ.get("MASTER_ADDR", "127.0.0.1")
+        addr = os.environ.get("GPRX_COLL_ADDR", "127.0.0.1")
         port = os.environ.get("GPRX_COLL_PORT")
         port_file = None
         if port is None:

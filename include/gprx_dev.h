@@ -81,6 +81,18 @@ gprx_status gprx_ctx_create_virtual(int device, int world, gprx_ctx** out);
  * on this layout), out[10] device bytes of the last sharded posterior solve's K(Z, X_own)
  * workspace per rank (its queries x this rank's own rows only). */
 gprx_status gprx_dev_dist_info(gprx_model* model, int64_t* out, int32_t nout);
+/* (round 6) out[11..13] of gprx_dev_dist_info: this process's rank's pushes per fit, from the
+ * schedule of the last distributed fit -- out[11] Linv_k pushes (each own diagonal block to every
+ * peer), out[12] final-tile pushes (each own tile L_ib, b < nc, to every peer that reads row i
+ * through its window), out[13] their bytes; out[14] the rank these describe. */
+/* Identity of a context, written to the first min(nout, 10) slots of out: out[0] rank, out[1]
+ * world, out[2] HIP device ordinal, out[3] transport (0 single GPU, 1 RCCL, 2 peer context over
+ * the caller's all-gather, 3 virtual ranks), out[4] ranks the RCCL communicator holds
+ * (ncclCommCount; -1 when there is none), out[5] the rank RCCL assigned (ncclCommUserRank; -1),
+ * out[6..8] the device's PCI domain, bus and device numbers (distinct GPUs have distinct
+ * triples), out[9] the CU share index of a shared-GPU rehearsal (GPRX_DIST_SHARED_GPU; else 0).
+ * Local: no collective. */
+gprx_status gprx_dev_ctx_info(gprx_ctx* ctx, int64_t* out, int32_t nout);
 /* Parity hook for the tile engine's diagonal-block factor: the 128 x 128 SPD block A (column-
  * major, host) factored by variant 0 (rank-8 register image), 1 (blocked) or 2 (blocked with
  * look-ahead): L (lower triangle meaningful, the upper keeps A), Linv = L^{-1} (column-major)

@@ -147,6 +147,31 @@ for step in "$@"; do
         done
         for f in "$O"/envab_*.json; do echo "$(basename "$f")"; python scripts/bench_brief.py "$f" | head -4; done
         ;;
+    predpmc)  # the predict kernel's issue split: two SQ passes
+        (timeout -k 10 60 rocprofv3 -L > "$O/counters_list.txt" 2>&1) || true
+        pmc_leg predict pmcp1_predict SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS \
+            SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE
+        pmc_leg predict pmcp2_predict SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_IDX_ACTIVE \
+            SQ_VALU_MFMA_COEXEC_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE
+        pmc_leg predict pmcp3_predict SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 \
+            SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_MFMA_F64 SQ_INSTS_VALU_CVT SQ_INSTS_SALU GRBM_GUI_ACTIVE
+        python scripts/pmc_generic.py "$O/predict_pmc.json" "$O/pmcp1_predict" "$O/pmcp2_predict" "$O/pmcp3_predict" \
+            --kernel predict
+        ;;
+    predmix)  # the instruction mix alone (one pass)
+        pmc_leg predict pmcp3_predict SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 \
+            SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_MFMA_F64 SQ_INSTS_VALU_CVT SQ_INSTS_SALU GRBM_GUI_ACTIVE
+        python scripts/pmc_generic.py "$O/predict_mix.json" "$O/pmcp3_predict" --kernel predict
+        ;;
+    lmlpmc)  # the LML leg's kernels: MFMA busy and the wait split
+        pmc_leg lml pmcl1_lml SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES \
+            SQ_BUSY_CYCLES GRBM_GUI_ACTIVE
+        python scripts/pmc_generic.py "$O/lml_pmc.json" "$O/pmcl1_lml"
+        ;;
+    fittrace)  # the C3 fit's tile timeline (fused build), for the launch decomposition
+        PT_TRACE_FIT=1 PT_TRACE_OUT="$O/pt_fit16384.npz" timeout -k 10 120 python scripts/pt_trace.py 16384 \
+            > "$O/pt_fit16384.json" 2> "$O/pt_fit16384.err" || fail fittrace $? "$O/pt_fit16384.err"
+        ;;
     *)
         echo "unknown step $step"; exit 2 ;;
     esac

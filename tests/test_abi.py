@@ -120,3 +120,58 @@ def test_hostcoll_socket_group(tmp_path):
                               stderr=subprocess.STDOUT, text=True) for r in range(3)]
     outs = [p.communicate(timeout=120)[0] for p in procs]
     assert all(p.returncode == 0 for p in procs), outs
+
+
+def test_hostcoll_admission_drops_strays():
+    """Rank 0 of a SocketGroup drops connections that announce a wrong token, a rank outside
+    1..world-1, a rank that already joined, or nothing at all, and keeps waiting for the real
+    ranks (a stray connection must not take a slot or hang the group)."""
+    import socket
+    import struct
+    import threading
+    from gpr_amd.hostcoll import SocketGroup
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    res = {}
+
+    def hub():
+        g = SocketGroup(0, 3, port=port, timeout=60, token="tok")
+        res["parts"] = g.allgather(b"zero")
+        g.close()
+
+    th = threading.Thread(target=hub)
+    th.start()
+
+    def stray(rank, tok, announce=True):
+        import time
+        for _ in range(200):
+            try:
+                s = socket.create_connection(("127.0.0.1", port), timeout=5)
+                break
+            except OSError:
+                time.sleep(0.02)
+        if announce:
+            t = tok.encode()
+            s.sendall(struct.pack("<ii", rank, len(t)) + t)
+        return s
+
+    strays = [stray(1, "bad"), stray(7, "tok"), stray(-1, "tok"), stray(0, "tok")]
+    r1 = SocketGroup(1, 3, port=port, timeout=60, token="tok")
+    strays.append(stray(1, "tok"))  # a duplicate of a rank that has joined
+    r2 = {}
+
+    def join2():
+        g = SocketGroup(2, 3, port=port, timeout=60, token="tok")
+        r2["parts"] = g.allgather(b"two")
+        g.close()
+
+    t2 = threading.Thread(target=join2)
+    t2.start()
+    p1 = r1.allgather(b"one")
+    t2.join(60)
+    th.join(60)
+    r1.close()
+    for s in strays:
+        s.close()
+    assert res["parts"] == [b"zero", b"one", b"two"] == p1 == r2["parts"]

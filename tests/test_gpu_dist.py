@@ -849,6 +849,47 @@ def test_bench_two_processes_rccl_fallback(tmp_path):
     assert rt["single_copy"] and not rt["torch_loaded_first"], rt
 
 
+def test_bench_spawns_ranks_without_launcher():
+    """`bench.py --gpus 2` with NO launcher: bench.py starts the two ranks
+    itself, before any GPU call, and relays rank 0's one JSON line.  Rehearsed on one GPU
+    (GPRX_DIST_SHARED_GPU: both ranks on device 0, the peer context).  The line must say
+    n_gpus 2 and ranks_seen 2, and carry per rank the device, the transport, the Linv / tile
+    pushes per fit and their bytes, and the measured diagonal-chain step,
+    consistent across the ranks."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["GPRX_DIST_SHARED_GPU"] = "1"
+    env["GPRX_BENCH_TIMEOUT_S"] = "280"
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--configs", "0", "--ntrain", "4096", "--lml", "0", "--build-iters", "0", "--cpu-n", "0",
+           "--predict-q", "256", "--variance-q", "0", "--cpu-lml-ns", "", "--cpu-predict-q", "0"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=root)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:]
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["ranks_seen"] == 2 and line["value"] > 0
+    assert line["launcher"] == "bench.py spawn"
+    assert line["config"]["parallelism"].startswith("sharded"), line["dist_error"]
+    ranks = sorted(line["ranks"], key=lambda x: x["rank"])
+    assert [x["rank"] for x in ranks] == [0, 1] and all(x["world"] == 2 for x in ranks)
+    for x in ranks:
+        assert x["transport"] == "peer" and x["device"] == 0 and x["pci"]
+        # every rank owns diagonal blocks: it pushes each Linv_k to its one peer, and final tiles
+        assert x["push_linv"] > 0 and x["push_tiles"] > 0
+        assert x["push_bytes"] == (x["push_linv"] + x["push_tiles"]) * 128 * 128 * 8
+        assert x["chain_step_us_median"] is not None and 1.0 < x["chain_step_us_median"] < 5000.0
+        assert x["diag_steps_owned"] > 0
+    # the ranks' diagonal blocks partition the 32 steps, and a Linv push per owned block
+    assert sum(x["diag_steps_owned"] for x in ranks) == 4096 // 128
+    assert sum(x["push_linv"] for x in ranks) == 4096 // 128
+    assert line["distinct_devices"] == 1  # (one shared GPU here; one per rank on a node)
+
+
 PEER_SLICE_SCRIPT = r"""
 import os, sys
 import numpy as np

@@ -132,6 +132,32 @@ def test_posterior_cov_and_core(ctx, ks):
     assert relerr(C, C_ref) <= 1e-6
 
 
+@pytest.mark.parametrize("ks", ["SumKernel(GaussianKernel(2,0.15,),PeriodicKernel(0.1,3.141592653589793,1,))",
+                                "GaussianKernel(0.7,1.3,)"])
+def test_posterior_variance_f32_near_training_points(ctx, ks):
+    """fp32 variances k(x,x) - |L^{-1} k_x|^2 at queries within 1e-3 of training samples, where
+    the difference cancels hardest (the expanded |u|^2 + |v|^2 - 2 u.v pair statistic
+    loses accuracy in fp32, so fp32 models keep the exact-difference build).  Against the oracle's
+    fp32 path (K in fp32, inverted in double as include/LAPACKUtils.h:85-97) at the fp32 bar,
+    on the scale of k(x,x); pairs (x, y != x) likewise."""
+    n, d, sigma = 400, 4, 0.3
+    X, Y = make_data(n, d)
+    X32, Y32 = X.astype(np.float32), Y.astype(np.float32)
+    M, _ = _fit(ctx, ks, X32, Y32, sigma, np.float32)
+    _, C_ref = O.fit(ks, X32, Y32, sigma, np.float32)
+    rng = np.random.default_rng(7)
+    Xa = (X32[rng.choice(n, 64, replace=False)] + 1e-3 * rng.standard_normal((64, d))).astype(np.float32)
+    v = M.posterior_cov(Xa, Xa)
+    v_ref = O.posterior_cov(ks, X32, C_ref, Xa, Xa, np.float32)
+    kaa = max(abs(O.kernel_eval(ks, a, a, with_grad=False)) for a in Xa.astype(np.float64))
+    assert np.max(np.abs(v - v_ref)) <= TOL[np.dtype(np.float32)] * max(1.0, kaa)
+    Xb = Xa[::-1].copy()
+    c = M.posterior_cov(Xa, Xb)
+    c_ref = O.posterior_cov(ks, X32, C_ref, Xa, Xb, np.float32)
+    assert np.max(np.abs(c - c_ref)) <= TOL[np.dtype(np.float32)] * max(1.0, kaa)
+    M.close()
+
+
 @pytest.mark.parametrize("ks", KERNELS)
 def test_lml(ctx, ks):
     n, d, sigma = 150, 2, 0.4
