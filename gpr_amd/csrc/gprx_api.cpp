@@ -144,6 +144,16 @@ std::string canonicalize(const gprx_kernel_desc& desc, KCanon<T>& K) {
                 L.c1 = T(-0.5) / (p2 * p2);
                 break;
         }
+        // the folded exp constants (fexp_fold: f64 predict epilogue only)
+        L.fold = 0;
+        L.f1 = L.f0 = T(0);
+        if (std::is_same<T, double>::value && (L.type == L_GAUSS || L.type == L_GAUSS_EXP || L.type == L_PERIODIC) &&
+            L.c0 > T(0) && std::isfinite(std::log((double)L.c0))) {
+            constexpr double kS = 92.33248261689366;  // 64 / ln 2
+            L.f1 = (T)((double)L.c1 * kS);
+            L.f0 = (T)(std::log((double)L.c0) * kS);
+            L.fold = 1;
+        }
         K.param_base[nleaf] = nparams;
         nparams += np;
         st.push_back(std::vector<unsigned>{1u << nleaf});

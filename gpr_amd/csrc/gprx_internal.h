@@ -38,6 +38,10 @@ struct KLeaf {
     int pslot;   // periodic table slot
     T c0, c1, c2;  // value constants (see leaf_value)
     T p[3];        // raw reference parameters (gradient formulas)
+    // exp leaves c0 exp(c1 x) with the scale folded into the exponent (f64 predict epilogue,
+    // fexp_fold): y = f1 x + f0 = (c1 x + ln c0) 64 / ln 2; fold = 0 when c0 <= 0 or not an exp leaf
+    T f1, f0;
+    int fold;
 };
 
 template <typename T>
@@ -196,6 +200,21 @@ __device__ __forceinline__ double fexp(double x) {
     return x < -745.5 ? 0.0 : v;
 }
 __device__ __forceinline__ float fexp(float x) { return expf(x); }
+// c0 exp(c1 x) for an exp leaf from y = f1 x + f0 = (c1 x + ln c0) 64 / ln2 (KLeaf::f1, f0; one
+// FMA in place of fexp's two multiplications before the reduction and the scale's multiplication
+// after it).  kd = rint(y), y - kd is exact (Sterbenz), r = (y - kd) ln2 / 64, |r| <= ln2/128,
+// then fexp's table and polynomial.  The rounding of y (|y| ulp / 2, ln2/64 of that in the
+// argument) matches the rounding of c1 x in the unfolded form within a factor of 2: ~1e-14
+// relative on the C3 tree's Gaussian leaf (x ~ 110).  y below -745.5 * 64/ln2 gives 0 as fexp.
+__device__ __forceinline__ double fexp_fold(double y) {
+    const double kd = __builtin_rint(y);
+    const double r = (y - kd) * (0.6931471805599453094 / 64.0);
+    const int n = (int)kd;
+    const double t = kExp2Tab64[n & 63];
+    const double p = fma(r * r, fma(r, fma(r, fma(r, 1.0 / 120.0, 1.0 / 24.0), 1.0 / 6.0), 0.5), r);
+    const double v = __builtin_ldexp(fma(t, p, t), n >> 6);
+    return y < -68834.5 ? 0.0 : v;
+}
 
 // sincos for both scalar types
 __device__ inline void gsincos(double x, double* s, double* c) { sincos(x, s, c); }

@@ -33,11 +33,30 @@ static inline int kp_of(const KCanon<T>& K, int d) {  // MFMA depth of the perio
 // loads, the type test is a uniform branch) and the per-pair work is an unrolled,
 // statically indexed loop over E registers.  The generic kernel_value reached from 32
 // unrolled call sites per thread was emitted as an out-of-line call per pair.
-template <typename T, int E, bool MUL>
+// FOLD (f64 predict): exp leaves with fold set take fexp_fold(f1 x + f0), which also carries
+// the leaf's scale; SET: the first leaf of a sum writes p (0 + x and 1 x are exact: the same
+// bits as adding to 0 / multiplying 1, one instruction less per pair).
+template <typename T, int E, bool MUL, bool FOLD = false, bool SET = false>
 __device__ __forceinline__ void leaf_into(const KLeaf<T>* __restrict__ L, const T (&r2)[E], const T (&s)[E],
                                           T (&p)[E]) {
     const int ty = L->type;
     const T c0 = L->c0, c1 = L->c1, c2 = L->c2;
+    if constexpr (FOLD && std::is_same<T, double>::value) {
+        if (L->fold) {
+            const T f1 = L->f1, f0 = L->f0;
+            const bool per = ty == L_PERIODIC;
+#pragma unroll
+            for (int e = 0; e < E; e++) {
+                const T f = fexp_fold(fma(f1, per ? s[e] : r2[e], f0));
+                p[e] = SET ? f : (MUL ? p[e] * f : p[e] + f);
+            }
+            return;
+        }
+    }
+    if constexpr (SET) {
+#pragma unroll
+        for (int e = 0; e < E; e++) p[e] = MUL ? T(1) : T(0);
+    }
     if (ty == L_PERIODIC) {
 #pragma unroll
         for (int e = 0; e < E; e++) {
@@ -67,12 +86,18 @@ __device__ __forceinline__ void leaf_into(const KLeaf<T>* __restrict__ L, const 
     }
 }
 
-template <typename T, int E>
+template <typename T, int E, bool FOLD = false>
 __device__ __forceinline__ void pair_values(const KCanon<T>* __restrict__ K, const T (&r2)[E], const T (&s)[E],
                                             T (&v)[E]) {
+    const int nl = K->nleaf;
+    if (FOLD && K->sum_leaves) {  // (nl >= 1: the first leaf writes v)
+        leaf_into<T, E, false, true, true>(&K->leaf[0], r2, s, v);
+#pragma unroll 1
+        for (int l = 1; l < nl; l++) leaf_into<T, E, false, true>(&K->leaf[l], r2, s, v);
+        return;
+    }
 #pragma unroll
     for (int e = 0; e < E; e++) v[e] = 0;
-    const int nl = K->nleaf;
     if (K->sum_leaves) {
 #pragma unroll 1
         for (int l = 0; l < nl; l++) leaf_into<T, E, false>(&K->leaf[l], r2, s, v);

@@ -260,7 +260,7 @@ __global__ __launch_bounds__(NT) void predict_mma_kernel(const KCanon<T>* __rest
                     pair_stats_nc<T, NPER, R2>(R2 ? ar[x][y][reg] : T(0), NPER ? ap[x][y][reg] : T(0), nu[y],
                                                R2 ? nvb[jl] : T(0), hd, r2[4 * u + y], sp[4 * u + y]);
             }
-            pair_values<T, 8>(Kd, r2, sp, v);
+            pair_values<T, 8, true>(Kd, r2, sp, v);  // (folded exp leaves: k_pairs.h leaf_into)
 #pragma unroll
             for (int u = 0; u < 2; u++) {
                 const T al = alb[wc * 32 + x * 16 + Tr::orow(lk, 2 * h + u)];

@@ -31,6 +31,13 @@ def main():
     print(f"predict {pr.get('pts_per_s_device')} pts/s tree frac {(pr.get('roofline_tree') or {}).get('frac')}")
     print(f"build {b.get('ms')} ms {b.get('gbs')} GB/s tree frac {(b.get('roofline_tree') or {}).get('frac')}")
     print(f"dist_error {d.get('dist_error')} replicas {(d.get('replicas') or {}).get('value')}")
+    if d.get("ranks"):
+        print(f"n_gpus {d.get('n_gpus')} ranks_seen {d.get('ranks_seen')} devices {d.get('distinct_devices')} "
+              f"launcher {d.get('launcher')} transport {d.get('dist_transport')}")
+        for r in d["ranks"]:
+            print("  rank", {k: r.get(k) for k in ("rank", "device", "pci", "transport", "rccl_count", "push_linv",
+                                                   "push_tiles", "push_bytes", "chain_step_us_median",
+                                                   "diag_steps_owned", "traced_fit_ms_factor", "error")})
 
 
 if __name__ == "__main__":

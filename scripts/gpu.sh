@@ -84,6 +84,12 @@ for step in "$@"; do
             > "$O/shared_bench.json" 2> "$O/shared_bench.err" || fail shared $? "$O/shared_bench.err"
         python scripts/bench_brief.py "$O/shared_bench.json"
         ;;
+    spawn)  # the driver's N > 1 command as it is (bench.py --gpus N, no launcher, default legs),
+            # rehearsed with SPAWN_N (default 2) ranks sharing this one GPU
+        GPRX_DIST_SHARED_GPU=1 timeout -k 10 900 python bench.py --gpus ${SPAWN_N:-2} $SPAWN_ARGS \
+            > "$O/spawn_bench.json" 2> "$O/spawn_bench.err" || fail spawn $? "$O/spawn_bench.err"
+        python scripts/bench_brief.py "$O/spawn_bench.json"
+        ;;
     peer)
         timeout -k 10 900 python -u -m pytest tests/test_gpu_dist.py -m gpu -x -q -k peer \
             --timeout 600 --timeout-method thread > "$O/peer.log" 2>&1 || fail peer $? "$O/peer.log"
