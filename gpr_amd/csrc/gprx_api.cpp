@@ -1834,7 +1834,12 @@ static void sparse_normal_eq(gprx_ctx* ctx, SparseNE<T>& st, const gprx_kernel_d
     st.Mp = Mp;
     st.mp = mp;
     st.ld = ld;
-    int64_t cmax = 32768;  // dense rows per streamed block (GPRX_SPARSE_CHUNK overrides, for tests)
+    // dense rows per streamed block (GPRX_SPARSE_CHUNK overrides, for tests): 262144 rows = four
+    // split-K launches at C5 instead of 31 -- the per-launch ramp, tail and partial-sum traffic
+    // amortised: syrk 0.737 -> 0.794 of the f64 peak, fit 88.1 -> 84.4 ms, same-box A/B
+    // (profiles/r06d_c5_chunk_ab.txt: 131072 84.3 ms / 0.78, one launch 85.6 ms / 0.80); the
+    // streamed block is ld x 262400 x 8 B = 4.6 GB of HBM
+    int64_t cmax = 262144;
     if (const char* ev = std::getenv("GPRX_SPARSE_CHUNK")) cmax = std::max<int64_t>(64, round_up(std::atoll(ev), 64));
     const int64_t chunk = std::max<int64_t>(BT, std::min<int64_t>(round_up(std::max<int64_t>(n, 1), 64), cmax));
     DevBuf &dXm = st.dXm, &dtm = st.dtm, &dX = st.dX, &dtx = st.dtx, &dY = st.dY, &dS = st.dS, &dA = st.dA,

@@ -234,9 +234,10 @@ extern "C" gprx_status gprx_dev_schedule(int32_t nc, int32_t nr, int32_t P, int3
                                          int64_t* ntasks) {
     try {
         // build: bit 0 = fused covariance build, bit 1 = the last nc row blocks are identity,
-        // bits 8..15 = chunk rule ratio + 1 (0: the one the simulation picks)
+        // bits 8..15 = chunk rule ratio + 1 (0: the one the simulation picks), bits 16..23 =
+        // paired updates' row offset + 1 (0: the simulation's choice, 1: none)
         const int64_t n = potrf_tiles_schedule_stats(nc, nr, P, (build & 1) != 0, est_us, (build & 2) ? nc : 0,
-                                                     ((build >> 8) & 0xff) - 1);
+                                                     ((build >> 8) & 0xff) - 1, nullptr, 0, ((build >> 16) & 0xff) - 1);
         if (ntasks) *ntasks = n;
         return GPRX_OK;
     } catch (const Error& e) {
@@ -249,7 +250,7 @@ extern "C" int64_t gprx_dev_schedule_list(int32_t nc, int32_t nr, int32_t P, int
                                           int64_t max) {
     try {
         return potrf_tiles_schedule_stats(nc, nr, P, (build & 1) != 0, nullptr, (build & 2) ? nc : 0,
-                                          ((build >> 8) & 0xff) - 1, out, max);
+                                          ((build >> 8) & 0xff) - 1, out, max, ((build >> 16) & 0xff) - 1);
     } catch (const Error& e) {
         std::fprintf(stderr, "gprx_dev_schedule_list: %s\n", e.msg.c_str());
         return -1;

@@ -587,7 +587,7 @@ template <typename T>
 void potrf_auto(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info, Exec& ex);
 bool potrf_uses_tiles();
 int64_t potrf_tiles_schedule_stats(int nc, int nr, int P, bool build, double* est_us, int ni = 0, int ratio = -1,
-                                   int32_t* list_out = nullptr, int64_t list_max = 0);
+                                   int32_t* list_out = nullptr, int64_t list_max = 0, int pair = -1);
 // Generic C = beta C + alpha A B^T on GT-multiples (column-major).  lower: only tiles
 // with col-tile <= row-tile are computed, and inside diagonal tiles only row >= col.
 template <typename T>

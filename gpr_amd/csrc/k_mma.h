@@ -20,7 +20,9 @@ namespace mm {
 constexpr int NT = 512;     // threads per workgroup
 constexpr int PAD = 16;     // LDS row pad (elements)
 
-enum { T_DIAGX = 0, T_TRSM = 1, T_UPD = 2, T_BUILD = 3, T_TPART = 4 };
+// T_UPD2 (round 6): the update of two vertically adjacent tiles (i, j), (i + 1, j) over the same
+// panels as one 256 x 128 product (tile_mma_tall): the single-GPU factorisation's paired chunks
+enum { T_DIAGX = 0, T_TRSM = 1, T_UPD = 2, T_BUILD = 3, T_TPART = 4, T_UPD2 = 5 };
 enum { C_TICKET = 0, C_ERR = 1, C_NCTL = 16 };  // control words at the head of the counter block
 
 typedef double d4_t __attribute__((ext_vector_type(4)));
@@ -473,7 +475,8 @@ template <typename T>
 constexpr size_t tall_lds() {
     return sizeof(T) * 2 * 3 * Stage<T>::GRP * Stage<T>::SRP;
 }
-template <typename T, int MID = 1>
+// ACC: acc += A B^T (acc not cleared: the factorisation's paired updates start it from -C)
+template <typename T, int MID = 1, bool ACC = false>
 __device__ __forceinline__ void tile_mma_tall(typename Mfma<T>::acc_t (&acc)[4][4], const T* __restrict__ A,
                                               int64_t lda, const T* __restrict__ B, int64_t ldb, int K, T* smem,
                                               const int t) {
@@ -497,10 +500,12 @@ __device__ __forceinline__ void tile_mma_tall(typename Mfma<T>::acc_t (&acc)[4][
                                              (__attribute__((address_space(3))) void*)(buf + g * S::SRP), 16, 0, 0);
         }
     };
+    if (!ACC) {
 #pragma unroll
-    for (int x = 0; x < 4; x++)
+        for (int x = 0; x < 4; x++)
 #pragma unroll
-        for (int y = 0; y < 4; y++) acc[x][y] = typename Tr::acc_t{0};
+            for (int y = 0; y < 4; y++) acc[x][y] = typename Tr::acc_t{0};
+    }
     const int nst = K / BK;
     if (nst > 0) issue(0);
     const T* ab = smem + (wr >> 1) * S::GRP * S::SRP;  // this wave's half of A

@@ -119,6 +119,43 @@ __device__ __forceinline__ void tile_gemm(T* __restrict__ C, int64_t ldc, const 
 }
 
 // ------------------------------------------------------------------------------------------
+// Paired update (T_UPD2): C -= A B^T on a 256 x 128 tile -- tiles (i, j) and (i + 1, j), which
+// are adjacent rows of the column-major factor (C and A are 256 rows at one ld) -- over K panels
+// of the same B (L_j).  The 8 waves take 64 x 64 blocks (tile_mma_tall: 16 MFMAs per 8 fragment
+// reads, 384 DMA'd rows per stage for twice the 128 x 128 tile's flops; probe 0.901 of the f64
+// MFMA bound against 0.877, f32 0.857 against 0.818, profiles/r05u).  Its 128 accumulator
+// registers fit the task loop because the C tile is not prefetched into registers beside them,
+// as tile_gemm does: the accumulators START from -C (loads issued before the first stage's DMAs,
+// their latency under the ring's fill), and -acc = C - A B^T is stored.  Off-diagonal tiles only.
+// ------------------------------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ void tile_gemm_tall(T* __restrict__ C, int64_t ldc, const T* __restrict__ A, int64_t lda,
+                                               const T* __restrict__ B, int64_t ldb, int K, T* smem, const int t) {
+    typedef Mfma<T> Tr;
+    typedef typename Tr::acc_t acc_t;
+    const int lane = t & 63, w = t >> 6;
+    const int wr = w & 3, wc = w >> 2, lr = lane & 15, lk = lane >> 4;
+    acc_t acc[4][4];
+#pragma unroll
+    for (int x = 0; x < 4; x++)
+#pragma unroll
+        for (int reg = 0; reg < 4; reg++) {
+            const T* ccol = C + (int64_t)(64 * wc + 16 * x + Tr::orow(lk, reg)) * ldc;
+#pragma unroll
+            for (int y = 0; y < 4; y++) acc[x][y][reg] = -ccol[64 * wr + 16 * y + lr];
+        }
+    mm::tile_mma_tall<T, 1, true>(acc, A, lda, B, ldb, K, smem, t);
+#pragma unroll
+    for (int x = 0; x < 4; x++)
+#pragma unroll
+        for (int reg = 0; reg < 4; reg++) {
+            T* ccol = C + (int64_t)(64 * wc + 16 * x + Tr::orow(lk, reg)) * ldc;
+#pragma unroll
+            for (int y = 0; y < 4; y++) st_sc1(ccol + 64 * wr + 16 * y + lr, -acc[x][y][reg]);
+        }
+}
+
+// ------------------------------------------------------------------------------------------
 // Diagonal 128x128 block: L (in place, lower) and Linv (DB x DB, column-major), 512 threads.
 //
 // The block lives in REGISTERS as a square image S: lower triangle = A (becoming L), strict
@@ -1268,6 +1305,16 @@ __device__ __forceinline__ void publish(int* flag, int v, bool release) {
     }
 }
 
+// two counters after one drain (a paired update's tiles)
+__device__ __forceinline__ void publish2(int* f1, int* f2, int v) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (wave_id() == 0) {
+        st_agent(f1, v);
+        st_agent(f2, v);
+    }
+}
+
 // stores of this workgroup visible to its own later loads (same CU)
 __device__ __forceinline__ void local_sync() {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1278,6 +1325,8 @@ template <typename T>
 constexpr size_t pt_lds_bytes() {
     return gemm_lds<T>() > diag_lds<T>() ? gemm_lds<T>() : diag_lds<T>();
 }
+static_assert(tall_lds<double>() <= pt_lds_bytes<double>() && tall_lds<float>() <= pt_lds_bytes<float>(),
+              "the paired update's ring exceeds the LDS of the launch");
 
 template <typename T>
 struct Args {
@@ -1525,6 +1574,7 @@ __device__ bool wait_inputs(const Args<T>& a, int type, int i, int j, int b0, in
     const unsigned* rp = nullptr;
     int rn = 0;
     unsigned ep = 0;
+    const int* lp3 = nullptr;  // T_UPD2: the second row's final blocks (>= lwant1)
     if (type == T_TPART) {  // its A operand final (Linv_{i-1} is waited for inside the task)
         vp = a.ver + (int64_t)i * a.nv + (i - 1);
         vwant = i - 1;
@@ -1574,6 +1624,16 @@ __device__ bool wait_inputs(const Args<T>& a, int type, int i, int j, int b0, in
                 ep = D.ep;
             }
         }
+    } else if (!DIST && type == T_UPD2) {  // tiles (i, j), (i + 1, j); rows i, i + 1 and j final through the chunk
+        vp = a.ver + (int64_t)i * a.nv + j;
+        vwant = b0;
+        vp2 = a.ver + (int64_t)(i + 1) * a.nv + j;
+        vwant2 = b0;
+        lp1 = a.lcnt + i;
+        lwant1 = b0 + nb;
+        lp2 = a.lcnt + j;
+        lwant2 = b0 + nb;
+        lp3 = a.lcnt + i + 1;
     } else if (type == T_TRSM) {
         vp = a.ver + (int64_t)i * a.nv + j;
         vwant = j;
@@ -1619,6 +1679,7 @@ __device__ bool wait_inputs(const Args<T>& a, int type, int i, int j, int b0, in
         // bitwise: all four loads are issued before any compare resolves
         int ok = int(ld_uni(vp) == vwant) & int(ld_uni(vp2) == vwant2) & int(ld_uni(lp1) >= lwant1) &
                  int(ld_uni(lp2) >= lwant2);
+        if (!DIST && lp3) ok &= int(ld_uni(lp3) >= lwant1);
         if constexpr (DIST) {
             if (rp) {  // lane l checks flag l (l < rn): one vector load, one ballot
                 const bool good = lane >= rn || ld_sys(rp + (lane < rn ? lane : 0)) == ep;
@@ -2548,6 +2609,11 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
                 tile_gemm<T, true>(Ci + (int64_t)j * GT * ld, ld, a.A + oa, lop, a.A + ob, lop, nb * GT, i == j, smem,
                                    tid);
             publish(a.ver + (int64_t)i * a.nv + j, b0 + nb, false);
+        } else if (type == T_UPD2) {  // tiles (i, j) and (i + 1, j): one 256 x 128 update
+            if (!(a.variant & 2))
+                tile_gemm_tall<T>(Ci + (int64_t)j * GT * ld, ld, a.A + (int64_t)i * GT + (int64_t)b0 * GT * ld, ld,
+                                  a.A + (int64_t)j * GT + (int64_t)b0 * GT * ld, ld, nb * GT, smem, tid);
+            publish2(a.ver + (int64_t)i * a.nv + j, a.ver + (int64_t)(i + 1) * a.nv + j, b0 + nb);
         } else if (type == T_TRSM) {
             T* Cik = Ci + (int64_t)j * GT * ld;
             if (!(a.variant & 1))
@@ -2625,6 +2691,9 @@ struct Cost {  // per-task durations (us, one CU), calibrated from GPRX_PT_TRACE
     double tpart_prog = 2.5;
     bool prog = false;  // this schedule is for the progressive form (set by the callers)
     int np = 4;         // TPART tasks per split step (tp_parts; set by the callers)
+    // a paired update (T_UPD2) per panel, relative to two single-tile panels (the 256 x 128
+    // mainloop's probe rate against the 128 x 128 tile's: 0.877 / 0.901)
+    double tall = 0.975;
 };
 
 // TPART tickets of one k in the order TPART(k, np-1), .., (k, 0): each part waits for
@@ -2705,12 +2774,24 @@ static void tile_chunks(int i, int j, int W, int near, std::vector<std::pair<int
 // L^{-T} rows): identity block a = i - (nr - ni) has zero L blocks before column block a.
 // tail > 0: the capped rule (ratio) only for the tiles of the last `tail` column blocks, the
 // fixed rule before them
+// pair > 0 (round 6): the off-diagonal tiles of column j from row j + pair down to the last label
+// row go in vertical pairs (j + pair, j + pair + 1), ..., each pair's identical chunks as ONE
+// T_UPD2 task (a 256 x 128 update: tile_gemm_tall); the `pair` - 1 tiles right below the
+// diagonal -- the diagonal chain's inputs -- and the identity rows stay single
 static Schedule make_schedule(int nc, int nr, int W, int near, int P, const Cost& cm0, bool build, int ni = 0,
-                              int ratio = 0, bool split = false, int tail = 0) {
+                              int ratio = 0, bool split = false, int tail = 0, int pair = 0) {
     Cost cm = cm0;
     if (split) cm.early = cm.early_s;
     const int nr0 = nr - ni;
     auto start_of = [&](int i) { return i >= nr0 ? i - nr0 : 0; };
+    // row i of column j: 1 the top of a pair, 2 its bottom, 0 single
+    auto pair_role = [&](int i, int j) {
+        if (pair <= 0 || i >= nr0) return 0;
+        const int r0 = j + pair;
+        if (i >= r0 && (i - r0) % 2 == 0 && i + 1 < nr0) return 1;
+        if (i - 1 >= r0 && (i - 1 - r0) % 2 == 0) return 2;
+        return 0;
+    };
     std::vector<Task> tasks;
     tasks.reserve((size_t)nr * nc * 2);
     auto add = [&](int type, int i, int j, int b0, int nb, double dur) {
@@ -2796,6 +2877,20 @@ static Schedule make_schedule(int nc, int nr, int W, int near, int P, const Cost
         }
         if (k + 1 < nc) make_diagx(k + 1);
         for (const Chunk& c : by_last[k]) {
+            const int role = pair_role(c.i, c.j);
+            if (role == 2) continue;  // (the pair's top row made the task: identical chunks)
+            if (role == 1) {
+                const int id = add(T_UPD2, c.i, c.j, c.b0, c.nb, cm.ovh + 2.0 * c.nb * cm.k128 * cm.tall);
+                bool e1, e2, e3;
+                for (int r = c.i; r <= c.i + 1; r++) dep(id, last_upd[(size_t)r * nc + c.j]);
+                const int p1 = prodL(c.i, k, e1), p3 = prodL(c.i + 1, k, e3), p2 = prodL(c.j, k, e2);
+                dep(id, p1, e1);
+                dep(id, p3, e3);
+                dep(id, p2, e2);
+                last_upd[(size_t)c.i * nc + c.j] = id;
+                last_upd[(size_t)(c.i + 1) * nc + c.j] = id;
+                continue;
+            }
             const double dur = cm.ovh + c.nb * cm.k128 * (c.i == c.j ? cm.diagf : 1.0);
             const int id = add(T_UPD, c.i, c.j, c.b0, c.nb, dur);
             dep(id, last_upd[(size_t)c.i * nc + c.j]);
@@ -3177,6 +3272,8 @@ struct Params {
     int ratio = -1;         // chunk-width rule of tile_chunks: < 0 picked per shape by the simulation
     int split = 1;          // f64: the split diagonal step (TPART tasks); GPRX_PT_SPLIT=0 turns it off
     int tail = 0;           // > 0: the capped chunk rule only in the last `tail` column blocks
+    int pair = -1;          // paired updates (make_schedule): < 0 picked per shape by the simulation,
+                            // 0 off, n > 0 pairs from row j + n (GPRX_PT_PAIR)
     Cost cm;
     int near_for(int nc) const { return near >= 0 ? near : (nc <= 64 ? 1 : 0); }
     Params() {
@@ -3190,6 +3287,8 @@ struct Params {
         if (const char* e = std::getenv("GPRX_PT_BUILD_US")) cm.build = std::atof(e);
         if (const char* e = std::getenv("GPRX_PT_SPLIT")) split = std::atoi(e);
         if (const char* e = std::getenv("GPRX_PT_TAIL")) tail = std::atoi(e);
+        if (const char* e = std::getenv("GPRX_PT_PAIR")) pair = std::atoi(e);
+        if (const char* e = std::getenv("GPRX_PT_TALL")) cm.tall = std::atof(e);
         if (const char* e = std::getenv("GPRX_PT_TPART_US")) cm.tpart = std::atof(e);
         if (const char* e = std::getenv("GPRX_PT_DIAGXS_US")) cm.diagx_s = std::atof(e);
         if (const char* e = std::getenv("GPRX_PT_TPARTP_US")) cm.tpart_prog = std::atof(e);
@@ -3214,20 +3313,35 @@ static const Params& params() {
 // simulation ranks it first too) -- unless GPRX_PT_RATIO fixes it (GPRX_PT_TAIL its reach)
 static const int kRatios[] = {0, 8, 4, 2};
 static const int kTails[] = {0, 16, 32};
+// Paired updates (T_UPD2): off, or pairs from 1 / 2 / 4 rows below the diagonal, whichever the
+// simulation ranks first (pairing halves the task count and runs the wider mainloop, but a pair
+// holds back both tiles' consumers until the later of the two rows is final)
+static const int kPairs[] = {0, 1, 2, 4};
 static Schedule best_schedule(int nc, int nr, const Params& pr, int P, bool build, int ni, bool split, bool f64) {
     const Cost cm = pr.cost(f64);
-    if (pr.ratio >= 0) return make_schedule(nc, nr, pr.W, pr.near_for(nc), P, cm, build, ni, pr.ratio, split, pr.tail);
     Schedule best;
     bool have = false;
-    for (int r : kRatios)
-        for (int tl : kTails) {
-            if ((r == 0 && tl) || (tl && tl >= nc)) continue;
-            Schedule S = make_schedule(nc, nr, pr.W, pr.near_for(nc), P, cm, build, ni, r, split, tl);
-            if (!have || S.est_us < best.est_us * 0.995) {  // a rule with more tasks must win by > 0.5%
+    for (int pq : kPairs) {
+        if (pr.pair >= 0 && pq != pr.pair) continue;
+        if (pr.pair < 0 && pq && pq >= nc - 1) continue;
+        auto consider = [&](Schedule&& S) {
+            // a rule with more tasks (or the paired form) must win by > 0.5%
+            if (!have || S.est_us < best.est_us * 0.995) {
                 best = std::move(S);
                 have = true;
             }
+        };
+        if (pr.ratio >= 0) {
+            consider(make_schedule(nc, nr, pr.W, pr.near_for(nc), P, cm, build, ni, pr.ratio, split, pr.tail, pq));
+            continue;
         }
+        for (int r : kRatios)
+            for (int tl : kTails) {
+                if ((r == 0 && tl) || (tl && tl >= nc)) continue;
+                consider(make_schedule(nc, nr, pr.W, pr.near_for(nc), P, cm, build, ni, r, split, tl, pq));
+            }
+    }
+    if (pr.pair > 0 && !have) return make_schedule(nc, nr, pr.W, pr.near_for(nc), P, cm, build, ni, 0, split, 0, pr.pair);
     return best;
 }
 
@@ -3534,13 +3648,14 @@ template void potrf_tiles_dist_launch<float>(const DistLaunch<float>&);
 // Host-only schedule statistics (no device work): tasks, predicted makespan, and a check
 // that every task's producers come earlier in the ticket order.
 int64_t potrf_tiles_schedule_stats(int nc, int nr, int P, bool build, double* est_us, int ni, int ratio,
-                                   int32_t* list_out, int64_t list_max) {
+                                   int32_t* list_out, int64_t list_max, int pair) {
     if (nc < 1 || nr < nc || P < 1 || ni < 0 || ni > nr - nc)
         throw Error{GPRX_ERR_ARG, "potrf tile schedule: need nc >= 1, nr >= nc + ni, P >= 1"};
-    const pt::Params& pr = pt::params();
+    pt::Params pr = pt::params();
+    if (pair >= 0) pr.pair = pair;
     const bool split = pt::split_for(true, P);  // the f64 schedule
     pt::Schedule S = ratio >= 0 ? pt::make_schedule(nc, nr, pr.W, pr.near_for(nc), P, pr.cost(true), build, ni, ratio, split,
-                                                    pr.tail)
+                                                    pr.tail, pr.pair > 0 ? pr.pair : 0)
                                 : pt::best_schedule(nc, nr, pr, P, build, ni, split, true);
     if (est_us) *est_us = S.est_us;
     if (list_out)  // the ticket list: {type | nb << 8, i, j, b0} per ticket

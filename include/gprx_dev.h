@@ -27,12 +27,14 @@ gprx_status gprx_dev_bench(gprx_ctx* ctx, gprx_dtype dtype, int32_t what, int64_
 /* Host-only: build the tile-dataflow potrf schedule for nc diagonal blocks, nr row blocks
  * and P workers (build bit 0: with the fused covariance-build tasks; bit 1: the last nc of
  * the nr row blocks are identity rows, the inverse riding along; bits 8..15: the update
- * chunk rule's ratio + 1, 0 = the rule the simulated makespan picks); returns its task count
+ * chunk rule's ratio + 1, 0 = the rule the simulated makespan picks; bits 16..23: the paired
+ * updates' first row below the diagonal + 1, 1 = no pairs, 0 = the simulation's choice); returns its task count
  * and simulated makespan (us).  Throws nothing, needs no
  * device: GPRX_ERR_ARG if the ticket order would violate a dependency. */
 gprx_status gprx_dev_schedule(int32_t nc, int32_t nr, int32_t P, int32_t build, double* est_us, int64_t* ntasks);
 /* Host-only: the same schedule's ticket list, 4 ints per ticket {type | chunk panels << 8, i, j,
- * first panel} (types 0 DIAGX, 1 TRSM, 2 UPD, 3 BUILD, 4 TPART with j = the part), at most max
+ * first panel} (types 0 DIAGX, 1 TRSM, 2 UPD, 3 BUILD, 4 TPART with j = the part, 5 UPD2: the
+ * tiles (i, j) and (i + 1, j) as one 256 x 128 update), at most max
  * tickets into out; returns the task count, -1 on bad arguments. */
 int64_t gprx_dev_schedule_list(int32_t nc, int32_t nr, int32_t P, int32_t build, int32_t* out, int64_t max);
 /* Host-only: the distributed factorisation's schedule (g ranks of P workers each, row blocks

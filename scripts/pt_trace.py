@@ -59,12 +59,12 @@ okc = dur_ticks > 500
 clock_ghz = float(np.median(cyc[okc] / dur_ticks[okc]) * 0.1)
 res = {"clock_ghz_median": clock_ghz, "n": n, "ms_devbench": ms.value, "span_us": span, "tasks": int(k), "workers": P,
        "busy_frac": float(ex.sum() / (span * P)), "wait_frac": float(wt.sum() / (span * P))}
-names = {0: "DIAGX", 1: "TRSM", 2: "UPD", 3: "BUILD", 4: "TPART"}
-for t in (0, 1, 2, 3, 4):
+names = {0: "DIAGX", 1: "TRSM", 2: "UPD", 3: "BUILD", 4: "TPART", 5: "UPD2"}
+for t in (0, 1, 2, 3, 4, 5):
     for b in sorted(set(nb[typ == t])):
         m = (typ == t) & (nb == b)
         diag = (tasks[:, 1] == tasks[:, 2])
-        key = f"{names[t]}{'' if t != 2 else '_nb' + str(b)}"
+        key = f"{names[t]}{'' if t not in (2, 5) else '_nb' + str(b)}"
         if t == 4:  # the split diagonal step's parts, by column block c
             for c in range(4):
                 mc = m & (tasks[:, 2] == c)
@@ -79,10 +79,11 @@ for t in (0, 1, 2, 3, 4):
             if md.any():
                 res[key]["diagtile_exec_us_mean"] = float(ex[md].mean())
 # worker time per task type, in ms of the whole chip (sum of exec / workers)
-res["chip_ms_by_type"] = {names[t]: round(float(ex[typ == t].sum() / P / 1e3), 3) for t in (0, 1, 2, 3, 4)}
+res["chip_ms_by_type"] = {names[t]: round(float(ex[typ == t].sum() / P / 1e3), 3) for t in (0, 1, 2, 3, 4, 5)}
 res["chip_ms_wait"] = round(float(wt.sum() / P / 1e3), 3)
 res["chip_ms_idle"] = round(float(span / 1e3 - (ex.sum() + wt.sum()) / P / 1e3), 3)
 res["upd_panels"] = int(nb[typ == 2].sum())
+res["upd2_panels"] = int(nb[typ == 5].sum())  # (each covers two tiles)
 # DIAGX chain
 d = np.where(typ == 0)[0]
 order = np.argsort(tasks[d, 1])

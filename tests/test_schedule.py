@@ -296,3 +296,67 @@ def test_schedule_split_step_needs_eight_workers():
     lst = _sched_list(9, 10, P=NPARTS - 1, ratio=0)
     assert not np.any((lst[:, 0] & 0xFF) == 4)
     assert len(lst) == _expected_tasks(9, 10) - tparts(9)
+
+
+def _sched_list(nc, nr, build=True, ratio=0, pair=0, ident=False):
+    """The ticket list (gprx_dev_schedule_list); pair: paired updates from row j + pair (0 none)."""
+    L = lib()
+    L.gprx_dev_schedule_list.argtypes = [ctypes.c_int32] * 4 + [ctypes.c_void_p, ctypes.c_int64]
+    L.gprx_dev_schedule_list.restype = ctypes.c_int64
+    out = np.zeros((400000, 4), np.int32)
+    flags = (1 if build else 0) | (2 if ident else 0) | ((ratio + 1) << 8) | ((pair + 1) << 16)
+    n = L.gprx_dev_schedule_list(nc, nr, 256, flags, out.ctypes.data, out.shape[0])
+    assert n > 0
+    return out[:n]
+
+
+@pytest.mark.parametrize("nc,pair", [(2, 1), (9, 1), (9, 2), (33, 2), (40, 4), (128, 2)])
+def test_schedule_paired_updates(nc, pair):
+    """Paired updates (T_UPD2, k_ptiles.hip make_schedule pair > 0): the off-diagonal tiles of
+    column j from row j + pair down to the label row go in vertical pairs, each pair's (identical)
+    chunks as one task; every tile's panels are still applied exactly once, in order, by tickets
+    that come after the producers of their operands (replayed here), the identity rows and the
+    `pair` - 1 tiles below the diagonal stay single, and the ticket order is valid."""
+    nr = nc + 1
+    st, n, est = _sched(nc, nr, build=True)
+    assert st == 0
+    L = _sched_list(nc, nr, pair=pair)
+    typ, nb = L[:, 0] & 0xFF, L[:, 0] >> 8
+    ii, jj, b0 = L[:, 1], L[:, 2], L[:, 3]
+    # per tile: the (b0, nb) chunks in ticket order
+    applied = {}
+    for q in np.where((typ == 2) | (typ == 5))[0]:
+        rows = [ii[q]] if typ[q] == 2 else [ii[q], ii[q] + 1]
+        if typ[q] == 5:
+            assert ii[q] > jj[q] and ii[q] - jj[q] >= pair and (ii[q] - jj[q] - pair) % 2 == 0 and ii[q] + 1 <= nc
+        for r in rows:
+            applied.setdefault((r, jj[q]), []).append((int(b0[q]), int(nb[q]), int(q)))
+    for (r, j), ch in applied.items():
+        e = j - 1 if r == j else j
+        pos = 0
+        for b, k, q in ch:  # contiguous, in order, covering [0, e)
+            assert b == pos, (r, j, ch)
+            pos += k
+        assert pos == e, (r, j, ch)
+    # the pairs replace two single tasks each: fewer tickets than the unpaired schedule
+    L0 = _sched_list(nc, nr, pair=0)
+    n_upd0 = int(((L0[:, 0] & 0xFF) == 2).sum())
+    n_pairs = int((typ == 5).sum())
+    assert int((typ == 2).sum()) + 2 * n_pairs == n_upd0
+    if nc >= 9:
+        assert n_pairs > 0
+    # producers before consumers: a paired task's operand rows are final (their TRSM / DIAGX
+    # tickets) for every panel of its chunk before it
+    final = {}
+    for q in range(len(L)):
+        if typ[q] == 1:
+            final[(ii[q], jj[q])] = q
+        elif typ[q] == 0:
+            final[(ii[q], ii[q])] = q
+    for q in np.where(typ == 5)[0]:
+        for b in range(b0[q], b0[q] + nb[q]):
+            for r in (ii[q], ii[q] + 1, jj[q]):
+                p = final.get((r, b))
+                if p is None and r == b + 1:  # L_{b+1,b}: published by DIAGX(b + 1) (or its parts)
+                    p = final.get((r, r))
+                assert p is not None and p < q, (q, r, b)
