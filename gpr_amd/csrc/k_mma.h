@@ -475,11 +475,15 @@ template <typename T>
 constexpr size_t tall_lds() {
     return sizeof(T) * 2 * 3 * Stage<T>::GRP * Stage<T>::SRP;
 }
-// ACC: acc += A B^T (acc not cleared: the factorisation's paired updates start it from -C)
-template <typename T, int MID = 1, bool ACC = false>
+// Csub (optional): acc = A B^T - C for the 256 x 128 tile C (ldc) -- C is read in four column
+// chunks of 16 values per lane, chunk c issued at stage c right after that stage's DMAs and
+// subtracted at stage c + 1 (after the stage's vmcnt wait), so its latency hides under the
+// MFMAs instead of holding the first one (the factorisation's paired updates, which have no
+// registers to prefetch the whole C tile beside their 128 accumulators)
+template <typename T, int MID = 1>
 __device__ __forceinline__ void tile_mma_tall(typename Mfma<T>::acc_t (&acc)[4][4], const T* __restrict__ A,
                                               int64_t lda, const T* __restrict__ B, int64_t ldb, int K, T* smem,
-                                              const int t) {
+                                              const int t, const T* __restrict__ Csub = nullptr, int64_t ldc = 0) {
     typedef Mfma<T> Tr;
     typedef Stage<T> S;
     constexpr int BK = BkOf<T>::v;
@@ -500,24 +504,61 @@ __device__ __forceinline__ void tile_mma_tall(typename Mfma<T>::acc_t (&acc)[4][
                                              (__attribute__((address_space(3))) void*)(buf + g * S::SRP), 16, 0, 0);
         }
     };
-    if (!ACC) {
 #pragma unroll
-        for (int x = 0; x < 4; x++)
+    for (int x = 0; x < 4; x++)
 #pragma unroll
-            for (int y = 0; y < 4; y++) acc[x][y] = typename Tr::acc_t{0};
-    }
+        for (int y = 0; y < 4; y++) acc[x][y] = typename Tr::acc_t{0};
+    // C chunk c: this lane's 16 values of columns 64 wc + 16 c + orow(lk, reg), rows 64 wr + 16 y + lr
+    T cb[4][4];
+    auto cload = [&](int c) {
+#pragma unroll
+        for (int reg = 0; reg < 4; reg++) {
+            const T* ccol = Csub + (int64_t)(64 * wc + 16 * c + Tr::orow(lk, reg)) * ldc + 64 * wr + lr;
+#pragma unroll
+            for (int y = 0; y < 4; y++) cb[y][reg] = ccol[16 * y];
+        }
+    };
+    auto csub = [&](auto xc) {  // (static chunk index: the accumulators stay register-indexed)
+        constexpr int x = decltype(xc)::value;
+#pragma unroll
+        for (int y = 0; y < 4; y++)
+#pragma unroll
+            for (int reg = 0; reg < 4; reg++) acc[x][y][reg] -= cb[y][reg];
+    };
     const int nst = K / BK;
     if (nst > 0) issue(0);
     const T* ab = smem + (wr >> 1) * S::GRP * S::SRP;  // this wave's half of A
     const T* bb = smem + 2 * S::GRP * S::SRP;
     const int ar = 64 * (wr & 1);
     T fa[2][4], fb[2][4];
-#pragma nounroll
-    for (int st = 0; st < nst; st++) {
-        wait_vm<0>();  // this wave's loads of stage st (issued a stage ago)
+    // one stage; CP (compile time) >= 0: the C chunk phase of stages 0..4 (subtract chunk CP - 1,
+    // load chunk CP) -- the first five stages are peeled so every accumulator index stays static
+    // (a run-time chunk index put the accumulators in scratch)
+    // SPREAD (f64, FeedOf::spread): the next stage's DMAs go out one behind each of the stage's
+    // first MFMAs instead of in a burst after the barrier, which held both waves of a SIMD (~60
+    // cycles an instruction) while its MFMA pipe idled
+    constexpr bool SPREAD = FeedOf<T>::spread && MID + IPW3 + 1 <= 16;
+    auto issue_u = [&](int st, int u) {
+        T* buf = smem + (st & 1) * STG3;
+        const int g = w * IPW3 + u, op = g / S::GRP, gg = g - op * S::GRP;
+        const int64_t col = (int64_t)st * BK + gg * S::CPI + lcol;
+        const T* src = (op == 2) ? (B + lrow + col * ldb) : (A + (int64_t)op * GT + lrow + col * lda);
+        __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(buf + g * S::SRP),
+                                         16, 0, 0);
+    };
+    auto stage = [&](int st, auto cp) {
+        constexpr int CP = decltype(cp)::value;
+        wait_vm<0>();  // this wave's loads of stage st (issued a stage ago), and C chunk CP - 1
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();  // every wave's; every wave done with the other buffer
-        if (st + 1 < nst) issue(st + 1);
+        if (!SPREAD && st + 1 < nst) issue(st + 1);
+        const bool more = st + 1 < nst;
+        if constexpr (CP >= 1) {
+            if (Csub) csub(std::integral_constant<int, CP - 1>{});
+        }
+        if constexpr (CP >= 0 && CP < 4) {
+            if (Csub) cload(CP);
+        }
         const T* a = ab + (st & 1) * STG3;
         const T* b = bb + (st & 1) * STG3;
         auto frag = [&](int kq, int r) {
@@ -541,9 +582,42 @@ __device__ __forceinline__ void tile_mma_tall(typename Mfma<T>::acc_t (&acc)[4][
                         __builtin_amdgcn_sched_barrier(0);
                     }
                     acc[x][y] = Tr::mma(fb[kq & 1][x], fa[kq & 1][y], acc[x][y]);
+                    if (SPREAD && kq == 0 && m > MID && m - MID - 1 < IPW3) {
+                        __builtin_amdgcn_sched_barrier(0);
+                        if (more) issue_u(st + 1, m - MID - 1);
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
                     m++;
                 }
         }
+    };
+    if (Csub) {
+        if (nst > 0) stage(0, std::integral_constant<int, 0>{});
+        if (nst > 1) stage(1, std::integral_constant<int, 1>{});
+        if (nst > 2) stage(2, std::integral_constant<int, 2>{});
+        if (nst > 3) stage(3, std::integral_constant<int, 3>{});
+        if (nst > 4) stage(4, std::integral_constant<int, 4>{});
+#pragma nounroll
+        for (int st = 5; st < nst; st++) stage(st, std::integral_constant<int, -1>{});
+        if (nst < 5) {  // short products: the chunks not yet subtracted (nst >= 1: chunk nst - 1 is loaded)
+            wait_vm<0>();
+            auto tail = [&](auto xc) {
+                constexpr int x = decltype(xc)::value;
+                if (nst == x + 1) csub(xc);
+                if (nst <= x) {
+                    cload(x);
+                    wait_vm<0>();
+                    csub(xc);
+                }
+            };
+            tail(std::integral_constant<int, 0>{});
+            tail(std::integral_constant<int, 1>{});
+            tail(std::integral_constant<int, 2>{});
+            tail(std::integral_constant<int, 3>{});
+        }
+    } else {
+#pragma nounroll
+        for (int st = 0; st < nst; st++) stage(st, std::integral_constant<int, -1>{});
     }
 }
 

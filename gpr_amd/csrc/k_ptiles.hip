@@ -125,8 +125,10 @@ __device__ __forceinline__ void tile_gemm(T* __restrict__ C, int64_t ldc, const 
 // reads, 384 DMA'd rows per stage for twice the 128 x 128 tile's flops; probe 0.901 of the f64
 // MFMA bound against 0.877, f32 0.857 against 0.818, profiles/r05u).  Its 128 accumulator
 // registers fit the task loop because the C tile is not prefetched into registers beside them,
-// as tile_gemm does: the accumulators START from -C (loads issued before the first stage's DMAs,
-// their latency under the ring's fill), and -acc = C - A B^T is stored.  Off-diagonal tiles only.
+// as tile_gemm does: C comes in four column chunks during the first stages and is subtracted
+// from the accumulators (tile_mma_tall Csub), and -acc = C - A B^T is stored.  (Starting the
+// accumulators from -C held the first MFMA for the whole 256 KB read: C3's launch lost 0.4 ms.)
+// Off-diagonal tiles only.
 // ------------------------------------------------------------------------------------------
 template <typename T>
 __device__ __forceinline__ void tile_gemm_tall(T* __restrict__ C, int64_t ldc, const T* __restrict__ A, int64_t lda,
@@ -136,15 +138,7 @@ __device__ __forceinline__ void tile_gemm_tall(T* __restrict__ C, int64_t ldc, c
     const int lane = t & 63, w = t >> 6;
     const int wr = w & 3, wc = w >> 2, lr = lane & 15, lk = lane >> 4;
     acc_t acc[4][4];
-#pragma unroll
-    for (int x = 0; x < 4; x++)
-#pragma unroll
-        for (int reg = 0; reg < 4; reg++) {
-            const T* ccol = C + (int64_t)(64 * wc + 16 * x + Tr::orow(lk, reg)) * ldc;
-#pragma unroll
-            for (int y = 0; y < 4; y++) acc[x][y][reg] = -ccol[64 * wr + 16 * y + lr];
-        }
-    mm::tile_mma_tall<T, 1, true>(acc, A, lda, B, ldb, K, smem, t);
+    mm::tile_mma_tall<T, 1>(acc, A, lda, B, ldb, K, smem, t, C, ldc);
 #pragma unroll
     for (int x = 0; x < 4; x++)
 #pragma unroll
@@ -2694,6 +2688,9 @@ struct Cost {  // per-task durations (us, one CU), calibrated from GPRX_PT_TRACE
     // a paired update (T_UPD2) per panel, relative to two single-tile panels (the 256 x 128
     // mainloop's probe rate against the 128 x 128 tile's: 0.877 / 0.901)
     double tall = 0.975;
+    // which chunks pair (make_schedule pair > 0): at least pair_nbmin panels wide, in the columns
+    // before the last pair_tail (GPRX_PT_PAIR_NBMIN / GPRX_PT_PAIR_TAIL)
+    int pair_nbmin = 1, pair_tail = 0;
 };
 
 // TPART tickets of one k in the order TPART(k, np-1), .., (k, 0): each part waits for
@@ -2877,7 +2874,8 @@ static Schedule make_schedule(int nc, int nr, int W, int near, int P, const Cost
         }
         if (k + 1 < nc) make_diagx(k + 1);
         for (const Chunk& c : by_last[k]) {
-            const int role = pair_role(c.i, c.j);
+            const bool pairable = c.nb >= cm.pair_nbmin && c.j < nc - cm.pair_tail;
+            const int role = pairable ? pair_role(c.i, c.j) : 0;
             if (role == 2) continue;  // (the pair's top row made the task: identical chunks)
             if (role == 1) {
                 const int id = add(T_UPD2, c.i, c.j, c.b0, c.nb, cm.ovh + 2.0 * c.nb * cm.k128 * cm.tall);
@@ -3272,7 +3270,7 @@ struct Params {
     int ratio = -1;         // chunk-width rule of tile_chunks: < 0 picked per shape by the simulation
     int split = 1;          // f64: the split diagonal step (TPART tasks); GPRX_PT_SPLIT=0 turns it off
     int tail = 0;           // > 0: the capped chunk rule only in the last `tail` column blocks
-    int pair = -1;          // paired updates (make_schedule): < 0 picked per shape by the simulation,
+    int pair = -1;          // paired updates (make_schedule): < 0 the precision's default (default_pair),
                             // 0 off, n > 0 pairs from row j + n (GPRX_PT_PAIR)
     Cost cm;
     int near_for(int nc) const { return near >= 0 ? near : (nc <= 64 ? 1 : 0); }
@@ -3289,6 +3287,8 @@ struct Params {
         if (const char* e = std::getenv("GPRX_PT_TAIL")) tail = std::atoi(e);
         if (const char* e = std::getenv("GPRX_PT_PAIR")) pair = std::atoi(e);
         if (const char* e = std::getenv("GPRX_PT_TALL")) cm.tall = std::atof(e);
+        if (const char* e = std::getenv("GPRX_PT_PAIR_NBMIN")) cm.pair_nbmin = std::max(1, std::atoi(e));
+        if (const char* e = std::getenv("GPRX_PT_PAIR_TAIL")) cm.pair_tail = std::max(0, std::atoi(e));
         if (const char* e = std::getenv("GPRX_PT_TPART_US")) cm.tpart = std::atof(e);
         if (const char* e = std::getenv("GPRX_PT_DIAGXS_US")) cm.diagx_s = std::atof(e);
         if (const char* e = std::getenv("GPRX_PT_TPARTP_US")) cm.tpart_prog = std::atof(e);
@@ -3313,17 +3313,19 @@ static const Params& params() {
 // simulation ranks it first too) -- unless GPRX_PT_RATIO fixes it (GPRX_PT_TAIL its reach)
 static const int kRatios[] = {0, 8, 4, 2};
 static const int kTails[] = {0, 16, 32};
-// Paired updates (T_UPD2): off, or pairs from 1 / 2 / 4 rows below the diagonal, whichever the
-// simulation ranks first (pairing halves the task count and runs the wider mainloop, but a pair
-// holds back both tiles' consumers until the later of the two rows is final)
-static const int kPairs[] = {0, 1, 2, 4};
+// Paired updates (T_UPD2) by precision, measured (same-box A/Bs, profiles/r06f_pair_ab.txt):
+// f32 pairs from row j + 4 (C4's factor 99.6 -> 96.3 ms: the f32 mainloop is bound by its LDS
+// fragment reads, which the 64 x 64 wave blocks cut by a third); f64 none (C3's launch 25.57 ->
+// 25.94 / 26.08 / 26.28 ms with pairs from row j + 4 / 2 / 1: the C tile, which a single update
+// prefetches into registers under its mainloop, must land before a pair's first MFMA).
+// GPRX_PT_PAIR fixes it for both.
+static int default_pair(bool f64) { return f64 ? 0 : 4; }
 static Schedule best_schedule(int nc, int nr, const Params& pr, int P, bool build, int ni, bool split, bool f64) {
     const Cost cm = pr.cost(f64);
     Schedule best;
     bool have = false;
-    for (int pq : kPairs) {
-        if (pr.pair >= 0 && pq != pr.pair) continue;
-        if (pr.pair < 0 && pq && pq >= nc - 1) continue;
+    const int want = pr.pair >= 0 ? pr.pair : default_pair(f64);
+    for (int pq : {want}) {
         auto consider = [&](Schedule&& S) {
             // a rule with more tasks (or the paired form) must win by > 0.5%
             if (!have || S.est_us < best.est_us * 0.995) {
@@ -3341,7 +3343,6 @@ static Schedule best_schedule(int nc, int nr, const Params& pr, int P, bool buil
                 consider(make_schedule(nc, nr, pr.W, pr.near_for(nc), P, cm, build, ni, r, split, tl, pq));
             }
     }
-    if (pr.pair > 0 && !have) return make_schedule(nc, nr, pr.W, pr.near_for(nc), P, cm, build, ni, 0, split, 0, pr.pair);
     return best;
 }
 

@@ -552,6 +552,19 @@ class Model:
         _check(st, self.ctx.h)
 
     def set_data(self, X, Y):
+        """X (n x d), Y (n x m): host arrays, or DeviceArrays of this context (read in HBM,
+        gprx_model_set_data takes host or device memory; a kernel with no device form then needs
+        host arrays)."""
+        if isinstance(X, DeviceArray) or isinstance(Y, DeviceArray):
+            if not (isinstance(X, DeviceArray) and isinstance(Y, DeviceArray)) or X.dtype != self.dtype \
+                    or Y.dtype != self.dtype:
+                raise TypeError("set_data: X and Y both DeviceArrays of the model's dtype, or both host arrays")
+            n, d = X.shape
+            m = Y.shape[1] if len(Y.shape) > 1 else 1
+            self._c(lib().gprx_model_set_data(self.h, ctypes.c_void_p(X.p), ctypes.c_void_p(Y.p), n, d, m))
+            self.n, self.d, self.m = n, d, m
+            self._Xh = None
+            return
         X = np.ascontiguousarray(X, self.dtype)
         Y = np.ascontiguousarray(Y, self.dtype)
         if Y.ndim == 1:

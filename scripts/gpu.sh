@@ -146,7 +146,7 @@ for step in "$@"; do
                 if [ "$v" = "-" ]; then
                     timeout -k 10 300 python bench.py $Q > "$O/envab_base_$rep.json" 2> "$O/envab.err" || fail envab $? "$O/envab.err"
                 else
-                    env "$v" timeout -k 10 300 python bench.py $Q > "$O/envab_${b}_$rep.json" 2> "$O/envab.err" \
+                    env $(echo "$v" | tr "," " ") timeout -k 10 300 python bench.py $Q > "$O/envab_${b}_$rep.json" 2> "$O/envab.err" \
                         || fail envab $? "$O/envab.err"
                 fi
             done
@@ -173,6 +173,14 @@ for step in "$@"; do
         pmc_leg lml pmcl1_lml SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES \
             SQ_BUSY_CYCLES GRBM_GUI_ACTIVE
         python scripts/pmc_generic.py "$O/lml_pmc.json" "$O/pmcl1_lml"
+        ;;
+    pairtrace)  # bare factorisation timelines with and without paired updates (f64 16384, f32 32768)
+        for pr in 0 4; do
+            GPRX_PT_PAIR=$pr timeout -k 10 120 python scripts/pt_trace.py 16384 > "$O/pt16384_pair$pr.json" \
+                2> "$O/pt_pair.err" || fail pairtrace $? "$O/pt_pair.err"
+            GPRX_PT_PAIR=$pr PT_TRACE_DTYPE=0 timeout -k 10 180 python scripts/pt_trace.py 32768 > "$O/pt32768f_pair$pr.json" \
+                2> "$O/pt_pair.err" || fail pairtrace $? "$O/pt_pair.err"
+        done
         ;;
     fittrace)  # the C3 fit's tile timeline (fused build), for the launch decomposition
         PT_TRACE_FIT=1 PT_TRACE_OUT="$O/pt_fit16384.npz" timeout -k 10 120 python scripts/pt_trace.py 16384 \

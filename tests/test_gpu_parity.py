@@ -280,3 +280,23 @@ def test_distributed_fit_one_rank(dtype, n):
         Md.close()
     finally:
         dctx.close()
+
+
+def test_set_data_from_device_memory(ctx):
+    """gprx_model_set_data reads host or device memory (include/gprx.h conventions; ADVICE r05:
+    it copied with hipMemcpyHostToDevice only): the same data as DeviceArrays of the context gives
+    the same fit, bit for bit, as host arrays."""
+    import gpr_amd
+    ks = "SumKernel(GaussianKernel(2,0.15,),PeriodicKernel(0.1,3.141592653589793,1,))"
+    X, Y = make_data(700, 6)
+    M_h, _ = _fit(ctx, ks, X, Y, 0.5, np.float64)
+    M_d = gpr_amd.Model(ctx, np.float64)
+    M_d.set_data(ctx.device_array(X), ctx.device_array(Y))
+    M_d.set_kernel(ks)
+    M_d.set_noise(0.5)
+    M_d.fit()
+    assert np.array_equal(M_d.alpha(), M_h.alpha())
+    Xq = make_queries(33, 6)
+    assert np.array_equal(M_d.predict(Xq), M_h.predict(Xq))
+    M_d.close()
+    M_h.close()

@@ -298,7 +298,7 @@ def test_schedule_split_step_needs_eight_workers():
     assert len(lst) == _expected_tasks(9, 10) - tparts(9)
 
 
-def _sched_list(nc, nr, build=True, ratio=0, pair=0, ident=False):
+def _sched_list_pair(nc, nr, build=True, ratio=0, pair=0, ident=False):
     """The ticket list (gprx_dev_schedule_list); pair: paired updates from row j + pair (0 none)."""
     L = lib()
     L.gprx_dev_schedule_list.argtypes = [ctypes.c_int32] * 4 + [ctypes.c_void_p, ctypes.c_int64]
@@ -320,7 +320,7 @@ def test_schedule_paired_updates(nc, pair):
     nr = nc + 1
     st, n, est = _sched(nc, nr, build=True)
     assert st == 0
-    L = _sched_list(nc, nr, pair=pair)
+    L = _sched_list_pair(nc, nr, pair=pair)
     typ, nb = L[:, 0] & 0xFF, L[:, 0] >> 8
     ii, jj, b0 = L[:, 1], L[:, 2], L[:, 3]
     # per tile: the (b0, nb) chunks in ticket order
@@ -339,7 +339,7 @@ def test_schedule_paired_updates(nc, pair):
             pos += k
         assert pos == e, (r, j, ch)
     # the pairs replace two single tasks each: fewer tickets than the unpaired schedule
-    L0 = _sched_list(nc, nr, pair=0)
+    L0 = _sched_list_pair(nc, nr, pair=0)
     n_upd0 = int(((L0[:, 0] & 0xFF) == 2).sum())
     n_pairs = int((typ == 5).sum())
     assert int((typ == 2).sum()) + 2 * n_pairs == n_upd0
