@@ -3313,18 +3313,25 @@ static const Params& params() {
 // simulation ranks it first too) -- unless GPRX_PT_RATIO fixes it (GPRX_PT_TAIL its reach)
 static const int kRatios[] = {0, 8, 4, 2};
 static const int kTails[] = {0, 16, 32};
-// Paired updates (T_UPD2) by precision, measured (same-box A/Bs, profiles/r06f_pair_ab.txt):
-// f32 pairs from row j + 4 (C4's factor 99.6 -> 96.3 ms: the f32 mainloop is bound by its LDS
-// fragment reads, which the 64 x 64 wave blocks cut by a third); f64 none (C3's launch 25.57 ->
-// 25.94 / 26.08 / 26.28 ms with pairs from row j + 4 / 2 / 1: the C tile, which a single update
-// prefetches into registers under its mainloop, must land before a pair's first MFMA).
-// GPRX_PT_PAIR fixes it for both.
-static int default_pair(bool f64) { return f64 ? 0 : 4; }
+// Paired updates (T_UPD2) by precision, from same-box A/Bs (profiles/r06f_pair_ab.txt,
+// r06lno_pair_sweep.txt): rows from j + 4, chunks of at least 4 panels, not in the last 32 (f64) /
+// 16 (f32) columns -- C3's launch 25.49-25.63 -> 24.68-24.72 ms (pairing every chunk: 25.77; every
+// chunk of >= 16 panels before the last 64 columns: 25.01-25.07), C4's f32 factor 99.26 ->
+// 95.28-95.37 ms.  Pairs delay their consumers (both rows wait for the later one), which the
+// narrow pieces near a tile's last panel and the chain-bound last columns cannot afford; the bulk
+// gains the wider mainloop.  GPRX_PT_PAIR / _NBMIN / _TAIL override.
+struct PairRule {
+    int pair, nbmin, tail;
+};
+static PairRule default_pair(bool f64) { return f64 ? PairRule{4, 4, 32} : PairRule{4, 4, 16}; }
 static Schedule best_schedule(int nc, int nr, const Params& pr, int P, bool build, int ni, bool split, bool f64) {
-    const Cost cm = pr.cost(f64);
+    Cost cm = pr.cost(f64);
+    const PairRule pd = default_pair(f64);
+    if (!std::getenv("GPRX_PT_PAIR_NBMIN")) cm.pair_nbmin = pd.nbmin;
+    if (!std::getenv("GPRX_PT_PAIR_TAIL")) cm.pair_tail = pd.tail;
     Schedule best;
     bool have = false;
-    const int want = pr.pair >= 0 ? pr.pair : default_pair(f64);
+    const int want = pr.pair >= 0 ? pr.pair : pd.pair;
     for (int pq : {want}) {
         auto consider = [&](Schedule&& S) {
             // a rule with more tasks (or the paired form) must win by > 0.5%

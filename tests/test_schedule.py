@@ -12,15 +12,16 @@ import pytest
 from gpr_amd.gprx import lib
 
 
-def _sched(nc, nr, P=256, build=False, ident=False, ratio=0):
+def _sched(nc, nr, P=256, build=False, ident=False, ratio=0, pair=0):
     """ratio: the chunk rule (0 = the fixed rule, r > 0 = width capped at r x the panels left,
-    None = the rule the simulated makespan picks)."""
+    None = the rule the simulated makespan picks); pair: paired updates from row j + pair (0 =
+    none, None = the f64 default, k_ptiles.hip default_pair)."""
     L = lib()
     L.gprx_dev_schedule.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                     ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]
     est = ctypes.c_double()
     n = ctypes.c_int64()
-    sel = 0 if ratio is None else (ratio + 1) << 8
+    sel = (0 if ratio is None else (ratio + 1) << 8) | (0 if pair is None else (pair + 1) << 16)
     st = L.gprx_dev_schedule(nc, nr, P, (1 if build else 0) | (2 if ident else 0) | sel, ctypes.byref(est),
                              ctypes.byref(n))
     return st, n.value, est.value
@@ -299,12 +300,14 @@ def test_schedule_split_step_needs_eight_workers():
 
 
 def _sched_list_pair(nc, nr, build=True, ratio=0, pair=0, ident=False):
-    """The ticket list (gprx_dev_schedule_list); pair: paired updates from row j + pair (0 none)."""
+    """The ticket list (gprx_dev_schedule_list); pair: paired updates from row j + pair (0 none,
+    None the default rule); ratio None: the simulation's chunk rule."""
     L = lib()
     L.gprx_dev_schedule_list.argtypes = [ctypes.c_int32] * 4 + [ctypes.c_void_p, ctypes.c_int64]
     L.gprx_dev_schedule_list.restype = ctypes.c_int64
     out = np.zeros((400000, 4), np.int32)
-    flags = (1 if build else 0) | (2 if ident else 0) | ((ratio + 1) << 8) | ((pair + 1) << 16)
+    flags = ((1 if build else 0) | (2 if ident else 0) | (0 if ratio is None else (ratio + 1) << 8)
+             | (0 if pair is None else (pair + 1) << 16))
     n = L.gprx_dev_schedule_list(nc, nr, 256, flags, out.ctypes.data, out.shape[0])
     assert n > 0
     return out[:n]
@@ -360,3 +363,18 @@ def test_schedule_paired_updates(nc, pair):
                 if p is None and r == b + 1:  # L_{b+1,b}: published by DIAGX(b + 1) (or its parts)
                     p = final.get((r, r))
                 assert p is not None and p < q, (q, r, b)
+
+
+def test_schedule_default_pairing_rule():
+    """The f64 default (k_ptiles.hip default_pair: rows from j + 4, chunks of >= 4 panels, not in
+    the last 32 columns) at C3's shape: a valid ticket order with paired tasks, none of them in the
+    last 32 column blocks or narrower than 4 panels; at C2's shape (32 column blocks) no pairs."""
+    st, n, est = _sched(128, 129, build=True, ratio=None, pair=None)
+    assert st == 0 and n > 0
+    L = _sched_list_pair(128, 129, ratio=None, pair=None)
+    typ, nb, jj = L[:, 0] & 0xFF, L[:, 0] >> 8, L[:, 2]
+    p = typ == 5
+    assert p.sum() > 1000
+    assert np.all(jj[p] < 128 - 32) and np.all(nb[p] >= 4)
+    L2 = _sched_list_pair(32, 33, ratio=None, pair=None)
+    assert not np.any((L2[:, 0] & 0xFF) == 5)
