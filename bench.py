@@ -268,6 +268,24 @@ def mfma_from_profile(leg, kernels):
     return None
 
 
+def predict_pmc_from_profile():
+    """The predict kernel's issue split from the newest committed PMC passes
+    (profiles/<tag>_predict_pmc.json, scripts/pmc_generic.py): MFMA busy and VALU issue as
+    fractions of the SIMD-cycles, the wait split of the wave-cycles, LDS bank conflicts."""
+    for path in reversed(_tagged("*_predict_pmc.json")):
+        try:
+            with open(path) as f:
+                ks = json.load(f)["kernels"]
+            k = next((v for n, v in ks.items() if n.startswith("predict_mma_kernel")), None)
+        except Exception:
+            continue
+        if k:
+            keys = ("mfma_busy_frac", "valu_active_frac", "wait_inst_frac", "wait_any_frac", "active_any_frac",
+                    "lds_conflict_frac", "clock_ghz", "dur_ms_mean")
+            return dict({x: k.get(x) for x in keys}, source=os.path.basename(path))
+    return None
+
+
 def make_dist_context(gpr_amd, group, rank, world, local_rank, shared):
     """The multi-process context of the sharded fit: an RCCL communicator over the GPUs
     (gprx_ctx_create_dist, nonblocking initialisation with a deadline), or, when any rank's
@@ -825,8 +843,17 @@ def main():
             pred["roofline_tree"] = {"bound": "mfma+valu (serial)", "t_roof_ms": 1e3 * t_roof,
                                      "t_device_ms": pms, "frac": 1e3 * t_roof / pms,
                                      "mfma_flop_per_pair": 6.0 * d, "valu_ops_per_pair": 28.0}
+            # the same tree bound with the f64 VALU at the issue cost the PMC passes measure on
+            # this kernel (7.3 cycles per f64 VALU instruction, the spec's rate
+            # assumes 4), i.e. at half the spec's FMA rate; the f64 VALU ops per pair after the
+            # folded exp: ~25
+            t_issue = pairs * 6.0 * d / (PEAK_FP64_TFLOPS * 1e12) + pairs * 25.0 / (PEAK_FP64_TFLOPS / 4 * 1e12)
+            pred["roofline_tree_issue"] = {"bound": "mfma + valu at the measured f64 issue cost (serial)",
+                                           "t_roof_ms": 1e3 * t_issue, "frac": 1e3 * t_issue / pms,
+                                           "valu_ops_per_pair": 25.0, "valu_rate": "half the spec f64 FMA rate"}
             if world == 1:
                 pred["rocprof"] = rocprof_from_profile("predict", ("predict_mma_kernel<double, 1, true>",), 1e3 * pms)
+                pred["pmc"] = predict_pmc_from_profile()
         if rank == 0 and world == 1 and args.cpu_predict_q > 0:
             try:
                 pred["cpu_baseline"] = cpu_predict_baseline(cfg, X, model.alpha(), args.cpu_predict_q)

@@ -77,6 +77,12 @@ for step in "$@"; do
         pmc_leg build pmcw_build WRITE_SIZE
         pmc_leg c3 pmcm_c3 SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE
         pmc_leg c4 pmcm_c4 SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE
+        # the predict kernel's issue split (bench.py attaches it as predict.pmc)
+        pmc_leg predict pmcp1_predict SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS \
+            SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE
+        pmc_leg predict pmcp2_predict SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_IDX_ACTIVE \
+            SQ_VALU_MFMA_COEXEC_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE
+        python scripts/pmc_generic.py "$O/predict_pmc.json" "$O/pmcp1_predict" "$O/pmcp2_predict" --kernel predict
         ;;
     shared)
         GPRX_DIST_SHARED_GPU=1 timeout -k 10 500 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \

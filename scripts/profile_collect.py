@@ -35,6 +35,10 @@ def main():
             subprocess.check_call([sys.executable, os.path.join(ROOT, "scripts", "pmc_traffic.py"), f, w,
                                    os.path.join(dst, f"{tag}_{leg}_pmc_traffic.json")], stdout=subprocess.DEVNULL)
             print("traffic", leg)
+    pp = os.path.join(src, "predict_pmc.json")  # (scripts/pmc_generic.py: the predict kernel's issue split)
+    if os.path.isfile(pp):
+        shutil.copy(pp, os.path.join(dst, f"{tag}_predict_pmc.json"))
+        print("pmc predict")
     for leg in ("c3", "c4"):
         m = os.path.join(src, f"pmcm_{leg}")
         if os.path.isdir(m):
