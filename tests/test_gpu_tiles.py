@@ -149,3 +149,39 @@ def test_predict_at_training_points(ctx, ks):
     assert np.all(np.isfinite(p))
     assert relerr(p, O.predict(ks, X, a_ref, Xq, np.float64)) <= 1e-6
     M.close()
+
+
+_TALL_CHILD = r"""
+import sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+import gpr_amd
+from gpr_amd.synth import make_data, make_queries
+ctx = gpr_amd.Context(0)
+X, Y = make_data(8192, 8)
+M = gpr_amd.Model(ctx, np.float64)
+M.set_data(X, Y)
+M.set_kernel("GaussianKernel(1.3,1,)")
+M.set_noise(0.5)
+M.fit()
+np.save(sys.argv[2], M.posterior_cov(make_queries(4096, 8), make_queries(4096, 8)))
+"""
+
+
+def test_posterior_tall_gemms_match_128_tiles(tmp_path):
+    """The posterior variance's bulk GEMMs on the 256 x 128 tile (k_syrk.hip gemm_tall_kernel,
+    its refill DMAs spread behind the MFMAs for f64) against the 128 x 128 tile
+    (GPRX_GEMM_TALL=0) at a size that routes to them (Q = 4096, N = 8192): the same sums in the
+    same k order, so the variances agree to the last bit."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    outs = []
+    for tag, env in (("on", {}), ("off", {"GPRX_GEMM_TALL": "0"})):
+        f = tmp_path / f"v_{tag}.npy"
+        r = subprocess.run([sys.executable, "-c", _TALL_CHILD, root, str(f)], env=dict(os.environ, **env),
+                           capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, r.stderr[-2000:]
+        outs.append(np.load(f))
+    assert np.array_equal(outs[0], outs[1])
