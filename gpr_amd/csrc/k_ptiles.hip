@@ -3314,16 +3314,17 @@ static const Params& params() {
 static const int kRatios[] = {0, 8, 4, 2};
 static const int kTails[] = {0, 16, 32};
 // Paired updates (T_UPD2) by precision, from same-box A/Bs (profiles/r06f_pair_ab.txt,
-// r06lno_pair_sweep.txt): rows from j + 4, chunks of at least 4 panels, not in the last 32 (f64) /
-// 16 (f32) columns -- C3's launch 25.49-25.63 -> 24.68-24.72 ms (pairing every chunk: 25.77; every
-// chunk of >= 16 panels before the last 64 columns: 25.01-25.07), C4's f32 factor 99.26 ->
-// 95.28-95.37 ms.  Pairs delay their consumers (both rows wait for the later one), which the
+// r06lno_pair_sweep.txt, r06uv_pair_tune.txt): rows from j + 4 (f64) / j + 2 (f32), chunks of at
+// least 4 panels, not in the last 32 (f64) / 16 (f32) columns -- C3's launch 25.49-25.63 ->
+// 24.68-24.85 ms (pairing every chunk: 25.77; every chunk of >= 16 panels before the last 64
+// columns: 25.01-25.07; rows from j + 3 or j + 6, >= 2 panels, the last 24 or 40 columns: within
+// 0.3% of the default), C4's f32 factor 99.26 -> 95.23-95.26 ms (rows from j + 4: 95.5).  Pairs delay their consumers (both rows wait for the later one), which the
 // narrow pieces near a tile's last panel and the chain-bound last columns cannot afford; the bulk
 // gains the wider mainloop.  GPRX_PT_PAIR / _NBMIN / _TAIL override.
 struct PairRule {
     int pair, nbmin, tail;
 };
-static PairRule default_pair(bool f64) { return f64 ? PairRule{4, 4, 32} : PairRule{4, 4, 16}; }
+static PairRule default_pair(bool f64) { return f64 ? PairRule{4, 4, 32} : PairRule{2, 4, 16}; }
 static Schedule best_schedule(int nc, int nr, const Params& pr, int P, bool build, int ni, bool split, bool f64) {
     Cost cm = pr.cost(f64);
     const PairRule pd = default_pair(f64);
