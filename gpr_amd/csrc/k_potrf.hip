@@ -484,11 +484,17 @@ void launch_gemm_nt(T* C, int64_t ldc, const T* A, int64_t lda, const T* B, int6
     }();
     const int64_t ntm = M / GT, ntn = N / GT;
     const int64_t nt128 = lower ? ntn * (ntn + 1) / 2 + (ntm - ntn) * ntn : ntm * ntn;
-    // bulk rectangular products: the 256 x 128 tile (half the workgroups of the 128 tile, which
-    // must still fill the chip twice over)
+    // in place (C = A B^T over A's own columns: the row solves' diagonal-block products, k_predict.hip
+    // trsm_rows, k_lml.hip, the panel TRSM below): every workgroup must own WHOLE rows, so that no
+    // other workgroup still reads the columns it overwrites -- with 64 x 64 tiles the workgroup of
+    // columns 64..127 could read columns 0..63 after its neighbour stored them (an intermittent
+    // error in a 64-row block of the result).  128 columns at most, the 128 (or 256) row tile.
+    const bool inplace = (const void*)C == (const void*)A;
+    GPRX_REQUIRE(!inplace || (ldc == lda && N <= GT && !lower), GPRX_ERR_ARG,
+                 "gprx: launch_gemm_nt in place needs ldc == lda, N <= 128, a full product");
     if (!lower && nt128 >= 2 * small_tiles && launch_gemm_tall<T>(C, ldc, A, lda, B, ldb, M, N, K, alpha, beta, s))
         return;
-    if (nt128 < small_tiles)
+    if (nt128 < small_tiles && !inplace)
         gemm_launch<T, 64>(C, ldc, A, lda, B, ldb, M, N, K, alpha, beta, lower, s);
     else
         gemm_launch<T, 128>(C, ldc, A, lda, B, ldb, M, N, K, alpha, beta, lower, s);

@@ -2720,6 +2720,9 @@ struct Schedule {
     std::vector<int4> list;
     double est_us = 0;
     int64_t ntasks = 0;
+    // identity rows paired (make_schedule): an odd identity row block 2s + 1 starts its updates at
+    // panel 2s with its partner -- its counters start there and its tile at column 2s is zeroed
+    bool ident_even = false;
 };
 
 // Chunks of the updates of tile (i, j): b in [0, e), e = j (i > j) or j - 1 (diagonal tile:
@@ -2781,9 +2784,34 @@ static Schedule make_schedule(int nc, int nr, int W, int near, int P, const Cost
     if (split) cm.early = cm.early_s;
     const int nr0 = nr - ni;
     auto start_of = [&](int i) { return i >= nr0 ? i - nr0 : 0; };
+    // identity rows in pairs (E_2s, E_2s+1): both update from panel 2s -- the bottom row's block at
+    // column 2s is a stored zero (potrf_tiles zeroes it and starts its counters at 2s), so its
+    // one extra panel subtracts nothing and the two rows' chunk lists are identical
+    static const bool id_pair = [] {
+        const char* e = std::getenv("GPRX_PT_IDPAIR");  // 0: identity rows single (A/B)
+        return !(e && std::atoi(e) == 0);
+    }();
+    const bool ident_even = id_pair && pair > 0 && ni > 1;
+    // identity pairs in the last pair_tail columns too (the tail rule spares the factor's
+    // chain-bound last columns; the identity rows' updates there are bulk work): LML N = 8192
+    // 73.66 -> 73.05 ms with both (profiles/r06z_idpair_ab.txt); GPRX_PT_IDTAIL=0 restricts them
+    static const bool id_tail = [] {
+        const char* e = std::getenv("GPRX_PT_IDTAIL");
+        return !(e && std::atoi(e) == 0);
+    }();
+    auto cstart = [&](int i) {
+        const int a = start_of(i);
+        return (ident_even && i >= nr0) ? a - (a & 1) : a;
+    };
     // row i of column j: 1 the top of a pair, 2 its bottom, 0 single
     auto pair_role = [&](int i, int j) {
-        if (pair <= 0 || i >= nr0) return 0;
+        if (pair <= 0) return 0;
+        if (i >= nr0) {  // identity rows: (E_2s, E_2s+1)
+            const int a = i - nr0;
+            if (!ident_even) return 0;
+            if ((a & 1) == 0) return a + 1 < ni ? 1 : 0;
+            return 2;
+        }
         const int r0 = j + pair;
         if (i >= r0 && (i - r0) % 2 == 0 && i + 1 < nr0) return 1;
         if (i - 1 >= r0 && (i - 1 - r0) % 2 == 0) return 2;
@@ -2827,7 +2855,7 @@ static Schedule make_schedule(int nc, int nr, int W, int near, int P, const Cost
         std::vector<std::pair<int, int>> ch;
         for (int j = 1; j < nc; j++)
             for (int i = j; i < nr; i++) {
-                tile_chunks(i, j, W, near, ch, start_of(i), (tail <= 0 || j >= nc - tail) ? ratio : 0);
+                tile_chunks(i, j, W, near, ch, cstart(i), (tail <= 0 || j >= nc - tail) ? ratio : 0);
                 for (auto& c : ch) by_last[c.first + c.second - 1].push_back(Chunk{i, j, c.first, c.second});
             }
     }
@@ -2874,7 +2902,7 @@ static Schedule make_schedule(int nc, int nr, int W, int near, int P, const Cost
         }
         if (k + 1 < nc) make_diagx(k + 1);
         for (const Chunk& c : by_last[k]) {
-            const bool pairable = c.nb >= cm.pair_nbmin && c.j < nc - cm.pair_tail;
+            const bool pairable = c.nb >= cm.pair_nbmin && (c.j < nc - cm.pair_tail || (c.i >= nr0 && id_tail));
             const int role = pairable ? pair_role(c.i, c.j) : 0;
             if (role == 2) continue;  // (the pair's top row made the task: identical chunks)
             if (role == 1) {
@@ -2968,6 +2996,7 @@ static Schedule make_schedule(int nc, int nr, int W, int near, int P, const Cost
     }
     S.est_us = now;
     S.ntasks = nt;
+    S.ident_even = ident_even;
     if (split) order_tparts(S.list);
     return S;
 }
@@ -3368,6 +3397,7 @@ struct PtState {
         int4* list = nullptr;
         int64_t n = 0;
         double est_us = 0;
+        bool ident_even = false;  // (Schedule::ident_even)
         std::vector<int4> host;
     };
     std::map<std::tuple<int, int, bool, int, bool, int>, Dev> sched;  // (nc, nr, fused, ni, split, sizeof(T))
@@ -3440,19 +3470,26 @@ __global__ void pt_init_counters(int* __restrict__ ctr, int64_t n, int64_t v0, i
 
 // counters of the identity row blocks (the inverse riding along): block a = i - nr0 has its
 // first a panels "applied" (they are zero) and its first a L blocks "final"
-__global__ void pt_init_identity_counters(int* __restrict__ lcnt, int* __restrict__ ver, int nc, int nr0, int ni) {
+// (even: the schedule pairs the identity rows, Schedule::ident_even -- an odd block's updates,
+// and so its ver counters, start one panel early)
+__global__ void pt_init_identity_counters(int* __restrict__ lcnt, int* __restrict__ ver, int nc, int nr0, int ni,
+                                          int even) {
     const int a = blockIdx.x, j = threadIdx.x;
     if (a >= ni) return;
     if (j == 0) lcnt[nr0 + a] = a;
-    for (int c = j; c < nc; c += blockDim.x) ver[(int64_t)(nr0 + a) * nc + c] = a;
+    const int v = even ? a - (a & 1) : a;
+    for (int c = j; c < nc; c += blockDim.x) ver[(int64_t)(nr0 + a) * nc + c] = v;
 }
 
-// identity rows: A[row0 + r][c] = (r == c) for the columns at or right of r's block
+// identity rows: A[row0 + r][c] = (r == c) for the columns at or right of r's block (even: an
+// odd block from the block left of its own, a zero tile its paired updates read)
 template <typename T>
-__global__ void pt_init_identity_rows(T* __restrict__ A, int64_t ld, int64_t row0, int64_t nid, int64_t ncol) {
+__global__ void pt_init_identity_rows(T* __restrict__ A, int64_t ld, int64_t row0, int64_t nid, int64_t ncol,
+                                      int even) {
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t c = blockIdx.y;
-    if (r >= nid || c >= ncol || c < (r / GT) * GT) return;
+    const int64_t rb = r / GT, c0 = (even ? rb - (rb & 1) : rb) * GT;
+    if (r >= nid || c >= ncol || c < c0) return;
     A[row0 + r + c * ld] = (r == c) ? T(1) : T(0);
 }
 
@@ -3491,6 +3528,7 @@ void potrf_tiles(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info
         PtState::Dev d;
         d.n = (int64_t)S.list.size();
         d.est_us = S.est_us;
+        d.ident_even = S.ident_even;
         GPRX_HIP(hipMalloc(&d.list, sizeof(int4) * std::max<int64_t>(1, d.n)));
         GPRX_HIP(hipMemcpy(d.list, S.list.data(), sizeof(int4) * d.n, hipMemcpyHostToDevice));
         d.host = S.list;
@@ -3516,9 +3554,9 @@ void potrf_tiles(T* A, int64_t ld, int64_t np, int64_t nrows, T* Linv, int* info
     }
     if (ni > 0) {
         hipLaunchKernelGGL(pt_init_identity_counters, dim3((unsigned)ni), dim3(128), 0, s, st.ctr + C_NCTL,
-                           st.ctr + C_NCTL + nr, nc, nr - ni, ni);
+                           st.ctr + C_NCTL + nr, nc, nr - ni, ni, sd.ident_even ? 1 : 0);
         hipLaunchKernelGGL(pt_init_identity_rows<T>, dim3((unsigned)((ni * (int64_t)GT + 255) / 256), (unsigned)np),
-                           dim3(256), 0, s, A, ld, (int64_t)(nr - ni) * GT, (int64_t)ni * GT, np);
+                           dim3(256), 0, s, A, ld, (int64_t)(nr - ni) * GT, (int64_t)ni * GT, np, sd.ident_even ? 1 : 0);
     }
     Args<T> a;
     a.A = A;

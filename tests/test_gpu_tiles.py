@@ -185,3 +185,24 @@ def test_posterior_tall_gemms_match_128_tiles(tmp_path):
         assert r.returncode == 0, r.stderr[-2000:]
         outs.append(np.load(f))
     assert np.array_equal(outs[0], outs[1])
+
+
+@pytest.mark.gpu
+def test_posterior_repeatable_in_place_solves():
+    """The row solves' diagonal-block products run in place (k_predict.hip trsm_rows: R_k =
+    R_k Linv_k^T); launch_gemm_nt keeps them on whole-row tiles (k_potrf.hip), since with 64 x 64
+    tiles the workgroup of columns 64..127 could read columns its neighbour had already
+    overwritten -- an intermittent error in a 64-query block (seen once in ~150 processes at
+    N = 8192, Q = 4096).  Repeated variances of one fit agree to the last bit."""
+    from gpr_amd.synth import make_data, make_queries
+    ctx = gpr_amd.Context(0)
+    X, Y = make_data(8192, 8)
+    M = gpr_amd.Model(ctx, np.float64)
+    M.set_data(X, Y)
+    M.set_kernel("GaussianKernel(1.3,1,)")
+    M.set_noise(0.5)
+    M.fit()
+    Q = make_queries(4096, 8)
+    v0 = M.posterior_cov(Q, Q)
+    for _ in range(6):
+        assert np.array_equal(M.posterior_cov(Q, Q), v0)

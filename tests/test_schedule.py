@@ -378,3 +378,60 @@ def test_schedule_default_pairing_rule():
     assert np.all(jj[p] < 128 - 32) and np.all(nb[p] >= 4)
     L2 = _sched_list_pair(32, 33, ratio=None, pair=None)
     assert not np.any((L2[:, 0] & 0xFF) == 5)
+
+
+@pytest.mark.parametrize("nc,pair", [(3, 1), (9, 2), (40, 4), (65, 4)])
+def test_schedule_paired_identity_rows(nc, pair):
+    """The LML mode with pairs (k_ptiles.hip make_schedule ident_even): identity row blocks go
+    in pairs (E_2s, E_2s+1), both updating from panel 2s -- the odd row's block at column 2s is
+    the zero tile potrf_tiles stores, so it has no producer; every other tile's panels are applied
+    once, in order, after their operands are final; the odd rows' TRSMs still start at their own
+    block; the ticket order is valid (simulated) and has paired identity-row tasks."""
+    nr = 2 * nc + 1
+    nr0 = nc + 1
+    st, n, est = _sched(nc, nr, build=True, ident=True, pair=pair)
+    assert st == 0
+    L = _sched_list_pair(nc, nr, pair=pair, ident=True)
+    typ, nb = L[:, 0] & 0xFF, L[:, 0] >> 8
+    ii, jj, b0 = L[:, 1], L[:, 2], L[:, 3]
+    applied = {}
+    for q in np.where((typ == 2) | (typ == 5))[0]:
+        rows = [ii[q]] if typ[q] == 2 else [ii[q], ii[q] + 1]
+        if typ[q] == 5 and ii[q] >= nr0:
+            assert (ii[q] - nr0) % 2 == 0 and ii[q] + 1 < nr
+        for r in rows:
+            applied.setdefault((r, jj[q]), []).append((int(b0[q]), int(nb[q]), int(q)))
+    start = lambda r: 0 if r < nr0 else (r - nr0) - ((r - nr0) & 1)
+    for (r, j), ch in applied.items():
+        e = j - 1 if r == j else j
+        pos = start(r)
+        for b, k, q in ch:
+            assert b == pos, (r, j, ch)
+            pos += k
+        assert pos == e, (r, j, ch)
+    for a in range(nc):  # every identity tile right of the block gets its updates
+        for j in range(a + 1, nc):
+            assert (nr0 + a, j) in applied
+    if nc >= 9:
+        assert np.any((typ == 5) & (ii >= nr0))
+    trs = {(int(ii[q]), int(jj[q])) for q in np.where(typ == 1)[0]}
+    for a in range(nc):
+        assert {k for (r, k) in trs if r == nr0 + a} == set(range(a, nc))
+    final = {}
+    for q in range(len(L)):
+        if typ[q] == 1:
+            final[(ii[q], jj[q])] = q
+        elif typ[q] == 0:
+            final[(ii[q], ii[q])] = q
+    for q in np.where((typ == 5) | (typ == 2))[0]:
+        rows = (ii[q], jj[q]) if typ[q] == 2 else (ii[q], ii[q] + 1, jj[q])
+        for b in range(b0[q], b0[q] + nb[q]):
+            for r in rows:
+                if r >= nr0 and b == r - nr0 - 1 and (r - nr0) % 2 == 1:
+                    continue  # the zero tile (E_2s+1, 2s)
+                if r < nc and b == r:
+                    continue  # a diagonal tile's own panel is never an operand
+                p = final.get((r, b))
+                if p is None and r == b + 1:
+                    p = final.get((r, r))
+                assert p is not None and p < q, (q, r, b)
