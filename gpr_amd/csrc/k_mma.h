@@ -462,6 +462,88 @@ __device__ __forceinline__ void tile_mma(typename Mfma<T>::acc_t (&acc)[2][4], c
     }
 }
 
+// acc = A B^T for a lower-triangular B (128 x 128: B[c][k] = 0 for k > c, stored zeros) -- the
+// TRSM task's L_ik = A_ik Linv_k^T -- with the work even across the waves in EVERY stage.  Wave w
+// owns output rows 16 w .. 16 w + 15 across all 128 columns (eight 16-column groups g, acc[g >>
+// 2][g & 3]), so at stage st each wave multiplies exactly the groups the triangle leaves live
+// (16 g + 15 >= st BK): 36 of the full product's 64 group-stages for f64.  tile_mma's MAP 1
+// balances the SIMDs' totals but not each stage -- the stage barriers hold every wave to the
+// busiest, and its TRSM took 16 us against 15.4 us for a full update panel (the C3 fit trace,
+// profiles/r06fb_pt_trace_fit16384.json).  9 fragment reads per 8 MFMAs (MAP 1: 6); stages
+// unrolled (K = 128), so the live groups are compile-time.  The in-place call (C = A) is safe:
+// A comes through the staging ring, and the stores follow the last stage.
+// acc[x][y][reg] = C(row = 16 w + lr, col = 16 (4 x + y) + orow(lk, reg)).
+template <typename T>
+__device__ __forceinline__ void tile_mma_trirows(typename Mfma<T>::acc_t (&acc)[2][4], const T* __restrict__ A,
+                                                 int64_t lda, const T* __restrict__ B, int64_t ldb, T* smem,
+                                                 const int t) {
+    typedef Mfma<T> Tr;
+    typedef typename Tr::acc_t acc_t;
+    constexpr int BK = BkOf<T>::v;
+    typedef Stage<T, BK> S;
+    constexpr int NST = GT / BK;
+    const int lane = t & 63, w = t >> 6;
+    const int lr = lane & 15, lk = lane >> 4;
+    const int lcol = lane / S::LPC, lrow = S::src_row(lane);
+    auto issue = [&](int st) {
+        T* buf = smem + (st % S::NB) * S::STG;
+#pragma unroll
+        for (int u = 0; u < S::IPW; u++) {
+            const int g = w * S::IPW + u;
+            const bool isB = g >= S::GRP;
+            const int gg = isB ? g - S::GRP : g;
+            const int64_t col = (int64_t)st * BK + gg * S::CPI + lcol;
+            const T* src = isB ? (B + lrow + col * ldb) : (A + lrow + col * lda);
+            __builtin_amdgcn_global_load_lds((const void*)src,
+                                             (__attribute__((address_space(3))) void*)(buf + g * S::SRP), 16, 0, 0);
+        }
+    };
+#pragma unroll
+    for (int x = 0; x < 2; x++)
+#pragma unroll
+        for (int y = 0; y < 4; y++) acc[x][y] = acc_t{0};
+#pragma unroll
+    for (int p = 0; p < S::AH; p++)
+        if (p < NST) issue(p);
+    auto stage = [&](auto stc) {
+        constexpr int st = decltype(stc)::value;
+        constexpr int ahead = NST - 1 - st;
+        if constexpr (S::AH >= 3 && ahead >= 2) wait_vm<2 * S::IPW>();
+        else if constexpr (S::AH >= 2 && ahead >= 1) wait_vm<S::IPW>();
+        else wait_vm<0>();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if constexpr (st + S::AH < NST) issue(st + S::AH);
+        constexpr int G0 = (st * BK) / 16;  // first live column group
+        const T* a = smem + (st % S::NB) * S::STG;
+        const T* b = a + S::GRP * S::SRP;
+        T fa[2], fb[2][8];
+        auto frag = [&](int kq, int r) {
+            const int kr = kq * 4 + lk;
+            fa[r] = a[S::at(kr, 16 * w + lr)];
+#pragma unroll
+            for (int g = G0; g < 8; g++) fb[r][g] = b[S::at(kr, 16 * g + lr)];
+        };
+        frag(0, 0);
+#pragma unroll
+        for (int kq = 0; kq < BK / 4; kq++) {
+            if (kq + 1 < BK / 4) frag(kq + 1, (kq + 1) & 1);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int g = G0; g < 8; g++) acc[g >> 2][g & 3] = Tr::mma(fb[kq & 1][g], fa[kq & 1], acc[g >> 2][g & 3]);
+        }
+    };
+    static_assert(NST <= 8, "trirows: at most 8 stages");
+    stage(std::integral_constant<int, 0>{});
+    if constexpr (NST > 1) stage(std::integral_constant<int, (NST > 1 ? 1 : 0)>{});
+    if constexpr (NST > 2) stage(std::integral_constant<int, (NST > 2 ? 2 : 0)>{});
+    if constexpr (NST > 3) stage(std::integral_constant<int, (NST > 3 ? 3 : 0)>{});
+    if constexpr (NST > 4) stage(std::integral_constant<int, (NST > 4 ? 4 : 0)>{});
+    if constexpr (NST > 5) stage(std::integral_constant<int, (NST > 5 ? 5 : 0)>{});
+    if constexpr (NST > 6) stage(std::integral_constant<int, (NST > 6 ? 6 : 0)>{});
+    if constexpr (NST > 7) stage(std::integral_constant<int, (NST > 7 ? 7 : 0)>{});
+}
+
 // 256 x 128 output tile (A: 256 rows, B: 128 rows), for stand-alone kernels only: 128
 // accumulator registers, which the factorisation's task loop (at 256 VGPRs) cannot hold.  The 8
 // waves take 4 x 2 blocks of 64 x 64: 16 MFMAs per k-step from 8 fragment reads (the 128 x 128

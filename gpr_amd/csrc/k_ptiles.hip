@@ -118,6 +118,34 @@ __device__ __forceinline__ void tile_gemm(T* __restrict__ C, int64_t ldc, const 
     }
 }
 
+// TRSM task: C = A B^T for the lower-triangular B = Linv_k, each wave 16 rows x 128 columns
+// (k_mma.h tile_mma_trirows: every stage's triangle split evenly over the waves); C may be A.
+// C3 fit trace: TRSM 15.7 -> 13.0 us per task; launch 24.75 -> 24.62 ms same box, C2 within
+// noise, C4 unchanged (profiles/r06t_trsm_rows_ab.txt; out of line: 24.78 ms, not kept).
+// GPRX_TRSM_ROWS=0 builds the MAP 1 form.
+#ifndef GPRX_TRSM_ROWS
+#define GPRX_TRSM_ROWS 1
+#endif
+template <typename T>
+__device__ __forceinline__ void tile_trsm(T* C, int64_t ldc, const T* A, int64_t lda,
+                                          const T* __restrict__ B, int64_t ldb, T* smem, const int t) {
+    if constexpr (!GPRX_TRSM_ROWS) {
+        tile_gemm<T, false, 1, GPRX_SHORT_FEED>(C, ldc, A, lda, B, ldb, GT, false, smem, t, true);
+    } else {
+        typedef Mfma<T> Tr;
+        const int lane = t & 63, w = t >> 6, lr = lane & 15, lk = lane >> 4;
+        typename Tr::acc_t acc[2][4];
+        mm::tile_mma_trirows<T>(acc, A, lda, B, ldb, smem, t);
+#pragma unroll
+        for (int x = 0; x < 2; x++)
+#pragma unroll
+            for (int y = 0; y < 4; y++)
+#pragma unroll
+                for (int reg = 0; reg < 4; reg++)
+                    st_sc1(C + (int64_t)(16 * (4 * x + y) + Tr::orow(lk, reg)) * ldc + 16 * w + lr, acc[x][y][reg]);
+    }
+}
+
 // ------------------------------------------------------------------------------------------
 // Paired update (T_UPD2): C -= A B^T on a 256 x 128 tile -- tiles (i, j) and (i + 1, j), which
 // are adjacent rows of the column-major factor (C and A are 256 rows at one ld) -- over K panels
@@ -2508,7 +2536,7 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
                 if (!loc && wv == 0) dist_release(D, b0, nb);  // this chunk's window reads are done
             } else if (type == T_TRSM) {
                 T* Cik = dist_tile(a.A, D, i, j);
-                tile_gemm<T, false, 1, GPRX_SHORT_FEED>(Cik, DB, Cik, DB, a.Linv + (int64_t)j * DB * DB, DB, GT, false, smem, tid, true);
+                tile_trsm<T>(Cik, DB, Cik, DB, a.Linv + (int64_t)j * DB * DB, DB, smem, tid);
                 publish(a.lcnt + i, j + 1, false);
                 if (i == D.nc) {  // the label rows z^T: every other rank's z area (the solves read it)
                     const unsigned all = ((1u << D.g) - 1u) & ~(1u << D.r);
@@ -2536,8 +2564,7 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
                 } else if (fused_ts && k > 0) {
                     diagx_ts<T>(Akm, Akk, DB, a.Linv + (int64_t)(k - 1) * DB * DB, a.lcnt + k, k, smem, tid, false);
                 } else if (k > 0) {
-                    tile_gemm<T, false, 1, GPRX_SHORT_FEED>(Akm, DB, Akm, DB, a.Linv + (int64_t)(k - 1) * DB * DB, DB, GT, false, smem,
-                                           tid, true);
+                    tile_trsm<T>(Akm, DB, Akm, DB, a.Linv + (int64_t)(k - 1) * DB * DB, DB, smem, tid);
                     publish(a.lcnt + k, k, false);
                     tile_gemm<T, true, 2, GPRX_SHORT_FEED>(Akk, DB, Akm, DB, Akm, DB, GT, true, smem, tid);
                     local_sync();
@@ -2611,7 +2638,7 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
         } else if (type == T_TRSM) {
             T* Cik = Ci + (int64_t)j * GT * ld;
             if (!(a.variant & 1))
-                tile_gemm<T, false, 1, GPRX_SHORT_FEED>(Cik, ld, Cik, ld, a.Linv + (int64_t)j * DB * DB, DB, GT, false, smem, tid, true);
+                tile_trsm<T>(Cik, ld, Cik, ld, a.Linv + (int64_t)j * DB * DB, DB, smem, tid);
             publish(a.lcnt + i, j + 1, false);
         } else {  // DIAGX(k = i)
             const int k = i;
@@ -2628,8 +2655,7 @@ __global__ __launch_bounds__(NT) void potrf_tiles_kernel(Args<T> a) {
                 dt[1] = dt[0];
             } else if (k > 0) {
                 T* Akm = Ci + (int64_t)(k - 1) * GT * ld;
-                tile_gemm<T, false, 1, GPRX_SHORT_FEED>(Akm, ld, Akm, ld, a.Linv + (int64_t)(k - 1) * DB * DB, DB, GT, false, smem,
-                                       tid, true);
+                tile_trsm<T>(Akm, ld, Akm, ld, a.Linv + (int64_t)(k - 1) * DB * DB, DB, smem, tid);
                 if (a.trace) dt[0] = wall_clock64();
                 publish(a.lcnt + k, k, false);  // L_{k,k-1} final: unblocks the updates of column k
                 if (a.trace) dt[1] = wall_clock64();
