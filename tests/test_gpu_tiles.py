@@ -206,3 +206,30 @@ def test_posterior_repeatable_in_place_solves():
     v0 = M.posterior_cov(Q, Q)
     for _ in range(6):
         assert np.array_equal(M.posterior_cov(Q, Q), v0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", [np.float64, np.float32])
+def test_paths_repeatable(dt):
+    """Every multi-workgroup path gives the same bits when repeated on the same model: the
+    fused fit (paired updates, balanced TRSM tiles), the LML + gradient (identity rows paired,
+    C = U U^T, the gradient pass), the mean and the variance.  Guards the class of the in-place
+    race above: a cross-workgroup read-after-write shows up as a call that differs."""
+    from gpr_amd.synth import make_data, make_queries
+    ctx = gpr_amd.Context(0)
+    X, Y = make_data(6144, 8)
+    M = gpr_amd.Model(ctx, dt)
+    M.set_data(X, Y)
+    M.set_kernel("SumKernel(GaussianKernel(1.3,1,),PeriodicKernel(0.7,1.1,2.0,))"
+                 if dt == np.float64 else "GaussianKernel(1.3,1,)")
+    M.set_noise(0.5)
+    Q = make_queries(2048, 8)
+    outs = []
+    for _ in range(3):
+        M.fit()
+        v, g, ld = M.lml(grad=True)
+        outs.append((M.alpha().copy(), np.asarray(M.predict(Q)).copy(), np.asarray(M.posterior_cov(Q, Q)).copy(),
+                     np.float64(v), np.asarray(g).copy(), np.float64(ld)))
+    for o in outs[1:]:
+        for a, b in zip(outs[0], o):
+            assert np.array_equal(a, b)
