@@ -13,6 +13,8 @@
 #include "gprx_internal.h"
 #include "k_tile.h"
 
+#include <algorithm>
+
 namespace gprx {
 
 template <typename T>
@@ -258,7 +260,9 @@ __global__ __launch_bounds__(256) void lml_grad_kernel(KCanon<T> K, const T* __r
             }
         }
     }
-    // workgroup reduction of the 3*nleaf partial sums, then one atomic per value
+    // workgroup reduction of the 3*nleaf partial sums into this workgroup's slot of gout (one
+    // writer per value; lml_grad_sum_kernel adds the slots in a fixed order: the gradient is the
+    // same bits on every call, which atomics did not give)
     for (int l = 0; l < K.nleaf; l++) {
         for (int q = 0; q < 3; q++) {
             double v = (q == 0) ? acc[l][0] : ((q == 1) ? acc[l][1] : acc[l][2]);
@@ -266,27 +270,60 @@ __global__ __launch_bounds__(256) void lml_grad_kernel(KCanon<T> K, const T* __r
             for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off);
             if ((t & 63) == 0) sm.red[t >> 6] = v;
             __syncthreads();
-            if (t == 0) atomicAdd(&gout[l * 3 + q], sm.red[0] + sm.red[1] + sm.red[2] + sm.red[3]);
+            if (t == 0)
+                gout[(int64_t)blockIdx.x * (MAX_LEAF * 3) + l * 3 + q] = (sm.red[0] + sm.red[1]) + (sm.red[2] + sm.red[3]);
             __syncthreads();
         }
     }
 }
+
+// acc[p] += sum over the workgroups' slots of value p, in a fixed order (block p: value p)
+__global__ void lml_grad_sum_kernel(const double* __restrict__ part, int64_t nblk, double* __restrict__ acc) {
+    __shared__ double red[256];
+    const int p = blockIdx.x, t = threadIdx.x;
+    double v = 0;
+    for (int64_t b = t; b < nblk; b += 256) v += part[b * (MAX_LEAF * 3) + p];
+    red[t] = v;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (t < o) red[t] += red[t + o];
+        __syncthreads();
+    }
+    if (t == 0) acc[p] += red[0];
+}
+
+// the per-workgroup slots: stream-ordered scratch (no device-wide synchronisation), summed into acc
+struct GradSlots {
+    double* p = nullptr;
+    hipStream_t s;
+    GradSlots(int64_t nblk, hipStream_t st) : s(st) {
+        GPRX_HIP(hipMallocAsync((void**)&p, sizeof(double) * MAX_LEAF * 3 * (size_t)std::max<int64_t>(nblk, 1), s));
+    }
+    void finish(int nleaf, int64_t nblk, double* acc) {
+        hipLaunchKernelGGL(lml_grad_sum_kernel, dim3((unsigned)(3 * nleaf)), dim3(256), 0, s, (const double*)p, nblk, acc);
+    }
+    ~GradSlots() { (void)hipFreeAsync(p, s); }
+};
 
 template <typename T>
 void launch_lml_grad(const KCanon<T>& K, const T* X, const T* tab, int64_t n, int d, const T* alpha, const T* C,
                      int64_t ldc, double* acc, hipStream_t s) {
     const int64_t nt = (n + BT - 1) / BT;
     const unsigned grid = (unsigned)(nt * (nt + 1) / 2);
+    if (grid == 0) return;
     ProfScope ps(KC_LML_GRAD, s, 0.0, (double)sizeof(T) * ((double)n * (n + 1) / 2 + (double)n * d));
+    GradSlots slots(grid, s);
     if (K.nper == 0)
-        hipLaunchKernelGGL((lml_grad_kernel<T, 0>), dim3(grid), dim3(256), 0, s, K, X, tab, n, d, alpha, C, ldc, acc,
-                           X, tab, n, alpha, (int64_t)1);
+        hipLaunchKernelGGL((lml_grad_kernel<T, 0>), dim3(grid), dim3(256), 0, s, K, X, tab, n, d, alpha, C, ldc,
+                           slots.p, X, tab, n, alpha, (int64_t)1);
     else if (K.nper == 1)
-        hipLaunchKernelGGL((lml_grad_kernel<T, 1>), dim3(grid), dim3(256), 0, s, K, X, tab, n, d, alpha, C, ldc, acc,
-                           X, tab, n, alpha, (int64_t)1);
+        hipLaunchKernelGGL((lml_grad_kernel<T, 1>), dim3(grid), dim3(256), 0, s, K, X, tab, n, d, alpha, C, ldc,
+                           slots.p, X, tab, n, alpha, (int64_t)1);
     else
-        hipLaunchKernelGGL((lml_grad_kernel<T, 2>), dim3(grid), dim3(256), 0, s, K, X, tab, n, d, alpha, C, ldc, acc,
-                           X, tab, n, alpha, (int64_t)1);
+        hipLaunchKernelGGL((lml_grad_kernel<T, 2>), dim3(grid), dim3(256), 0, s, K, X, tab, n, d, alpha, C, ldc,
+                           slots.p, X, tab, n, alpha, (int64_t)1);
+    slots.finish(K.nleaf, grid, acc);
+    GPRX_HIP(hipGetLastError());
 }
 
 template <typename T>
@@ -297,15 +334,17 @@ void launch_lml_grad_cross(const KCanon<T>& K, const T* Xa, const T* tabA, int64
     if (ntr * ntc == 0) return;
     const unsigned grid = (unsigned)(ntr * ntc);
     ProfScope ps(KC_LML_GRAD, s, 0.0, (double)sizeof(T) * ((double)na * nb + (double)(na + nb) * d));
+    GradSlots slots(grid, s);
     if (K.nper == 0)
         hipLaunchKernelGGL((lml_grad_kernel<T, 0, true>), dim3(grid), dim3(256), 0, s, K, Xa, tabA, na, d, a, C, ldc,
-                           acc, Xb, tabB, nb, b, ntr);
+                           slots.p, Xb, tabB, nb, b, ntr);
     else if (K.nper == 1)
         hipLaunchKernelGGL((lml_grad_kernel<T, 1, true>), dim3(grid), dim3(256), 0, s, K, Xa, tabA, na, d, a, C, ldc,
-                           acc, Xb, tabB, nb, b, ntr);
+                           slots.p, Xb, tabB, nb, b, ntr);
     else
         hipLaunchKernelGGL((lml_grad_kernel<T, 2, true>), dim3(grid), dim3(256), 0, s, K, Xa, tabA, na, d, a, C, ldc,
-                           acc, Xb, tabB, nb, b, ntr);
+                           slots.p, Xb, tabB, nb, b, ntr);
+    slots.finish(K.nleaf, grid, acc);
     GPRX_HIP(hipGetLastError());
 }
 

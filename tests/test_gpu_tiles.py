@@ -233,3 +233,22 @@ def test_paths_repeatable(dt):
     for o in outs[1:]:
         for a, b in zip(outs[0], o):
             assert np.array_equal(a, b)
+
+
+@pytest.mark.gpu
+def test_lml_gradient_fallback_repeatable():
+    """The gradient pass for trees the MFMA statistics do not carry (a product of leaves:
+    k_lml.hip lml_grad_kernel) sums per-workgroup slots in a fixed order instead of atomics:
+    repeated LML + gradient calls give the same bits."""
+    from gpr_amd.synth import make_data
+    ctx = gpr_amd.Context(0)
+    X, Y = make_data(2048, 4)
+    M = gpr_amd.Model(ctx, np.float64)
+    M.set_data(X, Y)
+    M.set_kernel("ProductKernel(GaussianKernel(1.5,1,),PeriodicKernel(1,1.3,0.9,))")
+    M.set_noise(0.5)
+    M.fit()
+    v0, g0, l0 = M.lml(grad=True)
+    for _ in range(4):
+        v, g, ld = M.lml(grad=True)
+        assert v == v0 and ld == l0 and np.array_equal(np.asarray(g), np.asarray(g0))
