@@ -80,7 +80,23 @@ __global__ __launch_bounds__(256) void dk_grad_kernel(const T* __restrict__ dK, 
         if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
         __syncthreads();
     }
-    if (threadIdx.x == 0) atomicAdd(out + p, 0.5 * red[0]);
+    if (threadIdx.x == 0) out[(int64_t)p * gridDim.x + blockIdx.x] = 0.5 * red[0];  // this block's slot
+}
+
+// out[p] = sum of the gx slots of parameter p in a fixed order (the same bits on every call)
+__global__ __launch_bounds__(256) void dk_grad_sum_kernel(const double* __restrict__ part, int gx,
+                                                          double* __restrict__ out) {
+    __shared__ double red[256];
+    const int p = blockIdx.x;
+    double v = 0;
+    for (int b = threadIdx.x; b < gx; b += 256) v += part[(int64_t)p * gx + b];
+    red[threadIdx.x] = v;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[p] = red[0];
 }
 
 }  // namespace
@@ -110,8 +126,12 @@ void launch_dk_grad(const T* dK, int P, int64_t n, const T* alpha, const T* C, i
     GPRX_HIP(hipMemsetAsync(out, 0, sizeof(double) * P, s));
     if (P <= 0 || n <= 0) return;
     const unsigned gx = (unsigned)std::min<int64_t>(1024, (n * n + 255) / 256);
-    hipLaunchKernelGGL(dk_grad_kernel<T>, dim3(gx, (unsigned)P), dim3(256), 0, s, dK, n, alpha, C, ldc, out);
+    double* part = nullptr;  // per-block slots (stream-ordered scratch)
+    GPRX_HIP(hipMallocAsync((void**)&part, sizeof(double) * gx * (size_t)P, s));
+    hipLaunchKernelGGL(dk_grad_kernel<T>, dim3(gx, (unsigned)P), dim3(256), 0, s, dK, n, alpha, C, ldc, part);
+    hipLaunchKernelGGL(dk_grad_sum_kernel, dim3((unsigned)P), dim3(256), 0, s, (const double*)part, (int)gx, out);
     GPRX_HIP(hipGetLastError());
+    GPRX_HIP(hipFreeAsync(part, s));
 }
 
 #define GPRX_INST(T)                                                                                              \
