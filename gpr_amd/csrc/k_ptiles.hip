@@ -3384,7 +3384,11 @@ static Schedule best_schedule(int nc, int nr, const Params& pr, int P, bool buil
     Cost cm = pr.cost(f64);
     const PairRule pd = default_pair(f64);
     if (!std::getenv("GPRX_PT_PAIR_NBMIN")) cm.pair_nbmin = pd.nbmin;
-    if (!std::getenv("GPRX_PT_PAIR_TAIL")) cm.pair_tail = pd.tail;
+    // with the inverse riding along (ni > 0, the LML) the factor's last columns are not the end of
+    // the launch -- the identity rows' updates follow them -- so they pair too: the LML's factor
+    // launch 46.83-47.00 -> 46.42-46.57 ms (last 16 columns spared: 46.49-46.60; same box,
+    // profiles/r06ls_lml_pair_sweep.txt)
+    if (!std::getenv("GPRX_PT_PAIR_TAIL")) cm.pair_tail = ni > 0 ? 0 : pd.tail;
     Schedule best;
     bool have = false;
     const int want = pr.pair >= 0 ? pr.pair : pd.pair;
