@@ -27,7 +27,11 @@ for r in range(reps):
     M.fit()
     v = np.asarray(M.posterior_cov(Xq, Xq))
     mu = np.asarray(M.predict(Xq)) if hasattr(M, "predict") else v
-    out = np.concatenate([v.ravel(), np.asarray(mu).ravel()])
+    parts = [v.ravel(), np.asarray(mu).ravel()]
+    if os.environ.get("DET_LML"):  # also the LML + gradient (factor with the inverse riding along)
+        lv, lg, ld = M.lml(grad=True)
+        parts.append(np.concatenate([[lv, ld], np.asarray(lg, np.float64).ravel()]))
+    out = np.concatenate(parts)
     if r < 2 and len(sys.argv) > 5:
         np.save(f"{sys.argv[5]}_rep{r}.npy", out)
     if ref is None:
