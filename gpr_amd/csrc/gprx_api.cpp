@@ -1802,6 +1802,11 @@ struct SparseNE {
     DevBuf dXm, dtm, dX, dtx, dY, dS, dA, dK, dLinv, dLinvK, dinfo, dflag, dz, dalpha, dV, dC, dFU, dFV, dKd;
     const T* pX = nullptr;  // the dense rows and labels in HBM: the caller's device memory, or dX / dY
     const T* pY = nullptr;
+    // the streamed block dA (ld x acols): columns from dA_zero on are known to hold zeros (its
+    // layout last zeroed whole for dA_p, dA_ld, dA_cols); a chunk zeroes only the columns between
+    // its own end and dA_zero, instead of the whole 4.6 GB block (two memsets of it per C5 fit)
+    void* dA_p = nullptr;
+    int64_t dA_ld = 0, dA_cols = 0, dA_zero = 0;
 };
 
 // The sparse fit's device state lives in the context between calls (its buffers -- the
@@ -1899,13 +1904,26 @@ static void sparse_normal_eq(gprx_ctx* ctx, SparseNE<T>& st, const gprx_kernel_d
     GPRX_HIP(hipMemsetAsync(dS.p, 0, sizeof(T) * sstride * P, s));
     const int64_t acols = chunk + 16 * 16;  // slack: the P <= 16 split-K slices may overhang ncp (zeros)
     dA.ensure(sizeof(T) * ld * acols);
+    if (dA.p != st.dA_p || st.dA_ld != ld || st.dA_cols != acols) {  // a new block layout: zero it whole
+        GPRX_HIP(hipMemsetAsync(dA.p, 0, sizeof(T) * ld * acols, s));
+        st.dA_p = dA.p;
+        st.dA_ld = ld;
+        st.dA_cols = acols;
+        st.dA_zero = 0;
+    }
     const T is2 = T(1) / (T(sigma) * T(sigma));  // inverse_sigma2 in T (:285)
     st.is2 = is2;
     DevBuf dKY;
     if (fused) dKY.ensure(sizeof(T) * (chunk128 / GT) * Mp);
     for (int64_t off = 0; off < n; off += chunk) {
         const int64_t nc = std::min(chunk, n - off), ncp = round_up(nc, 16);
-        if (nc < chunk || off == 0) GPRX_HIP(hipMemsetAsync(dA.p, 0, sizeof(T) * ld * acols, s));
+        // columns [nc, acols) must be zero for this chunk's products (the split-K slices overhang
+        // the data): zero what an earlier, longer chunk left there; this chunk dirties [0, ncp)
+        if (st.dA_zero > nc) {
+            GPRX_HIP(hipMemsetAsync(dA.as<T>() + nc * ld, 0, sizeof(T) * ld * (st.dA_zero - nc), s));
+            st.dA_zero = nc;
+        }
+        st.dA_zero = std::max(st.dA_zero, ncp);
         if (mma) {
             const int64_t nc128 = round_up(nc, GT);
             launch_pair_features<T>(K, st.pX + off * d, nc, d, dXm.as<T>(), true, dFV.as<T>(), nc128, s,

@@ -274,3 +274,35 @@ def test_sparse_reference_gradient_config(ctx):
             return ctx.sparse_lml(f"GaussianKernel({sg!r},{sc!r},)", Xn, Y, Xm, noise, jitter, grad=False)[0]
         assert abs(g[0] - (val(sigma + h / 2, scale) - val(sigma - h / 2, scale)) / h) <= 1
         assert abs(g[1] - (val(sigma, scale + h / 2) - val(sigma, scale - h / 2)) / h) <= 0.1
+
+
+def test_sparse_streamed_block_reuse(monkeypatch):
+    """The streamed Kmn block lives in the context between fits and only the columns a longer
+    chunk left behind are re-zeroed (gprx_api.cpp SparseNE::dA_zero): fits of different lengths
+    (a ragged last chunk, then whole chunks, then ragged again) on one context give the same bits
+    as the same fits on fresh contexts."""
+    import gpr_amd
+    monkeypatch.setenv("GPRX_SPARSE_CHUNK", "2048")
+    ks = CASES[0][0]
+    shapes = [(5000, 11), (4096, 12), (3000, 13), (5000, 11)]
+    shared = gpr_amd.Context(0)
+    try:
+        got = []
+        for n, seed in shapes:
+            X, Y = make_data(n, 8, 1)
+            X = X + 1e-3 * seed
+            Xm = X[:: n // 300][:300].copy()
+            got.append(shared.sparse_fit(ks, X, Y, Xm, 0.3, 1e-3, np.float64))
+    finally:
+        shared.close()
+    for (n, seed), g in zip(shapes, got):
+        X, Y = make_data(n, 8, 1)
+        X = X + 1e-3 * seed
+        Xm = X[:: n // 300][:300].copy()
+        fresh = gpr_amd.Context(0)
+        try:
+            ref = fresh.sparse_fit(ks, X, Y, Xm, 0.3, 1e-3, np.float64)
+        finally:
+            fresh.close()
+        for a, b in zip(g, ref):
+            assert np.array_equal(a, b)
